@@ -1,0 +1,110 @@
+/* xcp.h -- C ABI of the MI355X-native Xception + LSTM clip-classification path.
+ *
+ * Drop-in boundary for the hot path of Tonmoy1321/Multimodal-DeepFake-Detection:
+ * the Xception entry/middle/exit-flow SeparableConv2d stacks (Xception.py:37-201)
+ * and the per-clip LSTM of XceptionLSTMV / XceptionLSTMA (XceptionLSTMV.py:18-23,
+ * :66-70; XceptionLSTMA.py:14-19, :55-59).  The reference binds to these ops only
+ * implicitly, through torch.nn modules; the host mirror
+ * (multimodal-deepfake-detection_amd/Models, .../xcp) binds each entry point below
+ * with ctypes.
+ *
+ * Conventions (every entry point):
+ *  - plain device pointers and sizes; pointers are never freed or retained;
+ *  - activations are NHWC "pixel rows" of C channels; `dtype` selects the storage
+ *    type of activation / GEMM operands: 0 = fp32 (parity mode), 1 = bf16;
+ *    accumulation is fp32, BN statistics fp64, master weights / grads fp32;
+ *  - work is enqueued on `stream` (a hipStream_t) with no host synchronisation and
+ *    no allocation, so a caller may capture it into a hipGraph;
+ *  - return 0 on success, a hipError_t code, or XCP_EINVAL (1001) /
+ *    XCP_EUNSUPPORTED (1002).  No C++ exception crosses the ABI.
+ */
+#ifndef XCP_H_
+#define XCP_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* xcp_stream_t; /* hipStream_t */
+
+#define XCP_F32 0
+#define XCP_BF16 1
+#define XCP_ACT_NONE 0
+#define XCP_ACT_RELU 1
+#define XCP_ACT_BNRELU 2
+
+/* ---- pointwise 1x1 conv / skip conv / stem conv2 / LSTM input projection ----
+ * replaces nn.Conv2d(C, Cout, 1) of SeparableConv2d.pointwise (Xception.py:42,:46),
+ * Block.skip (Xception.py:55,:93), Xception.conv2 (Xception.py:122,:172; im2col
+ * gather mode 2, its input gradient via mode 3) and x @ W_ih^T of nn.LSTM.
+ * C[M,N] = A[M,K] . B[N,K]^T ; optional stats[ceil(M/128)][2][N] partial
+ * (sum, sum^2) of the stored C columns (BatchNorm batch statistics).
+ * gmode: 0 dense rows, 1 strided (skip conv, stride gS), 2 im2col 3x3 p0,
+ *        3 transposed im2col (conv input gradient); gC = channels per tap. */
+int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, xcp_stream_t stream);
+
+/* weight gradient of the above: P[s][N][K] = sum_{m in split s} G[m][N] X[m][K],
+ * rows split in S chunks of rows_per_split; X rows gathered as in gemm_nt
+ * (gmode 0-2).  Reduce P over s with xcp_colreduce_f32. */
+int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, float* P, int M, int N, int K, int S,
+                int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, xcp_stream_t stream);
+
+/* ---- depthwise 3x3 (SeparableConv2d.conv1, Xception.py:41,:45) ----
+ * Y = dw3x3(act(X)); act per XCP_ACT_* (BN scale/shift for XCP_ACT_BNRELU);
+ * Wt is the [9][C] fp32 tap-major packing of the [C,1,3,3] weight. */
+int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift, int N,
+               int H, int W, int C, xcp_stream_t stream);
+/* fused backward: dX = act'(X) * dgrad(dY) + dRes + scatter_stride(dSkip);
+ * dWpart[P][C][9] block partials of the weight gradient, P = xcp_dw_bwd_chunks(). */
+int xcp_dw_bwd_chunks(int N, int H, int W, int C);
+int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
+               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, int N, int H, int W,
+               int C, xcp_stream_t stream);
+
+/* ---- BatchNorm2d (Xception.py:56,67,73,78,119,123,143,147), tails, pooling ---- */
+int xcp_colreduce_f64(const float* in, int S, long L, double* out, int G, xcp_stream_t stream);
+int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, xcp_stream_t stream);
+int xcp_chanred_parts(long rows, int C);
+int xcp_row_stats(int dtype, const void* X, long rows, int C, float* part, xcp_stream_t stream);
+int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd, long rows, int C,
+                      float* part, xcp_stream_t stream);
+int xcp_bn_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* beta, float* rmean,
+                    float* rvar, float momentum, float eps, int train, float* mean, float* invstd, float* scale,
+                    float* shift, xcp_stream_t stream);
+int xcp_bn_bwd_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* mean,
+                        const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
+                        int accumulate, xcp_stream_t stream);
+int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, long rows, int C,
+               xcp_stream_t stream);
+int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const float* alpha, const float* bcoef,
+                     const float* delta, long rows, int C, xcp_stream_t stream);
+int xcp_relu_bwd(int dtype, void* dX, const void* X, long rows, int C, xcp_stream_t stream);
+/* Block tail (Xception.py:86,:93-98): Out = [maxpool3x3s2p1](Y*s1+t1) + (s2 ? S*s2+t2 : S) */
+int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int pool, const void* S, const float* s2,
+                 const float* t2, void* Out, unsigned char* amax, int N, int H, int W, int C, xcp_stream_t stream);
+int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void* dZ, int N, int H, int W, int C,
+                    xcp_stream_t stream);
+/* bn4 + ReLU + adaptive_avg_pool2d (Xception.py:193-198) -> F[N][C] fp32 */
+int xcp_avgpool_fwd(int dtype, const void* Y, const float* s, const float* t, float* F, int N, int HW, int C,
+                    xcp_stream_t stream);
+int xcp_avgpool_bwd(int dtype, const float* dF, const void* Y, const float* s, const float* t, void* dZ, int N, int HW,
+                    int C, xcp_stream_t stream);
+
+/* ---- stem conv1 (Xception.py:118,:168) and weight packing ---- */
+int xcp_conv1_fwd(int dtype, const float* X, const float* W, void* Y, int N, int IH, int IW, xcp_stream_t stream);
+int xcp_conv1_wgrad_parts(int N, int IH, int IW);
+int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int N, int IH, int IW, xcp_stream_t stream);
+int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int d2, int p0, int p1, int p2,
+                 xcp_stream_t stream);
+
+/* ---- LSTM recurrence (nn.LSTM, XceptionLSTMV.py:18-23, :67) ---- */
+int xcp_lstm_fwd(const float* xproj, const float* whhT, const float* bih, const float* bhh, float* out, float* hprev,
+                 float* cst, float* gates, float* hn, float* cn, int B, int T, int H, xcp_stream_t stream);
+int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const float* whh, const float* cst,
+                 const float* gates, float* dgates, int B, int T, int H, xcp_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XCP_H_ */

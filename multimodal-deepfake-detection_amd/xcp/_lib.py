@@ -1,0 +1,85 @@
+"""ctypes binding of the C ABI in ``include/xcp.h`` (``libxcp.so``).
+
+This is the reference-side binding a maintainer would add: the
+reference reaches these ops only implicitly through ``torch.nn``; here every
+entry point is bound by name with explicit argument types.  Loading fails
+loudly when the library is missing -- there is no fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libxcp.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+D = ctypes.c_double
+
+# name -> argument types (return type is always int status)
+SIGNATURES = {
+    "xcp_gemm_nt": [I, P, L, P, L, P, L, I, I, I, P, I, I, I, I, I, I, I, P],
+    "xcp_gemm_tn": [I, P, L, P, L, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
+    "xcp_dw_bwd_chunks": [I, I, I, I],
+    "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, P, P, I, I, I, I, P],
+    "xcp_colreduce_f64": [P, I, L, P, I, P],
+    "xcp_colreduce_f32": [P, I, L, P, I, P],
+    "xcp_chanred_parts": [L, I],
+    "xcp_row_stats": [I, P, L, I, P, P],
+    "xcp_bn_bwd_reduce": [I, P, P, P, P, L, I, P, P],
+    "xcp_bn_finalize": [P, I, I, D, P, P, P, P, F, F, I, P, P, P, P, P],
+    "xcp_bn_bwd_finalize": [P, I, I, D, P, P, P, P, P, P, P, P, I, P],
+    "xcp_bn_act": [I, P, P, P, P, I, L, I, P],
+    "xcp_bn_bwd_apply": [I, P, P, P, P, P, P, L, I, P],
+    "xcp_relu_bwd": [I, P, P, L, I, P],
+    "xcp_tail_fwd": [I, P, P, P, I, P, P, P, P, P, I, I, I, I, P],
+    "xcp_maxpool_bwd": [I, P, P, P, I, I, I, I, P],
+    "xcp_avgpool_fwd": [I, P, P, P, P, I, I, I, P],
+    "xcp_avgpool_bwd": [I, P, P, P, P, P, I, I, I, P],
+    "xcp_conv1_fwd": [I, P, P, P, I, I, I, P],
+    "xcp_conv1_wgrad_parts": [I, I, I],
+    "xcp_conv1_wgrad": [I, P, P, P, I, I, I, P],
+    "xcp_permute3": [I, P, P, I, I, I, I, I, I, P],
+    "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, I, I, I, P],
+    "xcp_lstm_bwd": [P, P, P, P, P, P, P, I, I, I, P],
+}
+
+# entry points that return a size, not a status
+SIZE_QUERIES = {"xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts"}
+
+_lib = None
+
+
+class XcpError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libxcp.so (after torch, so the process shares torch's HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- HIP runtime of torch must be the one resolved
+    if not os.path.exists(LIB_PATH):
+        raise XcpError(f"HIP library {LIB_PATH} is missing; run `python -m xcp.build` (hipcc, gfx950). "
+                       "There is no CPU fallback for the product path.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Call an entry point; raise XcpError on a non-zero status."""
+    fn = getattr(load(), name)
+    rc = fn(*args)
+    if name in SIZE_QUERIES:
+        return rc
+    if rc != 0:
+        raise XcpError(f"{name} failed with status {rc}")
+    return rc

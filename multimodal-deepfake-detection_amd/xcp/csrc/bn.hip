@@ -1,0 +1,548 @@
+// BatchNorm2d (train-mode batch statistics / eval-mode running statistics),
+// the block tails (MaxPool 3x3 s2 p1 + residual add), the final BN+ReLU+global
+// average pool, and their backward passes.  NHWC rows of C channels.
+//
+// Reference ops: nn.BatchNorm2d (Xception.py:56,67,73,78,119,123,143,147),
+// nn.MaxPool2d(3, strides, 1) (:86), residual `x += skip` (:98),
+// F.adaptive_avg_pool2d (:197), ReLU (:60,:83,:170,:174,:191,:195).
+//
+// Statistics are reduced deterministically: producers write fp32 per-tile
+// partial rows [R][2][C]; `xcp_colreduce` folds them into G fp64 rows; the
+// finalize kernels read those.  Normalisation uses the biased batch variance,
+// running_var is updated with the unbiased one (momentum 0.1), as PyTorch does.
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------- column reduce
+// out[g][l] = sum_{s in group g} in[s][l]   (in: fp32 [S][L]; out: OutT [G][L])
+template <typename OutT>
+__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ in, int S, long L, OutT* __restrict__ out,
+                                                        int G) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long col = (long)blockIdx.x * 64 + lane;
+  const int g = blockIdx.y;
+  const int spg = (S + G - 1) / G;
+  const int s0 = g * spg, s1 = min(S, s0 + spg);
+  double acc = 0.0;
+  if (col < L)
+    for (int s = s0 + w; s < s1; s += 4) acc += (double)in[(long)s * L + col];
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && col < L) out[(long)g * L + col] = (OutT)(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+}
+
+// ---------------------------------------------------------------- per-channel reductions
+// Generic channel-reduction skeleton: block = nch channel chunks x P row chunks;
+// thread (lcv, slot) accumulates CPT channels over rows slot, slot+SPB, ... of its
+// row chunk; the block folds the slots in LDS and writes partial[pchunk][2][C].
+struct ChanRed {
+  int C, CV, CVB, SPB, nch;
+  long rows, rows_per_chunk;
+};
+
+ChanRed make_chanred(long rows, int C, int CPT, int target_blocks) {
+  ChanRed r;
+  r.C = C;
+  r.CV = C / CPT;
+  r.nch = (r.CV + 63) / 64;
+  r.CVB = (r.CV + r.nch - 1) / r.nch;
+  r.SPB = 256 / r.CVB;
+  long P = target_blocks / r.nch;
+  if (P < 1) P = 1;
+  const long maxP = (rows + 4L * r.SPB - 1) / (4L * r.SPB);
+  if (P > maxP) P = maxP;
+  if (P < 1) P = 1;
+  r.rows = rows;
+  r.rows_per_chunk = (rows + P - 1) / P;
+  return r;
+}
+long chanred_P(const ChanRed& r) { return (r.rows + r.rows_per_chunk - 1) / r.rows_per_chunk; }
+
+template <int CPT>
+XCP_DEV void chanred_finish(const ChanRed& r, float (*acc)[CPT], float* part, int cchunk, int pchunk, int lcv, int slot) {
+  extern __shared__ __attribute__((aligned(16))) float red[];   // [SPB][2][CVB*CPT]
+  const int L = r.CVB * CPT;
+  if (slot < r.SPB) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      red[(slot * 2 + 0) * L + lcv * CPT + j] = acc[0][j];
+      red[(slot * 2 + 1) * L + lcv * CPT + j] = acc[1][j];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * L; i += 256) {
+    const int k = i / L, cl = i % L;
+    float s = 0.f;
+    for (int q = 0; q < r.SPB; ++q) s += red[(q * 2 + k) * L + cl];
+    const int c = cchunk * L + cl;
+    if (c < r.C) part[((long)pchunk * 2 + k) * r.C + c] = s;
+  }
+}
+
+// MODE 0: (x, x^2) of rows of X.  MODE 1: (dz, dz*yhat), yhat = (y-mean)*invstd.
+template <typename T, int MODE, int CPT>
+__global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av, const void* Bv, const float* mean,
+                                                      const float* invstd, float* part) {
+  const int cchunk = blockIdx.x % r.nch, pchunk = blockIdx.x / r.nch;
+  const int lcv = threadIdx.x % r.CVB, slot = threadIdx.x / r.CVB;
+  const int cv = cchunk * r.CVB + lcv;
+  const int c0 = cv * CPT;
+  const T* A = reinterpret_cast<const T*>(Av);
+  const T* B = reinterpret_cast<const T*>(Bv);
+  float acc[2][CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) acc[0][j] = acc[1][j] = 0.f;
+  if (slot < r.SPB && cv < r.CV) {
+    float mu[CPT], is[CPT];
+    if constexpr (MODE == 1) {
+      VecIO<float, CPT>::load(mean + c0, mu);
+      VecIO<float, CPT>::load(invstd + c0, is);
+    }
+    const long rb = (long)pchunk * r.rows_per_chunk, re = min(r.rows, rb + r.rows_per_chunk);
+    for (long p = rb + slot; p < re; p += r.SPB) {
+      float a[CPT];
+      VecIO<T, CPT>::load(A + p * r.C + c0, a);
+      if constexpr (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+          acc[0][j] += a[j];
+          acc[1][j] = fmaf(a[j], a[j], acc[1][j]);
+        }
+      } else {
+        float b[CPT];
+        VecIO<T, CPT>::load(B + p * r.C + c0, b);
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+          acc[0][j] += a[j];
+          acc[1][j] = fmaf(a[j], (b[j] - mu[j]) * is[j], acc[1][j]);
+        }
+      }
+    }
+  }
+  chanred_finish<CPT>(r, acc, part, cchunk, pchunk, lcv, slot);
+}
+
+// ---------------------------------------------------------------- finalize
+__global__ void bn_finalize_kernel(const double* __restrict__ part2, int G, int C, double count, const float* gamma,
+                                   const float* beta, float* rmean, float* rvar, float momentum, float eps, int train,
+                                   float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double mean, var;
+  if (train) {
+    double s = 0.0, q = 0.0;
+    for (int g = 0; g < G; ++g) {
+      s += part2[((long)g * 2 + 0) * C + c];
+      q += part2[((long)g * 2 + 1) * C + c];
+    }
+    mean = s / count;
+    var = q / count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    if (rmean) {
+      const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+      rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+      rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * is;
+  mean_o[c] = (float)mean;
+  invstd_o[c] = is;
+  scale_o[c] = sc;
+  shift_o[c] = beta[c] - (float)mean * sc;
+}
+
+// dbeta = sum dz, dgamma = sum dz*yhat;  dy = alpha*dz + bcoef*y + delta
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part2, int G, int C, double count, const float* gamma,
+                                       const float* mean, const float* invstd, float* alpha, float* bcoef, float* delta,
+                                       float* dgamma, float* dbeta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sdz = 0.0, sdzy = 0.0;
+  for (int g = 0; g < G; ++g) {
+    sdz += part2[((long)g * 2 + 0) * C + c];
+    sdzy += part2[((long)g * 2 + 1) * C + c];
+  }
+  const double is = invstd[c], gm = gamma[c], mu = mean[c];
+  const double a = gm * is;
+  const double mdz = sdz / count, mdzy = sdzy / count;
+  alpha[c] = (float)a;
+  bcoef[c] = (float)(-a * is * mdzy);
+  delta[c] = (float)(-a * mdz + a * is * mu * mdzy);
+  if (dgamma) {
+    dgamma[c] = (float)sdzy + (accumulate ? dgamma[c] : 0.f);
+    dbeta[c] = (float)sdz + (accumulate ? dbeta[c] : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------- elementwise
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ X, T* __restrict__ Y, const float* scale,
+                                                     const float* shift, int relu, long rows, int C) {
+  const int CV = C / CPT;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= rows * CV) return;
+  const int c0 = (int)(g % CV) * CPT;
+  const long p = g / CV;
+  float v[CPT], s[CPT], t[CPT];
+  VecIO<T, CPT>::load(X + p * C + c0, v);
+  VecIO<float, CPT>::load(scale + c0, s);
+  VecIO<float, CPT>::load(shift + c0, t);
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    v[j] = fmaf(v[j], s[j], t[j]);
+    if (relu) v[j] = fmaxf(v[j], 0.f);
+  }
+  VecIO<T, CPT>::store(Y + p * C + c0, v);
+}
+
+// dy = alpha*dz + bcoef*y + delta
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dZ, const T* __restrict__ Yv, T* dY,
+                                                           const float* alpha, const float* bcoef, const float* delta,
+                                                           long rows, int C) {
+  const int CV = C / CPT;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= rows * CV) return;
+  const int c0 = (int)(g % CV) * CPT;
+  const long p = g / CV;
+  float dz[CPT], y[CPT], al[CPT], bc[CPT], de[CPT];
+  VecIO<T, CPT>::load(dZ + p * C + c0, dz);
+  VecIO<T, CPT>::load(Yv + p * C + c0, y);
+  VecIO<float, CPT>::load(alpha + c0, al);
+  VecIO<float, CPT>::load(bcoef + c0, bc);
+  VecIO<float, CPT>::load(delta + c0, de);
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) dz[j] = fmaf(al[j], dz[j], fmaf(bc[j], y[j], de[j]));
+  VecIO<T, CPT>::store(dY + p * C + c0, dz);
+}
+
+// dx *= (x > 0)
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void relu_bwd_kernel(T* dX, const T* __restrict__ Xv, long rows, int C) {
+  const int CV = C / CPT;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= rows * CV) return;
+  const int c0 = (int)(g % CV) * CPT;
+  const long p = g / CV;
+  float d[CPT], x[CPT];
+  VecIO<T, CPT>::load(dX + p * C + c0, d);
+  VecIO<T, CPT>::load(Xv + p * C + c0, x);
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) d[j] = x[j] > 0.f ? d[j] : 0.f;
+  VecIO<T, CPT>::store(dX + p * C + c0, d);
+}
+
+// Block tail: out = [maxpool3x3s2p1](y*s1+t1) + (skip_mode==0 ? inp : ys*s2+t2)
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void tail_fwd_kernel(const T* __restrict__ Y, const float* s1, const float* t1, int pool,
+                                                       const T* __restrict__ S, const float* s2, const float* t2,
+                                                       T* __restrict__ Out, unsigned char* __restrict__ amax, int N, int H,
+                                                       int W, int C, int OH, int OW) {
+  const int CV = C / CPT;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long)N * OH * OW * CV) return;
+  const int c0 = (int)(g % CV) * CPT;
+  const long op = g / CV;   // output pixel
+  const int ow = (int)(op % OW);
+  const long t = op / OW;
+  const int oh = (int)(t % OH);
+  const int n = (int)(t / OH);
+  float sc[CPT], sh[CPT], o[CPT];
+  VecIO<float, CPT>::load(s1 + c0, sc);
+  VecIO<float, CPT>::load(t1 + c0, sh);
+  if (pool) {
+    float m[CPT];
+    unsigned char am[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) { m[j] = -INFINITY; am[j] = 0; }
+    for (int ky = 0; ky < 3; ++ky) {
+      const int ih = oh * 2 - 1 + ky;
+      if (ih < 0 || ih >= H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iw = ow * 2 - 1 + kx;
+        if (iw < 0 || iw >= W) continue;
+        float v[CPT];
+        VecIO<T, CPT>::load(Y + (((long)n * H + ih) * W + iw) * C + c0, v);
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+          const float z = fmaf(v[j], sc[j], sh[j]);
+          if (z > m[j] || (z != z)) { m[j] = z; am[j] = (unsigned char)(ky * 3 + kx); }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) { o[j] = m[j]; amax[op * C + c0 + j] = am[j]; }
+  } else {
+    VecIO<T, CPT>::load(Y + op * C + c0, o);
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) o[j] = fmaf(o[j], sc[j], sh[j]);
+  }
+  float s[CPT];
+  VecIO<T, CPT>::load(S + op * C + c0, s);
+  if (s2) {
+    float a2[CPT], b2[CPT];
+    VecIO<float, CPT>::load(s2 + c0, a2);
+    VecIO<float, CPT>::load(t2 + c0, b2);
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) s[j] = fmaf(s[j], a2[j], b2[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) o[j] += s[j];
+  VecIO<T, CPT>::store(Out + op * C + c0, o);
+}
+
+// maxpool backward by gather: dz[n,h,w] = sum over windows (oh,ow) containing (h,w)
+// whose argmax is (h,w) of dout[n,oh,ow]
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dOut, const unsigned char* __restrict__ amax,
+                                                          T* __restrict__ dZ, int N, int H, int W, int C, int OH, int OW) {
+  const int CV = C / CPT;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long)N * H * W * CV) return;
+  const int c0 = (int)(g % CV) * CPT;
+  const long p = g / CV;
+  const int w = (int)(p % W);
+  const long t = p / W;
+  const int h = (int)(t % H);
+  const int n = (int)(t / H);
+  float acc[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) acc[j] = 0.f;
+  // window oh covers rows 2oh-1 .. 2oh+1  =>  h/2 <= oh <= (h+1)/2
+  for (int oh = h / 2; oh <= (h + 1) / 2; ++oh) {
+    if (oh < 0 || oh >= OH) continue;
+    const int ky = h - (oh * 2 - 1);
+    if (ky < 0 || ky > 2) continue;
+    for (int ow = w / 2; ow <= (w + 1) / 2; ++ow) {
+      if (ow < 0 || ow >= OW) continue;
+      const int kx = w - (ow * 2 - 1);
+      if (kx < 0 || kx > 2) continue;
+      const long op = ((long)n * OH + oh) * OW + ow;
+      float d[CPT];
+      VecIO<T, CPT>::load(dOut + op * C + c0, d);
+      const unsigned char want = (unsigned char)(ky * 3 + kx);
+#pragma unroll
+      for (int j = 0; j < CPT; ++j)
+        if (amax[op * C + c0 + j] == want) acc[j] += d[j];
+    }
+  }
+  VecIO<T, CPT>::store(dZ + p * C + c0, acc);
+}
+
+// final: feats[n][c] = mean_{hw} relu(y*s+t)   (fp32 out)
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const T* __restrict__ Y, const float* s, const float* t,
+                                                          float* __restrict__ F, int N, int HW, int C) {
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long)N * C) return;
+  const int c = (int)(g % C);
+  const int n = (int)(g / C);
+  const float sc = s[c], sh = t[c];
+  float acc = 0.f;
+  for (int p = 0; p < HW; ++p) acc += fmaxf(fmaf(to_f(Y[((long)n * HW + p) * C + c]), sc, sh), 0.f);
+  F[g] = acc / (float)HW;
+}
+
+// dz[n,p,c] = (y*s+t > 0) ? dF[n][c] / HW : 0
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ dF, const T* __restrict__ Y,
+                                                          const float* s, const float* t, T* __restrict__ dZ, int N, int HW,
+                                                          int C) {
+  const int CV = C / CPT;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long)N * HW * CV) return;
+  const int c0 = (int)(g % CV) * CPT;
+  const long p = g / CV;
+  const int n = (int)(p / HW);
+  float y[CPT], sc[CPT], sh[CPT], d[CPT];
+  VecIO<T, CPT>::load(Y + p * C + c0, y);
+  VecIO<float, CPT>::load(s + c0, sc);
+  VecIO<float, CPT>::load(t + c0, sh);
+  VecIO<float, CPT>::load(dF + (long)n * C + c0, d);
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) y[j] = fmaf(y[j], sc[j], sh[j]) > 0.f ? d[j] * inv : 0.f;
+  VecIO<T, CPT>::store(dZ + p * C + c0, y);
+}
+
+inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
+
+template <typename T, int MODE>
+int chanred_launch(long rows, int C, const void* A, const void* B, const float* mean, const float* invstd, float* part,
+                   hipStream_t st) {
+  constexpr int CPT = 8;
+  ChanRed r = make_chanred(rows, C, CPT, 1024);
+  const long P = chanred_P(r);
+  const size_t smem = (size_t)r.SPB * 2 * r.CVB * CPT * sizeof(float);
+  hipLaunchKernelGGL((chanred_kernel<T, MODE, CPT>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, A, B, mean,
+                     invstd, part);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int xcp_colreduce_f64(const float* in, int S, long L, double* out, int G, hipStream_t st) {
+  if (L <= 0) return XCP_OK;
+  if (G > S) G = S;
+  if (G < 1) G = 1;
+  hipLaunchKernelGGL(colreduce_kernel<double>, dim3((unsigned)((L + 63) / 64), G), dim3(256), 0, st, in, S, L, out, G);
+  return (int)hipGetLastError();
+}
+
+int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, hipStream_t st) {
+  if (L <= 0) return XCP_OK;
+  if (G > S) G = S;
+  if (G < 1) G = 1;
+  hipLaunchKernelGGL(colreduce_kernel<float>, dim3((unsigned)((L + 63) / 64), G), dim3(256), 0, st, in, S, L, out, G);
+  return (int)hipGetLastError();
+}
+
+// number of partial rows the channel reductions below produce
+int xcp_chanred_parts(long rows, int C) {
+  ChanRed r = make_chanred(rows, C, 8, 1024);
+  return (int)chanred_P(r);
+}
+
+// part[P][2][C] = per-chunk (sum x, sum x^2) over rows of X[rows][C]
+int xcp_row_stats(int dtype, const void* X, long rows, int C, float* part, hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  if (dtype == XCP_BF16) return chanred_launch<bf16, 0>(rows, C, X, nullptr, nullptr, nullptr, part, st);
+  if (dtype == XCP_F32) return chanred_launch<float, 0>(rows, C, X, nullptr, nullptr, nullptr, part, st);
+  return XCP_EUNSUPPORTED;
+}
+
+// part[P][2][C] = per-chunk (sum dz, sum dz*(y-mean)*invstd)
+int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd, long rows, int C,
+                      float* part, hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  if (dtype == XCP_BF16) return chanred_launch<bf16, 1>(rows, C, dZ, Y, mean, invstd, part, st);
+  if (dtype == XCP_F32) return chanred_launch<float, 1>(rows, C, dZ, Y, mean, invstd, part, st);
+  return XCP_EUNSUPPORTED;
+}
+
+int xcp_bn_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* beta, float* rmean,
+                    float* rvar, float momentum, float eps, int train, float* mean, float* invstd, float* scale,
+                    float* shift, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part2, G, C, count, gamma, beta, rmean,
+                     rvar, momentum, eps, train, mean, invstd, scale, shift);
+  return (int)hipGetLastError();
+}
+
+int xcp_bn_bwd_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* mean,
+                        const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
+                        int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part2, G, C, count, gamma, mean,
+                     invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
+  return (int)hipGetLastError();
+}
+
+int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, long rows, int C,
+               hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const unsigned g = nblk(rows * (C / 8));
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((bn_act_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)X, (bf16*)Y, scale, shift, relu,
+                       rows, C);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((bn_act_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)X, (float*)Y, scale, shift,
+                       relu, rows, C);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const float* alpha, const float* bcoef,
+                     const float* delta, long rows, int C, hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const unsigned g = nblk(rows * (C / 8));
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)dZ, (const bf16*)Y,
+                       (bf16*)dY, alpha, bcoef, delta, rows, C);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)dZ, (const float*)Y,
+                       (float*)dY, alpha, bcoef, delta, rows, C);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+int xcp_relu_bwd(int dtype, void* dX, const void* X, long rows, int C, hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const unsigned g = nblk(rows * (C / 8));
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((relu_bwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (bf16*)dX, (const bf16*)X, rows, C);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((relu_bwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, (float*)dX, (const float*)X, rows, C);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int pool, const void* S, const float* s2,
+                 const float* t2, void* Out, unsigned char* amax, int N, int H, int W, int C, hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const int OH = pool ? (H - 1) / 2 + 1 : H, OW = pool ? (W - 1) / 2 + 1 : W;
+  const unsigned g = nblk((long)N * OH * OW * (C / 8));
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((tail_fwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)Y, s1, t1, pool,
+                       (const bf16*)S, s2, t2, (bf16*)Out, amax, N, H, W, C, OH, OW);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((tail_fwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)Y, s1, t1, pool,
+                       (const float*)S, s2, t2, (float*)Out, amax, N, H, W, C, OH, OW);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void* dZ, int N, int H, int W, int C,
+                    hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const unsigned g = nblk((long)N * H * W * (C / 8));
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)dOut, amax, (bf16*)dZ, N,
+                       H, W, C, OH, OW);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((maxpool_bwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)dOut, amax, (float*)dZ,
+                       N, H, W, C, OH, OW);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+int xcp_avgpool_fwd(int dtype, const void* Y, const float* s, const float* t, float* F, int N, int HW, int C,
+                    hipStream_t st) {
+  const unsigned g = nblk((long)N * C);
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<bf16>, dim3(g), dim3(256), 0, st, (const bf16*)Y, s, t, F, N, HW, C);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)Y, s, t, F, N, HW, C);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+int xcp_avgpool_bwd(int dtype, const float* dF, const void* Y, const float* s, const float* t, void* dZ, int N, int HW,
+                    int C, hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const unsigned g = nblk((long)N * HW * (C / 8));
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((avgpool_bwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, dF, (const bf16*)Y, s, t, (bf16*)dZ, N,
+                       HW, C);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((avgpool_bwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, dF, (const float*)Y, s, t, (float*)dZ,
+                       N, HW, C);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,433 @@
+// Pointwise 1x1 convolution as an MFMA GEMM (forward, dgrad) and its weight
+// gradient (wgrad, split over the pixel dimension).
+//
+// Reference ops replaced: the pointwise `nn.Conv2d(C, Cout, 1)` of
+// SeparableConv2d (Xception.py:42, called at :46), the stride-2 skip conv of
+// Block (Xception.py:55, called at :93) and the LSTM input projection
+// (x @ W_ih^T for all T at once, XceptionLSTMV.py:18-23 / :67).
+//
+//   gemm_nt : C[M,N] = A[M,K] . B[N,K]^T       (A = NHWC pixel rows, B = weight
+//             [Cout][Cin]); optional row gather of A (stride-s skip conv) and a
+//             BatchNorm-statistics epilogue (per-column sum / sum of squares of
+//             the stored values, one deterministic partial row per M-tile).
+//   gemm_tn : P[s][N,K] = sum_{m in split s} G[m,N]^T X[m,K]   (weight gradient;
+//             fp32 partial slabs, reduced deterministically by slab_reduce).
+//
+// Tile 128x128, 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16 tiles.
+// bf16: v_mfma_f32_16x16x32_bf16, fp32: v_mfma_f32_16x16x4_f32 (exact fp32).
+// LDS rows are 128 B (one 64-deep bf16 / 32-deep fp32 K-stage), 16-B chunks
+// XOR-swizzled with (row>>1)&7 so a 16-lane ds_read_b128 group is conflict-free.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, NT = 256;
+constexpr int ROWB = 128;                 // bytes per LDS row per K-stage
+constexpr int STAGE_BYTES = BM * ROWB;    // one operand, one stage (16 KB)
+
+template <typename T> struct GT;
+template <> struct GT<bf16> { static constexpr int EPC = 8; };
+template <> struct GT<float> { static constexpr int EPC = 4; };
+
+XCP_DEV int swz(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4); }
+
+// Row gather for the A operand (NT) / X operand (TN):
+//   mode 0: row m is at m*ld
+//   mode 1: strided 1x1 conv input, m = (n,oh,ow) over OHxOW -> pixel (n, oh*S, ow*S) of HxW
+//   mode 2: im2col of a 3x3 stride-1 pad-0 conv, m = (n,oh,ow) over OHxOW, column
+//           k = tap*Cg + c -> pixel (n, oh+ky, ow+kx) of HxW, channel c
+//   mode 3: transposed im2col (input gradient of that conv), m = (n,h,w) over HxW,
+//           k = tap*Cg + c -> pixel (n, h-ky, w-kx) of OHxOW (zero outside), channel c
+struct Gather {
+  int mode, H, W, OH, OW, S, Cg;
+};
+struct RowInfo {
+  long base;
+  int h, w;
+  bool ok;
+};
+XCP_DEV RowInfo row_info(const Gather& g, int m, int M) {
+  RowInfo r{0, 0, 0, m < M};
+  if (!r.ok || g.mode == 0) {
+    r.base = r.ok ? m : 0;
+    return r;
+  }
+  if (g.mode == 3) {
+    const int hw = g.H * g.W, n = m / hw, rem = m - n * hw;
+    r.h = rem / g.W;
+    r.w = rem - r.h * g.W;
+    r.base = (long)n * g.OH * g.OW;
+    return r;
+  }
+  const int ohw = g.OH * g.OW, n = m / ohw, rem = m - n * ohw;
+  const int oh = rem / g.OW, ow = rem - oh * g.OW;
+  r.base = (long)n * g.H * g.W + (long)oh * g.S * g.W + (long)ow * g.S;
+  return r;
+}
+// element offset of the chunk (row r, column k), or -1 for a zero chunk
+XCP_DEV long chunk_off(const Gather& g, const RowInfo& r, long ld, int k) {
+  if (g.mode <= 1) return r.base * ld + k;
+  const int tap = k / g.Cg, c = k - tap * g.Cg;
+  const int ky = tap / 3, kx = tap - ky * 3;
+  if (g.mode == 2) return (r.base + (long)ky * g.W + kx) * ld + c;
+  const int oh = r.h - ky, ow = r.w - kx;
+  if (oh < 0 || oh >= g.OH || ow < 0 || ow >= g.OW) return -1;
+  return (r.base + (long)oh * g.OW + ow) * ld + c;
+}
+
+struct NTArgs {
+  const void* A; long lda;
+  const void* B; long ldb;
+  void* C; long ldc;
+  int M, N, K;
+  float* stats;           // [gridM][2][N] partial (sum, sumsq) or nullptr
+  Gather ga;
+};
+
+template <typename T>
+__global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
+  constexpr int EPC = GT<T>::EPC;
+  constexpr int BK = 8 * EPC;
+  constexpr int CPITCH = BN * (int)sizeof(T) + 16;   // epilogue staging row pitch (bytes)
+  constexpr int SMEM_MAIN = 4 * STAGE_BYTES;
+  constexpr int SMEM_EPI = BM * CPITCH;
+  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 2 * 2 * BN * 4];
+  float* red = reinterpret_cast<float*>(smem + SMEM);   // [2 wm][2 (s,q)][BN]
+
+  const int gridN = (a.N + BN - 1) / BN;
+  const int gridM = (a.M + BM - 1) / BM;
+  const int id = xcd_remap(blockIdx.x, gridM * gridN);
+  const int bn = id % gridN, bm = id / gridN;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const T* A = reinterpret_cast<const T*>(a.A);
+  const T* B = reinterpret_cast<const T*>(a.B);
+
+  // per-thread global chunk coordinates (4 chunks per operand per stage)
+  RowInfo ar[4];
+  bool b_ok[4];
+  long b_off[4];
+  int crow[4], cchk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + NT * i;
+    crow[i] = q >> 3;
+    cchk[i] = q & 7;
+    const int n = n0 + crow[i];
+    ar[i] = row_info(a.ga, m0 + crow[i], a.M);
+    b_ok[i] = n < a.N;
+    b_off[i] = b_ok[i] ? (long)n * a.ldb : 0;
+  }
+
+  uint4 ra[4], rb[4];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = kt * BK + cchk[i] * EPC;
+      const bool kok = k < a.K;
+      const long ao = (ar[i].ok && kok) ? chunk_off(a.ga, ar[i], a.lda, k) : -1;
+      ra[i] = ao >= 0 ? *reinterpret_cast<const uint4*>(A + ao) : make_uint4(0, 0, 0, 0);
+      rb[i] = (b_ok[i] && kok) ? *reinterpret_cast<const uint4*>(B + b_off[i] + k) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* sa = smem + buf * 2 * STAGE_BYTES;
+    char* sb = sa + STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<uint4*>(sa + swz(crow[i], cchk[i])) = ra[i];
+      *reinterpret_cast<uint4*>(sb + swz(crow[i], cchk[i])) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.K + BK - 1) / BK;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* sa = smem + (kt & 1) * 2 * STAGE_BYTES;
+    const char* sb = sa + STAGE_BYTES;
+#pragma unroll
+    for (int cg = 0; cg < 2; ++cg) {
+      const int ch = cg * 4 + fg;
+      if constexpr (sizeof(T) == 2) {
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          af[t] = *reinterpret_cast<const bf16x8*>(sa + swz(wm * 64 + t * 16 + fr, ch));
+          bfr[t] = *reinterpret_cast<const bf16x8*>(sb + swz(wn * 64 + t * 16 + fr, ch));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      } else {
+        f32x4 af[4], bfr[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          af[t] = *reinterpret_cast<const f32x4*>(sa + swz(wm * 64 + t * 16 + fr, ch));
+          bfr[t] = *reinterpret_cast<const f32x4*>(sb + swz(wn * 64 + t * 16 + fr, ch));
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bfr[j][e], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) swrite((kt + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: round to T, BN statistics, stage through LDS, 16-B stores
+  float cs[4], cq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { cs[j] = 0.f; cq[j] = 0.f; }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = rnd<T>(acc[i][j][r]);
+        cs[j] += v;
+        cq[j] += v * v;
+        const int row = wm * 64 + i * 16 + fg * 4 + r, col = wn * 64 + j * 16 + fr;
+        *reinterpret_cast<T*>(smem + row * CPITCH + col * (int)sizeof(T)) = from_f<T>(v);
+      }
+  if (a.stats) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16, 64);
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 16, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+    }
+    if (fg == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[(wm * 2 + 0) * BN + wn * 64 + j * 16 + fr] = cs[j];
+        red[(wm * 2 + 1) * BN + wn * 64 + j * 16 + fr] = cq[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (a.stats && tid < BN) {
+    const int n = n0 + tid;
+    if (n < a.N) {
+      a.stats[((long)bm * 2 + 0) * a.N + n] = red[0 * BN + tid] + red[2 * BN + tid];
+      a.stats[((long)bm * 2 + 1) * a.N + n] = red[1 * BN + tid] + red[3 * BN + tid];
+    }
+  }
+  T* C = reinterpret_cast<T*>(a.C);
+  constexpr int CPR = BN * (int)sizeof(T) / 16;   // 16-B chunks per tile row
+  constexpr int ITER = BM * CPR / NT;
+#pragma unroll
+  for (int i = 0; i < ITER; ++i) {
+    const int q = tid + NT * i;
+    const int row = q / CPR, c = q % CPR;
+    const int m = m0 + row, n = n0 + c * EPC;
+    if (m < a.M && n < a.N)
+      *reinterpret_cast<uint4*>(C + (long)m * a.ldc + n) = *reinterpret_cast<const uint4*>(smem + row * CPITCH + c * 16);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Weight gradient: P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]
+// G: [M][ldg] (output-gradient pixel rows), X: [M][ldx] (layer-input pixel rows).
+// Both operands are pixel-major, so the reduction index m is the slow memory
+// dimension: tiles are staged [m][col] in LDS and bf16 fragments are read with
+// ds_read_b64_tr_b16 (4 m-rows x 16 cols per 16-lane group, transposed).
+constexpr int TBM = 32;                      // m rows per stage
+constexpr int TPITCH = 128 * 2 + 32;         // bf16 LDS row pitch (bytes): pitch/4 = 8 (mod 64)
+
+struct TNArgs {
+  const void* G; long ldg;
+  const void* X; long ldx;
+  float* P;                // [S][N][K] fp32 partials
+  int M, N, K, S, rows_per_split;
+  Gather gx;               // gather of the X operand rows / columns
+};
+
+XCP_DEV bf16x4 ds_read_tr(const char* p) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void gemm_tn_kernel(TNArgs a) {
+  // tile: 128 (n) x 128 (k); stage: 32 m-rows of G[., n0:n0+128] and X[., k0:k0+128]
+  constexpr int EPC = GT<T>::EPC;
+  constexpr int PITCH = (sizeof(T) == 2) ? TPITCH : (128 * 4 + 16);
+  constexpr int STG = TBM * PITCH;
+  __shared__ __attribute__((aligned(16))) char smem[4 * STG];
+
+  const int gridN = (a.N + 127) / 128, gridK = (a.K + 127) / 128;
+  const int tiles = gridN * gridK;
+  const int id = blockIdx.x;
+  const int s = id / tiles, t = id % tiles;
+  const int bn = t / gridK, bk = t % gridK;
+  const int n0 = bn * 128, k0 = bk * 128;
+  const int mbeg = s * a.rows_per_split;
+  const int mend = min(a.M, mbeg + a.rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;            // wave tile: n rows wm*64.., k cols wn*64..
+  const T* G = reinterpret_cast<const T*>(a.G);
+  const T* X = reinterpret_cast<const T*>(a.X);
+
+  // staging: each operand stage = 32 rows x 128 cols = 32 x (128/EPC) chunks
+  constexpr int CPR = 128 / EPC;            // 16 (bf16) or 32 (f32) chunks per row
+  constexpr int LPT = TBM * CPR / NT;       // loads per thread per operand: 2 or 4
+  uint4 rg[LPT], rx[LPT];
+  int srow[LPT], schk[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int q = tid + NT * i;
+    srow[i] = q / CPR;
+    schk[i] = q % CPR;
+  }
+  auto gload = [&](int mb) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int m = mb + srow[i];
+      const int n = n0 + schk[i] * EPC, k = k0 + schk[i] * EPC;
+      const bool mok = m < mend;
+      rg[i] = (mok && n < a.N) ? *reinterpret_cast<const uint4*>(G + (long)m * a.ldg + n) : make_uint4(0, 0, 0, 0);
+      const RowInfo xr = row_info(a.gx, m, mend);
+      const long xo = (xr.ok && k < a.K) ? chunk_off(a.gx, xr, a.ldx, k) : -1;
+      rx[i] = xo >= 0 ? *reinterpret_cast<const uint4*>(X + xo) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* sg = smem + buf * 2 * STG;
+    char* sx = sg + STG;
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      *reinterpret_cast<uint4*>(sg + srow[i] * PITCH + schk[i] * 16) = rg[i];
+      *reinterpret_cast<uint4*>(sx + srow[i] * PITCH + schk[i] * 16) = rx[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int q4 = fr >> 2, p4 = fr & 3;          // tr-read: lane 4q+p -> row q, cols 4p..4p+3
+  const int nst = (mend - mbeg + TBM - 1) / TBM;
+  if (nst > 0) {
+    gload(mbeg);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) gload(mbeg + (st + 1) * TBM);
+    const char* sg = smem + (st & 1) * 2 * STG;
+    const char* sx = sg + STG;
+    if constexpr (sizeof(T) == 2) {
+      // MFMA k-slots of lane group g: m rows {4g..4g+3} (elements 0-3) and {16+4g..} (4-7)
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int t4 = 0; t4 < 4; ++t4) {
+        const int ncol = wm * 64 + t4 * 16 + p4 * 4;
+        const int kcol = wn * 64 + t4 * 16 + p4 * 4;
+        bf16x4 a0 = ds_read_tr(sg + (4 * fg + q4) * PITCH + ncol * 2);
+        bf16x4 a1 = ds_read_tr(sg + (16 + 4 * fg + q4) * PITCH + ncol * 2);
+        bf16x4 b0 = ds_read_tr(sx + (4 * fg + q4) * PITCH + kcol * 2);
+        bf16x4 b1 = ds_read_tr(sx + (16 + 4 * fg + q4) * PITCH + kcol * 2);
+        af[t4] = bf16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        bfr[t4] = bf16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+      // fp32: 8 MFMA steps of 4 m-rows; lane group g holds m row 4*step + g
+#pragma unroll
+      for (int e = 0; e < TBM / 4; ++e) {
+        const int mr = 4 * e + fg;
+        float av[4], bv[4];
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4) {
+          av[t4] = *reinterpret_cast<const float*>(sg + mr * PITCH + (wm * 64 + t4 * 16 + fr) * 4);
+          bv[t4] = *reinterpret_cast<const float*>(sx + mr * PITCH + (wn * 64 + t4 * 16 + fr) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (st + 1 < nst) swrite((st + 1) & 1);
+    __syncthreads();
+  }
+  // write partial slab P[s][n][k]: acc[i][j][r] = C[n = wm*64+i*16+fg*4+r][k = wn*64+j*16+fr]
+  float* P = a.P + (long)s * a.N * a.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + wm * 64 + i * 16 + fg * 4 + r;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + wn * 64 + j * 16 + fr;
+        if (k < a.K) P[(long)n * a.K + k] = acc[i][j][r];
+      }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// C[M,N] = A[M,K] . B[N,K]^T ; see include/xcp.h
+int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
+  if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
+  if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
+  NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
+  const int grid = xcp_cdiv(M, BM) * xcp_cdiv(N, BN);
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL(gemm_nt_kernel<bf16>, dim3(grid), dim3(NT), 0, stream, a);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL(gemm_nt_kernel<float>, dim3(grid), dim3(NT), 0, stream, a);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+// P[s][N][K] partial weight gradients; S splits of rows_per_split rows each.
+int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, float* P, int M, int N, int K, int S,
+                int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, hipStream_t stream) {
+  if (N <= 0 || K <= 0 || S <= 0) return XCP_OK;
+  if ((K % 8) || (N % 8) || (ldg % 8) || (ldx % 8)) return XCP_EINVAL;
+  if (gmode < 0 || gmode > 2 || (gmode == 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
+  TNArgs a{G, ldg, X, ldx, P, M, N, K, S, rows_per_split, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
+  const int grid = xcp_cdiv(N, 128) * xcp_cdiv(K, 128) * S;
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL(gemm_tn_kernel<bf16>, dim3(grid), dim3(NT), 0, stream, a);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL(gemm_tn_kernel<float>, dim3(grid), dim3(NT), 0, stream, a);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

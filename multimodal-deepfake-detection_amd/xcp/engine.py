@@ -1,0 +1,411 @@
+"""Whole-backbone executor for Xception (forward + backward) on the xcp kernels.
+
+The reference runs ``Xception.forward`` (Xception.py:167-201) module by module
+through ATen; here one engine walks the same graph with the hand-written gfx950
+kernels of ``libxcp.so`` and keeps activations NHWC in HBM:
+
+* BatchNorm is never materialised inside a block: the pointwise GEMM epilogue
+  emits the batch statistics, and BN-apply + ReLU is folded into the load of the
+  next depthwise conv (``ACT_BNRELU``); only block outputs (``x += skip``,
+  Xception.py:98) and the stem output are written.
+* Backward reuses the saved raw tensors: the fused depthwise backward recomputes
+  the BN+ReLU input on the fly, applies the ReLU mask and adds the identity /
+  strided skip gradients.
+
+One engine serves one ``Xception`` module; it is driven through
+``XceptionFunction`` so autograd sees a single node whose inputs are the frames and
+every backbone parameter.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .ops import ACT_BNRELU, ACT_NONE, ACT_RELU
+
+
+def _bn_ref(m):
+    return {"weight": m.weight, "bias": m.bias, "running_mean": m.running_mean, "running_var": m.running_var,
+            "eps": m.eps, "momentum": m.momentum, "track": m.track_running_stats, "module": m}
+
+
+class _Unit:
+    """relu? -> SeparableConv2d -> BatchNorm2d, one element of Block.rep (Xception.py:61-79)."""
+
+    def __init__(self, sep, bn, relu, name, bn_name):
+        self.sep, self.bn, self.relu, self.name, self.bn_name = sep, bn, relu, name, bn_name
+        self.cin = sep.conv1.in_channels
+        self.cout = sep.pointwise.out_channels
+        if sep.conv1.kernel_size != (3, 3) or sep.conv1.stride != (1, 1) or sep.conv1.padding != (1, 1):
+            raise NotImplementedError("xcp engine supports the Xception 3x3/s1/p1 separable convs only")
+        if sep.conv1.bias is not None or sep.pointwise.bias is not None:
+            raise NotImplementedError("xcp engine: separable convs are bias-free in Xception")
+
+
+class _Block:
+    def __init__(self, blk, name):
+        self.name = name
+        self.units = []
+        self.pool = False
+        mods = list(blk.rep)
+        i, relu = 0, False
+        while i < len(mods):
+            m = mods[i]
+            if isinstance(m, nn.ReLU):
+                relu = True
+                i += 1
+            elif m.__class__.__name__ == "SeparableConv2d":
+                bn = mods[i + 1]
+                assert isinstance(bn, nn.BatchNorm2d)
+                self.units.append(_Unit(m, bn, relu, f"{name}.rep.{i}", f"{name}.rep.{i + 1}"))
+                relu = False
+                i += 2
+            elif isinstance(m, nn.MaxPool2d):
+                if (m.kernel_size, m.stride, m.padding) not in ((3, 2, 1), ((3, 3), (2, 2), (1, 1))):
+                    raise NotImplementedError("xcp engine: MaxPool2d(3, 2, 1) only")
+                self.pool = True
+                i += 1
+            else:
+                raise NotImplementedError(f"xcp engine: unexpected module {type(m)} in {name}.rep")
+        for u in self.units[1:]:
+            if not u.relu:
+                raise NotImplementedError("xcp engine: inner separable convs must be preceded by ReLU")
+        self.skip = blk.skip
+        self.skipbn = getattr(blk, "skipbn", None) if blk.skip is not None else None
+        self.stride = blk.skip.stride[0] if blk.skip is not None else 1
+        if self.pool and self.skip is None:
+            raise NotImplementedError("xcp engine: a pooled block needs a conv skip")
+        if self.skip is not None and self.stride != (2 if self.pool else 1):
+            raise NotImplementedError("xcp engine: skip stride must match the pooling")
+        self.cin = self.units[0].cin
+        self.cout = self.units[-1].cout
+
+
+class Stats:
+    __slots__ = ("mean", "invstd", "scale", "shift")
+
+    def __init__(self, C, dev):
+        buf = torch.empty(4 * C, device=dev, dtype=torch.float32)
+        self.mean, self.invstd, self.scale, self.shift = buf[:C], buf[C:2 * C], buf[2 * C:3 * C], buf[3 * C:]
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+class XceptionEngine:
+    def __init__(self, model, dtype=torch.bfloat16):
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("xcp engine dtype must be float32 (parity) or bfloat16")
+        self.model = model
+        self.dtype = dtype
+        self.blocks = [_Block(getattr(model, f"block{i}"), f"block{i}") for i in range(1, 13)]
+        self.exit_units = [_Unit(model.conv3, model.bn3, False, "conv3", "bn3"),
+                           _Unit(model.conv4, model.bn4, True, "conv4", "bn4")]
+        c1, c2 = model.conv1, model.conv2
+        if (c1.in_channels, c1.out_channels, c1.kernel_size, c1.stride, c1.padding) != (3, 32, (3, 3), (2, 2), (0, 0)):
+            raise NotImplementedError("xcp engine: Xception stem conv1 must be 3->32 3x3 s2 p0")
+        if (c2.in_channels, c2.out_channels, c2.kernel_size, c2.stride, c2.padding) != (32, 64, (3, 3), (1, 1), (0, 0)):
+            raise NotImplementedError("xcp engine: Xception stem conv2 must be 32->64 3x3 s1 p0")
+        self.bn_modules = [m for m in model.modules() if isinstance(m, nn.BatchNorm2d)]
+        self._pack_key = None
+        self._packed = {}
+        self._packed_bwd_key = None
+
+    # ------------------------------------------------------------ parameters
+    def named_params(self):
+        """Backbone parameters in a fixed order (the autograd inputs)."""
+        return [(n, p) for n, p in self.model.named_parameters() if not n.startswith("fc.")]
+
+    def _version_key(self):
+        return tuple((p.data_ptr(), p._version) for _, p in self.named_params()) + (self.dtype,)
+
+    def pack(self):
+        key = self._version_key()
+        if key == self._pack_key:
+            return self._packed
+        dt, pk = self.dtype, {}
+        m = self.model
+        dev = m.conv1.weight.device
+
+        def pw(conv):
+            co, ci = conv.out_channels, conv.in_channels
+            out = torch.empty(co * ci, device=dev, dtype=dt)
+            ops.permute3(conv.weight.detach(), out, co, ci, 1, (0, 1, 2))
+            return out
+
+        def dw(conv):
+            c = conv.in_channels
+            out = torch.empty(9 * c, device=dev, dtype=torch.float32)
+            ops.permute3(conv.weight.detach(), out, c, 9, 1, (1, 0, 2))
+            return out
+
+        for u in self._all_units():
+            pk[u.name + ".dw"] = dw(u.sep.conv1)
+            pk[u.name + ".pw"] = pw(u.sep.pointwise)
+        for b in self.blocks:
+            if b.skip is not None:
+                pk[b.name + ".skip"] = pw(b.skip)
+        w2 = torch.empty(64 * 9 * 32, device=dev, dtype=dt)
+        ops.permute3(m.conv2.weight.detach(), w2, 64, 32, 9, (0, 2, 1))   # [co][tap][ci]
+        pk["conv2"] = w2
+        self._packed, self._pack_key = pk, key
+        self._packed_bwd_key = None
+        return pk
+
+    def pack_bwd(self):
+        """Transposed weights for the input-gradient GEMMs."""
+        if self._packed_bwd_key == self._pack_key and self._pack_key is not None:
+            return self._packed
+        pk, dt, m = self._packed, self.dtype, self.model
+        dev = m.conv1.weight.device
+
+        def pwT(conv):
+            co, ci = conv.out_channels, conv.in_channels
+            out = torch.empty(co * ci, device=dev, dtype=dt)
+            ops.permute3(conv.weight.detach(), out, co, ci, 1, (1, 0, 2))
+            return out
+
+        for u in self._all_units():
+            pk[u.name + ".pwT"] = pwT(u.sep.pointwise)
+        for b in self.blocks:
+            if b.skip is not None:
+                pk[b.name + ".skipT"] = pwT(b.skip)
+        w2t = torch.empty(32 * 9 * 64, device=dev, dtype=dt)
+        ops.permute3(m.conv2.weight.detach(), w2t, 64, 32, 9, (1, 2, 0))  # [ci][tap][co]
+        pk["conv2T"] = w2t
+        self._packed_bwd_key = self._pack_key
+        return pk
+
+    def _all_units(self):
+        for b in self.blocks:
+            yield from b.units
+        yield from self.exit_units
+
+    # ------------------------------------------------------------ helpers
+    def _empty(self, n, dtype=None):
+        return torch.empty(n, device=self.device, dtype=dtype or self.dtype)
+
+    def _bn_stats(self, part, R, C, count, bnmod, train):
+        s = Stats(C, self.device)
+        ref = _bn_ref(bnmod)
+        if train:
+            if ref["momentum"] is None:
+                ref["momentum"] = 1.0 / float(bnmod.num_batches_tracked.item() + 1)
+            ops.finalize_stats(part, R, C, count, ref, True, s)
+        else:
+            ops.eval_stats(C, ref, s, self.device)
+        return s
+
+    def _pw(self, A, Wp, M, cout, cin, train, bnmod, lda=None, gather=(0, 0, 0, 0, 0, 1, 0)):
+        Y = self._empty(M * cout)
+        if train:
+            R = ops.nt_stat_rows(M)
+            part = self._empty(R * 2 * cout, torch.float32)
+            ops.gemm_nt(A, Wp, Y, M, cout, cin, lda=lda, stats=part, gather=gather)
+            st = self._bn_stats(part, R, cout, M, bnmod, True)
+        else:
+            ops.gemm_nt(A, Wp, Y, M, cout, cin, lda=lda, gather=gather)
+            st = self._bn_stats(None, 0, cout, M, bnmod, False)
+        return Y, st
+
+    # ------------------------------------------------------------ forward
+    def forward(self, x, train):
+        """x: [N,3,H,W] fp32 (NCHW, as XceptionLSTMV.extract_features feeds it).
+        Returns (features [N,2048] fp32, saved-state dict for backward)."""
+        ops.check_gpu(x)
+        self.device = x.device
+        x = x.contiguous().float()
+        N, C0, IH, IW = x.shape
+        if C0 != 3:
+            raise ValueError("Xception expects 3 input channels")
+        pk = self.pack()
+        m = self.model
+        S = {"N": N, "IH": IH, "IW": IW, "x": x, "train": train}
+        # ---- stem (Xception.py:168-174)
+        OH1, OW1 = (IH - 3) // 2 + 1, (IW - 3) // 2 + 1
+        rows1 = N * OH1 * OW1
+        c1 = self._empty(rows1 * 32)
+        ops.conv1_fwd(x, m.conv1.weight.detach(), c1, N, IH, IW)
+        if train:
+            part, R = ops.row_stats(c1, rows1, 32)
+            s1 = self._bn_stats(part, R, 32, rows1, m.bn1, True)
+        else:
+            s1 = self._bn_stats(None, 0, 32, rows1, m.bn1, False)
+        a1 = self._empty(rows1 * 32)
+        ops.bn_act(c1, a1, s1.scale, s1.shift, True, rows1, 32)
+        OH2, OW2 = OH1 - 2, OW1 - 2
+        rows2 = N * OH2 * OW2
+        c2, s2 = self._pw(a1, pk["conv2"], rows2, 64, 288, train, m.bn2, lda=32, gather=(2, OH1, OW1, OH2, OW2, 1, 32))
+        sout = self._empty(rows2 * 64)
+        ops.bn_act(c2, sout, s2.scale, s2.shift, True, rows2, 64)
+        S.update(c1=c1, s1=s1, a1=a1, c2=c2, s2=s2, sout=sout, OH1=OH1, OW1=OW1, OH2=OH2, OW2=OW2)
+        # ---- blocks (Xception.py:176-187)
+        xc, H, W = sout, OH2, OW2
+        S["blocks"] = []
+        for b in self.blocks:
+            xc, H, W, bs = self._block_fwd(b, xc, N, H, W, pk, train)
+            S["blocks"].append(bs)
+        # ---- exit flow (Xception.py:189-198)
+        M = N * H * W
+        ex = []
+        src, act, sc, sh = xc, ACT_NONE, None, None
+        for u in self.exit_units:
+            d = self._empty(M * u.cin)
+            ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, u.cin)
+            y, st = self._pw(d, pk[u.name + ".pw"], M, u.cout, u.cin, train, u.bn)
+            ex.append({"src": src, "act": act, "sc": sc, "sh": sh, "d": d, "y": y, "st": st})
+            src, act, sc, sh = y, ACT_BNRELU, st.scale, st.shift
+        feats = torch.empty(N, 2048, device=self.device, dtype=torch.float32)
+        last = ex[-1]
+        ops.avgpool_fwd(last["y"], last["st"].scale, last["st"].shift, feats, N, H * W, 2048)
+        S.update(exit=ex, xH=H, xW=W, x12=xc)
+        if train:
+            nbt = [b.num_batches_tracked for b in self.bn_modules if b.num_batches_tracked is not None]
+            if nbt:
+                torch._foreach_add_(nbt, 1)
+        return feats, S
+
+    def _block_fwd(self, b, x_in, N, H, W, pk, train):
+        M = N * H * W
+        units = []
+        src, act, sc, sh = x_in, (ACT_RELU if b.units[0].relu else ACT_NONE), None, None
+        for u in b.units:
+            d = self._empty(M * u.cin)
+            ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, u.cin)
+            y, st = self._pw(d, pk[u.name + ".pw"], M, u.cout, u.cin, train, u.bn)
+            units.append({"src": src, "act": act, "sc": sc, "sh": sh, "d": d, "y": y, "st": st})
+            src, act, sc, sh = y, ACT_BNRELU, st.scale, st.shift
+        if b.pool or b.stride != 1:
+            OH, OW = (H - 1) // b.stride + 1, (W - 1) // b.stride + 1
+        else:
+            OH, OW = H, W
+        Ms = N * OH * OW
+        ys = sks = None
+        if b.skip is not None:
+            ys, sks = self._pw(x_in, pk[b.name + ".skip"], Ms, b.cout, b.cin, train, b.skipbn, lda=b.cin,
+                               gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
+        out = self._empty(Ms * b.cout)
+        amax = torch.empty(Ms * b.cout, device=self.device, dtype=torch.uint8) if b.pool else None
+        st = units[-1]["st"]
+        ops.tail_fwd(units[-1]["y"], st.scale, st.shift, b.pool, ys if ys is not None else x_in,
+                     sks.scale if sks is not None else None, sks.shift if sks is not None else None, out, amax, N, H, W,
+                     b.cout)
+        bs = {"x_in": x_in, "units": units, "ys": ys, "sks": sks, "amax": amax, "H": H, "W": W, "OH": OH, "OW": OW}
+        return out, OH, OW, bs
+
+    # ------------------------------------------------------------ backward
+    def backward(self, S, dfeat):
+        """dfeat [N,2048] fp32 -> {param name: fp32 grad tensor} for every backbone parameter."""
+        if not S["train"]:
+            raise RuntimeError("xcp engine backward needs a train-mode forward (batch-stat BatchNorm)")
+        pk = self.pack_bwd()
+        m = self.model
+        N = S["N"]
+        dev = self.device
+        grads = {}
+        dfeat = dfeat.contiguous().float()
+
+        def g(name, shape):
+            t = torch.empty(shape, device=dev, dtype=torch.float32)
+            grads[name] = t
+            return t
+
+        def bn_bwd(bnmod, name, dZ, Y, rows, C, st):
+            dY = self._empty(rows * C)
+            ops.bn_backward(dZ, Y, rows, C, _bn_ref(bnmod), st, dY, g(name + ".weight", (C,)), g(name + ".bias", (C,)))
+            return dY
+
+        def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1)):
+            """dZ: gradient w.r.t. this unit's BN output.  Returns gradient w.r.t. the
+            depthwise input after the activation mask (+ residual / skip terms)."""
+            M = N * H * W
+            dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"])
+            dD = self._empty(M * u.cin)
+            ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, u.cin, u.cout)
+            ops.weight_grad(dY, rec["d"], M, u.cout, u.cin, g(u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1)))
+            dX = self._empty(M * u.cin)
+            ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX,
+                       g(u.name + ".conv1.weight", (u.cin, 1, 3, 3)), N, H, W, u.cin, dRes=dRes, dSkip=dSkip,
+                       skip_geom=skip_geom)
+            return dX
+
+        # ---- exit flow
+        H, W = S["xH"], S["xW"]
+        M = N * H * W
+        e3, e4 = S["exit"]
+        u3, u4 = self.exit_units
+        dZ4 = self._empty(M * 2048)
+        ops.avgpool_bwd(dfeat, e4["y"], e4["st"].scale, e4["st"].shift, dZ4, N, H * W, 2048)
+        dZ3 = unit_bwd(u4, e4, dZ4, H, W)
+        dX = unit_bwd(u3, e3, dZ3, H, W)
+        # ---- blocks, last to first
+        for b, bs in zip(reversed(self.blocks), reversed(S["blocks"])):
+            dX = self._block_bwd(b, bs, dX, N, pk, g, bn_bwd, unit_bwd)
+        # ---- stem
+        OH1, OW1, OH2, OW2 = S["OH1"], S["OW1"], S["OH2"], S["OW2"]
+        rows1, rows2 = N * OH1 * OW1, N * OH2 * OW2
+        ops.relu_bwd(dX, S["sout"], rows2, 64)
+        dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"])
+        dA1 = self._empty(rows1 * 32)
+        ops.gemm_nt(dC2, pk["conv2T"], dA1, rows1, 32, 576, lda=64, gather=(3, OH1, OW1, OH2, OW2, 1, 64))
+        w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
+        ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
+        ops.permute3(w2g, g("conv2.weight", (64, 32, 3, 3)), 64, 9, 32, (0, 2, 1))
+        ops.relu_bwd(dA1, S["a1"], rows1, 32)
+        dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"])
+        ops.conv1_wgrad(S["x"], dC1, g("conv1.weight", (32, 3, 3, 3)), N, S["IH"], S["IW"])
+        return grads
+
+    def _block_bwd(self, b, bs, dOut, N, pk, g, bn_bwd, unit_bwd):
+        H, W, OH, OW = bs["H"], bs["W"], bs["OH"], bs["OW"]
+        M, Ms = N * H * W, N * OH * OW
+        units = bs["units"]
+        if b.pool:
+            dZ = self._empty(M * b.cout)
+            ops.maxpool_bwd(dOut, bs["amax"], dZ, N, H, W, b.cout)
+        else:
+            dZ = dOut
+        dRes = dSkip = None
+        skip_geom = (0, 0, 1)
+        if b.skip is not None:
+            dYs = bn_bwd(b.skipbn, b.name + ".skipbn", dOut, bs["ys"], Ms, b.cout, bs["sks"])
+            ops.weight_grad(dYs, bs["x_in"], Ms, b.cout, b.cin, g(b.name + ".skip.weight", (b.cout, b.cin, 1, 1)),
+                            gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0),
+                            ldx=b.cin)
+            dXs = self._empty(Ms * b.cin)
+            ops.gemm_nt(dYs, pk[b.name + ".skipT"], dXs, Ms, b.cin, b.cout)
+            if b.stride != 1:
+                dSkip, skip_geom = dXs, (OH, OW, b.stride)
+            else:
+                dRes = dXs
+        else:
+            dRes = dOut
+        for i in range(len(b.units) - 1, -1, -1):
+            u, rec = b.units[i], units[i]
+            if i > 0:
+                dZ = unit_bwd(u, rec, dZ, H, W)
+            else:
+                dZ = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom)
+        return dZ
+
+
+class XceptionFunction(torch.autograd.Function):
+    """Autograd node for the whole backbone: inputs (frames, *backbone params),
+    output features [N,2048].  Gradients w.r.t. the frames are not produced (the
+    reference never differentiates w.r.t. its input clips)."""
+
+    @staticmethod
+    def forward(ctx, engine, train, x, *params):
+        feats, S = engine.forward(x, train)
+        ctx.engine, ctx.S = engine, S
+        ctx.names = [n for n, _ in engine.named_params()]
+        ctx.needs = [p.requires_grad for p in params]
+        return feats
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        grads = ctx.engine.backward(ctx.S, dfeat)
+        ctx.S = None
+        out = [grads.get(n) if need else None for n, need in zip(ctx.names, ctx.needs)]
+        return (None, None, None, *out)

@@ -1,0 +1,181 @@
+"""CPU oracle for the Xception + LSTM clip-classification path.
+
+TEST INFRASTRUCTURE ONLY.  This module is the checker: only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import it.
+The product path (``multimodal-deepfake-detection_amd``) never imports it and
+fails loudly when its HIP library is missing.
+
+It is a functional, fp32, PyTorch-CPU restatement of the reference algorithm
+(Tonmoy1321/Multimodal-DeepFake-Detection).  The arithmetic of the reference
+lives in third-party PyTorch (un-vendored, unpinned by the reference); this
+restatement uses the same ATen CPU ops (``F.conv2d``, ``F.batch_norm``,
+``F.max_pool2d``, the LSTM cell equations) so that on torch 2.10.0 it is
+bit-identical or within fp32 rounding of the reference.  It is pinned by the
+golden fixtures in ``tests/golden/`` that ``tools/capture_goldens.py`` captured
+by importing the reference in the build container
+(``tests/test_oracle_golden.py``).
+
+Parameters are passed as a flat ``{name: tensor}`` dict whose keys are the
+reference ``state_dict`` keys (e.g. ``block4.rep.1.conv1.weight``).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+BN_EPS = 1e-5          # nn.BatchNorm2d default (Xception.py:56,67,...)
+BN_MOMENTUM = 0.1      # nn.BatchNorm2d default
+
+# Block configuration, Xception.py:125-140: (in, out, reps, stride, start_with_relu, grow_first)
+BLOCKS = [
+    (64, 128, 2, 2, False, True),
+    (128, 256, 2, 2, True, True),
+    (256, 728, 2, 2, True, True),
+] + [(728, 728, 3, 1, True, True)] * 8 + [
+    (728, 1024, 2, 2, True, False),
+]
+
+
+def block_layout(cin, cout, reps, stride, start_with_relu, grow_first):
+    """Restates Block.__init__ (Xception.py:50-87): returns the ``rep`` list as
+    ('relu',) / ('sep', idx, cin, cout) / ('bn', idx, c) / ('pool', idx) entries, where idx
+    is the index inside ``nn.Sequential`` (state_dict key ``rep.<idx>``)."""
+    rep = []
+    filters = cin
+    if grow_first:
+        rep += [("relu",), ("sep", cin, cout), ("bn", cout)]
+        filters = cout
+    for _ in range(reps - 1):
+        rep += [("relu",), ("sep", filters, filters), ("bn", filters)]
+    if not grow_first:
+        rep += [("relu",), ("sep", cin, cout), ("bn", cout)]
+    if not start_with_relu:
+        rep = rep[1:]
+    if stride != 1:
+        rep.append(("pool",))
+    return [(e[0], i) + tuple(e[1:]) for i, e in enumerate(rep)]
+
+
+def _bn(x, sd, key, train, stats_out):
+    """nn.BatchNorm2d forward (train: batch stats, biased var for normalisation; running
+    stats updated with momentum 0.1 and unbiased var)."""
+    rm = sd[key + ".running_mean"].clone()
+    rv = sd[key + ".running_var"].clone()
+    y = F.batch_norm(x, rm, rv, sd[key + ".weight"], sd[key + ".bias"], train, BN_MOMENTUM, BN_EPS)
+    if stats_out is not None:
+        stats_out[key + ".running_mean"] = rm
+        stats_out[key + ".running_var"] = rv
+        nbt = sd.get(key + ".num_batches_tracked")
+        stats_out[key + ".num_batches_tracked"] = (nbt + 1) if (nbt is not None and train) else nbt
+    return y
+
+
+def sepconv(x, sd, key):
+    """SeparableConv2d.forward, Xception.py:44-47 (depthwise 3x3 p1 groups=C, then 1x1)."""
+    c = x.shape[1]
+    x = F.conv2d(x, sd[key + ".conv1.weight"], None, 1, 1, 1, c)
+    return F.conv2d(x, sd[key + ".pointwise.weight"])
+
+
+def block_forward(x, sd, key, cfg, train, stats_out):
+    """Block.forward, Xception.py:89-99."""
+    inp = x
+    for e in block_layout(*cfg):
+        kind, idx = e[0], e[1]
+        if kind == "relu":
+            x = F.relu(x)
+        elif kind == "sep":
+            x = sepconv(x, sd, f"{key}.rep.{idx}")
+        elif kind == "bn":
+            x = _bn(x, sd, f"{key}.rep.{idx}", train, stats_out)
+        elif kind == "pool":
+            x = F.max_pool2d(x, 3, cfg[3], 1)
+    if cfg[0] != cfg[1] or cfg[3] != 1:
+        skip = F.conv2d(inp, sd[key + ".skip.weight"], None, cfg[3])
+        skip = _bn(skip, sd, key + ".skipbn", train, stats_out)
+    else:
+        skip = inp
+    return x + skip
+
+
+def backbone_forward(x, sd, train=True, stats_out=None, prefix=""):
+    """Xception.forward, Xception.py:167-201, with ``fc = nn.Identity()``
+    (XceptionLSTMV.py:13).  ``x`` is [N,3,H,W] fp32; returns [N,2048]."""
+    p = prefix
+    x = F.conv2d(x, sd[p + "conv1.weight"], None, 2, 0)
+    x = F.relu(_bn(x, sd, p + "bn1", train, stats_out))
+    x = F.conv2d(x, sd[p + "conv2.weight"], None, 1, 0)
+    x = F.relu(_bn(x, sd, p + "bn2", train, stats_out))
+    for i, cfg in enumerate(BLOCKS):
+        x = block_forward(x, sd, f"{p}block{i + 1}", cfg, train, stats_out)
+    x = sepconv(x, sd, p + "conv3")
+    x = F.relu(_bn(x, sd, p + "bn3", train, stats_out))
+    x = sepconv(x, sd, p + "conv4")
+    x = F.relu(_bn(x, sd, p + "bn4", train, stats_out))
+    x = F.adaptive_avg_pool2d(x, (1, 1))
+    return x.view(x.size(0), -1)
+
+
+def lstm_forward(x, w_ih, w_hh, b_ih, b_hh):
+    """Single-layer batch_first nn.LSTM (XceptionLSTMV.py:18-23): gates in order i,f,g,o,
+    h0 = c0 = 0.  Returns (out[B,T,H], h_n[1,B,H], c_n[1,B,H])."""
+    B, T, _ = x.shape
+    H = w_hh.shape[1]
+    h = x.new_zeros(B, H)
+    c = x.new_zeros(B, H)
+    xp = torch.matmul(x, w_ih.t()) + b_ih + b_hh
+    outs = []
+    for t in range(T):
+        g = xp[:, t] + torch.matmul(h, w_hh.t())
+        i, f, gg, o = g.chunk(4, 1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        outs.append(h)
+    return torch.stack(outs, 1), h.unsqueeze(0), c.unsqueeze(0)
+
+
+def head_forward(feats, sd, prefix=""):
+    """XceptionLSTMV.forward, XceptionLSTMV.py:66-70 with dropout inactive (eval).
+    Returns (prob[B,1], logits[B,1])."""
+    p = prefix
+    out, _, _ = lstm_forward(feats, sd[p + "lstm.weight_ih_l0"], sd[p + "lstm.weight_hh_l0"],
+                             sd[p + "lstm.bias_ih_l0"], sd[p + "lstm.bias_hh_l0"])
+    h = out[:, -1, :]
+    for li in (0, 3, 6, 9):
+        h = F.relu(F.linear(h, sd[f"{p}fc_layers.{li}.weight"], sd[f"{p}fc_layers.{li}.bias"]))
+    logits = F.linear(h, sd[p + "fc_out.weight"], sd[p + "fc_out.bias"])
+    return torch.sigmoid(logits), logits
+
+
+def audio_frames(x):
+    """XceptionLSTMA.extract_features front end, XceptionLSTMA.py:43-46."""
+    B, T, c, n = x.shape
+    return F.interpolate(x.reshape(B * T, c, n, 1), size=(64, 64), mode="bilinear", align_corners=False)
+
+
+def clip_step(sd, clips, labels, unfrozen, audio=False):
+    """One train step of the clip model (train_audio.py:33-44 / train_visual.py BCE variant):
+    backbone in train mode, head dropout inactive, BCE loss, backward.
+    Returns dict(features, prob, logits, loss, grads{name: tensor}, stats{buffer: tensor})."""
+    params = {k: v.detach().clone() for k, v in sd.items()}
+    train_keys = [k for k in params if k.startswith(("lstm.", "fc_layers.", "fc_out."))]
+    if unfrozen:
+        train_keys += [k for k in params if k.startswith("feature_extractor.") and "running" not in k
+                       and "num_batches" not in k]
+    for k in train_keys:
+        params[k].requires_grad_(True)
+    B, T = clips.shape[:2]
+    frames = audio_frames(clips) if audio else clips.reshape(B * T, *clips.shape[2:])
+    stats = {}
+    feats = backbone_forward(frames, params, True, stats, prefix="feature_extractor.").view(B, T, -1)
+    prob, logits = head_forward(feats, params)
+    loss = F.binary_cross_entropy(prob, labels)
+    loss.backward()
+    grads = {k: params[k].grad for k in train_keys}
+    return dict(features=feats.detach(), prob=prob.detach(), logits=logits.detach(), loss=loss.detach(),
+                grads=grads, stats=stats)
+
+
+def kaiming_like_init(shape, out_channels, kh, kw, gen):
+    """Xception.py:154-158 init for a conv weight (N(0, sqrt(2/(kh*kw*out_channels))))."""
+    return torch.randn(shape, generator=gen) * math.sqrt(2.0 / (kh * kw * out_channels))
