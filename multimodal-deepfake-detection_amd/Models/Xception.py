@@ -126,10 +126,9 @@ class Xception(nn.Module):
 
     def features(self, x):
         """Backbone up to the global average pool: [N,3,H,W] fp32 -> [N,2048] fp32."""
+        from xcp import ops
         from xcp.engine import XceptionFunction
-        if not x.is_cuda:
-            raise RuntimeError("the xcp Xception runs on the MI355X only; move the model and input to 'cuda' "
-                               "(the CPU reference is the oracle used by the tests, not a product path)")
+        ops.check_gpu(x)
         eng = self._engine()
         params = [p for _, p in eng.named_params()]
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):

@@ -22,6 +22,55 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+class KernelTimer:
+    """Brackets selected kernel launches with HIP events on the stream they are
+    launched on (the current stream), for per-launch durations inside a timed
+    region.  ``classes``: name -> predicate(op_name, args_dict)."""
+
+    def __init__(self, classes):
+        self.classes = classes
+        self.events = {k: [] for k in classes}
+
+    def match(self, op, a):
+        for k, pred in self.classes.items():
+            if pred(op, a):
+                return k
+        return None
+
+    def mean_ms(self, k):
+        ev = self.events.get(k) or []
+        if not ev:
+            return None
+        return sum(s.elapsed_time(e) for s, e in ev) / len(ev)
+
+    def count(self, k):
+        return len(self.events.get(k) or [])
+
+
+_timer = None
+
+
+def set_kernel_timer(t):
+    global _timer
+    _timer = t
+
+
+class _timed:
+    def __init__(self, op, a):
+        self.key = _timer.match(op, a) if _timer is not None else None
+
+    def __enter__(self):
+        if self.key is not None:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.e = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+
+    def __exit__(self, *exc):
+        if self.key is not None:
+            self.e.record()
+            _timer.events[self.key].append((self.s, self.e))
+
+
 def check_gpu(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -31,8 +80,9 @@ def check_gpu(*ts):
 # ---------------------------------------------------------------- GEMM
 def gemm_nt(A, B, C, M, N, K, lda=None, ldb=None, ldc=None, stats=None, gather=(0, 0, 0, 0, 0, 1, 0)):
     dt = DT[A.dtype]
-    _lib.call("xcp_gemm_nt", dt, _p(A), lda or K, _p(B), ldb or K, _p(C), ldc or N, M, N, K, _p(stats), *gather,
-              stream())
+    with _timed("gemm_nt", {"M": M, "N": N, "K": K, "stats": stats}):
+        _lib.call("xcp_gemm_nt", dt, _p(A), lda or K, _p(B), ldb or K, _p(C), ldc or N, M, N, K, _p(stats), *gather,
+                  stream())
 
 
 def gemm_tn(G, X, P, M, N, K, S, rows_per_split, ldg=None, ldx=None, gather=(0, 0, 0, 0, 0, 1, 0)):
@@ -83,7 +133,8 @@ def weight_grad(G, X, M, N, K, out, gather=(0, 0, 0, 0, 0, 1, 0), ldg=None, ldx=
 
 # ---------------------------------------------------------------- depthwise
 def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
-    _lib.call("xcp_dw_fwd", DT[X.dtype], act, _p(X), _p(Y), _p(Wt), _p(scale), _p(shift), N, H, W, C, stream())
+    with _timed("dw_fwd", {"N": N, "H": H, "W": W, "C": C}):
+        _lib.call("xcp_dw_fwd", DT[X.dtype], act, _p(X), _p(Y), _p(Wt), _p(scale), _p(shift), N, H, W, C, stream())
 
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1)):

@@ -1,0 +1,294 @@
+"""Per-kernel numerics on the MI355X: every xcp kernel against a plain PyTorch fp32
+reference of the same op (run on the same device).  Tolerances: fp32 mode 1e-4
+relative (exact-fp32 MFMA, different summation order); bf16 mode checks against
+the fp32 reference of the bf16-rounded inputs with 2e-2 relative."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = [torch.float32, torch.bfloat16]
+
+
+def tol(dt):
+    return dict(rtol=1e-4, atol=1e-4) if dt == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def nhwc(x):  # [N,C,H,W] -> [N,H,W,C] contiguous
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+@pytest.fixture(scope="module")
+def ops(gpu):
+    from xcp import ops as o
+    o._lib.load()
+    return o
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,N,K", [(256, 128, 64), (1000, 728, 728), (361 * 3, 1024, 728), (100, 2048, 1536),
+                                   (77, 64, 288)])
+def test_gemm_nt_stats(ops, gpu, dt, M, N, K):
+    g = torch.Generator(device=gpu).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=gpu, generator=g).to(dt)
+    B = torch.randn(N, K, device=gpu, generator=g).to(dt) / K ** 0.5
+    C = torch.empty(M, N, device=gpu, dtype=dt)
+    R = ops.nt_stat_rows(M)
+    part = torch.empty(R, 2, N, device=gpu)
+    ops.gemm_nt(A, B, C, M, N, K, stats=part)
+    ref = A.float() @ B.float().t()
+    assert rel_err(C.float(), ref) < (1e-5 if dt == torch.float32 else 1e-2)
+    s = part.double().sum(0)
+    Cs = C.double()
+    torch.testing.assert_close(s[0], Cs.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(s[1], (Cs * Cs).sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_nt_strided_gather(ops, gpu, dt):
+    N, H, W, Cin, Cout = 3, 37, 37, 256, 728
+    x = torch.randn(N, Cin, H, W, device=gpu).to(dt)
+    w = torch.randn(Cout, Cin, 1, 1, device=gpu) / Cin ** 0.5
+    ref = F.conv2d(x.float(), w, stride=2)
+    OH, OW = ref.shape[2:]
+    Y = torch.empty(N * OH * OW, Cout, device=gpu, dtype=dt)
+    ops.gemm_nt(nhwc(x), w.reshape(Cout, Cin).to(dt).contiguous(), Y, N * OH * OW, Cout, Cin, lda=Cin,
+                gather=(1, H, W, OH, OW, 2, 0))
+    assert rel_err(nchw(Y.view(N, OH, OW, Cout)).float(), ref) < (1e-5 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_im2col_conv2_fwd_and_dgrad(ops, gpu, dt):
+    N, H, W = 2, 21, 19
+    x = torch.randn(N, 32, H, W, device=gpu).to(dt)
+    w = (torch.randn(64, 32, 3, 3, device=gpu) / 17).requires_grad_(True)
+    xr = x.float().requires_grad_(True)
+    ref = F.conv2d(xr, w)
+    OH, OW = H - 2, W - 2
+    wp = w.detach().permute(0, 2, 3, 1).reshape(64, 288).to(dt).contiguous()
+    Y = torch.empty(N * OH * OW, 64, device=gpu, dtype=dt)
+    ops.gemm_nt(nhwc(x), wp, Y, N * OH * OW, 64, 288, lda=32, gather=(2, H, W, OH, OW, 1, 32))
+    assert rel_err(nchw(Y.view(N, OH, OW, 64)).float(), ref) < (1e-5 if dt == torch.float32 else 1e-2)
+    dy = torch.randn_like(ref).to(dt)
+    ref.backward(dy.float())
+    wt = w.detach().permute(1, 2, 3, 0).reshape(32, 576).to(dt).contiguous()
+    dX = torch.empty(N * H * W, 32, device=gpu, dtype=dt)
+    ops.gemm_nt(nhwc(dy), wt, dX, N * H * W, 32, 576, lda=64, gather=(3, H, W, OH, OW, 1, 64))
+    assert rel_err(nchw(dX.view(N, H, W, 32)).float(), xr.grad) < (1e-5 if dt == torch.float32 else 1e-2)
+    # weight gradient via im2col TN gather, k = tap*32 + ci
+    wg = torch.empty(64 * 288, device=gpu)
+    ops.weight_grad(nhwc(dy), nhwc(x), N * OH * OW, 64, 288, wg, gather=(2, H, W, OH, OW, 1, 32), ldx=32)
+    wg = wg.view(64, 3, 3, 32).permute(0, 3, 1, 2)
+    assert rel_err(wg, w.grad) < (1e-5 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,N,K", [(5000, 128, 64), (92416 // 16, 728, 728), (300, 2048, 1536), (33, 512, 2048)])
+def test_gemm_tn(ops, gpu, dt, M, N, K):
+    g = torch.Generator(device=gpu).manual_seed(M)
+    G = torch.randn(M, N, device=gpu, generator=g).to(dt)
+    X = torch.randn(M, K, device=gpu, generator=g).to(dt)
+    out = torch.empty(N * K, device=gpu)
+    ops.weight_grad(G, X, M, N, K, out)
+    ref = G.float().t() @ X.float()
+    assert rel_err(out.view(N, K), ref) < (1e-5 if dt == torch.float32 else 1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9)])
+def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
+    W = H + 1
+    g = torch.Generator(device=gpu).manual_seed(C + H + act)
+    x = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
+    w = (torch.randn(C, 1, 3, 3, device=gpu, generator=g) / 3).requires_grad_(True)
+    sc = torch.rand(C, device=gpu, generator=g) + 0.5
+    sh = torch.randn(C, device=gpu, generator=g) * 0.2
+    xr = x.float().requires_grad_(True)
+    if act == 0:
+        a = xr
+    elif act == 1:
+        a = F.relu(xr)
+    else:
+        a = F.relu(xr * sc.view(1, C, 1, 1) + sh.view(1, C, 1, 1))
+    a.retain_grad()
+    ref = F.conv2d(a, w, None, 1, 1, 1, C)
+    Wt = w.detach().reshape(C, 9).t().contiguous()
+    Y = torch.empty(N * H * W, C, device=gpu, dtype=dt)
+    ops.dw_fwd(act, nhwc(x), Y, Wt, sc, sh, N, H, W, C)
+    assert rel_err(nchw(Y.view(N, H, W, C)).float(), ref) < (1e-6 if dt == torch.float32 else 1e-2)
+    dy = torch.randn(ref.shape, device=gpu, generator=g).to(dt)
+    ref.backward(dy.float())
+    # kernel output = gradient w.r.t. the transform's output (BN output for act 2) after the ReLU mask
+    if act == 0:
+        want = xr.grad
+    elif act == 1:
+        want = xr.grad
+    else:
+        z = xr.detach() * sc.view(1, C, 1, 1) + sh.view(1, C, 1, 1)
+        want = a.grad * (z > 0)
+    dX = torch.empty(N * H * W, C, device=gpu, dtype=dt)
+    dW = torch.empty(C * 9, device=gpu)
+    ops.dw_bwd(act, nhwc(dy), nhwc(x), Wt, sc, sh, dX, dW, N, H, W, C)
+    assert rel_err(nchw(dX.view(N, H, W, C)).float(), want) < (1e-6 if dt == torch.float32 else 1e-2)
+    assert rel_err(dW.view(C, 1, 3, 3), w.grad) < (1e-5 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_dw_bwd_residual_and_skip(ops, gpu, dt):
+    N, C, H, W = 2, 128, 15, 15
+    x = torch.randn(N, C, H, W, device=gpu).to(dt)
+    w = torch.randn(C, 1, 3, 3, device=gpu) / 3
+    Wt = w.reshape(C, 9).t().contiguous()
+    dy = torch.randn(N, C, H, W, device=gpu).to(dt)
+    res = torch.randn(N, C, H, W, device=gpu).to(dt)
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    sk = torch.randn(N, C, OH, OW, device=gpu).to(dt)
+    base = torch.empty(N * H * W, C, device=gpu, dtype=dt)
+    dW = torch.empty(C * 9, device=gpu)
+    ops.dw_bwd(1, nhwc(dy), nhwc(x), Wt, None, None, base, dW, N, H, W, C)
+    out = torch.empty_like(base)
+    ops.dw_bwd(1, nhwc(dy), nhwc(x), Wt, None, None, out, dW, N, H, W, C, dRes=nhwc(res), dSkip=nhwc(sk),
+               skip_geom=(OH, OW, 2))
+    want = nchw(base.view(N, H, W, C)).float() + res.float()
+    want[:, :, ::2, ::2] += sk.float()
+    assert rel_err(nchw(out.view(N, H, W, C)).float(), want) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("rows,C", [(100000, 128), (3 * 361, 728), (50, 2048)])
+def test_bn_forward_backward(ops, gpu, dt, rows, C):
+    from xcp.engine import Stats
+    g = torch.Generator(device=gpu).manual_seed(rows)
+    y = (torch.randn(rows, C, device=gpu, generator=g) * 2 + 0.7).to(dt)
+    gamma = (torch.rand(C, device=gpu, generator=g) + 0.5).requires_grad_(True)
+    beta = (torch.randn(C, device=gpu, generator=g) * 0.1).requires_grad_(True)
+    rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    part, R = ops.row_stats(y, rows, C)
+    st = Stats(C, gpu)
+    bn = {"weight": gamma, "bias": beta, "running_mean": rm, "running_var": rv, "eps": 1e-5, "momentum": 0.1,
+          "track": True}
+    ops.finalize_stats(part, R, C, rows, bn, True, st)
+    yr = y.float().requires_grad_(True)
+    rm2, rv2 = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    z = F.batch_norm(yr, rm2, rv2, gamma, beta, True, 0.1, 1e-5)
+    torch.testing.assert_close(rm, rm2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv, rv2, rtol=1e-5, atol=1e-6)
+    zk = torch.empty(rows, C, device=gpu, dtype=dt)
+    ops.bn_act(y, zk, st.scale, st.shift, False, rows, C)
+    assert rel_err(zk.float(), z) < (1e-6 if dt == torch.float32 else 1e-2)
+    dz = torch.randn(rows, C, device=gpu, generator=g).to(dt)
+    z.backward(dz.float())
+    dY = torch.empty(rows, C, device=gpu, dtype=dt)
+    dg, db = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+    ops.bn_backward(dz, y, rows, C, bn, st, dY, dg, db)
+    assert rel_err(dY.float(), yr.grad) < (1e-4 if dt == torch.float32 else 2e-2)
+    torch.testing.assert_close(dg, gamma.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db, beta.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("H", [147, 37, 19])
+def test_tail_maxpool_fwd_bwd(ops, gpu, dt, H):
+    N, C = 2, 128
+    g = torch.Generator(device=gpu).manual_seed(H)
+    y = torch.randn(N, C, H, H, device=gpu, generator=g).to(dt)
+    s1 = torch.rand(C, device=gpu, generator=g) + 0.5
+    t1 = torch.randn(C, device=gpu, generator=g)
+    OH = (H - 1) // 2 + 1
+    ys = torch.randn(N, C, OH, OH, device=gpu, generator=g).to(dt)
+    s2 = torch.rand(C, device=gpu, generator=g) + 0.5
+    t2 = torch.randn(C, device=gpu, generator=g)
+    zr = (y.float() * s1.view(1, C, 1, 1) + t1.view(1, C, 1, 1)).requires_grad_(True)
+    pooled = F.max_pool2d(zr, 3, 2, 1)
+    ref = pooled + ys.float() * s2.view(1, C, 1, 1) + t2.view(1, C, 1, 1)
+    out = torch.empty(N * OH * OH, C, device=gpu, dtype=dt)
+    amax = torch.empty(N * OH * OH * C, device=gpu, dtype=torch.uint8)
+    ops.tail_fwd(nhwc(y), s1, t1, True, nhwc(ys), s2, t2, out, amax, N, H, H, C)
+    assert rel_err(nchw(out.view(N, OH, OH, C)).float(), ref) < (1e-6 if dt == torch.float32 else 1e-2)
+    d = torch.randn(ref.shape, device=gpu, generator=g).to(dt)
+    pooled.backward(d.float())
+    dz = torch.empty(N * H * H, C, device=gpu, dtype=dt)
+    ops.maxpool_bwd(nhwc(d), amax, dz, N, H, H, C)
+    assert rel_err(nchw(dz.view(N, H, H, C)).float(), zr.grad) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_avgpool(ops, gpu, dt):
+    N, C, H = 3, 2048, 10
+    y = torch.randn(N, C, H, H, device=gpu).to(dt)
+    s = torch.rand(C, device=gpu) + 0.5
+    t = torch.randn(C, device=gpu)
+    zr = (y.float() * s.view(1, C, 1, 1) + t.view(1, C, 1, 1)).requires_grad_(True)
+    ref = F.adaptive_avg_pool2d(F.relu(zr), 1).view(N, C)
+    Fo = torch.empty(N, C, device=gpu)
+    ops.avgpool_fwd(nhwc(y), s, t, Fo, N, H * H, C)
+    torch.testing.assert_close(Fo, ref, **tol(dt))
+    dF = torch.randn(N, C, device=gpu)
+    ref.backward(dF)
+    dz = torch.empty(N * H * H, C, device=gpu, dtype=dt)
+    ops.avgpool_bwd(dF, nhwc(y), s, t, dz, N, H * H, C)
+    assert rel_err(nchw(dz.view(N, H, H, C)).float(), zr.grad) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_conv1_fwd_wgrad(ops, gpu, dt):
+    N, IH = 2, 75
+    x = torch.rand(N, 3, IH, IH, device=gpu)
+    w = (torch.randn(32, 3, 3, 3, device=gpu) / 5).requires_grad_(True)
+    ref = F.conv2d(x, w, None, 2, 0)
+    OH = ref.shape[2]
+    Y = torch.empty(N * OH * OH, 32, device=gpu, dtype=dt)
+    ops.conv1_fwd(x, w.detach().contiguous(), Y, N, IH, IH)
+    assert rel_err(nchw(Y.view(N, OH, OH, 32)).float(), ref) < (1e-6 if dt == torch.float32 else 1e-2)
+    dy = torch.randn(ref.shape, device=gpu).to(dt)
+    ref.backward(dy.float())
+    dW = torch.empty(32 * 27, device=gpu)
+    ops.conv1_wgrad(x, nhwc(dy), dW, N, IH, IH)
+    assert rel_err(dW.view(32, 3, 3, 3), w.grad) < (1e-5 if dt == torch.float32 else 1e-2)
+
+
+def test_permute3(ops, gpu):
+    x = torch.randn(5, 7, 9, device=gpu)
+    for perm in [(0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0)]:
+        out = torch.empty(x.numel(), device=gpu)
+        ops.permute3(x, out, 5, 7, 9, perm)
+        assert torch.equal(out.view([x.shape[p] for p in perm]), x.permute(*perm))
+    ob = torch.empty(x.numel(), device=gpu, dtype=torch.bfloat16)
+    ops.permute3(x, ob, 5, 7, 9, (2, 0, 1))
+    assert torch.equal(ob.view(9, 5, 7), x.permute(2, 0, 1).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("H,T", [(128, 16), (512, 12)])
+def test_lstm_module_vs_oracle(gpu, golden, H, T):
+    import numpy as np
+    from xcp.lstm import LSTM
+    g = golden("lstm.npz")
+    torch.manual_seed(0)
+    lstm = LSTM(2048, H, 1, batch_first=True).to(gpu)
+    x = torch.randn((2, T, 2048), generator=torch.Generator().manual_seed(555)).to(gpu).requires_grad_(True)
+    o, (h, c) = lstm(x)
+    p = f"H{H}"
+    np.testing.assert_allclose(o.detach().cpu().numpy(), g[f"{p}/out"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(h.detach().cpu().numpy(), g[f"{p}/h_n"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(c.detach().cpu().numpy(), g[f"{p}/c_n"], rtol=1e-4, atol=1e-5)
+    r = torch.randn(o.shape, generator=torch.Generator().manual_seed(556)).to(gpu)
+    rh = torch.randn(h.shape, generator=torch.Generator().manual_seed(557)).to(gpu)
+    ((o * r).sum() + (c * rh).sum()).backward()
+    np.testing.assert_allclose(x.grad.cpu().numpy(), g[f"{p}/dx"], rtol=1e-3, atol=1e-5)
+    for n, prm in lstm.named_parameters():
+        ref = g[f"{p}/grad/{n}"]
+        if ref.ndim == 0:
+            np.testing.assert_allclose(prm.grad.double().norm().item(), ref, rtol=1e-4)
+        else:
+            np.testing.assert_allclose(prm.grad.cpu().numpy(), ref, rtol=1e-3, atol=1e-5)
