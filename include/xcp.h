@@ -56,11 +56,16 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
 int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift, int N,
                int H, int W, int C, xcp_stream_t stream);
 /* fused backward: dX = act'(X) * dgrad(dY) + dRes + scatter_stride(dSkip);
- * dWpart[P][C][9] block partials of the weight gradient, P = xcp_dw_bwd_chunks(). */
+ * dWpart[P][C][9] workgroup partials of the weight gradient, P = xcp_dw_bwd_chunks();
+ * optional bnpart[P][2][C] = (sum dX, sum dX*(X-bmean)*binvstd): the backward
+ * partial sums of the BatchNorm that produced X (XCP_ACT_BNRELU only). */
 int xcp_dw_bwd_chunks(int N, int H, int W, int C);
+/* launch tuning knobs: 0 = depthwise forward / 1 = depthwise backward halo pixels per
+ * LDS tile (256 or 512).  Returns the previous value (-1: unknown knob). */
+int xcp_tune(int knob, int value);
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
-               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, int N, int H, int W,
-               int C, xcp_stream_t stream);
+               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, float* bnpart,
+               const float* bmean, const float* binvstd, int N, int H, int W, int C, xcp_stream_t stream);
 
 /* ---- BatchNorm2d (Xception.py:56,67,73,78,119,123,143,147), tails, pooling ---- */
 int xcp_colreduce_f64(const float* in, int S, long L, double* out, int G, xcp_stream_t stream);

@@ -23,7 +23,8 @@ SIGNATURES = {
     "xcp_gemm_tn": [I, P, L, P, L, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
-    "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, P, P, I, I, I, I, P],
+    "xcp_tune": [I, I],
+    "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_colreduce_f64": [P, I, L, P, I, P],
     "xcp_colreduce_f32": [P, I, L, P, I, P],
     "xcp_chanred_parts": [L, I],
@@ -47,7 +48,7 @@ SIGNATURES = {
 }
 
 # entry points that return a size, not a status
-SIZE_QUERIES = {"xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts"}
+SIZE_QUERIES = {"xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts", "xcp_tune"}
 
 _lib = None
 

@@ -1,28 +1,142 @@
 // Depthwise 3x3 convolution (stride 1, pad 1, no bias), NHWC, forward and fused
-// backward (dgrad + wgrad + activation mask + residual / skip-gradient adds).
+// backward (dgrad + wgrad + activation mask + residual / skip-gradient adds +
+// the BatchNorm-backward partial sums of the preceding BN).
 //
 // Reference op: SeparableConv2d.conv1 = nn.Conv2d(C, C, 3, 1, 1, groups=C,
 // bias=False) (Xception.py:41, called at :45), always preceded in the
 // backbone by a ReLU and usually by the previous BatchNorm (Block.rep,
-// Xception.py:61-87).  That input transform is applied on load:
-//   ACT_NONE   : a = x                         (block1's first rep, Xception.py:80-81)
-//   ACT_RELU   : a = max(x, 0)                 (first rep of blocks 2-12, :83)
-//   ACT_BNRELU : a = max(x*scale[c]+shift[c],0) (BN of the previous rep + ReLU)
-// HBM-bound: every thread owns CPT channels of a strip of R output pixels along
-// W and slides a 3x3 register window, so each input vector is fetched ~once.
+// Xception.py:61-87).  That input transform is applied when the tile is staged:
+//   ACT_NONE   : a = x                          (block1's first rep, Xception.py:80-81; conv3)
+//   ACT_RELU   : a = max(x, 0)                  (first rep of blocks 2-12, :83)
+//   ACT_BNRELU : a = max(x*scale[c]+shift[c], 0) (BN of the previous rep + ReLU)
+//
+// HBM-bound.  One workgroup = one spatial tile (TH x TW outputs) of one image for
+// one 64-byte channel slice (32 bf16 / 16 fp32 channels).  The (TH+2) x
+// (nseg*SEGL+2) halo of the input (and of dY in the backward) is staged into LDS
+// in the storage type with 16-byte loads, all issued before the first is consumed,
+// the activation applied once at staging.  Each lane then owns one dword of
+// channels (2 bf16 / 1 fp32) and computes SEGL outputs of a row segment from a
+// fully unrolled 3 x (SEGL+2) register window.  MAXPX (halo pixels per staged
+// tensor) trades halo re-reads against workgroups per CU; it is a launch knob
+// (xcp_tune) so both can be measured.
 #include "common.h"
 
 namespace {
 
-template <int ACT, int CPT>
-XCP_DEV void act_apply(float* v, const float* sc, const float* sh) {
-  if constexpr (ACT == ACT_RELU) {
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) v[j] = fmaxf(v[j], 0.f);
-  } else if constexpr (ACT == ACT_BNRELU) {
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) v[j] = fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f);
+constexpr int SLICE = 64;     // bytes of channels per pixel per workgroup
+constexpr int NW = 16;        // row workers per workgroup (256 threads = 16 workers x 16 dword lanes)
+constexpr int SEGL = 5;       // output pixels per row segment
+
+int g_fwd_maxpx = 512;        // tuning knobs (xcp_tune 0 / 1)
+int g_bwd_maxpx = 512;
+
+// Tile of TH x TW outputs; the LDS tile is (TH+2) x (nseg*SEGL+2) so every
+// segment is exactly SEGL wide (columns past TW / W are computed, never stored).
+struct TileGeo {
+  int TH, TW, HP, WP, nth, ntw, nseg;
+};
+
+inline TileGeo tile_geo(int H, int W, int maxpx) {
+  TileGeo g;
+  g.ntw = (W + 39) / 40;
+  g.TW = (W + g.ntw - 1) / g.ntw;
+  g.nseg = (g.TW + SEGL - 1) / SEGL;
+  g.WP = g.nseg * SEGL + 2;
+  int thmax = maxpx / g.WP - 2;
+  if (thmax < 1) thmax = 1;
+  g.nth = (H + thmax - 1) / thmax;
+  g.TH = (H + g.nth - 1) / g.nth;
+  g.HP = g.TH + 2;
+  return g;
+}
+
+template <typename T> struct DT;
+template <> struct DT<bf16> { static constexpr int EPT = 2; };
+template <> struct DT<float> { static constexpr int EPT = 1; };
+
+// dword <-> EPT floats
+XCP_DEV void unpack(unsigned u, float* v, bf16*) {
+  v[0] = __uint_as_float(u << 16);
+  v[1] = __uint_as_float(u & 0xffff0000u);
+}
+XCP_DEV void unpack(unsigned u, float* v, float*) { v[0] = __uint_as_float(u); }
+XCP_DEV unsigned pack(const float* v, bf16*) {
+  bf16x4 q;  // hardware RNE conversion (v_cvt_pk_bf16_f32)
+  q[0] = (bf16)v[0];
+  q[1] = (bf16)v[1];
+  const u16x4 r = __builtin_bit_cast(u16x4, q);
+  return (unsigned)r[0] | ((unsigned)r[1] << 16);
+}
+XCP_DEV unsigned pack(const float* v, float*) { return __float_as_uint(v[0]); }
+
+template <int ACT>
+XCP_DEV float act1(float x, float s, float t) {
+  if constexpr (ACT == ACT_RELU) return fmaxf(x, 0.f);
+  else if constexpr (ACT == ACT_BNRELU) return fmaxf(fmaf(x, s, t), 0.f);
+  else return x;
+}
+
+// Stage the halo of tensor `src` (pixel rows of C channels) into LDS `dst`
+// ([HP*WP][SLICE bytes]); with TRANSFORM the activation is applied.  All global
+// loads of a thread are issued before any is consumed (unconditional loads from a
+// clamped address, zero-selected afterwards).
+template <typename T, int ACT, bool TRANSFORM, int MAXPX>
+XCP_DEV void stage(const T* __restrict__ src, char* dst, const TileGeo& g, long nbase, int th0, int tw0, int H, int W,
+                   int C, int c0, const float* scale, const float* shift) {
+  constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B chunk
+  constexpr int CPP = SLICE / 16;            // chunks per pixel slice
+  constexpr int MAXIT = MAXPX * CPP / 256;
+  const int total = g.HP * g.WP * CPP;
+  static_assert(256 % CPP == 0, "a thread's chunk column must be fixed");
+  // this thread always stages the same 16-B channel chunk: fetch its BN affine once
+  float sc[EPC], sh[EPC];
+  if constexpr (TRANSFORM && ACT == ACT_BNRELU) {
+    const int cq = min(c0 + (int)(threadIdx.x % CPP) * EPC, C - EPC);
+    VecIO<float, EPC>::load(scale + cq, sc);
+    VecIO<float, EPC>::load(shift + cq, sh);
   }
+  uint4 v[MAXIT];
+  bool ok[MAXIT];
+#pragma unroll
+  for (int k = 0; k < MAXIT; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    const int p = i / CPP, q = i - p * CPP;
+    const int hy = p / g.WP, hx = p - hy * g.WP;
+    const int h = th0 - 1 + hy, w = tw0 - 1 + hx;
+    const int c = c0 + q * EPC;
+    ok[k] = i < total && h >= 0 && h < H && w >= 0 && w < W && c < C;
+    const T* ptr = ok[k] ? src + (nbase + (long)h * W + w) * C + c : src;
+    v[k] = *reinterpret_cast<const uint4*>(ptr);
+  }
+#pragma unroll
+  for (int k = 0; k < MAXIT; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    if (i >= total) break;
+    const int p = i / CPP, q = i - p * CPP;
+    uint4 u = ok[k] ? v[k] : make_uint4(0, 0, 0, 0);
+    if constexpr (TRANSFORM && ACT != ACT_NONE) {
+      if (ok[k]) {
+        float f[EPC];
+        VecIO<T, EPC>::load(reinterpret_cast<const T*>(&u), f);
+#pragma unroll
+        for (int j = 0; j < EPC; ++j) f[j] = act1<ACT>(f[j], sc[j], sh[j]);
+        VecIO<T, EPC>::store(reinterpret_cast<T*>(&u), f);
+      }
+    }
+    *reinterpret_cast<uint4*>(dst + p * SLICE + q * 16) = u;
+  }
+}
+
+XCP_DEV int block_coords(int ngroups, const TileGeo& g, int& grp, int& n, int& th0, int& tw0) {
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  grp = id % ngroups;
+  const int sp = id / ngroups;
+  const int ntiles = g.nth * g.ntw;
+  const int tile = sp % ntiles;
+  n = sp / ntiles;
+  th0 = (tile / g.ntw) * g.TH;
+  tw0 = (tile % g.ntw) * g.TW;
+  return sp;
 }
 
 struct DwArgs {
@@ -31,309 +145,325 @@ struct DwArgs {
   const float* Wt;      // [9][C] taps (tap = ky*3+kx)
   const float* scale;   // [C] (ACT_BNRELU)
   const float* shift;   // [C]
-  int N, H, W, C, R, nstrips;
+  int N, H, W, C, ngroups;
+  TileGeo g;
 };
 
-template <typename T, int ACT, int CPT>
+template <typename T, int ACT, int MAXPX>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
-  const int CV = a.C / CPT;
-  const long g = (long)blockIdx.x * 256 + threadIdx.x;
-  const int cv = (int)(g % CV);
-  const long u = g / CV;
-  const int strip = (int)(u % a.nstrips);
-  const long row = u / a.nstrips;   // n*H + h
-  if (row >= (long)a.N * a.H) return;
-  const int h = (int)(row % a.H);
-  const long nbase = (row - h) * a.W;   // pixel index of (n, 0, 0)
-  const int c0 = cv * CPT;
-  const int w0 = strip * a.R, w1 = min(a.W, w0 + a.R);
-  const T* X = reinterpret_cast<const T*>(a.X);
+  constexpr int EPT = DT<T>::EPT;
+  constexpr int CPG = SLICE / (int)sizeof(T);   // channels per group
+  __shared__ __attribute__((aligned(16))) char sA[MAXPX * SLICE];
+  const TileGeo& g = a.g;
+  int grp, n, th0, tw0;
+  block_coords(a.ngroups, g, grp, n, th0, tw0);
+  const int c0 = grp * CPG;
+  const long nbase = (long)n * a.H * a.W;
+  const int cl = threadIdx.x & 15, wk = threadIdx.x >> 4;
+  const int c = c0 + cl * EPT;
+  const int cc = c < a.C ? c : a.C - EPT;
+  float wt[9][EPT];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) wt[t][e] = a.Wt[(long)t * a.C + cc + e];
+  stage<T, ACT, true, MAXPX>(reinterpret_cast<const T*>(a.X), sA, g, nbase, th0, tw0, a.H, a.W, a.C, c0, a.scale,
+                             a.shift);
+  __syncthreads();
+  if (c >= a.C) return;
   T* Y = reinterpret_cast<T*>(a.Y);
-
-  float wt[9][CPT], sc[CPT], sh[CPT];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) VecIO<float, CPT>::load(a.Wt + (long)t * a.C + c0, wt[t]);
-  if constexpr (ACT == ACT_BNRELU) {
-    VecIO<float, CPT>::load(a.scale + c0, sc);
-    VecIO<float, CPT>::load(a.shift + c0, sh);
-  }
-  auto ld = [&](int hh, int ww, float* v) {
-    if (hh < 0 || hh >= a.H || ww < 0 || ww >= a.W) {
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) v[j] = 0.f;
-      return;
-    }
-    VecIO<T, CPT>::load(X + (nbase + (long)hh * a.W + ww) * a.C + c0, v);
-    act_apply<ACT, CPT>(v, sc, sh);
-  };
-  float win[3][3][CPT];   // [ky][col: w-1,w,w+1][ch]
-#pragma unroll
-  for (int ky = 0; ky < 3; ++ky) {
-    ld(h + ky - 1, w0 - 1, win[ky][0]);
-    ld(h + ky - 1, w0, win[ky][1]);
-  }
-  for (int w = w0; w < w1; ++w) {
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) ld(h + ky - 1, w + 1, win[ky][2]);
-    float o[CPT];
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-      float s = 0.f;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][kx][j], wt[ky * 3 + kx][j], s);
-      o[j] = s;
-    }
-    VecIO<T, CPT>::store(Y + (nbase + (long)h * a.W + w) * a.C + c0, o);
+  const int items = g.TH * g.nseg;
+  const char* lbase = sA + cl * 4;
+  for (int it = wk; it < items; it += NW) {
+    const int r = it / g.nseg, sg = it - r * g.nseg;
+    const int oh = th0 + r;
+    const int x0 = sg * SEGL;
+    if (oh >= a.H) continue;
+    const char* base = lbase + (r * g.WP + x0) * SLICE;
+    float win[3][SEGL + 2][EPT];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int j = 0; j < CPT; ++j) {
-        win[ky][0][j] = win[ky][1][j];
-        win[ky][1][j] = win[ky][2][j];
+      for (int k = 0; k < SEGL + 2; ++k)
+        unpack(*reinterpret_cast<const unsigned*>(base + (ky * g.WP + k) * SLICE), win[ky][k], (T*)nullptr);
+    T* yrow = Y + (nbase + (long)oh * a.W + tw0) * a.C + c;
+#pragma unroll
+    for (int j = 0; j < SEGL; ++j) {
+      float o[EPT];
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) {
+        float s = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
+        o[e] = s;
       }
+      const int x = x0 + j;
+      if (x < g.TW && tw0 + x < a.W) *reinterpret_cast<unsigned*>(yrow + (long)x * a.C) = pack(o, (T*)nullptr);
+    }
   }
 }
 
 // ---------------------------------------------------------------------------------
-// Fused backward.  Per output-gradient pixel p:
+// Fused backward.  Per pixel p of the tile:
 //   dA[p]   = sum_tap dY[p - off(tap)] * w[tap]          (transposed 3x3)
-//   dX[p]   = act'(p) * dA[p] + dRes[p] + (p at even (h,w) ? dSkip[p/2] : 0)
-//   dW[tap] += dY[p] * a[p + off(tap)]                   (block partial -> slab)
-// act'(p) = (a[p] > 0) for ACT_RELU / ACT_BNRELU (gradient w.r.t. the BN output
-// for ACT_BNRELU), 1 for ACT_NONE.
+//   dX[p]   = act'(p) * dA[p] + dRes[p] + (p at stride-multiple (h,w) ? dSkip[p/s] : 0)
+//   dW[tap] += dY[p] * a[p + off(tap)]                   (workgroup partial -> slab)
+// act'(p) = (a[p] > 0) for ACT_RELU / ACT_BNRELU, 1 for ACT_NONE.  For ACT_BNRELU
+// dX is the gradient w.r.t. the preceding BN's output z; when bnpart is given the
+// workgroup also emits that BN's backward partial sums (sum dz, sum dz*zhat) with
+// zhat = (x - mean) * invstd, taken over the stored (rounded) dz.
 struct DwBwdArgs {
-  const void* dY;       // [N,H,W,C] gradient of the depthwise output
-  const void* X;        // [N,H,W,C] raw depthwise input (pre-transform)
-  const float* Wt;      // [9][C]
+  const void* dY;
+  const void* X;
+  const float* Wt;
   const float* scale;
   const float* shift;
-  const void* dRes;     // [N,H,W,C] or null (identity-skip gradient)
-  const void* dSkip;    // [N,OH,OW,C] or null (stride-2 skip-conv input gradient)
+  const void* dRes;
+  const void* dSkip;
   int sOH, sOW, sS;
-  void* dX;             // [N,H,W,C] out
-  float* dWpart;        // [P][C][9] per-block-row partials
-  int N, H, W, C, R, nstrips;
-  int CVB, SPB;         // channel-vectors per block, strip slots per block
-  long strips_per_chunk;
+  void* dX;
+  float* dWpart;          // [P][C][9]
+  float* bnpart;          // [P][2][C] or null
+  const float* bmean;
+  const float* binvstd;
+  int N, H, W, C, ngroups;
+  TileGeo g;
 };
 
-template <typename T, int ACT, int CPT>
+template <typename T, int ACT, int MAXPX>
 __global__ __launch_bounds__(256) void dw_bwd_kernel(DwBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float red[];   // [SPB][CVB*CPT*9]
-  const int CV = a.C / CPT;
-  const int nchunks = (CV + a.CVB - 1) / a.CVB;
-  const int cchunk = blockIdx.x % nchunks;
-  const int pchunk = blockIdx.x / nchunks;
-  const int tid = threadIdx.x;
-  const int lcv = tid % a.CVB, slot = tid / a.CVB;
-  const int cv = cchunk * a.CVB + lcv;
-  const bool active = slot < a.SPB && cv < CV;
-  const int c0 = cv * CPT;
-  const T* dY = reinterpret_cast<const T*>(a.dY);
+  constexpr int EPT = DT<T>::EPT;
+  constexpr int CPG = SLICE / (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) char sm[2 * MAXPX * SLICE];
+  char* sA = sm;
+  char* sG = sm + MAXPX * SLICE;
+  const TileGeo& g = a.g;
+  int grp, n, th0, tw0;
+  const int sp = block_coords(a.ngroups, g, grp, n, th0, tw0);
+  const int c0 = grp * CPG;
+  const long nbase = (long)n * a.H * a.W;
   const T* X = reinterpret_cast<const T*>(a.X);
-  const T* dRes = reinterpret_cast<const T*>(a.dRes);
-  const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
-  T* dX = reinterpret_cast<T*>(a.dX);
-
-  float wt[9][CPT], sc[CPT], sh[CPT], dw[9][CPT];
+  const int cl = threadIdx.x & 15, wk = threadIdx.x >> 4;
+  const int c = c0 + cl * EPT;
+  const bool cok = c < a.C;
+  const int cc = cok ? c : a.C - EPT;
+  const bool bnsum = a.bnpart != nullptr;
+  float wt[9][EPT], dw[9][EPT], bs1[EPT], bs2[EPT], mu[EPT], is[EPT];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int j = 0; j < CPT; ++j) dw[t][j] = 0.f;
-  if (active) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) VecIO<float, CPT>::load(a.Wt + (long)t * a.C + c0, wt[t]);
-    if constexpr (ACT == ACT_BNRELU) {
-      VecIO<float, CPT>::load(a.scale + c0, sc);
-      VecIO<float, CPT>::load(a.shift + c0, sh);
+    for (int e = 0; e < EPT; ++e) {
+      wt[t][e] = a.Wt[(long)t * a.C + cc + e];
+      dw[t][e] = 0.f;
     }
-    const long total = (long)a.N * a.H * a.nstrips;
-    const long sbeg = (long)pchunk * a.strips_per_chunk;
-    const long send = min(total, sbeg + a.strips_per_chunk);
-    for (long su = sbeg + slot; su < send; su += a.SPB) {
-      const int strip = (int)(su % a.nstrips);
-      const long row = su / a.nstrips;
-      const int h = (int)(row % a.H);
-      const int n = (int)(row / a.H);
-      const long nbase = (long)n * a.H * a.W;
-      const int w0 = strip * a.R, w1 = min(a.W, w0 + a.R);
-      auto ldx = [&](int hh, int ww, float* v) {
-        if (hh < 0 || hh >= a.H || ww < 0 || ww >= a.W) {
 #pragma unroll
-          for (int j = 0; j < CPT; ++j) v[j] = 0.f;
-          return;
+  for (int e = 0; e < EPT; ++e) {
+    bs1[e] = bs2[e] = 0.f;
+    mu[e] = bnsum ? a.bmean[cc + e] : 0.f;
+    is[e] = bnsum ? a.binvstd[cc + e] : 0.f;
+  }
+  stage<T, ACT, true, MAXPX>(X, sA, g, nbase, th0, tw0, a.H, a.W, a.C, c0, a.scale, a.shift);
+  stage<T, ACT_NONE, false, MAXPX>(reinterpret_cast<const T*>(a.dY), sG, g, nbase, th0, tw0, a.H, a.W, a.C, c0,
+                                   nullptr, nullptr);
+  __syncthreads();
+  const T* dRes = reinterpret_cast<const T*>(a.dRes);
+  const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
+  T* dX = reinterpret_cast<T*>(a.dX);
+  const bool has_res = dRes != nullptr, has_skip = dSkip != nullptr;
+  const int items = g.TH * g.nseg;
+  const char* la = sA + cl * 4;
+  const char* lg = sG + cl * 4;
+  if (cok) {
+    for (int it = wk; it < items; it += NW) {
+      const int r = it / g.nseg, sg = it - r * g.nseg;
+      const int oh = th0 + r;
+      const int x0 = sg * SEGL;
+      if (oh >= a.H) continue;
+      // per-pixel global terms of this segment, issued before the LDS work
+      unsigned pres[SEGL], pskp[SEGL], pxr[SEGL];
+#pragma unroll
+      for (int j = 0; j < SEGL; ++j) {
+        const int ow = min(tw0 + x0 + j, a.W - 1);
+        const long pix = nbase + (long)oh * a.W + ow;
+        pres[j] = has_res ? *reinterpret_cast<const unsigned*>(dRes + pix * a.C + c) : 0u;
+        pxr[j] = bnsum ? *reinterpret_cast<const unsigned*>(X + pix * a.C + c) : 0u;
+        if (has_skip) {
+          const int sh2 = min(oh / a.sS, a.sOH - 1), sw2 = min(ow / a.sS, a.sOW - 1);
+          pskp[j] = *reinterpret_cast<const unsigned*>(dSkip + (((long)n * a.sOH + sh2) * a.sOW + sw2) * a.C + c);
+        } else {
+          pskp[j] = 0u;
         }
-        VecIO<T, CPT>::load(X + (nbase + (long)hh * a.W + ww) * a.C + c0, v);
-        act_apply<ACT, CPT>(v, sc, sh);
-      };
-      auto ldg = [&](int hh, int ww, float* v) {
-        if (hh < 0 || hh >= a.H || ww < 0 || ww >= a.W) {
-#pragma unroll
-          for (int j = 0; j < CPT; ++j) v[j] = 0.f;
-          return;
-        }
-        VecIO<T, CPT>::load(dY + (nbase + (long)hh * a.W + ww) * a.C + c0, v);
-      };
-      float xa[3][3][CPT], gy[3][3][CPT];
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        ldx(h + ky - 1, w0 - 1, xa[ky][0]);
-        ldx(h + ky - 1, w0, xa[ky][1]);
-        ldg(h + ky - 1, w0 - 1, gy[ky][0]);
-        ldg(h + ky - 1, w0, gy[ky][1]);
       }
-      for (int w = w0; w < w1; ++w) {
+      const char* ba = la + (r * g.WP + x0) * SLICE;
+      const char* bg = lg + (r * g.WP + x0) * SLICE;
+      float xa[3][SEGL + 2][EPT], gy[3][SEGL + 2][EPT];
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          ldx(h + ky - 1, w + 1, xa[ky][2]);
-          ldg(h + ky - 1, w + 1, gy[ky][2]);
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int k = 0; k < SEGL + 2; ++k) {
+          const int off = (ky * g.WP + k) * SLICE;
+          unpack(*reinterpret_cast<const unsigned*>(ba + off), xa[ky][k], (T*)nullptr);
+          unpack(*reinterpret_cast<const unsigned*>(bg + off), gy[ky][k], (T*)nullptr);
         }
-        float o[CPT];
+      const bool skip_row = has_skip && (oh % a.sS) == 0 && oh / a.sS < a.sOH;
+      T* xrow = dX + (nbase + (long)oh * a.W + tw0) * a.C + c;
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) {
-          // dgrad: input pixel p receives dY[p - off] * w[off]; off = (ky-1, kx-1)
+      for (int j = 0; j < SEGL; ++j) {
+        const int x = x0 + j, ow = tw0 + x;
+        const bool valid = x < g.TW && ow < a.W;
+        float o[EPT];
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {
+          // window column k <-> tile column x0 + k - 1; the centre of output j is k = j + 1
           float s = 0.f;
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) s = fmaf(gy[2 - ky][2 - kx][j], wt[ky * 3 + kx][j], s);
-          // wgrad: dY[p] * a[p + off]
-          const float gc = gy[1][1][j];
+            for (int kx = 0; kx < 3; ++kx) s = fmaf(gy[2 - ky][j + 2 - kx][e], wt[ky * 3 + kx][e], s);
+          const float gc = valid ? gy[1][j + 1][e] : 0.f;
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) dw[ky * 3 + kx][j] = fmaf(gc, xa[ky][kx][j], dw[ky * 3 + kx][j]);
-          if constexpr (ACT != ACT_NONE) s = xa[1][1][j] > 0.f ? s : 0.f;
-          o[j] = s;
+            for (int kx = 0; kx < 3; ++kx) dw[ky * 3 + kx][e] = fmaf(gc, xa[ky][j + kx][e], dw[ky * 3 + kx][e]);
+          if constexpr (ACT != ACT_NONE) s = xa[1][j + 1][e] > 0.f ? s : 0.f;
+          o[e] = s;
         }
-        const long pix = nbase + (long)h * a.W + w;
-        if (dRes) {
-          float r[CPT];
-          VecIO<T, CPT>::load(dRes + pix * a.C + c0, r);
+        if (bnsum && valid) {
+          float xr[EPT], orr[EPT];
+          unpack(pxr[j], xr, (T*)nullptr);
+          unpack(pack(o, (T*)nullptr), orr, (T*)nullptr);   // the stored (rounded) dz
 #pragma unroll
-          for (int j = 0; j < CPT; ++j) o[j] += r[j];
-        }
-        if (dSkip && (h % a.sS) == 0 && (w % a.sS) == 0) {
-          const int oh = h / a.sS, ow = w / a.sS;
-          if (oh < a.sOH && ow < a.sOW) {
-            float r[CPT];
-            VecIO<T, CPT>::load(dSkip + (((long)n * a.sOH + oh) * a.sOW + ow) * a.C + c0, r);
-#pragma unroll
-            for (int j = 0; j < CPT; ++j) o[j] += r[j];
+          for (int e = 0; e < EPT; ++e) {
+            bs1[e] += orr[e];
+            bs2[e] = fmaf(orr[e], (xr[e] - mu[e]) * is[e], bs2[e]);
           }
         }
-        VecIO<T, CPT>::store(dX + pix * a.C + c0, o);
+        if (has_res) {
+          float rr[EPT];
+          unpack(pres[j], rr, (T*)nullptr);
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+          for (int e = 0; e < EPT; ++e) o[e] += rr[e];
+        }
+        if (skip_row && (ow % a.sS) == 0 && ow / a.sS < a.sOW) {
+          float rr[EPT];
+          unpack(pskp[j], rr, (T*)nullptr);
 #pragma unroll
-          for (int j = 0; j < CPT; ++j) {
-            xa[ky][0][j] = xa[ky][1][j];
-            xa[ky][1][j] = xa[ky][2][j];
-            gy[ky][0][j] = gy[ky][1][j];
-            gy[ky][1][j] = gy[ky][2][j];
-          }
+          for (int e = 0; e < EPT; ++e) o[e] += rr[e];
+        }
+        if (valid) *reinterpret_cast<unsigned*>(xrow + (long)x * a.C) = pack(o, (T*)nullptr);
       }
     }
   }
-  // block reduction of dw over strip slots
-  const int L = a.CVB * CPT * 9;
-  if (slot < a.SPB) {
+  // ---- workgroup reduction over the 16 row workers (reuse the staging LDS)
+  __syncthreads();
+  constexpr int PER = 11;                      // 9 taps + 2 BN sums
+  float* red = reinterpret_cast<float*>(sm);   // [NW][16 lanes][EPT][PER]
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+  for (int e = 0; e < EPT; ++e) {
+    float* rp = red + ((wk * 16 + cl) * EPT + e) * PER;
 #pragma unroll
-      for (int j = 0; j < CPT; ++j) red[slot * L + (lcv * CPT + j) * 9 + t] = dw[t][j];
+    for (int t = 0; t < 9; ++t) rp[t] = dw[t][e];
+    rp[9] = bs1[e];
+    rp[10] = bs2[e];
   }
   __syncthreads();
-  for (int i = tid; i < L; i += 256) {
+  constexpr int L = 16 * EPT * PER;
+  for (int i = threadIdx.x; i < L; i += 256) {
     float s = 0.f;
-    for (int q = 0; q < a.SPB; ++q) s += red[q * L + i];
-    const int c = cchunk * a.CVB * CPT + i / 9;
-    if (c < a.C) a.dWpart[((long)pchunk * a.C + c) * 9 + (i % 9)] = s;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += red[q * L + i];
+    const int k = i % PER, ch = c0 + i / PER;
+    if (ch >= a.C) continue;
+    if (k < 9) a.dWpart[((long)sp * a.C + ch) * 9 + k] = s;
+    else if (bnsum) a.bnpart[((long)sp * 2 + (k - 9)) * a.C + ch] = s;
   }
 }
 
+template <typename T, int MAXPX>
+void launch_fwd_px(int act, const DwArgs& a, int blocks, hipStream_t st) {
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_NONE, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_RELU, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_BNRELU, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
+}
+
+template <typename T, int MAXPX>
+void launch_bwd_px(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_NONE, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_RELU, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_BNRELU, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
+}
+
 template <typename T>
-int launch_fwd(int act, const DwArgs& a, hipStream_t st) {
-  constexpr int CPT = 8;
-  const long work = (long)a.N * a.H * a.nstrips * (a.C / CPT);
-  const dim3 grid((unsigned)((work + 255) / 256));
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_NONE, CPT>), grid, dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_RELU, CPT>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_BNRELU, CPT>), grid, dim3(256), 0, st, a);
+int launch_fwd(int act, const DwArgs& a, int maxpx, hipStream_t st) {
+  const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
+  if (maxpx == 512) launch_fwd_px<T, 512>(act, a, blocks, st);
+  else launch_fwd_px<T, 256>(act, a, blocks, st);
   return (int)hipGetLastError();
 }
 
 template <typename T>
-int launch_bwd(int act, const DwBwdArgs& a, int nblocks, hipStream_t st) {
-  constexpr int CPT = 4;
-  const size_t smem = (size_t)a.SPB * a.CVB * CPT * 9 * sizeof(float);
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_NONE, CPT>), dim3(nblocks), dim3(256), smem, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_RELU, CPT>), dim3(nblocks), dim3(256), smem, st, a);
-  else hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_BNRELU, CPT>), dim3(nblocks), dim3(256), smem, st, a);
+int launch_bwd(int act, const DwBwdArgs& a, int maxpx, hipStream_t st) {
+  const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
+  if (maxpx == 512) launch_bwd_px<T, 512>(act, a, blocks, st);
+  else launch_bwd_px<T, 256>(act, a, blocks, st);
   return (int)hipGetLastError();
 }
 
-int strip_len(int W) {
-  const int ns = (W + 7) / 8;
-  return (W + ns - 1) / ns;
+inline int ngroups_for(int C, int dtype) {
+  const int cpg = SLICE / (dtype == XCP_BF16 ? 2 : 4);
+  return (C + cpg - 1) / cpg;
 }
 
 }  // namespace
 
 extern "C" {
 
+// Tuning knobs: 0 = depthwise forward halo pixels per tile (256 | 512),
+// 1 = depthwise backward halo pixels per tile (256 | 512).  Returns the old value.
+int xcp_tune(int knob, int value) {
+  int* k = knob == 0 ? &g_fwd_maxpx : knob == 1 ? &g_bwd_maxpx : nullptr;
+  if (!k) return -1;
+  const int old = *k;
+  if (value == 256 || value == 512) *k = value;
+  return old;
+}
+
 int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift, int N,
                int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
-  DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, 0, 0};
-  a.R = strip_len(W);
-  a.nstrips = (W + a.R - 1) / a.R;
-  if (dtype == XCP_BF16) return launch_fwd<bf16>(act, a, stream);
-  if (dtype == XCP_F32) return launch_fwd<float>(act, a, stream);
+  const int maxpx = g_fwd_maxpx;
+  DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, maxpx)};
+  if (dtype == XCP_BF16) return launch_fwd<bf16>(act, a, maxpx, stream);
+  if (dtype == XCP_F32) return launch_fwd<float>(act, a, maxpx, stream);
   return XCP_EUNSUPPORTED;
 }
 
-// number of pixel chunks the backward uses (size of the dWpart slab: [P][C][9])
+// number of partial rows (spatial workgroups) of the backward's slabs
 int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
-  const int R = strip_len(W);
-  const long strips = (long)N * H * ((W + R - 1) / R);
-  const int CV = C / 4;
-  const int CVB = (CV + ((CV + 63) / 64) - 1) / ((CV + 63) / 64);
-  const int SPB = 256 / CVB;
-  const int nch = (CV + CVB - 1) / CVB;
-  // aim for ~2048 blocks, each thread handling >= 2 strips
-  long P = 2048 / nch;
-  if (P < 1) P = 1;
-  const long maxP = (strips + 2L * SPB - 1) / (2L * SPB);
-  if (P > maxP) P = maxP;
-  if (P < 1) P = 1;
-  return (int)P;
+  (void)C;
+  const TileGeo g = tile_geo(H, W, g_bwd_maxpx);
+  return N * g.nth * g.ntw;
 }
 
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
-               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, int N, int H, int W,
-               int C, hipStream_t stream) {
+               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, float* bnpart,
+               const float* bmean, const float* binvstd, int N, int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
+  if (bnpart && (act != ACT_BNRELU || !bmean || !binvstd)) return XCP_EINVAL;
+  const int maxpx = g_bwd_maxpx;
   DwBwdArgs a{};
   a.dY = dY; a.X = X; a.Wt = Wt; a.scale = scale; a.shift = shift; a.dRes = dRes; a.dSkip = dSkip;
   a.sOH = sOH; a.sOW = sOW; a.sS = sS > 0 ? sS : 1; a.dX = dX; a.dWpart = dWpart;
+  a.bnpart = bnpart; a.bmean = bmean; a.binvstd = binvstd;
   a.N = N; a.H = H; a.W = W; a.C = C;
-  a.R = strip_len(W);
-  a.nstrips = (W + a.R - 1) / a.R;
-  const int CV = C / 4;
-  const int nch = (CV + 63) / 64;
-  a.CVB = (CV + nch - 1) / nch;
-  a.SPB = 256 / a.CVB;
-  const int P = xcp_dw_bwd_chunks(N, H, W, C);
-  const long strips = (long)N * H * a.nstrips;
-  a.strips_per_chunk = (strips + P - 1) / P;
-  const int nblocks = P * nch;
-  if (dtype == XCP_BF16) return launch_bwd<bf16>(act, a, nblocks, stream);
-  if (dtype == XCP_F32) return launch_bwd<float>(act, a, nblocks, stream);
+  a.ngroups = ngroups_for(C, dtype);
+  a.g = tile_geo(H, W, maxpx);
+  if (dtype == XCP_BF16) return launch_bwd<bf16>(act, a, maxpx, stream);
+  if (dtype == XCP_F32) return launch_bwd<float>(act, a, maxpx, stream);
   return XCP_EUNSUPPORTED;
 }
 

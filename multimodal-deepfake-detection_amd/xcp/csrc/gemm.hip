@@ -11,7 +11,7 @@
 //             BatchNorm-statistics epilogue (per-column sum / sum of squares of
 //             the stored values, one deterministic partial row per M-tile).
 //   gemm_tn : P[s][N,K] = sum_{m in split s} G[m,N]^T X[m,K]   (weight gradient;
-//             fp32 partial slabs, reduced deterministically by slab_reduce).
+//             fp32 partial slabs, reduced deterministically by xcp_colreduce_f32).
 //
 // Tile 128x128, 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16 tiles.
 // bf16: v_mfma_f32_16x16x32_bf16, fp32: v_mfma_f32_16x16x4_f32 (exact fp32).
@@ -28,6 +28,8 @@ constexpr int STAGE_BYTES = BM * ROWB;    // one operand, one stage (16 KB)
 template <typename T> struct GT;
 template <> struct GT<bf16> { static constexpr int EPC = 8; };
 template <> struct GT<float> { static constexpr int EPC = 4; };
+
+__device__ __attribute__((aligned(64))) uint4 g_zero16[4];   // zero line for masked LDS-DMA chunks
 
 XCP_DEV int swz(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
@@ -46,13 +48,14 @@ struct RowInfo {
   int h, w;
   bool ok;
 };
+template <int GM>
 XCP_DEV RowInfo row_info(const Gather& g, int m, int M) {
   RowInfo r{0, 0, 0, m < M};
-  if (!r.ok || g.mode == 0) {
+  if (!r.ok || GM == 0) {
     r.base = r.ok ? m : 0;
     return r;
   }
-  if (g.mode == 3) {
+  if constexpr (GM == 3) {
     const int hw = g.H * g.W, n = m / hw, rem = m - n * hw;
     r.h = rem / g.W;
     r.w = rem - r.h * g.W;
@@ -65,11 +68,12 @@ XCP_DEV RowInfo row_info(const Gather& g, int m, int M) {
   return r;
 }
 // element offset of the chunk (row r, column k), or -1 for a zero chunk
+template <int GM>
 XCP_DEV long chunk_off(const Gather& g, const RowInfo& r, long ld, int k) {
-  if (g.mode <= 1) return r.base * ld + k;
+  if constexpr (GM <= 1) return r.base * ld + k;
   const int tap = k / g.Cg, c = k - tap * g.Cg;
   const int ky = tap / 3, kx = tap - ky * 3;
-  if (g.mode == 2) return (r.base + (long)ky * g.W + kx) * ld + c;
+  if constexpr (GM == 2) return (r.base + (long)ky * g.W + kx) * ld + c;
   const int oh = r.h - ky, ow = r.w - kx;
   if (oh < 0 || oh >= g.OH || ow < 0 || ow >= g.OW) return -1;
   return (r.base + (long)oh * g.OW + ow) * ld + c;
@@ -84,7 +88,7 @@ struct NTArgs {
   Gather ga;
 };
 
-template <typename T>
+template <typename T, int GM>
 __global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
   constexpr int EPC = GT<T>::EPC;
   constexpr int BK = 8 * EPC;
@@ -105,40 +109,37 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
   const T* A = reinterpret_cast<const T*>(a.A);
   const T* B = reinterpret_cast<const T*>(a.B);
 
-  // per-thread global chunk coordinates (4 chunks per operand per stage)
+  // LDS-DMA staging (global_load_lds, 16 B per lane): wave w fills rows [32w, 32w+32)
+  // of each operand tile, 8 rows (1 KB, lane-linear in LDS) per instruction.  The
+  // XOR chunk swizzle is applied on the per-lane SOURCE address (LDS stays
+  // lane-linear); chunks past K / rows past M,N read a zero line.
+  const int pc = lane & 7;
   RowInfo ar[4];
-  bool b_ok[4];
-  long b_off[4];
-  int crow[4], cchk[4];
+  const T* bp[4];
+  int lcs[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int q = tid + NT * i;
-    crow[i] = q >> 3;
-    cchk[i] = q & 7;
-    const int n = n0 + crow[i];
-    ar[i] = row_info(a.ga, m0 + crow[i], a.M);
-    b_ok[i] = n < a.N;
-    b_off[i] = b_ok[i] ? (long)n * a.ldb : 0;
+    const int row = w * 32 + i * 8 + (lane >> 3);
+    lcs[i] = pc ^ ((row >> 1) & 7);
+    ar[i] = row_info<GM>(a.ga, m0 + row, a.M);
+    const int n = n0 + row;
+    bp[i] = n < a.N ? B + (long)n * a.ldb : nullptr;
   }
-
-  uint4 ra[4], rb[4];
-  auto gload = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = kt * BK + cchk[i] * EPC;
-      const bool kok = k < a.K;
-      const long ao = (ar[i].ok && kok) ? chunk_off(a.ga, ar[i], a.lda, k) : -1;
-      ra[i] = ao >= 0 ? *reinterpret_cast<const uint4*>(A + ao) : make_uint4(0, 0, 0, 0);
-      rb[i] = (b_ok[i] && kok) ? *reinterpret_cast<const uint4*>(B + b_off[i] + k) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto swrite = [&](int buf) {
+  auto issue = [&](int kt, int buf) {
     char* sa = smem + buf * 2 * STAGE_BYTES;
     char* sb = sa + STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<uint4*>(sa + swz(crow[i], cchk[i])) = ra[i];
-      *reinterpret_cast<uint4*>(sb + swz(crow[i], cchk[i])) = rb[i];
+      const int k = kt * BK + lcs[i] * EPC;
+      const bool kok = k < a.K;
+      const long ao = (ar[i].ok && kok) ? chunk_off<GM>(a.ga, ar[i], a.lda, k) : -1;
+      const void* srcA = ao >= 0 ? (const void*)(A + ao) : (const void*)g_zero16;
+      const void* srcB = (bp[i] != nullptr && kok) ? (const void*)(bp[i] + k) : (const void*)g_zero16;
+      const int dst = (w * 32 + i * 8) * ROWB;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)srcA,
+                                       (void __attribute__((address_space(3)))*)(sa + dst), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)srcB,
+                                       (void __attribute__((address_space(3)))*)(sb + dst), 16, 0, 0);
     }
   };
 
@@ -149,12 +150,11 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (a.K + BK - 1) / BK;
-  gload(0);
-  swrite(0);
-  __syncthreads();
+  issue(0, 0);
+  __syncthreads();   // vmcnt(0) + barrier: stage 0 landed for every wave
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload(kt + 1);
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);   // in flight while this stage computes
     const char* sa = smem + (kt & 1) * 2 * STAGE_BYTES;
     const char* sb = sa + STAGE_BYTES;
 #pragma unroll
@@ -167,10 +167,12 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
           af[t] = *reinterpret_cast<const bf16x8*>(sa + swz(wm * 64 + t * 16 + fr, ch));
           bfr[t] = *reinterpret_cast<const bf16x8*>(sb + swz(wn * 64 + t * 16 + fr, ch));
         }
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
       } else {
         f32x4 af[4], bfr[4];
 #pragma unroll
@@ -186,8 +188,7 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
             for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bfr[j][e], acc[i][j], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) swrite((kt + 1) & 1);
-    __syncthreads();
+    __syncthreads();   // next stage landed (vmcnt(0)) and this stage's reads done
   }
 
   // ---- epilogue: round to T, BN statistics, stage through LDS, 16-B stores
@@ -266,7 +267,7 @@ XCP_DEV bf16x4 ds_read_tr(const char* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
-template <typename T>
+template <typename T, int GM>
 __global__ __launch_bounds__(NT) void gemm_tn_kernel(TNArgs a) {
   // tile: 128 (n) x 128 (k); stage: 32 m-rows of G[., n0:n0+128] and X[., k0:k0+128]
   constexpr int EPC = GT<T>::EPC;
@@ -305,8 +306,8 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(TNArgs a) {
       const int n = n0 + schk[i] * EPC, k = k0 + schk[i] * EPC;
       const bool mok = m < mend;
       rg[i] = (mok && n < a.N) ? *reinterpret_cast<const uint4*>(G + (long)m * a.ldg + n) : make_uint4(0, 0, 0, 0);
-      const RowInfo xr = row_info(a.gx, m, mend);
-      const long xo = (xr.ok && k < a.K) ? chunk_off(a.gx, xr, a.ldx, k) : -1;
+      const RowInfo xr = row_info<GM>(a.gx, m, mend);
+      const long xo = (xr.ok && k < a.K) ? chunk_off<GM>(a.gx, xr, a.ldx, k) : -1;
       rx[i] = xo >= 0 ? *reinterpret_cast<const uint4*>(X + xo) : make_uint4(0, 0, 0, 0);
     }
   };
@@ -404,12 +405,21 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   const int grid = xcp_cdiv(M, BM) * xcp_cdiv(N, BN);
-  if (dtype == XCP_BF16)
-    hipLaunchKernelGGL(gemm_nt_kernel<bf16>, dim3(grid), dim3(NT), 0, stream, a);
-  else if (dtype == XCP_F32)
-    hipLaunchKernelGGL(gemm_nt_kernel<float>, dim3(grid), dim3(NT), 0, stream, a);
-  else
+#define XCP_NT_LAUNCH(TT)                                                                                      \
+  switch (gmode) {                                                                                             \
+    case 0: hipLaunchKernelGGL((gemm_nt_kernel<TT, 0>), dim3(grid), dim3(NT), 0, stream, a); break;          \
+    case 1: hipLaunchKernelGGL((gemm_nt_kernel<TT, 1>), dim3(grid), dim3(NT), 0, stream, a); break;          \
+    case 2: hipLaunchKernelGGL((gemm_nt_kernel<TT, 2>), dim3(grid), dim3(NT), 0, stream, a); break;          \
+    default: hipLaunchKernelGGL((gemm_nt_kernel<TT, 3>), dim3(grid), dim3(NT), 0, stream, a); break;         \
+  }
+  if (dtype == XCP_BF16) {
+    XCP_NT_LAUNCH(bf16)
+  } else if (dtype == XCP_F32) {
+    XCP_NT_LAUNCH(float)
+  } else {
     return XCP_EUNSUPPORTED;
+  }
+#undef XCP_NT_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -421,12 +431,20 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
   if (gmode < 0 || gmode > 2 || (gmode == 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   TNArgs a{G, ldg, X, ldx, P, M, N, K, S, rows_per_split, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   const int grid = xcp_cdiv(N, 128) * xcp_cdiv(K, 128) * S;
-  if (dtype == XCP_BF16)
-    hipLaunchKernelGGL(gemm_tn_kernel<bf16>, dim3(grid), dim3(NT), 0, stream, a);
-  else if (dtype == XCP_F32)
-    hipLaunchKernelGGL(gemm_tn_kernel<float>, dim3(grid), dim3(NT), 0, stream, a);
-  else
+#define XCP_TN_LAUNCH(TT)                                                                                      \
+  switch (gmode) {                                                                                             \
+    case 0: hipLaunchKernelGGL((gemm_tn_kernel<TT, 0>), dim3(grid), dim3(NT), 0, stream, a); break;          \
+    case 1: hipLaunchKernelGGL((gemm_tn_kernel<TT, 1>), dim3(grid), dim3(NT), 0, stream, a); break;          \
+    default: hipLaunchKernelGGL((gemm_tn_kernel<TT, 2>), dim3(grid), dim3(NT), 0, stream, a); break;         \
+  }
+  if (dtype == XCP_BF16) {
+    XCP_TN_LAUNCH(bf16)
+  } else if (dtype == XCP_F32) {
+    XCP_TN_LAUNCH(float)
+  } else {
     return XCP_EUNSUPPORTED;
+  }
+#undef XCP_TN_LAUNCH
   return (int)hipGetLastError();
 }
 

@@ -311,24 +311,29 @@ class XceptionEngine:
             grads[name] = t
             return t
 
-        def bn_bwd(bnmod, name, dZ, Y, rows, C, st):
+        def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None):
             dY = self._empty(rows * C)
-            ops.bn_backward(dZ, Y, rows, C, _bn_ref(bnmod), st, dY, g(name + ".weight", (C,)), g(name + ".bias", (C,)))
+            P = part[1] if part is not None else 0
+            ops.bn_backward(dZ, Y, rows, C, _bn_ref(bnmod), st, dY, g(name + ".weight", (C,)), g(name + ".bias", (C,)),
+                            part=part[0] if part is not None else None, R=P)
             return dY
 
-        def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1)):
-            """dZ: gradient w.r.t. this unit's BN output.  Returns gradient w.r.t. the
-            depthwise input after the activation mask (+ residual / skip terms)."""
+        def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None):
+            """dZ: gradient w.r.t. this unit's BN output (``part``: its fused BN-backward
+            partial sums, if the producer emitted them).  Returns (gradient w.r.t. the
+            depthwise input after the activation mask (+ residual / skip terms), and
+            -- when ``prev_st`` is the Stats of the BN feeding this unit -- that BN's
+            backward partial sums)."""
             M = N * H * W
-            dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"])
+            dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
             dD = self._empty(M * u.cin)
             ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, u.cin, u.cout)
             ops.weight_grad(dY, rec["d"], M, u.cout, u.cin, g(u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1)))
             dX = self._empty(M * u.cin)
-            ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX,
-                       g(u.name + ".conv1.weight", (u.cin, 1, 3, 3)), N, H, W, u.cin, dRes=dRes, dSkip=dSkip,
-                       skip_geom=skip_geom)
-            return dX
+            bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX,
+                             g(u.name + ".conv1.weight", (u.cin, 1, 3, 3)), N, H, W, u.cin, dRes=dRes, dSkip=dSkip,
+                             skip_geom=skip_geom, bn_stats=prev_st)
+            return dX, (bnp if prev_st is not None else None)
 
         # ---- exit flow
         H, W = S["xH"], S["xW"]
@@ -337,8 +342,8 @@ class XceptionEngine:
         u3, u4 = self.exit_units
         dZ4 = self._empty(M * 2048)
         ops.avgpool_bwd(dfeat, e4["y"], e4["st"].scale, e4["st"].shift, dZ4, N, H * W, 2048)
-        dZ3 = unit_bwd(u4, e4, dZ4, H, W)
-        dX = unit_bwd(u3, e3, dZ3, H, W)
+        dZ3, p3 = unit_bwd(u4, e4, dZ4, H, W, prev_st=e3["st"])
+        dX, _ = unit_bwd(u3, e3, dZ3, H, W, part=p3)
         # ---- blocks, last to first
         for b, bs in zip(reversed(self.blocks), reversed(S["blocks"])):
             dX = self._block_bwd(b, bs, dX, N, pk, g, bn_bwd, unit_bwd)
@@ -381,12 +386,13 @@ class XceptionEngine:
                 dRes = dXs
         else:
             dRes = dOut
+        part = None
         for i in range(len(b.units) - 1, -1, -1):
             u, rec = b.units[i], units[i]
             if i > 0:
-                dZ = unit_bwd(u, rec, dZ, H, W)
+                dZ, part = unit_bwd(u, rec, dZ, H, W, part=part, prev_st=units[i - 1]["st"])
             else:
-                dZ = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom)
+                dZ, _ = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, part=part)
         return dZ
 
 

@@ -137,12 +137,21 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
         _lib.call("xcp_dw_fwd", DT[X.dtype], act, _p(X), _p(Y), _p(Wt), _p(scale), _p(shift), N, H, W, C, stream())
 
 
-def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1)):
+def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
+           bn_stats=None):
+    """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
+    (that BN's Stats) is given, else (None, 0)."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
+    bnpart = None
+    if bn_stats is not None:
+        bnpart = torch.empty(P * 2 * C, device=dY.device, dtype=torch.float32)
     _lib.call("xcp_dw_bwd", DT[dY.dtype], act, _p(dY), _p(X), _p(Wt), _p(scale), _p(shift), _p(dRes), _p(dSkip),
-              skip_geom[0], skip_geom[1], skip_geom[2], _p(dX), _p(part), N, H, W, C, stream())
+              skip_geom[0], skip_geom[1], skip_geom[2], _p(dX), _p(part), _p(bnpart),
+              _p(bn_stats["mean"]) if bn_stats is not None else 0,
+              _p(bn_stats["invstd"]) if bn_stats is not None else 0, N, H, W, C, stream())
     reduce_slabs(part, P, C * 9, dW_out)
+    return bnpart, (P if bnpart is not None else 0)
 
 
 # ---------------------------------------------------------------- batchnorm
@@ -179,12 +188,15 @@ def row_stats(X, rows, C):
     return part, R
 
 
-def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta):
-    """dY = BatchNorm2d backward (train-mode batch stats) of dZ; writes dgamma/dbeta."""
-    R = _lib.call("xcp_chanred_parts", rows, C)
-    part = torch.empty(R * 2 * C, device=dZ.device, dtype=torch.float32)
-    _lib.call("xcp_bn_bwd_reduce", DT[dZ.dtype], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), rows, C, _p(part),
-              stream())
+def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0):
+    """dY = BatchNorm2d backward (train-mode batch stats) of dZ; writes dgamma/dbeta.
+    ``part`` ([R][2][C] partial (sum dz, sum dz*zhat)) may come fused from the
+    producer of dZ; otherwise it is reduced here."""
+    if part is None:
+        R = _lib.call("xcp_chanred_parts", rows, C)
+        part = torch.empty(R * 2 * C, device=dZ.device, dtype=torch.float32)
+        _lib.call("xcp_bn_bwd_reduce", DT[dZ.dtype], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), rows, C,
+                  _p(part), stream())
     G = min(STAT_GROUPS, R)
     p2 = torch.empty(G * 2 * C, device=dZ.device, dtype=torch.float64)
     colreduce_f64(part, R, 2 * C, p2, G)

@@ -106,7 +106,7 @@ def test_gemm_tn(ops, gpu, dt, M, N, K):
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("act", [0, 1, 2])
-@pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9)])
+@pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9), (1, 64, 147), (2, 256, 74)])
 def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
     W = H + 1
     g = torch.Generator(device=gpu).manual_seed(C + H + act)
@@ -139,9 +139,18 @@ def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
         want = a.grad * (z > 0)
     dX = torch.empty(N * H * W, C, device=gpu, dtype=dt)
     dW = torch.empty(C * 9, device=gpu)
-    ops.dw_bwd(act, nhwc(dy), nhwc(x), Wt, sc, sh, dX, dW, N, H, W, C)
-    assert rel_err(nchw(dX.view(N, H, W, C)).float(), want) < (1e-6 if dt == torch.float32 else 1e-2)
+    st = None
+    if act == 2:
+        st = {"mean": torch.randn(C, device=gpu, generator=g) * 0.1, "invstd": torch.rand(C, device=gpu, generator=g) + 0.5}
+    bnpart, P = ops.dw_bwd(act, nhwc(dy), nhwc(x), Wt, sc, sh, dX, dW, N, H, W, C, bn_stats=st)
+    dXn = nchw(dX.view(N, H, W, C)).float()
+    assert rel_err(dXn, want) < (1e-6 if dt == torch.float32 else 1e-2)
     assert rel_err(dW.view(C, 1, 3, 3), w.grad) < (1e-5 if dt == torch.float32 else 1e-2)
+    if act == 2:
+        sums = bnpart.view(P, 2, C).double().sum(0)
+        zhat = (x.float() - st["mean"].view(1, C, 1, 1)) * st["invstd"].view(1, C, 1, 1)
+        torch.testing.assert_close(sums[0], dXn.double().sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(sums[1], (dXn * zhat).double().sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

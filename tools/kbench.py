@@ -1,0 +1,94 @@
+"""Kernel micro-benchmarks at the bench's middle-flow shapes (N=256 frames of 19x19x728,
+bf16) and a few others: average launch time with HIP events, achieved GB/s or TFLOP/s.
+
+usage: python tools/kbench.py [names...]   (default: all)
+"""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "multimodal-deepfake-detection_amd"), REPO]
+
+from xcp import ops  # noqa: E402
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    dev = torch.device("cuda:0")
+    ops._lib.load()
+    sel = set(sys.argv[1:])
+    dt = torch.bfloat16
+    N, H, W, C = 256, 19, 19, 728
+    M = N * H * W
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(M, C, device=dev, generator=g).to(dt)
+    Y = torch.empty_like(X)
+    D = torch.randn(M, C, device=dev, generator=g).to(dt)
+    Wt = torch.randn(9, C, device=dev, generator=g)
+    sc = torch.rand(C, device=dev, generator=g) + 0.5
+    sh = torch.randn(C, device=dev, generator=g)
+    Wp = (torch.randn(C, C, device=dev, generator=g) / 27).to(dt)
+    stats = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
+    dW = torch.empty(C * 9, device=dev)
+    st = {"mean": torch.zeros(C, device=dev), "invstd": torch.ones(C, device=dev)}
+    tensor_bytes = M * C * 2
+    res = []
+
+    def rep(name, ms, byts=None, flops=None):
+        line = f"{name:34s} {ms * 1e3:9.1f} us"
+        if byts:
+            line += f"  {byts / ms / 1e6:8.1f} GB/s"
+        if flops:
+            line += f"  {flops / ms / 1e9:8.1f} TFLOP/s"
+        print(line, flush=True)
+        res.append((name, ms))
+
+    if not sel or "copy" in sel:
+        rep("torch copy (ref BW)", timeit(lambda: Y.copy_(X)), 2 * tensor_bytes)
+    if not sel or "dw_fwd" in sel:
+        for px in (512, 256):
+            old = ops._lib.call("xcp_tune", 0, px)
+            for act in (1, 2):
+                rep(f"dw_fwd act={act} maxpx={px}", timeit(lambda: ops.dw_fwd(act, X, Y, Wt, sc, sh, N, H, W, C)),
+                    2 * tensor_bytes)
+            ops._lib.call("xcp_tune", 0, old)
+    if not sel or "dw_bwd" in sel:
+        for px in (256, 512):
+            old = ops._lib.call("xcp_tune", 1, px)
+            rep(f"dw_bwd act=2 +bnsums maxpx={px}",
+                timeit(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)), 3 * tensor_bytes)
+            rep(f"dw_bwd act=1 maxpx={px}", timeit(lambda: ops.dw_bwd(1, D, X, Wt, sc, sh, Y, dW, N, H, W, C)),
+                3 * tensor_bytes)
+            ops._lib.call("xcp_tune", 1, old)
+    if not sel or "gemm" in sel:
+        rep("gemm_nt 728x728 +stats", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=stats)),
+            flops=2.0 * M * C * C)
+        out = torch.empty(C * C, device=dev)
+        rep("weight_grad 728x728", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)), flops=2.0 * M * C * C)
+    if not sel or "bn" in sel:
+        dgm, dbt = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        bn = {"weight": sc, "bias": sh, "running_mean": None, "running_var": None, "eps": 1e-5, "momentum": 0.1,
+              "track": False}
+        rep("bn_backward (reduce+apply)", timeit(lambda: ops.bn_backward(D, X, M, C, bn, st, Y, dgm, dbt)),
+            4 * tensor_bytes)
+    if not sel or "tail" in sel:
+        rep("tail_fwd identity", timeit(lambda: ops.tail_fwd(X, sc, sh, False, D, None, None, Y, None, N, H, W, C)),
+            3 * tensor_bytes)
+
+
+if __name__ == "__main__":
+    main()
