@@ -37,12 +37,14 @@ typedef void* xcp_stream_t; /* hipStream_t */
  * replaces nn.Conv2d(C, Cout, 1) of SeparableConv2d.pointwise (Xception.py:42,:46),
  * Block.skip (Xception.py:55,:93), Xception.conv2 (Xception.py:122,:172; im2col
  * gather mode 2, its input gradient via mode 3) and x @ W_ih^T of nn.LSTM.
- * C[M,N] = A[M,K] . B[N,K]^T ; optional stats[ceil(M/128)][2][N] partial
+ * C[M,N] = A[M,K] . B[N,K]^T ; optional stats[xcp_gemm_nt_stat_rows(M)][2][N] partial
  * (sum, sum^2) of the stored C columns (BatchNorm batch statistics).
  * gmode: 0 dense rows, 1 strided (skip conv, stride gS), 2 im2col 3x3 p0,
  *        3 transposed im2col (conv input gradient); gC = channels per tap. */
 int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                 float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, xcp_stream_t stream);
+/* number of partial rows in gemm_nt's stats array for M rows */
+int xcp_gemm_nt_stat_rows(int M);
 
 /* weight gradient of the above: P[s][N][K] = sum_{m in split s} G[m][N] X[m][K],
  * rows split in S chunks of rows_per_split; X rows gathered as in gemm_nt
@@ -61,7 +63,8 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
  * partial sums of the BatchNorm that produced X (XCP_ACT_BNRELU only). */
 int xcp_dw_bwd_chunks(int N, int H, int W, int C);
 /* launch tuning knobs: 0 = depthwise forward / 1 = depthwise backward halo pixels per
- * LDS tile (256 or 512).  Returns the previous value (-1: unknown knob). */
+ * LDS tile (256 or 512); 2 = pointwise GEMM tile (0: 128x128 2-stage, 1: 256x128
+ * 3-stage).  Returns the previous value (-1: unknown knob). */
 int xcp_tune(int knob, int value);
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
                const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, float* bnpart,

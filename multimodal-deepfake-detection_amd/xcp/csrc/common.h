@@ -113,6 +113,15 @@ XCP_DEV float wave_sum(float v) {
 //   MODE_NONE: x;  MODE_RELU: max(x,0);  MODE_BNRELU: max(x*scale[c]+shift[c], 0)
 enum XcpAct { ACT_NONE = 0, ACT_RELU = 1, ACT_BNRELU = 2 };
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits for every
+// outstanding global store of the wave (vmcnt(0)); after an epilogue that has
+// issued its stores that wait serialises the workgroup on store completion.
+XCP_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 static inline int xcp_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5

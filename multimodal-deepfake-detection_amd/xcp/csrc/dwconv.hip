@@ -356,8 +356,9 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwBwdArgs a) {
       }
     }
   }
-  // ---- workgroup reduction over the 16 row workers (reuse the staging LDS)
-  __syncthreads();
+  // ---- workgroup reduction over the 16 row workers (reuse the staging LDS);
+  // LDS-only barriers so the dX stores issued above are not waited for
+  lds_barrier();
   constexpr int PER = 11;                      // 9 taps + 2 BN sums
   float* red = reinterpret_cast<float*>(sm);   // [NW][16 lanes][EPT][PER]
 #pragma unroll
@@ -368,7 +369,7 @@ __global__ __launch_bounds__(256) void dw_bwd_kernel(DwBwdArgs a) {
     rp[9] = bs1[e];
     rp[10] = bs2[e];
   }
-  __syncthreads();
+  lds_barrier();
   constexpr int L = 16 * EPT * PER;
   for (int i = threadIdx.x; i < L; i += 256) {
     float s = 0.f;
@@ -418,11 +419,15 @@ inline int ngroups_for(int C, int dtype) {
 
 }  // namespace
 
+int xcp_internal_gemm_tune(int cfg);   // gemm.hip
+
 extern "C" {
 
 // Tuning knobs: 0 = depthwise forward halo pixels per tile (256 | 512),
-// 1 = depthwise backward halo pixels per tile (256 | 512).  Returns the old value.
+// 1 = depthwise backward halo pixels per tile (256 | 512), 2 = pointwise GEMM tile
+// config (0: 128x128 / 2-stage ring, 1: 256x128 / 3-stage).  Returns the old value.
 int xcp_tune(int knob, int value) {
+  if (knob == 2) return xcp_internal_gemm_tune(value);
   int* k = knob == 0 ? &g_fwd_maxpx : knob == 1 ? &g_bwd_maxpx : nullptr;
   if (!k) return -1;
   const int old = *k;

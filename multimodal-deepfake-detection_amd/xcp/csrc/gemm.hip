@@ -88,61 +88,100 @@ struct NTArgs {
   Gather ga;
 };
 
-template <typename T, int GM>
-__global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
+// ---------------------------------------------------------------------------------
+// NT kernel: (64*WMW) x 128 output tile per workgroup, WMW x 2 waves, each wave
+// 64 x 64 = 4 x 4 MFMA 16x16 tiles.  K advances in 128-byte stages (64 bf16 /
+// 32 fp32) through an LDS ring of STAGES slots filled by LDS-DMA (STAGES-1 in
+// flight while one is consumed; counted vmcnt + one raw barrier per stage).
+// MFMA roles are swapped (weights as the A operand) so each lane ends up holding
+// 4 consecutive output columns of one row: the epilogue stages 8-byte pieces and
+// takes the BatchNorm statistics from the staged tile while storing it.
+constexpr int NBN = 128;
+
+template <int N>
+XCP_DEV void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0, "unsupported count");
+}
+
+template <typename T, int GM, int WMW, int STAGES>
+__global__ __launch_bounds__(WMW * 128) void gemm_nt_kernel(NTArgs a) {
+  constexpr int NTH = WMW * 128;
+  constexpr int BMT = 64 * WMW;
   constexpr int EPC = GT<T>::EPC;
   constexpr int BK = 8 * EPC;
-  constexpr int CPITCH = BN * (int)sizeof(T) + 16;   // epilogue staging row pitch (bytes)
-  constexpr int SMEM_MAIN = 4 * STAGE_BYTES;
-  constexpr int SMEM_EPI = BM * CPITCH;
-  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + 2 * 2 * BN * 4];
-  float* red = reinterpret_cast<float*>(smem + SMEM);   // [2 wm][2 (s,q)][BN]
+  constexpr int A_BYTES = BMT * ROWB, B_BYTES = NBN * ROWB, SB = A_BYTES + B_BYTES;
+  constexpr int A_LOADS = 4, B_LOADS = 8 / WMW, NLOADS = A_LOADS + B_LOADS;
+  constexpr int CPITCH = NBN * (int)sizeof(T) + 16;   // epilogue staging row pitch (bytes)
+  constexpr int RING = STAGES * SB;
+  constexpr int SMEM = RING > BMT * CPITCH ? RING : BMT * CPITCH;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM + 2 * (NTH / 64) * NBN * 4];
+  float* red = reinterpret_cast<float*>(smem + SMEM);   // [2 (s,q)][waves][NBN]
 
-  const int gridN = (a.N + BN - 1) / BN;
-  const int gridM = (a.M + BM - 1) / BM;
+  const int gridN = (a.N + NBN - 1) / NBN;
+  const int gridM = (a.M + BMT - 1) / BMT;
   const int id = xcd_remap(blockIdx.x, gridM * gridN);
   const int bn = id % gridN, bm = id / gridN;
-  const int m0 = bm * BM, n0 = bn * BN;
+  const int m0 = bm * BMT, n0 = bn * NBN;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const T* A = reinterpret_cast<const T*>(a.A);
   const T* B = reinterpret_cast<const T*>(a.B);
 
-  // LDS-DMA staging (global_load_lds, 16 B per lane): wave w fills rows [32w, 32w+32)
-  // of each operand tile, 8 rows (1 KB, lane-linear in LDS) per instruction.  The
-  // XOR chunk swizzle is applied on the per-lane SOURCE address (LDS stays
-  // lane-linear); chunks past K / rows past M,N read a zero line.
+  // LDS-DMA staging (global_load_lds, 16 B per lane, lane-linear 1 KB = 8 rows of
+  // 128 B per instruction).  Wave w fills A rows [32w, 32w+32) and B rows
+  // [(64/WMW)w, ...).  The XOR chunk swizzle is applied to the per-lane SOURCE
+  // address; chunks past K and rows past M / N read a zero line.
   const int pc = lane & 7;
-  RowInfo ar[4];
-  const T* bp[4];
-  int lcs[4];
+  RowInfo ar[A_LOADS];
+  const T* ap[A_LOADS];
+  int alc[A_LOADS], blc[B_LOADS];
+  const T* bp[B_LOADS];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < A_LOADS; ++i) {
     const int row = w * 32 + i * 8 + (lane >> 3);
-    lcs[i] = pc ^ ((row >> 1) & 7);
+    alc[i] = pc ^ ((row >> 1) & 7);
     ar[i] = row_info<GM>(a.ga, m0 + row, a.M);
-    const int n = n0 + row;
-    bp[i] = n < a.N ? B + (long)n * a.ldb : nullptr;
+    ap[i] = ar[i].ok ? A + ar[i].base * a.lda + alc[i] * EPC : nullptr;   // modes 0 / 1
   }
-  auto issue = [&](int kt, int buf) {
-    char* sa = smem + buf * 2 * STAGE_BYTES;
-    char* sb = sa + STAGE_BYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = kt * BK + lcs[i] * EPC;
-      const bool kok = k < a.K;
-      const long ao = (ar[i].ok && kok) ? chunk_off<GM>(a.ga, ar[i], a.lda, k) : -1;
-      const void* srcA = ao >= 0 ? (const void*)(A + ao) : (const void*)g_zero16;
-      const void* srcB = (bp[i] != nullptr && kok) ? (const void*)(bp[i] + k) : (const void*)g_zero16;
-      const int dst = (w * 32 + i * 8) * ROWB;
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)srcA,
-                                       (void __attribute__((address_space(3)))*)(sa + dst), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)srcB,
-                                       (void __attribute__((address_space(3)))*)(sb + dst), 16, 0, 0);
+  for (int i = 0; i < B_LOADS; ++i) {
+    const int row = w * (64 / WMW) + i * 8 + (lane >> 3);
+    blc[i] = pc ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    bp[i] = n < a.N ? B + (long)n * a.ldb + blc[i] * EPC : nullptr;
+  }
+  auto glds = [](const void* src, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  auto issue = [&](int kt, int buf) {
+    char* sa = smem + buf * SB;
+    char* sb = sa + A_BYTES;
+    const int kb = kt * BK;
+#pragma unroll
+    for (int i = 0; i < A_LOADS; ++i) {
+      const void* src;
+      if constexpr (GM <= 1) {
+        src = (ap[i] != nullptr && kb + alc[i] * EPC < a.K) ? (const void*)(ap[i] + kb) : (const void*)g_zero16;
+      } else {
+        const int k = kb + alc[i] * EPC;
+        const long ao = (ar[i].ok && k < a.K) ? chunk_off<GM>(a.ga, ar[i], a.lda, k) : -1;
+        src = ao >= 0 ? (const void*)(A + ao) : (const void*)g_zero16;
+      }
+      glds(src, sa + (w * 32 + i * 8) * ROWB);
+    }
+#pragma unroll
+    for (int i = 0; i < B_LOADS; ++i) {
+      const void* src = (bp[i] != nullptr && kb + blc[i] * EPC < a.K) ? (const void*)(bp[i] + kb)
+                                                                        : (const void*)g_zero16;
+      glds(src, sb + (w * (64 / WMW) + i * 8) * ROWB);
     }
   };
 
+  // acc[mt][nt]: D = W_frag(nt) x A_frag(mt)  ->  lane holds C[m = ..mt*16+fr][n = ..nt*16+4fg+r]
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -150,13 +189,24 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (a.K + BK - 1) / BK;
-  issue(0, 0);
-  __syncthreads();   // vmcnt(0) + barrier: stage 0 landed for every wave
+  constexpr int D = STAGES - 1;
+#pragma unroll
+  for (int s0 = 0; s0 < D; ++s0)
+    if (s0 < nk) issue(s0, s0);
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);   // in flight while this stage computes
-    const char* sa = smem + (kt & 1) * 2 * STAGE_BYTES;
-    const char* sb = sa + STAGE_BYTES;
+    // stage kt landed for this wave (later stages may stay in flight), then for all waves
+    if constexpr (D >= 2) {
+      if (kt + 1 < nk) wait_vmcnt<NLOADS>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    // refill the slot consumed in iteration kt-1 (every wave is past it now)
+    if (kt + D < nk) issue(kt + D, (kt + D) % STAGES);
+    const char* sa = smem + (kt % STAGES) * SB;
+    const char* sb = sa + A_BYTES;
 #pragma unroll
     for (int cg = 0; cg < 2; ++cg) {
       const int ch = cg * 4 + fg;
@@ -167,12 +217,10 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
           af[t] = *reinterpret_cast<const bf16x8*>(sa + swz(wm * 64 + t * 16 + fr, ch));
           bfr[t] = *reinterpret_cast<const bf16x8*>(sb + swz(wn * 64 + t * 16 + fr, ch));
         }
-        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       } else {
         f32x4 af[4], bfr[4];
 #pragma unroll
@@ -185,64 +233,84 @@ __global__ __launch_bounds__(NT) void gemm_nt_kernel(NTArgs a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][e], bfr[j][e], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bfr[j][e], af[i][e], acc[i][j], 0, 0, 0);
       }
     }
-    __syncthreads();   // next stage landed (vmcnt(0)) and this stage's reads done
   }
+  __syncthreads();   // every wave done reading the ring before the epilogue reuses it
 
-  // ---- epilogue: round to T, BN statistics, stage through LDS, 16-B stores
-  float cs[4], cq[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) { cs[j] = 0.f; cq[j] = 0.f; }
+  // ---- epilogue: round to T, stage 4-column pieces through LDS
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = rnd<T>(acc[i][j][r]);
-        cs[j] += v;
-        cq[j] += v * v;
-        const int row = wm * 64 + i * 16 + fg * 4 + r, col = wn * 64 + j * 16 + fr;
-        *reinterpret_cast<T*>(smem + row * CPITCH + col * (int)sizeof(T)) = from_f<T>(v);
-      }
-  if (a.stats) {
-#pragma unroll
     for (int j = 0; j < 4; ++j) {
-      cs[j] += __shfl_xor(cs[j], 16, 64);
-      cs[j] += __shfl_xor(cs[j], 32, 64);
-      cq[j] += __shfl_xor(cq[j], 16, 64);
-      cq[j] += __shfl_xor(cq[j], 32, 64);
-    }
-    if (fg == 0) {
+      const int row = wm * 64 + i * 16 + fr, col = wn * 64 + j * 16 + fg * 4;
+      float v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        red[(wm * 2 + 0) * BN + wn * 64 + j * 16 + fr] = cs[j];
-        red[(wm * 2 + 1) * BN + wn * 64 + j * 16 + fr] = cq[j];
-      }
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
+      VecIO<T, 4>::store(reinterpret_cast<T*>(smem + row * CPITCH + col * (int)sizeof(T)), v);
     }
-  }
   __syncthreads();
-  if (a.stats && tid < BN) {
-    const int n = n0 + tid;
-    if (n < a.N) {
-      a.stats[((long)bm * 2 + 0) * a.N + n] = red[0 * BN + tid] + red[2 * BN + tid];
-      a.stats[((long)bm * 2 + 1) * a.N + n] = red[1 * BN + tid] + red[3 * BN + tid];
-    }
-  }
+  // ---- coalesced 16-B stores; BN statistics over the stored values
   T* C = reinterpret_cast<T*>(a.C);
-  constexpr int CPR = BN * (int)sizeof(T) / 16;   // 16-B chunks per tile row
-  constexpr int ITER = BM * CPR / NT;
+  constexpr int CPR = NBN * (int)sizeof(T) / 16;   // 16-B chunks per tile row
+  constexpr int RPI = NTH / CPR;                   // rows covered per iteration
+  constexpr int ITER = BMT / RPI;
+  const int c = tid % CPR, rq = tid / CPR;
+  const int n = n0 + c * EPC;
+  float s1[EPC], s2[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) s1[e] = s2[e] = 0.f;
 #pragma unroll
   for (int i = 0; i < ITER; ++i) {
-    const int q = tid + NT * i;
-    const int row = q / CPR, c = q % CPR;
-    const int m = m0 + row, n = n0 + c * EPC;
-    if (m < a.M && n < a.N)
-      *reinterpret_cast<uint4*>(C + (long)m * a.ldc + n) = *reinterpret_cast<const uint4*>(smem + row * CPITCH + c * 16);
+    const int row = rq + RPI * i;
+    const int m = m0 + row;
+    const uint4 v = *reinterpret_cast<const uint4*>(smem + row * CPITCH + c * 16);
+    if (m < a.M && n < a.N) {
+      *reinterpret_cast<uint4*>(C + (long)m * a.ldc + n) = v;
+      float f[EPC];
+      VecIO<T, EPC>::load(reinterpret_cast<const T*>(&v), f);
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        s1[e] += f[e];
+        s2[e] = fmaf(f[e], f[e], s2[e]);
+      }
+    }
+  }
+  if (a.stats) {
+    // threads sharing chunk c: tid = c + CPR*rq; fold rq within the wave, then across waves
+#pragma unroll
+    for (int e = 0; e < EPC; ++e)
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        red[(0 * (NTH / 64) + w) * NBN + c * EPC + e] = s1[e];
+        red[(1 * (NTH / 64) + w) * NBN + c * EPC + e] = s2[e];
+      }
+    }
+    lds_barrier();   // not __syncthreads(): the C stores above must not be waited for
+    if (tid < NBN) {
+      const int nn = n0 + tid;
+      if (nn < a.N) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < NTH / 64; ++q) {
+          t1 += red[(0 * (NTH / 64) + q) * NBN + tid];
+          t2 += red[(1 * (NTH / 64) + q) * NBN + tid];
+        }
+        a.stats[((long)bm * 2 + 0) * a.N + nn] = t1;
+        a.stats[((long)bm * 2 + 1) * a.N + nn] = t2;
+      }
+    }
   }
 }
+
+int g_nt_cfg = 0;   // xcp_tune knob 2: 0 = 128x128 tile / 2-stage ring, 1 = 256x128 / 3-stage
 
 // ---------------------------------------------------------------------------------
 // Weight gradient: P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]
@@ -277,7 +345,9 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(TNArgs a) {
 
   const int gridN = (a.N + 127) / 128, gridK = (a.K + 127) / 128;
   const int tiles = gridN * gridK;
-  const int id = blockIdx.x;
+  // logical ids of one row split are contiguous and land on one XCD, so the
+  // split's G / X rows are fetched from HBM once and re-served by that XCD's L2
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
   const int s = id / tiles, t = id % tiles;
   const int bn = t / gridK, bk = t % gridK;
   const int n0 = bn * 128, k0 = bk * 128;
@@ -404,13 +474,17 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
-  const int grid = xcp_cdiv(M, BM) * xcp_cdiv(N, BN);
+  const int wmw = g_nt_cfg == 1 ? 4 : 2;
+  const int grid = xcp_cdiv(M, 64 * wmw) * xcp_cdiv(N, NBN);
+#define XCP_NT_CFG(TT, GMV)                                                                                     \
+  if (wmw == 4) hipLaunchKernelGGL((gemm_nt_kernel<TT, GMV, 4, 3>), dim3(grid), dim3(512), 0, stream, a);        \
+  else hipLaunchKernelGGL((gemm_nt_kernel<TT, GMV, 2, 2>), dim3(grid), dim3(256), 0, stream, a);
 #define XCP_NT_LAUNCH(TT)                                                                                      \
   switch (gmode) {                                                                                             \
-    case 0: hipLaunchKernelGGL((gemm_nt_kernel<TT, 0>), dim3(grid), dim3(NT), 0, stream, a); break;          \
-    case 1: hipLaunchKernelGGL((gemm_nt_kernel<TT, 1>), dim3(grid), dim3(NT), 0, stream, a); break;          \
-    case 2: hipLaunchKernelGGL((gemm_nt_kernel<TT, 2>), dim3(grid), dim3(NT), 0, stream, a); break;          \
-    default: hipLaunchKernelGGL((gemm_nt_kernel<TT, 3>), dim3(grid), dim3(NT), 0, stream, a); break;         \
+    case 0: XCP_NT_CFG(TT, 0) break;                                                                           \
+    case 1: XCP_NT_CFG(TT, 1) break;                                                                           \
+    case 2: XCP_NT_CFG(TT, 2) break;                                                                           \
+    default: XCP_NT_CFG(TT, 3) break;                                                                          \
   }
   if (dtype == XCP_BF16) {
     XCP_NT_LAUNCH(bf16)
@@ -419,9 +493,23 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   } else {
     return XCP_EUNSUPPORTED;
   }
+#undef XCP_NT_CFG
 #undef XCP_NT_LAUNCH
   return (int)hipGetLastError();
 }
+
+// rows of the stats partial array gemm_nt writes ([rows][2][N])
+int xcp_gemm_nt_stat_rows(int M) { return xcp_cdiv(M, g_nt_cfg == 1 ? 256 : 128); }
+
+}  // extern "C"
+
+int xcp_internal_gemm_tune(int cfg) {
+  const int old = g_nt_cfg;
+  if (cfg == 0 || cfg == 1) g_nt_cfg = cfg;
+  return old;
+}
+
+extern "C" {
 
 // P[s][N][K] partial weight gradients; S splits of rows_per_split rows each.
 int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, float* P, int M, int N, int K, int S,

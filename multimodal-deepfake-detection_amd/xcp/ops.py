@@ -92,7 +92,7 @@ def gemm_tn(G, X, P, M, N, K, S, rows_per_split, ldg=None, ldx=None, gather=(0, 
 
 
 def nt_stat_rows(M):
-    return (M + 127) // 128
+    return _lib.call("xcp_gemm_nt_stat_rows", M)
 
 
 def colreduce_f64(inp, S, L, out, G):

@@ -86,9 +86,13 @@ def test_backbone64_vs_reference(gpu, golden, prec):
                 errs[n] = abs(p.grad.double().norm().item() - g[key]) / max(g[key], 1e-30)
         check_gradnorms(errs, bn_param_names(m), prec == "fp32")
         for n, t in m.state_dict().items():
-            if "running" in n:
+            if "running_var" in n:
                 np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"],
                                            rtol=1e-4 if prec == "fp32" else 2e-2, atol=1e-4, err_msg=n)
+            elif "running_mean" in n:   # a signed sum: absolute tolerance in bf16
+                np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"],
+                                           rtol=1e-4 if prec == "fp32" else 5e-2,
+                                           atol=1e-4 if prec == "fp32" else 5e-2, err_msg=n)
         m.eval()
         with torch.no_grad():
             fev = m(x).cpu().numpy()
@@ -157,3 +161,50 @@ def test_engine_deterministic(gpu):
         outs.append((f.detach().clone(), m.block5.rep[1].pointwise.weight.grad.clone(), m.conv1.weight.grad.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def test_bf16_gradient_noise_vs_torch_autocast(gpu):
+    """The bf16 path's gradient noise is compared with PyTorch's own bf16 autocast on the
+    same graph (the oracle's functional restatement run on the GPU under
+    torch.autocast(bfloat16), i.e. MIOpen/hipBLASLt kernels): per backbone weight, the
+    cosine similarity to the fp32 xcp gradient (itself pinned to the reference goldens).
+    The xcp bf16 median cosine must not be worse than autocast's by more than 0.02."""
+    import xcp
+    from Models.XceptionLSTMV import XceptionLSTMV
+    from oracle import xception_oracle as O
+    B, T, S = 2, 4, 299
+    x = seeded_uniform((B, T, 3, S, S), 1234).to(gpu)
+    y = torch.tensor([[0.0], [1.0]], device=gpu)
+
+    def xcp_grads(prec):
+        torch.manual_seed(0)
+        m = XceptionLSTMV(128, pretrained=False)
+        for p in m.feature_extractor.parameters():
+            p.requires_grad = True
+        m = m.to(gpu).train()
+        m.fc_layers.eval()
+        with xcp.precision(prec):
+            nn.BCELoss()(m(m.extract_features(x, gpu)), y).backward()
+        return {n: p.grad.detach().double() for n, p in m.named_parameters()}
+
+    g32 = xcp_grads("fp32")
+    g16 = xcp_grads("bf16")
+    torch.manual_seed(0)
+    sd = {k: v.to(gpu) for k, v in XceptionLSTMV(128, pretrained=False).state_dict().items()}
+    params = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v.clone())
+              for k, v in sd.items()}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        feats = O.backbone_forward(x.reshape(B * T, 3, S, S), params, True, {}, prefix="feature_extractor.")
+    prob, _ = O.head_forward(feats.float().view(B, T, -1), params)
+    nn.BCELoss()(prob, y).backward()
+    ga = {k: v.grad.detach().double() for k, v in params.items() if getattr(v, "grad", None) is not None}
+
+    def cosd(a, b):
+        return float((a * b).sum() / (a.norm() * b.norm() + 1e-300))
+
+    keys = [k for k in g32 if k.startswith("feature_extractor.") and k.endswith("weight") and g32[k].numel() > 100]
+    c16 = np.array([cosd(g16[k], g32[k]) for k in keys])
+    cau = np.array([cosd(ga[k], g32[k]) for k in keys])
+    print(f"median cos: xcp-bf16 {np.median(c16):.4f}  torch-autocast-bf16 {np.median(cau):.4f}; "
+          f"min: {c16.min():.4f} / {cau.min():.4f}")
+    assert np.median(c16) >= np.median(cau) - 0.02

@@ -75,10 +75,30 @@ def main():
                 3 * tensor_bytes)
             ops._lib.call("xcp_tune", 1, old)
     if not sel or "gemm" in sel:
-        rep("gemm_nt 728x728 +stats", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=stats)),
-            flops=2.0 * M * C * C)
+        for cfg in (0, 1):
+            old = ops._lib.call("xcp_tune", 2, cfg)
+            st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
+            rep(f"gemm_nt 728x728 +stats cfg={cfg}", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=st2)),
+                flops=2.0 * M * C * C)
+            ops._lib.call("xcp_tune", 2, old)
         out = torch.empty(C * C, device=dev)
         rep("weight_grad 728x728", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)), flops=2.0 * M * C * C)
+    if "gemmk" in sel:
+        for cfg in (0, 1):
+            old = ops._lib.call("xcp_tune", 2, cfg)
+            for K2 in (128, 728, 1456):
+                A2 = torch.randn(M, K2, device=dev, generator=g).to(dt)
+                W2 = (torch.randn(C, K2, device=dev, generator=g) / 27).to(dt)
+                st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
+                rep(f"gemm_nt K={K2} N=728 cfg={cfg}", timeit(lambda: ops.gemm_nt(A2, W2, Y, M, C, K2, stats=st2)),
+                    flops=2.0 * M * C * K2)
+            rep(f"gemm_nt K=728 nostats cfg={cfg}", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C)),
+                flops=2.0 * M * C * C)
+            W3 = (torch.randn(768, C, device=dev, generator=g) / 27).to(dt)
+            Y3 = torch.empty(M, 768, device=dev, dtype=dt)
+            rep(f"gemm_nt K=728 N=768 cfg={cfg}", timeit(lambda: ops.gemm_nt(X, W3, Y3, M, 768, C)),
+                flops=2.0 * M * 768 * C)
+            ops._lib.call("xcp_tune", 2, old)
     if not sel or "bn" in sel:
         dgm, dbt = torch.empty(C, device=dev), torch.empty(C, device=dev)
         bn = {"weight": sc, "bias": sh, "running_mean": None, "running_var": None, "eps": 1e-5, "momentum": 0.1,
