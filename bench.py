@@ -78,6 +78,27 @@ def cpu_baseline(args, frames):
                       f"fp32, oracle/xception_oracle.py (PyTorch CPU), {cpu_name}"}
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the two roofline kernels, from the newest committed
+    ``profiles/*_traffic.json`` (tools/pmc_traffic.py over separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes of this bench, FETCH_SIZE x2 gfx950 correction).  The middle-flow
+    shape is the most frequent dispatch of each kernel, so it is the group with most launches.
+    Returns ({kernel base: (bytes, source)}) or {} when no file exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")))
+    if not files:
+        return {}
+    data = json.load(open(files[-1]))
+    out = {}
+    for b in ("gemm_nt_kernel", "dw_fwd_kernel"):
+        cand = [v for v in data.values() if v.get("base") == b]
+        if cand:
+            v = max(cand, key=lambda v: v["launches"])
+            out[b] = (v["traffic_bytes"], f"{os.path.relpath(files[-1], REPO)}: {v['kernel']} grid={v['grid']}, "
+                                          f"2*FETCH_SIZE+WRITE_SIZE mean over {v['launches']} launches")
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,6 +179,7 @@ def main():
         M = B * T * 19 * 19
         roof = None
         extra = {}
+        traffic = pmc_traffic()
         if timer is not None:
             pw_ms = timer.mean_ms("pw_gemm_728")
             dw_ms = timer.mean_ms("dw_fwd_728")
@@ -165,7 +187,9 @@ def main():
                 flops = 2.0 * M * 728 * 728
                 ach = flops / (pw_ms * 1e-3) / 1e12
                 roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                        "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                        "traffic": traffic.get("gemm_nt_kernel", (None,))[0],
+                        "traffic_source": traffic.get("gemm_nt_kernel", (None, None))[1],
                         "kernel": "gemm_nt_kernel<bf16> (pointwise 1x1 728->728 @19x19, middle flow)",
                         "flops_per_launch": flops, "avg_launch_ms": round(pw_ms, 4),
                         "launches": timer.count("pw_gemm_728")}
@@ -173,7 +197,9 @@ def main():
                 byts = 2.0 * (2 * M * 728) + 4 * 9 * 728
                 gbs = byts / (dw_ms * 1e-3) / 1e9
                 extra["roofline_dw"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                        "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                                        "frac": round(gbs / PEAK_HBM_GBS, 4),
+                                        "traffic": traffic.get("dw_fwd_kernel", (None,))[0],
+                                        "traffic_source": traffic.get("dw_fwd_kernel", (None, None))[1],
                                         "kernel": "dw_fwd_kernel<bf16> (depthwise 3x3 C=728 @19x19)",
                                         "bytes_per_launch": byts, "avg_launch_ms": round(dw_ms, 4)}
         out = {"metric": "clips/sec (node) XceptionLSTMV 16x299x299 bf16 train",

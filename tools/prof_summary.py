@@ -1,10 +1,52 @@
-"""Summarise a rocprofv3 kernel trace (SQLite .db or kernel_stats/kernel_trace CSV):
-per-kernel total/avg time and share of GPU time; optionally only the last K steps."""
+"""Summarise a rocprofv3 kernel trace (kernel_trace CSV or SQLite .db): per-kernel total /
+average time and share of GPU time, then per (kernel instance, grid) -- the shape-level view
+that bench.py's live HIP-event timing is compared against.
+
+rocprofv3 reports some dispatches of one instantiation under its mangled name and others
+under a lossy demangled one ("gemm_nt_kernel<bool _Accum, int, E, 2, 2>"); dispatches are
+therefore grouped on (base name, grid, workgroup, LDS, VGPRs) and labelled with the decoded
+mangled name seen in that group.
+
+usage: python tools/prof_summary.py <kernel_trace.csv | .db | dir> [top]
+"""
 import csv
 import glob
 import os
+import re
 import sqlite3
 import sys
+from collections import defaultdict
+
+_TYPES = {"DF16b": "bf16", "f": "float", "d": "double", "h": "u8", "i": "int"}
+
+
+def decode(name):
+    """Decode the mangled names of this repo's kernels: _ZN12_GLOBAL__N_1<n><ident>I<args>E..."""
+    m = re.match(r"_ZN12_GLOBAL__N_1(\d+)(\w+)", name)
+    if not m:
+        return None
+    n = int(m.group(1))
+    ident = m.group(2)[:n]
+    rest = m.group(2)[n:]
+    args = []
+    if rest.startswith("I"):
+        body = rest[1:]
+        while body and not body.startswith("EE") and not body.startswith("Ev"):
+            mm = re.match(r"Li(-?\d+)E|(DF16b|f|d|h|i)", body)
+            if not mm:
+                break
+            args.append(mm.group(1) if mm.group(1) is not None else _TYPES[mm.group(2)])
+            body = body[mm.end():]
+    return f"{ident}<{', '.join(args)}>" if args else ident
+
+
+def base(name):
+    m = re.search(r"(\w+_kernel)", name)
+    if m:
+        b = m.group(1)
+        return re.sub(r"^\d+", "", b.replace("_ZN12_GLOBAL__N_1", ""))
+    n = name.replace("void ", "").split("(")[0]
+    return n[:60]
 
 
 def load(path):
@@ -12,38 +54,48 @@ def load(path):
     if path.endswith(".db"):
         c = sqlite3.connect(path)
         for name, dur, grid in c.execute("select name, duration, grid_x from kernels order by start"):
-            rows.append((name, dur, grid))
+            rows.append((name, dur, (grid,)))
     else:
         with open(path) as f:
             for r in csv.DictReader(f):
-                rows.append((r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), r.get("Grid_Size_X")))
+                key = (r.get("Grid_Size_X"), r.get("Workgroup_Size_X"), r.get("LDS_Block_Size"), r.get("VGPR_Count"))
+                rows.append((r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), key))
     return rows
-
-
-def short(n):
-    for p in ("void ", "(anonymous namespace)::", "_ZN12_GLOBAL__N_1"):
-        n = n.replace(p, "")
-    n = n.split("(")[0]
-    return n[:70]
 
 
 def main():
     path = sys.argv[1]
+    top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     if os.path.isdir(path):
-        cands = glob.glob(os.path.join(path, "**", "*.db"), recursive=True) + \
-            glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
+        cands = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True) + \
+            glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
         path = cands[0]
     rows = load(path)
-    agg = {}
-    for name, dur, _ in rows:
-        k = short(name)
-        t, c = agg.get(k, (0, 0))
-        agg[k] = (t + dur, c + 1)
-    total = sum(t for t, _ in agg.values())
-    print(f"source: {path}\ntotal kernel time {total / 1e6:.3f} ms over {len(rows)} dispatches")
-    print(f"{'kernel':72s} {'calls':>6s} {'total ms':>10s} {'avg us':>9s} {'%':>6s}")
-    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:40]:
-        print(f"{k:72s} {c:6d} {t / 1e6:10.3f} {t / c / 1e3:9.1f} {100 * t / total:6.2f}")
+    labels = {}
+    for name, _, key in rows:
+        d = decode(name)
+        if d:
+            labels[(base(name),) + key] = d
+    by_base = defaultdict(lambda: [0, 0])
+    by_inst = defaultdict(lambda: [0, 0])
+    for name, dur, key in rows:
+        b = base(name)
+        by_base[b][0] += dur
+        by_base[b][1] += 1
+        ik = (b,) + key
+        by_inst[ik][0] += dur
+        by_inst[ik][1] += 1
+    total = sum(t for t, _ in by_base.values())
+    print(f"source: {path}\ntotal kernel time {total / 1e6:.3f} ms over {len(rows)} dispatches\n")
+    print(f"{'kernel':60s} {'calls':>6s} {'total ms':>10s} {'avg us':>9s} {'%':>6s}")
+    for k, (t, c) in sorted(by_base.items(), key=lambda kv: -kv[1][0])[:top]:
+        print(f"{k:60s} {c:6d} {t / 1e6:10.3f} {t / c / 1e3:9.1f} {100 * t / total:6.2f}")
+    print(f"\nper instance and grid (grid = work-items, x)\n{'kernel instance':44s} {'grid':>10s} {'wg':>4s} "
+          f"{'calls':>6s} {'total ms':>10s} {'avg us':>9s} {'%':>6s}")
+    for k, (t, c) in sorted(by_inst.items(), key=lambda kv: -kv[1][0])[:top]:
+        lab = labels.get(k, k[0])
+        print(f"{lab[:44]:44s} {str(k[1]):>10s} {str(k[2]):>4s} {c:6d} {t / 1e6:10.3f} {t / c / 1e3:9.1f} "
+              f"{100 * t / total:6.2f}")
 
 
 if __name__ == "__main__":
