@@ -90,8 +90,8 @@ def pmc_traffic():
         return {}
     data = json.load(open(files[-1]))
     out = {}
-    for b in ("gemm_nt_kernel", "dw_fwd_kernel"):
-        cand = [v for v in data.values() if v.get("base") == b]
+    for b in ("gemm_nt", "dw_fwd_kernel"):
+        cand = [v for v in data.values() if v.get("base", "").startswith(b)]
         if cand:
             v = max(cand, key=lambda v: v["launches"])
             out[b] = (v["traffic_bytes"], f"{os.path.relpath(files[-1], REPO)}: {v['kernel']} grid={v['grid']}, "
@@ -188,9 +188,9 @@ def main():
                 ach = flops / (pw_ms * 1e-3) / 1e12
                 roof = {"bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / PEAK_BF16_TFLOPS, 4),
-                        "traffic": traffic.get("gemm_nt_kernel", (None,))[0],
-                        "traffic_source": traffic.get("gemm_nt_kernel", (None, None))[1],
-                        "kernel": "gemm_nt_kernel<bf16> (pointwise 1x1 728->728 @19x19, middle flow)",
+                        "traffic": traffic.get("gemm_nt", (None,))[0],
+                        "traffic_source": traffic.get("gemm_nt", (None, None))[1],
+                        "kernel": "gemm_nt256k64_kernel (bf16 pointwise 1x1 728->728 @19x19, middle flow)",
                         "flops_per_launch": flops, "avg_launch_ms": round(pw_ms, 4),
                         "launches": timer.count("pw_gemm_728")}
             if dw_ms:

@@ -64,7 +64,10 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
 int xcp_dw_bwd_chunks(int N, int H, int W, int C);
 /* launch tuning knobs: 0 = depthwise forward / 1 = depthwise backward halo pixels per
  * LDS tile (256 or 512); 2 = pointwise GEMM tile (0: 128x128 2-stage, 1: 256x128
- * 3-stage).  Returns the previous value (-1: unknown knob). */
+ * 3-stage, 2: auto -- 256x256 8-wave kernel for dense bf16 with >= 256 tiles and
+ * K >= 384, 3: that kernel for every dense bf16 call); 3 = 256x256 kernel schedule
+ * (0: staggered wave groups, 1: lockstep; measurement only).
+ * Returns the previous value (-1: unknown knob). */
 int xcp_tune(int knob, int value);
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
                const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, float* bnpart,

@@ -420,6 +420,7 @@ inline int ngroups_for(int C, int dtype) {
 }  // namespace
 
 int xcp_internal_gemm_tune(int cfg);   // gemm.hip
+int xcp_internal_gemm_var(int v);      // gemm.hip
 
 extern "C" {
 
@@ -428,6 +429,7 @@ extern "C" {
 // config (0: 128x128 / 2-stage ring, 1: 256x128 / 3-stage).  Returns the old value.
 int xcp_tune(int knob, int value) {
   if (knob == 2) return xcp_internal_gemm_tune(value);
+  if (knob == 3) return xcp_internal_gemm_var(value);
   int* k = knob == 0 ? &g_fwd_maxpx : knob == 1 ? &g_bwd_maxpx : nullptr;
   if (!k) return -1;
   const int old = *k;

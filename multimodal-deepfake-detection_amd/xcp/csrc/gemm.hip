@@ -13,7 +13,10 @@
 //   gemm_tn : P[s][N,K] = sum_{m in split s} G[m,N]^T X[m,K]   (weight gradient;
 //             fp32 partial slabs, reduced deterministically by xcp_colreduce_f32).
 //
-// Tile 128x128, 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16 tiles.
+// Dense bf16 NT calls with enough work run on a 256x256-tile, 8-wave kernel with a
+// four-phase quadrant schedule (gemm_nt256k64_kernel); everything else (fp32 parity
+// mode, gathered rows, small problems) on a 128x128-tile, 4-wave kernel (each wave
+// 64x64 = 4x4 MFMA 16x16 tiles).
 // bf16: v_mfma_f32_16x16x32_bf16, fp32: v_mfma_f32_16x16x4_f32 (exact fp32).
 // LDS rows are 128 B (one 64-deep bf16 / 32-deep fp32 K-stage), 16-B chunks
 // XOR-swizzled with (row>>1)&7 so a 16-lane ds_read_b128 group is conflict-free.
@@ -101,6 +104,7 @@ constexpr int NBN = 128;
 template <int N>
 XCP_DEV void wait_vmcnt() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else static_assert(N == 0, "unsupported count");
@@ -310,7 +314,247 @@ __global__ __launch_bounds__(WMW * 128) void gemm_nt_kernel(NTArgs a) {
   }
 }
 
-int g_nt_cfg = 0;   // xcp_tune knob 2: 0 = 128x128 tile / 2-stage ring, 1 = 256x128 / 3-stage
+constexpr int L_CP = 256 * 2 + 16;             // LDS-staged epilogue row pitch (bytes)
+
+// LDS-staged epilogue of the 256x256 kernels: acc[i][j][r] is C[row wr*128 + i*16 + fr]
+// [col wc*64 + j*16 + fg*4 + r]; rounded tile staged in LDS, written with coalesced 16-B
+// stores, BatchNorm partial sums per 128-row half ([ceil(M/128)][2][N] layout).
+XCP_DEV void epilogue256(f32x4 (&acc)[8][4], char* smem, const NTArgs& a, int m0, int n0, int bm, int tid) {
+  const int lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3, fr = lane & 15, fg = lane >> 4;
+  bf16* C = reinterpret_cast<bf16*>(a.C);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wr * 128 + i * 16 + fr, col = wc * 64 + j * 16 + fg * 4;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
+        VecIO<bf16, 4>::store(reinterpret_cast<bf16*>(smem + row * L_CP + col * 2), v);
+      }
+    __syncthreads();
+    const int c = tid & 31, rq = tid >> 5;
+    const int n = n0 + c * 8;
+    float t1[2][8], t2[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t1[h][e] = t2[h][e] = 0.f;
+    uint4 cv[16];
+#pragma unroll
+    for (int it = 0; it < 16; ++it) cv[it] = *reinterpret_cast<const uint4*>(smem + (rq + 16 * it) * L_CP + c * 16);
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int m = m0 + rq + 16 * it;
+      if (m < a.M && n < a.N) {
+        *reinterpret_cast<uint4*>(C + (long)m * a.ldc + n) = cv[it];
+        float f[8];
+        VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&cv[it]), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          t1[it >> 3][e] += f[e];
+          t2[it >> 3][e] = fmaf(f[e], f[e], t2[it >> 3][e]);
+        }
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          t1[h][e] += __shfl_xor(t1[h][e], 32, 64);
+          t2[h][e] += __shfl_xor(t2[h][e], 32, 64);
+        }
+      float* red = reinterpret_cast<float*>(smem);   // [h][q][wave][256]
+      lds_barrier();
+      if (lane < 32) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            red[((h * 2 + 0) * 8 + w) * 256 + c * 8 + e] = t1[h][e];
+            red[((h * 2 + 1) * 8 + w) * 256 + c * 8 + e] = t2[h][e];
+          }
+      }
+      lds_barrier();
+      const int h = tid >> 8, col = tid & 255;
+      const int nn = n0 + col, srow = bm * 2 + h;
+      if (nn < a.N && srow < (a.M + 127) / 128) {
+        float u1 = 0.f, u2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          u1 += red[((h * 2 + 0) * 8 + q) * 256 + col];
+          u2 += red[((h * 2 + 1) * 8 + q) * 256 + col];
+        }
+        a.stats[((long)srow * 2 + 0) * a.N + nn] = u1;
+        a.stats[((long)srow * 2 + 1) * a.N + nn] = u2;
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 256x256 bf16 NT kernel with 64-deep K-tiles (128-B LDS rows, so every 1-KB LDS-DMA
+// instruction fetches 8 whole 128-B lines; 64-B rows fetch 16 half lines and measured
+// half the load throughput).  Two ring slots of 64 KB.  8 waves (2 M-groups x 4 N),
+// wave tile 128x64; a K-tile is four phases, one 64x32 quadrant (16 MFMA) each:
+//   Q0 (A-top, B-left)  reads A-top + B-left   issues A-top(t+1)
+//   Q1 (A-top, B-right) reads B-right          issues B-left(t+1)
+//   Q2 (A-bot, B-right) reads A-bot            issues B-right(t+1)
+//   Q3 (A-bot, B-left)  --                     issues A-bot(t+1)
+// ("A-top" = the 64 rows of a wave group's first half, both groups: one half-tile of
+// 128 rows = 2 LDS-DMA loads per thread).  Tile t+1 goes to the slot of tile t-1,
+// whose last reads (Q2 of t-1) retired >= 3 barriers before Q0(t).  Each half-tile is
+// retired by a counted vmcnt in the phase BEFORE the one that reads it (so every
+// wave has waited before the barrier the reader passes): Q3 retires A-top / B-left of
+// t+1, Q0 retires B-right, Q1 retires A-bot.  Wave group 1 runs one barrier behind
+// group 0 (its MFMA cluster overlaps group 0's reads and load issue).
+constexpr int K_OP = 256 * 128;                // one operand, one slot (32 KB)
+constexpr int K_SLOT = 2 * K_OP;
+
+XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
+  if (n >= 4) wait_vmcnt<4>();
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else wait_vmcnt<0>();
+}
+
+template <bool STAG>
+__global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
+  constexpr int RING = 2 * K_SLOT, EPI = 256 * L_CP;
+  __shared__ __attribute__((aligned(16))) char smem[RING > EPI ? RING : EPI];
+  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
+  const int id = xcd_remap(blockIdx.x, gridM * gridN);
+  const int bn = id % gridN, bm = id / gridN;
+  const int m0 = bm * 256, n0 = bn * 256;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const bf16* A = reinterpret_cast<const bf16*>(a.A);
+  const bf16* B = reinterpret_cast<const bf16*>(a.B);
+
+  // half-tile rows loaded by this wave (2 x 8 rows per half-tile):
+  //   A-top: (w<4 ? 16w : 128+16(w-4)) + [0,16);  A-bot: that + 64
+  //   B-left: 64(w>>1) + 16(w&1) + [0,16);         B-right: that + 32
+  const int arow = (w < 4 ? 16 * w : 128 + 16 * (w - 4));
+  const int brow = 64 * (w >> 1) + 16 * (w & 1);
+  const int lr = lane >> 3;
+  const bf16* src[4][2];   // [half-tile][i]
+  int kc8[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool isA = (h == 0 || h == 3);
+      const int row = (isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0)) + i * 8 + lr;
+      kc8[h][i] = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+      src[h][i] = isA ? A + (long)min(m0 + row, a.M - 1) * a.lda + kc8[h][i]
+                      : B + (long)min(n0 + row, a.N - 1) * a.ldb + kc8[h][i];
+    }
+  const void* zero = g_zero16;
+  asm volatile("" : "+v"(zero));
+  auto glds = [](const void* p, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  // half-tile h of K-tile kt: h 0 = A-top, 1 = B-left, 2 = B-right, 3 = A-bot
+  auto issue = [&](int h, int kt) {
+    const bool isA = (h == 0 || h == 3);
+    const int row0 = isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0);
+    char* d = smem + (kt & 1) * K_SLOT + (isA ? 0 : K_OP) + row0 * 128;
+    const int kb = kt * 64;
+    if (kb + 64 <= a.K) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds(src[h][i] + kb, d + i * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds(kb + kc8[h][i] < a.K ? (const void*)(src[h][i] + kb) : zero, d + i * 1024);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (a.K + 63) / 64;
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue(h, 0);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  if (STAG && wr == 1) __builtin_amdgcn_s_barrier();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  bf16x8 af[4][2], bl[2][2], br[2][2];   // [frag][k-step]
+  auto mfma_q = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ih * 4 + i][jh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][ks], af[i][ks], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+  };
+  auto sync_mfma = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma_q(ih, b, jh);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* sa = smem + (kt & 1) * K_SLOT;
+    const char* sb = sa + K_OP;
+    const bool nxt = kt + 1 < nk;
+    // Q0: A-top x B-left
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bl[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + j * 16 + fr, ks * 4 + fg));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 16 + fr, ks * 4 + fg));
+    }
+    if (nxt) issue(0, kt + 1);
+    wait_cnt(2 + (nxt ? 2 : 0));          // B-right(kt) for Q1
+    sync_mfma(0, bl, 0);
+    // Q1: A-top x B-right
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        br[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + 32 + j * 16 + fr, ks * 4 + fg));
+    if (nxt) issue(1, kt + 1);
+    wait_cnt(nxt ? 4 : 0);                // A-bot(kt) for Q2
+    sync_mfma(0, br, 1);
+    // Q2: A-bot x B-right
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
+    if (nxt) issue(2, kt + 1);
+    sync_mfma(1, br, 1);
+    // Q3: A-bot x B-left
+    if (nxt) {
+      issue(3, kt + 1);
+      wait_cnt(4);                        // A-top / B-left(kt+1) for Q0(kt+1)
+    }
+    sync_mfma(1, bl, 0);
+  }
+  if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
+  epilogue256(acc, smem, a, m0, n0, bm, tid);
+}
+
+int g_nt256_var = 0;   // xcp_tune knob 3: 0 = staggered wave groups, 1 = lockstep (measurement)
+
+// xcp_tune knob 2: 0 = 128x128 tile / 2-stage ring, 1 = 256x128 / 3-stage,
+// 2 = auto (256x256 8-wave kernel for dense bf16 with >= 256 tiles and K >= 384, else 128x128),
+// 3 = 256x256 kernel for every dense bf16 call (tests)
+int g_nt_cfg = 2;
 
 // ---------------------------------------------------------------------------------
 // Weight gradient: P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]
@@ -474,6 +718,14 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
+  if (g_nt_cfg >= 2 && dtype == XCP_BF16 && gmode == 0) {
+    const int tiles = xcp_cdiv(M, 256) * xcp_cdiv(N, 256);
+    if ((tiles >= 256 && K >= 384) || g_nt_cfg == 3) {
+      if (g_nt256_var == 1) hipLaunchKernelGGL((gemm_nt256k64_kernel<false>), dim3(tiles), dim3(512), 0, stream, a);
+      else hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);
+      return (int)hipGetLastError();
+    }
+  }
   const int wmw = g_nt_cfg == 1 ? 4 : 2;
   const int grid = xcp_cdiv(M, 64 * wmw) * xcp_cdiv(N, NBN);
 #define XCP_NT_CFG(TT, GMV)                                                                                     \
@@ -503,9 +755,15 @@ int xcp_gemm_nt_stat_rows(int M) { return xcp_cdiv(M, g_nt_cfg == 1 ? 256 : 128)
 
 }  // extern "C"
 
+int xcp_internal_gemm_var(int v) {
+  const int old = g_nt256_var;
+  if (v == 0 || v == 1) g_nt256_var = v;
+  return old;
+}
+
 int xcp_internal_gemm_tune(int cfg) {
   const int old = g_nt_cfg;
-  if (cfg == 0 || cfg == 1) g_nt_cfg = cfg;
+  if (cfg >= 0 && cfg <= 3) g_nt_cfg = cfg;
   return old;
 }
 

@@ -54,6 +54,39 @@ def test_gemm_nt_stats(ops, gpu, dt, M, N, K):
     torch.testing.assert_close(s[1], (Cs * Cs).sum(0), rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,N,K,lda", [(256, 256, 32, 32), (1000, 728, 728, 728), (300, 2048, 1536, 1536),
+                                       (77, 64, 288, 288), (513, 264, 40, 40), (92416 // 8, 728, 728, 736),
+                                       (4100, 1024, 728, 1456)])
+@pytest.mark.parametrize("var", [0, 1])
+def test_gemm_nt256_stats(ops, gpu, M, N, K, lda, var):
+    """The 256x256 8-wave bf16 kernel (forced for every size): ragged M / N, K tails
+    (K % 32 != 0), a row pitch wider than K, and the 128-row stats partial layout."""
+    g = torch.Generator(device=gpu).manual_seed(M + N + K)
+    Abuf = torch.randn(M, lda, device=gpu, generator=g).bfloat16()
+    A = Abuf[:, :K]
+    B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
+    C = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+    old = ops._lib.call("xcp_tune", 2, 3)
+    oldv = ops._lib.call("xcp_tune", 3, var)
+    try:
+        R = ops.nt_stat_rows(M)
+        part = torch.full((R, 2, N), float("nan"), device=gpu)
+        ops.gemm_nt(Abuf, B, C, M, N, K, lda=lda, stats=part)
+        torch.cuda.synchronize()
+    finally:
+        ops._lib.call("xcp_tune", 2, old)
+        ops._lib.call("xcp_tune", 3, oldv)
+    ref = A.float() @ B.float().t()
+    assert rel_err(C.float(), ref) < 1e-2
+    s = part.double().sum(0)
+    Cs = C.double()
+    torch.testing.assert_close(s[0], Cs.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(s[1], (Cs * Cs).sum(0), rtol=1e-5, atol=1e-3)
+    # the partial of rows [128r, 128r+128) is row r
+    r = (M - 1) // 128
+    torch.testing.assert_close(part[r, 0].double(), Cs[128 * r:].sum(0), rtol=1e-5, atol=1e-3)
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 def test_gemm_nt_strided_gather(ops, gpu, dt):
     N, H, W, Cin, Cout = 3, 37, 37, 256, 728

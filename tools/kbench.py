@@ -75,7 +75,7 @@ def main():
                 3 * tensor_bytes)
             ops._lib.call("xcp_tune", 1, old)
     if not sel or "gemm" in sel:
-        for cfg in (0, 1):
+        for cfg in (0, 1, 2):
             old = ops._lib.call("xcp_tune", 2, cfg)
             st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
             rep(f"gemm_nt 728x728 +stats cfg={cfg}", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=st2)),
@@ -83,8 +83,19 @@ def main():
             ops._lib.call("xcp_tune", 2, old)
         out = torch.empty(C * C, device=dev)
         rep("weight_grad 728x728", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)), flops=2.0 * M * C * C)
+    if "gemmv" in sel:
+        for var in [int(v) for v in os.environ.get('XCP_VARS', '0,1').split(',')]:
+            old = ops._lib.call("xcp_tune", 3, var)
+            st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
+            rep(f"gemm256 var={var} +stats", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=st2)),
+                flops=2.0 * M * C * C)
+            rep(f"gemm256 var={var} nostats", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C)), flops=2.0 * M * C * C)
+            A2 = torch.randn(M, 1456, device=dev, generator=g).to(dt)
+            W2 = (torch.randn(C, 1456, device=dev, generator=g) / 27).to(dt)
+            rep(f"gemm256 var={var} K=1456", timeit(lambda: ops.gemm_nt(A2, W2, Y, M, C, 1456)), flops=2.0 * M * C * 1456)
+            ops._lib.call("xcp_tune", 3, old)
     if "gemmk" in sel:
-        for cfg in (0, 1):
+        for cfg in (0, 2):
             old = ops._lib.call("xcp_tune", 2, cfg)
             for K2 in (128, 728, 1456):
                 A2 = torch.randn(M, K2, device=dev, generator=g).to(dt)
