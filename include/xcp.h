@@ -66,7 +66,8 @@ int xcp_dw_bwd_chunks(int N, int H, int W, int C);
  * LDS tile (256 or 512); 2 = pointwise GEMM tile (0: 128x128 2-stage, 1: 256x128
  * 3-stage, 2: auto -- 256x256 8-wave kernel for dense bf16 with >= 256 tiles and
  * K >= 384, 3: that kernel for every dense bf16 call); 3 = 256x256 kernel schedule
- * (0: staggered wave groups, 1: lockstep; measurement only).
+ * (0: staggered wave groups, 1: lockstep; measurement only); 4 / 5 = depthwise
+ * forward / backward kernel family (0: row walk, 1: LDS tile).
  * Returns the previous value (-1: unknown knob). */
 int xcp_tune(int knob, int value);
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,

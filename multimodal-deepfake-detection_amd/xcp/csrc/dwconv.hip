@@ -417,6 +417,345 @@ inline int ngroups_for(int C, int dtype) {
   return (C + cpg - 1) / cpg;
 }
 
+
+// =================================================================================
+// Row-walk kernels (default).  The tile kernels above are VALU-bound (measured
+// 36 / 67 VALU lane-ops per element, fwd / bwd: halo index arithmetic, per-window
+// bf16 unpacking, unpacked fp32 math).  Here one WAVE owns one channel slice
+// (64 B: 32 bf16 / 16 fp32 channels) of one frame over RCOLS = 20 output columns and
+// walks down all H rows: lane (cl, s) = (lane & 15, lane >> 4) holds one channel
+// dword (2 bf16 -> float2, packed v_pk_fma_f32 math) for the 5 output columns
+// 5s .. 5s+4 of the wave's column range, with a rolling 3-row register window of 7
+// columns.  Each input row is loaded once per lane (7 dwords; the 2-column overlap
+// of neighbouring segments is served by L1/L2), activated and unpacked once, and
+// feeds 3 output rows; the next row is prefetched one step ahead.  No LDS, no
+// barriers: waves are independent (4 per workgroup = 4 neighbouring channel slices
+// of one frame, i.e. whole 128-B lines).  dW / BN partial sums are reduced over the
+// 4 lane segments with cross-lane shuffles and written once per (frame, column
+// group): P = N * ceil(W / 20).
+constexpr int RS = 5, RNS = 4, RCOLS = RS * RNS;
+typedef float rf2 __attribute__((ext_vector_type(2)));
+
+template <typename T> struct RV;
+template <> struct RV<bf16> {
+  typedef rf2 V;
+  static constexpr int EPT = 2;
+  static XCP_DEV V unpack(unsigned u) { return V{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; }
+  static XCP_DEV unsigned pack(V v) {
+    bf16x4 q;
+    q[0] = (bf16)v[0];
+    q[1] = (bf16)v[1];
+    const u16x4 r = __builtin_bit_cast(u16x4, q);
+    return (unsigned)r[0] | ((unsigned)r[1] << 16);
+  }
+  static XCP_DEV V load(const float* p) { return V{p[0], p[1]}; }
+  static XCP_DEV float get(V v, int e) { return v[e]; }
+};
+template <> struct RV<float> {
+  typedef float V;
+  static constexpr int EPT = 1;
+  static XCP_DEV V unpack(unsigned u) { return __uint_as_float(u); }
+  static XCP_DEV unsigned pack(V v) { return __float_as_uint(v); }
+  static XCP_DEV V load(const float* p) { return p[0]; }
+  static XCP_DEV float get(V v, int) { return v; }
+};
+
+template <typename V> XCP_DEV V vfma(V a, V b, V c) { return __builtin_elementwise_fma(a, b, c); }
+template <typename V> XCP_DEV V vmax0(V a) { return __builtin_elementwise_max(a, V(0.f)); }
+
+struct RowMap {
+  int n, cg, grp, unit;
+  bool live;
+};
+XCP_DEV RowMap row_map(int N, int ncg, int ngroups) {
+  RowMap m;
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  m.live = gw < N * ncg * ngroups;
+  m.grp = gw % ngroups;
+  m.unit = gw / ngroups;   // (frame, column group)
+  m.cg = m.unit % ncg;
+  m.n = m.unit / ncg;
+  return m;
+}
+
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void dw_fwd_row_kernel(DwArgs a) {
+  typedef RV<T> R;
+  typedef typename R::V V;
+  constexpr int EPT = R::EPT, CPG = 16 * EPT;
+  const int ncg = (a.W + RCOLS - 1) / RCOLS;
+  const RowMap mp = row_map(a.N, ncg, a.ngroups);
+  if (!mp.live) return;
+  const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
+  const int c = mp.grp * CPG + cl * EPT;
+  const bool cok = c < a.C;
+  const int cc = cok ? c : a.C - EPT;
+  const int x0 = mp.cg * RCOLS + sg * RS;
+  V wt[9], sc = V(1.f), sh = V(0.f);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wt[t] = R::load(a.Wt + (long)t * a.C + cc);
+  if constexpr (ACT == ACT_BNRELU) {
+    sc = R::load(a.scale + cc);
+    sh = R::load(a.shift + cc);
+  }
+  int off[RS + 2];
+  unsigned okm = 0;
+#pragma unroll
+  for (int k = 0; k < RS + 2; ++k) {
+    const int col = x0 - 1 + k;
+    off[k] = min(max(col, 0), a.W - 1) * a.C + cc;
+    okm |= (cok && col >= 0 && col < a.W) ? (1u << k) : 0u;
+  }
+  const T* X = reinterpret_cast<const T*>(a.X) + (long)mp.n * a.H * a.W * a.C;
+  T* Y = reinterpret_cast<T*>(a.Y) + (long)mp.n * a.H * a.W * a.C;
+  const int rstride = a.W * a.C;
+  // raw rows in flight: row r lives in slot r % 3 (3-row prefetch ring)
+  unsigned pf[3][RS + 2];
+  auto load = [&](int h, unsigned (&d)[RS + 2]) {
+    const T* row = X + h * rstride;
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) d[k] = *reinterpret_cast<const unsigned*>(row + off[k]);
+  };
+  // raw row -> activated, zero-padded values
+  auto cvt = [&](const unsigned (&r)[RS + 2], V (&o)[RS + 2], bool rowok) {
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) {
+      V v = R::unpack(r[k]);
+      if constexpr (ACT == ACT_BNRELU) v = vmax0(vfma(v, sc, sh));
+      else if constexpr (ACT == ACT_RELU) v = vmax0(v);
+      o[k] = (rowok && ((okm >> k) & 1)) ? v : V(0.f);
+    }
+  };
+  // step h: window rows (h-1, h, h+1) = (ra, rb, rc); rc is filled from slot s1 (row
+  // h+1), which is then refilled with row h+4
+  auto step = [&](int h, const V (&ra)[RS + 2], const V (&rb)[RS + 2], V (&rc)[RS + 2], unsigned (&s1)[RS + 2]) {
+    cvt(s1, rc, h + 1 < a.H);
+    if (h + 4 < a.H) load(h + 4, s1);
+    T* yrow = Y + h * rstride + c;
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      V o = V(0.f);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        o = vfma(ra[j + kx], wt[kx], o);
+        o = vfma(rb[j + kx], wt[3 + kx], o);
+        o = vfma(rc[j + kx], wt[6 + kx], o);
+      }
+      if (cok && x0 + j < a.W) *reinterpret_cast<unsigned*>(yrow + (x0 + j) * a.C) = R::pack(o);
+    }
+  };
+  V w0[RS + 2], w1[RS + 2], w2[RS + 2];
+#pragma unroll
+  for (int k = 0; k < RS + 2; ++k) w0[k] = V(0.f);
+  load(0, pf[0]);
+  if (a.H > 1) load(1, pf[1]);
+  if (a.H > 2) load(2, pf[2]);
+  if (a.H > 3) {
+    cvt(pf[0], w1, true);
+    load(3, pf[0]);
+  } else {
+    cvt(pf[0], w1, true);
+  }
+  for (int h = 0; h < a.H; h += 3) {
+    step(h, w0, w1, w2, pf[1]);
+    if (h + 1 < a.H) step(h + 1, w1, w2, w0, pf[2]);
+    if (h + 2 < a.H) step(h + 2, w2, w0, w1, pf[0]);
+  }
+}
+
+template <typename T, int ACT>
+__global__ __launch_bounds__(256, 2) void dw_bwd_row_kernel(DwBwdArgs a) {
+  typedef RV<T> R;
+  typedef typename R::V V;
+  constexpr int EPT = R::EPT, CPG = 16 * EPT;
+  const int ncg = (a.W + RCOLS - 1) / RCOLS;
+  const RowMap mp = row_map(a.N, ncg, a.ngroups);
+  if (!mp.live) return;
+  const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
+  const int c = mp.grp * CPG + cl * EPT;
+  const bool cok = c < a.C;
+  const int cc = cok ? c : a.C - EPT;
+  const int x0 = mp.cg * RCOLS + sg * RS;
+  const bool bnsum = a.bnpart != nullptr;
+  V wt[9], dw[9], sc = V(1.f), sh = V(0.f), bs1 = V(0.f), bs2 = V(0.f), mu = V(0.f), is = V(0.f);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wt[t] = R::load(a.Wt + (long)t * a.C + cc);
+    dw[t] = V(0.f);
+  }
+  if constexpr (ACT == ACT_BNRELU) {
+    sc = R::load(a.scale + cc);
+    sh = R::load(a.shift + cc);
+  }
+  if (bnsum) {
+    mu = R::load(a.bmean + cc);
+    is = R::load(a.binvstd + cc);
+  }
+  int off[RS + 2];
+  unsigned okm = 0;
+#pragma unroll
+  for (int k = 0; k < RS + 2; ++k) {
+    const int col = x0 - 1 + k;
+    off[k] = min(max(col, 0), a.W - 1) * a.C + cc;
+    okm |= (cok && col >= 0 && col < a.W) ? (1u << k) : 0u;
+  }
+  const long fbase = (long)mp.n * a.H * a.W * a.C;
+  const int rstride = a.W * a.C;
+  const T* X = reinterpret_cast<const T*>(a.X) + fbase;
+  const T* G = reinterpret_cast<const T*>(a.dY) + fbase;
+  const T* dRes = a.dRes ? reinterpret_cast<const T*>(a.dRes) + fbase : nullptr;
+  const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
+  T* dX = reinterpret_cast<T*>(a.dX) + fbase;
+  // raw rows in flight, row r in slot r % 3 of each ring (X: rows h..h+2, dY: h+1..h+3)
+  unsigned px[3][RS + 2], pg[3][RS + 2];
+  auto load = [&](const T* src, int h, unsigned (&d)[RS + 2]) {
+    const T* row = src + h * rstride;
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) d[k] = *reinterpret_cast<const unsigned*>(row + off[k]);
+  };
+  auto cvtg = [&](const unsigned (&r)[RS + 2], V (&gy)[RS + 2], bool rowok) {
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) gy[k] = (rowok && ((okm >> k) & 1)) ? R::unpack(r[k]) : V(0.f);
+  };
+  auto step = [&](int h, const V (&g0)[RS + 2], const V (&g1)[RS + 2], V (&g2)[RS + 2], unsigned (&sx)[RS + 2],
+                  unsigned (&sg)[RS + 2]) {
+    // activated X row h (zero padded), raw centre values kept for the BN sums
+    V xa[RS + 2];
+    unsigned xr[RS];
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) {
+      V v = R::unpack(sx[k]);
+      if constexpr (ACT == ACT_BNRELU) v = vmax0(vfma(v, sc, sh));
+      else if constexpr (ACT == ACT_RELU) v = vmax0(v);
+      xa[k] = ((okm >> k) & 1) ? v : V(0.f);
+      if (k >= 1 && k <= RS) xr[k - 1] = sx[k];
+    }
+    if (h + 3 < a.H) load(X, h + 3, sx);
+    cvtg(sg, g2, h + 1 < a.H);
+    if (h + 4 < a.H) load(G, h + 4, sg);
+    const int ro = h * rstride;
+    unsigned pres[RS], pskp[RS];
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      const int ow = min(x0 + j, a.W - 1);
+      pres[j] = dRes ? *reinterpret_cast<const unsigned*>(dRes + ro + ow * a.C + cc) : 0u;
+      pskp[j] = 0u;
+    }
+    const bool skip_row = dSkip && (h % a.sS) == 0 && h / a.sS < a.sOH;
+    if (skip_row) {
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const int ow = x0 + j;
+        if (ow % a.sS == 0 && ow / a.sS < a.sOW && ow < a.W)
+          pskp[j] = *reinterpret_cast<const unsigned*>(
+              dSkip + (((long)mp.n * a.sOH + h / a.sS) * a.sOW + ow / a.sS) * a.C + cc);
+      }
+    }
+    T* xrow = dX + ro + c;
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      // dA = transposed 3x3 over dY; window column k <-> tile column x0 + k - 1
+      V s = V(0.f);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        s = vfma(g2[j + 2 - kx], wt[kx], s);
+        s = vfma(g1[j + 2 - kx], wt[3 + kx], s);
+        s = vfma(g0[j + 2 - kx], wt[6 + kx], s);
+      }
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        dw[kx] = vfma(g2[j + 1], xa[j + kx], dw[kx]);
+        dw[3 + kx] = vfma(g1[j + 1], xa[j + kx], dw[3 + kx]);
+        dw[6 + kx] = vfma(g0[j + 1], xa[j + kx], dw[6 + kx]);
+      }
+      if constexpr (ACT != ACT_NONE) {
+        const V ctr = xa[j + 1];
+        if constexpr (EPT == 2) {
+          s[0] = ctr[0] > 0.f ? s[0] : 0.f;
+          s[1] = ctr[1] > 0.f ? s[1] : 0.f;
+        } else {
+          s = ctr > 0.f ? s : 0.f;
+        }
+      }
+      const bool valid = cok && x0 + j < a.W;
+      if (bnsum) {
+        const V dz = valid ? R::unpack(R::pack(s)) : V(0.f);   // the stored (rounded) dz
+        bs1 += dz;
+        bs2 = vfma(dz, (R::unpack(xr[j]) - mu) * is, bs2);
+      }
+      if (dRes) s += R::unpack(pres[j]);
+      if (skip_row) s += R::unpack(pskp[j]);
+      if (valid) *reinterpret_cast<unsigned*>(xrow + (x0 + j) * a.C) = R::pack(s);
+    }
+  };
+  V g0[RS + 2], g1[RS + 2], g2[RS + 2];
+#pragma unroll
+  for (int k = 0; k < RS + 2; ++k) g0[k] = V(0.f);
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+    if (r < a.H) {
+      load(X, r, px[r]);
+      load(G, r, pg[r]);
+    }
+  cvtg(pg[0], g1, true);
+  if (a.H > 3) load(G, 3, pg[0]);
+  for (int h = 0; h < a.H; h += 3) {
+    step(h, g0, g1, g2, px[0], pg[1]);
+    if (h + 1 < a.H) step(h + 1, g1, g2, g0, px[1], pg[2]);
+    if (h + 2 < a.H) step(h + 2, g2, g0, g1, px[2], pg[0]);
+  }
+  // reduce the 4 lane segments (lanes cl, cl+16, cl+32, cl+48) and write the partials
+  float red[EPT][11];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) red[e][t] = R::get(dw[t], e);
+    red[e][9] = R::get(bs1, e);
+    red[e][10] = R::get(bs2, e);
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+      red[e][q] += __shfl_xor(red[e][q], 16, 64);
+      red[e][q] += __shfl_xor(red[e][q], 32, 64);
+    }
+  }
+  if (sg == 0 && cok) {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) a.dWpart[((long)mp.unit * a.C + c + e) * 9 + t] = red[e][t];
+      if (bnsum) {
+        a.bnpart[((long)mp.unit * 2 + 0) * a.C + c + e] = red[e][9];
+        a.bnpart[((long)mp.unit * 2 + 1) * a.C + c + e] = red[e][10];
+      }
+    }
+  }
+}
+
+// xcp_tune knobs 4 / 5: forward / backward kernel family (0 = row walk, 1 = LDS tile).
+// Measured at 256 x 19 x 19 x 728 bf16: forward tile 65 us vs row 71 us; backward
+// (+BN sums) tile 205 us vs row 159-174 us.
+int g_dw_fwd_kernel = 1, g_dw_bwd_kernel = 0;
+
+template <typename T>
+int launch_fwd_row(int act, const DwArgs& a, hipStream_t st) {
+  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
+  const int blocks = (int)((waves + 3) / 4);
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_row_kernel<T, ACT_NONE>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_row_kernel<T, ACT_RELU>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_fwd_row_kernel<T, ACT_BNRELU>), dim3(blocks), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+int launch_bwd_row(int act, const DwBwdArgs& a, hipStream_t st) {
+  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
+  const int blocks = (int)((waves + 3) / 4);
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_row_kernel<T, ACT_NONE>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_row_kernel<T, ACT_RELU>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_bwd_row_kernel<T, ACT_BNRELU>), dim3(blocks), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 int xcp_internal_gemm_tune(int cfg);   // gemm.hip
@@ -430,6 +769,12 @@ extern "C" {
 int xcp_tune(int knob, int value) {
   if (knob == 2) return xcp_internal_gemm_tune(value);
   if (knob == 3) return xcp_internal_gemm_var(value);
+  if (knob == 4 || knob == 5) {
+    int& k = knob == 4 ? g_dw_fwd_kernel : g_dw_bwd_kernel;
+    const int old = k;
+    if (value == 0 || value == 1) k = value;
+    return old;
+  }
   int* k = knob == 0 ? &g_fwd_maxpx : knob == 1 ? &g_bwd_maxpx : nullptr;
   if (!k) return -1;
   const int old = *k;
@@ -443,6 +788,11 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
   const int maxpx = g_fwd_maxpx;
   DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, maxpx)};
+  if (g_dw_fwd_kernel == 0) {
+    if (dtype == XCP_BF16) return launch_fwd_row<bf16>(act, a, stream);
+    if (dtype == XCP_F32) return launch_fwd_row<float>(act, a, stream);
+    return XCP_EUNSUPPORTED;
+  }
   if (dtype == XCP_BF16) return launch_fwd<bf16>(act, a, maxpx, stream);
   if (dtype == XCP_F32) return launch_fwd<float>(act, a, maxpx, stream);
   return XCP_EUNSUPPORTED;
@@ -451,6 +801,7 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
 // number of partial rows (spatial workgroups) of the backward's slabs
 int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
   (void)C;
+  if (g_dw_bwd_kernel == 0) return N * ((W + RCOLS - 1) / RCOLS);
   const TileGeo g = tile_geo(H, W, g_bwd_maxpx);
   return N * g.nth * g.ntw;
 }
@@ -469,6 +820,11 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
   a.N = N; a.H = H; a.W = W; a.C = C;
   a.ngroups = ngroups_for(C, dtype);
   a.g = tile_geo(H, W, maxpx);
+  if (g_dw_bwd_kernel == 0) {
+    if (dtype == XCP_BF16) return launch_bwd_row<bf16>(act, a, stream);
+    if (dtype == XCP_F32) return launch_bwd_row<float>(act, a, stream);
+    return XCP_EUNSUPPORTED;
+  }
   if (dtype == XCP_BF16) return launch_bwd<bf16>(act, a, maxpx, stream);
   if (dtype == XCP_F32) return launch_bwd<float>(act, a, maxpx, stream);
   return XCP_EUNSUPPORTED;

@@ -137,10 +137,20 @@ def test_gemm_tn(ops, gpu, dt, M, N, K):
     assert rel_err(out.view(N, K), ref) < (1e-5 if dt == torch.float32 else 1e-3)
 
 
+@pytest.fixture(params=[0, 1], ids=["row", "tile"])
+def dw_family(request, ops):
+    """Run a depthwise test under both kernel families (xcp_tune knobs 4 / 5)."""
+    of = ops._lib.call("xcp_tune", 4, request.param)
+    ob = ops._lib.call("xcp_tune", 5, request.param)
+    yield request.param
+    ops._lib.call("xcp_tune", 4, of)
+    ops._lib.call("xcp_tune", 5, ob)
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("act", [0, 1, 2])
 @pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9), (1, 64, 147), (2, 256, 74)])
-def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
+def test_dw_fwd_bwd(ops, gpu, dw_family, dt, act, N, C, H):
     W = H + 1
     g = torch.Generator(device=gpu).manual_seed(C + H + act)
     x = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
@@ -187,7 +197,7 @@ def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-def test_dw_bwd_residual_and_skip(ops, gpu, dt):
+def test_dw_bwd_residual_and_skip(ops, gpu, dw_family, dt):
     N, C, H, W = 2, 128, 15, 15
     x = torch.randn(N, C, H, W, device=gpu).to(dt)
     w = torch.randn(C, 1, 3, 3, device=gpu) / 3

@@ -59,6 +59,19 @@ def main():
 
     if not sel or "copy" in sel:
         rep("torch copy (ref BW)", timeit(lambda: Y.copy_(X)), 2 * tensor_bytes)
+    if "dwrow" in sel:
+        for kern in (0, 1):
+            oldk = ops._lib.call("xcp_tune", 4, kern)
+            oldb = ops._lib.call("xcp_tune", 5, kern)
+            for act in (1, 2):
+                rep(f"dw_fwd act={act} kernel={kern}", timeit(lambda: ops.dw_fwd(act, X, Y, Wt, sc, sh, N, H, W, C)),
+                    2 * tensor_bytes)
+            rep(f"dw_bwd act=2 +bnsums kernel={kern}",
+                timeit(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)), 3 * tensor_bytes)
+            rep(f"dw_bwd act=1 +res kernel={kern}",
+                timeit(lambda: ops.dw_bwd(1, D, X, Wt, sc, sh, Y, dW, N, H, W, C, dRes=D)), 4 * tensor_bytes)
+            ops._lib.call("xcp_tune", 4, oldk)
+            ops._lib.call("xcp_tune", 5, oldb)
     if not sel or "dw_fwd" in sel:
         for px in (512, 256):
             old = ops._lib.call("xcp_tune", 0, px)
