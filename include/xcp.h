@@ -49,6 +49,8 @@ int xcp_gemm_nt_stat_rows(int M);
 /* weight gradient of the above: P[s][N][K] = sum_{m in split s} G[m][N] X[m][K],
  * rows split in S chunks of rows_per_split; X rows gathered as in gemm_nt
  * (gmode 0-2).  Reduce P over s with xcp_colreduce_f32. */
+/* rows per split to pass to xcp_gemm_tn for this problem (S = ceil(M / rows)). */
+int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K);
 int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, float* P, int M, int N, int K, int S,
                 int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, xcp_stream_t stream);
 
@@ -67,7 +69,9 @@ int xcp_dw_bwd_chunks(int N, int H, int W, int C);
  * 3-stage, 2: auto -- 256x256 8-wave kernel for dense bf16 with >= 256 tiles and
  * K >= 384, 3: that kernel for every dense bf16 call); 3 = 256x256 kernel schedule
  * (0: staggered wave groups, 1: lockstep; measurement only); 4 / 5 = depthwise
- * forward / backward kernel family (0: row walk, 1: LDS tile).
+ * forward / backward kernel family (0: row walk, 1: LDS tile); 6 = weight-gradient
+ * kernel (1: 256x256 for dense bf16, 0: 128x128); 7 = target workgroups of the
+ * 256x256 weight-gradient kernel.
  * Returns the previous value (-1: unknown knob). */
 int xcp_tune(int knob, int value);
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,

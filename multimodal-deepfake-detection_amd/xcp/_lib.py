@@ -21,6 +21,7 @@ D = ctypes.c_double
 SIGNATURES = {
     "xcp_gemm_nt": [I, P, L, P, L, P, L, I, I, I, P, I, I, I, I, I, I, I, P],
     "xcp_gemm_nt_stat_rows": [I],
+    "xcp_gemm_tn_rows_per_split": [I, I, I, I, I],
     "xcp_gemm_tn": [I, P, L, P, L, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
@@ -49,7 +50,7 @@ SIGNATURES = {
 }
 
 # entry points that return a size, not a status
-SIZE_QUERIES = {"xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts", "xcp_tune"}
+SIZE_QUERIES = {"xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts", "xcp_tune"}
 
 _lib = None
 

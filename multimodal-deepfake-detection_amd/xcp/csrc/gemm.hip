@@ -549,6 +549,12 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   epilogue256(acc, smem, a, m0, n0, bm, tid);
 }
 
+int g_tn_cfg = 1;      // xcp_tune knob 6: 1 = 256x256 weight-gradient kernel for dense bf16, 0 = 128x128
+int g_tn_wgs = 256;    // xcp_tune knob 7: target workgroups (splits x tiles) of the 256x256 kernel
+bool tn_big(int dtype, int gmode, int N, int K) {
+  return g_tn_cfg == 1 && dtype == XCP_BF16 && gmode == 0 && N >= 128 && K >= 128;
+}
+
 int g_nt256_var = 0;   // xcp_tune knob 3: 0 = staggered wave groups, 1 = lockstep (measurement)
 
 // xcp_tune knob 2: 0 = 128x128 tile / 2-stage ring, 1 = 256x128 / 3-stage,
@@ -707,6 +713,154 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(TNArgs a) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------
+// 256x256 bf16 weight-gradient kernel: P[s][n][k] = sum_{m in split s} G[m][n] X[m][k].
+// Same machinery as gemm_nt256k64_kernel (8 waves 2x4, wave tile 128 n x 64 k, two
+// 64 KB ring slots filled by LDS-DMA, staggered wave groups, counted vmcnt), but the
+// reduction index m is the ROW index of both operands: slabs are staged [m][256 cols]
+// (512-B rows; 16-B chunk c of row m stored at c ^ ((m & 7) << 1), which makes the
+// transposed reads conflict-free) and fragments are read with ds_read_b64_tr_b16.
+// A K-tile is 64 m-rows = two 32-row MFMA steps; its four phases are
+//   Q0 (m 0-31,  n-top) reads G n-top + X all   issues G m0(t+1)
+//   Q1 (m 0-31,  n-bot) reads G n-bot           issues X m0(t+1)
+//   Q2 (m 32-63, n-top) reads G n-top + X all   issues G m1(t+1)
+//   Q3 (m 32-63, n-bot) reads G n-bot           issues X m1(t+1)
+// so each half-tile (32 m-rows of one operand) is issued 3-4 phases before its first
+// read and restaged >= 3 phases after its last one; Q3 retires the m0 half-tiles of
+// t+1 and Q1 the m1 half-tiles (vmcnt(4), one phase before the reads).
+constexpr int T_OP = 64 * 512;                 // one operand, one slot (32 KB)
+constexpr int T_SLOT = 2 * T_OP;
+
+XCP_DEV int tswz(int m, int col) {             // byte offset of bf16 column col of slab row m
+  return m * 512 + ((((col >> 3) ^ ((m & 7) << 1))) << 4) + (col & 7) * 2;
+}
+
+__global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * T_SLOT];
+  const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
+  const int tiles = gridN * gridK;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);   // one split's tiles share an XCD (its rows stay in L2)
+  const int sp = id / tiles, t = id % tiles;
+  const int n0 = (t / gridK) * 256, k0 = (t % gridK) * 256;
+  const int mbeg = sp * a.rows_per_split;
+  const int mend = min(a.M, mbeg + a.rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const bf16* G = reinterpret_cast<const bf16*>(a.G);
+  const bf16* X = reinterpret_cast<const bf16*>(a.X);
+
+  // staging: a half-tile is 32 m-rows x 512 B; wave w loads rows 4w + 2i + (lane >> 5)
+  // (i = 0, 1), lane writes physical chunk lane & 31 = logical chunk lc
+  const int pc = lane & 31;
+  int rr[2], lc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rr[i] = 4 * w + 2 * i + (lane >> 5);
+    lc[i] = pc ^ ((rr[i] & 7) << 1);
+  }
+  const void* zero = g_zero16;
+  asm volatile("" : "+v"(zero));
+  auto glds = [](const void* p, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  // half-tile h (0: G m0, 1: X m0, 2: G m1, 3: X m1) of K-tile kt
+  auto issue = [&](int h, int kt) {
+    const bool isG = (h & 1) == 0;
+    const int mh = (h >> 1) * 32;
+    char* d = smem + (kt & 1) * T_SLOT + (isG ? 0 : T_OP);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = mh + rr[i];
+      const int m = mbeg + kt * 64 + r;
+      const int col = (isG ? n0 : k0) + lc[i] * 8;
+      const bool ok = m < mend && col < (isG ? a.N : a.K);
+      const void* src = ok ? (isG ? (const void*)(G + (long)m * a.ldg + col) : (const void*)(X + (long)m * a.ldx + col))
+                           : zero;
+      glds(src, d + (mh + 4 * w + 2 * i) * 512);   // 1 KB = slab rows mh+4w+2i, +1
+    }
+  };
+
+  f32x4 acc[8][4];   // [n-frag][k-frag]: lane holds P[n = .. + fr][k = .. + 4*fg + r]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (mend - mbeg + 63) / 64;
+  if (nk > 0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) issue(h, 0);
+  }
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int q4 = fr >> 2, p4 = fr & 3;   // tr read: lane 4q+p reads slab row q, columns 4p..4p+3
+  // fragment of 16 columns at cb for MFMA step ms: k-slots of lane group fg are
+  // m rows ms*32 + {4fg..4fg+3} (elements 0-3) and ms*32 + 16 + {4fg..} (4-7)
+  auto frag = [&](const char* slab, int ms, int cb) {
+    const int m0r = ms * 32 + 4 * fg + q4;
+    const int col = cb + 4 * p4;
+    const bf16x4 lo = ds_read_tr(slab + tswz(m0r, col));
+    const bf16x4 hi = ds_read_tr(slab + tswz(m0r + 16, col));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  bf16x8 gf[4], xf[4];
+  auto sync_mfma = [&](int ih) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], gf[i], acc[ih * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* sg = smem + (kt & 1) * T_SLOT;
+    const char* sx = sg + T_OP;
+    const bool nxt = kt + 1 < nk;
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
+      // n-top
+#pragma unroll
+      for (int j = 0; j < 4; ++j) xf[j] = frag(sx, ms, wc * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gf[i] = frag(sg, ms, wr * 128 + i * 16);
+      if (nxt) issue(2 * ms, kt + 1);
+      sync_mfma(0);
+      // n-bot
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gf[i] = frag(sg, ms, wr * 128 + 64 + i * 16);
+      if (nxt) {
+        issue(2 * ms + 1, kt + 1);
+        wait_vmcnt<4>();   // ms 0: m1 half-tiles of kt (for Q2); ms 1: m0 half-tiles of kt+1
+      } else {
+        wait_vmcnt<0>();
+      }
+      sync_mfma(1);
+    }
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+
+  float* P = a.P + (long)sp * a.N * a.K;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = n0 + wr * 128 + i * 16 + fr;
+    if (n >= a.N) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wc * 64 + j * 16 + 4 * fg;
+      if (k < a.K) *reinterpret_cast<f32x4*>(P + (long)n * a.K + k) = acc[i][j];
+    }
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -755,6 +909,14 @@ int xcp_gemm_nt_stat_rows(int M) { return xcp_cdiv(M, g_nt_cfg == 1 ? 256 : 128)
 
 }  // extern "C"
 
+int xcp_internal_tn_tune(int knob, int v) {
+  int& k = knob == 6 ? g_tn_cfg : g_tn_wgs;
+  const int old = k;
+  if (knob == 6 && (v == 0 || v == 1)) k = v;
+  if (knob == 7 && v >= 8 && v <= 8192) k = v;
+  return old;
+}
+
 int xcp_internal_gemm_var(int v) {
   const int old = g_nt256_var;
   if (v == 0 || v == 1) g_nt256_var = v;
@@ -769,6 +931,24 @@ int xcp_internal_gemm_tune(int cfg) {
 
 extern "C" {
 
+// Rows per split for xcp_gemm_tn (S = ceil(M / rows)): about one workgroup per CU for
+// the 256x256 kernel (each split's partial slab costs 4*N*K bytes of writes and
+// reads), ~1024 workgroups of the 128x128 kernel otherwise.
+int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K) {
+  if (M <= 0) return 64;
+  const bool big = tn_big(dtype, gmode, N, K);
+  const int tile = big ? 256 : 128, align = big ? 64 : 32;
+  const int tiles = xcp_cdiv(N, tile) * xcp_cdiv(K, tile);
+  const int target = big ? g_tn_wgs : 1024, min_rows = big ? 512 : 256;
+  int S = target / (tiles > 0 ? tiles : 1);
+  S = S < 1 ? 1 : S;
+  const int smax = xcp_cdiv(M, min_rows);
+  S = S < smax ? S : smax;
+  int rps = xcp_cdiv(M, S);
+  rps = xcp_cdiv(rps, align) * align;
+  return rps;
+}
+
 // P[s][N][K] partial weight gradients; S splits of rows_per_split rows each.
 int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, float* P, int M, int N, int K, int S,
                 int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, hipStream_t stream) {
@@ -776,6 +956,10 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
   if ((K % 8) || (N % 8) || (ldg % 8) || (ldx % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 2 || (gmode == 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   TNArgs a{G, ldg, X, ldx, P, M, N, K, S, rows_per_split, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
+  if (tn_big(dtype, gmode, N, K)) {
+    hipLaunchKernelGGL(gemm_tn256_kernel, dim3(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S), dim3(512), 0, stream, a);
+    return (int)hipGetLastError();
+  }
   const int grid = xcp_cdiv(N, 128) * xcp_cdiv(K, 128) * S;
 #define XCP_TN_LAUNCH(TT)                                                                                      \
   switch (gmode) {                                                                                             \

@@ -114,18 +114,10 @@ def reduce_slabs(P, S, L, out):
         colreduce_f32(P, S, L, out, 1)
 
 
-def tn_splits(M, N, K, target=1024, min_rows=256):
-    tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    S = max(1, min(target // max(1, tiles), (M + min_rows - 1) // min_rows))
-    rps = (M + S - 1) // S
-    rps = ((rps + 31) // 32) * 32
-    S = (M + rps - 1) // rps
-    return S, rps
-
-
 def weight_grad(G, X, M, N, K, out, gather=(0, 0, 0, 0, 0, 1, 0), ldg=None, ldx=None):
     """out[N][K] (fp32) = G[M][N]^T X[M][K]."""
-    S, rps = tn_splits(M, N, K)
+    rps = _lib.call("xcp_gemm_tn_rows_per_split", DT[G.dtype], gather[0], M, N, K)
+    S = (M + rps - 1) // rps
     P = torch.empty(S * N * K, device=G.device, dtype=torch.float32)
     gemm_tn(G, X, P, M, N, K, S, rps, ldg=ldg, ldx=ldx, gather=gather)
     reduce_slabs(P, S, N * K, out)

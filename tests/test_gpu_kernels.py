@@ -126,13 +126,20 @@ def test_gemm_im2col_conv2_fwd_and_dgrad(ops, gpu, dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("M,N,K", [(5000, 128, 64), (92416 // 16, 728, 728), (300, 2048, 1536), (33, 512, 2048)])
-def test_gemm_tn(ops, gpu, dt, M, N, K):
+@pytest.mark.parametrize("M,N,K", [(5000, 128, 64), (92416 // 16, 728, 728), (300, 2048, 1536), (33, 512, 2048),
+                                   (1000, 264, 136), (7777, 1024, 728)])
+@pytest.mark.parametrize("tn", [1, 0], ids=["tn256", "tn128"])
+def test_gemm_tn(ops, gpu, dt, M, N, K, tn):
+    old = ops._lib.call("xcp_tune", 6, tn)
     g = torch.Generator(device=gpu).manual_seed(M)
     G = torch.randn(M, N, device=gpu, generator=g).to(dt)
     X = torch.randn(M, K, device=gpu, generator=g).to(dt)
     out = torch.empty(N * K, device=gpu)
-    ops.weight_grad(G, X, M, N, K, out)
+    try:
+        ops.weight_grad(G, X, M, N, K, out)
+        torch.cuda.synchronize()
+    finally:
+        ops._lib.call("xcp_tune", 6, old)
     ref = G.float().t() @ X.float()
     assert rel_err(out.view(N, K), ref) < (1e-5 if dt == torch.float32 else 1e-3)
 

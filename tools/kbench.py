@@ -95,7 +95,18 @@ def main():
                 flops=2.0 * M * C * C)
             ops._lib.call("xcp_tune", 2, old)
         out = torch.empty(C * C, device=dev)
-        rep("weight_grad 728x728", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)), flops=2.0 * M * C * C)
+        for tn in (1, 0):
+            old = ops._lib.call("xcp_tune", 6, tn)
+            rep(f"weight_grad 728x728 tn={tn}", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)),
+                flops=2.0 * M * C * C)
+            ops._lib.call("xcp_tune", 6, old)
+    if "tnwgs" in sel:
+        out = torch.empty(C * C, device=dev)
+        for wgs in (128, 256, 384, 512, 768):
+            old = ops._lib.call("xcp_tune", 7, wgs)
+            rep(f"weight_grad 728x728 wgs={wgs}", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)),
+                flops=2.0 * M * C * C)
+            ops._lib.call("xcp_tune", 7, old)
     if "gemmv" in sel:
         for var in [int(v) for v in os.environ.get('XCP_VARS', '0,1').split(',')]:
             old = ops._lib.call("xcp_tune", 3, var)
