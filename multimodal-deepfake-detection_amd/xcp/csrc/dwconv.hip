@@ -731,10 +731,11 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_row_kernel(DwBwdArgs a) {
   }
 }
 
-// xcp_tune knobs 4 / 5: forward / backward kernel family (0 = row walk, 1 = LDS tile).
-// Measured at 256 x 19 x 19 x 728 bf16: forward tile 65 us vs row 71 us; backward
-// (+BN sums) tile 205 us vs row 159-174 us.
-int g_dw_fwd_kernel = 1, g_dw_bwd_kernel = 0;
+// xcp_tune knobs 4 / 5: forward / backward kernel family (0 = row walk, 1 = LDS tile,
+// 2 = LDS-staged row walk).  Measured at 256 x 19 x 19 x 728 bf16: forward tile 61-65 us,
+// row 70-72, LDS row 72-79; backward (+BN sums) tile 199-207 us, row 159-174, LDS row
+// 145.  The row walks are VALU-bound (~34 VALU lane-ops per element in the backward).
+int g_dw_fwd_kernel = 1, g_dw_bwd_kernel = 2;
 
 template <typename T>
 int launch_fwd_row(int act, const DwArgs& a, hipStream_t st) {
@@ -756,6 +757,378 @@ int launch_bwd_row(int act, const DwBwdArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+
+// =================================================================================
+// LDS-staged row-walk kernels (default).  Same wave decomposition as the row-walk
+// kernels above (one wave = one 64-B channel slice of one frame over 20 output
+// columns, walking all H rows, lane (cl, s) owning one channel dword of output
+// columns 5s..5s+4), but every HBM access is 16 B per lane: each input row of the
+// wave (22 pixels x 64 B, 1408 B) is brought into a per-wave LDS ring by LDS-DMA
+// (global_load_lds, out-of-range pixels and rows from a zero line), lanes read their
+// 7-column windows from LDS, and each output row is staged in LDS and written with
+// 16-B stores.  The measured limit of the register-load variant was the texture
+// address path (one VMEM lane-op per 2 channels); here it is one per 8.
+// Waves are independent (no barriers).  Every step issues the same number of VMEM
+// instructions (masked lanes read the zero line / write a sink), so the per-wave
+// vmcnt counts are static; VMEM operations retire in issue order.
+constexpr int LROW = (RCOLS + 2) * SLICE;   // 1408 B: one staged row of one tensor
+__device__ __attribute__((aligned(64))) uint4 g_dzero[4];
+__device__ __attribute__((aligned(64))) uint4 g_dsink[64];
+
+// s_waitcnt vmcnt(N) as a real S_WAITCNT (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] |
+// lgkmcnt[11:8] | vmcnt_hi[15:14]), so the compiler's own wait insertion sees it
+template <int N>
+XCP_DEV void vmwait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
+}
+
+// Stage pixels x0w-1 .. x0w+20 (64-B slice at channel c0) of row h of a frame into
+// dst (LDS, 1408 B) with two LDS-DMA instructions (88 lanes of 16 B).
+template <typename T>
+XCP_DEV void stage_row(const T* frame, int h, int H, int W, int C, int x0w, int c0, char* dst, int lane) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ch = i * 64 + lane;            // chunk: pixel ch >> 2, 16-B part ch & 3
+    const int col = x0w - 1 + (ch >> 2);
+    const int c = c0 + (ch & 3) * EPC;
+    const bool ok = h < H && col >= 0 && col < W && c < C;
+    const void* src = ok ? (const void*)(frame + ((long)h * W + col) * C + c) : (const void*)g_dzero;
+    if (i == 0 || lane < 24)
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                       (void __attribute__((address_space(3)))*)(dst + i * 1024), 16, 0, 0);
+  }
+}
+
+// Write the staged output row (20 pixels x 64 B in `stg`) to row h: two 16-B stores
+// per lane-slot; lanes without a valid pixel write the sink.
+template <typename T>
+XCP_DEV void store_row(T* frame, int h, int W, int C, int x0w, int c0, const char* stg, int lane) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ch = i * 64 + lane;
+    const int p = ch >> 2, col = x0w + p;
+    const int c = c0 + (ch & 3) * EPC;
+    const bool ok = p < RCOLS && col < W && c < C;
+    const uint4 v = *reinterpret_cast<const uint4*>(stg + min(ch, 4 * RCOLS - 1) * 16);
+    uint4* dstp = ok ? reinterpret_cast<uint4*>(frame + ((long)h * W + col) * C + c) : g_dsink + lane;
+    *dstp = v;
+  }
+}
+
+// Prefetch depth (rows in flight per staged tensor): each step waits only for the
+// loads issued D steps earlier (measured: one row of look-ahead leaves the walk
+// latency-bound, ~2.4 us per row step).
+constexpr int FD = 3, BD = 2;
+
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void dw_fwd_lds_kernel(DwArgs a) {
+  typedef RV<T> R;
+  typedef typename R::V V;
+  constexpr int EPT = R::EPT, CPG = 16 * EPT, NS = FD + 1;
+  __shared__ __attribute__((aligned(16))) char sm[4][NS * LROW];     // per wave: LDS-DMA row ring
+  __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];  // per wave: output staging
+  // (a separate object: the compiler then knows staging reads never alias in-flight DMA)
+  const int ncg = (a.W + RCOLS - 1) / RCOLS;
+  const RowMap mp = row_map(a.N, ncg, a.ngroups);
+  if (!mp.live) return;
+  const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
+  char* ring = sm[threadIdx.x >> 6];
+  char* stg = so[threadIdx.x >> 6];
+  const int c0 = mp.grp * CPG;
+  const int c = c0 + cl * EPT;
+  const bool cok = c < a.C;
+  const int cc = cok ? c : a.C - EPT;
+  const int x0w = mp.cg * RCOLS, x0 = x0w + sg * RS;
+  V wt[9], sc = V(1.f), sh = V(0.f);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wt[t] = R::load(a.Wt + (long)t * a.C + cc);
+  if constexpr (ACT == ACT_BNRELU) {
+    sc = R::load(a.scale + cc);
+    sh = R::load(a.shift + cc);
+  }
+  unsigned okm = 0;
+#pragma unroll
+  for (int k = 0; k < RS + 2; ++k) {
+    const int col = x0 - 1 + k;
+    okm |= (col >= 0 && col < a.W) ? (1u << k) : 0u;
+  }
+  const T* X = reinterpret_cast<const T*>(a.X) + (long)mp.n * a.H * a.W * a.C;
+  T* Y = reinterpret_cast<T*>(a.Y) + (long)mp.n * a.H * a.W * a.C;
+  const int lofs = sg * RS * SLICE + cl * 4;   // this lane's window column 0 in a staged row
+  auto slot = [&](int r) { return ring + (r % NS) * LROW; };   // row r lives in slot r % NS
+  auto cvt = [&](const char* row, V (&o)[RS + 2], bool rowok) {
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) {
+      V v = R::unpack(*reinterpret_cast<const unsigned*>(row + lofs + k * SLICE));
+      if constexpr (ACT == ACT_BNRELU) {
+        v = vmax0(vfma(v, sc, sh));
+        v = (rowok && ((okm >> k) & 1)) ? v : V(0.f);   // padding is zero after the activation
+      } else if constexpr (ACT == ACT_RELU) {
+        v = vmax0(v);
+      }
+      o[k] = v;
+    }
+  };
+  // VMEM per step h: 2 loads (row h+1+FD) + 2 stores (row h).  Row h+1 was issued at
+  // step h-FD; issued after it: 2 stores + (FD-1) x (2 loads + 2 stores).
+  auto step = [&](int h, const V (&ra)[RS + 2], const V (&rb)[RS + 2], V (&rc)[RS + 2]) {
+    vmwait<2 + 4 * (FD - 1)>();
+    cvt(slot(h + 1), rc, h + 1 < a.H);
+    stage_row<T>(X, h + 1 + FD, a.H, a.W, a.C, x0w, c0, slot(h + 1 + FD), lane);   // slot of row h (consumed)
+    V o[RS];
+#pragma unroll
+    for (int j = 0; j < RS; ++j) o[j] = V(0.f);
+    // independent accumulation chains (consecutive packed FMAs never depend on each other)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int j = 0; j < RS; ++j) o[j] = vfma((ky == 0 ? ra : ky == 1 ? rb : rc)[j + kx], wt[ky * 3 + kx], o[j]);
+#pragma unroll
+    for (int j = 0; j < RS; ++j) *reinterpret_cast<unsigned*>(stg + (sg * RS + j) * SLICE + cl * 4) = R::pack(o[j]);
+    store_row<T>(Y, h, a.W, a.C, x0w, c0, stg, lane);
+  };
+  V w0[RS + 2], w1[RS + 2], w2[RS + 2];
+#pragma unroll
+  for (int k = 0; k < RS + 2; ++k) w0[k] = V(0.f);
+#pragma unroll
+  for (int r = 0; r <= FD; ++r) stage_row<T>(X, r, a.H, a.W, a.C, x0w, c0, slot(r), lane);
+  vmwait<0>();
+  cvt(slot(0), w1, true);
+  for (int h = 0; h < a.H; h += 3) {
+    step(h, w0, w1, w2);
+    if (h + 1 < a.H) step(h + 1, w1, w2, w0);
+    if (h + 2 < a.H) step(h + 2, w2, w0, w1);
+  }
+}
+
+template <typename T, int ACT, bool RES>
+__global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
+  typedef RV<T> R;
+  typedef typename R::V V;
+  constexpr int EPT = R::EPT, CPG = 16 * EPT;
+  constexpr int NT_ = RES ? 3 : 2;                       // staged tensors: X, dY (, dRes)
+  constexpr int NS = BD + 1;
+  __shared__ __attribute__((aligned(16))) char sm[4][NS * NT_ * LROW];
+  __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];   // output staging (separate object)
+  const int ncg = (a.W + RCOLS - 1) / RCOLS;
+  const RowMap mp = row_map(a.N, ncg, a.ngroups);
+  if (!mp.live) return;
+  const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
+  char* ring = sm[threadIdx.x >> 6];
+  char* rx = ring;                  // X rows, slot r % NS
+  char* rg = ring + NS * LROW;      // dY rows, slot r % NS
+  char* rres = ring + 2 * NS * LROW;   // dRes rows (RES)
+  char* stg = so[threadIdx.x >> 6];
+  const int c0 = mp.grp * CPG;
+  const int c = c0 + cl * EPT;
+  const bool cok = c < a.C;
+  const int cc = cok ? c : a.C - EPT;
+  const int x0w = mp.cg * RCOLS, x0 = x0w + sg * RS;
+  const bool bnsum = a.bnpart != nullptr;
+  V wt[9], dw[9], sc = V(1.f), sh = V(0.f), bs1 = V(0.f), bs2 = V(0.f), mu = V(0.f), is = V(0.f);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wt[t] = R::load(a.Wt + (long)t * a.C + cc);
+    dw[t] = V(0.f);
+  }
+  if constexpr (ACT == ACT_BNRELU) {
+    sc = R::load(a.scale + cc);
+    sh = R::load(a.shift + cc);
+  }
+  if (bnsum) {
+    mu = R::load(a.bmean + cc);
+    is = R::load(a.binvstd + cc);
+  }
+  unsigned okm = 0;
+#pragma unroll
+  for (int k = 0; k < RS + 2; ++k) {
+    const int col = x0 - 1 + k;
+    okm |= (col >= 0 && col < a.W) ? (1u << k) : 0u;
+  }
+  const long fbase = (long)mp.n * a.H * a.W * a.C;
+  const T* X = reinterpret_cast<const T*>(a.X) + fbase;
+  const T* G = reinterpret_cast<const T*>(a.dY) + fbase;
+  const T* dRes = RES ? reinterpret_cast<const T*>(a.dRes) + fbase : nullptr;
+  const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
+  T* dX = reinterpret_cast<T*>(a.dX) + fbase;
+  const int lofs = sg * RS * SLICE + cl * 4;
+  auto rd = [&](const char* row, int k) { return *reinterpret_cast<const unsigned*>(row + lofs + k * SLICE); };
+  auto cvtg = [&](const char* row, V (&gy)[RS + 2]) {
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) gy[k] = R::unpack(rd(row, k));   // staged zero padding
+  };
+  auto sx = [&](int r) { return rx + (r % NS) * LROW; };
+  auto sgs = [&](int r) { return rg + (r % NS) * LROW; };
+  auto sr = [&](int r) { return rres + (r % NS) * LROW; };
+  // VMEM per step h: loads X h+BD, dY h+1+BD (, dRes h+BD) = L, then 2 stores of row h.
+  // At step h the rows issued at step h-BD+1 ... are not needed yet; the step-h rows
+  // (X h, dY h+1, dRes h) were issued at step h-BD: issued after them are 2 stores
+  // + (BD-1) x (L + 2).
+  constexpr int L = RES ? 6 : 4;
+  auto step = [&](int h, const V (&g0)[RS + 2], const V (&g1)[RS + 2], V (&g2)[RS + 2]) {
+    char* sxh = sx(h);
+    char* sgn = sgs(h + 1);
+    char* srh = sr(h);
+    vmwait<2 + (BD - 1) * (L + 2)>();
+    // strided-skip gradient terms of this row: plain loads issued before this step's
+    // LDS-DMA, so waiting for them never waits for the prefetch
+    const bool skip_row = dSkip && (h % a.sS) == 0 && h / a.sS < a.sOH;
+    unsigned pskp[RS];
+#pragma unroll
+    for (int j = 0; j < RS; ++j) pskp[j] = 0u;
+    if (skip_row) {
+#pragma unroll
+      for (int j = 0; j < RS; ++j) {
+        const int ow = x0 + j;
+        if (cok && ow % a.sS == 0 && ow / a.sS < a.sOW && ow < a.W)
+          pskp[j] = *reinterpret_cast<const unsigned*>(
+              dSkip + (((long)mp.n * a.sOH + h / a.sS) * a.sOW + ow / a.sS) * a.C + c);
+      }
+    }
+    // activated X row h (slot sxh; zero padded after the activation), raw centre values
+    V xa[RS + 2];
+    unsigned xr[RS];
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) {
+      const unsigned u = rd(sxh, k);
+      V v = R::unpack(u);
+      if constexpr (ACT == ACT_BNRELU) {
+        v = vmax0(vfma(v, sc, sh));
+        v = ((okm >> k) & 1) ? v : V(0.f);
+      } else if constexpr (ACT == ACT_RELU) {
+        v = vmax0(v);
+      }
+      xa[k] = v;
+      if (k >= 1 && k <= RS) xr[k - 1] = u;
+    }
+    cvtg(sgn, g2);   // dY row h+1
+    unsigned pres[RS];
+    if constexpr (RES) {
+#pragma unroll
+      for (int j = 0; j < RS; ++j) pres[j] = rd(srh, j + 1);
+    }
+    stage_row<T>(X, h + BD, a.H, a.W, a.C, x0w, c0, sx(h + BD), lane);          // slot of X row h-1
+    stage_row<T>(G, h + 1 + BD, a.H, a.W, a.C, x0w, c0, sgs(h + 1 + BD), lane);   // slot of dY row h
+    if constexpr (RES) stage_row<T>(dRes, h + BD, a.H, a.W, a.C, x0w, c0, sr(h + BD), lane);
+    // independent accumulation chains: consecutive packed FMAs never depend on each other
+    V sj[RS];
+#pragma unroll
+    for (int j = 0; j < RS; ++j) sj[j] = V(0.f);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int j = 0; j < RS; ++j)
+          sj[j] = vfma((ky == 0 ? g2 : ky == 1 ? g1 : g0)[j + 2 - kx], wt[ky * 3 + kx], sj[j]);
+#pragma unroll
+    for (int j = 0; j < RS; ++j)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        dw[kx] = vfma(g2[j + 1], xa[j + kx], dw[kx]);
+        dw[3 + kx] = vfma(g1[j + 1], xa[j + kx], dw[3 + kx]);
+        dw[6 + kx] = vfma(g0[j + 1], xa[j + kx], dw[6 + kx]);
+      }
+#pragma unroll
+    for (int j = 0; j < RS; ++j) {
+      V s = sj[j];
+      if constexpr (ACT != ACT_NONE) {
+        const V ctr = xa[j + 1];
+        if constexpr (EPT == 2) {
+          s[0] = ctr[0] > 0.f ? s[0] : 0.f;
+          s[1] = ctr[1] > 0.f ? s[1] : 0.f;
+        } else {
+          s = ctr > 0.f ? s : 0.f;
+        }
+      }
+      if (bnsum) {
+        const bool valid = cok && x0 + j < a.W;
+        const V dz = valid ? R::unpack(R::pack(s)) : V(0.f);   // the stored (rounded) dz
+        bs1 += dz;
+        bs2 = vfma(dz, (R::unpack(xr[j]) - mu) * is, bs2);
+      }
+      if constexpr (RES) s += R::unpack(pres[j]);
+      if (skip_row) s += R::unpack(pskp[j]);
+      *reinterpret_cast<unsigned*>(stg + (sg * RS + j) * SLICE + cl * 4) = R::pack(s);
+    }
+    store_row<T>(dX, h, a.W, a.C, x0w, c0, stg, lane);
+  };
+  V g0[RS + 2], g1[RS + 2], g2[RS + 2];
+#pragma unroll
+  for (int k = 0; k < RS + 2; ++k) g0[k] = V(0.f);
+  // prologue: X rows 0 .. BD-1, dY rows 0 .. BD, dRes rows 0 .. BD-1
+#pragma unroll
+  for (int r = 0; r <= BD; ++r) {
+    if (r < BD) stage_row<T>(X, r, a.H, a.W, a.C, x0w, c0, sx(r), lane);
+    stage_row<T>(G, r, a.H, a.W, a.C, x0w, c0, sgs(r), lane);
+    if constexpr (RES)
+      if (r < BD) stage_row<T>(dRes, r, a.H, a.W, a.C, x0w, c0, sr(r), lane);
+  }
+  vmwait<0>();
+  cvtg(sgs(0), g1);
+  for (int h = 0; h < a.H; h += 3) {
+    step(h, g0, g1, g2);
+    if (h + 1 < a.H) step(h + 1, g1, g2, g0);
+    if (h + 2 < a.H) step(h + 2, g2, g0, g1);
+  }
+  // reduce the 4 lane segments (lanes cl, cl+16, cl+32, cl+48) and write the partials
+  float red[EPT][11];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) red[e][t] = R::get(dw[t], e);
+    red[e][9] = R::get(bs1, e);
+    red[e][10] = R::get(bs2, e);
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+      red[e][q] += __shfl_xor(red[e][q], 16, 64);
+      red[e][q] += __shfl_xor(red[e][q], 32, 64);
+    }
+  }
+  if (sg == 0 && cok) {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) a.dWpart[((long)mp.unit * a.C + c + e) * 9 + t] = red[e][t];
+      if (bnsum) {
+        a.bnpart[((long)mp.unit * 2 + 0) * a.C + c + e] = red[e][9];
+        a.bnpart[((long)mp.unit * 2 + 1) * a.C + c + e] = red[e][10];
+      }
+    }
+  }
+}
+
+template <typename T>
+int launch_fwd_lds(int act, const DwArgs& a, hipStream_t st) {
+  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
+  const int blocks = (int)((waves + 3) / 4);
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_lds_kernel<T, ACT_NONE>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_lds_kernel<T, ACT_RELU>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_fwd_lds_kernel<T, ACT_BNRELU>), dim3(blocks), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <typename T, bool RES>
+void launch_bwd_lds_r(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_NONE, RES>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_RELU, RES>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_BNRELU, RES>), dim3(blocks), dim3(256), 0, st, a);
+}
+
+template <typename T>
+int launch_bwd_lds(int act, const DwBwdArgs& a, hipStream_t st) {
+  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
+  const int blocks = (int)((waves + 3) / 4);
+  if (a.dRes) launch_bwd_lds_r<T, true>(act, a, blocks, st);
+  else launch_bwd_lds_r<T, false>(act, a, blocks, st);
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 int xcp_internal_gemm_tune(int cfg);   // gemm.hip
@@ -774,7 +1147,7 @@ int xcp_tune(int knob, int value) {
   if (knob == 4 || knob == 5) {
     int& k = knob == 4 ? g_dw_fwd_kernel : g_dw_bwd_kernel;
     const int old = k;
-    if (value == 0 || value == 1) k = value;
+    if (value >= 0 && value <= 2) k = value;
     return old;
   }
   int* k = knob == 0 ? &g_fwd_maxpx : knob == 1 ? &g_bwd_maxpx : nullptr;
@@ -790,6 +1163,11 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
   const int maxpx = g_fwd_maxpx;
   DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, maxpx)};
+  if (g_dw_fwd_kernel == 2) {
+    if (dtype == XCP_BF16) return launch_fwd_lds<bf16>(act, a, stream);
+    if (dtype == XCP_F32) return launch_fwd_lds<float>(act, a, stream);
+    return XCP_EUNSUPPORTED;
+  }
   if (g_dw_fwd_kernel == 0) {
     if (dtype == XCP_BF16) return launch_fwd_row<bf16>(act, a, stream);
     if (dtype == XCP_F32) return launch_fwd_row<float>(act, a, stream);
@@ -803,7 +1181,7 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
 // number of partial rows (spatial workgroups) of the backward's slabs
 int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
   (void)C;
-  if (g_dw_bwd_kernel == 0) return N * ((W + RCOLS - 1) / RCOLS);
+  if (g_dw_bwd_kernel != 1) return N * ((W + RCOLS - 1) / RCOLS);
   const TileGeo g = tile_geo(H, W, g_bwd_maxpx);
   return N * g.nth * g.ntw;
 }
@@ -822,6 +1200,11 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
   a.N = N; a.H = H; a.W = W; a.C = C;
   a.ngroups = ngroups_for(C, dtype);
   a.g = tile_geo(H, W, maxpx);
+  if (g_dw_bwd_kernel == 2) {
+    if (dtype == XCP_BF16) return launch_bwd_lds<bf16>(act, a, stream);
+    if (dtype == XCP_F32) return launch_bwd_lds<float>(act, a, stream);
+    return XCP_EUNSUPPORTED;
+  }
   if (g_dw_bwd_kernel == 0) {
     if (dtype == XCP_BF16) return launch_bwd_row<bf16>(act, a, stream);
     if (dtype == XCP_F32) return launch_bwd_row<float>(act, a, stream);

@@ -736,6 +736,7 @@ XCP_DEV int tswz(int m, int col) {             // byte offset of bf16 column col
   return m * 512 + ((((col >> 3) ^ ((m & 7) << 1))) << 4) + (col & 7) * 2;
 }
 
+template <int ABL>
 __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * T_SLOT];
   const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
@@ -814,11 +815,16 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (ABL == 2) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(xf[i]), "v"(gf[i]));
+    } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], gf[i], acc[ih * 4 + i][j], 0, 0, 0);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], gf[i], acc[ih * 4 + i][j], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
@@ -833,12 +839,12 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
       for (int j = 0; j < 4; ++j) xf[j] = frag(sx, ms, wc * 64 + j * 16);
 #pragma unroll
       for (int i = 0; i < 4; ++i) gf[i] = frag(sg, ms, wr * 128 + i * 16);
-      if (nxt) issue(2 * ms, kt + 1);
+      if (ABL != 1 && nxt) issue(2 * ms, kt + 1);
       sync_mfma(0);
       // n-bot
 #pragma unroll
       for (int i = 0; i < 4; ++i) gf[i] = frag(sg, ms, wr * 128 + 64 + i * 16);
-      if (nxt) {
+      if (ABL != 1 && nxt) {
         issue(2 * ms + 1, kt + 1);
         wait_vmcnt<4>();   // ms 0: m1 half-tiles of kt (for Q2); ms 1: m0 half-tiles of kt+1
       } else {
@@ -919,7 +925,7 @@ int xcp_internal_tn_tune(int knob, int v) {
 
 int xcp_internal_gemm_var(int v) {
   const int old = g_nt256_var;
-  if (v == 0 || v == 1) g_nt256_var = v;
+  if (v == 0 || v == 1 || v == 5 || v == 6) g_nt256_var = v;
   return old;
 }
 
@@ -957,7 +963,10 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
   if (gmode < 0 || gmode > 2 || (gmode == 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   TNArgs a{G, ldg, X, ldx, P, M, N, K, S, rows_per_split, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (tn_big(dtype, gmode, N, K)) {
-    hipLaunchKernelGGL(gemm_tn256_kernel, dim3(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S), dim3(512), 0, stream, a);
+    const dim3 grid(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S);
+    if (g_nt256_var == 5) hipLaunchKernelGGL(gemm_tn256_kernel<1>, grid, dim3(512), 0, stream, a);
+    else if (g_nt256_var == 6) hipLaunchKernelGGL(gemm_tn256_kernel<2>, grid, dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL(gemm_tn256_kernel<0>, grid, dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(N, 128) * xcp_cdiv(K, 128) * S;

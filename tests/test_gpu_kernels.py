@@ -144,7 +144,7 @@ def test_gemm_tn(ops, gpu, dt, M, N, K, tn):
     assert rel_err(out.view(N, K), ref) < (1e-5 if dt == torch.float32 else 1e-3)
 
 
-@pytest.fixture(params=[0, 1], ids=["row", "tile"])
+@pytest.fixture(params=[2, 0, 1], ids=["ldsrow", "row", "tile"])
 def dw_family(request, ops):
     """Run a depthwise test under both kernel families (xcp_tune knobs 4 / 5)."""
     of = ops._lib.call("xcp_tune", 4, request.param)

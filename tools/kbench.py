@@ -60,7 +60,7 @@ def main():
     if not sel or "copy" in sel:
         rep("torch copy (ref BW)", timeit(lambda: Y.copy_(X)), 2 * tensor_bytes)
     if "dwrow" in sel:
-        for kern in (0, 1):
+        for kern in [int(v) for v in os.environ.get("XCP_DWK", "2,0,1").split(",")]:
             oldk = ops._lib.call("xcp_tune", 4, kern)
             oldb = ops._lib.call("xcp_tune", 5, kern)
             for act in (1, 2):
@@ -100,6 +100,17 @@ def main():
             rep(f"weight_grad 728x728 tn={tn}", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)),
                 flops=2.0 * M * C * C)
             ops._lib.call("xcp_tune", 6, old)
+    if "tnabl" in sel:
+        out = torch.empty(C * C, device=dev)
+        P = torch.empty(28 * C * C, device=dev)
+        rps = ops._lib.call("xcp_gemm_tn_rows_per_split", 1, 0, M, C, C)
+        S = (M + rps - 1) // rps
+        for var in (0, 5, 6):
+            old = ops._lib.call("xcp_tune", 3, var)
+            rep(f"gemm_tn kernel only S={S} var={var}", timeit(lambda: ops.gemm_tn(D, X, P, M, C, C, S, rps)),
+                flops=2.0 * M * C * C)
+            ops._lib.call("xcp_tune", 3, old)
+        rep(f"reduce_slabs S={S}", timeit(lambda: ops.reduce_slabs(P, S, C * C, out)), 4 * S * C * C)
     if "tnwgs" in sel:
         out = torch.empty(C * C, device=dev)
         for wgs in (128, 256, 384, 512, 768):
