@@ -71,7 +71,7 @@ int xcp_dw_bwd_chunks(int N, int H, int W, int C);
  * (0: staggered wave groups, 1: lockstep; measurement only); 4 / 5 = depthwise
  * forward / backward kernel family (0: row walk, 1: LDS tile); 6 = weight-gradient
  * kernel (1: 256x256 for dense bf16, 0: 128x128); 7 = target workgroups of the
- * 256x256 weight-gradient kernel.
+ * 256x256 weight-gradient kernel; 8 = stem conv1 kernels (1: tiled, 0: per-pixel).
  * Returns the previous value (-1: unknown knob). */
 int xcp_tune(int knob, int value);
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,

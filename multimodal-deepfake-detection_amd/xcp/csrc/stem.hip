@@ -120,7 +120,198 @@ __global__ __launch_bounds__(256) void permute3_kernel(const float* __restrict__
   out[g] = from_f<TO>(in[((long)idx[0] * d1 + idx[1]) * d2 + idx[2]]);
 }
 
+
+// ---------------------------------------------------------------------------------
+// Tiled conv1 (default).  The per-pixel kernels above re-read each input value ~9x
+// through L1 with scalar stride-2 loads and, in the forward, fetch the 864 weights
+// per thread with vector loads; both measured ~0.45 TB/s.  Here a workgroup stages
+// the 2*TH+1 input rows (3 channels, fp32) of TH output rows of one frame in LDS with
+// coalesced loads.  Forward: a thread computes all 32 channels of one output pixel,
+// channel pairs with packed FMAs, weights through the scalar cache (uniform
+// addresses).  Weight gradient: a thread owns one output-channel pair x all 27 taps
+// (27 packed accumulators) for every 16th pixel of the tile, loops over tiles
+// (persistent), and the 16 pixel groups are reduced in LDS at the end.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// LDS row pitch of the staged input (floats): IW rounded up to 64 (one 4-B LDS-DMA
+// instruction fills 64 consecutive floats of a row)
+XCP_DEV int pitch1(int IW) { return (IW + 63) & ~63; }
+__device__ float g_zero1[64];
+
+// Stage the 3 x (2*TH+1) input rows of output rows [oh0, oh0+TH) with 4-B LDS-DMA
+// (wave w fills rows w, w+4, ...; all issued before one wait).  Rows past the frame
+// and columns past IW read zeros.
+template <int TH>
+XCP_DEV void stage_rows(const float* __restrict__ X, float* sx, int n, int oh0, int IH, int IW, int tid) {
+  constexpr int R = 2 * TH + 1;
+  const int rows = min(R, IH - 2 * oh0), P = pitch1(IW);
+  const int lane = tid & 63, w = tid >> 6;
+  for (int rr = w; rr < 3 * R; rr += 4) {
+    const int ci = rr / R, r = rr - ci * R;
+    const float* src = X + (((long)n * 3 + ci) * IH + 2 * oh0 + r) * IW;
+    for (int j = 0; j < P; j += 64) {
+      const int col = j + lane;
+      const float* p = (r < rows && col < IW) ? src + col : g_zero1 + lane;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                       (void __attribute__((address_space(3)))*)(sx + rr * P + j), 4, 0, 0);
+    }
+  }
+}
+
+template <typename T, int TH>
+__global__ __launch_bounds__(256) void conv1_fwd_tile_kernel(const float* __restrict__ X, const float* __restrict__ Wt,
+                                                             T* __restrict__ Y, int N, int IH, int IW, int OH, int OW) {
+  extern __shared__ __attribute__((aligned(16))) float sx[];   // [3][2*TH+1][pitch] input, then [27][32] weights
+  constexpr int R = 2 * TH + 1;
+  const int P = pitch1(IW);
+  float* sw = sx + 3 * R * P;
+  const int ntile = (OH + TH - 1) / TH;
+  const int n = blockIdx.x / ntile, oh0 = (blockIdx.x % ntile) * TH;
+  const int tid = threadIdx.x;
+  stage_rows<TH>(X, sx, n, oh0, IH, IW, tid);
+  for (int i = tid; i < C1 * K1; i += 256) sw[(i % K1) * C1 + i / K1] = Wt[i];   // [co][k] -> [k][co]
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's LDS-DMA landed (then the barrier)
+  __syncthreads();
+  const int npx = min(TH, OH - oh0) * OW;
+  // two pixels per thread and pass; taps outer, the 32 weights of a tap read from LDS
+  // (one address for the whole wave: broadcast), channel pairs x pixel pairs packed
+  for (int p0 = 2 * tid; p0 < npx; p0 += 512) {
+    const int p1 = min(p0 + 1, npx - 1);
+    const int r0 = p0 / OW, r1 = p1 / OW;
+    const int b0 = 2 * r0 * P + 2 * (p0 - r0 * OW), b1 = 2 * r1 * P + 2 * (p1 - r1 * OW);
+    f2v acc[C1];   // acc[co] = (pixel p0, pixel p1)
+#pragma unroll
+    for (int co = 0; co < C1; ++co) acc[co] = f2v(0.f);
+#pragma unroll 3
+    for (int k = 0; k < K1; ++k) {
+      const int ci = k / 9, ky = (k % 9) / 3, kx = k % 3;
+      const int off = (ci * R + ky) * P + kx;
+      const f2v x{sx[b0 + off], sx[b1 + off]};
+      const float4* wk = reinterpret_cast<const float4*>(sw + k * C1);
+#pragma unroll
+      for (int q = 0; q < C1 / 4; ++q) {
+        const float4 w4 = wk[q];
+        acc[4 * q + 0] = __builtin_elementwise_fma(x, f2v(w4.x), acc[4 * q + 0]);
+        acc[4 * q + 1] = __builtin_elementwise_fma(x, f2v(w4.y), acc[4 * q + 1]);
+        acc[4 * q + 2] = __builtin_elementwise_fma(x, f2v(w4.z), acc[4 * q + 2]);
+        acc[4 * q + 3] = __builtin_elementwise_fma(x, f2v(w4.w), acc[4 * q + 3]);
+      }
+    }
+    float o[C1];
+#pragma unroll
+    for (int co = 0; co < C1; ++co) o[co] = acc[co][0];
+    T* yp = Y + ((long)n * OH * OW + (long)oh0 * OW + p0) * C1;
+#pragma unroll
+    for (int q = 0; q < C1; q += 8) VecIO<T, 8>::store(yp + q, o + q);
+    if (p0 + 1 < npx) {
+#pragma unroll
+      for (int co = 0; co < C1; ++co) o[co] = acc[co][1];
+#pragma unroll
+      for (int q = 0; q < C1; q += 8) VecIO<T, 8>::store(yp + C1 + q, o + q);
+    }
+  }
+}
+
+constexpr int W1_TH = 2;
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv1_wgrad_tile_kernel(const float* __restrict__ X, const T* __restrict__ dY,
+                                                               float* __restrict__ part, int N, int IH, int IW, int OH,
+                                                               int OW) {
+  constexpr int TH = W1_TH, R = 2 * TH + 1;
+  extern __shared__ __attribute__((aligned(16))) float sm1[];   // input [3][R][pitch] fp32, then dY [TH*OW][C1] (T)
+  const int P = pitch1(IW);
+  float* sx = sm1;
+  T* sdy = reinterpret_cast<T*>(sm1 + 3 * R * P);   // 3*R*P floats: a multiple of 4 -> 16-B aligned
+  const int tid = threadIdx.x, cq = tid & 7, pg = tid >> 3;   // channels 4cq..4cq+3; 32 pixel groups
+  const int ntile = (OH + TH - 1) / TH;
+  f2v acc[2][K1];   // [channel pair][tap]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < K1; ++k) acc[h][k] = f2v(0.f);
+  for (int t = blockIdx.x; t < N * ntile; t += gridDim.x) {
+    const int n = t / ntile, oh0 = (t % ntile) * TH;
+    const int npx = min(TH, OH - oh0) * OW;
+    __syncthreads();   // previous tile consumed
+    stage_rows<TH>(X, sx, n, oh0, IH, IW, tid);
+    {   // dY rows of the tile: contiguous [npx][32] in NHWC, 16-B LDS-DMA
+      const T* src = dY + (((long)n * OH + oh0) * OW) * C1;
+      constexpr int EPC = 16 / (int)sizeof(T);
+      const int chunks = npx * C1 / EPC;
+      const int lane = tid & 63;
+      for (int i0 = (tid >> 6) * 64; i0 < chunks; i0 += 256) {
+        const bool ok = i0 + lane < chunks;
+        const void* p = ok ? (const void*)(src + (long)(i0 + lane) * EPC) : (const void*)g_zero1;
+        if (ok)
+          __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                           (void __attribute__((address_space(3)))*)(reinterpret_cast<char*>(sdy) +
+                                                                                     (long)i0 * 16),
+                                           16, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+    __syncthreads();
+    for (int p = pg; p < npx; p += 32) {
+      const int r = p / OW, ow = p - r * OW;
+      float d[4];
+      VecIO<T, 4>::load(sdy + p * C1 + 4 * cq, d);
+      const f2v d0{d[0], d[1]}, d1{d[2], d[3]};
+      const float* xb = sx + 2 * r * P + 2 * ow;
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const float* xr = xb + (ci * R + ky) * P;
+          const float2 x01 = *reinterpret_cast<const float2*>(xr);
+          const float x2 = xr[2];
+          const int k = ci * 9 + ky * 3;
+          acc[0][k] = __builtin_elementwise_fma(f2v(x01.x), d0, acc[0][k]);
+          acc[1][k] = __builtin_elementwise_fma(f2v(x01.x), d1, acc[1][k]);
+          acc[0][k + 1] = __builtin_elementwise_fma(f2v(x01.y), d0, acc[0][k + 1]);
+          acc[1][k + 1] = __builtin_elementwise_fma(f2v(x01.y), d1, acc[1][k + 1]);
+          acc[0][k + 2] = __builtin_elementwise_fma(f2v(x2), d0, acc[0][k + 2]);
+          acc[1][k + 2] = __builtin_elementwise_fma(f2v(x2), d1, acc[1][k + 2]);
+        }
+    }
+  }
+  // reduce the 32 pixel groups: lanes xor 8 / 16 / 32 within the wave, then the 4 waves in LDS
+  __syncthreads();
+  float* red = sm1;   // [4 waves][C1][K1]
+  const int w = tid >> 6;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float v = acc[h][k][e];
+        v += __shfl_xor(v, 8, 64);
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if ((tid & 63) < 8) red[(w * C1 + 4 * cq + 2 * h + e) * K1 + k] = v;
+      }
+  __syncthreads();
+  for (int i = tid; i < C1 * K1; i += 256) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v += red[q * C1 * K1 + i];
+    part[(long)blockIdx.x * (C1 * K1) + i] = v;
+  }
+}
+
 }  // namespace
+
+namespace {
+int g_conv1_tile = 1;   // 1 = tiled conv1 kernels, 0 = per-pixel kernels (xcp_tune knob 8)
+constexpr int F1_TH = 4;
+}
+
+int xcp_internal_conv1_tune(int v) {
+  const int old = g_conv1_tile;
+  if (v == 0 || v == 1) g_conv1_tile = v;
+  return old;
+}
 
 extern "C" {
 
@@ -128,6 +319,19 @@ int xcp_conv1_fwd(int dtype, const float* X, const float* W, void* Y, int N, int
   const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
   const long total = (long)N * OH * OW * (C1 / 8);
   if (total <= 0) return XCP_OK;
+  const size_t lds = ((size_t)3 * (2 * F1_TH + 1) * ((IW + 63) & ~63) + C1 * K1) * sizeof(float);
+  if (g_conv1_tile == 1 && lds <= 64 * 1024) {
+    const unsigned blocks = (unsigned)(N * ((OH + F1_TH - 1) / F1_TH));
+    if (dtype == XCP_BF16)
+      hipLaunchKernelGGL((conv1_fwd_tile_kernel<bf16, F1_TH>), dim3(blocks), dim3(256), lds, st, X, W, (bf16*)Y, N, IH,
+                         IW, OH, OW);
+    else if (dtype == XCP_F32)
+      hipLaunchKernelGGL((conv1_fwd_tile_kernel<float, F1_TH>), dim3(blocks), dim3(256), lds, st, X, W, (float*)Y, N,
+                         IH, IW, OH, OW);
+    else
+      return XCP_EUNSUPPORTED;
+    return (int)hipGetLastError();
+  }
   const unsigned g = (unsigned)((total + 255) / 256);
   if (dtype == XCP_BF16)
     hipLaunchKernelGGL(conv1_fwd_kernel<bf16>, dim3(g), dim3(256), 0, st, X, W, (bf16*)Y, N, IH, IW, OH, OW);
@@ -139,8 +343,19 @@ int xcp_conv1_fwd(int dtype, const float* X, const float* W, void* Y, int N, int
 }
 
 // number of partial rows xcp_conv1_wgrad writes ([parts][32*27])
+static size_t conv1_wgrad_lds(int dtype, int IW, int OW) {
+  const size_t in = (size_t)3 * (2 * W1_TH + 1) * ((IW + 63) & ~63) * sizeof(float);
+  const size_t dy = (size_t)W1_TH * OW * C1 * (dtype == XCP_BF16 ? 2 : 4);
+  const size_t red = (size_t)4 * C1 * K1 * sizeof(float);
+  return (in + dy > red ? in + dy : red);
+}
+
 int xcp_conv1_wgrad_parts(int N, int IH, int IW) {
   const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
+  if (g_conv1_tile == 1 && conv1_wgrad_lds(XCP_F32, IW, OW) <= 64 * 1024) {
+    const int tiles = N * ((OH + W1_TH - 1) / W1_TH);
+    return tiles < 1024 ? tiles : 1024;
+  }
   const long P = (long)N * OH * OW;
   long blocks = 1024;
   const long minpix = 64 * 8;
@@ -153,6 +368,18 @@ int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int 
   const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
   const long P = (long)N * OH * OW;
   const int blocks = xcp_conv1_wgrad_parts(N, IH, IW);
+  if (g_conv1_tile == 1 && conv1_wgrad_lds(XCP_F32, IW, OW) <= 64 * 1024) {
+    const size_t lds = conv1_wgrad_lds(dtype, IW, OW);
+    if (dtype == XCP_BF16)
+      hipLaunchKernelGGL(conv1_wgrad_tile_kernel<bf16>, dim3(blocks), dim3(256), lds, st, X, (const bf16*)dY, part, N, IH,
+                         IW, OH, OW);
+    else if (dtype == XCP_F32)
+      hipLaunchKernelGGL(conv1_wgrad_tile_kernel<float>, dim3(blocks), dim3(256), lds, st, X, (const float*)dY, part, N,
+                         IH, IW, OH, OW);
+    else
+      return XCP_EUNSUPPORTED;
+    return (int)hipGetLastError();
+  }
   const long ppb = (P + blocks - 1) / blocks;
   if (dtype == XCP_BF16)
     hipLaunchKernelGGL(conv1_wgrad_kernel<bf16>, dim3(blocks), dim3(256), 0, st, X, (const bf16*)dY, part, N, IH, IW, OH,

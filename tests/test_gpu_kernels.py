@@ -301,8 +301,11 @@ def test_avgpool(ops, gpu, dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-def test_conv1_fwd_wgrad(ops, gpu, dt):
-    N, IH = 2, 75
+@pytest.mark.parametrize("tile", [1, 0], ids=["tiled", "perpixel"])
+@pytest.mark.parametrize("IH", [75, 299])
+def test_conv1_fwd_wgrad(ops, gpu, dt, tile, IH):
+    N = 2
+    old = ops._lib.call("xcp_tune", 8, tile)
     x = torch.rand(N, 3, IH, IH, device=gpu)
     w = (torch.randn(32, 3, 3, 3, device=gpu) / 5).requires_grad_(True)
     ref = F.conv2d(x, w, None, 2, 0)
@@ -314,6 +317,8 @@ def test_conv1_fwd_wgrad(ops, gpu, dt):
     ref.backward(dy.float())
     dW = torch.empty(32 * 27, device=gpu)
     ops.conv1_wgrad(x, nhwc(dy), dW, N, IH, IH)
+    torch.cuda.synchronize()
+    ops._lib.call("xcp_tune", 8, old)
     assert rel_err(dW.view(32, 3, 3, 3), w.grad) < (1e-5 if dt == torch.float32 else 1e-2)
 
 

@@ -118,6 +118,20 @@ def main():
             rep(f"weight_grad 728x728 wgs={wgs}", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)),
                 flops=2.0 * M * C * C)
             ops._lib.call("xcp_tune", 7, old)
+    if "stem" in sel:
+        NS, IH = 256, 299
+        OH = (IH - 3) // 2 + 1
+        xin = torch.rand(NS, 3, IH, IH, device=dev, generator=g)
+        w1 = torch.randn(32, 3, 3, 3, device=dev, generator=g) / 5
+        c1 = torch.empty(NS * OH * OH, 32, device=dev, dtype=dt)
+        d1 = torch.randn(NS * OH * OH, 32, device=dev, generator=g).to(dt)
+        gw = torch.empty(32 * 27, device=dev)
+        byts = xin.numel() * 4 + c1.numel() * 2
+        for tile in (1, 0):
+            old = ops._lib.call("xcp_tune", 8, tile)
+            rep(f"conv1_fwd tile={tile}", timeit(lambda: ops.conv1_fwd(xin, w1, c1, NS, IH, IH), iters=5), byts)
+            rep(f"conv1_wgrad tile={tile}", timeit(lambda: ops.conv1_wgrad(xin, d1, gw, NS, IH, IH), iters=5), byts)
+            ops._lib.call("xcp_tune", 8, old)
     if "gemmv" in sel:
         for var in [int(v) for v in os.environ.get('XCP_VARS', '0,1').split(',')]:
             old = ops._lib.call("xcp_tune", 3, var)
