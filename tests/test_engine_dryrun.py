@@ -30,6 +30,8 @@ def fake_lib(monkeypatch):
             return 5
         if name == "xcp_conv1_wgrad_parts":
             return 3
+        if name in ("xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows"):
+            return 256
         return 0
 
     monkeypatch.setattr(_lib, "call", fake_call)
