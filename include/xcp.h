@@ -114,9 +114,12 @@ int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int 
 int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int d2, int p0, int p1, int p2,
                  xcp_stream_t stream);
 
-/* ---- LSTM recurrence (nn.LSTM, XceptionLSTMV.py:18-23, :67) ---- */
-int xcp_lstm_fwd(const float* xproj, const float* whhT, const float* bih, const float* bhh, float* out, float* hprev,
-                 float* cst, float* gates, float* hn, float* cn, int B, int T, int H, xcp_stream_t stream);
+/* ---- LSTM recurrence (nn.LSTM, XceptionLSTMV.py:18-23, :67) ----
+ * whh is W_hh [4H][H] as nn.LSTM stores it (weight_hh_l0); whhT ([H][4H]) is read only by the
+ * generic kernel, i.e. when xcp_lstm_needs_whhT(H) returns 1 (H = 64 / 128 run register-resident). */
+int xcp_lstm_needs_whhT(int H);
+int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
+                 float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, xcp_stream_t stream);
 int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const float* whh, const float* cst,
                  const float* gates, float* dgates, int B, int T, int H, xcp_stream_t stream);
 

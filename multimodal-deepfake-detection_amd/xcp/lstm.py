@@ -28,15 +28,18 @@ class LSTMFunction(torch.autograd.Function):
         M = B * T
         xproj = torch.empty(M, 4 * H, device=dev, dtype=torch.float32)
         ops.gemm_nt(xf, w_ih.detach().contiguous(), xproj, M, 4 * H, I)
-        whhT = torch.empty(H * 4 * H, device=dev, dtype=torch.float32)
-        ops.permute3(w_hh.detach().contiguous(), whhT, 4 * H, H, 1, (1, 0, 2))
+        whh = w_hh.detach().contiguous()
+        whhT = None
+        if ops.lstm_needs_whhT(H):
+            whhT = torch.empty(H * 4 * H, device=dev, dtype=torch.float32)
+            ops.permute3(whh, whhT, 4 * H, H, 1, (1, 0, 2))
         out = torch.empty(B, T, H, device=dev, dtype=torch.float32)
         hprev = torch.empty(B, T, H, device=dev, dtype=torch.float32)
         cst = torch.empty(B, T, H, device=dev, dtype=torch.float32)
         gates = torch.empty(B, T, 4 * H, device=dev, dtype=torch.float32)
         hn = torch.empty(1, B, H, device=dev, dtype=torch.float32)
         cn = torch.empty(1, B, H, device=dev, dtype=torch.float32)
-        ops.lstm_fwd(xproj, whhT, b_ih.detach(), b_hh.detach(), out, hprev, cst, gates, hn, cn, B, T, H)
+        ops.lstm_fwd(xproj, whh, whhT, b_ih.detach(), b_hh.detach(), out, hprev, cst, gates, hn, cn, B, T, H)
         ctx.save_for_backward(xf, w_ih, w_hh, hprev, cst, gates)
         ctx.dims = (B, T, I, H)
         ctx.x_dtype = x.dtype

@@ -241,8 +241,12 @@ def permute3(inp, out, d0, d1, d2, perm):
 
 
 # ---------------------------------------------------------------- LSTM
-def lstm_fwd(xproj, whhT, bih, bhh, out, hprev, cst, gates, hn, cn, B, T, H):
-    _lib.call("xcp_lstm_fwd", _p(xproj), _p(whhT), _p(bih), _p(bhh), _p(out), _p(hprev), _p(cst), _p(gates), _p(hn),
+def lstm_needs_whhT(H):
+    return _lib.call("xcp_lstm_needs_whhT", H) != 0
+
+
+def lstm_fwd(xproj, whh, whhT, bih, bhh, out, hprev, cst, gates, hn, cn, B, T, H):
+    _lib.call("xcp_lstm_fwd", _p(xproj), _p(whh), _p(whhT), _p(bih), _p(bhh), _p(out), _p(hprev), _p(cst), _p(gates), _p(hn),
               _p(cn), B, T, H, stream())
 
 

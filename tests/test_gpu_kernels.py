@@ -333,11 +333,21 @@ def test_permute3(ops, gpu):
     assert torch.equal(ob.view(9, 5, 7), x.permute(2, 0, 1).to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("kernel", ["register", "generic"])
 @pytest.mark.parametrize("H,T", [(128, 16), (512, 12)])
-def test_lstm_module_vs_oracle(gpu, golden, H, T):
+def test_lstm_module_vs_oracle(ops, gpu, golden, H, T, kernel):
+    """Both recurrence kernels (xcp_tune knob 9) against the reference nn.LSTM goldens."""
     import numpy as np
     from xcp.lstm import LSTM
     g = golden("lstm.npz")
+    old = ops._lib.call("xcp_tune", 9, 0 if kernel == "register" else 1)
+    try:
+        _lstm_case(gpu, g, H, T, np, LSTM)
+    finally:
+        ops._lib.call("xcp_tune", 9, old)
+
+
+def _lstm_case(gpu, g, H, T, np, LSTM):
     torch.manual_seed(0)
     lstm = LSTM(2048, H, 1, batch_first=True).to(gpu)
     x = torch.randn((2, T, 2048), generator=torch.Generator().manual_seed(555)).to(gpu).requires_grad_(True)
@@ -356,3 +366,31 @@ def test_lstm_module_vs_oracle(gpu, golden, H, T):
             np.testing.assert_allclose(prm.grad.double().norm().item(), ref, rtol=1e-4)
         else:
             np.testing.assert_allclose(prm.grad.cpu().numpy(), ref, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("kernel", ["register", "generic"])
+def test_lstm_h64_vs_oracle(ops, gpu, kernel):
+    """H = 64 (the second register-resident instantiation) against the oracle's nn.LSTM
+    restatement (oracle/xception_oracle.py lstm_forward, autograd for the gradients)."""
+    from oracle import xception_oracle as O
+    from xcp.lstm import LSTM
+    old = ops._lib.call("xcp_tune", 9, 0 if kernel == "register" else 1)
+    try:
+        torch.manual_seed(3)
+        lstm = LSTM(256, 64, 1, batch_first=True).to(gpu)
+        x = torch.randn((3, 9, 256), generator=torch.Generator().manual_seed(7))
+        xg = x.to(gpu).requires_grad_(True)
+        o, (h, c) = lstm(xg)
+        r = torch.randn(o.shape, generator=torch.Generator().manual_seed(8))
+        (o * r.to(gpu)).sum().backward()
+        cp = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in lstm.named_parameters()}
+        xc = x.clone().requires_grad_(True)
+        ro, rh, rc = O.lstm_forward(xc, cp["weight_ih_l0"], cp["weight_hh_l0"], cp["bias_ih_l0"], cp["bias_hh_l0"])
+        (ro * r).sum().backward()
+        torch.testing.assert_close(o.detach().cpu(), ro.detach(), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(c.detach().cpu(), rc.detach(), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(xg.grad.cpu(), xc.grad, rtol=1e-3, atol=1e-5)
+        for n, p in lstm.named_parameters():
+            torch.testing.assert_close(p.grad.cpu(), cp[n].grad, rtol=1e-3, atol=1e-5)
+    finally:
+        ops._lib.call("xcp_tune", 9, old)
