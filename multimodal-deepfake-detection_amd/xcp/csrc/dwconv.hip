@@ -1136,6 +1136,7 @@ int xcp_internal_gemm_var(int v);      // gemm.hip
 int xcp_internal_tn_tune(int knob, int v);   // gemm.hip
 int xcp_internal_conv1_tune(int v);          // stem.hip
 int xcp_internal_lstm_tune(int v);           // lstm.hip
+int xcp_internal_nt_grid(int v);             // gemm.hip
 
 extern "C" {
 
@@ -1148,6 +1149,7 @@ int xcp_tune(int knob, int value) {
   if (knob == 6 || knob == 7) return xcp_internal_tn_tune(knob, value);
   if (knob == 8) return xcp_internal_conv1_tune(value);
   if (knob == 9) return xcp_internal_lstm_tune(value);
+  if (knob == 10) return xcp_internal_nt_grid(value);
   if (knob == 4 || knob == 5) {
     int& k = knob == 4 ? g_dw_fwd_kernel : g_dw_bwd_kernel;
     const int old = k;

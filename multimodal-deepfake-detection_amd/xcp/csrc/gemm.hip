@@ -34,6 +34,8 @@ template <> struct GT<float> { static constexpr int EPC = 4; };
 
 __device__ __attribute__((aligned(64))) uint4 g_zero16[4];   // zero line for masked LDS-DMA chunks
 
+template <int V> struct IC { static constexpr int value = V; };
+
 XCP_DEV int swz(int row, int chunk) { return row * ROWB + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
 // Row gather for the A operand (NT) / X operand (TN):
@@ -319,6 +321,7 @@ constexpr int L_CP = 256 * 2 + 16;             // LDS-staged epilogue row pitch 
 // LDS-staged epilogue of the 256x256 kernels: acc[i][j][r] is C[row wr*128 + i*16 + fr]
 // [col wc*64 + j*16 + fg*4 + r]; rounded tile staged in LDS, written with coalesced 16-B
 // stores, BatchNorm partial sums per 128-row half ([ceil(M/128)][2][N] layout).
+template <int EPIV = 0>
 XCP_DEV void epilogue256(f32x4 (&acc)[8][4], char* smem, const NTArgs& a, int m0, int n0, int bm, int tid) {
   const int lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3, fr = lane & 15, fg = lane >> 4;
   bf16* C = reinterpret_cast<bf16*>(a.C);
@@ -348,7 +351,7 @@ XCP_DEV void epilogue256(f32x4 (&acc)[8][4], char* smem, const NTArgs& a, int m0
     for (int it = 0; it < 16; ++it) {
       const int m = m0 + rq + 16 * it;
       if (m < a.M && n < a.N) {
-        *reinterpret_cast<uint4*>(C + (long)m * a.ldc + n) = cv[it];
+        if (EPIV == 0 || a.M < 0) *reinterpret_cast<uint4*>(C + (long)m * a.ldc + n) = cv[it];
         float f[8];
         VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&cv[it]), f);
 #pragma unroll
@@ -418,7 +421,8 @@ XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
   else wait_vmcnt<0>();
 }
 
-template <bool STAG>
+// EPIV (measurement only, xcp_tune knob 3 = 2 / 3): 1 = no C stores, 2 = no epilogue
+template <bool STAG, int EPIV = 0>
 __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   constexpr int RING = 2 * K_SLOT, EPI = 256 * L_CP;
   __shared__ __attribute__((aligned(16))) char smem[RING > EPI ? RING : EPI];
@@ -546,7 +550,283 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
     sync_mfma(1, bl, 0);
   }
   if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
-  epilogue256(acc, smem, a, m0, n0, bm, tid);
+  if constexpr (EPIV == 2) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (a.M < 0) a.stats[tid] = t;
+  } else {
+    epilogue256<EPIV>(acc, smem, a, m0, n0, bm, tid);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Persistent 256x256 bf16 NT kernel: the tile machinery of gemm_nt256k64_kernel (two
+// 64 KB LDS-DMA ring slots, 8 waves 2x4, four-phase quadrant schedule, staggered wave
+// groups, counted vmcnt), but one workgroup per CU walks a static list of tiles (tile =
+// round * grid + XCD-remapped workgroup id, so same-XCD workgroups hold neighbouring tiles
+// and share A rows in L2) and the K pipeline runs ACROSS tile boundaries: the last K-tile
+// of a tile prefetches K-tile 0 of the next one like any other stage, so no tile starts
+// with an exposed load.  That requires an epilogue that never touches LDS:
+//   * C stores: lanes fg / fg^1 (16 apart) swap 8-B pieces so every lane owns 16
+//     contiguous bytes; one store instruction writes 16 rows x 64 B.
+//   * BatchNorm partial sums of each 128-row half ([ceil(M/128)][2][N]) from the rounded
+//     registers: sums over the wave's 8 row fragments, then a 4-step reduce-scatter over
+//     the 16 row lanes (30 shuffles); lane fr ends with 2 adjacent columns of one statistic.
+// The epilogue's EPI_VM vector-memory ops per thread sit between A-bot(0) of the next tile
+// and the waits of that tile's first two phases; those waits allow for them, so the stores
+// drain under the next tile's MFMAs (the Q3 wait of K-tile 0 retires them).  A last K-tile
+// with <= 32 valid columns skips its second 32-deep MFMA step (K = 728: 736 instead of 768).
+constexpr int EPI_VM = 17;
+
+template <int N>
+XCP_DEV void wait_vm_imm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+XCP_DEV void wait_cnt_p(int n) {   // n in {0, 2, 4, E, E+2, E+4}
+  switch (n) {
+    case 0: wait_vm_imm<0>(); break;
+    case 2: wait_vm_imm<2>(); break;
+    case 4: wait_vm_imm<4>(); break;
+    case EPI_VM: wait_vm_imm<EPI_VM>(); break;
+    case EPI_VM + 2: wait_vm_imm<EPI_VM + 2>(); break;
+    default: wait_vm_imm<EPI_VM + 4>(); break;
+  }
+}
+
+template <bool STAG, int EPIV = 0>   // EPIV (measurement): 1 no C stores, 2 no stats, 3 neither
+__global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
+  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
+  const int tiles = gridM * gridN, G = gridDim.x;
+  // round r holds tiles [rG, rG+G): full rounds give each XCD a contiguous block of G/8 tiles;
+  // the last, partial round of R tiles goes to workgroups b < R (spread over all XCDs),
+  // again XCD-contiguous within it
+  const int full = tiles / G, R = tiles - full * G;
+  auto tile_of = [&](int r) { return r < full ? r * G + xcd_remap(blockIdx.x, G) : r * G + xcd_remap(blockIdx.x, R); };
+  const int my_tiles = full + ((int)blockIdx.x < R ? 1 : 0);
+  if (my_tiles == 0) return;            // uniform; before any barrier
+  int round = 0, tile = tile_of(0);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3, fr = lane & 15, fg = lane >> 4;
+  const bf16* A = reinterpret_cast<const bf16*>(a.A);
+  const bf16* B = reinterpret_cast<const bf16*>(a.B);
+  bf16* C = reinterpret_cast<bf16*>(a.C);
+
+  // half-tile rows loaded by this wave (as gemm_nt256k64_kernel)
+  const int arow = (w < 4 ? 16 * w : 128 + 16 * (w - 4));
+  const int brow = 64 * (w >> 1) + 16 * (w & 1);
+  const int lr = lane >> 3;
+  // swizzled 16-B chunk column (in elements) of the row a load of half-tile h, piece i fills
+  auto kc8 = [&](int h, int i) {
+    const bool isA = (h == 0 || h == 3);
+    const int row = (isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0)) + i * 8 + lr;
+    return ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+  };
+  const void* zero = g_zero16;
+  asm volatile("" : "+v"(zero));
+  auto glds = [](const void* p, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  // per-lane source element offsets (chunk column included; the host guarantees they fit
+  // 31 bits) of the tile the loads currently target: re-pointed to the next tile at the
+  // start of each tile's last K-tile
+  int src[4][2];
+  auto set_target = [&](int am0, int bn0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool isA = (h == 0 || h == 3);
+        const int row = (isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0)) + i * 8 + lr;
+        src[h][i] = (isA ? min(am0 + row, a.M - 1) * (int)a.lda : min(bn0 + row, a.N - 1) * (int)a.ldb) + kc8(h, i);
+      }
+  };
+  // half-tile h (0 A-top, 1 B-left, 2 B-right, 3 A-bot) of K-tile kt of the target tile into ring slot sl
+  auto issue = [&](int h, int kt, int sl) {
+    const bool isA = (h == 0 || h == 3);
+    const int row0 = isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0);
+    char* d = smem + sl * K_SLOT + (isA ? 0 : K_OP) + row0 * 128;
+    const int kb = kt * 64;
+    const bf16* base = isA ? A : B;
+    if (kb + 64 <= a.K) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) glds(base + (src[h][i] + kb), d + i * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        glds(kb + kc8(h, i) < a.K ? (const void*)(base + (src[h][i] + kb)) : zero, d + i * 1024);
+    }
+  };
+
+  const int nk = (a.K + 63) / 64;
+  const bool half_tail = a.K - (nk - 1) * 64 <= 32;
+  const int stat_rows = (a.M + 127) / 128;
+  set_target((tile / gridN) * 256, (tile % gridN) * 256);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue(h, 0, 0);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  if (STAG && wr == 1) __builtin_amdgcn_s_barrier();
+
+  f32x4 acc[8][4];
+  bf16x8 af[4][2], bl[2][2], br[2][2];   // [frag][k-step]
+  int slot = 0;
+  bool after_epi = false;
+  for (;;) {
+    const bool more = round + 1 < my_tiles;
+    const int next = more ? tile_of(round + 1) : tile;
+    const int cm0 = (tile / gridN) * 256, cn0 = (tile % gridN) * 256;
+    const int xm0 = (next / gridN) * 256, xn0 = (next % gridN) * 256;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool last = kt + 1 == nk;
+      const bool nxt = !last || more;
+      const int nkt = last ? 0 : kt + 1, nsl = slot ^ 1;
+      if (last && more) set_target(xm0, xn0);
+      const int e = (kt == 0 && after_epi) ? EPI_VM : 0;   // epilogue ops younger than this tile's loads
+      const bool one = last && half_tail;                  // only the first 32-deep step holds data
+      const char* sa = smem + slot * K_SLOT;
+      const char* sb = sa + K_OP;
+      auto mfma_q = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          if (ks == 1 && one) break;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[ih * 4 + i][jh * 2 + j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][ks], af[i][ks], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+        }
+      };
+      auto sync_mfma = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        mfma_q(ih, b, jh);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_barrier();
+      };
+      // Q0: A-top x B-left
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 1 && one) break;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bl[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + j * 16 + fr, ks * 4 + fg));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 16 + fr, ks * 4 + fg));
+      }
+      if (nxt) issue(0, nkt, nsl);
+      wait_cnt_p(2 + e + (nxt ? 2 : 0));   // B-right(kt) for Q1
+      sync_mfma(0, bl, 0);
+      // Q1: A-top x B-right
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 1 && one) break;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          br[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + 32 + j * 16 + fr, ks * 4 + fg));
+      }
+      if (nxt) issue(1, nkt, nsl);
+      wait_cnt_p(e + (nxt ? 4 : 0));       // A-bot(kt) for Q2
+      sync_mfma(0, br, 1);
+      // Q2: A-bot x B-right
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 1 && one) break;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
+      }
+      if (nxt) issue(2, nkt, nsl);
+      sync_mfma(1, br, 1);
+      // Q3: A-bot x B-left
+      if (nxt) {
+        issue(3, nkt, nsl);
+        wait_cnt_p(4);                     // A-top / B-left of the next K-tile (and the epilogue's stores)
+      }
+      sync_mfma(1, bl, 0);
+      slot = nsl;
+    }
+
+    // ---- LDS-free epilogue: round, BN partial sums, 16-B stores
+    const int bm = cm0 / 256;
+    const int mrow = cm0 + wr * 128 + fr;
+    const int ncol = cn0 + wc * 64;
+    const bool odd = fg & 1;
+    float s1[16], s2[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s1[q] = s2[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mrow + i * 16;
+      const bool mok = m < a.M;
+      uint2 pc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bf16x4 q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = (bf16)acc[i][j][r];
+        pc[j] = __builtin_bit_cast(uint2, q);
+        if (mok) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float f = (float)q[r];
+            s1[j * 4 + r] += f;
+            s2[j * 4 + r] = fmaf(f, f, s2[j * 4 + r]);
+          }
+        }
+      }
+      const uint2 snd0 = odd ? pc[0] : pc[1], snd1 = odd ? pc[2] : pc[3];
+      uint2 rc0, rc1;
+      rc0.x = __shfl_xor(snd0.x, 16, 64);
+      rc0.y = __shfl_xor(snd0.y, 16, 64);
+      rc1.x = __shfl_xor(snd1.x, 16, 64);
+      rc1.y = __shfl_xor(snd1.y, 16, 64);
+      const uint4 st0 = odd ? make_uint4(rc0.x, rc0.y, pc[1].x, pc[1].y) : make_uint4(pc[0].x, pc[0].y, rc0.x, rc0.y);
+      const uint4 st1 = odd ? make_uint4(rc1.x, rc1.y, pc[3].x, pc[3].y) : make_uint4(pc[2].x, pc[2].y, rc1.x, rc1.y);
+      const int c0 = ncol + (odd ? 16 + (fg - 1) * 4 : fg * 4);
+      bf16* crow = C + (long)m * a.ldc;
+      const bool wr_ok = (EPIV & 1) == 0 || a.M < 0;
+      if (wr_ok && mok && c0 < a.N) *reinterpret_cast<uint4*>(crow + c0) = st0;
+      if (wr_ok && mok && c0 + 32 < a.N) *reinterpret_cast<uint4*>(crow + c0 + 32) = st1;
+    }
+    if (a.stats && ((EPIV & 2) == 0 || a.M < 0)) {
+      // reduce-scatter of v[32] = (s1[16], s2[16]) over the 16 row lanes
+      float u[16], v8[8], v4[4], v2[2];
+      const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) u[q] = (b3 ? s2[q] : s1[q]) + __shfl_xor(b3 ? s1[q] : s2[q], 8, 64);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v8[q] = (b2 ? u[8 + q] : u[q]) + __shfl_xor(b2 ? u[q] : u[8 + q], 4, 64);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v4[q] = (b1 ? v8[4 + q] : v8[q]) + __shfl_xor(b1 ? v8[q] : v8[4 + q], 2, 64);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) v2[q] = (b0 ? v4[2 + q] : v4[q]) + __shfl_xor(b0 ? v4[q] : v4[2 + q], 1, 64);
+      // lane fr holds index 2fr, 2fr+1 of v: statistic fr>>3, j = (fr&7)>>1, r = (fr&1)*2 + q
+      const int col = ncol + ((fr & 7) >> 1) * 16 + fg * 4 + (fr & 1) * 2;
+      const int srow = bm * 2 + wr;
+      if (srow < stat_rows && col < a.N)
+        *reinterpret_cast<float2*>(a.stats + ((long)srow * 2 + (fr >> 3)) * a.N + col) = make_float2(v2[0], v2[1]);
+    }
+    asm volatile("" ::: "memory");
+    if (!more) break;
+    tile = next;
+    ++round;
+    after_epi = true;
+  }
+  if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
 }
 
 int g_tn_cfg = 1;      // xcp_tune knob 6: 1 = 256x256 weight-gradient kernel for dense bf16, 0 = 128x128
@@ -555,7 +835,11 @@ bool tn_big(int dtype, int gmode, int N, int K) {
   return g_tn_cfg == 1 && dtype == XCP_BF16 && gmode == 0 && N >= 128 && K >= 128;
 }
 
-int g_nt256_var = 0;   // xcp_tune knob 3: 0 = staggered wave groups, 1 = lockstep (measurement)
+// xcp_tune knob 3: 4 = one tile per workgroup, staggered wave groups (default), 1 = lockstep;
+// 0 / 7 = persistent kernel staggered / lockstep (measured slower: see DESIGN.md); 2 / 3 / 8-10 = ablations
+int g_nt256_var = 4;
+int g_num_cus = 256;   // set from the device at first use (xcp_gemm_nt)
+int g_nt_grid = 0;     // xcp_tune knob 10: persistent grid size (0 = one workgroup per CU)
 
 // xcp_tune knob 2: 0 = 128x128 tile / 2-stage ring, 1 = 256x128 / 3-stage,
 // 2 = auto (256x256 8-wave kernel for dense bf16 with >= 256 tiles and K >= 384, else 128x128),
@@ -879,10 +1163,29 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (g_nt_cfg >= 2 && dtype == XCP_BF16 && gmode == 0) {
+    static const int cus = [] {
+      int d = 0, n = 0;
+      if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+        n = 0;
+      return n > 0 ? n : 256;
+    }();
+    g_num_cus = cus;
     const int tiles = xcp_cdiv(M, 256) * xcp_cdiv(N, 256);
     if ((tiles >= 256 && K >= 384) || g_nt_cfg == 3) {
-      if (g_nt256_var == 1) hipLaunchKernelGGL((gemm_nt256k64_kernel<false>), dim3(tiles), dim3(512), 0, stream, a);
-      else hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);
+      const bool fits31 = (long)M * lda < (1L << 31) && (long)N * ldb < (1L << 31);
+      if ((g_nt256_var == 0 || g_nt256_var >= 7) && fits31) {
+        const int cap = g_nt_grid > 0 ? g_nt_grid : g_num_cus;
+        const int grid = tiles < cap ? tiles : cap;
+        if (g_nt256_var == 7) hipLaunchKernelGGL((gemm_nt256p_kernel<false>), dim3(grid), dim3(512), 0, stream, a);
+        else if (g_nt256_var == 8) hipLaunchKernelGGL((gemm_nt256p_kernel<true, 1>), dim3(grid), dim3(512), 0, stream, a);
+        else if (g_nt256_var == 9) hipLaunchKernelGGL((gemm_nt256p_kernel<true, 2>), dim3(grid), dim3(512), 0, stream, a);
+        else if (g_nt256_var == 10) hipLaunchKernelGGL((gemm_nt256p_kernel<true, 3>), dim3(grid), dim3(512), 0, stream, a);
+        else hipLaunchKernelGGL((gemm_nt256p_kernel<true>), dim3(grid), dim3(512), 0, stream, a);
+      } else if (g_nt256_var == 1) hipLaunchKernelGGL((gemm_nt256k64_kernel<false>), dim3(tiles), dim3(512), 0, stream, a);
+      else if (g_nt256_var >= 7) hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);
+      else if (g_nt256_var == 2) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 1>), dim3(tiles), dim3(512), 0, stream, a);
+      else if (g_nt256_var == 3) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 2>), dim3(tiles), dim3(512), 0, stream, a);
+      else hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);   // var 4
       return (int)hipGetLastError();
     }
   }
@@ -925,7 +1228,13 @@ int xcp_internal_tn_tune(int knob, int v) {
 
 int xcp_internal_gemm_var(int v) {
   const int old = g_nt256_var;
-  if (v == 0 || v == 1 || v == 5 || v == 6) g_nt256_var = v;
+  if (v >= 0 && v <= 10) g_nt256_var = v;
+  return old;
+}
+
+int xcp_internal_nt_grid(int v) {
+  const int old = g_nt_grid;
+  if (v >= 0 && v <= 4096) g_nt_grid = v;
   return old;
 }
 

@@ -56,11 +56,13 @@ def test_gemm_nt_stats(ops, gpu, dt, M, N, K):
 
 @pytest.mark.parametrize("M,N,K,lda", [(256, 256, 32, 32), (1000, 728, 728, 728), (300, 2048, 1536, 1536),
                                        (77, 64, 288, 288), (513, 264, 40, 40), (92416 // 8, 728, 728, 736),
-                                       (4100, 1024, 728, 1456)])
-@pytest.mark.parametrize("var", [0, 1])
+                                       (4100, 1024, 728, 1456), (46208, 728, 728, 736), (77073, 264, 40, 40)])
+@pytest.mark.parametrize("var", [0, 7, 4, 1])
 def test_gemm_nt256_stats(ops, gpu, M, N, K, lda, var):
-    """The 256x256 8-wave bf16 kernel (forced for every size): ragged M / N, K tails
-    (K % 32 != 0), a row pitch wider than K, and the 128-row stats partial layout."""
+    """The 256x256 8-wave bf16 kernels (forced for every size; knob 3: 0 / 7 persistent,
+    staggered / lockstep wave groups; 4 / 1 one tile per workgroup): ragged M / N, K tails
+    (K % 32 != 0, K <= 32: a single half-depth K-tile), a row pitch wider than K, several
+    tiles per persistent workgroup (the last two sizes), and the 128-row stats layout."""
     g = torch.Generator(device=gpu).manual_seed(M + N + K)
     Abuf = torch.randn(M, lda, device=gpu, generator=g).bfloat16()
     A = Abuf[:, :K]

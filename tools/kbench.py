@@ -143,6 +143,30 @@ def main():
             W2 = (torch.randn(C, 1456, device=dev, generator=g) / 27).to(dt)
             rep(f"gemm256 var={var} K=1456", timeit(lambda: ops.gemm_nt(A2, W2, Y, M, C, 1456)), flops=2.0 * M * C * 1456)
             ops._lib.call("xcp_tune", 3, old)
+    if "epi" in sel:
+        st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
+        for var in (0, 8, 9, 10, 4, 2, 3):
+            old = ops._lib.call("xcp_tune", 3, var)
+            rep(f"gemm256 var={var} +stats", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=st2)),
+                flops=2.0 * M * C * C)
+            ops._lib.call("xcp_tune", 3, old)
+    if "pgrid" in sel:
+        for var in (10, 0):
+            old = ops._lib.call("xcp_tune", 3, var)
+            for gsz in (256, 248, 240, 192, 128):
+                oldg = ops._lib.call("xcp_tune", 10, gsz)
+                rep(f"gemm256p var={var} grid={gsz}", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C)),
+                    flops=2.0 * M * C * C)
+                ops._lib.call("xcp_tune", 10, oldg)
+            ops._lib.call("xcp_tune", 3, old)
+    if "blas" in sel:
+        rep("hipBLASLt X @ Wp^T 728x728", timeit(lambda: torch.matmul(X, Wp.t())), flops=2.0 * M * C * C)
+        rep("hipBLASLt D^T @ X 728x728", timeit(lambda: torch.matmul(D.t(), X)), flops=2.0 * M * C * C)
+        W7 = torch.randn(768, 768, device=dev, generator=g).to(dt)
+        X7 = torch.randn(M, 768, device=dev, generator=g).to(dt)
+        rep("hipBLASLt 768x768", timeit(lambda: torch.matmul(X7, W7.t())), flops=2.0 * M * 768 * 768)
+        X8 = torch.randn(8192, 8192, device=dev, generator=g).to(dt)
+        rep("hipBLASLt 8192^3", timeit(lambda: torch.matmul(X8, X8), iters=10), flops=2.0 * 8192 ** 3)
     if "gemmk" in sel:
         for cfg in (0, 2):
             old = ops._lib.call("xcp_tune", 2, cfg)
