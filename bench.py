@@ -123,7 +123,7 @@ def main():
     model = model.to(dev).train()
     params = [p for p in model.parameters() if p.requires_grad]
     buckets = ddp.GradBuckets(params, world=world)
-    opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4)
+    opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4, fused=True)   # one fused launch per step
     crit = nn.BCELoss()
 
     B, T, S = args.batch, args.frames, args.size

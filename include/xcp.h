@@ -83,8 +83,18 @@ int xcp_colreduce_f64(const float* in, int S, long L, double* out, int G, xcp_st
 int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, xcp_stream_t stream);
 int xcp_chanred_parts(long rows, int C);
 int xcp_row_stats(int dtype, const void* X, long rows, int C, float* part, xcp_stream_t stream);
-int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd, long rows, int C,
-                      float* part, xcp_stream_t stream);
+/* ms / mt (both null, or both set): scale / shift of the BN when dZ is the gradient of
+ * relu(bn(Y)) -- the ReLU mask (Y*ms+mt > 0) is applied on the fly (replaces xcp_relu_bwd) */
+int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd,
+                      const float* ms, const float* mt, long rows, int C, float* part, xcp_stream_t stream);
+/* train-mode finalize straight from fp32 partial rows part[R][2][C] (sum, sum of squares /
+ * sum dz, sum dz*zhat); fp64 accumulation; replaces colreduce_f64 + the two entries below */
+int xcp_bn_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* beta,
+                         float* rmean, float* rvar, float momentum, float eps, float* mean_o, float* invstd_o,
+                         float* scale_o, float* shift_o, xcp_stream_t stream);
+int xcp_bn_bwd_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* mean,
+                             const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma,
+                             float* dbeta, xcp_stream_t stream);
 int xcp_bn_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* beta, float* rmean,
                     float* rvar, float momentum, float eps, int train, float* mean, float* invstd, float* scale,
                     float* shift, xcp_stream_t stream);
@@ -94,7 +104,7 @@ int xcp_bn_bwd_finalize(const double* part2, int G, int C, double count, const f
 int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, long rows, int C,
                xcp_stream_t stream);
 int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const float* alpha, const float* bcoef,
-                     const float* delta, long rows, int C, xcp_stream_t stream);
+                     const float* delta, const float* ms, const float* mt, long rows, int C, xcp_stream_t stream);
 int xcp_relu_bwd(int dtype, void* dX, const void* X, long rows, int C, xcp_stream_t stream);
 /* Block tail (Xception.py:86,:93-98): Out = [maxpool3x3s2p1](Y*s1+t1) + (s2 ? S*s2+t2 : S) */
 int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int pool, const void* S, const float* s2,
@@ -113,6 +123,10 @@ int xcp_conv1_wgrad_parts(int N, int IH, int IW);
 int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int N, int IH, int IW, xcp_stream_t stream);
 int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int d2, int p0, int p1, int p2,
                  xcp_stream_t stream);
+
+/* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][10] int64
+ * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block), nblocks in total */
+int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream_t stream);
 
 /* ---- LSTM recurrence (nn.LSTM, XceptionLSTMV.py:18-23, :67) ----
  * whh is W_hh [4H][H] as nn.LSTM stores it (weight_hh_l0); whhT ([H][4H]) is read only by the

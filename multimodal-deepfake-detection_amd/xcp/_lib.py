@@ -31,11 +31,13 @@ SIGNATURES = {
     "xcp_colreduce_f32": [P, I, L, P, I, P],
     "xcp_chanred_parts": [L, I],
     "xcp_row_stats": [I, P, L, I, P, P],
-    "xcp_bn_bwd_reduce": [I, P, P, P, P, L, I, P, P],
+    "xcp_bn_bwd_reduce": [I, P, P, P, P, P, P, L, I, P, P],
+    "xcp_bn_finalize_part": [P, I, I, D, P, P, P, P, F, F, P, P, P, P, P],
+    "xcp_bn_bwd_finalize_part": [P, I, I, D, P, P, P, P, P, P, P, P, P],
     "xcp_bn_finalize": [P, I, I, D, P, P, P, P, F, F, I, P, P, P, P, P],
     "xcp_bn_bwd_finalize": [P, I, I, D, P, P, P, P, P, P, P, P, I, P],
     "xcp_bn_act": [I, P, P, P, P, I, L, I, P],
-    "xcp_bn_bwd_apply": [I, P, P, P, P, P, P, L, I, P],
+    "xcp_bn_bwd_apply": [I, P, P, P, P, P, P, P, P, L, I, P],
     "xcp_relu_bwd": [I, P, P, L, I, P],
     "xcp_tail_fwd": [I, P, P, P, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_maxpool_bwd": [I, P, P, P, I, I, I, I, P],
@@ -45,6 +47,7 @@ SIGNATURES = {
     "xcp_conv1_wgrad_parts": [I, I, I],
     "xcp_conv1_wgrad": [I, P, P, P, I, I, I, P],
     "xcp_permute3": [I, P, P, I, I, I, I, I, I, P],
+    "xcp_permute3_batch": [P, I, I, P],
     "xcp_lstm_needs_whhT": [I],
     "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
     "xcp_lstm_bwd": [P, P, P, P, P, P, P, I, I, I, P],

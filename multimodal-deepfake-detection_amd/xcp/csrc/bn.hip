@@ -82,9 +82,12 @@ XCP_DEV void chanred_finish(const ChanRed& r, float (*acc)[CPT], float* part, in
 }
 
 // MODE 0: (x, x^2) of rows of X.  MODE 1: (dz, dz*yhat), yhat = (y-mean)*invstd.
+// MODE 2: MODE 1 with dz masked by the ReLU that followed the BN (y*ms+mt > 0), i.e. the
+// gradient w.r.t. relu(bn(y)) given; the mask is recomputed from y, never read.
 template <typename T, int MODE, int CPT>
 __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av, const void* Bv, const float* mean,
-                                                      const float* invstd, float* part) {
+                                                      const float* invstd, const float* ms, const float* mt,
+                                                      float* part) {
   const int cchunk = blockIdx.x % r.nch, pchunk = blockIdx.x / r.nch;
   const int lcv = threadIdx.x % r.CVB, slot = threadIdx.x / r.CVB;
   const int cv = cchunk * r.CVB + lcv;
@@ -95,10 +98,14 @@ __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av,
 #pragma unroll
   for (int j = 0; j < CPT; ++j) acc[0][j] = acc[1][j] = 0.f;
   if (slot < r.SPB && cv < r.CV) {
-    float mu[CPT], is[CPT];
-    if constexpr (MODE == 1) {
+    float mu[CPT], is[CPT], sm[CPT], tm[CPT];
+    if constexpr (MODE >= 1) {
       VecIO<float, CPT>::load(mean + c0, mu);
       VecIO<float, CPT>::load(invstd + c0, is);
+    }
+    if constexpr (MODE == 2) {
+      VecIO<float, CPT>::load(ms + c0, sm);
+      VecIO<float, CPT>::load(mt + c0, tm);
     }
     const long rb = (long)pchunk * r.rows_per_chunk, re = min(r.rows, rb + r.rows_per_chunk);
     for (long p = rb + slot; p < re; p += r.SPB) {
@@ -113,6 +120,10 @@ __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av,
       } else {
         float b[CPT];
         VecIO<T, CPT>::load(B + p * r.C + c0, b);
+        if constexpr (MODE == 2) {
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) a[j] = fmaf(b[j], sm[j], tm[j]) > 0.f ? a[j] : 0.f;
+        }
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
           acc[0][j] += a[j];
@@ -180,6 +191,89 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ part2, int G, 
   }
 }
 
+// Fused reduction + finalize straight from the fp32 partial rows part[R][2][C] (the GEMM
+// epilogue's / the fused depthwise backward's per-chunk sums), replacing colreduce_f64 +
+// *_finalize: one 1024-thread workgroup per 32 channels; lane l of wave w sums statistic
+// l>>5 of channel l&31 over rows w, w+16, ... in fp64 (four independent accumulators, so
+// many loads stay in flight), the 16 waves fold in LDS, and 32 threads finalize.
+constexpr int FIN_CH = 32, FIN_WAVES = 16;
+
+XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int c0, double (*red)[64], double& s0,
+                        double& s1) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = c0 + (lane & 31), stat = lane >> 5;
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C) {
+    const float* col = part + (long)stat * C + c;
+    int r = w;
+    for (; r + 3 * FIN_WAVES < R; r += 4 * FIN_WAVES) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += (double)col[(long)(r + u * FIN_WAVES) * 2 * C];
+    }
+    for (; r < R; r += FIN_WAVES) a[0] += (double)col[(long)r * 2 * C];
+  }
+  red[w][lane] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  s0 = s1 = 0.0;
+  if (threadIdx.x < FIN_CH) {
+#pragma unroll
+    for (int q = 0; q < FIN_WAVES; ++q) {
+      s0 += red[q][threadIdx.x];
+      s1 += red[q][threadIdx.x + 32];
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C,
+                                                                double count, const float* gamma, const float* beta,
+                                                                float* rmean, float* rvar, float momentum, float eps,
+                                                                float* mean_o, float* invstd_o, float* scale_o,
+                                                                float* shift_o) {
+  __shared__ double red[FIN_WAVES][64];
+  const int c0 = blockIdx.x * FIN_CH;
+  double s, q;
+  fin_reduce(part, R, C, c0, red, s, q);
+  const int c = c0 + threadIdx.x;
+  if (threadIdx.x >= FIN_CH || c >= C) return;
+  const double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  if (rmean) {
+    const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+  }
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * is;
+  mean_o[c] = (float)mean;
+  invstd_o[c] = is;
+  scale_o[c] = sc;
+  shift_o[c] = beta[c] - (float)mean * sc;
+}
+
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_part_kernel(const float* __restrict__ part, int R, int C,
+                                                                    double count, const float* gamma,
+                                                                    const float* mean, const float* invstd,
+                                                                    float* alpha, float* bcoef, float* delta,
+                                                                    float* dgamma, float* dbeta) {
+  __shared__ double red[FIN_WAVES][64];
+  const int c0 = blockIdx.x * FIN_CH;
+  double sdz, sdzy;
+  fin_reduce(part, R, C, c0, red, sdz, sdzy);
+  const int c = c0 + threadIdx.x;
+  if (threadIdx.x >= FIN_CH || c >= C) return;
+  const double is = invstd[c], gm = gamma[c], mu = mean[c];
+  const double a = gm * is;
+  const double mdz = sdz / count, mdzy = sdzy / count;
+  alpha[c] = (float)a;
+  bcoef[c] = (float)(-a * is * mdzy);
+  delta[c] = (float)(-a * mdz + a * is * mu * mdzy);
+  if (dgamma) {
+    dgamma[c] = (float)sdzy;
+    dbeta[c] = (float)sdz;
+  }
+}
+
 // ---------------------------------------------------------------- elementwise
 template <typename T, int CPT>
 __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ X, T* __restrict__ Y, const float* scale,
@@ -202,10 +296,10 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ X, T*
 }
 
 // dy = alpha*dz + bcoef*y + delta
-template <typename T, int CPT>
+template <typename T, int CPT, bool MASK>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dZ, const T* __restrict__ Yv, T* dY,
                                                            const float* alpha, const float* bcoef, const float* delta,
-                                                           long rows, int C) {
+                                                           const float* ms, const float* mt, long rows, int C) {
   const int CV = C / CPT;
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
   if (g >= rows * CV) return;
@@ -217,6 +311,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   VecIO<float, CPT>::load(alpha + c0, al);
   VecIO<float, CPT>::load(bcoef + c0, bc);
   VecIO<float, CPT>::load(delta + c0, de);
+  if constexpr (MASK) {   // dZ is the gradient of relu(bn(y)): mask recomputed from y
+    float sm[CPT], tm[CPT];
+    VecIO<float, CPT>::load(ms + c0, sm);
+    VecIO<float, CPT>::load(mt + c0, tm);
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) dz[j] = fmaf(y[j], sm[j], tm[j]) > 0.f ? dz[j] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < CPT; ++j) dz[j] = fmaf(al[j], dz[j], fmaf(bc[j], y[j], de[j]));
   VecIO<T, CPT>::store(dY + p * C + c0, dz);
@@ -375,13 +476,13 @@ inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
 template <typename T, int MODE>
 int chanred_launch(long rows, int C, const void* A, const void* B, const float* mean, const float* invstd, float* part,
-                   hipStream_t st) {
+                   hipStream_t st, const float* ms = nullptr, const float* mt = nullptr) {
   constexpr int CPT = 8;
   ChanRed r = make_chanred(rows, C, CPT, 1024);
   const long P = chanred_P(r);
   const size_t smem = (size_t)r.SPB * 2 * r.CVB * CPT * sizeof(float);
   hipLaunchKernelGGL((chanred_kernel<T, MODE, CPT>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, A, B, mean,
-                     invstd, part);
+                     invstd, ms, mt, part);
   return (int)hipGetLastError();
 }
 
@@ -420,12 +521,40 @@ int xcp_row_stats(int dtype, const void* X, long rows, int C, float* part, hipSt
 }
 
 // part[P][2][C] = per-chunk (sum dz, sum dz*(y-mean)*invstd)
-int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd, long rows, int C,
-                      float* part, hipStream_t st) {
+// ms / mt (may be null): affine of the BN whose ReLU'd output dZ is the gradient of
+int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd, const float* ms,
+                      const float* mt, long rows, int C, float* part, hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
+  if ((ms == nullptr) != (mt == nullptr)) return XCP_EINVAL;
+  if (ms) {
+    if (dtype == XCP_BF16) return chanred_launch<bf16, 2>(rows, C, dZ, Y, mean, invstd, part, st, ms, mt);
+    if (dtype == XCP_F32) return chanred_launch<float, 2>(rows, C, dZ, Y, mean, invstd, part, st, ms, mt);
+    return XCP_EUNSUPPORTED;
+  }
   if (dtype == XCP_BF16) return chanred_launch<bf16, 1>(rows, C, dZ, Y, mean, invstd, part, st);
   if (dtype == XCP_F32) return chanred_launch<float, 1>(rows, C, dZ, Y, mean, invstd, part, st);
   return XCP_EUNSUPPORTED;
+}
+
+// BatchNorm finalize straight from fp32 partial rows part[R][2][C] (train mode)
+int xcp_bn_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* beta,
+                         float* rmean, float* rvar, float momentum, float eps, float* mean_o, float* invstd_o,
+                         float* scale_o, float* shift_o, hipStream_t st) {
+  if (C <= 0) return XCP_OK;
+  if (R <= 0) return XCP_EINVAL;
+  hipLaunchKernelGGL(bn_finalize_part_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part, R, C,
+                     count, gamma, beta, rmean, rvar, momentum, eps, mean_o, invstd_o, scale_o, shift_o);
+  return (int)hipGetLastError();
+}
+
+int xcp_bn_bwd_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* mean,
+                             const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
+                             hipStream_t st) {
+  if (C <= 0) return XCP_OK;
+  if (R <= 0) return XCP_EINVAL;
+  hipLaunchKernelGGL(bn_bwd_finalize_part_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part,
+                     R, C, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta);
+  return (int)hipGetLastError();
 }
 
 int xcp_bn_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* beta, float* rmean,
@@ -460,16 +589,21 @@ int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const floa
 }
 
 int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const float* alpha, const float* bcoef,
-                     const float* delta, long rows, int C, hipStream_t st) {
+                     const float* delta, const float* ms, const float* mt, long rows, int C, hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
+  if ((ms == nullptr) != (mt == nullptr)) return XCP_EINVAL;
   const unsigned g = nblk(rows * (C / 8));
-  if (dtype == XCP_BF16)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)dZ, (const bf16*)Y,
-                       (bf16*)dY, alpha, bcoef, delta, rows, C);
-  else if (dtype == XCP_F32)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)dZ, (const float*)Y,
-                       (float*)dY, alpha, bcoef, delta, rows, C);
-  else
+#define XCP_APPLY(TT, MK)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, 8, MK>), dim3(g), dim3(256), 0, st, (const TT*)dZ, (const TT*)Y,  \
+                     (TT*)dY, alpha, bcoef, delta, ms, mt, rows, C)
+  if (dtype == XCP_BF16) {
+    if (ms) XCP_APPLY(bf16, true);
+    else XCP_APPLY(bf16, false);
+  } else if (dtype == XCP_F32) {
+    if (ms) XCP_APPLY(float, true);
+    else XCP_APPLY(float, false);
+  } else
+#undef XCP_APPLY
     return XCP_EUNSUPPORTED;
   return (int)hipGetLastError();
 }

@@ -120,6 +120,37 @@ __global__ __launch_bounds__(256) void permute3_kernel(const float* __restrict__
   out[g] = from_f<TO>(in[((long)idx[0] * d1 + idx[1]) * d2 + idx[2]]);
 }
 
+// Many permute3 jobs in one launch (the per-step weight packing of every layer).  jobs is a
+// device array of [njobs][10] int64: in, out, d0, d1, d2, p0, p1, p2, out dtype, first block.
+// Workgroup b finds its job by binary search over the first-block column (uniform per block).
+__global__ __launch_bounds__(256) void permute3_batch_kernel(const long long* __restrict__ jobs, int njobs) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[(long)mid * 10 + 9] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const long long* j = jobs + (long)lo * 10;
+  const float* in = reinterpret_cast<const float*>(j[0]);
+  const int d0 = (int)j[2], d1 = (int)j[3], d2 = (int)j[4], p0 = (int)j[5], p1 = (int)j[6], p2 = (int)j[7];
+  const long total = (long)d0 * d1 * d2;
+  const long g = (long)(b - (int)j[9]) * 256 + threadIdx.x;
+  if (g >= total) return;
+  const int dims[3] = {d0, d1, d2};
+  const int od1 = dims[p1], od2 = dims[p2];
+  const int o2 = (int)(g % od2);
+  const long t = g / od2;
+  const int o1 = (int)(t % od1);
+  const int o0 = (int)(t / od1);
+  int idx[3];
+  idx[p0] = o0;
+  idx[p1] = o1;
+  idx[p2] = o2;
+  const float v = in[((long)idx[0] * d1 + idx[1]) * d2 + idx[2]];
+  if (j[8] == XCP_BF16) reinterpret_cast<bf16*>(j[1])[g] = (bf16)v;
+  else reinterpret_cast<float*>(j[1])[g] = v;
+}
 
 // ---------------------------------------------------------------------------------
 // Tiled conv1 (default).  The per-pixel kernels above re-read each input value ~9x
@@ -404,6 +435,14 @@ int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int 
     hipLaunchKernelGGL(permute3_kernel<float>, dim3(g), dim3(256), 0, st, in, (float*)out, d0, d1, d2, p0, p1, p2);
   else
     return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+// njobs permute3 jobs ([njobs][10] int64 on the device, see permute3_batch_kernel) covering
+// nblocks 256-element blocks in total; the host validates the permutations when it builds them
+int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, hipStream_t st) {
+  if (njobs <= 0 || nblocks <= 0) return XCP_OK;
+  hipLaunchKernelGGL(permute3_batch_kernel, dim3(nblocks), dim3(256), 0, st, jobs, njobs);
   return (int)hipGetLastError();
 }
 

@@ -111,6 +111,8 @@ class XceptionEngine:
         self._pack_key = None
         self._packed = {}
         self._packed_bwd_key = None
+        self._bufs = {}
+        self._pack_fwd, self._pack_bwd = ops.PermuteBatch(), ops.PermuteBatch()
 
     # ------------------------------------------------------------ parameters
     def named_params(self):
@@ -120,60 +122,64 @@ class XceptionEngine:
     def _version_key(self):
         return tuple((p.data_ptr(), p._version) for _, p in self.named_params()) + (self.dtype,)
 
+    def _buf(self, name, n, dtype, dev):
+        """Persistent packed-weight buffer (re-used every step, so the batched pack's job
+        table stays valid)."""
+        t = self._bufs.get(name)
+        if t is None or t.numel() != n or t.dtype != dtype or t.device != dev:
+            t = self._bufs[name] = torch.empty(n, device=dev, dtype=dtype)
+        return t
+
     def pack(self):
+        """Weights in kernel layouts (bf16 / fp32 pointwise [co][ci], depthwise taps [9][C],
+        conv2 [co][tap][ci]), all repacked by one batched launch when a parameter changed."""
         key = self._version_key()
         if key == self._pack_key:
             return self._packed
-        dt, pk = self.dtype, {}
+        dt, pk, jobs = self.dtype, {}, []
         m = self.model
         dev = m.conv1.weight.device
 
-        def pw(conv):
-            co, ci = conv.out_channels, conv.in_channels
-            out = torch.empty(co * ci, device=dev, dtype=dt)
-            ops.permute3(conv.weight.detach(), out, co, ci, 1, (0, 1, 2))
-            return out
-
-        def dw(conv):
-            c = conv.in_channels
-            out = torch.empty(9 * c, device=dev, dtype=torch.float32)
-            ops.permute3(conv.weight.detach(), out, c, 9, 1, (1, 0, 2))
-            return out
+        def add(name, w, n_dtype, d0, d1, d2, perm):
+            out = self._buf(name, d0 * d1 * d2, n_dtype, dev)
+            jobs.append((w.detach(), out, d0, d1, d2, perm))
+            pk[name] = out
 
         for u in self._all_units():
-            pk[u.name + ".dw"] = dw(u.sep.conv1)
-            pk[u.name + ".pw"] = pw(u.sep.pointwise)
+            c = u.sep.conv1.in_channels
+            add(u.name + ".dw", u.sep.conv1.weight, torch.float32, c, 9, 1, (1, 0, 2))
+            pw = u.sep.pointwise
+            add(u.name + ".pw", pw.weight, dt, pw.out_channels, pw.in_channels, 1, (0, 1, 2))
         for b in self.blocks:
             if b.skip is not None:
-                pk[b.name + ".skip"] = pw(b.skip)
-        w2 = torch.empty(64 * 9 * 32, device=dev, dtype=dt)
-        ops.permute3(m.conv2.weight.detach(), w2, 64, 32, 9, (0, 2, 1))   # [co][tap][ci]
-        pk["conv2"] = w2
+                add(b.name + ".skip", b.skip.weight, dt, b.skip.out_channels, b.skip.in_channels, 1, (0, 1, 2))
+        add("conv2", m.conv2.weight, dt, 64, 32, 9, (0, 2, 1))   # [co][tap][ci]
+        self._pack_fwd.run(jobs)
         self._packed, self._pack_key = pk, key
         self._packed_bwd_key = None
         return pk
 
     def pack_bwd(self):
-        """Transposed weights for the input-gradient GEMMs."""
+        """Transposed weights for the input-gradient GEMMs (one batched launch)."""
         if self._packed_bwd_key == self._pack_key and self._pack_key is not None:
             return self._packed
         pk, dt, m = self._packed, self.dtype, self.model
         dev = m.conv1.weight.device
+        jobs = []
 
-        def pwT(conv):
-            co, ci = conv.out_channels, conv.in_channels
-            out = torch.empty(co * ci, device=dev, dtype=dt)
-            ops.permute3(conv.weight.detach(), out, co, ci, 1, (1, 0, 2))
-            return out
+        def add(name, w, d0, d1, d2, perm):
+            out = self._buf(name, d0 * d1 * d2, dt, dev)
+            jobs.append((w.detach(), out, d0, d1, d2, perm))
+            pk[name] = out
 
         for u in self._all_units():
-            pk[u.name + ".pwT"] = pwT(u.sep.pointwise)
+            pw = u.sep.pointwise
+            add(u.name + ".pwT", pw.weight, pw.out_channels, pw.in_channels, 1, (1, 0, 2))
         for b in self.blocks:
             if b.skip is not None:
-                pk[b.name + ".skipT"] = pwT(b.skip)
-        w2t = torch.empty(32 * 9 * 64, device=dev, dtype=dt)
-        ops.permute3(m.conv2.weight.detach(), w2t, 64, 32, 9, (1, 2, 0))  # [ci][tap][co]
-        pk["conv2T"] = w2t
+                add(b.name + ".skipT", b.skip.weight, b.skip.out_channels, b.skip.in_channels, 1, (1, 0, 2))
+        add("conv2T", m.conv2.weight, 64, 32, 9, (1, 2, 0))   # [ci][tap][co]
+        self._pack_bwd.run(jobs)
         self._packed_bwd_key = self._pack_key
         return pk
 
@@ -311,11 +317,11 @@ class XceptionEngine:
             grads[name] = t
             return t
 
-        def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None):
+        def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
             dY = self._empty(rows * C)
             P = part[1] if part is not None else 0
             ops.bn_backward(dZ, Y, rows, C, _bn_ref(bnmod), st, dY, g(name + ".weight", (C,)), g(name + ".bias", (C,)),
-                            part=part[0] if part is not None else None, R=P)
+                            part=part[0] if part is not None else None, R=P, relu=relu)
             return dY
 
         def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None):
@@ -350,15 +356,13 @@ class XceptionEngine:
         # ---- stem
         OH1, OW1, OH2, OW2 = S["OH1"], S["OW1"], S["OH2"], S["OW2"]
         rows1, rows2 = N * OH1 * OW1, N * OH2 * OW2
-        ops.relu_bwd(dX, S["sout"], rows2, 64)
-        dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"])
+        dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"], relu=True)   # relu (Xception.py:174) fused
         dA1 = self._empty(rows1 * 32)
         ops.gemm_nt(dC2, pk["conv2T"], dA1, rows1, 32, 576, lda=64, gather=(3, OH1, OW1, OH2, OW2, 1, 64))
         w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
         ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
         ops.permute3(w2g, g("conv2.weight", (64, 32, 3, 3)), 64, 9, 32, (0, 2, 1))
-        ops.relu_bwd(dA1, S["a1"], rows1, 32)
-        dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"])
+        dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], relu=True)   # relu (Xception.py:170) fused
         ops.conv1_wgrad(S["x"], dC1, g("conv1.weight", (32, 3, 3, 3)), N, S["IH"], S["IW"])
         return grads
 

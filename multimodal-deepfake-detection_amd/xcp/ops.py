@@ -147,17 +147,30 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
 
 
 # ---------------------------------------------------------------- batchnorm
-STAT_GROUPS = 64
+
+
+FIN_MAX_ROWS = 2048   # above this many partial rows, pre-reduce to FIN_GROUPS rows (fp64 sums, fp32 out)
+FIN_GROUPS = 256
+
+
+def _fold(part, R, C):
+    if R <= FIN_MAX_ROWS:
+        return part, R
+    p2 = torch.empty(FIN_GROUPS * 2 * C, device=part.device, dtype=torch.float32)
+    colreduce_f32(part, R, 2 * C, p2, FIN_GROUPS)
+    return p2, FIN_GROUPS
 
 
 def finalize_stats(part, R, C, count, bn, train, out):
     """part: fp32 [R][2][C] partial sums -> out dict of mean/invstd/scale/shift (fp32 [C]).
-    Updates bn running stats in place when train."""
-    dev = part.device
-    G = min(STAT_GROUPS, R)
-    p2 = torch.empty(G * 2 * C, device=dev, dtype=torch.float64)
-    colreduce_f64(part, R, 2 * C, p2, G)
-    _bn_finalize(p2, G, C, count, bn, train, out)
+    Updates bn running stats in place (train mode batch statistics)."""
+    if not train:
+        raise ValueError("finalize_stats computes batch statistics (train mode); use eval_stats")
+    track = bn["track"]
+    part, R = _fold(part, R, C)
+    _lib.call("xcp_bn_finalize_part", _p(part), R, C, float(count), _p(bn["weight"]), _p(bn["bias"]),
+              _p(bn["running_mean"]) if track else 0, _p(bn["running_var"]) if track else 0, float(bn["momentum"]),
+              float(bn["eps"]), _p(out["mean"]), _p(out["invstd"]), _p(out["scale"]), _p(out["shift"]), stream())
 
 
 def _bn_finalize(p2, G, C, count, bn, train, out):
@@ -180,23 +193,25 @@ def row_stats(X, rows, C):
     return part, R
 
 
-def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0):
+def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=False):
     """dY = BatchNorm2d backward (train-mode batch stats) of dZ; writes dgamma/dbeta.
     ``part`` ([R][2][C] partial (sum dz, sum dz*zhat)) may come fused from the
-    producer of dZ; otherwise it is reduced here."""
+    producer of dZ; otherwise it is reduced here.  relu=True: dZ is the gradient of
+    relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift)."""
+    ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
     if part is None:
         R = _lib.call("xcp_chanred_parts", rows, C)
         part = torch.empty(R * 2 * C, device=dZ.device, dtype=torch.float32)
-        _lib.call("xcp_bn_bwd_reduce", DT[dZ.dtype], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), rows, C,
-                  _p(part), stream())
-    G = min(STAT_GROUPS, R)
-    p2 = torch.empty(G * 2 * C, device=dZ.device, dtype=torch.float64)
-    colreduce_f64(part, R, 2 * C, p2, G)
+        _lib.call("xcp_bn_bwd_reduce", DT[dZ.dtype], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), ms, mt, rows,
+                  C, _p(part), stream())
+    elif relu:
+        raise ValueError("a fused partial cannot carry the ReLU mask")
     coef = torch.empty(3 * C, device=dZ.device, dtype=torch.float32)
-    _lib.call("xcp_bn_bwd_finalize", _p(p2), G, C, float(rows), _p(bn["weight"]), _p(st["mean"]), _p(st["invstd"]),
-              _p(coef), _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta), 0, stream())
-    _lib.call("xcp_bn_bwd_apply", DT[dZ.dtype], _p(dZ), _p(Y), _p(dY), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), rows,
-              C, stream())
+    part, R = _fold(part, R, C)
+    _lib.call("xcp_bn_bwd_finalize_part", _p(part), R, C, float(rows), _p(bn["weight"]), _p(st["mean"]),
+              _p(st["invstd"]), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta), stream())
+    _lib.call("xcp_bn_bwd_apply", DT[dZ.dtype], _p(dZ), _p(Y), _p(dY), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), ms,
+              mt, rows, C, stream())
 
 
 def bn_act(X, Y, scale, shift, relu, rows, C):
@@ -238,6 +253,33 @@ def conv1_wgrad(X, dY, out, N, IH, IW):
 
 def permute3(inp, out, d0, d1, d2, perm):
     _lib.call("xcp_permute3", DT[out.dtype], _p(inp), _p(out), d0, d1, d2, perm[0], perm[1], perm[2], stream())
+
+
+class PermuteBatch:
+    """A fixed list of permute3 jobs (fp32 source -> packed destination) run as one launch.
+    The device job table is rebuilt only when a source or destination pointer changes."""
+
+    def __init__(self):
+        self._key = None
+        self._table = None
+        self._nblocks = 0
+
+    def run(self, jobs):
+        """jobs: list of (src fp32 tensor, dst tensor, d0, d1, d2, perm)."""
+        key = tuple((s.data_ptr(), d.data_ptr(), d0, d1, d2, tuple(pm), d.dtype) for s, d, d0, d1, d2, pm in jobs)
+        if key != self._key:
+            rows, blk = [], 0
+            for s, d, d0, d1, d2, pm in jobs:
+                n = d0 * d1 * d2
+                if sorted(pm) != [0, 1, 2] or s.numel() != n or d.numel() != n or s.dtype != torch.float32 \
+                        or not s.is_contiguous() or not d.is_contiguous():
+                    raise ValueError("permute job: bad permutation, size, dtype or layout")
+                check_gpu(s, d)
+                rows.append([s.data_ptr(), d.data_ptr(), d0, d1, d2, pm[0], pm[1], pm[2], DT[d.dtype], blk])
+                blk += (n + 255) // 256
+            self._table = torch.tensor(rows, dtype=torch.int64).to(jobs[0][1].device)
+            self._nblocks, self._key = blk, key
+        _lib.call("xcp_permute3_batch", _p(self._table), len(jobs), self._nblocks, stream())
 
 
 # ---------------------------------------------------------------- LSTM

@@ -226,9 +226,12 @@ def test_dw_bwd_residual_and_skip(ops, gpu, dw_family, dt):
     assert rel_err(nchw(out.view(N, H, W, C)).float(), want) < (1e-6 if dt == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("rows,C", [(100000, 128), (3 * 361, 728), (50, 2048)])
-def test_bn_forward_backward(ops, gpu, dt, rows, C):
+def test_bn_forward_backward(ops, gpu, dt, rows, C, relu):
+    """BN statistics / running buffers, apply, and backward; relu=True: the gradient
+    arrives for relu(bn(y)) (stem, Xception.py:170/:174) and the mask is recomputed."""
     from xcp.engine import Stats
     g = torch.Generator(device=gpu).manual_seed(rows)
     y = (torch.randn(rows, C, device=gpu, generator=g) * 2 + 0.7).to(dt)
@@ -249,10 +252,10 @@ def test_bn_forward_backward(ops, gpu, dt, rows, C):
     ops.bn_act(y, zk, st.scale, st.shift, False, rows, C)
     assert rel_err(zk.float(), z) < (1e-6 if dt == torch.float32 else 1e-2)
     dz = torch.randn(rows, C, device=gpu, generator=g).to(dt)
-    z.backward(dz.float())
+    (F.relu(z) if relu else z).backward(dz.float())
     dY = torch.empty(rows, C, device=gpu, dtype=dt)
     dg, db = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
-    ops.bn_backward(dz, y, rows, C, bn, st, dY, dg, db)
+    ops.bn_backward(dz, y, rows, C, bn, st, dY, dg, db, relu=relu)
     assert rel_err(dY.float(), yr.grad) < (1e-4 if dt == torch.float32 else 2e-2)
     torch.testing.assert_close(dg, gamma.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db, beta.grad, rtol=1e-4, atol=1e-3)
