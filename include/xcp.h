@@ -124,6 +124,15 @@ int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int 
 int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int d2, int p0, int p1, int p2,
                  xcp_stream_t stream);
 
+/* ---- stem conv2 (Xception.py:122, :172) as a direct MFMA convolution, bf16 ----
+ * mode 0: Y[N][IH-2][IW-2][64] = conv3x3(X[N][IH][IW][32], W[64][9][32]); stats (may be null):
+ *         BatchNorm partial sums [parts][2][64] of the stored values
+ * mode 1: input gradient: Y[N][IH+2][IW+2][32] from X = dY[N][IH][IW][64], W = [32][9][64]
+ * xcp_conv3x3_parts returns the workgroup count (stats rows), 0 if the width is unsupported */
+int xcp_conv3x3_parts(int mode, int N, int IH, int IW);
+int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, int N, int IH, int IW,
+                xcp_stream_t stream);
+
 /* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][10] int64
  * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block), nblocks in total */
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream_t stream);

@@ -48,6 +48,8 @@ SIGNATURES = {
     "xcp_conv1_wgrad": [I, P, P, P, I, I, I, P],
     "xcp_permute3": [I, P, P, I, I, I, I, I, I, P],
     "xcp_permute3_batch": [P, I, I, P],
+    "xcp_conv3x3_parts": [I, I, I, I],
+    "xcp_conv3x3": [I, P, P, P, P, I, I, I, P],
     "xcp_lstm_needs_whhT": [I],
     "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
     "xcp_lstm_bwd": [P, P, P, P, P, P, P, I, I, I, P],
@@ -55,7 +57,7 @@ SIGNATURES = {
 
 # entry points that return a size, not a status
 SIZE_QUERIES = {"xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts", "xcp_tune",
-                "xcp_lstm_needs_whhT"}
+                "xcp_lstm_needs_whhT", "xcp_conv3x3_parts"}
 
 _lib = None
 

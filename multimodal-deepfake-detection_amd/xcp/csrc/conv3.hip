@@ -1,0 +1,318 @@
+// Stem conv2 (3x3, 32 -> 64, stride 1, pad 0) forward and its input gradient as direct
+// MFMA convolutions over LDS-resident row tiles.
+//
+// Reference op: Xception.conv2 = nn.Conv2d(32, 64, 3, bias=False) (Xception.py:122,
+// called at :172) at 149x149 -> 147x147.  Its backward w.r.t. the input is the same
+// kind of convolution: dA[h][w][ci] = sum dY[h-2+ky][w-2+kx][co] W[co][8-tap][ci] over the
+// zero-padded (pad 2) gradient, i.e. a 64 -> 32 conv with the flipped, transposed kernel.
+// The generic implicit-GEMM path (gemm.hip gather modes 2 / 3) re-reads every input chunk
+// nine times through L2 and wastes half of its 128-wide N tile on 64 / 32 output channels
+// (0.94 / 1.38 ms per call at 256 x 149^2); both directions are HBM-bound
+// (~1.07 GB moved per call, ~195 us at 5.5 TB/s).
+//
+// conv3x3_kernel<CIN, COUT, PAD, TH>: a persistent 512-thread workgroup per CU walks tiles
+// of TH output rows (one frame, all COUT channels); the (TH+2) x (IW+2*PAD) input pixels
+// of the NEXT tile stream into the second of two LDS buffers by LDS-DMA (16-B chunks
+// XOR-swizzled by column through the per-lane source address so the fragment reads below
+// are bank-conflict-free at lane offsets fixed per tap column; image padding reads a zero
+// line).
+// Each wave owns two 16-channel output groups (COUT = 64: waves 0/2 channels 0-31, 1/3
+// channels 32-63) and keeps their kernel slice in VGPRs as MFMA A-fragments (2 x 9 x CIN/32
+// fragments: 72 VGPRs forward, 144 for the 64-deep dgrad) and walks (output row, 16-pixel
+// group) items:
+//   D[16 co][16 px] += W[co][tap][32 ci] x In[32 ci][px + tap]   (v_mfma_f32_16x16x32_bf16)
+// each B-fragment read from LDS feeds 2 MFMAs (18 / 36 MFMAs per item).  Lanes fg / fg^1 (16 apart)
+// swap 8-B pieces of the rounded tile so every lane stores 16 contiguous bytes: one store
+// instruction covers 16 consecutive output pixels x 64 B (the whole row segment for
+// COUT = 32).  With STATS each workgroup writes its BatchNorm partial sums (sum, sum of
+// squares of the stored values) as one row of [wg][2][COUT].  The kernel fragments are
+// loaded once per workgroup.
+#include "common.h"
+
+namespace {
+
+__device__ __attribute__((aligned(64))) uint4 g_czero[4];
+
+// 16-B chunk swizzle of LDS column x (brute-force checked: conflict-free ds_read_b128 for
+// 16 consecutive columns at any row offset); depends on x mod 8 only
+template <int CIN>
+XCP_DEV int cswz(int x) {
+  if constexpr (CIN == 32) return (x >> 1) & 3;
+  else return x & 7;
+}
+
+
+template <int CIN, int COUT, int PAD, int TH, int MAXIW, bool STATS, int NW, bool PIPE, int VAR = 0>
+__global__ __launch_bounds__(NW * 64, 1) void conv3x3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wp,
+                                                         bf16* __restrict__ Y, float* __restrict__ stats, int N,
+                                                         int IH, int IW) {
+  constexpr int CPP = CIN / 8;                // 16-B chunks per pixel
+  constexpr int PB = CPP * 16;                // LDS bytes per pixel
+  constexpr int KS = CIN / 32;                // 32-deep MFMA steps per tap
+  constexpr int CG = 2;                       // output-channel groups per wave
+  constexpr int NCP = COUT / 32;              // channel-group pairs (waves split over them)
+  constexpr int BUF = ((TH + 2) * (MAXIW + 2 * PAD) + 16) * PB;   // + slack for junk columns past OW
+  constexpr int F3 = 3 * KS;                  // B-fragments per pipeline third (9 x KS per item)
+  static_assert(COUT % 32 == 0, "pieces are exchanged between channel-group pairs");
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int OH = IH + 2 * PAD - 2, OW = IW + 2 * PAD - 2, LW = IW + 2 * PAD;
+  const int tiles_h = (OH + TH - 1) / TH, ntiles = N * tiles_h, G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
+  const int wsc = __builtin_amdgcn_readfirstlane(w);   // wave index, in an SGPR
+  const int tile_px = (TH + 2) * LW, total = tile_px * CPP;
+
+  // stage tile t (input rows oh0-PAD .. oh0-PAD+TH+1, zero outside the image) into buffer b
+  auto stage = [&](int t, int b) {
+    const int n = t / tiles_h, oh0 = (t - n * tiles_h) * TH;
+    const bf16* Xn = X + (long)n * IH * IW * CIN;
+    for (int q0 = w * 64; q0 < total; q0 += 64 * NW) {
+      const int q = q0 + lane;
+      if (q < total) {
+        const int p = q / CPP, cpos = q - p * CPP;
+        const int r = p / LW, x = p - r * LW;
+        const int ih = oh0 - PAD + r, iw = x - PAD;
+        const int c = cpos ^ cswz<CIN>(PIPE ? x : p);
+        const void* src = (ih >= 0 && ih < IH && iw >= 0 && iw < IW)
+                              ? (const void*)(Xn + ((long)ih * IW + iw) * CIN + c * 8)
+                              : (const void*)g_czero;
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                         (void __attribute__((address_space(3)))*)(smem + b * BUF + q0 * 16), 16,
+                                         0, 0);
+      }
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t >= ntiles) return;   // uniform, before any barrier
+  stage(t, 0);
+
+  // ---- kernel fragments, loaded once: wf[cg][tap][ks] = W[co0+cg*16+fr][tap'][ks*32 + fg*8 .. +8]
+  // (Wp is [COUT][9][CIN]; PAD == 2 is the flipped kernel: tap' = 8 - tap)
+  const int cp = wsc % NCP, co0 = cp * 32;
+  bf16x8 wf[CG][9][KS];
+#pragma unroll
+  for (int cg = 0; cg < CG; ++cg)
+#pragma unroll
+    for (int tp0 = 0; tp0 < 9; ++tp0)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int tp = PAD ? 8 - tp0 : tp0;
+        wf[cg][tp0][ks] =
+            *reinterpret_cast<const bf16x8*>(Wp + ((long)(co0 + cg * 16 + fr) * 9 + tp) * CIN + ks * 32 + fg * 8);
+      }
+  float s1[CG * 4], s2[CG * 4];
+#pragma unroll
+  for (int q = 0; q < CG * 4; ++q) s1[q] = s2[q] = 0.f;
+
+  const int npg = (OW + 15) / 16;
+  // swizzled chunk byte offset of this lane's fragment at tap column kx (item-invariant: the
+  // swizzle depends on the column modulo 8 and items start at multiples of 16)
+  // (the dgrad, out of registers, swizzles by LDS pixel index instead and computes each
+  // read's chunk on the fly -- cswz(x) and cswz(p) are both conflict-free)
+  int loff[3][KS];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) loff[kx][ks] = PIPE ? ((ks * 4 + fg) ^ cswz<CIN>(fr + kx)) << 4 : 0;
+  for (int k = 0; t < ntiles; ++k, t += G) {
+    // tile t landed (this wave's DMA and its previous stores) -> for every wave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + G < ntiles) stage(t + G, (k + 1) & 1);   // streams in under this tile's MFMAs
+    const char* sb = smem + (k & 1) * BUF;
+    const int n = t / tiles_h, oh0 = (t - n * tiles_h) * TH;
+    // this wave's items (row-major over (row, 16-pixel group)), software-pipelined over three
+    // thirds of the 9 x KS B-fragments: the reads of the next third fly under the MFMAs of
+    // the current one (two thirds live at a time)
+    const int it0 = wsc / NCP, its = NW / NCP;
+    const int rows_here = min(TH, OH - oh0);
+    const int nit = it0 < rows_here * npg ? (rows_here * npg - it0 + its - 1) / its : 0;
+    // fragment f (tap f / KS, 32-channel step f % KS) of item it: the item's lane base, the
+    // tap's pixel offset and the lane's swizzled chunk (loff); columns past OW read junk (in
+    // the buffer's slack) that is never stored
+    auto frag = [&](int it, int f) {
+      const int r = it / npg, pg = it - r * npg;
+      const int tp = f / KS, ks = f - tp * KS;
+      if constexpr (PIPE) {
+        const char* base = sb + (r * LW + pg * 16 + fr) * PB;
+        return *reinterpret_cast<const bf16x8*>(base + ((tp / 3) * LW + tp % 3) * PB + loff[tp % 3][ks]);
+      } else {
+        const int p = (r + tp / 3) * LW + pg * 16 + fr + tp % 3;
+        return *reinterpret_cast<const bf16x8*>(sb + p * PB + (((ks * 4 + fg) ^ cswz<CIN>(p)) << 4));
+      }
+    };
+    bf16x8 bA[F3], bB[F3], bC[F3];
+    auto load3 = [&](bf16x8 (&b)[F3], int it, int part) {
+#pragma unroll
+      for (int f = 0; f < F3; ++f) b[f] = frag(it, part * F3 + f);
+    };
+    auto mfma3 = [&](f32x4 (&acc)[CG], const bf16x8 (&b)[F3], int part) {
+#pragma unroll
+      for (int f = 0; f < F3; ++f) {
+        const int ff = part * F3 + f;
+#pragma unroll
+        for (int cg = 0; cg < CG; ++cg)
+          acc[cg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cg][ff / KS][ff % KS], b[f], acc[cg], 0, 0, 0);
+      }
+    };
+    if (PIPE && nit > 0) load3(bA, it0, 0);
+    for (int j = 0; j < nit; ++j) {
+      const int it = it0 + j * its;
+      const int r = it / npg, pg = it - r * npg;
+      const int oh = oh0 + r;
+      f32x4 acc[CG];
+#pragma unroll
+      for (int cg = 0; cg < CG; ++cg) acc[cg] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (PIPE) {   // thirds rotate: the next third's reads fly under this third's MFMAs
+        load3(bB, it, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma3(acc, bA, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        load3(bC, it, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma3(acc, bB, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (j + 1 < nit) load3(bA, it + its, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma3(acc, bC, 2);
+      } else {                // every read of the item ahead of its MFMAs (fewer live registers)
+        load3(bA, it, 0);
+        load3(bB, it, 1);
+        load3(bC, it, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma3(acc, bA, 0);
+        mfma3(acc, bB, 1);
+        mfma3(acc, bC, 2);
+      }
+      // acc[cg][i] = out[pixel pg*16 + fr][co = co0 + cg*16 + 4fg + i]
+      const int ow = pg * 16 + fr;
+      const bool ok = ow < OW;
+      const bool odd = fg & 1;
+      uint2 pc[2];
+#pragma unroll
+      for (int cg = 0; cg < CG; ++cg) {
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = (bf16)acc[cg][i];
+        pc[cg] = __builtin_bit_cast(uint2, v);
+        if (STATS && ok) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float f = (float)v[i];
+            s1[cg * 4 + i] += f;
+            s2[cg * 4 + i] = fmaf(f, f, s2[cg * 4 + i]);
+          }
+        }
+      }
+      const uint2 snd = odd ? pc[0] : pc[1];
+      uint2 rc;
+      rc.x = __shfl_xor(snd.x, 16, 64);
+      rc.y = __shfl_xor(snd.y, 16, 64);
+      const uint4 d = odd ? make_uint4(rc.x, rc.y, pc[1].x, pc[1].y) : make_uint4(pc[0].x, pc[0].y, rc.x, rc.y);
+      bf16* ypix = Y + (((long)n * OH + oh) * OW + ow) * COUT + co0 + (odd ? 16 + 4 * (fg - 1) : 4 * fg);
+      if (ok && (VAR != 1 || N < 0)) *reinterpret_cast<uint4*>(ypix) = d;
+    }
+    __syncthreads();   // every wave is done reading buffer k&1 before it is restaged
+  }
+
+  if constexpr (STATS) {
+    // reduce over the 16 pixel lanes (xor 1..8), then over the waves in LDS
+#pragma unroll
+    for (int q = 0; q < CG * 4; ++q) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[q] += __shfl_xor(s1[q], o, 64);
+        s2[q] += __shfl_xor(s2[q], o, 64);
+      }
+    }
+    float* red = reinterpret_cast<float*>(smem);   // [NW / NCP wave rows][2][COUT]; no tile is staged any more
+    if (fr == 0) {
+#pragma unroll
+      for (int cg = 0; cg < CG; ++cg)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          red[((w / NCP) * 2 + 0) * COUT + co0 + cg * 16 + 4 * fg + i] = s1[cg * 4 + i];
+          red[((w / NCP) * 2 + 1) * COUT + co0 + cg * 16 + 4 * fg + i] = s2[cg * 4 + i];
+        }
+    }
+    __syncthreads();
+    if (tid < 2 * COUT) {
+      const int kk = tid / COUT, co = tid - kk * COUT;
+      float tot = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW / NCP; ++q) tot += red[(q * 2 + kk) * COUT + co];
+      stats[((long)blockIdx.x * 2 + kk) * COUT + co] = tot;
+    }
+  }
+}
+
+// rows per tile and the widest input each direction supports (two LDS tile buffers of 57 /
+// 77 KB per workgroup, one workgroup per CU); the Xception stem at 299^2 is 149 -> 147
+// (forward), 147 -> 149 (dgrad)
+constexpr int TH_FWD = 4, TH_DGRAD = 2, MAXIW_FWD = 149, MAXIW_DGRAD = 147;
+// waves per workgroup (two per SIMD); the 64-deep dgrad keeps 144 VGPRs of kernel fragments
+// and has no room for the rotating read pipeline
+constexpr int NW_FWD = 8, NW_DGRAD = 8;
+
+int g_conv3_var = 0;   // xcp_tune knob 11 (measurement): 1 = no output stores
+
+int conv3_cus() {
+  static const int cus = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      n = 0;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+}  // namespace
+
+int xcp_internal_conv3_var(int v) {
+  const int old = g_conv3_var;
+  if (v >= 0 && v <= 1) g_conv3_var = v;
+  return old;
+}
+
+extern "C" {
+
+// persistent workgroups (= rows of the stats partial array) of xcp_conv3x3; 0 when the
+// width is unsupported
+int xcp_conv3x3_parts(int mode, int N, int IH, int IW) {
+  if (IW > (mode == 0 ? MAXIW_FWD : MAXIW_DGRAD)) return 0;
+  const int OH = mode == 0 ? IH - 2 : IH + 2;
+  const int th = mode == 0 ? TH_FWD : TH_DGRAD;
+  const int tiles = N * ((OH + th - 1) / th);
+  return tiles < conv3_cus() ? tiles : conv3_cus();
+}
+
+// mode 0: Y[N][IH-2][IW-2][64] = conv3x3(X[N][IH][IW][32], W[64][9][32]) (+ BN partial sums)
+// mode 1: Y[N][IH+2][IW+2][32] = input gradient of that conv from X = dY[N][IH][IW][64],
+//         W = the forward kernel transposed to [32][9][64] (flipped inside).  bf16 only.
+int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, int N, int IH, int IW,
+                hipStream_t st) {
+  if (N <= 0) return XCP_OK;
+  if (IH < 3 || IW < 3 || (mode != 0 && mode != 1) || (mode == 1 && stats)) return XCP_EINVAL;
+  if (IW > (mode == 0 ? MAXIW_FWD : MAXIW_DGRAD)) return XCP_EUNSUPPORTED;
+  const dim3 grid((unsigned)xcp_conv3x3_parts(mode, N, IH, IW));
+  if (mode == 0 && g_conv3_var == 1) {
+    hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD, MAXIW_FWD, true, NW_FWD, true, 1>), grid, dim3(64 * NW_FWD), 0, st, (const bf16*)X,
+                       (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+  } else if (mode == 1 && g_conv3_var == 1) {
+    hipLaunchKernelGGL((conv3x3_kernel<64, 32, 2, TH_DGRAD, MAXIW_DGRAD, false, NW_DGRAD, false, 1>), grid, dim3(64 * NW_DGRAD), 0, st,
+                       (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+  } else if (mode == 0) {
+    if (stats)
+      hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD, MAXIW_FWD, true, NW_FWD, true>), grid, dim3(64 * NW_FWD), 0, st, (const bf16*)X,
+                         (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+    else
+      hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD, MAXIW_FWD, false, NW_FWD, true>), grid, dim3(64 * NW_FWD), 0, st,
+                         (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+  } else {
+    hipLaunchKernelGGL((conv3x3_kernel<64, 32, 2, TH_DGRAD, MAXIW_DGRAD, false, NW_DGRAD, false>), grid, dim3(64 * NW_DGRAD), 0, st,
+                       (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

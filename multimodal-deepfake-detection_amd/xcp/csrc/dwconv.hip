@@ -1137,6 +1137,7 @@ int xcp_internal_tn_tune(int knob, int v);   // gemm.hip
 int xcp_internal_conv1_tune(int v);          // stem.hip
 int xcp_internal_lstm_tune(int v);           // lstm.hip
 int xcp_internal_nt_grid(int v);             // gemm.hip
+int xcp_internal_conv3_var(int v);           // conv3.hip
 
 extern "C" {
 
@@ -1150,6 +1151,7 @@ int xcp_tune(int knob, int value) {
   if (knob == 8) return xcp_internal_conv1_tune(value);
   if (knob == 9) return xcp_internal_lstm_tune(value);
   if (knob == 10) return xcp_internal_nt_grid(value);
+  if (knob == 11) return xcp_internal_conv3_var(value);
   if (knob == 4 || knob == 5) {
     int& k = knob == 4 ? g_dw_fwd_kernel : g_dw_bwd_kernel;
     const int old = k;

@@ -242,7 +242,15 @@ class XceptionEngine:
         ops.bn_act(c1, a1, s1.scale, s1.shift, True, rows1, 32)
         OH2, OW2 = OH1 - 2, OW1 - 2
         rows2 = N * OH2 * OW2
-        c2, s2 = self._pw(a1, pk["conv2"], rows2, 64, 288, train, m.bn2, lda=32, gather=(2, OH1, OW1, OH2, OW2, 1, 32))
+        R2 = ops.conv3x3_parts(0, N, OH1, OW1) if self.dtype == torch.bfloat16 else 0
+        if R2 > 0:   # direct MFMA conv (conv3.hip)
+            c2 = self._empty(rows2 * 64)
+            part = self._empty(R2 * 2 * 64, torch.float32) if train else None
+            ops.conv3x3(0, a1, pk["conv2"], c2, part, N, OH1, OW1)
+            s2 = self._bn_stats(part, R2, 64, rows2, m.bn2, train)
+        else:        # implicit GEMM (im2col gather)
+            c2, s2 = self._pw(a1, pk["conv2"], rows2, 64, 288, train, m.bn2, lda=32,
+                              gather=(2, OH1, OW1, OH2, OW2, 1, 32))
         sout = self._empty(rows2 * 64)
         ops.bn_act(c2, sout, s2.scale, s2.shift, True, rows2, 64)
         S.update(c1=c1, s1=s1, a1=a1, c2=c2, s2=s2, sout=sout, OH1=OH1, OW1=OW1, OH2=OH2, OW2=OW2)
@@ -358,7 +366,10 @@ class XceptionEngine:
         rows1, rows2 = N * OH1 * OW1, N * OH2 * OW2
         dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"], relu=True)   # relu (Xception.py:174) fused
         dA1 = self._empty(rows1 * 32)
-        ops.gemm_nt(dC2, pk["conv2T"], dA1, rows1, 32, 576, lda=64, gather=(3, OH1, OW1, OH2, OW2, 1, 64))
+        if self.dtype == torch.bfloat16 and ops.conv3x3_parts(1, N, OH2, OW2) > 0:
+            ops.conv3x3(1, dC2, pk["conv2T"], dA1, None, N, OH2, OW2)
+        else:
+            ops.gemm_nt(dC2, pk["conv2T"], dA1, rows1, 32, 576, lda=64, gather=(3, OH1, OW1, OH2, OW2, 1, 64))
         w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
         ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
         ops.permute3(w2g, g("conv2.weight", (64, 32, 3, 3)), 64, 9, 32, (0, 2, 1))

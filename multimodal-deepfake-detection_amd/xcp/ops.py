@@ -251,6 +251,18 @@ def conv1_wgrad(X, dY, out, N, IH, IW):
     reduce_slabs(part, R, 32 * 27, out)
 
 
+def conv3x3_parts(mode, N, IH, IW):
+    return _lib.call("xcp_conv3x3_parts", mode, N, IH, IW)
+
+
+def conv3x3(mode, X, W, Y, stats, N, IH, IW):
+    """Stem conv2 as a direct MFMA conv (bf16): mode 0 forward 32->64 (+ BN partial sums),
+    mode 1 its input gradient 64->32 (W = the [32][9][64] transposed kernel)."""
+    if X.dtype != torch.bfloat16:
+        raise ValueError("xcp_conv3x3 is bf16 only")
+    _lib.call("xcp_conv3x3", mode, _p(X), _p(W), _p(Y), _p(stats), N, IH, IW, stream())
+
+
 def permute3(inp, out, d0, d1, d2, perm):
     _lib.call("xcp_permute3", DT[out.dtype], _p(inp), _p(out), d0, d1, d2, perm[0], perm[1], perm[2], stream())
 

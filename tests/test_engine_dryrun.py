@@ -32,6 +32,8 @@ def fake_lib(monkeypatch):
             return 3
         if name in ("xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows"):
             return 256
+        if name == "xcp_conv3x3_parts":
+            return 9
         return 0
 
     monkeypatch.setattr(_lib, "call", fake_call)

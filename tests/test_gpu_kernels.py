@@ -399,3 +399,31 @@ def test_lstm_h64_vs_oracle(ops, gpu, kernel):
             torch.testing.assert_close(p.grad.cpu(), cp[n].grad, rtol=1e-3, atol=1e-5)
     finally:
         ops._lib.call("xcp_tune", 9, old)
+
+
+@pytest.mark.parametrize("N,IH,IW", [(2, 149, 149), (3, 21, 38), (1, 6, 147)])
+def test_conv3x3_stem_fwd_dgrad(ops, gpu, N, IH, IW):
+    """Direct MFMA stem conv2 (conv3.hip) against F.conv2d / its input gradient (bf16
+    operands, fp32 reference on the same rounded values), BN partial sums against the
+    stored output; the 149 case is the 299^2 bench shape."""
+    g = torch.Generator(device=gpu).manual_seed(IH * IW)
+    x = torch.randn(N, 32, IH, IW, device=gpu, generator=g).bfloat16()
+    w = (torch.randn(64, 32, 3, 3, device=gpu, generator=g) / 288 ** 0.5).bfloat16()
+    OH, OW = IH - 2, IW - 2
+    R = ops.conv3x3_parts(0, N, IH, IW)
+    stats = torch.full((R, 2, 64), float("nan"), device=gpu)
+    Y = torch.full((N * OH * OW, 64), float("nan"), device=gpu, dtype=torch.bfloat16)
+    Wp = w.permute(0, 2, 3, 1).reshape(64, 9 * 32).contiguous()          # [co][tap][ci]
+    ops.conv3x3(0, nhwc(x), Wp, Y, stats, N, IH, IW)
+    ref = F.conv2d(x.float(), w.float())
+    assert rel_err(nchw(Y.view(N, OH, OW, 64)).float(), ref) < 1e-2
+    s, Yd = stats.double().sum(0), Y.double()
+    torch.testing.assert_close(s[0], Yd.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(s[1], (Yd * Yd).sum(0), rtol=1e-5, atol=1e-3)
+    # input gradient: a 64 -> 32 conv of the pad-2 gradient with the flipped kernel
+    dy = torch.randn(N, 64, OH, OW, device=gpu, generator=g).bfloat16()
+    WT = w.permute(1, 2, 3, 0).reshape(32, 9 * 64).contiguous()          # [ci][tap][co]
+    DX = torch.full((N * IH * IW, 32), float("nan"), device=gpu, dtype=torch.bfloat16)
+    ops.conv3x3(1, nhwc(dy), WT, DX, None, N, OH, OW)
+    ref_dx = torch.nn.grad.conv2d_input((N, 32, IH, IW), w.float(), dy.float())
+    assert rel_err(nchw(DX.view(N, IH, IW, 32)).float(), ref_dx) < 1e-2

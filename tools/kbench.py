@@ -132,6 +132,23 @@ def main():
             rep(f"conv1_fwd tile={tile}", timeit(lambda: ops.conv1_fwd(xin, w1, c1, NS, IH, IH), iters=5), byts)
             rep(f"conv1_wgrad tile={tile}", timeit(lambda: ops.conv1_wgrad(xin, d1, gw, NS, IH, IH), iters=5), byts)
             ops._lib.call("xcp_tune", 8, old)
+    if "conv3" in sel:
+        NS, IH = 256, 149
+        OH = IH - 2
+        a1 = torch.randn(NS * IH * IH, 32, device=dev, generator=g).to(dt)
+        w2 = (torch.randn(64, 9 * 32, device=dev, generator=g) / 17).to(dt)
+        w2t = (torch.randn(32, 9 * 64, device=dev, generator=g) / 24).to(dt)
+        c2 = torch.empty(NS * OH * OH, 64, device=dev, dtype=dt)
+        R = ops.conv3x3_parts(0, NS, IH, IH)
+        st3 = torch.empty(R * 2 * 64, device=dev)
+        byts = a1.numel() * 2 + c2.numel() * 2
+        for var in (0, 1):
+            old = ops._lib.call("xcp_tune", 11, var)
+            rep(f"conv3x3 fwd +stats var={var}", timeit(lambda: ops.conv3x3(0, a1, w2, c2, st3, NS, IH, IH)), byts,
+                flops=2.0 * c2.numel() * 288)
+            rep(f"conv3x3 dgrad var={var}", timeit(lambda: ops.conv3x3(1, c2, w2t, a1, None, NS, OH, OH)), byts,
+                flops=2.0 * a1.numel() * 576)
+            ops._lib.call("xcp_tune", 11, old)
     if "gemmv" in sel:
         for var in [int(v) for v in os.environ.get('XCP_VARS', '0,1').split(',')]:
             old = ops._lib.call("xcp_tune", 3, var)
