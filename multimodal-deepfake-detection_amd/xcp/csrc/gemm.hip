@@ -396,6 +396,76 @@ XCP_DEV void epilogue256(f32x4 (&acc)[8][4], char* smem, const NTArgs& a, int m0
     }
 }
 
+// LDS-free epilogue of the 256x256 NT kernels (acc[i][j][r] = C[m0 + wr*128 + i*16 + fr]
+// [n0 + wc*64 + j*16 + fg*4 + r]): lanes fg / fg^1 (16 apart) swap 8-B pieces so each lane
+// stores 16 contiguous bytes (one store instruction = 16 rows x 64 B); the BatchNorm partial
+// sums of each 128-row half ([ceil(M/128)][2][N]) come from the rounded registers: sums over
+// the wave's 8 row fragments, then a 4-step reduce-scatter over the 16 row lanes (30
+// shuffles), after which lane fr holds 2 adjacent columns of one statistic.
+template <int EPIV = 0>
+XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n0, int wr, int wc, int fr, int fg) {
+  bf16* C = reinterpret_cast<bf16*>(a.C);
+  const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
+  const int mrow = m0 + wr * 128 + fr;
+  const int ncol = n0 + wc * 64;
+  const bool odd = fg & 1;
+  float s1[16], s2[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) s1[q] = s2[q] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mrow + i * 16;
+    const bool mok = m < a.M;
+    uint2 pc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x4 q;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) q[r] = (bf16)acc[i][j][r];
+      pc[j] = __builtin_bit_cast(uint2, q);
+      if (mok) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float f = (float)q[r];
+          s1[j * 4 + r] += f;
+          s2[j * 4 + r] = fmaf(f, f, s2[j * 4 + r]);
+        }
+      }
+    }
+    const uint2 snd0 = odd ? pc[0] : pc[1], snd1 = odd ? pc[2] : pc[3];
+    uint2 rc0, rc1;
+    rc0.x = __shfl_xor(snd0.x, 16, 64);
+    rc0.y = __shfl_xor(snd0.y, 16, 64);
+    rc1.x = __shfl_xor(snd1.x, 16, 64);
+    rc1.y = __shfl_xor(snd1.y, 16, 64);
+    const uint4 st0 = odd ? make_uint4(rc0.x, rc0.y, pc[1].x, pc[1].y) : make_uint4(pc[0].x, pc[0].y, rc0.x, rc0.y);
+    const uint4 st1 = odd ? make_uint4(rc1.x, rc1.y, pc[3].x, pc[3].y) : make_uint4(pc[2].x, pc[2].y, rc1.x, rc1.y);
+    const int c0 = ncol + (odd ? 16 + (fg - 1) * 4 : fg * 4);
+    bf16* crow = C + (long)m * a.ldc;
+    const bool wr_ok = (EPIV & 1) == 0 || a.M < 0;
+    if (wr_ok && mok && c0 < a.N) *reinterpret_cast<uint4*>(crow + c0) = st0;
+    if (wr_ok && mok && c0 + 32 < a.N) *reinterpret_cast<uint4*>(crow + c0 + 32) = st1;
+  }
+  if (a.stats && ((EPIV & 2) == 0 || a.M < 0)) {
+    // reduce-scatter of v[32] = (s1[16], s2[16]) over the 16 row lanes
+    float u[16], v8[8], v4[4], v2[2];
+    const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u[q] = (b3 ? s2[q] : s1[q]) + __shfl_xor(b3 ? s1[q] : s2[q], 8, 64);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v8[q] = (b2 ? u[8 + q] : u[q]) + __shfl_xor(b2 ? u[q] : u[8 + q], 4, 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v4[q] = (b1 ? v8[4 + q] : v8[q]) + __shfl_xor(b1 ? v8[q] : v8[4 + q], 2, 64);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) v2[q] = (b0 ? v4[2 + q] : v4[q]) + __shfl_xor(b0 ? v4[q] : v4[2 + q], 1, 64);
+    // lane fr holds index 2fr, 2fr+1 of v: statistic fr>>3, j = (fr&7)>>1, r = (fr&1)*2 + q
+    const int col = ncol + ((fr & 7) >> 1) * 16 + fg * 4 + (fr & 1) * 2;
+    const int srow = bm * 2 + wr;
+    if (srow < stat_rows && col < a.N)
+      *reinterpret_cast<float2*>(a.stats + ((long)srow * 2 + (fr >> 3)) * a.N + col) = make_float2(v2[0], v2[1]);
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // 256x256 bf16 NT kernel with 64-deep K-tiles (128-B LDS rows, so every 1-KB LDS-DMA
 // instruction fetches 8 whole 128-B lines; 64-B rows fetch 16 half lines and measured
@@ -421,7 +491,8 @@ XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
   else wait_vmcnt<0>();
 }
 
-// EPIV (measurement only, xcp_tune knob 3 = 2 / 3): 1 = no C stores, 2 = no epilogue
+// EPIV: 0 = LDS-staged epilogue, 4 = LDS-free register epilogue (knob 3 = 11); measurement
+// only (knob 3 = 2 / 3): 1 = no C stores, 2 = no epilogue
 template <bool STAG, int EPIV = 0>
 __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   constexpr int RING = 2 * K_SLOT, EPI = 256 * L_CP;
@@ -557,6 +628,8 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (a.M < 0) a.stats[tid] = t;
+  } else if constexpr (EPIV == 4) {
+    epilogue256_regs(acc, a, m0, n0, wr, wc, fr, fg);
   } else {
     epilogue256<EPIV>(acc, smem, a, m0, n0, bm, tid);
   }
@@ -665,7 +738,6 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
 
   const int nk = (a.K + 63) / 64;
   const bool half_tail = a.K - (nk - 1) * 64 <= 32;
-  const int stat_rows = (a.M + 127) / 128;
   set_target((tile / gridN) * 256, (tile % gridN) * 256);
 #pragma unroll
   for (int h = 0; h < 4; ++h) issue(h, 0, 0);
@@ -760,66 +832,7 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
       slot = nsl;
     }
 
-    // ---- LDS-free epilogue: round, BN partial sums, 16-B stores
-    const int bm = cm0 / 256;
-    const int mrow = cm0 + wr * 128 + fr;
-    const int ncol = cn0 + wc * 64;
-    const bool odd = fg & 1;
-    float s1[16], s2[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) s1[q] = s2[q] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mrow + i * 16;
-      const bool mok = m < a.M;
-      uint2 pc[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bf16x4 q;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) q[r] = (bf16)acc[i][j][r];
-        pc[j] = __builtin_bit_cast(uint2, q);
-        if (mok) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float f = (float)q[r];
-            s1[j * 4 + r] += f;
-            s2[j * 4 + r] = fmaf(f, f, s2[j * 4 + r]);
-          }
-        }
-      }
-      const uint2 snd0 = odd ? pc[0] : pc[1], snd1 = odd ? pc[2] : pc[3];
-      uint2 rc0, rc1;
-      rc0.x = __shfl_xor(snd0.x, 16, 64);
-      rc0.y = __shfl_xor(snd0.y, 16, 64);
-      rc1.x = __shfl_xor(snd1.x, 16, 64);
-      rc1.y = __shfl_xor(snd1.y, 16, 64);
-      const uint4 st0 = odd ? make_uint4(rc0.x, rc0.y, pc[1].x, pc[1].y) : make_uint4(pc[0].x, pc[0].y, rc0.x, rc0.y);
-      const uint4 st1 = odd ? make_uint4(rc1.x, rc1.y, pc[3].x, pc[3].y) : make_uint4(pc[2].x, pc[2].y, rc1.x, rc1.y);
-      const int c0 = ncol + (odd ? 16 + (fg - 1) * 4 : fg * 4);
-      bf16* crow = C + (long)m * a.ldc;
-      const bool wr_ok = (EPIV & 1) == 0 || a.M < 0;
-      if (wr_ok && mok && c0 < a.N) *reinterpret_cast<uint4*>(crow + c0) = st0;
-      if (wr_ok && mok && c0 + 32 < a.N) *reinterpret_cast<uint4*>(crow + c0 + 32) = st1;
-    }
-    if (a.stats && ((EPIV & 2) == 0 || a.M < 0)) {
-      // reduce-scatter of v[32] = (s1[16], s2[16]) over the 16 row lanes
-      float u[16], v8[8], v4[4], v2[2];
-      const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) u[q] = (b3 ? s2[q] : s1[q]) + __shfl_xor(b3 ? s1[q] : s2[q], 8, 64);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v8[q] = (b2 ? u[8 + q] : u[q]) + __shfl_xor(b2 ? u[q] : u[8 + q], 4, 64);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v4[q] = (b1 ? v8[4 + q] : v8[q]) + __shfl_xor(b1 ? v8[q] : v8[4 + q], 2, 64);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) v2[q] = (b0 ? v4[2 + q] : v4[q]) + __shfl_xor(b0 ? v4[q] : v4[2 + q], 1, 64);
-      // lane fr holds index 2fr, 2fr+1 of v: statistic fr>>3, j = (fr&7)>>1, r = (fr&1)*2 + q
-      const int col = ncol + ((fr & 7) >> 1) * 16 + fg * 4 + (fr & 1) * 2;
-      const int srow = bm * 2 + wr;
-      if (srow < stat_rows && col < a.N)
-        *reinterpret_cast<float2*>(a.stats + ((long)srow * 2 + (fr >> 3)) * a.N + col) = make_float2(v2[0], v2[1]);
-    }
+    epilogue256_regs<EPIV>(acc, a, cm0, cn0, wr, wc, fr, fg);
     asm volatile("" ::: "memory");
     if (!more) break;
     tile = next;
@@ -835,9 +848,10 @@ bool tn_big(int dtype, int gmode, int N, int K) {
   return g_tn_cfg == 1 && dtype == XCP_BF16 && gmode == 0 && N >= 128 && K >= 128;
 }
 
-// xcp_tune knob 3: 4 = one tile per workgroup, staggered wave groups (default), 1 = lockstep;
+// xcp_tune knob 3: 11 = one tile per workgroup, staggered wave groups, LDS-free register
+// epilogue (default); 4 = the same with the LDS-staged epilogue; 1 = lockstep;
 // 0 / 7 = persistent kernel staggered / lockstep (measured slower: see DESIGN.md); 2 / 3 / 8-10 = ablations
-int g_nt256_var = 4;
+int g_nt256_var = 11;
 int g_num_cus = 256;   // set from the device at first use (xcp_gemm_nt)
 int g_nt_grid = 0;     // xcp_tune knob 10: persistent grid size (0 = one workgroup per CU)
 
@@ -1185,6 +1199,7 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
       else if (g_nt256_var >= 7) hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);
       else if (g_nt256_var == 2) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 1>), dim3(tiles), dim3(512), 0, stream, a);
       else if (g_nt256_var == 3) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 2>), dim3(tiles), dim3(512), 0, stream, a);
+      else if (g_nt256_var == 11) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 4>), dim3(tiles), dim3(512), 0, stream, a);
       else hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);   // var 4
       return (int)hipGetLastError();
     }
@@ -1228,7 +1243,7 @@ int xcp_internal_tn_tune(int knob, int v) {
 
 int xcp_internal_gemm_var(int v) {
   const int old = g_nt256_var;
-  if (v >= 0 && v <= 10) g_nt256_var = v;
+  if (v >= 0 && v <= 11) g_nt256_var = v;
   return old;
 }
 

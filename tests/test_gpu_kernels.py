@@ -57,7 +57,7 @@ def test_gemm_nt_stats(ops, gpu, dt, M, N, K):
 @pytest.mark.parametrize("M,N,K,lda", [(256, 256, 32, 32), (1000, 728, 728, 728), (300, 2048, 1536, 1536),
                                        (77, 64, 288, 288), (513, 264, 40, 40), (92416 // 8, 728, 728, 736),
                                        (4100, 1024, 728, 1456), (46208, 728, 728, 736), (77073, 264, 40, 40)])
-@pytest.mark.parametrize("var", [0, 7, 4, 1])
+@pytest.mark.parametrize("var", [0, 7, 4, 11, 1])
 def test_gemm_nt256_stats(ops, gpu, M, N, K, lda, var):
     """The 256x256 8-wave bf16 kernels (forced for every size; knob 3: 0 / 7 persistent,
     staggered / lockstep wave groups; 4 / 1 one tile per workgroup): ragged M / N, K tails
