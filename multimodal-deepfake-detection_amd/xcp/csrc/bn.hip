@@ -81,13 +81,61 @@ XCP_DEV void chanred_finish(const ChanRed& r, float (*acc)[CPT], float* part, in
   }
 }
 
+// Gradient of MaxPool2d(3, 2, 1) (Xception.py:86) w.r.t. its input at pixel p, channels
+// c0..c0+CPT-1, gathered from the pooled gradient dOut and the forward's argmax taps (amax,
+// one byte per element, read 8 at a time): input (h, w) lies in at most 2 x 2 windows.
+// Rounded to the storage type, i.e. exactly the value a materialised maxpool backward stores.
+struct PoolSrc {
+  const void* dOut;
+  const unsigned char* amax;
+  int H, W, OH, OW;
+};
+
+template <typename T, int CPT>
+XCP_DEV void pool_grad(const PoolSrc& ps, long p, int c0, int C, float* acc) {
+  static_assert(CPT == 8, "amax is read 8 bytes at a time");
+  const T* dOut = reinterpret_cast<const T*>(ps.dOut);
+  // 32-bit index math (pixel counts stay far below 2^31; 64-bit division is emulated)
+  const unsigned pi = (unsigned)p, W = (unsigned)ps.W, H = (unsigned)ps.H;
+  const unsigned t = pi / W, w = pi - t * W;
+  const unsigned n = t / H, h = t - n * H;
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) acc[j] = 0.f;
+  // window oh covers rows 2oh-1 .. 2oh+1  =>  h/2 <= oh <= (h+1)/2 (one window for even h)
+  const int oh0 = (int)h >> 1, ow0 = (int)w >> 1;
+  const int noh = ((h & 1) && oh0 + 1 < ps.OH) ? 2 : 1, now = ((w & 1) && ow0 + 1 < ps.OW) ? 2 : 1;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    if (a >= noh) break;
+    const int oh = oh0 + a, ky = (int)h - (oh * 2 - 1);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if (b >= now) break;
+      const int ow = ow0 + b, kx = (int)w - (ow * 2 - 1);
+      const long op = ((long)n * ps.OH + oh) * ps.OW + ow;
+      float d[CPT];
+      VecIO<T, CPT>::load(dOut + op * C + c0, d);
+      const uint2 am = *reinterpret_cast<const uint2*>(ps.amax + op * C + c0);
+      const unsigned want = (unsigned)(ky * 3 + kx);
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        const unsigned a = ((j < 4 ? am.x : am.y) >> (8 * (j & 3))) & 0xffu;
+        if (a == want) acc[j] += d[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) acc[j] = rnd<T>(acc[j]);
+}
+
 // MODE 0: (x, x^2) of rows of X.  MODE 1: (dz, dz*yhat), yhat = (y-mean)*invstd.
 // MODE 2: MODE 1 with dz masked by the ReLU that followed the BN (y*ms+mt > 0), i.e. the
 // gradient w.r.t. relu(bn(y)) given; the mask is recomputed from y, never read.
+// MODE 3: MODE 1 with dz gathered from a max-pool backward (pool_grad), never materialised.
 template <typename T, int MODE, int CPT>
 __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av, const void* Bv, const float* mean,
                                                       const float* invstd, const float* ms, const float* mt,
-                                                      float* part) {
+                                                      PoolSrc ps, float* part) {
   const int cchunk = blockIdx.x % r.nch, pchunk = blockIdx.x / r.nch;
   const int lcv = threadIdx.x % r.CVB, slot = threadIdx.x / r.CVB;
   const int cv = cchunk * r.CVB + lcv;
@@ -110,7 +158,8 @@ __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av,
     const long rb = (long)pchunk * r.rows_per_chunk, re = min(r.rows, rb + r.rows_per_chunk);
     for (long p = rb + slot; p < re; p += r.SPB) {
       float a[CPT];
-      VecIO<T, CPT>::load(A + p * r.C + c0, a);
+      if constexpr (MODE == 3) pool_grad<T, CPT>(ps, p, c0, r.C, a);
+      else VecIO<T, CPT>::load(A + p * r.C + c0, a);
       if constexpr (MODE == 0) {
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
@@ -295,18 +344,20 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ X, T*
   VecIO<T, CPT>::store(Y + p * C + c0, v);
 }
 
-// dy = alpha*dz + bcoef*y + delta
-template <typename T, int CPT, bool MASK>
+// dy = alpha*dz + bcoef*y + delta   (POOL: dz gathered from a max-pool backward)
+template <typename T, int CPT, bool MASK, bool POOL = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dZ, const T* __restrict__ Yv, T* dY,
                                                            const float* alpha, const float* bcoef, const float* delta,
-                                                           const float* ms, const float* mt, long rows, int C) {
+                                                           const float* ms, const float* mt, long rows, int C,
+                                                           PoolSrc ps) {
   const int CV = C / CPT;
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
   if (g >= rows * CV) return;
   const int c0 = (int)(g % CV) * CPT;
   const long p = g / CV;
   float dz[CPT], y[CPT], al[CPT], bc[CPT], de[CPT];
-  VecIO<T, CPT>::load(dZ + p * C + c0, dz);
+  if constexpr (POOL) pool_grad<T, CPT>(ps, p, c0, C, dz);
+  else VecIO<T, CPT>::load(dZ + p * C + c0, dz);
   VecIO<T, CPT>::load(Yv + p * C + c0, y);
   VecIO<float, CPT>::load(alpha + c0, al);
   VecIO<float, CPT>::load(bcoef + c0, bc);
@@ -401,38 +452,14 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const T* __restrict__ Y, 
 // maxpool backward by gather: dz[n,h,w] = sum over windows (oh,ow) containing (h,w)
 // whose argmax is (h,w) of dout[n,oh,ow]
 template <typename T, int CPT>
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dOut, const unsigned char* __restrict__ amax,
-                                                          T* __restrict__ dZ, int N, int H, int W, int C, int OH, int OW) {
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolSrc ps, T* __restrict__ dZ, int N, int C) {
   const int CV = C / CPT;
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (long)N * H * W * CV) return;
+  if (g >= (long)N * ps.H * ps.W * CV) return;
   const int c0 = (int)(g % CV) * CPT;
   const long p = g / CV;
-  const int w = (int)(p % W);
-  const long t = p / W;
-  const int h = (int)(t % H);
-  const int n = (int)(t / H);
   float acc[CPT];
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) acc[j] = 0.f;
-  // window oh covers rows 2oh-1 .. 2oh+1  =>  h/2 <= oh <= (h+1)/2
-  for (int oh = h / 2; oh <= (h + 1) / 2; ++oh) {
-    if (oh < 0 || oh >= OH) continue;
-    const int ky = h - (oh * 2 - 1);
-    if (ky < 0 || ky > 2) continue;
-    for (int ow = w / 2; ow <= (w + 1) / 2; ++ow) {
-      if (ow < 0 || ow >= OW) continue;
-      const int kx = w - (ow * 2 - 1);
-      if (kx < 0 || kx > 2) continue;
-      const long op = ((long)n * OH + oh) * OW + ow;
-      float d[CPT];
-      VecIO<T, CPT>::load(dOut + op * C + c0, d);
-      const unsigned char want = (unsigned char)(ky * 3 + kx);
-#pragma unroll
-      for (int j = 0; j < CPT; ++j)
-        if (amax[op * C + c0 + j] == want) acc[j] += d[j];
-    }
-  }
+  pool_grad<T, CPT>(ps, p, c0, C, acc);
   VecIO<T, CPT>::store(dZ + p * C + c0, acc);
 }
 
@@ -476,14 +503,18 @@ inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
 template <typename T, int MODE>
 int chanred_launch(long rows, int C, const void* A, const void* B, const float* mean, const float* invstd, float* part,
-                   hipStream_t st, const float* ms = nullptr, const float* mt = nullptr) {
+                   hipStream_t st, const float* ms = nullptr, const float* mt = nullptr, PoolSrc ps = PoolSrc{}) {
   constexpr int CPT = 8;
   ChanRed r = make_chanred(rows, C, CPT, 1024);
   const long P = chanred_P(r);
   const size_t smem = (size_t)r.SPB * 2 * r.CVB * CPT * sizeof(float);
   hipLaunchKernelGGL((chanred_kernel<T, MODE, CPT>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, A, B, mean,
-                     invstd, ms, mt, part);
+                     invstd, ms, mt, ps, part);
   return (int)hipGetLastError();
+}
+
+inline PoolSrc pool_src(const void* dOut, const unsigned char* amax, int H, int W) {
+  return PoolSrc{dOut, amax, H, W, (H - 1) / 2 + 1, (W - 1) / 2 + 1};
 }
 
 }  // namespace
@@ -533,6 +564,18 @@ int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mea
   }
   if (dtype == XCP_BF16) return chanred_launch<bf16, 1>(rows, C, dZ, Y, mean, invstd, part, st);
   if (dtype == XCP_F32) return chanred_launch<float, 1>(rows, C, dZ, Y, mean, invstd, part, st);
+  return XCP_EUNSUPPORTED;
+}
+
+// xcp_bn_bwd_reduce with dZ = the MaxPool2d(3,2,1) backward of dOut [N][OH][OW][C] (argmax
+// taps amax), gathered on the fly instead of materialised; Y is [N][H][W][C]
+int xcp_bn_bwd_reduce_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, const float* mean,
+                           const float* invstd, int N, int H, int W, int C, float* part, hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const long rows = (long)N * H * W;
+  const PoolSrc ps = pool_src(dOut, amax, H, W);
+  if (dtype == XCP_BF16) return chanred_launch<bf16, 3>(rows, C, nullptr, Y, mean, invstd, part, st, nullptr, nullptr, ps);
+  if (dtype == XCP_F32) return chanred_launch<float, 3>(rows, C, nullptr, Y, mean, invstd, part, st, nullptr, nullptr, ps);
   return XCP_EUNSUPPORTED;
 }
 
@@ -595,7 +638,7 @@ int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const f
   const unsigned g = nblk(rows * (C / 8));
 #define XCP_APPLY(TT, MK)                                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, 8, MK>), dim3(g), dim3(256), 0, st, (const TT*)dZ, (const TT*)Y,  \
-                     (TT*)dY, alpha, bcoef, delta, ms, mt, rows, C)
+                     (TT*)dY, alpha, bcoef, delta, ms, mt, rows, C, PoolSrc{})
   if (dtype == XCP_BF16) {
     if (ms) XCP_APPLY(bf16, true);
     else XCP_APPLY(bf16, false);
@@ -604,6 +647,25 @@ int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const f
     else XCP_APPLY(float, false);
   } else
 #undef XCP_APPLY
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+// xcp_bn_bwd_apply with dZ = the MaxPool2d(3,2,1) backward of dOut (see xcp_bn_bwd_reduce_pool)
+int xcp_bn_bwd_apply_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, void* dY,
+                          const float* alpha, const float* bcoef, const float* delta, int N, int H, int W, int C,
+                          hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const long rows = (long)N * H * W;
+  const unsigned g = nblk(rows * (C / 8));
+  const PoolSrc ps = pool_src(dOut, amax, H, W);
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, 8, false, true>), dim3(g), dim3(256), 0, st, nullptr, (const bf16*)Y,
+                       (bf16*)dY, alpha, bcoef, delta, nullptr, nullptr, rows, C, ps);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, 8, false, true>), dim3(g), dim3(256), 0, st, nullptr,
+                       (const float*)Y, (float*)dY, alpha, bcoef, delta, nullptr, nullptr, rows, C, ps);
+  else
     return XCP_EUNSUPPORTED;
   return (int)hipGetLastError();
 }
@@ -639,14 +701,12 @@ int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int
 int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void* dZ, int N, int H, int W, int C,
                     hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
-  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   const unsigned g = nblk((long)N * H * W * (C / 8));
+  const PoolSrc ps = pool_src(dOut, amax, H, W);
   if (dtype == XCP_BF16)
-    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)dOut, amax, (bf16*)dZ, N,
-                       H, W, C, OH, OW);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, ps, (bf16*)dZ, N, C);
   else if (dtype == XCP_F32)
-    hipLaunchKernelGGL((maxpool_bwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)dOut, amax, (float*)dZ,
-                       N, H, W, C, OH, OW);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, ps, (float*)dZ, N, C);
   else
     return XCP_EUNSUPPORTED;
   return (int)hipGetLastError();

@@ -842,10 +842,12 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
 }
 
-int g_tn_cfg = 1;      // xcp_tune knob 6: 1 = 256x256 weight-gradient kernel for dense bf16, 0 = 128x128
+// xcp_tune knob 6: 2 = 256x256 weight-gradient kernel with the 4-slot 32-row ring for dense
+// bf16 (default), 1 = 256x256 with the 2-slot 64-row ring, 0 = 128x128
+int g_tn_cfg = 2;
 int g_tn_wgs = 256;    // xcp_tune knob 7: target workgroups (splits x tiles) of the 256x256 kernel
 bool tn_big(int dtype, int gmode, int N, int K) {
-  return g_tn_cfg == 1 && dtype == XCP_BF16 && gmode == 0 && N >= 128 && K >= 128;
+  return g_tn_cfg >= 1 && dtype == XCP_BF16 && gmode == 0 && N >= 128 && K >= 128;
 }
 
 // xcp_tune knob 3: 11 = one tile per workgroup, staggered wave groups, LDS-free register
@@ -1165,6 +1167,149 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
     }
   }
 }
+
+// ---------------------------------------------------------------------------------
+// The same 256x256 weight-gradient tile with a deeper load pipeline.  Measured on the
+// 728x728 middle-flow shape, gemm_tn256_kernel is load-bound: 152 us per call, 79 us with
+// its LDS-DMA loads removed (MFMA + LDS reads alone), 148 us with its MFMAs removed.  Its
+// two 64-row K-tile slots give the loads of K-tile t+1 only the MFMAs of K-tile t to land
+// in.  Here a K-tile is 32 m-rows (one MFMA step; G and X slabs of 32 x 512 B = 32 KB per
+// slot) and the ring has 4 slots, so three K-tiles are in flight while one is consumed:
+//   phase A (n-top): reads X all + G n-top   issues G(t+3)
+//   phase B (n-bot): reads G n-bot           issues X(t+3), retires t+1 (counted vmcnt)
+// Slot (t+3)&3 = (t-1)&3 was last read in phase B of t-1, two barriers earlier.
+constexpr int R4_OP = 32 * 512;                // one operand, one slot (16 KB)
+constexpr int R4_SLOT = 2 * R4_OP;
+
+template <int N>
+XCP_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(512) void gemm_tn256r4_kernel(TNArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * R4_SLOT];
+  const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
+  const int tiles = gridN * gridK;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);   // one split's tiles share an XCD (its rows stay in L2)
+  const int sp = id / tiles, t = id % tiles;
+  const int n0 = (t / gridK) * 256, k0 = (t % gridK) * 256;
+  const int mbeg = sp * a.rows_per_split;
+  const int mend = min(a.M, mbeg + a.rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const bf16* G = reinterpret_cast<const bf16*>(a.G);
+  const bf16* X = reinterpret_cast<const bf16*>(a.X);
+
+  // staging: a slab is 32 m-rows x 512 B; wave w loads rows 4w + 2i + (lane >> 5) (i = 0, 1),
+  // lane writes physical chunk lane & 31 = logical chunk lc
+  const int pc = lane & 31;
+  int rr[2], lc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rr[i] = 4 * w + 2 * i + (lane >> 5);
+    lc[i] = pc ^ ((rr[i] & 7) << 1);
+  }
+  const void* zero = g_zero16;
+  asm volatile("" : "+v"(zero));
+  auto glds = [](const void* p, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  // operand op (0: G, 1: X) of K-tile kt into slot kt & 3
+  auto issue = [&](int op, int kt) {
+    char* d = smem + (kt & 3) * R4_SLOT + op * R4_OP;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = mbeg + kt * 32 + rr[i];
+      const int col = (op == 0 ? n0 : k0) + lc[i] * 8;
+      const bool ok = m < mend && col < (op == 0 ? a.N : a.K);
+      const void* src = ok ? (op == 0 ? (const void*)(G + (long)m * a.ldg + col) : (const void*)(X + (long)m * a.ldx + col))
+                           : zero;
+      glds(src, d + (4 * w + 2 * i) * 512);   // 1 KB = slab rows 4w+2i, +1
+    }
+  };
+  // outstanding-load count after K-tile j's loads when waiting for them at the end of K-tile
+  // t (loads of K-tiles j+1 .. min(t+3, nk-1) may stay in flight; 4 per K-tile per thread)
+  auto wait_for = [&](int ahead) {
+    if (ahead >= 2) wait_vm<8>();
+    else if (ahead == 1) wait_vm<4>();
+    else wait_vm<0>();
+  };
+
+  f32x4 acc[8][4];   // [n-frag][k-frag]: lane holds P[n = .. + fr][k = .. + 4*fg + r]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (mend - mbeg + 31) / 32;
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    if (j < nk) {
+      issue(0, j);
+      issue(1, j);
+    }
+  wait_for(min(nk - 1, 2));   // K-tile 0 landed
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int q4 = fr >> 2, p4 = fr & 3;   // tr read: lane 4q+p reads slab row q, columns 4p..4p+3
+  // fragment of 16 columns at cb: k-slots of lane group fg are slab rows {4fg..4fg+3}
+  // (elements 0-3) and {16+4fg..} (4-7)
+  auto frag = [&](const char* slab, int cb) {
+    const int m0r = 4 * fg + q4;
+    const int col = cb + 4 * p4;
+    const bf16x4 lo = ds_read_tr(slab + tswz(m0r, col));
+    const bf16x4 hi = ds_read_tr(slab + tswz(m0r + 16, col));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  };
+  bf16x8 gf[4], xf[4];
+  auto sync_mfma = [&](int ih) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], gf[i], acc[ih * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* sg = smem + (kt & 3) * R4_SLOT;
+    const char* sx = sg + R4_OP;
+    const bool nxt = kt + 3 < nk;
+    // phase A: n-top
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xf[j] = frag(sx, wc * 64 + j * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gf[i] = frag(sg, wr * 128 + i * 16);
+    if (nxt) issue(0, kt + 3);
+    sync_mfma(0);
+    // phase B: n-bot
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gf[i] = frag(sg, wr * 128 + 64 + i * 16);
+    if (nxt) issue(1, kt + 3);
+    if (kt + 1 < nk) wait_for(min(kt + 3, nk - 1) - (kt + 1));   // K-tile kt+1 landed (this wave)
+    sync_mfma(1);
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+
+  float* P = a.P + (long)sp * a.N * a.K;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = n0 + wr * 128 + i * 16 + fr;
+    if (n >= a.N) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wc * 64 + j * 16 + 4 * fg;
+      if (k < a.K) *reinterpret_cast<f32x4*>(P + (long)n * a.K + k) = acc[i][j];
+    }
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -1236,7 +1381,7 @@ int xcp_gemm_nt_stat_rows(int M) { return xcp_cdiv(M, g_nt_cfg == 1 ? 256 : 128)
 int xcp_internal_tn_tune(int knob, int v) {
   int& k = knob == 6 ? g_tn_cfg : g_tn_wgs;
   const int old = k;
-  if (knob == 6 && (v == 0 || v == 1)) k = v;
+  if (knob == 6 && v >= 0 && v <= 2) k = v;
   if (knob == 7 && v >= 8 && v <= 8192) k = v;
   return old;
 }
@@ -1290,7 +1435,8 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
     const dim3 grid(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S);
     if (g_nt256_var == 5) hipLaunchKernelGGL(gemm_tn256_kernel<1>, grid, dim3(512), 0, stream, a);
     else if (g_nt256_var == 6) hipLaunchKernelGGL(gemm_tn256_kernel<2>, grid, dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL(gemm_tn256_kernel<0>, grid, dim3(512), 0, stream, a);
+    else if (g_tn_cfg == 1) hipLaunchKernelGGL(gemm_tn256_kernel<0>, grid, dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL(gemm_tn256r4_kernel, grid, dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(N, 128) * xcp_cdiv(K, 128) * S;

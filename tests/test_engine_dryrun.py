@@ -63,7 +63,8 @@ def test_lstmv_step_call_sequence(fake_lib, unfrozen):
     names = set(fake_lib)
     assert {"xcp_gemm_nt", "xcp_dw_fwd", "xcp_tail_fwd", "xcp_avgpool_fwd", "xcp_lstm_fwd", "xcp_lstm_bwd"} <= names
     if unfrozen:
-        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd", "xcp_conv1_wgrad"} <= names
+        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd", "xcp_conv1_wgrad",
+                "xcp_conv3x3"} <= names
         for n, p in m.feature_extractor.named_parameters():
             assert p.grad is not None and p.grad.shape == p.shape, n
     else:

@@ -130,7 +130,7 @@ def test_gemm_im2col_conv2_fwd_and_dgrad(ops, gpu, dt):
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("M,N,K", [(5000, 128, 64), (92416 // 16, 728, 728), (300, 2048, 1536), (33, 512, 2048),
                                    (1000, 264, 136), (7777, 1024, 728)])
-@pytest.mark.parametrize("tn", [1, 0], ids=["tn256", "tn128"])
+@pytest.mark.parametrize("tn", [2, 1, 0], ids=["tn256r4", "tn256", "tn128"])
 def test_gemm_tn(ops, gpu, dt, M, N, K, tn):
     old = ops._lib.call("xcp_tune", 6, tn)
     g = torch.Generator(device=gpu).manual_seed(M)
@@ -285,6 +285,26 @@ def test_tail_maxpool_fwd_bwd(ops, gpu, dt, H):
     dz = torch.empty(N * H * H, C, device=gpu, dtype=dt)
     ops.maxpool_bwd(nhwc(d), amax, dz, N, H, H, C)
     assert rel_err(nchw(dz.view(N, H, H, C)).float(), zr.grad) < (1e-6 if dt == torch.float32 else 1e-2)
+    # BN backward whose dz is this max-pool gradient, gathered on the fly: bitwise equal to
+    # the materialised path (the gathered dz is rounded to the storage type the same way)
+    from xcp.engine import Stats
+    st = Stats(C, gpu)
+    st.mean.copy_(torch.randn(C, device=gpu, generator=g))
+    st.invstd.copy_(torch.rand(C, device=gpu, generator=g) + 0.5)
+    bn = {"weight": s1, "bias": t1, "running_mean": None, "running_var": None, "eps": 1e-5, "momentum": 0.1,
+          "track": False}
+    rows = N * H * H
+    outs = []
+    for pool in (False, True):
+        dY = torch.empty(rows, C, device=gpu, dtype=dt)
+        dg, db = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+        if pool:
+            ops.bn_backward(None, nhwc(y), rows, C, bn, st, dY, dg, db, pool=(nhwc(d), amax, N, H, H))
+        else:
+            ops.bn_backward(dz, nhwc(y), rows, C, bn, st, dY, dg, db)
+        outs.append((dY, dg, db))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

@@ -95,7 +95,7 @@ def main():
                 flops=2.0 * M * C * C)
             ops._lib.call("xcp_tune", 2, old)
         out = torch.empty(C * C, device=dev)
-        for tn in (1, 0):
+        for tn in (2, 1, 0):
             old = ops._lib.call("xcp_tune", 6, tn)
             rep(f"weight_grad 728x728 tn={tn}", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)),
                 flops=2.0 * M * C * C)
