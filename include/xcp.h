@@ -141,6 +141,13 @@ int xcp_conv3x3_parts(int mode, int N, int IH, int IW);
 int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, int N, int IH, int IW,
                 xcp_stream_t stream);
 
+/* ---- clip input (video_dataloader.py:22-68): uint8 frames -> fp32 model input ----
+ * in [B][Tmax][H][W][3] uint8 (device), len [B] int32 (device): frames t >= len[b] are padding;
+ * out [B][Tmax][3][H][W] fp32 = x / 255 (zeros for padding), bit-identical to the host loader;
+ * W a multiple of 4 */
+int xcp_frames_u8_to_f32(const unsigned char* in, const int* len, float* out, int B, int Tmax, int H, int W,
+                         xcp_stream_t stream);
+
 /* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][10] int64
  * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block), nblocks in total */
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream_t stream);

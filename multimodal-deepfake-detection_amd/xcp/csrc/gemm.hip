@@ -842,9 +842,10 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
 }
 
-// xcp_tune knob 6: 2 = 256x256 weight-gradient kernel with the 4-slot 32-row ring for dense
-// bf16 (default), 1 = 256x256 with the 2-slot 64-row ring, 0 = 128x128
-int g_tn_cfg = 2;
+// xcp_tune knob 6: 1 = 256x256 weight-gradient kernel (2-slot 64-row ring) for dense bf16
+// (default); 2 = the 4-slot 32-row ring (deeper prefetch measured no faster: 175 vs 168 us,
+// the loads are bandwidth- not latency-bound); 0 = 128x128
+int g_tn_cfg = 1;
 int g_tn_wgs = 256;    // xcp_tune knob 7: target workgroups (splits x tiles) of the 256x256 kernel
 bool tn_big(int dtype, int gmode, int N, int K) {
   return g_tn_cfg >= 1 && dtype == XCP_BF16 && gmode == 0 && N >= 128 && K >= 128;

@@ -265,6 +265,17 @@ def conv1_wgrad(X, dY, out, N, IH, IW):
     reduce_slabs(part, R, 32 * 27, out)
 
 
+def frames_u8_to_f32(frames, lengths, out):
+    """frames: uint8 [B, Tmax, H, W, 3] (device), lengths: int32 [B] (device) -> out fp32
+    [B, Tmax, 3, H, W] = frames / 255, zero past each clip's length (video_dataloader.py:35, :59-64)."""
+    check_gpu(frames, lengths, out)
+    B, T, H, W, C = frames.shape
+    if C != 3 or frames.dtype != torch.uint8 or lengths.dtype != torch.int32 or out.dtype != torch.float32 \
+            or tuple(out.shape) != (B, T, 3, H, W) or not (frames.is_contiguous() and out.is_contiguous()):
+        raise ValueError("frames_u8_to_f32: expects uint8 [B,T,H,W,3], int32 [B] and fp32 [B,T,3,H,W]")
+    _lib.call("xcp_frames_u8_to_f32", _p(frames), _p(lengths), _p(out), B, T, H, W, stream())
+
+
 def conv3x3_parts(mode, N, IH, IW):
     return _lib.call("xcp_conv3x3_parts", mode, N, IH, IW)
 

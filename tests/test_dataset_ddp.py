@@ -27,6 +27,38 @@ def test_face_loader(tmp_path):
     assert float(clips[1, 3:].abs().sum()) == 0.0   # zero padded
 
 
+def test_face_loader_u8_host_side(tmp_path):
+    """uint8 loader (GPU-expanded path): same files, order, labels and padding as
+    get_face_dataloader; converting its batch on the host reproduces the fp32 batch."""
+    from Dataset.video_dataloader import get_face_dataloader_u8
+    rs = np.random.RandomState(2)
+    a = rs.randint(0, 256, (3, 8, 12, 3), dtype=np.uint8)
+    b = rs.randint(0, 256, (5, 8, 12, 3), dtype=np.uint8)
+    np.save(tmp_path / "real_a.npy", a)
+    np.save(tmp_path / "fake_b.npy", b)
+    ref, ref_labels = next(iter(get_face_dataloader(str(tmp_path), batch_size=2)))
+    u8, labels, lengths = next(iter(get_face_dataloader_u8(str(tmp_path), batch_size=2)))
+    assert u8.dtype == torch.uint8 and u8.shape == (2, 5, 8, 12, 3)
+    assert lengths.tolist() == [5, 3] and labels.tolist() == ref_labels.tolist()
+    host = u8.to(torch.float32).permute(0, 1, 4, 2, 3) / 255.0
+    assert torch.equal(host, ref)
+
+
+@pytest.mark.gpu
+def test_face_loader_u8_gpu_bitwise(tmp_path):
+    """xcp_frames_u8_to_f32 (frames.hip) on the GPU equals the reference loader's fp32 batch
+    bit for bit (x / 255, NCHW permute, zero padding of short clips)."""
+    from Dataset.video_dataloader import clips_u8_to_device, get_face_dataloader_u8
+    rs = np.random.RandomState(3)
+    for i, t in enumerate((4, 7, 2)):
+        np.save(tmp_path / f"{'real' if i == 1 else 'fake'}_{i}.npy", rs.randint(0, 256, (t, 20, 36, 3), dtype=np.uint8))
+    ref, _ = next(iter(get_face_dataloader(str(tmp_path), batch_size=3)))
+    batch = next(iter(get_face_dataloader_u8(str(tmp_path), batch_size=3)))
+    clips, _ = clips_u8_to_device(batch, torch.device("cuda:0"))
+    torch.cuda.synchronize()
+    assert torch.equal(clips.cpu(), ref)
+
+
 def test_audio_loader(tmp_path):
     m = np.random.RandomState(1).randn(120, 13).astype(np.float32)
     np.save(tmp_path / "real_x.npy", m)
