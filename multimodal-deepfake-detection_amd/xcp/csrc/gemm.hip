@@ -1333,7 +1333,7 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     const int tiles = xcp_cdiv(M, 256) * xcp_cdiv(N, 256);
     if ((tiles >= 256 && K >= 384) || g_nt_cfg == 3) {
       const bool fits31 = (long)M * lda < (1L << 31) && (long)N * ldb < (1L << 31);
-      if ((g_nt256_var == 0 || g_nt256_var >= 7) && fits31) {
+      if ((g_nt256_var == 0 || (g_nt256_var >= 7 && g_nt256_var <= 10)) && fits31) {
         const int cap = g_nt_grid > 0 ? g_nt_grid : g_num_cus;
         const int grid = tiles < cap ? tiles : cap;
         if (g_nt256_var == 7) hipLaunchKernelGGL((gemm_nt256p_kernel<false>), dim3(grid), dim3(512), 0, stream, a);
@@ -1342,10 +1342,10 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
         else if (g_nt256_var == 10) hipLaunchKernelGGL((gemm_nt256p_kernel<true, 3>), dim3(grid), dim3(512), 0, stream, a);
         else hipLaunchKernelGGL((gemm_nt256p_kernel<true>), dim3(grid), dim3(512), 0, stream, a);
       } else if (g_nt256_var == 1) hipLaunchKernelGGL((gemm_nt256k64_kernel<false>), dim3(tiles), dim3(512), 0, stream, a);
+      else if (g_nt256_var == 11) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 4>), dim3(tiles), dim3(512), 0, stream, a);
       else if (g_nt256_var >= 7) hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);
       else if (g_nt256_var == 2) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 1>), dim3(tiles), dim3(512), 0, stream, a);
       else if (g_nt256_var == 3) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 2>), dim3(tiles), dim3(512), 0, stream, a);
-      else if (g_nt256_var == 11) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 4>), dim3(tiles), dim3(512), 0, stream, a);
       else hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);   // var 4
       return (int)hipGetLastError();
     }
