@@ -140,6 +140,11 @@ int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int 
 int xcp_conv3x3_parts(int mode, int N, int IH, int IW);
 int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, int N, int IH, int IW,
                 xcp_stream_t stream);
+/* weight gradient of mode 0 (replaces the autograd wgrad of Xception.conv2, Xception.py:122):
+ * P[parts][64][9*32] fp32 slabs whose sum is dW[co][kh*3+kw][ci], from dY[N][IH-2][IW-2][64]
+ * and X[N][IH][IW][32]; xcp_conv3x3_wgrad_parts returns the slab count, 0 if unsupported */
+int xcp_conv3x3_wgrad_parts(int N, int IH, int IW);
+int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, int IW, xcp_stream_t stream);
 
 /* ---- clip input (video_dataloader.py:22-68): uint8 frames -> fp32 model input ----
  * in [B][Tmax][H][W][3] uint8 (device), len [B] int32 (device): frames t >= len[b] are padding;

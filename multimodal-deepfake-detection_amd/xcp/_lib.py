@@ -53,6 +53,8 @@ SIGNATURES = {
     "xcp_frames_u8_to_f32": [P, P, P, I, I, I, I, P],
     "xcp_conv3x3_parts": [I, I, I, I],
     "xcp_conv3x3": [I, P, P, P, P, I, I, I, P],
+    "xcp_conv3x3_wgrad_parts": [I, I, I],
+    "xcp_conv3x3_wgrad": [P, P, P, I, I, I, P],
     "xcp_lstm_needs_whhT": [I],
     "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
     "xcp_lstm_bwd": [P, P, P, P, P, P, P, I, I, I, P],
@@ -60,7 +62,7 @@ SIGNATURES = {
 
 # entry points that return a size, not a status
 SIZE_QUERIES = {"xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts", "xcp_tune",
-                "xcp_lstm_needs_whhT", "xcp_conv3x3_parts"}
+                "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts"}
 
 _lib = None
 

@@ -122,6 +122,14 @@ XCP_DEV void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// ds_read_b64_tr_b16: within each 16-lane group, lane 4q+p addresses row q, columns 4p..4p+3
+// of a 4 x 16 bf16 block; lane i receives column i of the 4 rows
+XCP_DEV bf16x4 ds_read_tr(const char* p) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
 static inline int xcp_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5

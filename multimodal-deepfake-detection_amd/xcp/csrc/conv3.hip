@@ -246,6 +246,135 @@ __global__ __launch_bounds__(NW * 64, 1) void conv3x3_kernel(const bf16* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Stem conv2 weight gradient: dW[co][tap][ci] = sum over output pixels p of
+// dY[p][co] * X[p + tap][ci]  (tap = kh*3 + kw; 64 x 288 outputs, 2 * 64 * 288 flops per
+// output pixel), the reduction running over all N * 147 * 147 pixels.  The generic path
+// (gemm.hip gemm_tn_kernel, im2col gather mode 2) took 1.0 ms per call at 256 x 149^2:
+// every X chunk is gathered nine times and the output tile is half empty.
+//
+// conv3x3_wgrad_kernel: one 512-thread workgroup per band of output rows of one frame
+// (bands sized so the grid is about one workgroup per CU) slides down its band one output
+// row at a time.  LDS holds a 3-slot ring of dY rows ([160 px][64 co], 16-B chunks
+// XOR-swizzled by pixel & 7) and a 5-slot ring of X rows ([192 px][32 ci], chunks swizzled
+// by bit 2 of the pixel); both are filled by LDS-DMA two rows ahead (4 KB-instructions per
+// wave per row, counted vmcnt), pixels past the row read a zero line.  Wave w owns the
+// 16 x 16 (co, ci) block (w >> 1, w & 1) for all nine taps (9 accumulators): per 32-pixel
+// chunk it reads one transposed dY fragment (ds_read_b64_tr_b16, reused by the 9 taps) and
+// nine shifted X fragments, 9 MFMAs (v_mfma_f32_16x16x32_bf16 with the pixels as the
+// reduction index).  Each workgroup writes one fp32 slab P[wg][64][288]; the slabs are
+// summed by colreduce.
+constexpr int WG_GPX = 160, WG_APX = 192;                  // pixels per dY / X ring slot
+constexpr int WG_GSLOT = WG_GPX * 128, WG_ASLOT = WG_APX * 64;
+constexpr int WG_GI = WG_GSLOT / 1024, WG_AI = WG_ASLOT / 1024;   // 1-KB DMA instructions per row: 20, 12
+static_assert((WG_GI + WG_AI) % 8 == 0, "uniform DMA count per wave");
+constexpr int WG_PER_WAVE = (WG_GI + WG_AI) / 8;            // 4
+
+template <int VAR = 0>
+__global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
+                                                               float* __restrict__ P, int N, int IH, int IW, int nb,
+                                                               int RB) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * WG_GSLOT + 5 * WG_ASLOT];
+  char* gs = smem;
+  char* as = smem + 3 * WG_GSLOT;
+  const int OH = IH - 2, OW = IW - 2;
+  const int n = blockIdx.x / nb, band = blockIdx.x - n * nb;
+  const int r0 = band * RB, r1 = min(OH, r0 + RB);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
+  const int wsc = __builtin_amdgcn_readfirstlane(w);
+  const bf16* Gn = dY + (long)n * OH * OW * 64;
+  const bf16* Xn = X + (long)n * IH * IW * 32;
+  auto dma = [](const void* src, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  // DMA instruction j of a dY row (j < WG_GI) or of an X row
+  auto g_instr = [&](int row, int j) {
+    const int q = j * 64 + lane, px = q >> 3, c = (q & 7) ^ (px & 7);
+    const void* src = px < OW ? (const void*)(Gn + ((long)row * OW + px) * 64 + c * 8) : (const void*)g_czero;
+    dma(src, gs + (row % 3) * WG_GSLOT + j * 1024);
+  };
+  auto a_instr = [&](int row, int j) {
+    const int q = j * 64 + lane, px = q >> 2, c = (q & 3) ^ (((px >> 2) & 1) << 1);
+    const void* src = px < IW ? (const void*)(Xn + ((long)row * IW + px) * 32 + c * 8) : (const void*)g_czero;
+    dma(src, as + (row % 5) * WG_ASLOT + j * 1024);
+  };
+  // loads of step oh: dY row oh and X row oh + 2 (4 instructions per wave)
+  auto issue_step = [&](int oh) {
+#pragma unroll
+    for (int i = 0; i < WG_PER_WAVE; ++i) {
+      const int j = wsc * WG_PER_WAVE + i;
+      if (j < WG_GI) g_instr(oh, j);
+      else a_instr(oh + 2, j - WG_GI);
+    }
+  };
+  if (r0 >= r1) return;   // uniform
+  // prologue: dY row r0 and X rows r0, r0 + 1, r0 + 2 (56 instructions, 7 per wave), then step r0 + 1
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int j = wsc * 7 + i;
+    if (j < WG_GI) g_instr(r0, j);
+    else a_instr(r0 + (j - WG_GI) / WG_AI, (j - WG_GI) % WG_AI);
+  }
+  if (r0 + 1 < r1) issue_step(r0 + 1);
+
+  const int cb = wsc >> 1, bb = wsc & 1;   // co block (16), ci block (16)
+  const int q4 = fr >> 2, p4 = fr & 3;
+  // per-lane byte offsets inside a slot: dY fragment rows 4fg + q4 (+16), columns 16cb + 4p4;
+  // X fragment columns 16bb + 4p4 at pixel rows 4fg + q4 (+16) + chunk + kw
+  const int gch = 2 * cb + (p4 >> 1), ach = 2 * bb + (p4 >> 1), sub = (p4 & 1) * 8;
+  f32x4 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nch = (OW + 31) / 32;
+  for (int oh = r0; oh < r1; ++oh) {
+    if (oh + 1 < r1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();   // (not __syncthreads: that would also drain the next row's DMA)
+    if (oh + 2 < r1) issue_step(oh + 2);
+    const char* gslot = gs + (oh % 3) * WG_GSLOT;
+    const char* a0 = as + (oh % 5) * WG_ASLOT;
+    const char* a1 = as + ((oh + 1) % 5) * WG_ASLOT;
+    const char* a2 = as + ((oh + 2) % 5) * WG_ASLOT;
+    const char* arow[3] = {a0, a1, a2};
+    for (int ch = 0; ch < nch; ++ch) {
+      const int pb = ch * 32 + 4 * fg + q4;
+      bf16x8 A;
+      {
+        const int plo = pb, phi = pb + 16;
+        const bf16x4 lo = ds_read_tr(gslot + plo * 128 + ((gch ^ (plo & 7)) << 4) + sub);
+        const bf16x4 hi = ds_read_tr(gslot + phi * 128 + ((gch ^ (phi & 7)) << 4) + sub);
+        A = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      bf16x8 B[9];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int plo = pb + kw, phi = pb + kw + 16;
+          const bf16x4 lo = ds_read_tr(arow[kh] + plo * 64 + ((ach ^ (((plo >> 2) & 1) << 1)) << 4) + sub);
+          const bf16x4 hi = ds_read_tr(arow[kh] + phi * 64 + ((ach ^ (((phi >> 2) & 1) << 1)) << 4) + sub);
+          B[kh * 3 + kw] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      if constexpr (VAR != 1) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[t], acc[t], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) asm volatile("" ::"v"(A), "v"(B[t]));
+      }
+    }
+  }
+  // acc[t][r] = dW[co = 16cb + 4fg + r][tap t][ci = 16bb + fr]
+  float* Pb = P + (long)blockIdx.x * 64 * 288;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Pb[(16 * cb + 4 * fg + r) * 288 + t * 32 + 16 * bb + fr] = acc[t][r];
+}
+
+// bands per frame for the weight-gradient grid: about one workgroup per CU, >= 8 rows a band
+
 // rows per tile and the widest input each direction supports (two LDS tile buffers of 57 /
 // 77 KB per workgroup, one workgroup per CU); the Xception stem at 299^2 is 149 -> 147
 // (forward), 147 -> 149 (dgrad)
@@ -254,7 +383,8 @@ constexpr int TH_FWD = 4, TH_DGRAD = 2, MAXIW_FWD = 149, MAXIW_DGRAD = 147;
 // and has no room for the rotating read pipeline
 constexpr int NW_FWD = 8, NW_DGRAD = 8;
 
-int g_conv3_var = 0;   // xcp_tune knob 11 (measurement): 1 = no output stores
+int g_conv3_var = 0;   // xcp_tune knob 11 (measurement): 1 = no output stores (forward / dgrad), no MFMAs (wgrad)
+
 
 int conv3_cus() {
   static const int cus = [] {
@@ -264,6 +394,16 @@ int conv3_cus() {
     return n > 0 ? n : 256;
   }();
   return cus;
+}
+
+// weight-gradient grid: bands of output rows per frame, about one workgroup per CU and
+// at least 8 rows a band
+void wgrad_bands(int N, int OH, int& nb, int& rb) {
+  nb = (conv3_cus() + N - 1) / N;
+  if (nb > OH / 8) nb = OH / 8;
+  if (nb < 1) nb = 1;
+  rb = (OH + nb - 1) / nb;
+  nb = (OH + rb - 1) / rb;
 }
 
 }  // namespace
@@ -312,6 +452,31 @@ int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, i
     hipLaunchKernelGGL((conv3x3_kernel<64, 32, 2, TH_DGRAD, MAXIW_DGRAD, false, NW_DGRAD, false>), grid, dim3(64 * NW_DGRAD), 0, st,
                        (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
   }
+  return (int)hipGetLastError();
+}
+
+// slabs (= workgroups) of xcp_conv3x3_wgrad; 0 when the width is unsupported
+int xcp_conv3x3_wgrad_parts(int N, int IH, int IW) {
+  if (N <= 0 || IH < 3 || IW < 3 || IW - 2 > WG_GPX) return 0;
+  int nb, rb;
+  wgrad_bands(N, IH - 2, nb, rb);
+  return N * nb;
+}
+
+// P[parts][64][9 * 32] (fp32 slabs, sum them for dW[co][tap][ci]) = weight gradient of
+// Y = conv3x3(X) from dY[N][IH-2][IW-2][64] and X[N][IH][IW][32].  bf16 only.
+int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, int IW, hipStream_t st) {
+  if (N <= 0) return XCP_OK;
+  if (IH < 3 || IW < 3) return XCP_EINVAL;
+  if (IW - 2 > WG_GPX) return XCP_EUNSUPPORTED;
+  int nb, rb;
+  wgrad_bands(N, IH - 2, nb, rb);
+  if (g_conv3_var == 1)
+    hipLaunchKernelGGL((conv3x3_wgrad_kernel<1>), dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N,
+                       IH, IW, nb, rb);
+  else
+    hipLaunchKernelGGL((conv3x3_wgrad_kernel<0>), dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N,
+                       IH, IW, nb, rb);
   return (int)hipGetLastError();
 }
 

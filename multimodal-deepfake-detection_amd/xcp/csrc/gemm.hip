@@ -880,12 +880,6 @@ struct TNArgs {
   Gather gx;               // gather of the X operand rows / columns
 };
 
-XCP_DEV bf16x4 ds_read_tr(const char* p) {
-  typedef short s4 __attribute__((ext_vector_type(4)));
-  s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p));
-  return __builtin_bit_cast(bf16x4, v);
-}
-
 template <typename T, int GM>
 __global__ __launch_bounds__(NT) void gemm_tn_kernel(TNArgs a) {
   // tile: 128 (n) x 128 (k); stage: 32 m-rows of G[., n0:n0+128] and X[., k0:k0+128]

@@ -373,7 +373,10 @@ class XceptionEngine:
         else:
             ops.gemm_nt(dC2, pk["conv2T"], dA1, rows1, 32, 576, lda=64, gather=(3, OH1, OW1, OH2, OW2, 1, 64))
         w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
-        ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
+        if self.dtype == torch.bfloat16 and ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0:
+            ops.conv3x3_wgrad(dC2, S["a1"], w2g, N, OH1, OW1)
+        else:
+            ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
         ops.permute3(w2g, g("conv2.weight", (64, 32, 3, 3)), 64, 9, 32, (0, 2, 1))
         dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], relu=True)   # relu (Xception.py:170) fused
         ops.conv1_wgrad(S["x"], dC1, g("conv1.weight", (32, 3, 3, 3)), N, S["IH"], S["IW"])

@@ -288,6 +288,23 @@ def conv3x3(mode, X, W, Y, stats, N, IH, IW):
     _lib.call("xcp_conv3x3", mode, _p(X), _p(W), _p(Y), _p(stats), N, IH, IW, stream())
 
 
+def conv3x3_wgrad_parts(N, IH, IW):
+    return _lib.call("xcp_conv3x3_wgrad_parts", N, IH, IW)
+
+
+def conv3x3_wgrad(dY, X, out, N, IH, IW):
+    """out[64][9*32] fp32 = weight gradient of the stem conv2 (tap-major, [co][kh*3+kw][ci])
+    from dY [N,IH-2,IW-2,64] and X [N,IH,IW,32] (bf16): per-workgroup slabs + colreduce."""
+    if dY.dtype != torch.bfloat16 or X.dtype != torch.bfloat16:
+        raise ValueError("xcp_conv3x3_wgrad is bf16 only")
+    S = conv3x3_wgrad_parts(N, IH, IW)
+    if S <= 0:
+        raise ValueError("xcp_conv3x3_wgrad: unsupported width")
+    P = torch.empty(S * 64 * 288, device=dY.device, dtype=torch.float32)
+    _lib.call("xcp_conv3x3_wgrad", _p(dY), _p(X), _p(P), N, IH, IW, stream())
+    reduce_slabs(P, S, 64 * 288, out)
+
+
 def permute3(inp, out, d0, d1, d2, perm):
     _lib.call("xcp_permute3", DT[out.dtype], _p(inp), _p(out), d0, d1, d2, perm[0], perm[1], perm[2], stream())
 

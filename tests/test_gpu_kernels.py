@@ -447,3 +447,9 @@ def test_conv3x3_stem_fwd_dgrad(ops, gpu, N, IH, IW):
     ops.conv3x3(1, nhwc(dy), WT, DX, None, N, OH, OW)
     ref_dx = torch.nn.grad.conv2d_input((N, 32, IH, IW), w.float(), dy.float())
     assert rel_err(nchw(DX.view(N, IH, IW, 32)).float(), ref_dx) < 1e-2
+    # weight gradient (slabs + colreduce) against conv2d_weight on the same bf16 operands
+    dW = torch.full((64 * 288,), float("nan"), device=gpu)
+    ops.conv3x3_wgrad(nhwc(dy), nhwc(x), dW, N, IH, IW)
+    ref_dw = torch.nn.grad.conv2d_weight(x.float(), (64, 32, 3, 3), dy.float())
+    got = dW.view(64, 3, 3, 32).permute(0, 3, 1, 2)
+    assert rel_err(got, ref_dw) < 1e-4

@@ -148,7 +148,14 @@ def main():
                 flops=2.0 * c2.numel() * 288)
             rep(f"conv3x3 dgrad var={var}", timeit(lambda: ops.conv3x3(1, c2, w2t, a1, None, NS, OH, OH)), byts,
                 flops=2.0 * a1.numel() * 576)
+            dw2 = torch.empty(64 * 288, device=dev)
+            rep(f"conv3x3 wgrad var={var}", timeit(lambda: ops.conv3x3_wgrad(c2, a1, dw2, NS, IH, IH)), byts,
+                flops=2.0 * c2.numel() * 288)
             ops._lib.call("xcp_tune", 11, old)
+        dw2 = torch.empty(64 * 288, device=dev)
+        rep("gemm_tn im2col wgrad", timeit(lambda: ops.weight_grad(c2, a1, NS * OH * OH, 64, 288, dw2,
+                                                                      gather=(2, IH, IH, OH, OH, 1, 32), ldx=32)), byts,
+            flops=2.0 * c2.numel() * 288)
     if "gemmv" in sel:
         for var in [int(v) for v in os.environ.get('XCP_VARS', '0,1').split(',')]:
             old = ops._lib.call("xcp_tune", 3, var)
