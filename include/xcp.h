@@ -112,10 +112,12 @@ int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int
 int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void* dZ, int N, int H, int W, int C,
                     xcp_stream_t stream);
 /* BatchNorm backward reduce / apply whose dZ is the MaxPool2d(3,2,1) backward (Xception.py:86)
- * of dOut [N][OH][OW][C] with argmax taps amax, gathered on the fly (never materialised);
- * Y / dY are [N][H][W][C] */
+ * of dOut [N][OH][OW][C] with argmax taps amax, gathered on the fly; Y / dY are [N][H][W][C].
+ * reduce: dZ (may be null) receives the gathered gradient (max-pool backward + BN reduce in one
+ * pass; the apply then reads it with xcp_bn_bwd_apply) */
 int xcp_bn_bwd_reduce_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, const float* mean,
-                           const float* invstd, int N, int H, int W, int C, float* part, xcp_stream_t stream);
+                           const float* invstd, int N, int H, int W, int C, float* part, void* dZ,
+                           xcp_stream_t stream);
 int xcp_bn_bwd_apply_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, void* dY,
                           const float* alpha, const float* bcoef, const float* delta, int N, int H, int W, int C,
                           xcp_stream_t stream);

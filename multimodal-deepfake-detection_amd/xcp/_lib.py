@@ -41,7 +41,7 @@ SIGNATURES = {
     "xcp_relu_bwd": [I, P, P, L, I, P],
     "xcp_tail_fwd": [I, P, P, P, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_maxpool_bwd": [I, P, P, P, I, I, I, I, P],
-    "xcp_bn_bwd_reduce_pool": [I, P, P, P, P, P, I, I, I, I, P, P],
+    "xcp_bn_bwd_reduce_pool": [I, P, P, P, P, P, I, I, I, I, P, P, P],
     "xcp_bn_bwd_apply_pool": [I, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_avgpool_fwd": [I, P, P, P, P, I, I, I, P],
     "xcp_avgpool_bwd": [I, P, P, P, P, P, I, I, I, P],

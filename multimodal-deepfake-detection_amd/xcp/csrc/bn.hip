@@ -132,6 +132,8 @@ XCP_DEV void pool_grad(const PoolSrc& ps, long p, int c0, int C, float* acc) {
 // MODE 2: MODE 1 with dz masked by the ReLU that followed the BN (y*ms+mt > 0), i.e. the
 // gradient w.r.t. relu(bn(y)) given; the mask is recomputed from y, never read.
 // MODE 3: MODE 1 with dz gathered from a max-pool backward (pool_grad), never materialised.
+// MODE 4: MODE 3 that also stores the gathered dz to A (the max-pool backward and the BN
+// reduce in one pass).
 template <typename T, int MODE, int CPT>
 __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av, const void* Bv, const float* mean,
                                                       const float* invstd, const float* ms, const float* mt,
@@ -158,8 +160,12 @@ __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av,
     const long rb = (long)pchunk * r.rows_per_chunk, re = min(r.rows, rb + r.rows_per_chunk);
     for (long p = rb + slot; p < re; p += r.SPB) {
       float a[CPT];
-      if constexpr (MODE == 3) pool_grad<T, CPT>(ps, p, c0, r.C, a);
-      else VecIO<T, CPT>::load(A + p * r.C + c0, a);
+      if constexpr (MODE >= 3) {
+        pool_grad<T, CPT>(ps, p, c0, r.C, a);
+        if constexpr (MODE == 4) VecIO<T, CPT>::store(const_cast<T*>(A) + p * r.C + c0, a);
+      } else {
+        VecIO<T, CPT>::load(A + p * r.C + c0, a);
+      }
       if constexpr (MODE == 0) {
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
@@ -463,6 +469,58 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolSrc ps, T* __restr
   VecIO<T, CPT>::store(dZ + p * C + c0, acc);
 }
 
+// The same gradient computed per 2 x 2 quad of input pixels (2a..2a+1, 2b..2b+1): the quad
+// lies in windows (a..a+1, b..b+1), so each thread loads 4 windows' dOut / argmax once and
+// writes 4 pixels (the per-pixel form loads 2.25 windows per pixel).  Sums in the order of
+// pool_grad, so the result is bitwise the same.
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(PoolSrc ps, T* __restrict__ dZ, int N, int C) {
+  const T* dOut = reinterpret_cast<const T*>(ps.dOut);
+  const unsigned CV = (unsigned)C / CPT;
+  const unsigned g = blockIdx.x * 256u + threadIdx.x;
+  if (g >= (unsigned)N * ps.OH * ps.OW * CV) return;
+  const unsigned q = g / CV, c0 = (g - q * CV) * CPT;
+  const unsigned t = q / (unsigned)ps.OW, b = q - t * ps.OW;
+  const unsigned n = t / (unsigned)ps.OH, a = t - n * ps.OH;
+  const bool hb = b + 1 < (unsigned)ps.OW, ha = a + 1 < (unsigned)ps.OH;
+  float d[4][CPT];
+  unsigned am[4][2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool ok = (k & 1 ? hb : true) && (k & 2 ? ha : true);
+    const unsigned oh = a + (k >> 1), ow = b + (k & 1);
+    const long op = ((long)(n * ps.OH + (ok ? oh : a)) * ps.OW + (ok ? ow : b)) * C + c0;
+    VecIO<T, CPT>::load(dOut + op, d[k]);
+    const uint2 m = *reinterpret_cast<const uint2*>(ps.amax + op);
+    am[k][0] = ok ? m.x : 0xffffffffu;   // 0xff never matches a tap
+    am[k][1] = ok ? m.y : 0xffffffffu;
+  }
+  auto tap = [&](int k, int j) { return (am[k][j >> 2] >> (8 * (j & 3))) & 0xffu; };
+  const unsigned h0 = 2 * a, w0 = 2 * b;
+  // pixel (dy, dx) of the quad: its windows in pool_grad order and the tap it has in each
+  //   (0,0): w00 t4          (0,1): w00 t5, w01 t3
+  //   (1,0): w00 t7, w10 t1  (1,1): w00 t8, w01 t6, w10 t2, w11 t0
+#pragma unroll
+  for (int py = 0; py < 2; ++py) {
+    if (h0 + py >= (unsigned)ps.H) break;
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      if (w0 + px >= (unsigned)ps.W) break;
+      float acc[CPT];
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        float s = 0.f;
+        if (tap(0, j) == (unsigned)((1 + py) * 3 + 1 + px)) s += d[0][j];
+        if (px && tap(1, j) == (unsigned)((1 + py) * 3)) s += d[1][j];
+        if (py && tap(2, j) == (unsigned)(1 + px)) s += d[2][j];
+        if (py && px && tap(3, j) == 0u) s += d[3][j];
+        acc[j] = s;
+      }
+      VecIO<T, CPT>::store(dZ + ((long)(n * ps.H + h0 + py) * ps.W + w0 + px) * C + c0, acc);
+    }
+  }
+}
+
 // final: feats[n][c] = mean_{hw} relu(y*s+t)   (fp32 out)
 template <typename T>
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const T* __restrict__ Y, const float* s, const float* t,
@@ -501,6 +559,8 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
 
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
+int g_pool_quad = 1;   // xcp_tune knob 12: max-pool backward per input quad (1) or per pixel (0)
+
 template <typename T, int MODE>
 int chanred_launch(long rows, int C, const void* A, const void* B, const float* mean, const float* invstd, float* part,
                    hipStream_t st, const float* ms = nullptr, const float* mt = nullptr, PoolSrc ps = PoolSrc{}) {
@@ -518,6 +578,12 @@ inline PoolSrc pool_src(const void* dOut, const unsigned char* amax, int H, int 
 }
 
 }  // namespace
+
+int xcp_internal_pool_quad(int v) {
+  const int old = g_pool_quad;
+  if (v == 0 || v == 1) g_pool_quad = v;
+  return old;
+}
 
 extern "C" {
 
@@ -569,11 +635,18 @@ int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mea
 
 // xcp_bn_bwd_reduce with dZ = the MaxPool2d(3,2,1) backward of dOut [N][OH][OW][C] (argmax
 // taps amax), gathered on the fly instead of materialised; Y is [N][H][W][C]
+// (dZ, may be null: also store the gathered gradient there -- max-pool backward and BN reduce
+// in one pass)
 int xcp_bn_bwd_reduce_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, const float* mean,
-                           const float* invstd, int N, int H, int W, int C, float* part, hipStream_t st) {
+                           const float* invstd, int N, int H, int W, int C, float* part, void* dZ, hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
   const long rows = (long)N * H * W;
   const PoolSrc ps = pool_src(dOut, amax, H, W);
+  if (dZ) {
+    if (dtype == XCP_BF16) return chanred_launch<bf16, 4>(rows, C, dZ, Y, mean, invstd, part, st, nullptr, nullptr, ps);
+    if (dtype == XCP_F32) return chanred_launch<float, 4>(rows, C, dZ, Y, mean, invstd, part, st, nullptr, nullptr, ps);
+    return XCP_EUNSUPPORTED;
+  }
   if (dtype == XCP_BF16) return chanred_launch<bf16, 3>(rows, C, nullptr, Y, mean, invstd, part, st, nullptr, nullptr, ps);
   if (dtype == XCP_F32) return chanred_launch<float, 3>(rows, C, nullptr, Y, mean, invstd, part, st, nullptr, nullptr, ps);
   return XCP_EUNSUPPORTED;
@@ -701,8 +774,13 @@ int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int
 int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void* dZ, int N, int H, int W, int C,
                     hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
-  const unsigned g = nblk((long)N * H * W * (C / 8));
   const PoolSrc ps = pool_src(dOut, amax, H, W);
+  if (dtype == XCP_BF16 && g_pool_quad) {
+    const unsigned gq = nblk((long)N * ps.OH * ps.OW * (C / 8));
+    hipLaunchKernelGGL((maxpool_bwd_quad_kernel<bf16, 8>), dim3(gq), dim3(256), 0, st, ps, (bf16*)dZ, N, C);
+    return (int)hipGetLastError();
+  }
+  const unsigned g = nblk((long)N * H * W * (C / 8));
   if (dtype == XCP_BF16)
     hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, ps, (bf16*)dZ, N, C);
   else if (dtype == XCP_F32)

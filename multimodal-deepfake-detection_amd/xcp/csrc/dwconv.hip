@@ -1138,6 +1138,7 @@ int xcp_internal_conv1_tune(int v);          // stem.hip
 int xcp_internal_lstm_tune(int v);           // lstm.hip
 int xcp_internal_nt_grid(int v);             // gemm.hip
 int xcp_internal_conv3_var(int v);           // conv3.hip
+int xcp_internal_pool_quad(int v);           // bn.hip
 
 extern "C" {
 
@@ -1152,6 +1153,7 @@ int xcp_tune(int knob, int value) {
   if (knob == 9) return xcp_internal_lstm_tune(value);
   if (knob == 10) return xcp_internal_nt_grid(value);
   if (knob == 11) return xcp_internal_conv3_var(value);
+  if (knob == 12) return xcp_internal_pool_quad(value);
   if (knob == 4 || knob == 5) {
     int& k = knob == 4 ? g_dw_fwd_kernel : g_dw_bwd_kernel;
     const int old = k;

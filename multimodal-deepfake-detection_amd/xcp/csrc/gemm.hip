@@ -848,7 +848,8 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
 int g_tn_cfg = 1;
 int g_tn_wgs = 256;    // xcp_tune knob 7: target workgroups (splits x tiles) of the 256x256 kernel
 bool tn_big(int dtype, int gmode, int N, int K) {
-  return g_tn_cfg >= 1 && dtype == XCP_BF16 && gmode == 0 && N >= 128 && K >= 128;
+  // (narrower outputs stream faster through the 128-tile kernel: 0.57 vs 0.95 ms at 5.5M x 128 x 128)
+  return g_tn_cfg >= 1 && dtype == XCP_BF16 && gmode == 0 && N >= 256 && K >= 256;
 }
 
 // xcp_tune knob 3: 11 = one tile per workgroup, staggered wave groups, LDS-free register

@@ -386,9 +386,10 @@ class XceptionEngine:
         H, W, OH, OW = bs["H"], bs["W"], bs["OH"], bs["OW"]
         Ms = N * OH * OW
         units = bs["units"]
-        # pooled block: materialise the max-pool gradient once.  (Gathering it inside the BN
-        # backward reduce and apply instead -- ops.bn_backward(pool=...) -- measured slower:
-        # 1.88 vs 1.62 ms at 147^2 x 128, the 2x2-window gather being latency-bound.)
+        # pooled block: materialise the max-pool gradient once (per-quad gather kernel).
+        # Gathering it inside the BN-backward reduce instead -- ops.bn_backward(pool=...),
+        # storing it there or gathering it again in the apply -- measured slower:
+        # 1.83 / 1.88 vs 1.56 ms at 147^2 x 128.
         pool = None
         if b.pool:
             dZ = self._empty(N * H * W * b.cout)

@@ -198,11 +198,13 @@ def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=
     ``part`` ([R][2][C] partial (sum dz, sum dz*zhat)) may come fused from the
     producer of dZ; otherwise it is reduced here.  relu=True: dZ is the gradient of
     relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift).
-    pool=(dOut, amax, N, H, W): dZ (pass None) is the MaxPool2d(3,2,1) backward of dOut,
-    gathered inside the reduce / apply kernels instead of materialised."""
+    pool=(dOut, amax, N, H, W): the gradient is the MaxPool2d(3,2,1) backward of dOut,
+    gathered inside the reduce kernel; with dZ None it is gathered again by the apply
+    kernel (never materialised), otherwise the reduce also stores it into dZ (an output
+    buffer) and the apply reads it back."""
     ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
-    if pool is not None and (relu or part is not None or dZ is not None):
-        raise ValueError("pool gradient source excludes dZ, part and relu")
+    if pool is not None and (relu or part is not None):
+        raise ValueError("pool gradient source excludes part and relu")
     dev, dt = Y.device, Y.dtype
     if part is None:
         R = _lib.call("xcp_chanred_parts", rows, C)
@@ -210,7 +212,7 @@ def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=
         if pool is not None:
             dOut, amax, N, H, W = pool
             _lib.call("xcp_bn_bwd_reduce_pool", DT[dt], _p(dOut), _p(amax), _p(Y), _p(st["mean"]), _p(st["invstd"]),
-                      N, H, W, C, _p(part), stream())
+                      N, H, W, C, _p(part), _p(dZ), stream())
         else:
             _lib.call("xcp_bn_bwd_reduce", DT[dt], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), ms, mt, rows, C,
                       _p(part), stream())
@@ -220,7 +222,7 @@ def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=
     part, R = _fold(part, R, C)
     _lib.call("xcp_bn_bwd_finalize_part", _p(part), R, C, float(rows), _p(bn["weight"]), _p(st["mean"]),
               _p(st["invstd"]), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta), stream())
-    if pool is not None:
+    if pool is not None and dZ is None:
         _lib.call("xcp_bn_bwd_apply_pool", DT[dt], _p(dOut), _p(amax), _p(Y), _p(dY), _p(coef), _p(coef[C:]),
                   _p(coef[2 * C:]), N, H, W, C, stream())
     else:

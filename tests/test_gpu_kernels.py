@@ -262,7 +262,7 @@ def test_bn_forward_backward(ops, gpu, dt, rows, C, relu):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("H", [147, 37, 19])
+@pytest.mark.parametrize("H", [147, 37, 19, 20])
 def test_tail_maxpool_fwd_bwd(ops, gpu, dt, H):
     N, C = 2, 128
     g = torch.Generator(device=gpu).manual_seed(H)
@@ -284,6 +284,11 @@ def test_tail_maxpool_fwd_bwd(ops, gpu, dt, H):
     pooled.backward(d.float())
     dz = torch.empty(N * H * H, C, device=gpu, dtype=dt)
     ops.maxpool_bwd(nhwc(d), amax, dz, N, H, H, C)
+    old = ops._lib.call("xcp_tune", 12, 0)   # per-pixel form: bitwise equal to the per-quad default
+    dzp = torch.full_like(dz, float("nan"))
+    ops.maxpool_bwd(nhwc(d), amax, dzp, N, H, H, C)
+    ops._lib.call("xcp_tune", 12, old)
+    assert torch.equal(dzp, dz)
     assert rel_err(nchw(dz.view(N, H, H, C)).float(), zr.grad) < (1e-6 if dt == torch.float32 else 1e-2)
     # BN backward whose dz is this max-pool gradient, gathered on the fly: bitwise equal to
     # the materialised path (the gathered dz is rounded to the storage type the same way)
@@ -295,16 +300,21 @@ def test_tail_maxpool_fwd_bwd(ops, gpu, dt, H):
           "track": False}
     rows = N * H * H
     outs = []
-    for pool in (False, True):
+    dz2 = torch.full_like(dz, float("nan"))
+    for pool in ("no", "gather", "store"):
         dY = torch.empty(rows, C, device=gpu, dtype=dt)
         dg, db = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
-        if pool:
+        if pool == "gather":
             ops.bn_backward(None, nhwc(y), rows, C, bn, st, dY, dg, db, pool=(nhwc(d), amax, N, H, H))
+        elif pool == "store":   # max-pool backward + reduce in one pass, dz materialised by it
+            ops.bn_backward(dz2, nhwc(y), rows, C, bn, st, dY, dg, db, pool=(nhwc(d), amax, N, H, H))
         else:
             ops.bn_backward(dz, nhwc(y), rows, C, bn, st, dY, dg, db)
         outs.append((dY, dg, db))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    assert torch.equal(dz2, dz)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

@@ -100,6 +100,64 @@ def main():
             rep(f"weight_grad 728x728 tn={tn}", timeit(lambda: ops.weight_grad(D, X, M, C, C, out)),
                 flops=2.0 * M * C * C)
             ops._lib.call("xcp_tune", 6, old)
+    if "tnshape" in sel:   # the step's weight-gradient shapes, 256-tile kernel (cfg 1) vs 128-tile (cfg 0)
+        for (m, n, k) in ((5531904, 128, 128), (5531904, 128, 64), (1401856, 256, 256), (1401856, 256, 128),
+                          (350464, 728, 256), (350464, 728, 728), (92416, 1024, 728), (25600, 2048, 1536)):
+            Gt = torch.randn(m, n, device=dev, generator=g).to(dt)
+            Xt = torch.randn(m, k, device=dev, generator=g).to(dt)
+            out = torch.empty(n * k, device=dev)
+            for tn in (1, 0):
+                old = ops._lib.call("xcp_tune", 6, tn)
+                rep(f"wgrad {m}x{n}x{k} tn={tn}", timeit(lambda: ops.weight_grad(Gt, Xt, m, n, k, out), iters=10),
+                    2 * m * (n + k), flops=2.0 * m * n * k)
+                ops._lib.call("xcp_tune", 6, old)
+            del Gt, Xt
+    if "dwent" in sel:   # entry-flow depthwise shapes
+        for (n_, h_, c_) in ((256, 147, 128), (256, 147, 64), (256, 74, 256), (256, 37, 728)):
+            m_ = n_ * h_ * h_
+            Xe = torch.randn(m_, c_, device=dev, generator=g).to(dt)
+            De = torch.randn(m_, c_, device=dev, generator=g).to(dt)
+            Ye = torch.empty_like(Xe)
+            We = torch.randn(9 * c_, device=dev, generator=g) / 3
+            sce, she = torch.rand(c_, device=dev) + 0.5, torch.randn(c_, device=dev) * 0.1
+            ste = {"mean": torch.zeros(c_, device=dev), "invstd": torch.ones(c_, device=dev)}
+            dWe = torch.empty(9 * c_, device=dev)
+            tb = m_ * c_ * 2
+            rep(f"dw_fwd act=2 {h_}^2x{c_}", timeit(lambda: ops.dw_fwd(2, Xe, Ye, We, sce, she, n_, h_, h_, c_), iters=10), 2 * tb)
+            rep(f"dw_bwd act=2 +bn {h_}^2x{c_}",
+                timeit(lambda: ops.dw_bwd(2, De, Xe, We, sce, she, Ye, dWe, n_, h_, h_, c_, bn_stats=ste), iters=10), 3 * tb)
+            rep(f"copy {h_}^2x{c_}", timeit(lambda: Ye.copy_(Xe), iters=10), 2 * tb)
+            del Xe, De, Ye
+    if "poolbn" in sel:   # pooled block tail backward: max-pool gradient + BN backward
+        from xcp.engine import Stats
+        for (n_, h_, c_) in ((256, 147, 128), (256, 74, 256), (256, 37, 728)):
+            oh_ = (h_ - 1) // 2 + 1
+            m_ = n_ * h_ * h_
+            Ye = torch.randn(m_, c_, device=dev, generator=g).to(dt)
+            dOut = torch.randn(n_ * oh_ * oh_, c_, device=dev, generator=g).to(dt)
+            amax = torch.randint(0, 9, (n_ * oh_ * oh_ * c_,), device=dev, dtype=torch.uint8)
+            dZ = torch.empty(m_, c_, device=dev, dtype=dt)
+            dYe = torch.empty_like(dZ)
+            ste = Stats(c_, dev)
+            ste.mean.zero_(); ste.invstd.fill_(1.0)
+            bn = {"weight": torch.ones(c_, device=dev), "bias": torch.zeros(c_, device=dev), "running_mean": None,
+                  "running_var": None, "eps": 1e-5, "momentum": 0.1, "track": False}
+            dg, db = torch.empty(c_, device=dev), torch.empty(c_, device=dev)
+
+            def two():
+                ops.maxpool_bwd(dOut, amax, dZ, n_, h_, h_, c_)
+                ops.bn_backward(dZ, Ye, m_, c_, bn, ste, dYe, dg, db)
+
+            for qv in (0, 1):
+                old = ops._lib.call("xcp_tune", 12, qv)
+                rep(f"maxpool_bwd quad={qv} {h_}^2x{c_}", timeit(lambda: ops.maxpool_bwd(dOut, amax, dZ, n_, h_, h_, c_),
+                                                                 iters=10))
+                ops._lib.call("xcp_tune", 12, old)
+            rep(f"maxpool_bwd + bn_bwd {h_}^2x{c_}", timeit(two, iters=10))
+            rep(f"bn_bwd(pool, store) {h_}^2x{c_}",
+                timeit(lambda: ops.bn_backward(dZ, Ye, m_, c_, bn, ste, dYe, dg, db, pool=(dOut, amax, n_, h_, h_)),
+                       iters=10))
+            del Ye, dZ, dYe
     if "tnabl" in sel:
         out = torch.empty(C * C, device=dev)
         P = torch.empty(28 * C * C, device=dev)
