@@ -111,6 +111,13 @@ int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int
                  const float* t2, void* Out, unsigned char* amax, int N, int H, int W, int C, xcp_stream_t stream);
 int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void* dZ, int N, int H, int W, int C,
                     xcp_stream_t stream);
+/* xcp_maxpool_bwd fused with the BatchNorm-backward reduce (Xception.py:85-86: the BN before
+ * the pool) of its output against Y [N][H][W][C]: part[P][2][C] = per-chunk (sum dz,
+ * sum dz*(y-mean)*invstd), P = xcp_maxpool_bwd_bnred_parts(...) */
+int xcp_maxpool_bwd_bnred_parts(int N, int H, int W, int C);
+int xcp_maxpool_bwd_bnred(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
+                          const float* mean, const float* invstd, int N, int H, int W, int C, float* part,
+                          xcp_stream_t stream);
 /* BatchNorm backward reduce / apply whose dZ is the MaxPool2d(3,2,1) backward (Xception.py:86)
  * of dOut [N][OH][OW][C] with argmax taps amax, gathered on the fly; Y / dY are [N][H][W][C].
  * reduce: dZ (may be null) receives the gathered gradient (max-pool backward + BN reduce in one

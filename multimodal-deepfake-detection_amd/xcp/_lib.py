@@ -41,6 +41,8 @@ SIGNATURES = {
     "xcp_relu_bwd": [I, P, P, L, I, P],
     "xcp_tail_fwd": [I, P, P, P, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_maxpool_bwd": [I, P, P, P, I, I, I, I, P],
+    "xcp_maxpool_bwd_bnred_parts": [I, I, I, I],
+    "xcp_maxpool_bwd_bnred": [I, P, P, P, P, P, P, I, I, I, I, P, P],
     "xcp_bn_bwd_reduce_pool": [I, P, P, P, P, P, I, I, I, I, P, P, P],
     "xcp_bn_bwd_apply_pool": [I, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_avgpool_fwd": [I, P, P, P, P, I, I, I, P],
@@ -62,7 +64,8 @@ SIGNATURES = {
 
 # entry points that return a size, not a status
 SIZE_QUERIES = {"xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts", "xcp_tune",
-                "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts"}
+                "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
+                "xcp_maxpool_bwd_bnred_parts"}
 
 _lib = None
 

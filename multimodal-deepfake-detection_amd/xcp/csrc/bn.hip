@@ -473,15 +473,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolSrc ps, T* __restr
 // lies in windows (a..a+1, b..b+1), so each thread loads 4 windows' dOut / argmax once and
 // writes 4 pixels (the per-pixel form loads 2.25 windows per pixel).  Sums in the order of
 // pool_grad, so the result is bitwise the same.
+// quad q = (n, a, b): fill g[py*2+px][j] with the gradient of input pixel (2a+py, 2b+px)
+// (rounded to T; pixels past H / W are left out by the callers)
 template <typename T, int CPT>
-__global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(PoolSrc ps, T* __restrict__ dZ, int N, int C) {
+XCP_DEV void pool_quad(const PoolSrc& ps, unsigned n, unsigned a, unsigned b, int C, unsigned c0,
+                       float (&g)[4][CPT]) {
   const T* dOut = reinterpret_cast<const T*>(ps.dOut);
-  const unsigned CV = (unsigned)C / CPT;
-  const unsigned g = blockIdx.x * 256u + threadIdx.x;
-  if (g >= (unsigned)N * ps.OH * ps.OW * CV) return;
-  const unsigned q = g / CV, c0 = (g - q * CV) * CPT;
-  const unsigned t = q / (unsigned)ps.OW, b = q - t * ps.OW;
-  const unsigned n = t / (unsigned)ps.OH, a = t - n * ps.OH;
   const bool hb = b + 1 < (unsigned)ps.OW, ha = a + 1 < (unsigned)ps.OH;
   float d[4][CPT];
   unsigned am[4][2];
@@ -496,17 +493,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(PoolSrc ps, T* __
     am[k][1] = ok ? m.y : 0xffffffffu;
   }
   auto tap = [&](int k, int j) { return (am[k][j >> 2] >> (8 * (j & 3))) & 0xffu; };
-  const unsigned h0 = 2 * a, w0 = 2 * b;
-  // pixel (dy, dx) of the quad: its windows in pool_grad order and the tap it has in each
+  // pixel (py, px) of the quad: its windows in pool_grad order and the tap it has in each
   //   (0,0): w00 t4          (0,1): w00 t5, w01 t3
   //   (1,0): w00 t7, w10 t1  (1,1): w00 t8, w01 t6, w10 t2, w11 t0
 #pragma unroll
-  for (int py = 0; py < 2; ++py) {
-    if (h0 + py >= (unsigned)ps.H) break;
+  for (int py = 0; py < 2; ++py)
 #pragma unroll
-    for (int px = 0; px < 2; ++px) {
-      if (w0 + px >= (unsigned)ps.W) break;
-      float acc[CPT];
+    for (int px = 0; px < 2; ++px)
 #pragma unroll
       for (int j = 0; j < CPT; ++j) {
         float s = 0.f;
@@ -514,11 +507,80 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(PoolSrc ps, T* __
         if (px && tap(1, j) == (unsigned)((1 + py) * 3)) s += d[1][j];
         if (py && tap(2, j) == (unsigned)(1 + px)) s += d[2][j];
         if (py && px && tap(3, j) == 0u) s += d[3][j];
-        acc[j] = s;
+        g[py * 2 + px][j] = rnd<T>(s);
       }
-      VecIO<T, CPT>::store(dZ + ((long)(n * ps.H + h0 + py) * ps.W + w0 + px) * C + c0, acc);
+}
+
+// The max-pool gradient computed per 2 x 2 quad of input pixels (2a..2a+1, 2b..2b+1): the
+// quad lies in windows (a..a+1, b..b+1), so each thread loads 4 windows' dOut / argmax once
+// and writes 4 pixels (the per-pixel form loads 2.25 windows per pixel).  Sums in the order
+// of pool_grad, so the result is bitwise the same.
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(PoolSrc ps, T* __restrict__ dZ, int N, int C) {
+  const unsigned CV = (unsigned)C / CPT;
+  const unsigned gi = blockIdx.x * 256u + threadIdx.x;
+  if (gi >= (unsigned)N * ps.OH * ps.OW * CV) return;
+  const unsigned q = gi / CV, c0 = (gi - q * CV) * CPT;
+  const unsigned t = q / (unsigned)ps.OW, b = q - t * ps.OW;
+  const unsigned n = t / (unsigned)ps.OH, a = t - n * ps.OH;
+  float g[4][CPT];
+  pool_quad<T, CPT>(ps, n, a, b, C, c0, g);
+#pragma unroll
+  for (int py = 0; py < 2; ++py) {
+    if (2 * a + py >= (unsigned)ps.H) break;
+#pragma unroll
+    for (int px = 0; px < 2; ++px) {
+      if (2 * b + px >= (unsigned)ps.W) break;
+      VecIO<T, CPT>::store(dZ + ((long)(n * ps.H + 2 * a + py) * ps.W + 2 * b + px) * C + c0, g[py * 2 + px]);
     }
   }
+}
+
+// The same, fused with the BatchNorm-backward reduce of the BN that precedes the pool:
+// part[P][2][C] = per-chunk (sum dz, sum dz*(y-mean)*invstd) over the stored dz (chanred
+// layout, ChanRed over quads).
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc ps, T* __restrict__ dZ,
+                                                              const T* __restrict__ Y, const float* mean,
+                                                              const float* invstd, float* part) {
+  const int cchunk = blockIdx.x % r.nch, pchunk = blockIdx.x / r.nch;
+  const int lcv = threadIdx.x % r.CVB, slot = threadIdx.x / r.CVB;
+  const int cv = cchunk * r.CVB + lcv;
+  const int c0 = cv * CPT;
+  float acc[2][CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) acc[0][j] = acc[1][j] = 0.f;
+  if (slot < r.SPB && cv < r.CV) {
+    float mu[CPT], is[CPT];
+    VecIO<float, CPT>::load(mean + c0, mu);
+    VecIO<float, CPT>::load(invstd + c0, is);
+    const long rb = (long)pchunk * r.rows_per_chunk, re = min(r.rows, rb + r.rows_per_chunk);
+    for (long p = rb + slot; p < re; p += r.SPB) {
+      const unsigned q = (unsigned)p;
+      const unsigned t = q / (unsigned)ps.OW, b = q - t * ps.OW;
+      const unsigned n = t / (unsigned)ps.OH, a = t - n * ps.OH;
+      float y[4][CPT];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned h = min(2 * a + (k >> 1), (unsigned)ps.H - 1), w = min(2 * b + (k & 1), (unsigned)ps.W - 1);
+        VecIO<T, CPT>::load(Y + ((long)(n * ps.H + h) * ps.W + w) * r.C + c0, y[k]);
+      }
+      float g[4][CPT];
+      pool_quad<T, CPT>(ps, n, a, b, r.C, (unsigned)c0, g);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned h = 2 * a + (k >> 1), w = 2 * b + (k & 1);
+        if (h >= (unsigned)ps.H || w >= (unsigned)ps.W) continue;
+        VecIO<T, CPT>::store(dZ + ((long)(n * ps.H + h) * ps.W + w) * r.C + c0, g[k]);
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+          acc[0][j] += g[k][j];
+          acc[1][j] = fmaf(g[k][j], (y[k][j] - mu[j]) * is[j], acc[1][j]);
+        }
+      }
+    }
+  }
+  chanred_finish<CPT>(r, acc, part, cchunk, pchunk, lcv, slot);
 }
 
 // final: feats[n][c] = mean_{hw} relu(y*s+t)   (fp32 out)
@@ -785,6 +847,33 @@ int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void
     hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, ps, (bf16*)dZ, N, C);
   else if (dtype == XCP_F32)
     hipLaunchKernelGGL((maxpool_bwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, ps, (float*)dZ, N, C);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+// partial rows (P) of xcp_maxpool_bwd_bnred
+int xcp_maxpool_bwd_bnred_parts(int N, int H, int W, int C) {
+  const long quads = (long)N * ((H - 1) / 2 + 1) * ((W - 1) / 2 + 1);
+  return (int)chanred_P(make_chanred(quads, C, 8, 1024));
+}
+
+// xcp_maxpool_bwd + the BN-backward reduce of its output against Y [N][H][W][C] in one pass:
+// part[P][2][C] = (sum dz, sum dz*(y-mean)*invstd) partials, as xcp_bn_bwd_reduce
+int xcp_maxpool_bwd_bnred(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
+                          const float* mean, const float* invstd, int N, int H, int W, int C, float* part,
+                          hipStream_t st) {
+  if (C % 8) return XCP_EINVAL;
+  const PoolSrc ps = pool_src(dOut, amax, H, W);
+  const ChanRed r = make_chanred((long)N * ps.OH * ps.OW, C, 8, 1024);
+  const long P = chanred_P(r);
+  const size_t smem = (size_t)r.SPB * 2 * r.CVB * 8 * sizeof(float);
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((maxpool_bwd_red_kernel<bf16, 8>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, ps,
+                       (bf16*)dZ, (const bf16*)Y, mean, invstd, part);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((maxpool_bwd_red_kernel<float, 8>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, ps,
+                       (float*)dZ, (const float*)Y, mean, invstd, part);
   else
     return XCP_EUNSUPPORTED;
   return (int)hipGetLastError();

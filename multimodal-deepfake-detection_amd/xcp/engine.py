@@ -386,14 +386,15 @@ class XceptionEngine:
         H, W, OH, OW = bs["H"], bs["W"], bs["OH"], bs["OW"]
         Ms = N * OH * OW
         units = bs["units"]
-        # pooled block: materialise the max-pool gradient once (per-quad gather kernel).
-        # Gathering it inside the BN-backward reduce instead -- ops.bn_backward(pool=...),
-        # storing it there or gathering it again in the apply -- measured slower:
-        # 1.83 / 1.88 vs 1.56 ms at 147^2 x 128.
+        # pooled block: one pass materialises the max-pool gradient (per-quad gather) and
+        # reduces it for the last unit's BN backward (1.50 vs 1.58 ms with a separate reduce
+        # at 147^2 x 128).  Gathering it inside the BN-backward kernels instead --
+        # ops.bn_backward(pool=...) -- measured slower: 1.83 / 1.88 ms.
         pool = None
+        part = None
         if b.pool:
             dZ = self._empty(N * H * W * b.cout)
-            ops.maxpool_bwd(dOut, bs["amax"], dZ, N, H, W, b.cout)
+            part = ops.maxpool_bwd_bnred(dOut, bs["amax"], dZ, units[-1]["y"], units[-1]["st"], N, H, W, b.cout)
         else:
             dZ = dOut
         dRes = dSkip = None
@@ -411,7 +412,6 @@ class XceptionEngine:
                 dRes = dXs
         else:
             dRes = dOut
-        part = None
         for i in range(len(b.units) - 1, -1, -1):
             u, rec = b.units[i], units[i]
             src = pool if i == len(b.units) - 1 else None

@@ -247,6 +247,16 @@ def maxpool_bwd(dOut, amax, dZ, N, H, W, C):
     _lib.call("xcp_maxpool_bwd", DT[dOut.dtype], _p(dOut), _p(amax), _p(dZ), N, H, W, C, stream())
 
 
+def maxpool_bwd_bnred(dOut, amax, dZ, Y, st, N, H, W, C):
+    """maxpool_bwd into dZ plus the BN-backward reduce of dZ against Y (st: that BN's Stats)
+    in one pass.  Returns (part [P][2][C], P) for bn_backward(part=...)."""
+    R = _lib.call("xcp_maxpool_bwd_bnred_parts", N, H, W, C)
+    part = torch.empty(R * 2 * C, device=Y.device, dtype=torch.float32)
+    _lib.call("xcp_maxpool_bwd_bnred", DT[dOut.dtype], _p(dOut), _p(amax), _p(dZ), _p(Y), _p(st["mean"]),
+              _p(st["invstd"]), N, H, W, C, _p(part), stream())
+    return part, R
+
+
 def avgpool_fwd(Y, s, t, F, N, HW, C):
     _lib.call("xcp_avgpool_fwd", DT[Y.dtype], _p(Y), _p(s), _p(t), _p(F), N, HW, C, stream())
 

@@ -32,8 +32,10 @@ def fake_lib(monkeypatch):
             return 3
         if name in ("xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows"):
             return 256
-        if name == "xcp_conv3x3_parts":
+        if name in ("xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts"):
             return 9
+        if name == "xcp_maxpool_bwd_bnred_parts":
+            return 4
         return 0
 
     monkeypatch.setattr(_lib, "call", fake_call)
@@ -63,8 +65,8 @@ def test_lstmv_step_call_sequence(fake_lib, unfrozen):
     names = set(fake_lib)
     assert {"xcp_gemm_nt", "xcp_dw_fwd", "xcp_tail_fwd", "xcp_avgpool_fwd", "xcp_lstm_fwd", "xcp_lstm_bwd"} <= names
     if unfrozen:
-        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd", "xcp_conv1_wgrad",
-                "xcp_conv3x3"} <= names
+        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd_bnred", "xcp_conv1_wgrad",
+                "xcp_conv3x3", "xcp_conv3x3_wgrad"} <= names
         for n, p in m.feature_extractor.named_parameters():
             assert p.grad is not None and p.grad.shape == p.shape, n
     else:

@@ -315,6 +315,17 @@ def test_tail_maxpool_fwd_bwd(ops, gpu, dt, H):
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
+    # max-pool backward fused with the BN reduce: same dz bit for bit, same BN backward up to
+    # the fp32 summation order of the partials
+    dz3 = torch.full_like(dz, float("nan"))
+    part, R = ops.maxpool_bwd_bnred(nhwc(d), amax, dz3, nhwc(y), st, N, H, H, C)
+    assert torch.equal(dz3, dz)
+    dY = torch.empty(rows, C, device=gpu, dtype=dt)
+    dg, db = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+    ops.bn_backward(dz3, nhwc(y), rows, C, bn, st, dY, dg, db, part=part, R=R)
+    torch.testing.assert_close(dg, outs[0][1], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(db, outs[0][2], rtol=1e-4, atol=1e-4)
+    assert rel_err(dY.float(), outs[0][0].float()) < (1e-5 if dt == torch.float32 else 1e-2)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

@@ -154,6 +154,14 @@ def main():
                                                                  iters=10))
                 ops._lib.call("xcp_tune", 12, old)
             rep(f"maxpool_bwd + bn_bwd {h_}^2x{c_}", timeit(two, iters=10))
+
+            def fused():
+                part, R = ops.maxpool_bwd_bnred(dOut, amax, dZ, Ye, ste, n_, h_, h_, c_)
+                ops.bn_backward(dZ, Ye, m_, c_, bn, ste, dYe, dg, db, part=part, R=R)
+
+            rep(f"maxpool_bwd_bnred + apply {h_}^2x{c_}", timeit(fused, iters=10))
+            rep(f"maxpool_bwd_bnred alone {h_}^2x{c_}",
+                timeit(lambda: ops.maxpool_bwd_bnred(dOut, amax, dZ, Ye, ste, n_, h_, h_, c_), iters=10))
             rep(f"bn_bwd(pool, store) {h_}^2x{c_}",
                 timeit(lambda: ops.bn_backward(dZ, Ye, m_, c_, bn, ste, dYe, dg, db, pool=(dOut, amax, n_, h_, h_)),
                        iters=10))
