@@ -1040,7 +1040,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   const int id = xcd_remap(blockIdx.x, gridDim.x);   // one split's tiles share an XCD (its rows stay in L2)
   const int sp = id / tiles, t = id % tiles;
   const int n0 = (t / gridK) * 256, k0 = (t % gridK) * 256;
-  const int mbeg = sp * a.rows_per_split;
+  const int mbeg = ABL >= 3 ? 0 : sp * a.rows_per_split;   // ABL 3, 4 (measurement): every split reads split 0 rows
   const int mend = min(a.M, mbeg + a.rows_per_split);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 2, wc = w & 3;
@@ -1111,7 +1111,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (ABL == 2) {
+    if constexpr (ABL == 2 || ABL == 4) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(xf[i]), "v"(gf[i]));
     } else {
@@ -1384,7 +1384,7 @@ int xcp_internal_tn_tune(int knob, int v) {
 
 int xcp_internal_gemm_var(int v) {
   const int old = g_nt256_var;
-  if (v >= 0 && v <= 11) g_nt256_var = v;
+  if (v >= 0 && v <= 13) g_nt256_var = v;
   return old;
 }
 
@@ -1431,6 +1431,8 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
     const dim3 grid(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S);
     if (g_nt256_var == 5) hipLaunchKernelGGL(gemm_tn256_kernel<1>, grid, dim3(512), 0, stream, a);
     else if (g_nt256_var == 6) hipLaunchKernelGGL(gemm_tn256_kernel<2>, grid, dim3(512), 0, stream, a);
+    else if (g_nt256_var == 12) hipLaunchKernelGGL(gemm_tn256_kernel<3>, grid, dim3(512), 0, stream, a);
+    else if (g_nt256_var == 13) hipLaunchKernelGGL(gemm_tn256_kernel<4>, grid, dim3(512), 0, stream, a);
     else if (g_tn_cfg == 1) hipLaunchKernelGGL(gemm_tn256_kernel<0>, grid, dim3(512), 0, stream, a);
     else hipLaunchKernelGGL(gemm_tn256r4_kernel, grid, dim3(512), 0, stream, a);
     return (int)hipGetLastError();

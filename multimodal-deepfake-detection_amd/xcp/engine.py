@@ -16,6 +16,7 @@ One engine serves one ``Xception`` module; it is driven through
 ``XceptionFunction`` so autograd sees a single node whose inputs are the frames and
 every backbone parameter.
 """
+import os
 import math
 
 import torch
@@ -93,6 +94,10 @@ class Stats:
         return getattr(self, k)
 
 
+# pointwise weight gradients on a side stream (XCP_WGRAD_STREAM=0 keeps them in order)
+WGRAD_SIDE_STREAM = os.environ.get("XCP_WGRAD_STREAM", "1") != "0"
+
+
 class XceptionEngine:
     def __init__(self, model, dtype=torch.bfloat16):
         if dtype not in (torch.float32, torch.bfloat16):
@@ -113,6 +118,12 @@ class XceptionEngine:
         self._packed_bwd_key = None
         self._bufs = {}
         self._pack_fwd, self._pack_bwd = ops.PermuteBatch(), ops.PermuteBatch()
+
+    def _side_stream(self, dev):
+        st = getattr(self, "_side", None)
+        if st is None or st.device != dev:
+            st = self._side = torch.cuda.Stream(dev)
+        return st
 
     # ------------------------------------------------------------ parameters
     def named_params(self):
@@ -325,6 +336,22 @@ class XceptionEngine:
             grads[name] = t
             return t
 
+        # Pointwise weight gradients run on a side stream: they depend only on dY (and a saved
+        # activation), nothing downstream waits for them until the backward returns, so they
+        # overlap the dgrad GEMMs and depthwise backward kernels of the main stream.
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev) if WGRAD_SIDE_STREAM else None
+
+        def wgrad(*args, **kw):
+            if side is None:
+                ops.weight_grad(*args, **kw)
+                return
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                ops.weight_grad(*args, **kw)
+            for t in (args[0], args[1], args[5]):   # G, X, out: kept alive for the side stream
+                t.record_stream(side)
+
         def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False, pool=None):
             dY = self._empty(rows * C)
             P = part[1] if part is not None else 0
@@ -344,7 +371,7 @@ class XceptionEngine:
             dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part, pool=pool)
             dD = self._empty(M * u.cin)
             ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, u.cin, u.cout)
-            ops.weight_grad(dY, rec["d"], M, u.cout, u.cin, g(u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1)))
+            wgrad(dY, rec["d"], M, u.cout, u.cin, g(u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1)))
             dX = self._empty(M * u.cin)
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX,
                              g(u.name + ".conv1.weight", (u.cin, 1, 3, 3)), N, H, W, u.cin, dRes=dRes, dSkip=dSkip,
@@ -362,7 +389,7 @@ class XceptionEngine:
         dX, _ = unit_bwd(u3, e3, dZ3, H, W, part=p3)
         # ---- blocks, last to first
         for b, bs in zip(reversed(self.blocks), reversed(S["blocks"])):
-            dX = self._block_bwd(b, bs, dX, N, pk, g, bn_bwd, unit_bwd)
+            dX = self._block_bwd(b, bs, dX, N, pk, g, bn_bwd, unit_bwd, wgrad)
         # ---- stem
         OH1, OW1, OH2, OW2 = S["OH1"], S["OW1"], S["OH2"], S["OW2"]
         rows1, rows2 = N * OH1 * OW1, N * OH2 * OW2
@@ -380,9 +407,11 @@ class XceptionEngine:
         ops.permute3(w2g, g("conv2.weight", (64, 32, 3, 3)), 64, 9, 32, (0, 2, 1))
         dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], relu=True)   # relu (Xception.py:170) fused
         ops.conv1_wgrad(S["x"], dC1, g("conv1.weight", (32, 3, 3, 3)), N, S["IH"], S["IW"])
+        if side is not None:
+            main.wait_stream(side)
         return grads
 
-    def _block_bwd(self, b, bs, dOut, N, pk, g, bn_bwd, unit_bwd):
+    def _block_bwd(self, b, bs, dOut, N, pk, g, bn_bwd, unit_bwd, wgrad):
         H, W, OH, OW = bs["H"], bs["W"], bs["OH"], bs["OW"]
         Ms = N * OH * OW
         units = bs["units"]
@@ -401,7 +430,7 @@ class XceptionEngine:
         skip_geom = (0, 0, 1)
         if b.skip is not None:
             dYs = bn_bwd(b.skipbn, b.name + ".skipbn", dOut, bs["ys"], Ms, b.cout, bs["sks"])
-            ops.weight_grad(dYs, bs["x_in"], Ms, b.cout, b.cin, g(b.name + ".skip.weight", (b.cout, b.cin, 1, 1)),
+            wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, g(b.name + ".skip.weight", (b.cout, b.cin, 1, 1)),
                             gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0),
                             ldx=b.cin)
             dXs = self._empty(Ms * b.cin)

@@ -40,6 +40,8 @@ def fake_lib(monkeypatch):
 
     monkeypatch.setattr(_lib, "call", fake_call)
     monkeypatch.setattr(ops, "check_gpu", lambda *a: None)
+    from xcp import engine
+    monkeypatch.setattr(engine, "WGRAD_SIDE_STREAM", False)   # no HIP streams on the CPU
 
     class _S:
         cuda_stream = 0

@@ -171,7 +171,7 @@ def main():
         P = torch.empty(28 * C * C, device=dev)
         rps = ops._lib.call("xcp_gemm_tn_rows_per_split", 1, 0, M, C, C)
         S = (M + rps - 1) // rps
-        for var in (0, 5, 6):
+        for var in [int(v) for v in os.environ.get("XCP_VARS", "0,5,6").split(",")]:
             old = ops._lib.call("xcp_tune", 3, var)
             rep(f"gemm_tn kernel only S={S} var={var}", timeit(lambda: ops.gemm_tn(D, X, P, M, C, C, S, rps)),
                 flops=2.0 * M * C * C)
