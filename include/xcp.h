@@ -162,6 +162,11 @@ int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, in
 int xcp_frames_u8_to_f32(const unsigned char* in, const int* len, float* out, int B, int Tmax, int H, int W,
                          xcp_stream_t stream);
 
+/* ---- audio front end (XceptionLSTMA.py:44-46): F.interpolate(bilinear, align_corners=False) ----
+ * out [NC][OH][OW] fp32 = bilinear resize of in [NC][IH][IW] fp32 (ATen's source-index and
+ * weight formulas in fp32); MFCC frames [B*T*3][13][1] -> [B*T*3][64][64] */
+int xcp_resize_bilinear(const float* in, float* out, int NC, int IH, int IW, int OH, int OW, xcp_stream_t stream);
+
 /* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][10] int64
  * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block), nblocks in total */
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream_t stream);

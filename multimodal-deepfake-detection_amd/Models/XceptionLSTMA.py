@@ -2,12 +2,12 @@
 
 Same module surface as the reference.  ``extract_features`` reshapes
 ``[B,T,3,13]`` to ``[B*T,3,13,1]``, resizes bilinearly to 64x64
-(align_corners=False, XceptionLSTMA.py:46) and runs the xcp backbone.
+(align_corners=False, XceptionLSTMA.py:46) with the HIP kernel ``xcp_resize_bilinear``
+and runs the xcp backbone.
 """
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
-
+from xcp import ops
 from xcp.lstm import LSTM
 
 from .Xception import xception
@@ -35,7 +35,7 @@ class XceptionLSTMA(nn.Module):
             self.feature_extractor.to(device)
         batch_size, time_steps, c, n_mfcc = audio_batch.shape
         frames = audio_batch.reshape(batch_size * time_steps, c, n_mfcc, 1)
-        frames = F.interpolate(frames, size=(64, 64), mode="bilinear", align_corners=False)
+        frames = ops.resize_bilinear(frames, (64, 64))
         frame_features = self.feature_extractor(frames)
         return frame_features.view(batch_size, time_steps, frame_features.shape[-1])
 

@@ -46,6 +46,44 @@ __global__ __launch_bounds__(256) void frames_u8_kernel(const unsigned char* __r
     *reinterpret_cast<float4*>(out + (((frame * 3 + c) * H + h) * W + w0)) = make_float4(v[c][0], v[c][1], v[c][2], v[c][3]);
 }
 
+
+// Bilinear resize, align_corners=False (F.interpolate(..., mode="bilinear"), as the audio
+// front end XceptionLSTMA.py:46 uses it: MFCC [B*T, 3, 13, 1] -> [B*T, 3, 64, 64]).
+// Source coordinates, indices and weights follow ATen's upsample_bilinear2d in fp32:
+//   src = max(scale * (dst + 0.5) - 0.5, 0), scale = in / out, i0 = min(floor(src), in - 1),
+//   i1 = i0 + (i0 < in - 1), l1 = clamp(src - i0, 0, 1), l0 = 1 - l1,
+//   out = (a * w0 + b * w1) * h0 + (c * w0 + d * w1) * h1  (products, then sums).
+// in [NC][IH][IW], out [NC][OH][OW] fp32; one thread per output pixel.
+XCP_DEV void lin_idx(int dst, int in, float scale, int& i0, int& i1, float& l0, float& l1) {
+#pragma clang fp contract(off)
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  src = src < 0.f ? 0.f : src;
+  i0 = min((int)floorf(src), in - 1);
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  float l = src - (float)i0;
+  l = l < 0.f ? 0.f : (l > 1.f ? 1.f : l);
+  l1 = l;
+  l0 = 1.f - l;
+}
+
+__global__ __launch_bounds__(256) void resize_bilinear_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                              int IH, int IW, int OH, int OW, float sh, float sw,
+                                                              long total) {
+#pragma clang fp contract(off)
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= total) return;
+  const long plane = g / ((long)OH * OW);
+  const int r = (int)(g - plane * OH * OW), oh = r / OW, ow = r - oh * OW;
+  int h0, h1, w0, w1;
+  float lh0, lh1, lw0, lw1;
+  lin_idx(oh, IH, sh, h0, h1, lh0, lh1);
+  lin_idx(ow, IW, sw, w0, w1, lw0, lw1);
+  const float* p = in + plane * IH * IW;
+  const float t0 = p[h0 * IW + w0] * lw0 + p[h0 * IW + w1] * lw1;
+  const float t1 = p[h1 * IW + w0] * lw0 + p[h1 * IW + w1] * lw1;
+  out[g] = t0 * lh0 + t1 * lh1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -58,6 +96,16 @@ int xcp_frames_u8_to_f32(const unsigned char* in, const int* len, float* out, in
   const long total = (long)B * Tmax * H * (W / 4);
   hipLaunchKernelGGL(frames_u8_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, len, out, Tmax, H,
                      W, total);
+  return (int)hipGetLastError();
+}
+
+// out [NC][OH][OW] = bilinear resize (align_corners=False) of in [NC][IH][IW], fp32
+int xcp_resize_bilinear(const float* in, float* out, int NC, int IH, int IW, int OH, int OW, hipStream_t st) {
+  if (NC <= 0 || OH <= 0 || OW <= 0) return XCP_OK;
+  if (IH <= 0 || IW <= 0) return XCP_EINVAL;
+  const long total = (long)NC * OH * OW;
+  hipLaunchKernelGGL(resize_bilinear_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, out, IH, IW,
+                     OH, OW, (float)IH / (float)OH, (float)IW / (float)OW, total);
   return (int)hipGetLastError();
 }
 

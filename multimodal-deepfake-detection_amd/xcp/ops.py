@@ -288,6 +288,20 @@ def frames_u8_to_f32(frames, lengths, out):
     _lib.call("xcp_frames_u8_to_f32", _p(frames), _p(lengths), _p(out), B, T, H, W, stream())
 
 
+def resize_bilinear(x, size):
+    """F.interpolate(x, size, mode="bilinear", align_corners=False) for fp32 NCHW x on the GPU
+    (the XceptionLSTMA front end, XceptionLSTMA.py:46)."""
+    check_gpu(x)
+    if x.dtype != torch.float32 or x.dim() != 4:
+        raise ValueError("resize_bilinear: expects fp32 [N, C, H, W]")
+    x = x.contiguous()
+    N, C, IH, IW = x.shape
+    OH, OW = size
+    out = torch.empty((N, C, OH, OW), device=x.device, dtype=torch.float32)
+    _lib.call("xcp_resize_bilinear", _p(x), _p(out), N * C, IH, IW, OH, OW, stream())
+    return out
+
+
 def conv3x3_parts(mode, N, IH, IW):
     return _lib.call("xcp_conv3x3_parts", mode, N, IH, IW)
 

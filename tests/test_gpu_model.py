@@ -208,3 +208,48 @@ def test_bf16_gradient_noise_vs_torch_autocast(gpu):
     print(f"median cos: xcp-bf16 {np.median(c16):.4f}  torch-autocast-bf16 {np.median(cau):.4f}; "
           f"min: {c16.min():.4f} / {cau.min():.4f}")
     assert np.median(c16) >= np.median(cau) - 0.02
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_xceptionlstma_step_vs_reference(gpu, golden, prec):
+    """XceptionLSTMA(512) audio step (B=2, T=6 MFCC clips, frozen backbone as shipped):
+    the HIP bilinear front end against the reference's F.interpolate frames (rel 1e-6),
+    then features / logits / loss / head gradient norms at the tolerances above."""
+    import xcp
+    from xcp import ops
+    from Models.XceptionLSTMA import XceptionLSTMA
+    g = golden("audio_b2t6.npz")
+    B, T = int(g["B"]), int(g["T"])
+    x = seeded_normal((B, T, 3, 13), 777).to(gpu)
+    frames = ops.resize_bilinear(x.reshape(B * T, 3, 13, 1), (64, 64))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(frames[:2].cpu().numpy(), g["frames"], rtol=1e-6, atol=1e-7)
+    f = frames.detach().double().reshape(-1).cpu().numpy()
+    np.testing.assert_allclose(f[g["frames_fp/idx"]], g["frames_fp/val"], rtol=1e-6, atol=1e-7)
+    torch.manual_seed(0)
+    m = XceptionLSTMA(512, pretrained=False).to(gpu).train()
+    m.fc_layers.eval()
+    logits = {}
+    m.fc_out.register_forward_hook(lambda mod, i, o: logits.__setitem__("v", o.detach()))
+    y = torch.tensor([[1.0], [0.0]], device=gpu)[:B]
+    with xcp.precision(prec):
+        feats = m.extract_features(x, gpu)
+        prob = m(feats)
+        loss = nn.BCELoss()(prob, y)
+        loss.backward()
+    torch.cuda.synchronize()
+    f32 = prec == "fp32"
+    if f32:
+        assert relerr(feats.detach().cpu(), g["features"]) < 1e-4
+    else:
+        assert cos(feats.detach().cpu(), g["features"]) > 0.999
+    np.testing.assert_allclose(logits["v"].cpu().numpy(), g["logits"], atol=1e-4 if f32 else 3e-2, rtol=0)
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-5 if f32 else 2e-2)
+    errs = {}
+    for n, p in m.named_parameters():
+        key = f"gradnorm/{n}"
+        if p.grad is None:
+            assert key not in g, n
+            continue
+        errs[n] = abs(p.grad.double().norm().item() - g[key]) / max(g[key], 1e-30)
+    check_gradnorms(errs, bn_param_names(m), f32)

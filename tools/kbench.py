@@ -113,7 +113,10 @@ def main():
                 ops._lib.call("xcp_tune", 6, old)
             del Gt, Xt
     if "dwent" in sel:   # entry-flow depthwise shapes
-        for (n_, h_, c_) in ((256, 147, 128), (256, 147, 64), (256, 74, 256), (256, 37, 728)):
+        shapes = os.environ.get("XCP_DWSHAPES")
+        shapes = [tuple(int(v) for v in t.split("x")) for t in shapes.split(",")] if shapes else \
+            [(256, 147, 128), (256, 147, 64), (256, 74, 256), (256, 37, 728)]
+        for (n_, h_, c_) in shapes:
             m_ = n_ * h_ * h_
             Xe = torch.randn(m_, c_, device=dev, generator=g).to(dt)
             De = torch.randn(m_, c_, device=dev, generator=g).to(dt)
