@@ -8,6 +8,10 @@ Adam(lr 1e-5, wd 1e-4) (train_visual.py:540-577 semantics).  Default mode is the
 unfrozen backbone (train_visual.py:551-556, every epoch after the 3rd); the
 frozen backbone (as shipped, XceptionLSTMV.py:15-16) is ``--mode frozen``.
 
+``--model lstma`` runs the audio configuration instead (C4: XceptionLSTMA(512) on MFCC
+clips [b, 120, 3, 13] resized to 64x64 on the GPU, frozen backbone as shipped,
+Adam lr 1e-4, train_audio.py:33-44); it is a secondary line, not the headline metric.
+
 Launch: ``python bench.py [--gpus N --steps K --warmup W]``; N>1 under
 ``torch.distributed.run`` (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from env).
 Rank 0 prints ONE JSON line.
@@ -36,34 +40,54 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", choices=["lstmv", "lstma"], default="lstmv")
     ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
-    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--frames", type=int, default=None, help="frames per clip (default 16; 120 for lstma)")
     ap.add_argument("--size", type=int, default=299)
-    ap.add_argument("--mode", choices=["unfrozen", "frozen"], default="unfrozen")
+    ap.add_argument("--mode", choices=["unfrozen", "frozen"], default=None,
+                    help="backbone training (default unfrozen; frozen for lstma, as shipped)")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-kernel-timing", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    audio = a.model == "lstma"
+    a.frames = a.frames or (120 if audio else 16)
+    a.mode = a.mode or ("frozen" if audio else "unfrozen")
+    if audio:
+        a.size = 64
+    return a
+
+
+def middle_hw(size):
+    """Spatial size of the 728-channel middle flow: stem conv1 s2, conv2, then three s2 blocks."""
+    h = (size - 3) // 2 + 1 - 2
+    for _ in range(3):
+        h = (h - 1) // 2 + 1
+    return h
 
 
 def cpu_baseline(args, frames):
     """Oracle (CPU fp32 restatement of the reference, oracle/) on a bounded sample:
     one clip of the same shape, 1 warm-up + cpu_steps timed train steps."""
+    from Models.XceptionLSTMA import XceptionLSTMA
     from Models.XceptionLSTMV import XceptionLSTMV
     from oracle import xception_oracle as O
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
     torch.set_num_threads(cores)
     torch.manual_seed(0)
-    sd = XceptionLSTMV(128, pretrained=False).state_dict()
-    x = torch.rand((1, frames, 3, args.size, args.size), generator=torch.Generator().manual_seed(1234))
+    audio = args.model == "lstma"
+    sd = (XceptionLSTMA(512, pretrained=False) if audio else XceptionLSTMV(128, pretrained=False)).state_dict()
+    gen = torch.Generator().manual_seed(1234)
+    x = torch.randn((1, frames, 3, 13), generator=gen) if audio else \
+        torch.rand((1, frames, 3, args.size, args.size), generator=gen)
     y = torch.tensor([[1.0]])
     unfrozen = args.mode == "unfrozen"
-    O.clip_step(sd, x, y, unfrozen)
+    O.clip_step(sd, x, y, unfrozen, audio=audio)
     t0 = time.perf_counter()
     for _ in range(args.cpu_steps):
-        O.clip_step(sd, x, y, unfrozen)
+        O.clip_step(sd, x, y, unfrozen, audio=audio)
     dt = (time.perf_counter() - t0) / args.cpu_steps
     cpu_name = ""
     try:
@@ -74,7 +98,8 @@ def cpu_baseline(args, frames):
     except OSError:
         pass
     return {"value": round(1.0 / dt, 4), "unit": "clips/s", "cores": cores, "kind": "port",
-            "sample": f"{args.cpu_steps} timed + 1 warm-up {args.mode} train steps of 1 clip x {frames}x3x{args.size}^2, "
+            "sample": f"{args.cpu_steps} timed + 1 warm-up {args.mode} train steps of 1 clip x "
+                      f"{frames}x{'3x13 MFCC -> 64^2' if audio else f'3x{args.size}^2'}, "
                       f"fp32, oracle/xception_oracle.py (PyTorch CPU), {cpu_name}"}
 
 
@@ -111,24 +136,30 @@ def main():
 
     import xcp
     from xcp import ddp, ops
+    from Models.XceptionLSTMA import XceptionLSTMA
     from Models.XceptionLSTMV import XceptionLSTMV
     xcp.set_compute_dtype(args.dtype)
     xcp.load_library()
+    audio = args.model == "lstma"
 
     torch.manual_seed(0)
-    model = XceptionLSTMV(128, pretrained=False)
+    model = XceptionLSTMA(512, pretrained=False) if audio else XceptionLSTMV(128, pretrained=False)
     if args.mode == "unfrozen":
         for p in model.feature_extractor.parameters():
             p.requires_grad = True
     model = model.to(dev).train()
     params = [p for p in model.parameters() if p.requires_grad]
     buckets = ddp.GradBuckets(params, world=world)
-    opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4, fused=True)   # one fused launch per step
+    if audio:   # train_audio.py:33-44
+        opt = torch.optim.Adam(params, lr=1e-4, fused=True)
+    else:       # train_visual.py:540-577
+        opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4, fused=True)   # one fused launch per step
     crit = nn.BCELoss()
 
     B, T, S = args.batch, args.frames, args.size
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    clips = torch.rand((B, T, 3, S, S), generator=g, device=dev)
+    clips = torch.randn((B, T, 3, 13), generator=g, device=dev) if audio else \
+        torch.rand((B, T, 3, S, S), generator=g, device=dev)
     gl = torch.Generator(device=dev).manual_seed(4321 + rank)
     labels = torch.randint(0, 2, (B, 1), generator=gl, device=dev).float()
 
@@ -152,9 +183,10 @@ def main():
 
     timer = None
     if not args.no_kernel_timing:
-        timer = ops.KernelTimer({"pw_gemm_728": lambda name, a: name == "gemm_nt" and a["M"] == B * T * 19 * 19
+        hm = middle_hw(S)
+        timer = ops.KernelTimer({"pw_gemm_728": lambda name, a: name == "gemm_nt" and a["M"] == B * T * hm * hm
                                  and a["N"] == 728 and a["K"] == 728 and a["stats"] is not None,
-                                 "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == 728 and a["H"] == 19})
+                                 "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == 728 and a["H"] == hm})
         ops.set_kernel_timer(timer)
     torch.cuda.synchronize()
     if world > 1:
@@ -176,10 +208,11 @@ def main():
     value = clips_total / elapsed
     out = None
     if rank == 0:
-        M = B * T * 19 * 19
+        hm = middle_hw(S)
+        M = B * T * hm * hm
         roof = None
         extra = {}
-        traffic = pmc_traffic()
+        traffic = {} if audio else pmc_traffic()   # the committed PMC passes are of the headline (lstmv) bench
         if timer is not None:
             pw_ms = timer.mean_ms("pw_gemm_728")
             dw_ms = timer.mean_ms("dw_fwd_728")
@@ -190,7 +223,7 @@ def main():
                         "frac": round(ach / PEAK_BF16_TFLOPS, 4),
                         "traffic": traffic.get("gemm_nt", (None,))[0],
                         "traffic_source": traffic.get("gemm_nt", (None, None))[1],
-                        "kernel": "gemm_nt256k64_kernel (bf16 pointwise 1x1 728->728 @19x19, middle flow)",
+                        "kernel": f"gemm_nt256k64_kernel (bf16 pointwise 1x1 728->728 @{hm}x{hm}, middle flow)",
                         "flops_per_launch": flops, "avg_launch_ms": round(pw_ms, 4),
                         "launches": timer.count("pw_gemm_728")}
             if dw_ms:
@@ -200,15 +233,18 @@ def main():
                                         "frac": round(gbs / PEAK_HBM_GBS, 4),
                                         "traffic": traffic.get("dw_fwd_kernel", (None,))[0],
                                         "traffic_source": traffic.get("dw_fwd_kernel", (None, None))[1],
-                                        "kernel": "dw_fwd_kernel<bf16> (depthwise 3x3 C=728 @19x19)",
+                                        "kernel": f"dw_fwd_kernel<bf16> (depthwise 3x3 C=728 @{hm}x{hm})",
                                         "bytes_per_launch": byts, "avg_launch_ms": round(dw_ms, 4)}
-        out = {"metric": "clips/sec (node) XceptionLSTMV 16x299x299 bf16 train",
+        metric = (f"clips/sec (node) XceptionLSTMA MFCC {T}x3x13 (64x64) {args.dtype} train" if audio else
+                  "clips/sec (node) XceptionLSTMV 16x299x299 bf16 train")
+        name = "XceptionLSTMA(hidden=512)" if audio else "XceptionLSTMV(hidden=128)"
+        shape = f"{T} MFCC frames x 3x13 -> 64x64" if audio else f"{T} frames x 3x{S}x{S}"
+        out = {"metric": metric,
                "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (on-device U[0,1) clips, "
-               "seeded per rank; random-init weights, Xception.py:154-160 scheme)",
-               "config": {"workload": f"XceptionLSTMV(hidden=128) {args.mode}-backbone train step, "
-                                      f"{B} clips/GPU x {T} frames x 3x{S}x{S}, BCE + Adam",
+               "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": f"synthetic (on-device {'N(0,1) MFCC' if audio else 'U[0,1)'} "
+               "clips, seeded per rank; random-init weights, Xception.py:154-160 scheme)",
+               "config": {"workload": f"{name} {args.mode}-backbone train step, {B} clips/GPU x {shape}, BCE + Adam",
                           "global_batch": B * world, "frames": T, "size": S, "mode": args.mode,
                           "parallelism": f"dp{world}"},
                "roofline": roof, "loss": round(float(loss.item()), 5)}
