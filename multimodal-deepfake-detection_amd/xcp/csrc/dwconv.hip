@@ -1139,6 +1139,10 @@ int xcp_internal_lstm_tune(int v);           // lstm.hip
 int xcp_internal_nt_grid(int v);             // gemm.hip
 int xcp_internal_conv3_var(int v);           // conv3.hip
 int xcp_internal_pool_quad(int v);           // bn.hip
+int xcp_internal_dw_fwd_frame(int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift,
+                              int N, int H, int W, int C, hipStream_t st);   // dwframe.hip
+int xcp_internal_dwf_var(int v);             // dwframe.hip
+int g_dw_frame = 0;   // xcp_tune knob 13: small-frame persistent depthwise forward (1; measured slower, see dwframe.hip) or not (0)
 
 extern "C" {
 
@@ -1154,6 +1158,12 @@ int xcp_tune(int knob, int value) {
   if (knob == 10) return xcp_internal_nt_grid(value);
   if (knob == 11) return xcp_internal_conv3_var(value);
   if (knob == 12) return xcp_internal_pool_quad(value);
+  if (knob == 14) return xcp_internal_dwf_var(value);
+  if (knob == 13) {
+    const int old = g_dw_frame;
+    if (value == 0 || value == 1) g_dw_frame = value;
+    return old;
+  }
   if (knob == 4 || knob == 5) {
     int& k = knob == 4 ? g_dw_fwd_kernel : g_dw_bwd_kernel;
     const int old = k;
@@ -1171,6 +1181,10 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
                int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
+  if (dtype == XCP_BF16 && g_dw_frame) {
+    const int rc = xcp_internal_dw_fwd_frame(act, X, Y, Wt, scale, shift, N, H, W, C, stream);
+    if (rc != XCP_EUNSUPPORTED) return rc;
+  }
   const int maxpx = g_fwd_maxpx;
   DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, maxpx)};
   if (g_dw_fwd_kernel == 2) {

@@ -146,19 +146,25 @@ def test_gemm_tn(ops, gpu, dt, M, N, K, tn):
     assert rel_err(out.view(N, K), ref) < (1e-5 if dt == torch.float32 else 1e-3)
 
 
-@pytest.fixture(params=[2, 0, 1], ids=["ldsrow", "row", "tile"])
+@pytest.fixture(params=[2, 0, 1, 3], ids=["ldsrow", "row", "tile", "frame"])
 def dw_family(request, ops):
-    """Run a depthwise test under both kernel families (xcp_tune knobs 4 / 5)."""
-    of = ops._lib.call("xcp_tune", 4, request.param)
-    ob = ops._lib.call("xcp_tune", 5, request.param)
-    yield request.param
+    """Run a depthwise test under every kernel family (xcp_tune knobs 4 / 5; 13 switches the
+    small-frame persistent forward (dwframe.hip, bf16, frames up to 20 x 20) on for "frame"
+    and off for the others)."""
+    fam = request.param
+    of = ops._lib.call("xcp_tune", 4, fam if fam < 3 else 1)
+    ob = ops._lib.call("xcp_tune", 5, fam if fam < 3 else 2)
+    oq = ops._lib.call("xcp_tune", 13, 1 if fam == 3 else 0)
+    yield fam
     ops._lib.call("xcp_tune", 4, of)
     ops._lib.call("xcp_tune", 5, ob)
+    ops._lib.call("xcp_tune", 13, oq)
 
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("act", [0, 1, 2])
-@pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9), (1, 64, 147), (2, 256, 74)])
+@pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9), (1, 64, 147), (2, 256, 74),
+                                   (5, 728, 3), (2, 200, 1)])
 def test_dw_fwd_bwd(ops, gpu, dw_family, dt, act, N, C, H):
     W = H + 1
     g = torch.Generator(device=gpu).manual_seed(C + H + act)

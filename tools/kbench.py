@@ -169,6 +169,47 @@ def main():
                 timeit(lambda: ops.bn_backward(dZ, Ye, m_, c_, bn, ste, dYe, dg, db, pool=(dOut, amax, n_, h_, h_)),
                        iters=10))
             del Ye, dZ, dYe
+    if "cold" in sel:   # middle-flow kernels with the Infinity Cache / L2 flushed before every launch
+        flush = torch.zeros(768 * 2 ** 18, device=dev, dtype=torch.float32)   # read (clean lines) before each launch
+
+        def cold(fn, iters=10):
+            tot = 0.0
+            for i in range(iters + 2):
+                flush.sum()
+                s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s_.record()
+                fn()
+                e_.record()
+                torch.cuda.synchronize()
+                if i >= 2:
+                    tot += s_.elapsed_time(e_)
+            return tot / iters
+
+        rep("cold copy", cold(lambda: Y.copy_(X)), 2 * tensor_bytes)
+        for fr in (0, 1):
+            old = ops._lib.call("xcp_tune", 13, fr)
+            rep(f"cold dw_fwd act=2 frame={fr}", cold(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
+            rep(f"warm dw_fwd act=2 frame={fr}", timeit(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
+            ops._lib.call("xcp_tune", 13, old)
+        for var in (1, 2, 3):
+            ov = ops._lib.call("xcp_tune", 14, var)
+            rep(f"warm dw_fwd frame var={var}", timeit(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
+            ops._lib.call("xcp_tune", 14, ov)
+        rep("cold dw_bwd act=2 +bnsums", cold(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)),
+            3 * tensor_bytes)
+        rep("cold dw_bwd act=1 +res", cold(lambda: ops.dw_bwd(1, D, X, Wt, sc, sh, Y, dW, N, H, W, C, dRes=D)),
+            4 * tensor_bytes)
+        dgm, dbt = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        bn = {"weight": sc, "bias": sh, "running_mean": None, "running_var": None, "eps": 1e-5, "momentum": 0.1,
+              "track": False}
+        rep("cold bn_backward (reduce+apply)", cold(lambda: ops.bn_backward(D, X, M, C, bn, st, Y, dgm, dbt)),
+            5 * tensor_bytes)
+        rep("cold gemm_nt 728 +stats", cold(lambda: ops.gemm_nt(X, Wp, Y, M, C, C,
+                                                              stats=torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev))),
+            flops=2.0 * M * C * C)
+        outw = torch.empty(C * C, device=dev)
+        rep("cold weight_grad 728", cold(lambda: ops.weight_grad(D, X, M, C, C, outw)), flops=2.0 * M * C * C)
+        del flush
     if "tnabl" in sel:
         out = torch.empty(C * C, device=dev)
         P = torch.empty(28 * C * C, device=dev)
