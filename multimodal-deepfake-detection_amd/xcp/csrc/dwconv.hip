@@ -821,7 +821,7 @@ XCP_DEV void store_row(T* frame, int h, int W, int C, int x0w, int c0, const cha
 // Prefetch depth (rows in flight per staged tensor): each step waits only for the
 // loads issued D steps earlier (measured: one row of look-ahead leaves the walk
 // latency-bound, ~2.4 us per row step).
-constexpr int FD = 3, BD = 2;
+constexpr int FD = 3;
 
 template <typename T, int ACT>
 __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(DwArgs a) {
@@ -906,7 +906,7 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(DwArgs a) {
   }
 }
 
-template <typename T, int ACT, bool RES>
+template <typename T, int ACT, bool RES, int BD = 2>
 __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
   typedef RV<T> R;
   typedef typename R::V V;
@@ -1113,11 +1113,20 @@ int launch_fwd_lds(int act, const DwArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+int g_dwb_bd = 2;   // xcp_tune knob 15: backward row-walk prefetch depth (2, 3; 4 without a residual)
+
+template <typename T, bool RES, int BD>
+void launch_bwd_lds_rb(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_NONE, RES, BD>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_RELU, RES, BD>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_BNRELU, RES, BD>), dim3(blocks), dim3(256), 0, st, a);
+}
+
 template <typename T, bool RES>
 void launch_bwd_lds_r(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_NONE, RES>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_RELU, RES>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_BNRELU, RES>), dim3(blocks), dim3(256), 0, st, a);
+  if (g_dwb_bd >= 4 && !RES) launch_bwd_lds_rb<T, RES, 4>(act, a, blocks, st);
+  else if (g_dwb_bd >= 3) launch_bwd_lds_rb<T, RES, 3>(act, a, blocks, st);
+  else launch_bwd_lds_rb<T, RES, 2>(act, a, blocks, st);
 }
 
 template <typename T>
@@ -1159,6 +1168,11 @@ int xcp_tune(int knob, int value) {
   if (knob == 11) return xcp_internal_conv3_var(value);
   if (knob == 12) return xcp_internal_pool_quad(value);
   if (knob == 14) return xcp_internal_dwf_var(value);
+  if (knob == 15) {
+    const int old = g_dwb_bd;
+    if (value >= 2 && value <= 4) g_dwb_bd = value;
+    return old;
+  }
   if (knob == 13) {
     const int old = g_dw_frame;
     if (value == 0 || value == 1) g_dw_frame = value;

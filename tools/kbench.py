@@ -195,10 +195,13 @@ def main():
             ov = ops._lib.call("xcp_tune", 14, var)
             rep(f"warm dw_fwd frame var={var}", timeit(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
             ops._lib.call("xcp_tune", 14, ov)
-        rep("cold dw_bwd act=2 +bnsums", cold(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)),
-            3 * tensor_bytes)
-        rep("cold dw_bwd act=1 +res", cold(lambda: ops.dw_bwd(1, D, X, Wt, sc, sh, Y, dW, N, H, W, C, dRes=D)),
-            4 * tensor_bytes)
+        for bd in (2, 3, 4):
+            ob = ops._lib.call("xcp_tune", 15, bd)
+            rep(f"cold dw_bwd act=2 +bnsums bd={bd}",
+                cold(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)), 3 * tensor_bytes)
+            rep(f"cold dw_bwd act=1 +res bd={bd}", cold(lambda: ops.dw_bwd(1, D, X, Wt, sc, sh, Y, dW, N, H, W, C, dRes=D)),
+                4 * tensor_bytes)
+            ops._lib.call("xcp_tune", 15, ob)
         dgm, dbt = torch.empty(C, device=dev), torch.empty(C, device=dev)
         bn = {"weight": sc, "bias": sh, "running_mean": None, "running_var": None, "eps": 1e-5, "momentum": 0.1,
               "track": False}
