@@ -178,7 +178,7 @@ int xcp_lstm_needs_whhT(int H);
 int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
                  float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, xcp_stream_t stream);
 int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const float* whh, const float* cst,
-                 const float* gates, float* dgates, int B, int T, int H, xcp_stream_t stream);
+                 const float* gates, float* dgates, float* work, int B, int T, int H, xcp_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -60,7 +60,7 @@ SIGNATURES = {
     "xcp_conv3x3_wgrad": [P, P, P, I, I, I, P],
     "xcp_lstm_needs_whhT": [I],
     "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
-    "xcp_lstm_bwd": [P, P, P, P, P, P, P, I, I, I, P],
+    "xcp_lstm_bwd": [P, P, P, P, P, P, P, P, I, I, I, P],
 }
 
 # entry points that return a size, not a status

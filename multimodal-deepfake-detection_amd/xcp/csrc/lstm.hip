@@ -263,9 +263,173 @@ __global__ __launch_bounds__(1024) void lstm_bwd_reg_kernel(const float* __restr
   }
 }
 
-int g_lstm_kernel = 0;   // xcp_tune knob 9: 0 = register-resident kernels where H allows, 1 = generic
+
+// ---------------------------------------------------------------------------------
+// Per-step kernels for large H (XceptionLSTMA: H = 512, T = 120).  One workgroup per clip
+// cannot keep up there: it streams the whole W_hh (4H x H fp32 = 4 MB) through one CU per
+// step (~530 us a step).  Here every time step is one launch spread over H / 2 workgroups
+// (256 at H = 512), each owning 2 hidden units -- their 8 gate rows of W_hh (forward) or
+// their 2 columns (backward); the launch boundary is the grid-wide step barrier and makes
+// h_t / dgates_t visible to every CU.
+//
+// forward step t: thread (row r = gate q of unit uu, k-slice s of H/32) dots its W_hh row
+// slice with h_{t-1} (staged in LDS, rows padded against bank conflicts) for every clip,
+// the 32 slices reduce by shuffles, and (clip, unit) threads run the cell.
+constexpr int LS_UPW = 2;              // hidden units per workgroup
+constexpr int LS_MAXB = 32;            // clips (register partials per thread)
+
+template <int KS>   // KS = H / 32 (k values per slice)
+__global__ __launch_bounds__(256) void lstm_fwd_step_kernel(const float* __restrict__ xproj, const float* __restrict__ whh,
+                                                            const float* __restrict__ bih, const float* __restrict__ bhh,
+                                                            float* __restrict__ out, float* __restrict__ hprev,
+                                                            float* __restrict__ cst, float* __restrict__ gates,
+                                                            float* __restrict__ hn, float* __restrict__ cn, int B, int T,
+                                                            int t) {
+  constexpr int H = KS * 32, G4 = 4 * H, PS = KS + 4;   // LDS slice pitch (floats)
+  extern __shared__ float sm[];                          // h_{t-1} [B][32][PS], then pre [8][B]
+  float* sh = sm;
+  float* spre = sm + B * 32 * PS;
+  const int tid = threadIdx.x, u0 = blockIdx.x * LS_UPW;
+  const int r = tid >> 5, s = tid & 31, q = r >> 1, uu = r & 1;
+  const int j = q * H + u0 + uu;
+  // W_hh row slice
+  float w[KS];
+#pragma unroll
+  for (int i = 0; i < KS; i += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(whh + (long)j * H + s * KS + i);
+    w[i] = v.x; w[i + 1] = v.y; w[i + 2] = v.z; w[i + 3] = v.w;
+  }
+  // stage h_{t-1} (zero at t = 0)
+  for (int e = tid; e < B * H / 4; e += 256) {
+    const int b = e / (H / 4), k4 = (e - b * (H / 4)) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t > 0) v = *reinterpret_cast<const float4*>(out + ((long)b * T + t - 1) * H + k4);
+    *reinterpret_cast<float4*>(sh + (b * 32 + k4 / KS) * PS + (k4 % KS)) = v;
+  }
+  __syncthreads();
+  for (int b = 0; b < B; ++b) {
+    const float* hb = sh + (b * 32 + s) * PS;
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < KS; i += 2) {
+      a0 = fmaf(w[i], hb[i], a0);
+      a1 = fmaf(w[i + 1], hb[i + 1], a1);
+    }
+    float acc = a0 + a1;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (s == 0) spre[r * B + b] = acc;
+  }
+  __syncthreads();
+  if (tid < B * LS_UPW) {
+    const int b = tid / LS_UPW, v = tid - b * LS_UPW, k = u0 + v;
+    const float* xp = xproj + ((long)b * T + t) * G4;
+    float pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int jj = g * H + k;
+      pre[g] = spre[(g * 2 + v) * B + b] + xp[jj] + bih[jj] + bhh[jj];
+    }
+    const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanhf(pre[2]), og = sigm(pre[3]);
+    const long ob = ((long)b * T + t) * H;
+    const float cp = t > 0 ? cst[ob - H + k] : 0.f;
+    const float c = fmaf(fg, cp, ig * gg);
+    const float h = og * tanhf(c);
+    float* gt = gates + ((long)b * T + t) * G4;
+    gt[k] = ig; gt[H + k] = fg; gt[2 * H + k] = gg; gt[3 * H + k] = og;
+    hprev[ob + k] = t > 0 ? sh[(b * 32 + k / KS) * PS + k % KS] : 0.f;
+    cst[ob + k] = c;
+    out[ob + k] = h;
+    if (t == T - 1) {
+      hn[(long)b * H + k] = h;
+      cn[(long)b * H + k] = c;
+    }
+  }
+}
+
+// backward step t: dh_t[b][k] = dout[b][t][k] + sum_j dgates_{t+1}[b][j] W_hh[j][k] (dhn at
+// t = T-1): thread (clip b, j-slice sl of 4H/16) against the workgroup's 2 W_hh columns in
+// LDS, 16-slice shuffle reduction; (clip, unit) threads run the cell backward with the cell
+// gradient carried in dcw [B][H] (each unit's carry is only touched by its workgroup).
+__global__ __launch_bounds__(256) void lstm_bwd_step_kernel(const float* __restrict__ dout, const float* __restrict__ dhn,
+                                                            const float* __restrict__ dcn, const float* __restrict__ whh,
+                                                            const float* __restrict__ cst, const float* __restrict__ gates,
+                                                            float* __restrict__ dgates, float* __restrict__ dcw, int B,
+                                                            int T, int H, int t) {
+  extern __shared__ float sm[];   // W columns [4H][2], dh [B][2]
+  const int G4 = 4 * H;
+  float* swc = sm;
+  float* sdh = sm + G4 * 2;
+  const int tid = threadIdx.x, u0 = blockIdx.x * LS_UPW;
+  if (t < T - 1) {
+    for (int jj = tid; jj < G4; jj += 256) {
+      const float2 v = *reinterpret_cast<const float2*>(whh + (long)jj * H + u0);
+      swc[2 * jj] = v.x;
+      swc[2 * jj + 1] = v.y;
+    }
+    __syncthreads();
+    const int per = G4 / 16;
+    for (int b0 = 0; b0 < B; b0 += 16) {
+      const int b = b0 + (tid >> 4), sl = tid & 15;
+      float a0 = 0.f, a1 = 0.f;
+      if (b < B) {
+        const float* dg = dgates + ((long)b * T + t + 1) * G4 + sl * per;
+        const float* wc = swc + 2 * sl * per;
+        for (int i = 0; i < per; i += 4) {
+          const float4 g4 = *reinterpret_cast<const float4*>(dg + i);
+          const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a0 = fmaf(gv[e], wc[2 * (i + e)], a0);
+            a1 = fmaf(gv[e], wc[2 * (i + e) + 1], a1);
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        a0 += __shfl_xor(a0, o, 64);
+        a1 += __shfl_xor(a1, o, 64);
+      }
+      if (sl == 0 && b < B) {
+        sdh[b * 2] = a0;
+        sdh[b * 2 + 1] = a1;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < B * LS_UPW) {
+    const int b = tid / LS_UPW, v = tid - b * LS_UPW, k = u0 + v;
+    const long ob = ((long)b * T + t) * H;
+    const float dhr = t < T - 1 ? sdh[b * 2 + v] : (dhn ? dhn[(long)b * H + k] : 0.f);
+    const float dcr = t < T - 1 ? dcw[(long)b * H + k] : (dcn ? dcn[(long)b * H + k] : 0.f);
+    const float dh = dhr + (dout ? dout[ob + k] : 0.f);
+    const float c = cst[ob + k];
+    const float cp = t > 0 ? cst[ob - H + k] : 0.f;
+    const float* gt = gates + ((long)b * T + t) * G4;
+    const float ig = gt[k], fg = gt[H + k], gg = gt[2 * H + k], og = gt[3 * H + k];
+    const float tc = tanhf(c);
+    const float dO = dh * tc;
+    const float dc = dcr + dh * og * (1.f - tc * tc);
+    const float dI = dc * gg, dG = dc * ig, dF = dc * cp;
+    dcw[(long)b * H + k] = dc * fg;
+    float* dg = dgates + ((long)b * T + t) * G4;
+    dg[k] = dI * ig * (1.f - ig);
+    dg[H + k] = dF * fg * (1.f - fg);
+    dg[2 * H + k] = dG * (1.f - gg * gg);
+    dg[3 * H + k] = dO * og * (1.f - og);
+  }
+}
+
+int g_lstm_kernel = 0;   // xcp_tune knob 9: 0 = register-resident / per-step kernels where H allows, 1 = generic
 
 bool lstm_reg(int H) { return g_lstm_kernel == 0 && (H == 128 || H == 64); }
+// per-step kernels: H = 32 * KS for the instantiated KS, clips within the register partials
+bool lstm_step(int B, int H) {
+  const size_t fwd_lds = ((size_t)B * 32 * (H / 32 + 4) + 8 * B) * sizeof(float);
+  const size_t bwd_lds = ((size_t)8 * H + 2 * B) * sizeof(float);
+  return g_lstm_kernel == 0 && !lstm_reg(H) && (H == 256 || H == 512 || H == 1024) && B <= LS_MAXB &&
+         fwd_lds <= 65536 && bwd_lds <= 65536;
+}
 
 }  // namespace
 
@@ -278,8 +442,8 @@ int xcp_internal_lstm_tune(int value) {
 
 extern "C" {
 
-// 1 when the recurrence runs on the register-resident kernels (whhT is then unused)
-int xcp_lstm_needs_whhT(int H) { return lstm_reg(H) ? 0 : 1; }
+// 1 when the recurrence runs on the generic kernels, which read the transposed W_hh
+int xcp_lstm_needs_whhT(int H) { return lstm_reg(H) || lstm_step(1, H) ? 0 : 1; }
 
 int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
                  float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, hipStream_t st) {
@@ -293,6 +457,21 @@ int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const 
                          gates, hn, cn, T);
     return (int)hipGetLastError();
   }
+  if (lstm_step(B, H)) {
+    const size_t smem = ((size_t)B * 32 * (H / 32 + 4) + 8 * B) * sizeof(float);
+    for (int t = 0; t < T; ++t) {
+      if (H == 256)
+        hipLaunchKernelGGL(lstm_fwd_step_kernel<8>, dim3(H / LS_UPW), dim3(256), smem, st, xproj, whh, bih, bhh, out,
+                           hprev, cst, gates, hn, cn, B, T, t);
+      else if (H == 512)
+        hipLaunchKernelGGL(lstm_fwd_step_kernel<16>, dim3(H / LS_UPW), dim3(256), smem, st, xproj, whh, bih, bhh, out,
+                           hprev, cst, gates, hn, cn, B, T, t);
+      else
+        hipLaunchKernelGGL(lstm_fwd_step_kernel<32>, dim3(H / LS_UPW), dim3(256), smem, st, xproj, whh, bih, bhh, out,
+                           hprev, cst, gates, hn, cn, B, T, t);
+    }
+    return (int)hipGetLastError();
+  }
   if (!whhT) return XCP_EINVAL;
   const size_t smem = (size_t)6 * H * sizeof(float);
   hipLaunchKernelGGL(lstm_fwd_kernel, dim3(B), dim3(256), smem, st, xproj, whhT, bih, bhh, out, hprev, cst, gates, hn, cn,
@@ -301,8 +480,16 @@ int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const 
 }
 
 int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const float* whh, const float* cst,
-                 const float* gates, float* dgates, int B, int T, int H, hipStream_t st) {
+                 const float* gates, float* dgates, float* work, int B, int T, int H, hipStream_t st) {
   if (B <= 0 || T <= 0) return XCP_OK;
+  if (lstm_step(B, H)) {
+    if (!work) return XCP_EINVAL;
+    const size_t smem = ((size_t)8 * H + 2 * B) * sizeof(float);
+    for (int t = T - 1; t >= 0; --t)
+      hipLaunchKernelGGL(lstm_bwd_step_kernel, dim3(H / LS_UPW), dim3(256), smem, st, dout, dhn, dcn, whh, cst, gates,
+                         dgates, work, B, T, H, t);
+    return (int)hipGetLastError();
+  }
   if (lstm_reg(H)) {
     if (H == 128)
       hipLaunchKernelGGL(lstm_bwd_reg_kernel<128>, dim3(B), dim3(1024), 0, st, dout, dhn, dcn, whh, cst, gates, dgates,

@@ -448,6 +448,32 @@ def test_lstm_h64_vs_oracle(ops, gpu, kernel):
         ops._lib.call("xcp_tune", 9, old)
 
 
+@pytest.mark.parametrize("H,B,T", [(256, 5, 7), (512, 17, 4), (1024, 3, 3)])
+def test_lstm_step_kernels_vs_oracle(ops, gpu, H, B, T):
+    """Per-step recurrence kernels (large H: one launch per time step over H/2 workgroups)
+    against the oracle's nn.LSTM restatement, including a carried-in gradient on c_n."""
+    from oracle import xception_oracle as O
+    from xcp.lstm import LSTM
+    torch.manual_seed(H)
+    lstm = LSTM(128, H, 1, batch_first=True).to(gpu)
+    x = torch.randn((B, T, 128), generator=torch.Generator().manual_seed(H + 1))
+    xg = x.to(gpu).requires_grad_(True)
+    o, (h, c) = lstm(xg)
+    r = torch.randn(o.shape, generator=torch.Generator().manual_seed(H + 2))
+    rc = torch.randn(c.shape, generator=torch.Generator().manual_seed(H + 3))
+    ((o * r.to(gpu)).sum() + (c * rc.to(gpu)).sum()).backward()
+    cp = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in lstm.named_parameters()}
+    xc = x.clone().requires_grad_(True)
+    ro, rh, rcn = O.lstm_forward(xc, cp["weight_ih_l0"], cp["weight_hh_l0"], cp["bias_ih_l0"], cp["bias_hh_l0"])
+    ((ro * r).sum() + (rcn * rc).sum()).backward()
+    torch.testing.assert_close(o.detach().cpu(), ro.detach(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(h.detach().cpu(), rh.detach(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(c.detach().cpu(), rcn.detach(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(xg.grad.cpu(), xc.grad, rtol=1e-3, atol=1e-5)
+    for n, p in lstm.named_parameters():
+        torch.testing.assert_close(p.grad.cpu(), cp[n].grad, rtol=1e-3, atol=1e-5)
+
+
 @pytest.mark.parametrize("N,IH,IW", [(2, 149, 149), (3, 21, 38), (1, 6, 147)])
 def test_conv3x3_stem_fwd_dgrad(ops, gpu, N, IH, IW):
     """Direct MFMA stem conv2 (conv3.hip) against F.conv2d / its input gradient (bf16

@@ -26,7 +26,8 @@ from Models.XceptionLSTMV import XceptionLSTMV  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
-    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--frames", type=int, default=None)
+    ap.add_argument("--model", choices=["lstmv", "lstma"], default="lstmv")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--top", type=int, default=60)
     args = ap.parse_args()
@@ -34,15 +35,22 @@ def main():
     xcp.set_compute_dtype("bf16")
     xcp.load_library()
     torch.manual_seed(0)
-    model = XceptionLSTMV(128, pretrained=False)
-    for p in model.feature_extractor.parameters():
-        p.requires_grad = True
+    audio = args.model == "lstma"
+    args.frames = args.frames or (120 if audio else 16)
+    if audio:   # bench.py --model lstma: frozen backbone, Adam 1e-4
+        from Models.XceptionLSTMA import XceptionLSTMA
+        model = XceptionLSTMA(512, pretrained=False)
+    else:
+        model = XceptionLSTMV(128, pretrained=False)
+        for p in model.feature_extractor.parameters():
+            p.requires_grad = True
     model = model.to(dev).train()
     params = [p for p in model.parameters() if p.requires_grad]
     buckets = ddp.GradBuckets(params, world=1)
     opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4, fused=True)   # one fused launch per step
     crit = nn.BCELoss()
-    clips = torch.rand((args.batch, args.frames, 3, 299, 299), device=dev)
+    clips = torch.randn((args.batch, args.frames, 3, 13), device=dev) if audio else \
+        torch.rand((args.batch, args.frames, 3, 299, 299), device=dev)
     labels = torch.randint(0, 2, (args.batch, 1), device=dev).float()
 
     def step():
