@@ -1151,6 +1151,9 @@ int xcp_internal_pool_quad(int v);           // bn.hip
 int xcp_internal_dw_fwd_frame(int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift,
                               int N, int H, int W, int C, hipStream_t st);   // dwframe.hip
 int xcp_internal_dwf_var(int v);             // dwframe.hip
+int xcp_internal_dw_small(int v);            // dwframe.hip
+int xcp_internal_dw_fwd_small(int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift,
+                              int N, int H, int W, int C, hipStream_t st);   // dwframe.hip
 int g_dw_frame = 0;   // xcp_tune knob 13: small-frame persistent depthwise forward (1; measured slower, see dwframe.hip) or not (0)
 
 extern "C" {
@@ -1168,6 +1171,7 @@ int xcp_tune(int knob, int value) {
   if (knob == 11) return xcp_internal_conv3_var(value);
   if (knob == 12) return xcp_internal_pool_quad(value);
   if (knob == 14) return xcp_internal_dwf_var(value);
+  if (knob == 16) return xcp_internal_dw_small(value);
   if (knob == 15) {
     const int old = g_dwb_bd;
     if (value >= 2 && value <= 4) g_dwb_bd = value;
@@ -1195,6 +1199,10 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
                int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
+  if (dtype == XCP_BF16 && W <= 8) {
+    const int rc = xcp_internal_dw_fwd_small(act, X, Y, Wt, scale, shift, N, H, W, C, stream);
+    if (rc != XCP_EUNSUPPORTED) return rc;
+  }
   if (dtype == XCP_BF16 && g_dw_frame) {
     const int rc = xcp_internal_dw_fwd_frame(act, X, Y, Wt, scale, shift, N, H, W, C, stream);
     if (rc != XCP_EUNSUPPORTED) return rc;

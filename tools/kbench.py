@@ -126,7 +126,11 @@ def main():
             ste = {"mean": torch.zeros(c_, device=dev), "invstd": torch.ones(c_, device=dev)}
             dWe = torch.empty(9 * c_, device=dev)
             tb = m_ * c_ * 2
-            rep(f"dw_fwd act=2 {h_}^2x{c_}", timeit(lambda: ops.dw_fwd(2, Xe, Ye, We, sce, she, n_, h_, h_, c_), iters=10), 2 * tb)
+            for sm_ in (0, 1):
+                osm = ops._lib.call("xcp_tune", 16, sm_)
+                rep(f"dw_fwd act=2 {h_}^2x{c_} small={sm_}",
+                    timeit(lambda: ops.dw_fwd(2, Xe, Ye, We, sce, she, n_, h_, h_, c_), iters=10), 2 * tb)
+                ops._lib.call("xcp_tune", 16, osm)
             rep(f"dw_bwd act=2 +bn {h_}^2x{c_}",
                 timeit(lambda: ops.dw_bwd(2, De, Xe, We, sce, she, Ye, dWe, n_, h_, h_, c_, bn_stats=ste), iters=10), 3 * tb)
             rep(f"copy {h_}^2x{c_}", timeit(lambda: Ye.copy_(Xe), iters=10), 2 * tb)
