@@ -118,8 +118,15 @@ XCP_DEV void stage(const T* __restrict__ src, char* dst, const TileGeo& g, long 
       if (ok[k]) {
         float f[EPC];
         VecIO<T, EPC>::load(reinterpret_cast<const T*>(&u), f);
+        typedef float p2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int j = 0; j < EPC; ++j) f[j] = act1<ACT>(f[j], sc[j], sh[j]);
+        for (int j = 0; j < EPC; j += 2) {   // packed pairs (v_pk_fma_f32 / v_pk_max_f32)
+          p2 v = p2{f[j], f[j + 1]};
+          if constexpr (ACT == ACT_BNRELU) v = __builtin_elementwise_fma(v, p2{sc[j], sc[j + 1]}, p2{sh[j], sh[j + 1]});
+          v = __builtin_elementwise_max(v, p2(0.f));
+          f[j] = v[0];
+          f[j + 1] = v[1];
+        }
         VecIO<T, EPC>::store(reinterpret_cast<T*>(&u), f);
       }
     }
@@ -190,14 +197,29 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
 #pragma unroll
     for (int j = 0; j < SEGL; ++j) {
       float o[EPT];
+      if constexpr (EPT == 2) {   // packed pairs: one v_pk_fma_f32 per tap for both channels
+        typedef float p2 __attribute__((ext_vector_type(2)));
+        p2 sa = p2(0.f), sb = p2(0.f), sc3 = p2(0.f);
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        float s = 0.f;
+        for (int kx = 0; kx < 3; ++kx) {
+          sa = __builtin_elementwise_fma(p2{win[0][j + kx][0], win[0][j + kx][1]}, p2{wt[kx][0], wt[kx][1]}, sa);
+          sb = __builtin_elementwise_fma(p2{win[1][j + kx][0], win[1][j + kx][1]}, p2{wt[3 + kx][0], wt[3 + kx][1]}, sb);
+          sc3 = __builtin_elementwise_fma(p2{win[2][j + kx][0], win[2][j + kx][1]}, p2{wt[6 + kx][0], wt[6 + kx][1]},
+                                          sc3);
+        }
+        const p2 t2 = (sa + sb) + sc3;
+        o[0] = t2[0];
+        o[1] = t2[1];
+      } else {
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+        for (int e = 0; e < EPT; ++e) {
+          float s = 0.f;
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
-        o[e] = s;
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
+          o[e] = s;
+        }
       }
       const int x = x0 + j;
       if (x < g.TW && tw0 + x < a.W) *reinterpret_cast<unsigned*>(yrow + (long)x * a.C) = pack(o, (T*)nullptr);
