@@ -375,13 +375,20 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(const float* __restr
       if (b < B) {
         const float* dg = dgates + ((long)b * T + t + 1) * G4 + sl * per;
         const float* wc = swc + 2 * sl * per;
-        for (int i = 0; i < per; i += 4) {
-          const float4 g4 = *reinterpret_cast<const float4*>(dg + i);
-          const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+        // 8 independent 16-B loads in flight per batch (the loop is L2-latency-bound otherwise)
+        for (int i0 = 0; i0 < per; i0 += 32) {
+          float4 g4[8];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            a0 = fmaf(gv[e], wc[2 * (i + e)], a0);
-            a1 = fmaf(gv[e], wc[2 * (i + e) + 1], a1);
+          for (int q = 0; q < 8; ++q) g4[q] = *reinterpret_cast<const float4*>(dg + i0 + 4 * q);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float gv[4] = {g4[q].x, g4[q].y, g4[q].z, g4[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int i = i0 + 4 * q + e;
+              a0 = fmaf(gv[e], wc[2 * i], a0);
+              a1 = fmaf(gv[e], wc[2 * i + 1], a1);
+            }
           }
         }
       }
