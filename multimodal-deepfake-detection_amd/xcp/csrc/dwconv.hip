@@ -915,8 +915,8 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(DwArgs a) {
   }
 }
 
-template <typename T, int ACT, bool RES, int BD = 2>
-__global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
+template <typename T, int ACT, bool RES, int BD = 2, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void dw_bwd_lds_kernel(DwBwdArgs a) {
   typedef RV<T> R;
   typedef typename R::V V;
   constexpr int EPT = R::EPT, CPG = 16 * EPT;
@@ -1124,11 +1124,20 @@ int launch_fwd_lds(int act, const DwArgs& a, hipStream_t st) {
 
 int g_dwb_bd = 2;   // xcp_tune knob 15: backward row-walk prefetch depth (2, 3; 4 without a residual)
 
+int g_dwb_occ = 2;   // xcp_tune knob 17: waves per SIMD the backward row-walk kernel is compiled for (2 | 3)
+
+template <typename T, bool RES, int BD, int OCC>
+void launch_bwd_lds_rbo(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_NONE, RES, BD, OCC>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU)
+    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_RELU, RES, BD, OCC>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_BNRELU, RES, BD, OCC>), dim3(blocks), dim3(256), 0, st, a);
+}
+
 template <typename T, bool RES, int BD>
 void launch_bwd_lds_rb(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_NONE, RES, BD>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_RELU, RES, BD>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_BNRELU, RES, BD>), dim3(blocks), dim3(256), 0, st, a);
+  if (g_dwb_occ == 3 && !RES && BD == 2) launch_bwd_lds_rbo<T, RES, BD, 3>(act, a, blocks, st);
+  else launch_bwd_lds_rbo<T, RES, BD, 2>(act, a, blocks, st);
 }
 
 template <typename T, bool RES>
@@ -1181,6 +1190,11 @@ int xcp_tune(int knob, int value) {
   if (knob == 12) return xcp_internal_pool_quad(value);
   if (knob == 14) return xcp_internal_dwf_var(value);
   if (knob == 16) return xcp_internal_dw_small(value);
+  if (knob == 17) {
+    const int old = g_dwb_occ;
+    if (value == 2 || value == 3) g_dwb_occ = value;
+    return old;
+  }
   if (knob == 15) {
     const int old = g_dwb_bd;
     if (value >= 2 && value <= 4) g_dwb_bd = value;

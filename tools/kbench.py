@@ -199,7 +199,14 @@ def main():
             ov = ops._lib.call("xcp_tune", 14, var)
             rep(f"warm dw_fwd frame var={var}", timeit(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
             ops._lib.call("xcp_tune", 14, ov)
-        for bd in (2, 3, 4):
+        for occ in (2, 3):
+            oo = ops._lib.call("xcp_tune", 17, occ)
+            rep(f"cold dw_bwd act=2 +bnsums occ={occ}",
+                cold(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)), 3 * tensor_bytes)
+            rep(f"warm dw_bwd act=2 +bnsums occ={occ}",
+                timeit(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)), 3 * tensor_bytes)
+            ops._lib.call("xcp_tune", 17, oo)
+        for bd in ():
             ob = ops._lib.call("xcp_tune", 15, bd)
             rep(f"cold dw_bwd act=2 +bnsums bd={bd}",
                 cold(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)), 3 * tensor_bytes)
