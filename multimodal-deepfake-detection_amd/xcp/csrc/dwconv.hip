@@ -792,18 +792,51 @@ XCP_DEV void vmwait() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
 }
 
-// Stage pixels x0w-1 .. x0w+20 (64-B slice at channel c0) of row h of a frame into
-// dst (LDS, 1408 B) with two LDS-DMA instructions (88 lanes of 16 B).
+// Per-lane element offsets, within one frame row, of the two 16-B chunks a lane moves in
+// stage_row / store_row (-1: the zero line / the sink).  Computed once per wave, so a row
+// step's addresses are one scalar row offset plus these (no per-step 64-bit multiplies).
+struct RowLanes {
+  int off[2];
+};
+
+// load side: pixels x0w-1 .. x0w+20 of the 64-B slice at channel c0
 template <typename T>
-XCP_DEV void stage_row(const T* frame, int h, int H, int W, int C, int x0w, int c0, char* dst, int lane) {
+XCP_DEV RowLanes row_lanes_load(int W, int C, int x0w, int c0, int lane) {
   constexpr int EPC = 16 / (int)sizeof(T);
+  RowLanes r;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int ch = i * 64 + lane;            // chunk: pixel ch >> 2, 16-B part ch & 3
     const int col = x0w - 1 + (ch >> 2);
     const int c = c0 + (ch & 3) * EPC;
-    const bool ok = h < H && col >= 0 && col < W && c < C;
-    const void* src = ok ? (const void*)(frame + ((long)h * W + col) * C + c) : (const void*)g_dzero;
+    r.off[i] = (col >= 0 && col < W && c < C) ? col * C + c : -1;
+  }
+  return r;
+}
+
+// store side: pixels x0w .. x0w+19
+template <typename T>
+XCP_DEV RowLanes row_lanes_store(int W, int C, int x0w, int c0, int lane) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  RowLanes r;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ch = i * 64 + lane;
+    const int p = ch >> 2, col = x0w + p;
+    const int c = c0 + (ch & 3) * EPC;
+    r.off[i] = (p < RCOLS && col < W && c < C) ? col * C + c : -1;
+  }
+  return r;
+}
+
+// Stage pixels x0w-1 .. x0w+20 (64-B slice at channel c0) of row h of a frame into
+// dst (LDS, 1408 B) with two LDS-DMA instructions (88 lanes of 16 B).
+template <typename T>
+XCP_DEV void stage_row(const T* frame, int h, int H, int W, int C, const RowLanes& rl, char* dst, int lane) {
+  const T* row = frame + (long)h * W * C;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const void* src = (h < H && rl.off[i] >= 0) ? (const void*)(row + rl.off[i]) : (const void*)g_dzero;
     if (i == 0 || lane < 24)
       __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                        (void __attribute__((address_space(3)))*)(dst + i * 1024), 16, 0, 0);
@@ -813,16 +846,13 @@ XCP_DEV void stage_row(const T* frame, int h, int H, int W, int C, int x0w, int 
 // Write the staged output row (20 pixels x 64 B in `stg`) to row h: two 16-B stores
 // per lane-slot; lanes without a valid pixel write the sink.
 template <typename T>
-XCP_DEV void store_row(T* frame, int h, int W, int C, int x0w, int c0, const char* stg, int lane) {
-  constexpr int EPC = 16 / (int)sizeof(T);
+XCP_DEV void store_row(T* frame, int h, int W, int C, const RowLanes& rl, const char* stg, int lane) {
+  T* row = frame + (long)h * W * C;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int ch = i * 64 + lane;
-    const int p = ch >> 2, col = x0w + p;
-    const int c = c0 + (ch & 3) * EPC;
-    const bool ok = p < RCOLS && col < W && c < C;
     const uint4 v = *reinterpret_cast<const uint4*>(stg + min(ch, 4 * RCOLS - 1) * 16);
-    uint4* dstp = ok ? reinterpret_cast<uint4*>(frame + ((long)h * W + col) * C + c) : g_dsink + lane;
+    uint4* dstp = rl.off[i] >= 0 ? reinterpret_cast<uint4*>(row + rl.off[i]) : g_dsink + lane;
     *dstp = v;
   }
 }
@@ -851,6 +881,8 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(DwArgs a) {
   const bool cok = c < a.C;
   const int cc = cok ? c : a.C - EPT;
   const int x0w = mp.cg * RCOLS, x0 = x0w + sg * RS;
+  const RowLanes rl_ld = row_lanes_load<T>(a.W, a.C, x0w, c0, lane);
+  const RowLanes rl_st = row_lanes_store<T>(a.W, a.C, x0w, c0, lane);
   V wt[9], sc = V(1.f), sh = V(0.f);
 #pragma unroll
   for (int t = 0; t < 9; ++t) wt[t] = R::load(a.Wt + (long)t * a.C + cc);
@@ -886,7 +918,7 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(DwArgs a) {
   auto step = [&](int h, const V (&ra)[RS + 2], const V (&rb)[RS + 2], V (&rc)[RS + 2]) {
     vmwait<2 + 4 * (FD - 1)>();
     cvt(slot(h + 1), rc, h + 1 < a.H);
-    stage_row<T>(X, h + 1 + FD, a.H, a.W, a.C, x0w, c0, slot(h + 1 + FD), lane);   // slot of row h (consumed)
+    stage_row<T>(X, h + 1 + FD, a.H, a.W, a.C, rl_ld, slot(h + 1 + FD), lane);   // slot of row h (consumed)
     V o[RS];
 #pragma unroll
     for (int j = 0; j < RS; ++j) o[j] = V(0.f);
@@ -899,13 +931,13 @@ __global__ __launch_bounds__(256) void dw_fwd_lds_kernel(DwArgs a) {
         for (int j = 0; j < RS; ++j) o[j] = vfma((ky == 0 ? ra : ky == 1 ? rb : rc)[j + kx], wt[ky * 3 + kx], o[j]);
 #pragma unroll
     for (int j = 0; j < RS; ++j) *reinterpret_cast<unsigned*>(stg + (sg * RS + j) * SLICE + cl * 4) = R::pack(o[j]);
-    store_row<T>(Y, h, a.W, a.C, x0w, c0, stg, lane);
+    store_row<T>(Y, h, a.W, a.C, rl_st, stg, lane);
   };
   V w0[RS + 2], w1[RS + 2], w2[RS + 2];
 #pragma unroll
   for (int k = 0; k < RS + 2; ++k) w0[k] = V(0.f);
 #pragma unroll
-  for (int r = 0; r <= FD; ++r) stage_row<T>(X, r, a.H, a.W, a.C, x0w, c0, slot(r), lane);
+  for (int r = 0; r <= FD; ++r) stage_row<T>(X, r, a.H, a.W, a.C, rl_ld, slot(r), lane);
   vmwait<0>();
   cvt(slot(0), w1, true);
   for (int h = 0; h < a.H; h += 3) {
@@ -938,6 +970,8 @@ __global__ __launch_bounds__(256, OCC) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const bool cok = c < a.C;
   const int cc = cok ? c : a.C - EPT;
   const int x0w = mp.cg * RCOLS, x0 = x0w + sg * RS;
+  const RowLanes rl_ld = row_lanes_load<T>(a.W, a.C, x0w, c0, lane);
+  const RowLanes rl_st = row_lanes_store<T>(a.W, a.C, x0w, c0, lane);
   const bool bnsum = a.bnpart != nullptr;
   V wt[9], dw[9], sc = V(1.f), sh = V(0.f), bs1 = V(0.f), bs2 = V(0.f), mu = V(0.f), is = V(0.f);
 #pragma unroll
@@ -1021,9 +1055,9 @@ __global__ __launch_bounds__(256, OCC) void dw_bwd_lds_kernel(DwBwdArgs a) {
 #pragma unroll
       for (int j = 0; j < RS; ++j) pres[j] = rd(srh, j + 1);
     }
-    stage_row<T>(X, h + BD, a.H, a.W, a.C, x0w, c0, sx(h + BD), lane);          // slot of X row h-1
-    stage_row<T>(G, h + 1 + BD, a.H, a.W, a.C, x0w, c0, sgs(h + 1 + BD), lane);   // slot of dY row h
-    if constexpr (RES) stage_row<T>(dRes, h + BD, a.H, a.W, a.C, x0w, c0, sr(h + BD), lane);
+    stage_row<T>(X, h + BD, a.H, a.W, a.C, rl_ld, sx(h + BD), lane);          // slot of X row h-1
+    stage_row<T>(G, h + 1 + BD, a.H, a.W, a.C, rl_ld, sgs(h + 1 + BD), lane);   // slot of dY row h
+    if constexpr (RES) stage_row<T>(dRes, h + BD, a.H, a.W, a.C, rl_ld, sr(h + BD), lane);
     // independent accumulation chains: consecutive packed FMAs never depend on each other
     V sj[RS];
 #pragma unroll
@@ -1065,7 +1099,7 @@ __global__ __launch_bounds__(256, OCC) void dw_bwd_lds_kernel(DwBwdArgs a) {
       if (skip_row) s += R::unpack(pskp[j]);
       *reinterpret_cast<unsigned*>(stg + (sg * RS + j) * SLICE + cl * 4) = R::pack(s);
     }
-    store_row<T>(dX, h, a.W, a.C, x0w, c0, stg, lane);
+    store_row<T>(dX, h, a.W, a.C, rl_st, stg, lane);
   };
   V g0[RS + 2], g1[RS + 2], g2[RS + 2];
 #pragma unroll
@@ -1073,10 +1107,10 @@ __global__ __launch_bounds__(256, OCC) void dw_bwd_lds_kernel(DwBwdArgs a) {
   // prologue: X rows 0 .. BD-1, dY rows 0 .. BD, dRes rows 0 .. BD-1
 #pragma unroll
   for (int r = 0; r <= BD; ++r) {
-    if (r < BD) stage_row<T>(X, r, a.H, a.W, a.C, x0w, c0, sx(r), lane);
-    stage_row<T>(G, r, a.H, a.W, a.C, x0w, c0, sgs(r), lane);
+    if (r < BD) stage_row<T>(X, r, a.H, a.W, a.C, rl_ld, sx(r), lane);
+    stage_row<T>(G, r, a.H, a.W, a.C, rl_ld, sgs(r), lane);
     if constexpr (RES)
-      if (r < BD) stage_row<T>(dRes, r, a.H, a.W, a.C, x0w, c0, sr(r), lane);
+      if (r < BD) stage_row<T>(dRes, r, a.H, a.W, a.C, rl_ld, sr(r), lane);
   }
   vmwait<0>();
   cvtg(sgs(0), g1);
