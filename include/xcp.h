@@ -173,7 +173,9 @@ int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream
 
 /* ---- LSTM recurrence (nn.LSTM, XceptionLSTMV.py:18-23, :67) ----
  * whh is W_hh [4H][H] as nn.LSTM stores it (weight_hh_l0); whhT ([H][4H]) is read only by the
- * generic kernel, i.e. when xcp_lstm_needs_whhT(H) returns 1 (H = 64 / 128 run register-resident). */
+ * generic kernel, i.e. when xcp_lstm_needs_whhT(H) returns 1 (H = 64 / 128 run register-resident,
+ * H = 256 / 512 / 1024 on per-step kernels).  xcp_lstm_bwd's work: B*H + 4*H*H floats (the per-step
+ * kernels' cell-gradient carry and a transposed W_hh). */
 int xcp_lstm_needs_whhT(int H);
 int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
                  float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, xcp_stream_t stream);

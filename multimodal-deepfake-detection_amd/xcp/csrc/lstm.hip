@@ -347,12 +347,24 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(const float* __restr
   }
 }
 
+// whhT[k][j] = whh[j][k] (once per backward call, so a workgroup's W_hh columns are rows)
+__global__ __launch_bounds__(256) void lstm_transpose_kernel(const float* __restrict__ whh, float* __restrict__ whhT,
+                                                             int H) {
+  __shared__ float tl[32][33];
+  const int G4 = 4 * H;
+  const int j0 = blockIdx.x * 32, k0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8) tl[r][tx] = whh[(long)(j0 + r) * H + k0 + tx];
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) whhT[(long)(k0 + r) * G4 + j0 + tx] = tl[tx][r];
+}
+
 // backward step t: dh_t[b][k] = dout[b][t][k] + sum_j dgates_{t+1}[b][j] W_hh[j][k] (dhn at
 // t = T-1): thread (clip b, j-slice sl of 4H/16) against the workgroup's 2 W_hh columns in
 // LDS, 16-slice shuffle reduction; (clip, unit) threads run the cell backward with the cell
 // gradient carried in dcw [B][H] (each unit's carry is only touched by its workgroup).
 __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(const float* __restrict__ dout, const float* __restrict__ dhn,
-                                                            const float* __restrict__ dcn, const float* __restrict__ whh,
+                                                            const float* __restrict__ dcn, const float* __restrict__ whhT,
                                                             const float* __restrict__ cst, const float* __restrict__ gates,
                                                             float* __restrict__ dgates, float* __restrict__ dcw, int B,
                                                             int T, int H, int t) {
@@ -362,10 +374,9 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(const float* __restr
   float* sdh = sm + G4 * 2;
   const int tid = threadIdx.x, u0 = blockIdx.x * LS_UPW;
   if (t < T - 1) {
-    for (int jj = tid; jj < G4; jj += 256) {
-      const float2 v = *reinterpret_cast<const float2*>(whh + (long)jj * H + u0);
-      swc[2 * jj] = v.x;
-      swc[2 * jj + 1] = v.y;
+    for (int jj = tid; jj < G4; jj += 256) {   // rows u0, u0+1 of W_hh^T (contiguous)
+      swc[2 * jj] = whhT[(long)u0 * G4 + jj];
+      swc[2 * jj + 1] = whhT[(long)(u0 + 1) * G4 + jj];
     }
     __syncthreads();
     const int per = G4 / 16;
@@ -491,9 +502,11 @@ int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const fl
   if (B <= 0 || T <= 0) return XCP_OK;
   if (lstm_step(B, H)) {
     if (!work) return XCP_EINVAL;
+    float* whhT = work + (long)B * H;
+    hipLaunchKernelGGL(lstm_transpose_kernel, dim3(4 * H / 32, H / 32), dim3(256), 0, st, whh, whhT, H);
     const size_t smem = ((size_t)8 * H + 2 * B) * sizeof(float);
     for (int t = T - 1; t >= 0; --t)
-      hipLaunchKernelGGL(lstm_bwd_step_kernel, dim3(H / LS_UPW), dim3(256), smem, st, dout, dhn, dcn, whh, cst, gates,
+      hipLaunchKernelGGL(lstm_bwd_step_kernel, dim3(H / LS_UPW), dim3(256), smem, st, dout, dhn, dcn, whhT, cst, gates,
                          dgates, work, B, T, H, t);
     return (int)hipGetLastError();
   }

@@ -373,6 +373,7 @@ def lstm_fwd(xproj, whh, whhT, bih, bhh, out, hprev, cst, gates, hn, cn, B, T, H
 
 
 def lstm_bwd(dout, dhn, dcn, whh, cst, gates, dgates, B, T, H):
-    work = torch.empty(B * H, device=whh.device, dtype=torch.float32)   # cell-gradient carry (per-step kernels)
+    # per-step kernels: cell-gradient carry [B][H] + W_hh^T [H][4H]
+    work = torch.empty(B * H + 4 * H * H, device=whh.device, dtype=torch.float32)
     _lib.call("xcp_lstm_bwd", _p(dout), _p(dhn), _p(dcn), _p(whh), _p(cst), _p(gates), _p(dgates), _p(work), B, T, H,
               stream())
