@@ -462,11 +462,30 @@ class XceptionFunction(torch.autograd.Function):
         ctx.engine, ctx.S = engine, S
         ctx.names = [n for n, _ in engine.named_params()]
         ctx.needs = [p.requires_grad for p in params]
+        ctx.params = params
         return feats
 
     @staticmethod
     def backward(ctx, dfeat):
+        """Accumulates the backbone gradients into ``param.grad`` itself -- one fused
+        ``_foreach_add_`` for all of them (a parameter without a gradient takes the engine's
+        tensor) -- and returns None for the parameters, instead of handing ~170 tensors to
+        autograd's per-parameter accumulation (one add kernel each, ~0.8 ms per step).
+        Post-accumulate-grad hooks therefore do not fire for backbone parameters; xcp.ddp
+        reduces such buckets in ``GradBuckets.allreduce``."""
         grads = ctx.engine.backward(ctx.S, dfeat)
         ctx.S = None
-        out = [grads.get(n) if need else None for n, need in zip(ctx.names, ctx.needs)]
-        return (None, None, None, *out)
+        acc, new = [], []
+        for n, need, p in zip(ctx.names, ctx.needs, ctx.params):
+            gt = grads.get(n) if need else None
+            if gt is None:
+                continue
+            if p.grad is None:
+                p.grad = gt
+            else:
+                acc.append(p.grad)
+                new.append(gt)
+        if acc:
+            torch._foreach_add_(acc, new)
+        ctx.params = None
+        return (None, None, None, *([None] * len(ctx.names)))
