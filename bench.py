@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--optim", choices=["fused", "torch"], default="fused",
+                    help="fused: xcp.optim.FusedAdamClip (clip + Adam in two HIP launches); torch: "
+                         "clip_grad_norm_ + torch.optim.Adam(fused=True)")
     a = ap.parse_args()
     audio = a.model == "lstma"
     a.frames = a.frames or (120 if audio else 16)
@@ -150,10 +153,12 @@ def main():
     model = model.to(dev).train()
     params = [p for p in model.parameters() if p.requires_grad]
     buckets = ddp.GradBuckets(params, world=world)
-    if audio:   # train_audio.py:33-44
-        opt = torch.optim.Adam(params, lr=1e-4, fused=True)
-    else:       # train_visual.py:540-577
-        opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4, fused=True)   # one fused launch per step
+    lr, wd = (1e-4, 0.0) if audio else (1e-5, 1e-4)   # train_audio.py:33-44 / train_visual.py:540-577
+    if args.optim == "fused":
+        from xcp.optim import FusedAdamClip
+        opt = FusedAdamClip(params, lr=lr, weight_decay=wd, max_norm=1.0)
+    else:
+        opt = torch.optim.Adam(params, lr=lr, weight_decay=wd, fused=True)
     crit = nn.BCELoss()
 
     B, T, S = args.batch, args.frames, args.size
@@ -171,8 +176,9 @@ def main():
         loss = crit(prob, labels)
         loss.backward()
         buckets.allreduce()
-        torch.nn.utils.clip_grad_norm_(params, 1.0)
-        opt.step()
+        if args.optim == "torch":
+            torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()   # (the fused optimizer clips to norm 1.0 inside)
         return loss
 
     for _ in range(args.warmup):
@@ -246,6 +252,8 @@ def main():
                "clips, seeded per rank; random-init weights, Xception.py:154-160 scheme)",
                "config": {"workload": f"{name} {args.mode}-backbone train step, {B} clips/GPU x {shape}, BCE + Adam",
                           "global_batch": B * world, "frames": T, "size": S, "mode": args.mode,
+                          "optimizer": "clip 1.0 + Adam, " + ("xcp FusedAdamClip" if args.optim == "fused"
+                                                               else "torch fused Adam"),
                           "parallelism": f"dp{world}"},
                "roofline": roof, "loss": round(float(loss.item()), 5)}
         out.update(extra)

@@ -167,6 +167,15 @@ int xcp_frames_u8_to_f32(const unsigned char* in, const int* len, float* out, in
  * weight formulas in fp32); MFCC frames [B*T*3][13][1] -> [B*T*3][64][64] */
 int xcp_resize_bilinear(const float* in, float* out, int NC, int IH, int IW, int OH, int OW, xcp_stream_t stream);
 
+/* ---- training step (train_visual.py:575-577): clip_grad_norm_ + Adam (L2 weight decay) ----
+ * tab: DEVICE [nchunks][6] int64 (param, grad, exp_avg, exp_avg_sq, first element, length <= 16384),
+ * all fp32.  xcp_opt_sumsq: out[0] = min(1, max_norm / (||g|| + 1e-6)) (1 if max_norm <= 0),
+ * out[1] = ||g||, part = [nchunks] scratch.  xcp_opt_adam: g' = g * coef[0] (coef may be null),
+ * g' += wd p; m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2; p -= lr / bc1 * m / (sqrt(v) / bc2sqrt + eps) */
+int xcp_opt_sumsq(const long long* tab, int nchunks, float* part, float max_norm, float* out, xcp_stream_t stream);
+int xcp_opt_adam(const long long* tab, int nchunks, const float* coef, float lr, float b1, float b2, float eps, float wd,
+                 float bc1, float bc2sqrt, xcp_stream_t stream);
+
 /* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][10] int64
  * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block), nblocks in total */
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream_t stream);

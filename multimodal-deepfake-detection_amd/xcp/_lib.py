@@ -54,6 +54,8 @@ SIGNATURES = {
     "xcp_permute3_batch": [P, I, I, P],
     "xcp_frames_u8_to_f32": [P, P, P, I, I, I, I, P],
     "xcp_resize_bilinear": [P, P, I, I, I, I, I, P],
+    "xcp_opt_sumsq": [P, I, P, F, P, P],
+    "xcp_opt_adam": [P, I, P, F, F, F, F, F, F, F, P],
     "xcp_conv3x3_parts": [I, I, I, I],
     "xcp_conv3x3": [I, P, P, P, P, I, I, I, P],
     "xcp_conv3x3_wgrad_parts": [I, I, I],

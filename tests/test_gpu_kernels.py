@@ -506,3 +506,28 @@ def test_conv3x3_stem_fwd_dgrad(ops, gpu, N, IH, IW):
     ref_dw = torch.nn.grad.conv2d_weight(x.float(), (64, 32, 3, 3), dy.float())
     got = dW.view(64, 3, 3, 32).permute(0, 3, 1, 2)
     assert rel_err(got, ref_dw) < 1e-4
+
+
+@pytest.mark.parametrize("max_norm", [None, 1.0, 1e-3])
+def test_fused_adam_clip_vs_torch(ops, gpu, max_norm):
+    """xcp.optim.FusedAdamClip (csrc/optim.hip) against clip_grad_norm_ + torch.optim.Adam (L2
+    weight decay) over three steps, on tensors below, at and above the 16384-element chunk."""
+    from xcp.optim import FusedAdamClip
+    g = torch.Generator(device=gpu).manual_seed(11)
+    shapes = [(3,), (128, 129), (16384,), (40000,), (7, 5, 3, 3)]
+    a = [torch.randn(s, device=gpu, generator=g).requires_grad_(True) for s in shapes]
+    b = [t.detach().clone().requires_grad_(True) for t in a]
+    opt_a = FusedAdamClip(a, lr=1e-2, weight_decay=1e-2, max_norm=max_norm)
+    opt_b = torch.optim.Adam(b, lr=1e-2, weight_decay=1e-2)
+    for step in range(3):
+        grads = [torch.randn(s, device=gpu, generator=g) for s in shapes]
+        for p, q, gr in zip(a, b, grads):
+            p.grad = gr.clone()
+            q.grad = gr.clone()
+        na = opt_a.step()
+        if max_norm is not None:
+            nb = torch.nn.utils.clip_grad_norm_(b, max_norm)
+            torch.testing.assert_close(na, nb, rtol=1e-5, atol=0)
+        opt_b.step()
+        for p, q in zip(a, b):
+            torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
