@@ -3,22 +3,28 @@
 BASELINE.json metric: "clips/sec (node) XceptionLSTMV 16x299x299 bf16 train at
 1/2/4/8 MI355X".  One step = one training pass over b clips per GPU (synthetic,
 on-device, seeded per rank): backbone (train-mode BN) -> LSTM(128) -> FC head ->
-BCELoss -> backward -> gradient all-reduce (RCCL) -> clip_grad_norm_(1.0) ->
-Adam(lr 1e-5, wd 1e-4) (train_visual.py:540-577 semantics).  Default mode is the
-unfrozen backbone (train_visual.py:551-556, every epoch after the 3rd); the
-frozen backbone (as shipped, XceptionLSTMV.py:15-16) is ``--mode frozen``.
+BCELoss -> backward (gradient all-reduce over RCCL overlapped with it) ->
+clip_grad_norm_(1.0) -> Adam(lr 1e-5, wd 1e-4) (train_visual.py:533-577 semantics).
+The headline is the unfrozen backbone (train_visual.py:551-556, every epoch after the
+3rd); the frozen backbone (as shipped, XceptionLSTMV.py:15-16) is measured in the same
+run and reported under "frozen".
 
-``--model lstma`` runs the audio configuration instead (C4: XceptionLSTMA(512) on MFCC
-clips [b, 120, 3, 13] resized to 64x64 on the GPU, frozen backbone as shipped,
-Adam lr 1e-4, train_audio.py:33-44); it is a secondary line, not the headline metric.
+Other configurations (secondary lines, BASELINE.json configs):
+  --model xception : C2, Xception(num_classes=1) trained per frame, 64 frames of 299^2
+                     (BCEWithLogits, Adam) -> frames/s
+  --model lstma    : C4, XceptionLSTMA(512) on MFCC clips [b, 120, 3, 13] resized to 64^2
+                     on the GPU, frozen backbone as shipped, Adam lr 1e-4 (train_audio.py:33-44)
 
-Launch: ``python bench.py [--gpus N --steps K --warmup W]``; N>1 under
-``torch.distributed.run`` (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from env).
-Rank 0 prints ONE JSON line.
+Launch: ``python bench.py [--gpus N --steps K --warmup W]``.  Under torch.distributed.run
+(WORLD_SIZE set) one process drives one GPU; with --gpus N > 1 and no WORLD_SIZE this
+process starts N ranks itself through torch.distributed.run (before touching the GPU) and
+exits with their status.  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
@@ -26,10 +32,6 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 for _p in (os.path.join(REPO, "multimodal-deepfake-detection_amd"), REPO):
     if _p not in sys.path:
         sys.path.insert(0, _p)
-
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-import torch.nn as nn  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, spec)
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E (spec)
@@ -40,15 +42,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", choices=["lstmv", "lstma"], default="lstmv")
-    ap.add_argument("--batch", type=int, default=16, help="clips per GPU")
+    ap.add_argument("--model", choices=["lstmv", "lstma", "xception"], default="lstmv")
+    ap.add_argument("--batch", type=int, default=None, help="clips (frames for xception) per GPU")
     ap.add_argument("--frames", type=int, default=None, help="frames per clip (default 16; 120 for lstma)")
     ap.add_argument("--size", type=int, default=299)
-    ap.add_argument("--mode", choices=["unfrozen", "frozen"], default=None,
-                    help="backbone training (default unfrozen; frozen for lstma, as shipped)")
+    ap.add_argument("--mode", choices=["unfrozen", "frozen", "both"], default=None,
+                    help="backbone training (lstmv default: both, unfrozen is the headline; lstma: frozen)")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--optim", choices=["fused", "torch"], default="fused",
                     help="fused: xcp.optim.FusedAdamClip (clip + Adam in two HIP launches); torch: "
@@ -56,10 +58,21 @@ def parse():
     a = ap.parse_args()
     audio = a.model == "lstma"
     a.frames = a.frames or (120 if audio else 16)
-    a.mode = a.mode or ("frozen" if audio else "unfrozen")
+    a.batch = a.batch or (64 if a.model == "xception" else 16)
+    a.mode = a.mode or ("frozen" if audio else "unfrozen" if a.model == "xception" else "both")
     if audio:
         a.size = 64
     return a
+
+
+def launch_ranks(args):
+    """--gpus N without a torch.distributed.run parent: start N ranks (one per GPU) through it.
+    Runs before any GPU call in this process; the ranks inherit stdout (rank 0 prints the line)."""
+    port = 29400 + os.getpid() % 1000
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def middle_hw(size):
@@ -70,14 +83,102 @@ def middle_hw(size):
     return h
 
 
+# ------------------------------------------------------------------------------ step roofline
+BLOCKS = [(64, 128, 2, 2, False, True), (128, 256, 2, 2, True, True), (256, 728, 2, 2, True, True)] + \
+    [(728, 728, 3, 1, True, True)] * 8 + [(728, 1024, 2, 2, True, False)]   # Xception.py:125-140
+
+
+def step_roofline(size, frames, unfrozen, s=2):
+    """Ideal time of one backbone step of this design: sum over its kernels of
+    max(flops / MFMA peak, bytes / HBM peak), with each kernel's algorithmic flops and the
+    bytes it must move (read its inputs once, write its outputs once; s = bytes per element).
+    Returns (ms, total flops, total bytes).  The LSTM / FC head (< 0.1 % of the flops) is left
+    out.  SURVEY §8(d): step roofline time = sum_ops max(flops/peak_flops, bytes/peak_bw)."""
+    ops_ = []
+
+    def op(fl, by):
+        ops_.append((fl, by))
+
+    n = frames
+    oh1 = (size - 3) // 2 + 1
+    oh2 = oh1 - 2
+    p1, p2 = n * oh1 * oh1, n * oh2 * oh2
+    op(2 * 27 * 32 * p1, 4 * 3 * n * size * size + s * 32 * p1)                  # conv1
+    op(0, s * 32 * p1 * 3)                                                      # bn1 stats + apply
+    op(2 * 288 * 64 * p2, s * (32 * p1 + 64 * p2))                              # conv2 (+stats)
+    op(0, s * 64 * p2 * 2)                                                      # bn2 apply
+    bwd = []
+    h = oh2
+
+    def unit(cin, cout, hw, reduce=False):
+        P = n * hw * hw
+        op(0, 2 * s * P * cin + 36 * cin)                       # depthwise fwd (BN+ReLU on load)
+        op(2 * P * cin * cout, s * P * (cin + cout))            # pointwise (+BN stats epilogue)
+        # BN backward: apply (read dz, y; write dy); its reduce comes fused from the consumer's
+        # depthwise backward / the max-pool backward, except after a residual / the avg-pool
+        bwd.append((0, (5 if reduce else 3) * s * P * cout))
+        bwd.append((2 * P * cin * cout, s * P * (cin + cout)))  # pointwise dgrad
+        bwd.append((2 * P * cin * cout, s * P * (cin + cout)))  # pointwise wgrad
+        bwd.append((0, 3 * s * P * cin))                        # depthwise dgrad + wgrad (+BN partials)
+
+    for cin, cout, reps, stride, _, grow in BLOCKS:
+        filt = [(cin, cout)] + [(cout, cout)] * (reps - 1) if grow else [(cin, cin)] * (reps - 1) + [(cin, cout)]
+        for i, (a, b) in enumerate(filt):
+            unit(a, b, h, reduce=(i == len(filt) - 1 and stride == 1))
+        oh = (h - 1) // stride + 1
+        P, Ps = n * h * h, n * oh * oh
+        if stride != 1 or cin != cout:
+            op(2 * Ps * cin * cout, s * Ps * (cin + cout))                      # skip conv (+stats)
+            bwd.append((0, 5 * s * Ps * cout))                                  # skip BN backward
+            bwd.append((4 * Ps * cin * cout, 2 * s * Ps * (cin + cout)))        # skip dgrad + wgrad
+        op(0, s * (P * cout + 2 * Ps * cout) + (Ps * cout if stride != 1 else 0))   # tail (BN, pool, add)
+        if stride != 1:
+            bwd.append((0, s * (Ps * cout + 2 * P * cout) + Ps * cout))        # max-pool backward (+BN reduce)
+        else:
+            bwd.append((0, s * P * cout))                                       # residual gradient read
+        h = oh
+    unit(1024, 1536, h)
+    unit(1536, 2048, h, reduce=True)
+    op(0, s * n * h * h * 2048)                                                 # bn4 + ReLU + avgpool
+    if unfrozen:
+        bwd.append((0, 2 * s * n * h * h * 2048))                               # avgpool backward
+        bwd.append((0, 5 * s * 64 * p2))                                        # bn2 backward
+        bwd.append((2 * 576 * 32 * p1, s * (64 * p2 + 32 * p1)))               # conv2 dgrad
+        bwd.append((2 * 288 * 64 * p2, s * (64 * p2 + 32 * p1)))                # conv2 wgrad
+        bwd.append((0, 5 * s * 32 * p1))                                        # bn1 backward
+        bwd.append((2 * 27 * 32 * p1, 4 * 3 * n * size * size + s * 32 * p1))  # conv1 wgrad
+        ops_.extend(bwd)
+    ms = sum(max(fl / (PEAK_BF16_TFLOPS * 1e12), by / (PEAK_HBM_GBS * 1e9)) for fl, by in ops_) * 1e3
+    return ms, sum(fl for fl, _ in ops_), sum(by for _, by in ops_)
+
+
+# ------------------------------------------------------------------------------ CPU baseline
+def host_cores():
+    """CPUs this process may use: its affinity, capped by a cgroup CPU quota when one is set."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(args, frames):
-    """Oracle (CPU fp32 restatement of the reference, oracle/) on a bounded sample:
-    one clip of the same shape, 1 warm-up + cpu_steps timed train steps."""
+    """Oracle (oracle/xception_oracle.py: the CPU fp32 restatement of the reference, PyTorch on
+    every host core this process may run on) on a bounded sample: one clip of the same shape,
+    1 warm-up + cpu_steps timed full train steps (forward, BCE, backward, clip_grad_norm_, Adam),
+    for each backbone mode the GPU line reports."""
+    import torch
     from Models.XceptionLSTMA import XceptionLSTMA
     from Models.XceptionLSTMV import XceptionLSTMV
     from oracle import xception_oracle as O
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    cores = host_cores()
     torch.set_num_threads(cores)
     torch.manual_seed(0)
     audio = args.model == "lstma"
@@ -86,12 +187,17 @@ def cpu_baseline(args, frames):
     x = torch.randn((1, frames, 3, 13), generator=gen) if audio else \
         torch.rand((1, frames, 3, args.size, args.size), generator=gen)
     y = torch.tensor([[1.0]])
-    unfrozen = args.mode == "unfrozen"
-    O.clip_step(sd, x, y, unfrozen, audio=audio)
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        O.clip_step(sd, x, y, unfrozen, audio=audio)
-    dt = (time.perf_counter() - t0) / args.cpu_steps
+    optim = dict(lr=1e-4, weight_decay=0.0, max_norm=None) if audio else dict(lr=1e-5, weight_decay=1e-4, max_norm=1.0)
+    modes = ["unfrozen", "frozen"] if args.mode == "both" else [args.mode]
+    res = {}
+    for mode in modes:
+        log(f"cpu baseline {mode}: {cores} threads, 1 + {args.cpu_steps} steps")
+        O.clip_step(sd, x, y, mode == "unfrozen", audio=audio, optim=optim)
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_steps):
+            O.clip_step(sd, x, y, mode == "unfrozen", audio=audio, optim=optim)
+        res[mode] = args.cpu_steps / (time.perf_counter() - t0)
+        log(f"cpu baseline {mode}: {res[mode]:.4f} clips/s")
     cpu_name = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -100,10 +206,15 @@ def cpu_baseline(args, frames):
                 break
     except OSError:
         pass
-    return {"value": round(1.0 / dt, 4), "unit": "clips/s", "cores": cores, "kind": "port",
-            "sample": f"{args.cpu_steps} timed + 1 warm-up {args.mode} train steps of 1 clip x "
-                      f"{frames}x{'3x13 MFCC -> 64^2' if audio else f'3x{args.size}^2'}, "
-                      f"fp32, oracle/xception_oracle.py (PyTorch CPU), {cpu_name}"}
+    head = modes[0]
+    out = {"value": round(res[head], 4), "unit": "clips/s", "cores": cores, "kind": "port",
+           "sample": f"{args.cpu_steps} timed + 1 warm-up {head} train steps (BCE, backward, clip, Adam) of 1 clip x "
+                     f"{frames}x{'3x13 MFCC -> 64^2' if audio else f'3x{args.size}^2'}, fp32, oracle/xception_oracle.py "
+                     f"(PyTorch CPU, {cores} threads = the CPUs this process may use: affinity capped by "
+                     f"the cgroup quota), {cpu_name}"}
+    if "frozen" in res and head != "frozen":
+        out["frozen"] = round(res["frozen"], 4)
+    return out
 
 
 def pmc_traffic():
@@ -127,9 +238,108 @@ def pmc_traffic():
     return out
 
 
+# ------------------------------------------------------------------------------ GPU runs
+class Run:
+    """One model + optimiser + synthetic batch on this rank; step() is one training step."""
+
+    def __init__(self, args, mode, dev, rank, world):
+        import torch
+        import torch.nn as nn
+        from xcp import ddp
+        self.torch = torch
+        self.args, self.mode, self.world = args, mode, world
+        torch.manual_seed(0)
+        B, T, S = args.batch, args.frames, args.size
+        if args.model == "xception":
+            from Models.Xception import xception
+            model = xception(num_classes=1)
+            self.crit = nn.BCEWithLogitsLoss()
+        elif args.model == "lstma":
+            from Models.XceptionLSTMA import XceptionLSTMA
+            model = XceptionLSTMA(512, pretrained=False)
+            self.crit = nn.BCELoss()
+        else:
+            from Models.XceptionLSTMV import XceptionLSTMV
+            model = XceptionLSTMV(128, pretrained=False)
+            self.crit = nn.BCELoss()
+        backbone = model if args.model == "xception" else model.feature_extractor
+        for p in backbone.parameters():
+            p.requires_grad = mode == "unfrozen"
+        if args.model == "xception":
+            model.fc.weight.requires_grad = model.fc.bias.requires_grad = True
+        self.model = model.to(dev).train()
+        self.params = list(self.model.parameters())
+        self.buckets = ddp.GradBuckets(self.params, world=world, module=self.model)
+        lr, wd = (1e-4, 0.0) if args.model == "lstma" else (1e-5, 1e-4)
+        if args.optim == "fused":
+            from xcp.optim import FusedAdamClip
+            self.opt = FusedAdamClip(self.params, lr=lr, weight_decay=wd, max_norm=1.0)
+        else:
+            self.opt = torch.optim.Adam([p for p in self.params if p.requires_grad], lr=lr, weight_decay=wd, fused=True)
+        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        if args.model == "lstma":
+            self.x = torch.randn((B, T, 3, 13), generator=g, device=dev)
+        elif args.model == "xception":
+            self.x = torch.rand((B, 3, S, S), generator=g, device=dev)
+        else:
+            self.x = torch.rand((B, T, 3, S, S), generator=g, device=dev)
+        gl = torch.Generator(device=dev).manual_seed(4321 + rank)
+        self.y = torch.randint(0, 2, (B, 1), generator=gl, device=dev).float()
+        self.dev = dev
+
+    def step(self):
+        from xcp import ddp
+        self.buckets.zero()
+        ddp.broadcast_buffers(self.model)
+        if self.args.model == "xception":
+            out = self.model(self.x)
+        else:
+            out = self.model(self.model.extract_features(self.x, self.dev))
+        loss = self.crit(out, self.y)
+        loss.backward()
+        self.buckets.allreduce()
+        if self.args.optim == "torch":
+            self.torch.nn.utils.clip_grad_norm_([p for p in self.params if p.grad is not None], 1.0)
+        self.opt.step()   # (the fused optimiser clips to norm 1.0 inside)
+        return loss
+
+
+def timed(run, steps, warmup, world, timer=None):
+    import torch
+    import torch.distributed as dist
+    from xcp import ops
+    for _ in range(warmup):
+        run.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if timer is not None:
+        ops.set_kernel_timer(timer)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = run.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.set_kernel_timer(None)
+    if world > 1:
+        e = torch.tensor([elapsed], device=run.dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = e.item()
+    return elapsed, float(loss.item())
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    import torch
+    import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -138,90 +348,44 @@ def main():
     dev = torch.device("cuda", local)
 
     import xcp
-    from xcp import ddp, ops
-    from Models.XceptionLSTMA import XceptionLSTMA
-    from Models.XceptionLSTMV import XceptionLSTMV
+    from xcp import ops
     xcp.set_compute_dtype(args.dtype)
     xcp.load_library()
-    audio = args.model == "lstma"
-
-    torch.manual_seed(0)
-    model = XceptionLSTMA(512, pretrained=False) if audio else XceptionLSTMV(128, pretrained=False)
-    if args.mode == "unfrozen":
-        for p in model.feature_extractor.parameters():
-            p.requires_grad = True
-    model = model.to(dev).train()
-    params = [p for p in model.parameters() if p.requires_grad]
-    buckets = ddp.GradBuckets(params, world=world)
-    lr, wd = (1e-4, 0.0) if audio else (1e-5, 1e-4)   # train_audio.py:33-44 / train_visual.py:540-577
-    if args.optim == "fused":
-        from xcp.optim import FusedAdamClip
-        opt = FusedAdamClip(params, lr=lr, weight_decay=wd, max_norm=1.0)
-    else:
-        opt = torch.optim.Adam(params, lr=lr, weight_decay=wd, fused=True)
-    crit = nn.BCELoss()
-
+    audio, single = args.model == "lstma", args.model == "xception"
     B, T, S = args.batch, args.frames, args.size
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    clips = torch.randn((B, T, 3, 13), generator=g, device=dev) if audio else \
-        torch.rand((B, T, 3, S, S), generator=g, device=dev)
-    gl = torch.Generator(device=dev).manual_seed(4321 + rank)
-    labels = torch.randint(0, 2, (B, 1), generator=gl, device=dev).float()
+    frames = B if single else B * T
+    modes = ["unfrozen", "frozen"] if args.mode == "both" else [args.mode]
 
-    def step():
-        buckets.zero()
-        ddp.broadcast_buffers(model)
-        feats = model.extract_features(clips, dev)
-        prob = model(feats)
-        loss = crit(prob, labels)
-        loss.backward()
-        buckets.allreduce()
-        if args.optim == "torch":
-            torch.nn.utils.clip_grad_norm_(params, 1.0)
-        opt.step()   # (the fused optimizer clips to norm 1.0 inside)
-        return loss
+    results = {}
+    for mode in modes:
+        if rank == 0:
+            log(f"{args.model} {mode}: building model")
+        run = Run(args, mode, dev, rank, world)
+        timer = None
+        if not args.no_kernel_timing and mode == modes[0] and not audio:
+            hm = middle_hw(S)
+            timer = ops.KernelTimer({"pw_gemm_728": lambda name, a: name == "gemm_nt" and a["M"] == frames * hm * hm
+                                     and a["N"] == 728 and a["K"] == 728 and a["stats"] is not None,
+                                     "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == 728 and a["H"] == hm})
+        steps = args.steps if mode == modes[0] else max(3, args.steps // 2)
+        elapsed, loss = timed(run, steps, args.warmup, world, timer)
+        results[mode] = (elapsed, steps, loss, timer)
+        if rank == 0:
+            log(f"{args.model} {mode}: {1e3 * elapsed / steps:.2f} ms/step")
+        del run
+        torch.cuda.empty_cache()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-
-    timer = None
-    if not args.no_kernel_timing:
-        hm = middle_hw(S)
-        timer = ops.KernelTimer({"pw_gemm_728": lambda name, a: name == "gemm_nt" and a["M"] == B * T * hm * hm
-                                 and a["N"] == 728 and a["K"] == 728 and a["stats"] is not None,
-                                 "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == 728 and a["H"] == hm})
-        ops.set_kernel_timer(timer)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ops.set_kernel_timer(None)
-    if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = e.item()
-
-    clips_total = B * world * args.steps
-    value = clips_total / elapsed
-    out = None
     if rank == 0:
+        head = modes[0]
+        elapsed, steps, loss, timer = results[head]
+        units = B * world * steps
+        value = units / elapsed
         hm = middle_hw(S)
-        M = B * T * hm * hm
-        roof = None
-        extra = {}
-        traffic = {} if audio else pmc_traffic()   # the committed PMC passes are of the headline (lstmv) bench
+        M = frames * hm * hm
+        roof, extra = None, {}
+        traffic = {} if (audio or single) else pmc_traffic()   # the committed PMC passes are of the headline bench
         if timer is not None:
-            pw_ms = timer.mean_ms("pw_gemm_728")
-            dw_ms = timer.mean_ms("dw_fwd_728")
+            pw_ms, dw_ms = timer.mean_ms("pw_gemm_728"), timer.mean_ms("dw_fwd_728")
             if pw_ms:
                 flops = 2.0 * M * 728 * 728
                 ach = flops / (pw_ms * 1e-3) / 1e12
@@ -230,8 +394,7 @@ def main():
                         "traffic": traffic.get("gemm_nt", (None,))[0],
                         "traffic_source": traffic.get("gemm_nt", (None, None))[1],
                         "kernel": f"gemm_nt256k64_kernel (bf16 pointwise 1x1 728->728 @{hm}x{hm}, middle flow)",
-                        "flops_per_launch": flops, "avg_launch_ms": round(pw_ms, 4),
-                        "launches": timer.count("pw_gemm_728")}
+                        "flops_per_launch": flops, "avg_launch_ms": round(pw_ms, 4), "launches": timer.count("pw_gemm_728")}
             if dw_ms:
                 byts = 2.0 * (2 * M * 728) + 4 * 9 * 728
                 gbs = byts / (dw_ms * 1e-3) / 1e9
@@ -241,25 +404,47 @@ def main():
                                         "traffic_source": traffic.get("dw_fwd_kernel", (None, None))[1],
                                         "kernel": f"dw_fwd_kernel<bf16> (depthwise 3x3 C=728 @{hm}x{hm})",
                                         "bytes_per_launch": byts, "avg_launch_ms": round(dw_ms, 4)}
-        metric = (f"clips/sec (node) XceptionLSTMA MFCC {T}x3x13 (64x64) {args.dtype} train" if audio else
-                  "clips/sec (node) XceptionLSTMV 16x299x299 bf16 train")
-        name = "XceptionLSTMA(hidden=512)" if audio else "XceptionLSTMV(hidden=128)"
-        shape = f"{T} MFCC frames x 3x13 -> 64x64" if audio else f"{T} frames x 3x{S}x{S}"
-        out = {"metric": metric,
-               "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": f"synthetic (on-device {'N(0,1) MFCC' if audio else 'U[0,1)'} "
-               "clips, seeded per rank; random-init weights, Xception.py:154-160 scheme)",
-               "config": {"workload": f"{name} {args.mode}-backbone train step, {B} clips/GPU x {shape}, BCE + Adam",
-                          "global_batch": B * world, "frames": T, "size": S, "mode": args.mode,
+        if not audio and args.dtype == "bf16":
+            ideal, fl, by = step_roofline(S, frames, head == "unfrozen")
+            ms = 1e3 * elapsed / steps
+            extra["step_roofline"] = {"ideal_ms": round(ideal, 3), "ms_per_step": round(ms, 3),
+                                      "frac": round(ideal / ms, 4), "flops": fl, "bytes": by,
+                                      "model": "sum over the backbone's kernels of max(flops / 2.5 PF bf16, bytes / "
+                                               "8 TB/s), bytes = each kernel's inputs read once + outputs written once "
+                                               "(bench.py step_roofline)"}
+        if "frozen" in results and head != "frozen":
+            e2, s2, l2, _ = results["frozen"]
+            fz = {"value": round(B * world * s2 / e2, 3), "ms_per_step": round(1e3 * e2 / s2, 3), "steps": s2,
+                  "loss": round(l2, 5)}
+            if not audio:
+                ideal, _, _ = step_roofline(S, frames, False)
+                fz["step_roofline_frac"] = round(ideal / (1e3 * e2 / s2), 4)
+            extra["frozen"] = fz
+        if audio:
+            metric = f"clips/sec (node) XceptionLSTMA MFCC {T}x3x13 (64x64) {args.dtype} train"
+            name, shape = "XceptionLSTMA(hidden=512)", f"{T} MFCC frames x 3x13 -> 64x64"
+        elif single:
+            metric = f"frames/sec (node) Xception single-frame {S}x{S} {args.dtype} train"
+            name, shape = "Xception(num_classes=1)", f"3x{S}x{S} frames"
+        else:
+            metric = "clips/sec (node) XceptionLSTMV 16x299x299 bf16 train"
+            name, shape = "XceptionLSTMV(hidden=128)", f"{T} frames x 3x{S}x{S}"
+        unit = "frames/s" if single else "clips/s"
+        out = {"metric": metric, "value": round(value, 3), "unit": unit, "n_gpus": world, "steps": steps,
+               "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / steps, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+               "data": f"synthetic (on-device {'N(0,1) MFCC' if audio else 'U[0,1)'} inputs, seeded per rank; "
+                       "random-init weights, Xception.py:154-160 scheme)",
+               "config": {"workload": f"{name} {head}-backbone train step, {B} {'frames' if single else 'clips'}/GPU x "
+                                      f"{shape}, {'BCEWithLogits' if single else 'BCE'} + clip 1.0 + Adam",
+                          "global_batch": B * world, "frames": 1 if single else T, "size": S, "mode": head,
                           "optimizer": "clip 1.0 + Adam, " + ("xcp FusedAdamClip" if args.optim == "fused"
                                                                else "torch fused Adam"),
                           "parallelism": f"dp{world}"},
-               "roofline": roof, "loss": round(float(loss.item()), 5)}
+               "roofline": roof, "loss": round(loss, 5)}
         out.update(extra)
-    if rank == 0 and args.cpu_baseline == "on" and world == 1:
-        out["cpu_baseline"] = cpu_baseline(args, T)
-    if rank == 0:
+        if args.cpu_baseline == "on" and world == 1 and not single:
+            out["cpu_baseline"] = cpu_baseline(args, T)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -40,19 +40,23 @@ typedef void* xcp_stream_t; /* hipStream_t */
  * C[M,N] = A[M,K] . B[N,K]^T ; optional stats[xcp_gemm_nt_stat_rows(M)][2][N] partial
  * (sum, sum^2) of the stored C columns (BatchNorm batch statistics).
  * gmode: 0 dense rows, 1 strided (skip conv, stride gS), 2 im2col 3x3 p0,
- *        3 transposed im2col (conv input gradient); gC = channels per tap. */
+ *        3 transposed im2col (conv input gradient); gC = channels per tap.
+ * tile: 0 = automatic (256x256 8-wave kernel for dense bf16 with >= 256 output tiles and
+ *       K >= 384, else 128x128), 1 = force 128x128, 2 = force 256x256 (dense bf16 only). */
 int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, xcp_stream_t stream);
+                float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, xcp_stream_t stream);
 /* number of partial rows in gemm_nt's stats array for M rows */
 int xcp_gemm_nt_stat_rows(int M);
 
 /* weight gradient of the above: P[s][N][K] = sum_{m in split s} G[m][N] X[m][K],
  * rows split in S chunks of rows_per_split; X rows gathered as in gemm_nt
- * (gmode 0-2).  Reduce P over s with xcp_colreduce_f32. */
+ * (gmode 0-2).  Reduce P over s with xcp_colreduce_f32.  tile: 0 automatic (256x256 for
+ * dense bf16 with N, K >= 256), 1 = 128x128, 2 = 256x256; pass the same value to both calls. */
 /* rows per split to pass to xcp_gemm_tn for this problem (S = ceil(M / rows)). */
-int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K);
+int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K, int tile);
 int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, float* P, int M, int N, int K, int S,
-                int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, xcp_stream_t stream);
+                int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile,
+                xcp_stream_t stream);
 
 /* ---- depthwise 3x3 (SeparableConv2d.conv1, Xception.py:41,:45) ----
  * Y = dw3x3(act(X)); act per XCP_ACT_* (BN scale/shift for XCP_ACT_BNRELU);
@@ -64,23 +68,14 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
  * optional bnpart[P][2][C] = (sum dX, sum dX*(X-bmean)*binvstd): the backward
  * partial sums of the BatchNorm that produced X (XCP_ACT_BNRELU only). */
 int xcp_dw_bwd_chunks(int N, int H, int W, int C);
-/* launch tuning knobs: 0 = depthwise forward / 1 = depthwise backward halo pixels per
- * LDS tile (256 or 512); 2 = pointwise GEMM tile (0: 128x128 2-stage, 1: 256x128
- * 3-stage, 2: auto -- 256x256 8-wave kernel for dense bf16 with >= 256 tiles and
- * K >= 384, 3: that kernel for every dense bf16 call); 3 = 256x256 kernel schedule
- * (0: staggered wave groups, 1: lockstep; measurement only); 4 / 5 = depthwise
- * forward / backward kernel family (0: row walk, 1: LDS tile); 6 = weight-gradient
- * kernel (1: 256x256 for dense bf16, 0: 128x128); 7 = target workgroups of the
- * 256x256 weight-gradient kernel; 8 = stem conv1 kernels (1: tiled, 0: per-pixel).
- * Returns the previous value (-1: unknown knob). */
-int xcp_tune(int knob, int value);
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
                const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, float* bnpart,
                const float* bmean, const float* binvstd, int N, int H, int W, int C, xcp_stream_t stream);
 
 /* ---- BatchNorm2d (Xception.py:56,67,73,78,119,123,143,147), tails, pooling ---- */
-int xcp_colreduce_f64(const float* in, int S, long L, double* out, int G, xcp_stream_t stream);
-int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, xcp_stream_t stream);
+/* out[g][l] = sum over the g-th of G contiguous groups of slabs s of in[s][l] (fp64 sums, fp32 out);
+ * accumulate = 1 (G = 1 only): out[l] += that sum (gradient accumulation into param.grad) */
+int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, int accumulate, xcp_stream_t stream);
 int xcp_chanred_parts(long rows, int C);
 int xcp_row_stats(int dtype, const void* X, long rows, int C, float* part, xcp_stream_t stream);
 /* ms / mt (both null, or both set): scale / shift of the BN when dZ is the gradient of
@@ -92,15 +87,13 @@ int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mea
 int xcp_bn_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* beta,
                          float* rmean, float* rvar, float momentum, float eps, float* mean_o, float* invstd_o,
                          float* scale_o, float* shift_o, xcp_stream_t stream);
+/* (dgamma, dbeta may be null; accumulate = 1 adds to them: gradient accumulation into param.grad) */
 int xcp_bn_bwd_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* mean,
                              const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma,
-                             float* dbeta, xcp_stream_t stream);
+                             float* dbeta, int accumulate, xcp_stream_t stream);
 int xcp_bn_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* beta, float* rmean,
                     float* rvar, float momentum, float eps, int train, float* mean, float* invstd, float* scale,
                     float* shift, xcp_stream_t stream);
-int xcp_bn_bwd_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* mean,
-                        const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
-                        int accumulate, xcp_stream_t stream);
 int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, long rows, int C,
                xcp_stream_t stream);
 int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const float* alpha, const float* bcoef,
@@ -117,16 +110,6 @@ int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void
 int xcp_maxpool_bwd_bnred_parts(int N, int H, int W, int C);
 int xcp_maxpool_bwd_bnred(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
                           const float* mean, const float* invstd, int N, int H, int W, int C, float* part,
-                          xcp_stream_t stream);
-/* BatchNorm backward reduce / apply whose dZ is the MaxPool2d(3,2,1) backward (Xception.py:86)
- * of dOut [N][OH][OW][C] with argmax taps amax, gathered on the fly; Y / dY are [N][H][W][C].
- * reduce: dZ (may be null) receives the gathered gradient (max-pool backward + BN reduce in one
- * pass; the apply then reads it with xcp_bn_bwd_apply) */
-int xcp_bn_bwd_reduce_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, const float* mean,
-                           const float* invstd, int N, int H, int W, int C, float* part, void* dZ,
-                           xcp_stream_t stream);
-int xcp_bn_bwd_apply_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, void* dY,
-                          const float* alpha, const float* bcoef, const float* delta, int N, int H, int W, int C,
                           xcp_stream_t stream);
 /* bn4 + ReLU + adaptive_avg_pool2d (Xception.py:193-198) -> F[N][C] fp32 */
 int xcp_avgpool_fwd(int dtype, const void* Y, const float* s, const float* t, float* F, int N, int HW, int C,
@@ -180,16 +163,33 @@ int xcp_opt_adam(const long long* tab, int nchunks, const float* coef, float lr,
  * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block), nblocks in total */
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream_t stream);
 
+/* ---- classification heads / losses of the training scripts (fp32) ----
+ * ArcFace (train_visual.py:455-474, m 0.5; train_au_face.py:423-442, m 0.30): X [B][D], W [C][D],
+ * labels int64 [B] (null: plain s * cos), out [B][C] = s * cos(theta + m at the label, theta elsewhere);
+ * xcp_arcface_bwd: dX [B][D], dW [C][D] from dout [B][C] (C <= 16).
+ * Focal / class-weighted cross entropy (CBFocalLoss, train_au_face.py:445-458; gamma 0 and no
+ * weights = nn.CrossEntropyLoss, train_visual.py:527): loss[0] = mean_i (1-pt_i)^gamma ce_i,
+ * ce_i = w[y_i] (logsumexp(Z_i) - Z_i[y_i]), pt = exp(-ce); with dZ: dZ = gout[0] * dloss/dZ
+ * (gout: device scalar, null = 1). */
+int xcp_arcface_fwd(const float* X, const float* W, const long long* labels, float* out, int B, int C, int D, float s,
+                    float m, xcp_stream_t stream);
+int xcp_arcface_bwd(const float* X, const float* W, const long long* labels, const float* dout, float* dX, float* dW,
+                    int B, int C, int D, float s, float m, xcp_stream_t stream);
+int xcp_focal_ce(const float* Z, const long long* labels, const float* weights, float gamma, const float* gout,
+                 float* loss, float* dZ, int B, int C, xcp_stream_t stream);
+
 /* ---- LSTM recurrence (nn.LSTM, XceptionLSTMV.py:18-23, :67) ----
  * whh is W_hh [4H][H] as nn.LSTM stores it (weight_hh_l0); whhT ([H][4H]) is read only by the
- * generic kernel, i.e. when xcp_lstm_needs_whhT(H) returns 1 (H = 64 / 128 run register-resident,
- * H = 256 / 512 / 1024 on per-step kernels).  xcp_lstm_bwd's work: B*H + 4*H*H floats (the per-step
- * kernels' cell-gradient carry and a transposed W_hh). */
-int xcp_lstm_needs_whhT(int H);
+ * generic kernel, i.e. when xcp_lstm_needs_whhT(B, H, kernel) returns 1 (H = 64 / 128 run
+ * register-resident, H = 256 / 512 / 1024 on per-step kernels while B fits their LDS budget).
+ * kernel: 0 = automatic, 1 = the generic kernels.  xcp_lstm_bwd's work: B*H + 4*H*H floats (the
+ * per-step kernels' cell-gradient carry and a transposed W_hh). */
+int xcp_lstm_needs_whhT(int B, int H, int kernel);
 int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
-                 float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, xcp_stream_t stream);
+                 float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, int kernel,
+                 xcp_stream_t stream);
 int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const float* whh, const float* cst,
-                 const float* gates, float* dgates, float* work, int B, int T, int H, xcp_stream_t stream);
+                 const float* gates, float* dgates, float* work, int B, int T, int H, int kernel, xcp_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -4,9 +4,14 @@ Mirrors /root/reference/Xception.py: same classes (``SeparableConv2d``
 :37-47, ``Block`` :50-99, ``Xception`` :102-201, ``xception()`` :205-213), same
 submodule names and registration order, same init (:154-160, identical RNG
 consumption), hence identical ``state_dict`` keys/shapes and bit-identical
-seeded init.  ``Xception.forward`` runs the whole backbone on the hand-written
-gfx950 kernels through ``xcp.engine`` (one autograd node); there is no CPU
-path -- a non-GPU input raises.
+seeded init.  The convolutions, BatchNorms and max-pools are the ``xcp.modules``
+subclasses of the torch.nn classes, whose forward runs the ``torch.ops.xcp.*`` custom
+ops, so every sub-module (``model.block4``, ``SeparableConv2d``, ``Block``) runs on its
+own as in the reference.  ``Xception.forward`` runs the whole backbone as ONE fused
+pass of the gfx950 kernels (``xcp.engine``, one autograd node); when forward hooks or
+pre-hooks are registered on any sub-module it composes the sub-modules instead (the
+reference's Xception.py:167-201 order), so the hooks fire.  There is no CPU path: a
+non-GPU input raises.
 
 Offline: ``xception(pretrained=True)`` never fetches (the reference downloads
 from data.lip6.fr, Xception.py:33,212).  It loads a local copy named by
@@ -18,6 +23,9 @@ import os
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
+
+from xcp import modules as xm
 
 __all__ = ["xception"]
 
@@ -29,13 +37,14 @@ class SeparableConv2d(nn.Module):
 
     def __init__(self, in_channels, out_channels, kernel_size=1, stride=1, padding=0, dilation=1, bias=False):
         super(SeparableConv2d, self).__init__()
-        self.conv1 = nn.Conv2d(in_channels, in_channels, kernel_size, stride, padding, dilation, groups=in_channels,
-                               bias=bias)
-        self.pointwise = nn.Conv2d(in_channels, out_channels, 1, 1, 0, 1, 1, bias=bias)
+        self.conv1 = xm.DepthwiseConv2d(in_channels, in_channels, kernel_size, stride, padding, dilation,
+                                        groups=in_channels, bias=bias)
+        self.pointwise = xm.PointwiseConv2d(in_channels, out_channels, 1, 1, 0, 1, 1, bias=bias)
 
-    def forward(self, x):
-        raise RuntimeError("SeparableConv2d runs inside the fused xcp Xception engine; call the Xception module "
-                           "(per-module execution is not provided on MI355X)")
+    def forward(self, x):   # Xception.py:44-47
+        x = self.conv1(x)
+        x = self.pointwise(x)
+        return x
 
 
 class Block(nn.Module):
@@ -45,8 +54,8 @@ class Block(nn.Module):
     def __init__(self, in_filters, out_filters, reps, strides=1, start_with_relu=True, grow_first=True):
         super(Block, self).__init__()
         if out_filters != in_filters or strides != 1:
-            self.skip = nn.Conv2d(in_filters, out_filters, 1, stride=strides, bias=False)
-            self.skipbn = nn.BatchNorm2d(out_filters)
+            self.skip = xm.PointwiseConv2d(in_filters, out_filters, 1, stride=strides, bias=False)
+            self.skipbn = xm.BatchNorm2d(out_filters)
         else:
             self.skip = None
         self.relu = nn.ReLU(inplace=True)
@@ -55,26 +64,33 @@ class Block(nn.Module):
         if grow_first:
             rep.append(self.relu)
             rep.append(SeparableConv2d(in_filters, out_filters, 3, stride=1, padding=1, bias=False))
-            rep.append(nn.BatchNorm2d(out_filters))
+            rep.append(xm.BatchNorm2d(out_filters))
             filters = out_filters
         for _ in range(reps - 1):
             rep.append(self.relu)
             rep.append(SeparableConv2d(filters, filters, 3, stride=1, padding=1, bias=False))
-            rep.append(nn.BatchNorm2d(filters))
+            rep.append(xm.BatchNorm2d(filters))
         if not grow_first:
             rep.append(self.relu)
             rep.append(SeparableConv2d(in_filters, out_filters, 3, stride=1, padding=1, bias=False))
-            rep.append(nn.BatchNorm2d(out_filters))
+            rep.append(xm.BatchNorm2d(out_filters))
         if not start_with_relu:
             rep = rep[1:]
         else:
             rep[0] = nn.ReLU(inplace=False)
         if strides != 1:
-            rep.append(nn.MaxPool2d(3, strides, 1))
+            rep.append(xm.MaxPool2d(3, strides, 1))
         self.rep = nn.Sequential(*rep)
 
-    def forward(self, inp):
-        raise RuntimeError("Block runs inside the fused xcp Xception engine; call the Xception module")
+    def forward(self, inp):   # Xception.py:89-99
+        x = self.rep(inp)
+        if self.skip is not None:
+            skip = self.skip(inp)
+            skip = self.skipbn(skip)
+        else:
+            skip = inp
+        x += skip
+        return x
 
 
 class Xception(nn.Module):
@@ -83,11 +99,11 @@ class Xception(nn.Module):
     def __init__(self, num_classes=1000):
         super(Xception, self).__init__()
         self.num_classes = num_classes
-        self.conv1 = nn.Conv2d(3, 32, 3, 2, 0, bias=False)
-        self.bn1 = nn.BatchNorm2d(32)
+        self.conv1 = xm.StemConv2d(3, 32, 3, 2, 0, bias=False)
+        self.bn1 = xm.BatchNorm2d(32)
         self.relu = nn.ReLU(inplace=True)
-        self.conv2 = nn.Conv2d(32, 64, 3, bias=False)
-        self.bn2 = nn.BatchNorm2d(64)
+        self.conv2 = xm.StemConv2d(32, 64, 3, bias=False)
+        self.bn2 = xm.BatchNorm2d(64)
         self.block1 = Block(64, 128, 2, 2, start_with_relu=False, grow_first=True)
         self.block2 = Block(128, 256, 2, 2, start_with_relu=True, grow_first=True)
         self.block3 = Block(256, 728, 2, 2, start_with_relu=True, grow_first=True)
@@ -101,9 +117,9 @@ class Xception(nn.Module):
         self.block11 = Block(728, 728, 3, 1, start_with_relu=True, grow_first=True)
         self.block12 = Block(728, 1024, 2, 2, start_with_relu=True, grow_first=False)
         self.conv3 = SeparableConv2d(1024, 1536, 3, 1, 1)
-        self.bn3 = nn.BatchNorm2d(1536)
+        self.bn3 = xm.BatchNorm2d(1536)
         self.conv4 = SeparableConv2d(1536, 2048, 3, 1, 1)
-        self.bn4 = nn.BatchNorm2d(2048)
+        self.bn4 = xm.BatchNorm2d(2048)
         self.fc = nn.Linear(2048, num_classes)
         # ------- init weights (Xception.py:154-160) --------
         for m in self.modules():
@@ -114,6 +130,7 @@ class Xception(nn.Module):
                 m.weight.data.fill_(1)
                 m.bias.data.zero_()
         self._xcp_engines = {}
+        self._xcp_grad_sink = None   # xcp.ddp.GradBuckets(module=...) registers itself here
 
     def _engine(self):
         from xcp import compute_dtype
@@ -136,12 +153,44 @@ class Xception(nn.Module):
         feats, _ = eng.forward(x, self.training)
         return feats
 
+    def _hooked(self):
+        """True when a forward (pre-)hook is registered on a sub-module or globally: the fused
+        engine would skip those modules' forward calls, so the module path runs instead."""
+        from torch.nn.modules import module as _m
+        if _m._global_forward_hooks or _m._global_forward_pre_hooks:
+            return True
+        return any(m._forward_hooks or m._forward_pre_hooks for m in self.modules() if m is not self)
+
+    def forward_modules(self, x):
+        """Xception.forward as the reference composes it (Xception.py:167-201), each sub-module on
+        the xcp custom ops.  Returns fp32 features through ``fc``."""
+        x = self.conv1(x)
+        x = self.bn1(x)
+        x = self.relu(x)
+        x = self.conv2(x)
+        x = self.bn2(x)
+        x = self.relu(x)
+        for i in range(1, 13):
+            x = getattr(self, f"block{i}")(x)
+        x = self.conv3(x)
+        x = self.bn3(x)
+        x = self.relu(x)
+        x = self.conv4(x)
+        x = self.bn4(x)
+        x = self.relu(x)
+        x = F.adaptive_avg_pool2d(x, (1, 1))
+        x = x.reshape(x.size(0), -1).float()
+        return self.fc(x)
+
     def forward(self, x):
+        if self._hooked():
+            return self.forward_modules(x)
         return self.fc(self.features(x))
 
-    def __getstate__(self):
+    def __getstate__(self):   # copies (torch.save, deepcopy for AveragedModel) share no engine / sink
         d = self.__dict__.copy()
         d["_xcp_engines"] = {}
+        d["_xcp_grad_sink"] = None
         return d
 
 

@@ -19,23 +19,20 @@ D = ctypes.c_double
 
 # name -> argument types (return type is always int status)
 SIGNATURES = {
-    "xcp_gemm_nt": [I, P, L, P, L, P, L, I, I, I, P, I, I, I, I, I, I, I, P],
+    "xcp_gemm_nt": [I, P, L, P, L, P, L, I, I, I, P, I, I, I, I, I, I, I, I, P],
     "xcp_gemm_nt_stat_rows": [I],
-    "xcp_gemm_tn_rows_per_split": [I, I, I, I, I],
-    "xcp_gemm_tn": [I, P, L, P, L, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "xcp_gemm_tn_rows_per_split": [I, I, I, I, I, I],
+    "xcp_gemm_tn": [I, P, L, P, L, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
-    "xcp_tune": [I, I],
     "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, I, I, I, I, P],
-    "xcp_colreduce_f64": [P, I, L, P, I, P],
-    "xcp_colreduce_f32": [P, I, L, P, I, P],
+    "xcp_colreduce_f32": [P, I, L, P, I, I, P],
     "xcp_chanred_parts": [L, I],
     "xcp_row_stats": [I, P, L, I, P, P],
     "xcp_bn_bwd_reduce": [I, P, P, P, P, P, P, L, I, P, P],
     "xcp_bn_finalize_part": [P, I, I, D, P, P, P, P, F, F, P, P, P, P, P],
-    "xcp_bn_bwd_finalize_part": [P, I, I, D, P, P, P, P, P, P, P, P, P],
+    "xcp_bn_bwd_finalize_part": [P, I, I, D, P, P, P, P, P, P, P, P, I, P],
     "xcp_bn_finalize": [P, I, I, D, P, P, P, P, F, F, I, P, P, P, P, P],
-    "xcp_bn_bwd_finalize": [P, I, I, D, P, P, P, P, P, P, P, P, I, P],
     "xcp_bn_act": [I, P, P, P, P, I, L, I, P],
     "xcp_bn_bwd_apply": [I, P, P, P, P, P, P, P, P, L, I, P],
     "xcp_relu_bwd": [I, P, P, L, I, P],
@@ -43,8 +40,6 @@ SIGNATURES = {
     "xcp_maxpool_bwd": [I, P, P, P, I, I, I, I, P],
     "xcp_maxpool_bwd_bnred_parts": [I, I, I, I],
     "xcp_maxpool_bwd_bnred": [I, P, P, P, P, P, P, I, I, I, I, P, P],
-    "xcp_bn_bwd_reduce_pool": [I, P, P, P, P, P, I, I, I, I, P, P, P],
-    "xcp_bn_bwd_apply_pool": [I, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_avgpool_fwd": [I, P, P, P, P, I, I, I, P],
     "xcp_avgpool_bwd": [I, P, P, P, P, P, I, I, I, P],
     "xcp_conv1_fwd": [I, P, P, P, I, I, I, P],
@@ -60,14 +55,17 @@ SIGNATURES = {
     "xcp_conv3x3": [I, P, P, P, P, I, I, I, P],
     "xcp_conv3x3_wgrad_parts": [I, I, I],
     "xcp_conv3x3_wgrad": [P, P, P, I, I, I, P],
-    "xcp_lstm_needs_whhT": [I],
-    "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, P],
-    "xcp_lstm_bwd": [P, P, P, P, P, P, P, P, I, I, I, P],
+    "xcp_arcface_fwd": [P, P, P, P, I, I, I, F, F, P],
+    "xcp_arcface_bwd": [P, P, P, P, P, P, I, I, I, F, F, P],
+    "xcp_focal_ce": [P, P, P, F, P, P, P, I, I, P],
+    "xcp_lstm_needs_whhT": [I, I, I],
+    "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "xcp_lstm_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],
 }
 
 # entry points that return a size, not a status
-SIZE_QUERIES = {"xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts", "xcp_conv1_wgrad_parts", "xcp_tune",
-                "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
+SIZE_QUERIES = {"xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
+                "xcp_conv1_wgrad_parts", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
                 "xcp_maxpool_bwd_bnred_parts"}
 
 _lib = None

@@ -7,17 +7,16 @@
 // F.adaptive_avg_pool2d (:197), ReLU (:60,:83,:170,:174,:191,:195).
 //
 // Statistics are reduced deterministically: producers write fp32 per-tile
-// partial rows [R][2][C]; `xcp_colreduce` folds them into G fp64 rows; the
-// finalize kernels read those.  Normalisation uses the biased batch variance,
+// partial rows [R][2][C]; the finalize kernels fold them in fp64.  Normalisation uses the biased batch variance,
 // running_var is updated with the unbiased one (momentum 0.1), as PyTorch does.
 #include "common.h"
 
 namespace {
 
 // ---------------------------------------------------------------- column reduce
-// out[g][l] = sum_{s in group g} in[s][l]   (in: fp32 [S][L]; out: OutT [G][L])
-template <typename OutT>
-__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ in, int S, long L, OutT* __restrict__ out,
+// out[g][l] = sum_{s in group g} in[s][l]   (in: fp32 [S][L]; out: fp32 [G][L]; ACC: out +=)
+template <bool ACC>
+__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ in, int S, long L, float* __restrict__ out,
                                                         int G) {
   __shared__ double red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -30,7 +29,10 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict_
     for (int s = s0 + w; s < s1; s += 4) acc += (double)in[(long)s * L + col];
   red[w][lane] = acc;
   __syncthreads();
-  if (w == 0 && col < L) out[(long)g * L + col] = (OutT)(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+  if (w == 0 && col < L) {
+    const float v = (float)(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+    out[(long)g * L + col] = ACC ? out[(long)g * L + col] + v : v;
+  }
 }
 
 // ---------------------------------------------------------------- per-channel reductions
@@ -81,63 +83,21 @@ XCP_DEV void chanred_finish(const ChanRed& r, float (*acc)[CPT], float* part, in
   }
 }
 
-// Gradient of MaxPool2d(3, 2, 1) (Xception.py:86) w.r.t. its input at pixel p, channels
-// c0..c0+CPT-1, gathered from the pooled gradient dOut and the forward's argmax taps (amax,
-// one byte per element, read 8 at a time): input (h, w) lies in at most 2 x 2 windows.
-// Rounded to the storage type, i.e. exactly the value a materialised maxpool backward stores.
+// Source of the MaxPool2d(3, 2, 1) (Xception.py:86) gradient: the pooled gradient dOut and the
+// forward's argmax taps (amax, one byte per element, read 8 at a time).
 struct PoolSrc {
   const void* dOut;
   const unsigned char* amax;
   int H, W, OH, OW;
 };
 
-template <typename T, int CPT>
-XCP_DEV void pool_grad(const PoolSrc& ps, long p, int c0, int C, float* acc) {
-  static_assert(CPT == 8, "amax is read 8 bytes at a time");
-  const T* dOut = reinterpret_cast<const T*>(ps.dOut);
-  // 32-bit index math (pixel counts stay far below 2^31; 64-bit division is emulated)
-  const unsigned pi = (unsigned)p, W = (unsigned)ps.W, H = (unsigned)ps.H;
-  const unsigned t = pi / W, w = pi - t * W;
-  const unsigned n = t / H, h = t - n * H;
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) acc[j] = 0.f;
-  // window oh covers rows 2oh-1 .. 2oh+1  =>  h/2 <= oh <= (h+1)/2 (one window for even h)
-  const int oh0 = (int)h >> 1, ow0 = (int)w >> 1;
-  const int noh = ((h & 1) && oh0 + 1 < ps.OH) ? 2 : 1, now = ((w & 1) && ow0 + 1 < ps.OW) ? 2 : 1;
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    if (a >= noh) break;
-    const int oh = oh0 + a, ky = (int)h - (oh * 2 - 1);
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      if (b >= now) break;
-      const int ow = ow0 + b, kx = (int)w - (ow * 2 - 1);
-      const long op = ((long)n * ps.OH + oh) * ps.OW + ow;
-      float d[CPT];
-      VecIO<T, CPT>::load(dOut + op * C + c0, d);
-      const uint2 am = *reinterpret_cast<const uint2*>(ps.amax + op * C + c0);
-      const unsigned want = (unsigned)(ky * 3 + kx);
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) {
-        const unsigned a = ((j < 4 ? am.x : am.y) >> (8 * (j & 3))) & 0xffu;
-        if (a == want) acc[j] += d[j];
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) acc[j] = rnd<T>(acc[j]);
-}
-
 // MODE 0: (x, x^2) of rows of X.  MODE 1: (dz, dz*yhat), yhat = (y-mean)*invstd.
 // MODE 2: MODE 1 with dz masked by the ReLU that followed the BN (y*ms+mt > 0), i.e. the
 // gradient w.r.t. relu(bn(y)) given; the mask is recomputed from y, never read.
-// MODE 3: MODE 1 with dz gathered from a max-pool backward (pool_grad), never materialised.
-// MODE 4: MODE 3 that also stores the gathered dz to A (the max-pool backward and the BN
-// reduce in one pass).
 template <typename T, int MODE, int CPT>
 __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av, const void* Bv, const float* mean,
                                                       const float* invstd, const float* ms, const float* mt,
-                                                      PoolSrc ps, float* part) {
+                                                      float* part) {
   const int cchunk = blockIdx.x % r.nch, pchunk = blockIdx.x / r.nch;
   const int lcv = threadIdx.x % r.CVB, slot = threadIdx.x / r.CVB;
   const int cv = cchunk * r.CVB + lcv;
@@ -160,12 +120,7 @@ __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av,
     const long rb = (long)pchunk * r.rows_per_chunk, re = min(r.rows, rb + r.rows_per_chunk);
     for (long p = rb + slot; p < re; p += r.SPB) {
       float a[CPT];
-      if constexpr (MODE >= 3) {
-        pool_grad<T, CPT>(ps, p, c0, r.C, a);
-        if constexpr (MODE == 4) VecIO<T, CPT>::store(const_cast<T*>(A) + p * r.C + c0, a);
-      } else {
-        VecIO<T, CPT>::load(A + p * r.C + c0, a);
-      }
+      VecIO<T, CPT>::load(A + p * r.C + c0, a);
       if constexpr (MODE == 0) {
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
@@ -223,33 +178,9 @@ __global__ void bn_finalize_kernel(const double* __restrict__ part2, int G, int 
   shift_o[c] = beta[c] - (float)mean * sc;
 }
 
-// dbeta = sum dz, dgamma = sum dz*yhat;  dy = alpha*dz + bcoef*y + delta
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part2, int G, int C, double count, const float* gamma,
-                                       const float* mean, const float* invstd, float* alpha, float* bcoef, float* delta,
-                                       float* dgamma, float* dbeta, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sdz = 0.0, sdzy = 0.0;
-  for (int g = 0; g < G; ++g) {
-    sdz += part2[((long)g * 2 + 0) * C + c];
-    sdzy += part2[((long)g * 2 + 1) * C + c];
-  }
-  const double is = invstd[c], gm = gamma[c], mu = mean[c];
-  const double a = gm * is;
-  const double mdz = sdz / count, mdzy = sdzy / count;
-  alpha[c] = (float)a;
-  bcoef[c] = (float)(-a * is * mdzy);
-  delta[c] = (float)(-a * mdz + a * is * mu * mdzy);
-  if (dgamma) {
-    dgamma[c] = (float)sdzy + (accumulate ? dgamma[c] : 0.f);
-    dbeta[c] = (float)sdz + (accumulate ? dbeta[c] : 0.f);
-  }
-}
-
 // Fused reduction + finalize straight from the fp32 partial rows part[R][2][C] (the GEMM
-// epilogue's / the fused depthwise backward's per-chunk sums), replacing colreduce_f64 +
-// *_finalize: one 1024-thread workgroup per 32 channels; lane l of wave w sums statistic
-// l>>5 of channel l&31 over rows w, w+16, ... in fp64 (four independent accumulators, so
+// epilogue's / the fused depthwise backward's per-chunk sums): one 1024-thread workgroup
+// per 32 channels; lane l of wave w sums statistic l>>5 of channel l&31 over rows w, w+16, ... in fp64 (four independent accumulators, so
 // many loads stay in flight), the 16 waves fold in LDS, and 32 threads finalize.
 constexpr int FIN_CH = 32, FIN_WAVES = 16;
 
@@ -310,7 +241,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_part_kernel(const float*
                                                                     double count, const float* gamma,
                                                                     const float* mean, const float* invstd,
                                                                     float* alpha, float* bcoef, float* delta,
-                                                                    float* dgamma, float* dbeta) {
+                                                                    float* dgamma, float* dbeta, int accumulate) {
   __shared__ double red[FIN_WAVES][64];
   const int c0 = blockIdx.x * FIN_CH;
   double sdz, sdzy;
@@ -324,8 +255,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_part_kernel(const float*
   bcoef[c] = (float)(-a * is * mdzy);
   delta[c] = (float)(-a * mdz + a * is * mu * mdzy);
   if (dgamma) {
-    dgamma[c] = (float)sdzy;
-    dbeta[c] = (float)sdz;
+    dgamma[c] = accumulate ? dgamma[c] + (float)sdzy : (float)sdzy;
+    dbeta[c] = accumulate ? dbeta[c] + (float)sdz : (float)sdz;
   }
 }
 
@@ -350,20 +281,18 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ X, T*
   VecIO<T, CPT>::store(Y + p * C + c0, v);
 }
 
-// dy = alpha*dz + bcoef*y + delta   (POOL: dz gathered from a max-pool backward)
-template <typename T, int CPT, bool MASK, bool POOL = false>
+// dy = alpha*dz + bcoef*y + delta   (dbeta = sum dz, dgamma = sum dz*yhat come from the finalize)
+template <typename T, int CPT, bool MASK>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dZ, const T* __restrict__ Yv, T* dY,
                                                            const float* alpha, const float* bcoef, const float* delta,
-                                                           const float* ms, const float* mt, long rows, int C,
-                                                           PoolSrc ps) {
+                                                           const float* ms, const float* mt, long rows, int C) {
   const int CV = C / CPT;
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
   if (g >= rows * CV) return;
   const int c0 = (int)(g % CV) * CPT;
   const long p = g / CV;
   float dz[CPT], y[CPT], al[CPT], bc[CPT], de[CPT];
-  if constexpr (POOL) pool_grad<T, CPT>(ps, p, c0, C, dz);
-  else VecIO<T, CPT>::load(dZ + p * C + c0, dz);
+  VecIO<T, CPT>::load(dZ + p * C + c0, dz);
   VecIO<T, CPT>::load(Yv + p * C + c0, y);
   VecIO<float, CPT>::load(alpha + c0, al);
   VecIO<float, CPT>::load(bcoef + c0, bc);
@@ -455,24 +384,9 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const T* __restrict__ Y, 
   VecIO<T, CPT>::store(Out + op * C + c0, o);
 }
 
-// maxpool backward by gather: dz[n,h,w] = sum over windows (oh,ow) containing (h,w)
-// whose argmax is (h,w) of dout[n,oh,ow]
-template <typename T, int CPT>
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolSrc ps, T* __restrict__ dZ, int N, int C) {
-  const int CV = C / CPT;
-  const long g = (long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (long)N * ps.H * ps.W * CV) return;
-  const int c0 = (int)(g % CV) * CPT;
-  const long p = g / CV;
-  float acc[CPT];
-  pool_grad<T, CPT>(ps, p, c0, C, acc);
-  VecIO<T, CPT>::store(dZ + p * C + c0, acc);
-}
-
-// The same gradient computed per 2 x 2 quad of input pixels (2a..2a+1, 2b..2b+1): the quad
+// Max-pool backward by gather, per 2 x 2 quad of input pixels (2a..2a+1, 2b..2b+1): the quad
 // lies in windows (a..a+1, b..b+1), so each thread loads 4 windows' dOut / argmax once and
-// writes 4 pixels (the per-pixel form loads 2.25 windows per pixel).  Sums in the order of
-// pool_grad, so the result is bitwise the same.
+// writes 4 pixels (a per-pixel gather loads 2.25 windows per pixel).
 // quad q = (n, a, b): fill g[py*2+px][j] with the gradient of input pixel (2a+py, 2b+px)
 // (rounded to T; pixels past H / W are left out by the callers)
 template <typename T, int CPT>
@@ -493,7 +407,7 @@ XCP_DEV void pool_quad(const PoolSrc& ps, unsigned n, unsigned a, unsigned b, in
     am[k][1] = ok ? m.y : 0xffffffffu;
   }
   auto tap = [&](int k, int j) { return (am[k][j >> 2] >> (8 * (j & 3))) & 0xffu; };
-  // pixel (py, px) of the quad: its windows in pool_grad order and the tap it has in each
+  // pixel (py, px) of the quad: its windows in (oh, ow) order and the tap it has in each
   //   (0,0): w00 t4          (0,1): w00 t5, w01 t3
   //   (1,0): w00 t7, w10 t1  (1,1): w00 t8, w01 t6, w10 t2, w11 t0
 #pragma unroll
@@ -511,10 +425,7 @@ XCP_DEV void pool_quad(const PoolSrc& ps, unsigned n, unsigned a, unsigned b, in
       }
 }
 
-// The max-pool gradient computed per 2 x 2 quad of input pixels (2a..2a+1, 2b..2b+1): the
-// quad lies in windows (a..a+1, b..b+1), so each thread loads 4 windows' dOut / argmax once
-// and writes 4 pixels (the per-pixel form loads 2.25 windows per pixel).  Sums in the order
-// of pool_grad, so the result is bitwise the same.
+// dZ = max-pool backward of dOut (one thread per input quad and 8 channels)
 template <typename T, int CPT>
 __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(PoolSrc ps, T* __restrict__ dZ, int N, int C) {
   const unsigned CV = (unsigned)C / CPT;
@@ -621,17 +532,15 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restric
 
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
-int g_pool_quad = 1;   // xcp_tune knob 12: max-pool backward per input quad (1) or per pixel (0)
-
 template <typename T, int MODE>
 int chanred_launch(long rows, int C, const void* A, const void* B, const float* mean, const float* invstd, float* part,
-                   hipStream_t st, const float* ms = nullptr, const float* mt = nullptr, PoolSrc ps = PoolSrc{}) {
+                   hipStream_t st, const float* ms = nullptr, const float* mt = nullptr) {
   constexpr int CPT = 8;
   ChanRed r = make_chanred(rows, C, CPT, 1024);
   const long P = chanred_P(r);
   const size_t smem = (size_t)r.SPB * 2 * r.CVB * CPT * sizeof(float);
   hipLaunchKernelGGL((chanred_kernel<T, MODE, CPT>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, A, B, mean,
-                     invstd, ms, mt, ps, part);
+                     invstd, ms, mt, part);
   return (int)hipGetLastError();
 }
 
@@ -641,27 +550,16 @@ inline PoolSrc pool_src(const void* dOut, const unsigned char* amax, int H, int 
 
 }  // namespace
 
-int xcp_internal_pool_quad(int v) {
-  const int old = g_pool_quad;
-  if (v == 0 || v == 1) g_pool_quad = v;
-  return old;
-}
-
 extern "C" {
 
-int xcp_colreduce_f64(const float* in, int S, long L, double* out, int G, hipStream_t st) {
+int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, int accumulate, hipStream_t st) {
   if (L <= 0) return XCP_OK;
   if (G > S) G = S;
   if (G < 1) G = 1;
-  hipLaunchKernelGGL(colreduce_kernel<double>, dim3((unsigned)((L + 63) / 64), G), dim3(256), 0, st, in, S, L, out, G);
-  return (int)hipGetLastError();
-}
-
-int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, hipStream_t st) {
-  if (L <= 0) return XCP_OK;
-  if (G > S) G = S;
-  if (G < 1) G = 1;
-  hipLaunchKernelGGL(colreduce_kernel<float>, dim3((unsigned)((L + 63) / 64), G), dim3(256), 0, st, in, S, L, out, G);
+  if (accumulate && G != 1) return XCP_EINVAL;
+  const dim3 grid((unsigned)((L + 63) / 64), G);
+  if (accumulate) hipLaunchKernelGGL(colreduce_kernel<true>, grid, dim3(256), 0, st, in, S, L, out, G);
+  else hipLaunchKernelGGL(colreduce_kernel<false>, grid, dim3(256), 0, st, in, S, L, out, G);
   return (int)hipGetLastError();
 }
 
@@ -695,25 +593,6 @@ int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mea
   return XCP_EUNSUPPORTED;
 }
 
-// xcp_bn_bwd_reduce with dZ = the MaxPool2d(3,2,1) backward of dOut [N][OH][OW][C] (argmax
-// taps amax), gathered on the fly instead of materialised; Y is [N][H][W][C]
-// (dZ, may be null: also store the gathered gradient there -- max-pool backward and BN reduce
-// in one pass)
-int xcp_bn_bwd_reduce_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, const float* mean,
-                           const float* invstd, int N, int H, int W, int C, float* part, void* dZ, hipStream_t st) {
-  if (C % 8) return XCP_EINVAL;
-  const long rows = (long)N * H * W;
-  const PoolSrc ps = pool_src(dOut, amax, H, W);
-  if (dZ) {
-    if (dtype == XCP_BF16) return chanred_launch<bf16, 4>(rows, C, dZ, Y, mean, invstd, part, st, nullptr, nullptr, ps);
-    if (dtype == XCP_F32) return chanred_launch<float, 4>(rows, C, dZ, Y, mean, invstd, part, st, nullptr, nullptr, ps);
-    return XCP_EUNSUPPORTED;
-  }
-  if (dtype == XCP_BF16) return chanred_launch<bf16, 3>(rows, C, nullptr, Y, mean, invstd, part, st, nullptr, nullptr, ps);
-  if (dtype == XCP_F32) return chanred_launch<float, 3>(rows, C, nullptr, Y, mean, invstd, part, st, nullptr, nullptr, ps);
-  return XCP_EUNSUPPORTED;
-}
-
 // BatchNorm finalize straight from fp32 partial rows part[R][2][C] (train mode)
 int xcp_bn_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* beta,
                          float* rmean, float* rvar, float momentum, float eps, float* mean_o, float* invstd_o,
@@ -727,11 +606,11 @@ int xcp_bn_finalize_part(const float* part, int R, int C, double count, const fl
 
 int xcp_bn_bwd_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* mean,
                              const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
-                             hipStream_t st) {
+                             int accumulate, hipStream_t st) {
   if (C <= 0) return XCP_OK;
   if (R <= 0) return XCP_EINVAL;
   hipLaunchKernelGGL(bn_bwd_finalize_part_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part,
-                     R, C, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta);
+                     R, C, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
   return (int)hipGetLastError();
 }
 
@@ -740,14 +619,6 @@ int xcp_bn_finalize(const double* part2, int G, int C, double count, const float
                     float* shift, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part2, G, C, count, gamma, beta, rmean,
                      rvar, momentum, eps, train, mean, invstd, scale, shift);
-  return (int)hipGetLastError();
-}
-
-int xcp_bn_bwd_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* mean,
-                        const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
-                        int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part2, G, C, count, gamma, mean,
-                     invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
   return (int)hipGetLastError();
 }
 
@@ -773,7 +644,7 @@ int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const f
   const unsigned g = nblk(rows * (C / 8));
 #define XCP_APPLY(TT, MK)                                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, 8, MK>), dim3(g), dim3(256), 0, st, (const TT*)dZ, (const TT*)Y,  \
-                     (TT*)dY, alpha, bcoef, delta, ms, mt, rows, C, PoolSrc{})
+                     (TT*)dY, alpha, bcoef, delta, ms, mt, rows, C)
   if (dtype == XCP_BF16) {
     if (ms) XCP_APPLY(bf16, true);
     else XCP_APPLY(bf16, false);
@@ -782,25 +653,6 @@ int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const f
     else XCP_APPLY(float, false);
   } else
 #undef XCP_APPLY
-    return XCP_EUNSUPPORTED;
-  return (int)hipGetLastError();
-}
-
-// xcp_bn_bwd_apply with dZ = the MaxPool2d(3,2,1) backward of dOut (see xcp_bn_bwd_reduce_pool)
-int xcp_bn_bwd_apply_pool(int dtype, const void* dOut, const unsigned char* amax, const void* Y, void* dY,
-                          const float* alpha, const float* bcoef, const float* delta, int N, int H, int W, int C,
-                          hipStream_t st) {
-  if (C % 8) return XCP_EINVAL;
-  const long rows = (long)N * H * W;
-  const unsigned g = nblk(rows * (C / 8));
-  const PoolSrc ps = pool_src(dOut, amax, H, W);
-  if (dtype == XCP_BF16)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, 8, false, true>), dim3(g), dim3(256), 0, st, nullptr, (const bf16*)Y,
-                       (bf16*)dY, alpha, bcoef, delta, nullptr, nullptr, rows, C, ps);
-  else if (dtype == XCP_F32)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, 8, false, true>), dim3(g), dim3(256), 0, st, nullptr,
-                       (const float*)Y, (float*)dY, alpha, bcoef, delta, nullptr, nullptr, rows, C, ps);
-  else
     return XCP_EUNSUPPORTED;
   return (int)hipGetLastError();
 }
@@ -837,16 +689,11 @@ int xcp_maxpool_bwd(int dtype, const void* dOut, const unsigned char* amax, void
                     hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
   const PoolSrc ps = pool_src(dOut, amax, H, W);
-  if (dtype == XCP_BF16 && g_pool_quad) {
-    const unsigned gq = nblk((long)N * ps.OH * ps.OW * (C / 8));
-    hipLaunchKernelGGL((maxpool_bwd_quad_kernel<bf16, 8>), dim3(gq), dim3(256), 0, st, ps, (bf16*)dZ, N, C);
-    return (int)hipGetLastError();
-  }
-  const unsigned g = nblk((long)N * H * W * (C / 8));
+  const unsigned g = nblk((long)N * ps.OH * ps.OW * (C / 8));
   if (dtype == XCP_BF16)
-    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, ps, (bf16*)dZ, N, C);
+    hipLaunchKernelGGL((maxpool_bwd_quad_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, ps, (bf16*)dZ, N, C);
   else if (dtype == XCP_F32)
-    hipLaunchKernelGGL((maxpool_bwd_kernel<float, 8>), dim3(g), dim3(256), 0, st, ps, (float*)dZ, N, C);
+    hipLaunchKernelGGL((maxpool_bwd_quad_kernel<float, 8>), dim3(g), dim3(256), 0, st, ps, (float*)dZ, N, C);
   else
     return XCP_EUNSUPPORTED;
   return (int)hipGetLastError();

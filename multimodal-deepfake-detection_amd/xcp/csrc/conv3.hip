@@ -42,7 +42,7 @@ XCP_DEV int cswz(int x) {
 }
 
 
-template <int CIN, int COUT, int PAD, int TH, int MAXIW, bool STATS, int NW, bool PIPE, int VAR = 0>
+template <int CIN, int COUT, int PAD, int TH, int MAXIW, bool STATS, int NW, bool PIPE>
 __global__ __launch_bounds__(NW * 64, 1) void conv3x3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wp,
                                                          bf16* __restrict__ Y, float* __restrict__ stats, int N,
                                                          int IH, int IW) {
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv3x3_kernel(const bf16* __restr
       rc.y = __shfl_xor(snd.y, 16, 64);
       const uint4 d = odd ? make_uint4(rc.x, rc.y, pc[1].x, pc[1].y) : make_uint4(pc[0].x, pc[0].y, rc.x, rc.y);
       bf16* ypix = Y + (((long)n * OH + oh) * OW + ow) * COUT + co0 + (odd ? 16 + 4 * (fg - 1) : 4 * fg);
-      if (ok && (VAR != 1 || N < 0)) *reinterpret_cast<uint4*>(ypix) = d;
+      if (ok) *reinterpret_cast<uint4*>(ypix) = d;
     }
     __syncthreads();   // every wave is done reading buffer k&1 before it is restaged
   }
@@ -270,7 +270,6 @@ constexpr int WG_GI = WG_GSLOT / 1024, WG_AI = WG_ASLOT / 1024;   // 1-KB DMA in
 static_assert((WG_GI + WG_AI) % 8 == 0, "uniform DMA count per wave");
 constexpr int WG_PER_WAVE = (WG_GI + WG_AI) / 8;            // 4
 
-template <int VAR = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
                                                                float* __restrict__ P, int N, int IH, int IW, int nb,
                                                                int RB) {
@@ -356,13 +355,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __res
           const bf16x4 hi = ds_read_tr(arow[kh] + phi * 64 + ((ach ^ (((phi >> 2) & 1) << 1)) << 4) + sub);
           B[kh * 3 + kw] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
-      if constexpr (VAR != 1) {
 #pragma unroll
-        for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[t], acc[t], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int t = 0; t < 9; ++t) asm volatile("" ::"v"(A), "v"(B[t]));
-      }
+      for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[t], acc[t], 0, 0, 0);
     }
   }
   // acc[t][r] = dW[co = 16cb + 4fg + r][tap t][ci = 16bb + fr]
@@ -382,8 +376,6 @@ constexpr int TH_FWD = 4, TH_DGRAD = 2, MAXIW_FWD = 149, MAXIW_DGRAD = 147;
 // waves per workgroup (two per SIMD); the 64-deep dgrad keeps 144 VGPRs of kernel fragments
 // and has no room for the rotating read pipeline
 constexpr int NW_FWD = 8, NW_DGRAD = 8;
-
-int g_conv3_var = 0;   // xcp_tune knob 11 (measurement): 1 = no output stores (forward / dgrad), no MFMAs (wgrad)
 
 
 int conv3_cus() {
@@ -408,11 +400,6 @@ void wgrad_bands(int N, int OH, int& nb, int& rb) {
 
 }  // namespace
 
-int xcp_internal_conv3_var(int v) {
-  const int old = g_conv3_var;
-  if (v >= 0 && v <= 1) g_conv3_var = v;
-  return old;
-}
 
 extern "C" {
 
@@ -435,13 +422,7 @@ int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, i
   if (IH < 3 || IW < 3 || (mode != 0 && mode != 1) || (mode == 1 && stats)) return XCP_EINVAL;
   if (IW > (mode == 0 ? MAXIW_FWD : MAXIW_DGRAD)) return XCP_EUNSUPPORTED;
   const dim3 grid((unsigned)xcp_conv3x3_parts(mode, N, IH, IW));
-  if (mode == 0 && g_conv3_var == 1) {
-    hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD, MAXIW_FWD, true, NW_FWD, true, 1>), grid, dim3(64 * NW_FWD), 0, st, (const bf16*)X,
-                       (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
-  } else if (mode == 1 && g_conv3_var == 1) {
-    hipLaunchKernelGGL((conv3x3_kernel<64, 32, 2, TH_DGRAD, MAXIW_DGRAD, false, NW_DGRAD, false, 1>), grid, dim3(64 * NW_DGRAD), 0, st,
-                       (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
-  } else if (mode == 0) {
+  if (mode == 0) {
     if (stats)
       hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD, MAXIW_FWD, true, NW_FWD, true>), grid, dim3(64 * NW_FWD), 0, st, (const bf16*)X,
                          (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
@@ -471,12 +452,8 @@ int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, in
   if (IW - 2 > WG_GPX) return XCP_EUNSUPPORTED;
   int nb, rb;
   wgrad_bands(N, IH - 2, nb, rb);
-  if (g_conv3_var == 1)
-    hipLaunchKernelGGL((conv3x3_wgrad_kernel<1>), dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N,
-                       IH, IW, nb, rb);
-  else
-    hipLaunchKernelGGL((conv3x3_wgrad_kernel<0>), dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N,
-                       IH, IW, nb, rb);
+  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N, IH, IW,
+                     nb, rb);
   return (int)hipGetLastError();
 }
 

@@ -16,9 +16,8 @@
 // in the storage type with 16-byte loads, all issued before the first is consumed,
 // the activation applied once at staging.  Each lane then owns one dword of
 // channels (2 bf16 / 1 fp32) and computes SEGL outputs of a row segment from a
-// fully unrolled 3 x (SEGL+2) register window.  MAXPX (halo pixels per staged
-// tensor) trades halo re-reads against workgroups per CU; it is a launch knob
-// (xcp_tune) so both can be measured.
+// fully unrolled 3 x (SEGL+2) register window.  FWD_MAXPX (halo pixels per staged
+// tile) trades halo re-reads against workgroups per CU (512: 5 workgroups per CU).
 #include "common.h"
 
 namespace {
@@ -27,8 +26,7 @@ constexpr int SLICE = 64;     // bytes of channels per pixel per workgroup
 constexpr int NW = 16;        // row workers per workgroup (256 threads = 16 workers x 16 dword lanes)
 constexpr int SEGL = 5;       // output pixels per row segment
 
-int g_fwd_maxpx = 512;        // tuning knobs (xcp_tune 0 / 1)
-int g_bwd_maxpx = 512;
+constexpr int FWD_MAXPX = 512;   // halo pixels per staged forward tile (29.5 KB of LDS at 19x19)
 
 // Tile of TH x TW outputs; the LDS tile is (TH+2) x (nseg*SEGL+2) so every
 // segment is exactly SEGL wide (columns past TW / W are computed, never stored).
@@ -215,7 +213,7 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
-// Fused backward.  Per pixel p of the tile:
+// Fused backward.  Per pixel p:
 //   dA[p]   = sum_tap dY[p - off(tap)] * w[tap]          (transposed 3x3)
 //   dX[p]   = act'(p) * dA[p] + dRes[p] + (p at stride-multiple (h,w) ? dSkip[p/s] : 0)
 //   dW[tap] += dY[p] * a[p + off(tap)]                   (workgroup partial -> slab)
@@ -238,186 +236,15 @@ struct DwBwdArgs {
   const float* bmean;
   const float* binvstd;
   int N, H, W, C, ngroups;
-  TileGeo g;
 };
 
-template <typename T, int ACT, int MAXPX>
-__global__ __launch_bounds__(256) void dw_bwd_kernel(DwBwdArgs a) {
-  constexpr int EPT = DT<T>::EPT;
-  constexpr int CPG = SLICE / (int)sizeof(T);
-  __shared__ __attribute__((aligned(16))) char sm[2 * MAXPX * SLICE];
-  char* sA = sm;
-  char* sG = sm + MAXPX * SLICE;
-  const TileGeo& g = a.g;
-  int grp, n, th0, tw0;
-  const int sp = block_coords(a.ngroups, g, grp, n, th0, tw0);
-  const int c0 = grp * CPG;
-  const long nbase = (long)n * a.H * a.W;
-  const T* X = reinterpret_cast<const T*>(a.X);
-  const int cl = threadIdx.x & 15, wk = threadIdx.x >> 4;
-  const int c = c0 + cl * EPT;
-  const bool cok = c < a.C;
-  const int cc = cok ? c : a.C - EPT;
-  const bool bnsum = a.bnpart != nullptr;
-  float wt[9][EPT], dw[9][EPT], bs1[EPT], bs2[EPT], mu[EPT], is[EPT];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-      wt[t][e] = a.Wt[(long)t * a.C + cc + e];
-      dw[t][e] = 0.f;
-    }
-#pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    bs1[e] = bs2[e] = 0.f;
-    mu[e] = bnsum ? a.bmean[cc + e] : 0.f;
-    is[e] = bnsum ? a.binvstd[cc + e] : 0.f;
-  }
-  stage<T, ACT, true, MAXPX>(X, sA, g, nbase, th0, tw0, a.H, a.W, a.C, c0, a.scale, a.shift);
-  stage<T, ACT_NONE, false, MAXPX>(reinterpret_cast<const T*>(a.dY), sG, g, nbase, th0, tw0, a.H, a.W, a.C, c0,
-                                   nullptr, nullptr);
-  __syncthreads();
-  const T* dRes = reinterpret_cast<const T*>(a.dRes);
-  const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
-  T* dX = reinterpret_cast<T*>(a.dX);
-  const bool has_res = dRes != nullptr, has_skip = dSkip != nullptr;
-  const int items = g.TH * g.nseg;
-  const char* la = sA + cl * 4;
-  const char* lg = sG + cl * 4;
-  if (cok) {
-    for (int it = wk; it < items; it += NW) {
-      const int r = it / g.nseg, sg = it - r * g.nseg;
-      const int oh = th0 + r;
-      const int x0 = sg * SEGL;
-      if (oh >= a.H) continue;
-      // per-pixel global terms of this segment, issued before the LDS work
-      unsigned pres[SEGL], pskp[SEGL], pxr[SEGL];
-#pragma unroll
-      for (int j = 0; j < SEGL; ++j) {
-        const int ow = min(tw0 + x0 + j, a.W - 1);
-        const long pix = nbase + (long)oh * a.W + ow;
-        pres[j] = has_res ? *reinterpret_cast<const unsigned*>(dRes + pix * a.C + c) : 0u;
-        pxr[j] = bnsum ? *reinterpret_cast<const unsigned*>(X + pix * a.C + c) : 0u;
-        if (has_skip) {
-          const int sh2 = min(oh / a.sS, a.sOH - 1), sw2 = min(ow / a.sS, a.sOW - 1);
-          pskp[j] = *reinterpret_cast<const unsigned*>(dSkip + (((long)n * a.sOH + sh2) * a.sOW + sw2) * a.C + c);
-        } else {
-          pskp[j] = 0u;
-        }
-      }
-      const char* ba = la + (r * g.WP + x0) * SLICE;
-      const char* bg = lg + (r * g.WP + x0) * SLICE;
-      float xa[3][SEGL + 2][EPT], gy[3][SEGL + 2][EPT];
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int k = 0; k < SEGL + 2; ++k) {
-          const int off = (ky * g.WP + k) * SLICE;
-          unpack(*reinterpret_cast<const unsigned*>(ba + off), xa[ky][k], (T*)nullptr);
-          unpack(*reinterpret_cast<const unsigned*>(bg + off), gy[ky][k], (T*)nullptr);
-        }
-      const bool skip_row = has_skip && (oh % a.sS) == 0 && oh / a.sS < a.sOH;
-      T* xrow = dX + (nbase + (long)oh * a.W + tw0) * a.C + c;
-#pragma unroll
-      for (int j = 0; j < SEGL; ++j) {
-        const int x = x0 + j, ow = tw0 + x;
-        const bool valid = x < g.TW && ow < a.W;
-        float o[EPT];
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) {
-          // window column k <-> tile column x0 + k - 1; the centre of output j is k = j + 1
-          float s = 0.f;
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) s = fmaf(gy[2 - ky][j + 2 - kx][e], wt[ky * 3 + kx][e], s);
-          const float gc = valid ? gy[1][j + 1][e] : 0.f;
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) dw[ky * 3 + kx][e] = fmaf(gc, xa[ky][j + kx][e], dw[ky * 3 + kx][e]);
-          if constexpr (ACT != ACT_NONE) s = xa[1][j + 1][e] > 0.f ? s : 0.f;
-          o[e] = s;
-        }
-        if (bnsum && valid) {
-          float xr[EPT], orr[EPT];
-          unpack(pxr[j], xr, (T*)nullptr);
-          unpack(pack(o, (T*)nullptr), orr, (T*)nullptr);   // the stored (rounded) dz
-#pragma unroll
-          for (int e = 0; e < EPT; ++e) {
-            bs1[e] += orr[e];
-            bs2[e] = fmaf(orr[e], (xr[e] - mu[e]) * is[e], bs2[e]);
-          }
-        }
-        if (has_res) {
-          float rr[EPT];
-          unpack(pres[j], rr, (T*)nullptr);
-#pragma unroll
-          for (int e = 0; e < EPT; ++e) o[e] += rr[e];
-        }
-        if (skip_row && (ow % a.sS) == 0 && ow / a.sS < a.sOW) {
-          float rr[EPT];
-          unpack(pskp[j], rr, (T*)nullptr);
-#pragma unroll
-          for (int e = 0; e < EPT; ++e) o[e] += rr[e];
-        }
-        if (valid) *reinterpret_cast<unsigned*>(xrow + (long)x * a.C) = pack(o, (T*)nullptr);
-      }
-    }
-  }
-  // ---- workgroup reduction over the 16 row workers (reuse the staging LDS);
-  // LDS-only barriers so the dX stores issued above are not waited for
-  lds_barrier();
-  constexpr int PER = 11;                      // 9 taps + 2 BN sums
-  float* red = reinterpret_cast<float*>(sm);   // [NW][16 lanes][EPT][PER]
-#pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-    float* rp = red + ((wk * 16 + cl) * EPT + e) * PER;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) rp[t] = dw[t][e];
-    rp[9] = bs1[e];
-    rp[10] = bs2[e];
-  }
-  lds_barrier();
-  constexpr int L = 16 * EPT * PER;
-  for (int i = threadIdx.x; i < L; i += 256) {
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) s += red[q * L + i];
-    const int k = i % PER, ch = c0 + i / PER;
-    if (ch >= a.C) continue;
-    if (k < 9) a.dWpart[((long)sp * a.C + ch) * 9 + k] = s;
-    else if (bnsum) a.bnpart[((long)sp * 2 + (k - 9)) * a.C + ch] = s;
-  }
-}
-
-template <typename T, int MAXPX>
-void launch_fwd_px(int act, const DwArgs& a, int blocks, hipStream_t st) {
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_NONE, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_RELU, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_BNRELU, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
-}
-
-template <typename T, int MAXPX>
-void launch_bwd_px(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_NONE, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_RELU, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_bwd_kernel<T, ACT_BNRELU, MAXPX>), dim3(blocks), dim3(256), 0, st, a);
-}
-
 template <typename T>
-int launch_fwd(int act, const DwArgs& a, int maxpx, hipStream_t st) {
+int launch_fwd(int act, const DwArgs& a, hipStream_t st) {
   const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
-  if (maxpx == 512) launch_fwd_px<T, 512>(act, a, blocks, st);
-  else launch_fwd_px<T, 256>(act, a, blocks, st);
-  return (int)hipGetLastError();
-}
-
-template <typename T>
-int launch_bwd(int act, const DwBwdArgs& a, int maxpx, hipStream_t st) {
-  const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
-  if (maxpx == 512) launch_bwd_px<T, 512>(act, a, blocks, st);
-  else launch_bwd_px<T, 256>(act, a, blocks, st);
+  constexpr int P = FWD_MAXPX;
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_NONE, P>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_RELU, P>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_BNRELU, P>), dim3(blocks), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -428,20 +255,13 @@ inline int ngroups_for(int C, int dtype) {
 
 
 // =================================================================================
-// Row-walk kernels (default).  The tile kernels above are VALU-bound (measured
-// 36 / 67 VALU lane-ops per element, fwd / bwd: halo index arithmetic, per-window
-// bf16 unpacking, unpacked fp32 math).  Here one WAVE owns one channel slice
-// (64 B: 32 bf16 / 16 fp32 channels) of one frame over RCOLS = 20 output columns and
-// walks down all H rows: lane (cl, s) = (lane & 15, lane >> 4) holds one channel
-// dword (2 bf16 -> float2, packed v_pk_fma_f32 math) for the 5 output columns
-// 5s .. 5s+4 of the wave's column range, with a rolling 3-row register window of 7
-// columns.  Each input row is loaded once per lane (7 dwords; the 2-column overlap
-// of neighbouring segments is served by L1/L2), activated and unpacked once, and
-// feeds 3 output rows; the next row is prefetched one step ahead.  No LDS, no
-// barriers: waves are independent (4 per workgroup = 4 neighbouring channel slices
-// of one frame, i.e. whole 128-B lines).  dW / BN partial sums are reduced over the
-// 4 lane segments with cross-lane shuffles and written once per (frame, column
-// group): P = N * ceil(W / 20).
+// Backward: one WAVE owns one channel slice (64 B: 32 bf16 / 16 fp32 channels) of one
+// frame over RCOLS = 20 output columns and walks down all H rows: lane (cl, s) =
+// (lane & 15, lane >> 4) holds one channel dword (2 bf16 -> float2, packed
+// v_pk_fma_f32 math) for the 5 output columns 5s .. 5s+4 of the wave's column range,
+// with rolling 3-row register windows.  dW / BN partial sums are reduced over the 4
+// lane segments with cross-lane shuffles and written once per (frame, column group):
+// P = N * ceil(W / 20).
 constexpr int RS = 5, RNS = 4, RCOLS = RS * RNS;
 typedef float rf2 __attribute__((ext_vector_type(2)));
 
@@ -487,296 +307,13 @@ XCP_DEV RowMap row_map(int N, int ncg, int ngroups) {
   return m;
 }
 
-template <typename T, int ACT>
-__global__ __launch_bounds__(256) void dw_fwd_row_kernel(DwArgs a) {
-  typedef RV<T> R;
-  typedef typename R::V V;
-  constexpr int EPT = R::EPT, CPG = 16 * EPT;
-  const int ncg = (a.W + RCOLS - 1) / RCOLS;
-  const RowMap mp = row_map(a.N, ncg, a.ngroups);
-  if (!mp.live) return;
-  const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
-  const int c = mp.grp * CPG + cl * EPT;
-  const bool cok = c < a.C;
-  const int cc = cok ? c : a.C - EPT;
-  const int x0 = mp.cg * RCOLS + sg * RS;
-  V wt[9], sc = V(1.f), sh = V(0.f);
-#pragma unroll
-  for (int t = 0; t < 9; ++t) wt[t] = R::load(a.Wt + (long)t * a.C + cc);
-  if constexpr (ACT == ACT_BNRELU) {
-    sc = R::load(a.scale + cc);
-    sh = R::load(a.shift + cc);
-  }
-  int off[RS + 2];
-  unsigned okm = 0;
-#pragma unroll
-  for (int k = 0; k < RS + 2; ++k) {
-    const int col = x0 - 1 + k;
-    off[k] = min(max(col, 0), a.W - 1) * a.C + cc;
-    okm |= (cok && col >= 0 && col < a.W) ? (1u << k) : 0u;
-  }
-  const T* X = reinterpret_cast<const T*>(a.X) + (long)mp.n * a.H * a.W * a.C;
-  T* Y = reinterpret_cast<T*>(a.Y) + (long)mp.n * a.H * a.W * a.C;
-  const int rstride = a.W * a.C;
-  // raw rows in flight: row r lives in slot r % 3 (3-row prefetch ring)
-  unsigned pf[3][RS + 2];
-  auto load = [&](int h, unsigned (&d)[RS + 2]) {
-    const T* row = X + h * rstride;
-#pragma unroll
-    for (int k = 0; k < RS + 2; ++k) d[k] = *reinterpret_cast<const unsigned*>(row + off[k]);
-  };
-  // raw row -> activated, zero-padded values
-  auto cvt = [&](const unsigned (&r)[RS + 2], V (&o)[RS + 2], bool rowok) {
-#pragma unroll
-    for (int k = 0; k < RS + 2; ++k) {
-      V v = R::unpack(r[k]);
-      if constexpr (ACT == ACT_BNRELU) v = vmax0(vfma(v, sc, sh));
-      else if constexpr (ACT == ACT_RELU) v = vmax0(v);
-      o[k] = (rowok && ((okm >> k) & 1)) ? v : V(0.f);
-    }
-  };
-  // step h: window rows (h-1, h, h+1) = (ra, rb, rc); rc is filled from slot s1 (row
-  // h+1), which is then refilled with row h+4
-  auto step = [&](int h, const V (&ra)[RS + 2], const V (&rb)[RS + 2], V (&rc)[RS + 2], unsigned (&s1)[RS + 2]) {
-    cvt(s1, rc, h + 1 < a.H);
-    if (h + 4 < a.H) load(h + 4, s1);
-    T* yrow = Y + h * rstride + c;
-#pragma unroll
-    for (int j = 0; j < RS; ++j) {
-      V o = V(0.f);
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        o = vfma(ra[j + kx], wt[kx], o);
-        o = vfma(rb[j + kx], wt[3 + kx], o);
-        o = vfma(rc[j + kx], wt[6 + kx], o);
-      }
-      if (cok && x0 + j < a.W) *reinterpret_cast<unsigned*>(yrow + (x0 + j) * a.C) = R::pack(o);
-    }
-  };
-  V w0[RS + 2], w1[RS + 2], w2[RS + 2];
-#pragma unroll
-  for (int k = 0; k < RS + 2; ++k) w0[k] = V(0.f);
-  load(0, pf[0]);
-  if (a.H > 1) load(1, pf[1]);
-  if (a.H > 2) load(2, pf[2]);
-  if (a.H > 3) {
-    cvt(pf[0], w1, true);
-    load(3, pf[0]);
-  } else {
-    cvt(pf[0], w1, true);
-  }
-  for (int h = 0; h < a.H; h += 3) {
-    step(h, w0, w1, w2, pf[1]);
-    if (h + 1 < a.H) step(h + 1, w1, w2, w0, pf[2]);
-    if (h + 2 < a.H) step(h + 2, w2, w0, w1, pf[0]);
-  }
-}
-
-template <typename T, int ACT>
-__global__ __launch_bounds__(256, 2) void dw_bwd_row_kernel(DwBwdArgs a) {
-  typedef RV<T> R;
-  typedef typename R::V V;
-  constexpr int EPT = R::EPT, CPG = 16 * EPT;
-  const int ncg = (a.W + RCOLS - 1) / RCOLS;
-  const RowMap mp = row_map(a.N, ncg, a.ngroups);
-  if (!mp.live) return;
-  const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
-  const int c = mp.grp * CPG + cl * EPT;
-  const bool cok = c < a.C;
-  const int cc = cok ? c : a.C - EPT;
-  const int x0 = mp.cg * RCOLS + sg * RS;
-  const bool bnsum = a.bnpart != nullptr;
-  V wt[9], dw[9], sc = V(1.f), sh = V(0.f), bs1 = V(0.f), bs2 = V(0.f), mu = V(0.f), is = V(0.f);
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    wt[t] = R::load(a.Wt + (long)t * a.C + cc);
-    dw[t] = V(0.f);
-  }
-  if constexpr (ACT == ACT_BNRELU) {
-    sc = R::load(a.scale + cc);
-    sh = R::load(a.shift + cc);
-  }
-  if (bnsum) {
-    mu = R::load(a.bmean + cc);
-    is = R::load(a.binvstd + cc);
-  }
-  int off[RS + 2];
-  unsigned okm = 0;
-#pragma unroll
-  for (int k = 0; k < RS + 2; ++k) {
-    const int col = x0 - 1 + k;
-    off[k] = min(max(col, 0), a.W - 1) * a.C + cc;
-    okm |= (cok && col >= 0 && col < a.W) ? (1u << k) : 0u;
-  }
-  const long fbase = (long)mp.n * a.H * a.W * a.C;
-  const int rstride = a.W * a.C;
-  const T* X = reinterpret_cast<const T*>(a.X) + fbase;
-  const T* G = reinterpret_cast<const T*>(a.dY) + fbase;
-  const T* dRes = a.dRes ? reinterpret_cast<const T*>(a.dRes) + fbase : nullptr;
-  const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
-  T* dX = reinterpret_cast<T*>(a.dX) + fbase;
-  // raw rows in flight, row r in slot r % 3 of each ring (X: rows h..h+2, dY: h+1..h+3)
-  unsigned px[3][RS + 2], pg[3][RS + 2];
-  auto load = [&](const T* src, int h, unsigned (&d)[RS + 2]) {
-    const T* row = src + h * rstride;
-#pragma unroll
-    for (int k = 0; k < RS + 2; ++k) d[k] = *reinterpret_cast<const unsigned*>(row + off[k]);
-  };
-  auto cvtg = [&](const unsigned (&r)[RS + 2], V (&gy)[RS + 2], bool rowok) {
-#pragma unroll
-    for (int k = 0; k < RS + 2; ++k) gy[k] = (rowok && ((okm >> k) & 1)) ? R::unpack(r[k]) : V(0.f);
-  };
-  auto step = [&](int h, const V (&g0)[RS + 2], const V (&g1)[RS + 2], V (&g2)[RS + 2], unsigned (&sx)[RS + 2],
-                  unsigned (&sg)[RS + 2]) {
-    // activated X row h (zero padded), raw centre values kept for the BN sums
-    V xa[RS + 2];
-    unsigned xr[RS];
-#pragma unroll
-    for (int k = 0; k < RS + 2; ++k) {
-      V v = R::unpack(sx[k]);
-      if constexpr (ACT == ACT_BNRELU) v = vmax0(vfma(v, sc, sh));
-      else if constexpr (ACT == ACT_RELU) v = vmax0(v);
-      xa[k] = ((okm >> k) & 1) ? v : V(0.f);
-      if (k >= 1 && k <= RS) xr[k - 1] = sx[k];
-    }
-    if (h + 3 < a.H) load(X, h + 3, sx);
-    cvtg(sg, g2, h + 1 < a.H);
-    if (h + 4 < a.H) load(G, h + 4, sg);
-    const int ro = h * rstride;
-    unsigned pres[RS], pskp[RS];
-#pragma unroll
-    for (int j = 0; j < RS; ++j) {
-      const int ow = min(x0 + j, a.W - 1);
-      pres[j] = dRes ? *reinterpret_cast<const unsigned*>(dRes + ro + ow * a.C + cc) : 0u;
-      pskp[j] = 0u;
-    }
-    const bool skip_row = dSkip && (h % a.sS) == 0 && h / a.sS < a.sOH;
-    if (skip_row) {
-#pragma unroll
-      for (int j = 0; j < RS; ++j) {
-        const int ow = x0 + j;
-        if (ow % a.sS == 0 && ow / a.sS < a.sOW && ow < a.W)
-          pskp[j] = *reinterpret_cast<const unsigned*>(
-              dSkip + (((long)mp.n * a.sOH + h / a.sS) * a.sOW + ow / a.sS) * a.C + cc);
-      }
-    }
-    T* xrow = dX + ro + c;
-#pragma unroll
-    for (int j = 0; j < RS; ++j) {
-      // dA = transposed 3x3 over dY; window column k <-> tile column x0 + k - 1
-      V s = V(0.f);
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        s = vfma(g2[j + 2 - kx], wt[kx], s);
-        s = vfma(g1[j + 2 - kx], wt[3 + kx], s);
-        s = vfma(g0[j + 2 - kx], wt[6 + kx], s);
-      }
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        dw[kx] = vfma(g2[j + 1], xa[j + kx], dw[kx]);
-        dw[3 + kx] = vfma(g1[j + 1], xa[j + kx], dw[3 + kx]);
-        dw[6 + kx] = vfma(g0[j + 1], xa[j + kx], dw[6 + kx]);
-      }
-      if constexpr (ACT != ACT_NONE) {
-        const V ctr = xa[j + 1];
-        if constexpr (EPT == 2) {
-          s[0] = ctr[0] > 0.f ? s[0] : 0.f;
-          s[1] = ctr[1] > 0.f ? s[1] : 0.f;
-        } else {
-          s = ctr > 0.f ? s : 0.f;
-        }
-      }
-      const bool valid = cok && x0 + j < a.W;
-      if (bnsum) {
-        const V dz = valid ? R::unpack(R::pack(s)) : V(0.f);   // the stored (rounded) dz
-        bs1 += dz;
-        bs2 = vfma(dz, (R::unpack(xr[j]) - mu) * is, bs2);
-      }
-      if (dRes) s += R::unpack(pres[j]);
-      if (skip_row) s += R::unpack(pskp[j]);
-      if (valid) *reinterpret_cast<unsigned*>(xrow + (x0 + j) * a.C) = R::pack(s);
-    }
-  };
-  V g0[RS + 2], g1[RS + 2], g2[RS + 2];
-#pragma unroll
-  for (int k = 0; k < RS + 2; ++k) g0[k] = V(0.f);
-#pragma unroll
-  for (int r = 0; r < 3; ++r)
-    if (r < a.H) {
-      load(X, r, px[r]);
-      load(G, r, pg[r]);
-    }
-  cvtg(pg[0], g1, true);
-  if (a.H > 3) load(G, 3, pg[0]);
-  for (int h = 0; h < a.H; h += 3) {
-    step(h, g0, g1, g2, px[0], pg[1]);
-    if (h + 1 < a.H) step(h + 1, g1, g2, g0, px[1], pg[2]);
-    if (h + 2 < a.H) step(h + 2, g2, g0, g1, px[2], pg[0]);
-  }
-  // reduce the 4 lane segments (lanes cl, cl+16, cl+32, cl+48) and write the partials
-  float red[EPT][11];
-#pragma unroll
-  for (int e = 0; e < EPT; ++e) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) red[e][t] = R::get(dw[t], e);
-    red[e][9] = R::get(bs1, e);
-    red[e][10] = R::get(bs2, e);
-#pragma unroll
-    for (int q = 0; q < 11; ++q) {
-      red[e][q] += __shfl_xor(red[e][q], 16, 64);
-      red[e][q] += __shfl_xor(red[e][q], 32, 64);
-    }
-  }
-  if (sg == 0 && cok) {
-#pragma unroll
-    for (int e = 0; e < EPT; ++e) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) a.dWpart[((long)mp.unit * a.C + c + e) * 9 + t] = red[e][t];
-      if (bnsum) {
-        a.bnpart[((long)mp.unit * 2 + 0) * a.C + c + e] = red[e][9];
-        a.bnpart[((long)mp.unit * 2 + 1) * a.C + c + e] = red[e][10];
-      }
-    }
-  }
-}
-
-// xcp_tune knobs 4 / 5: forward / backward kernel family (0 = row walk, 1 = LDS tile,
-// 2 = LDS-staged row walk).  Measured at 256 x 19 x 19 x 728 bf16: forward tile 61-65 us,
-// row 70-72, LDS row 72-79; backward (+BN sums) tile 199-207 us, row 159-174, LDS row
-// 145.  The row walks are VALU-bound (~34 VALU lane-ops per element in the backward).
-int g_dw_fwd_kernel = 1, g_dw_bwd_kernel = 2;
-
-template <typename T>
-int launch_fwd_row(int act, const DwArgs& a, hipStream_t st) {
-  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
-  const int blocks = (int)((waves + 3) / 4);
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_row_kernel<T, ACT_NONE>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_row_kernel<T, ACT_RELU>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_fwd_row_kernel<T, ACT_BNRELU>), dim3(blocks), dim3(256), 0, st, a);
-  return (int)hipGetLastError();
-}
-
-template <typename T>
-int launch_bwd_row(int act, const DwBwdArgs& a, hipStream_t st) {
-  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
-  const int blocks = (int)((waves + 3) / 4);
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_row_kernel<T, ACT_NONE>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_bwd_row_kernel<T, ACT_RELU>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_bwd_row_kernel<T, ACT_BNRELU>), dim3(blocks), dim3(256), 0, st, a);
-  return (int)hipGetLastError();
-}
-
-
 // =================================================================================
-// LDS-staged row-walk kernels (default).  Same wave decomposition as the row-walk
-// kernels above (one wave = one 64-B channel slice of one frame over 20 output
-// columns, walking all H rows, lane (cl, s) owning one channel dword of output
-// columns 5s..5s+4), but every HBM access is 16 B per lane: each input row of the
+// LDS-staged row walk: every HBM access is 16 B per lane: each input row of the
 // wave (22 pixels x 64 B, 1408 B) is brought into a per-wave LDS ring by LDS-DMA
 // (global_load_lds, out-of-range pixels and rows from a zero line), lanes read their
 // 7-column windows from LDS, and each output row is staged in LDS and written with
-// 16-B stores.  The measured limit of the register-load variant was the texture
-// address path (one VMEM lane-op per 2 channels); here it is one per 8.
+// 16-B stores (a register-load row walk was limited by the texture address path at one
+// VMEM lane-op per 2 channels; here it is one per 8).
 // Waves are independent (no barriers).  Every step issues the same number of VMEM
 // instructions (masked lanes read the zero line / write a sink), so the per-wave
 // vmcnt counts are static; VMEM operations retire in issue order.
@@ -857,102 +394,13 @@ XCP_DEV void store_row(T* frame, int h, int W, int C, const RowLanes& rl, const 
   }
 }
 
-// Prefetch depth (rows in flight per staged tensor): each step waits only for the
-// loads issued D steps earlier (measured: one row of look-ahead leaves the walk
-// latency-bound, ~2.4 us per row step).
-constexpr int FD = 3;
-
-template <typename T, int ACT>
-__global__ __launch_bounds__(256) void dw_fwd_lds_kernel(DwArgs a) {
-  typedef RV<T> R;
-  typedef typename R::V V;
-  constexpr int EPT = R::EPT, CPG = 16 * EPT, NS = FD + 1;
-  __shared__ __attribute__((aligned(16))) char sm[4][NS * LROW];     // per wave: LDS-DMA row ring
-  __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];  // per wave: output staging
-  // (a separate object: the compiler then knows staging reads never alias in-flight DMA)
-  const int ncg = (a.W + RCOLS - 1) / RCOLS;
-  const RowMap mp = row_map(a.N, ncg, a.ngroups);
-  if (!mp.live) return;
-  const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
-  char* ring = sm[threadIdx.x >> 6];
-  char* stg = so[threadIdx.x >> 6];
-  const int c0 = mp.grp * CPG;
-  const int c = c0 + cl * EPT;
-  const bool cok = c < a.C;
-  const int cc = cok ? c : a.C - EPT;
-  const int x0w = mp.cg * RCOLS, x0 = x0w + sg * RS;
-  const RowLanes rl_ld = row_lanes_load<T>(a.W, a.C, x0w, c0, lane);
-  const RowLanes rl_st = row_lanes_store<T>(a.W, a.C, x0w, c0, lane);
-  V wt[9], sc = V(1.f), sh = V(0.f);
-#pragma unroll
-  for (int t = 0; t < 9; ++t) wt[t] = R::load(a.Wt + (long)t * a.C + cc);
-  if constexpr (ACT == ACT_BNRELU) {
-    sc = R::load(a.scale + cc);
-    sh = R::load(a.shift + cc);
-  }
-  unsigned okm = 0;
-#pragma unroll
-  for (int k = 0; k < RS + 2; ++k) {
-    const int col = x0 - 1 + k;
-    okm |= (col >= 0 && col < a.W) ? (1u << k) : 0u;
-  }
-  const T* X = reinterpret_cast<const T*>(a.X) + (long)mp.n * a.H * a.W * a.C;
-  T* Y = reinterpret_cast<T*>(a.Y) + (long)mp.n * a.H * a.W * a.C;
-  const int lofs = sg * RS * SLICE + cl * 4;   // this lane's window column 0 in a staged row
-  auto slot = [&](int r) { return ring + (r % NS) * LROW; };   // row r lives in slot r % NS
-  auto cvt = [&](const char* row, V (&o)[RS + 2], bool rowok) {
-#pragma unroll
-    for (int k = 0; k < RS + 2; ++k) {
-      V v = R::unpack(*reinterpret_cast<const unsigned*>(row + lofs + k * SLICE));
-      if constexpr (ACT == ACT_BNRELU) {
-        v = vmax0(vfma(v, sc, sh));
-        v = (rowok && ((okm >> k) & 1)) ? v : V(0.f);   // padding is zero after the activation
-      } else if constexpr (ACT == ACT_RELU) {
-        v = vmax0(v);
-      }
-      o[k] = v;
-    }
-  };
-  // VMEM per step h: 2 loads (row h+1+FD) + 2 stores (row h).  Row h+1 was issued at
-  // step h-FD; issued after it: 2 stores + (FD-1) x (2 loads + 2 stores).
-  auto step = [&](int h, const V (&ra)[RS + 2], const V (&rb)[RS + 2], V (&rc)[RS + 2]) {
-    vmwait<2 + 4 * (FD - 1)>();
-    cvt(slot(h + 1), rc, h + 1 < a.H);
-    stage_row<T>(X, h + 1 + FD, a.H, a.W, a.C, rl_ld, slot(h + 1 + FD), lane);   // slot of row h (consumed)
-    V o[RS];
-#pragma unroll
-    for (int j = 0; j < RS; ++j) o[j] = V(0.f);
-    // independent accumulation chains (consecutive packed FMAs never depend on each other)
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int j = 0; j < RS; ++j) o[j] = vfma((ky == 0 ? ra : ky == 1 ? rb : rc)[j + kx], wt[ky * 3 + kx], o[j]);
-#pragma unroll
-    for (int j = 0; j < RS; ++j) *reinterpret_cast<unsigned*>(stg + (sg * RS + j) * SLICE + cl * 4) = R::pack(o[j]);
-    store_row<T>(Y, h, a.W, a.C, rl_st, stg, lane);
-  };
-  V w0[RS + 2], w1[RS + 2], w2[RS + 2];
-#pragma unroll
-  for (int k = 0; k < RS + 2; ++k) w0[k] = V(0.f);
-#pragma unroll
-  for (int r = 0; r <= FD; ++r) stage_row<T>(X, r, a.H, a.W, a.C, rl_ld, slot(r), lane);
-  vmwait<0>();
-  cvt(slot(0), w1, true);
-  for (int h = 0; h < a.H; h += 3) {
-    step(h, w0, w1, w2);
-    if (h + 1 < a.H) step(h + 1, w1, w2, w0);
-    if (h + 2 < a.H) step(h + 2, w2, w0, w1);
-  }
-}
-
-template <typename T, int ACT, bool RES, int BD = 2, int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void dw_bwd_lds_kernel(DwBwdArgs a) {
+template <typename T, int ACT, bool RES>
+__global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
   typedef RV<T> R;
   typedef typename R::V V;
   constexpr int EPT = R::EPT, CPG = 16 * EPT;
   constexpr int NT_ = RES ? 3 : 2;                       // staged tensors: X, dY (, dRes)
+  constexpr int BD = 2;                                  // rows of look-ahead per staged tensor
   constexpr int NS = BD + 1;
   __shared__ __attribute__((aligned(16))) char sm[4][NS * NT_ * LROW];
   __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];   // output staging (separate object)
@@ -1146,147 +594,48 @@ __global__ __launch_bounds__(256, OCC) void dw_bwd_lds_kernel(DwBwdArgs a) {
   }
 }
 
-template <typename T>
-int launch_fwd_lds(int act, const DwArgs& a, hipStream_t st) {
-  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
-  const int blocks = (int)((waves + 3) / 4);
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_lds_kernel<T, ACT_NONE>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_lds_kernel<T, ACT_RELU>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_fwd_lds_kernel<T, ACT_BNRELU>), dim3(blocks), dim3(256), 0, st, a);
-  return (int)hipGetLastError();
-}
-
-int g_dwb_bd = 2;   // xcp_tune knob 15: backward row-walk prefetch depth (2, 3; 4 without a residual)
-
-int g_dwb_occ = 2;   // xcp_tune knob 17: waves per SIMD the backward row-walk kernel is compiled for (2 | 3)
-
-template <typename T, bool RES, int BD, int OCC>
-void launch_bwd_lds_rbo(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_NONE, RES, BD, OCC>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU)
-    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_RELU, RES, BD, OCC>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT_BNRELU, RES, BD, OCC>), dim3(blocks), dim3(256), 0, st, a);
-}
-
-template <typename T, bool RES, int BD>
-void launch_bwd_lds_rb(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (g_dwb_occ == 3 && !RES && BD == 2) launch_bwd_lds_rbo<T, RES, BD, 3>(act, a, blocks, st);
-  else launch_bwd_lds_rbo<T, RES, BD, 2>(act, a, blocks, st);
-}
-
-template <typename T, bool RES>
-void launch_bwd_lds_r(int act, const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (g_dwb_bd >= 4 && !RES) launch_bwd_lds_rb<T, RES, 4>(act, a, blocks, st);
-  else if (g_dwb_bd >= 3) launch_bwd_lds_rb<T, RES, 3>(act, a, blocks, st);
-  else launch_bwd_lds_rb<T, RES, 2>(act, a, blocks, st);
+template <typename T, int ACT>
+void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
+  if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false>), dim3(blocks), dim3(256), 0, st, a);
 }
 
 template <typename T>
 int launch_bwd_lds(int act, const DwBwdArgs& a, hipStream_t st) {
   const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
   const int blocks = (int)((waves + 3) / 4);
-  if (a.dRes) launch_bwd_lds_r<T, true>(act, a, blocks, st);
-  else launch_bwd_lds_r<T, false>(act, a, blocks, st);
+  if (act == ACT_NONE) launch_bwd_act<T, ACT_NONE>(a, blocks, st);
+  else if (act == ACT_RELU) launch_bwd_act<T, ACT_RELU>(a, blocks, st);
+  else launch_bwd_act<T, ACT_BNRELU>(a, blocks, st);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-int xcp_internal_gemm_tune(int cfg);   // gemm.hip
-int xcp_internal_gemm_var(int v);      // gemm.hip
-int xcp_internal_tn_tune(int knob, int v);   // gemm.hip
-int xcp_internal_conv1_tune(int v);          // stem.hip
-int xcp_internal_lstm_tune(int v);           // lstm.hip
-int xcp_internal_nt_grid(int v);             // gemm.hip
-int xcp_internal_conv3_var(int v);           // conv3.hip
-int xcp_internal_pool_quad(int v);           // bn.hip
-int xcp_internal_dw_fwd_frame(int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift,
-                              int N, int H, int W, int C, hipStream_t st);   // dwframe.hip
-int xcp_internal_dwf_var(int v);             // dwframe.hip
-int xcp_internal_dw_small(int v);            // dwframe.hip
 int xcp_internal_dw_fwd_small(int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift,
                               int N, int H, int W, int C, hipStream_t st);   // dwframe.hip
-int g_dw_frame = 0;   // xcp_tune knob 13: small-frame persistent depthwise forward (1; measured slower, see dwframe.hip) or not (0)
 
 extern "C" {
-
-// Tuning knobs: 0 = depthwise forward halo pixels per tile (256 | 512),
-// 1 = depthwise backward halo pixels per tile (256 | 512), 2 = pointwise GEMM tile
-// config (0: 128x128 / 2-stage ring, 1: 256x128 / 3-stage).  Returns the old value.
-int xcp_tune(int knob, int value) {
-  if (knob == 2) return xcp_internal_gemm_tune(value);
-  if (knob == 3) return xcp_internal_gemm_var(value);
-  if (knob == 6 || knob == 7) return xcp_internal_tn_tune(knob, value);
-  if (knob == 8) return xcp_internal_conv1_tune(value);
-  if (knob == 9) return xcp_internal_lstm_tune(value);
-  if (knob == 10) return xcp_internal_nt_grid(value);
-  if (knob == 11) return xcp_internal_conv3_var(value);
-  if (knob == 12) return xcp_internal_pool_quad(value);
-  if (knob == 14) return xcp_internal_dwf_var(value);
-  if (knob == 16) return xcp_internal_dw_small(value);
-  if (knob == 17) {
-    const int old = g_dwb_occ;
-    if (value == 2 || value == 3) g_dwb_occ = value;
-    return old;
-  }
-  if (knob == 15) {
-    const int old = g_dwb_bd;
-    if (value >= 2 && value <= 4) g_dwb_bd = value;
-    return old;
-  }
-  if (knob == 13) {
-    const int old = g_dw_frame;
-    if (value == 0 || value == 1) g_dw_frame = value;
-    return old;
-  }
-  if (knob == 4 || knob == 5) {
-    int& k = knob == 4 ? g_dw_fwd_kernel : g_dw_bwd_kernel;
-    const int old = k;
-    if (value >= 0 && value <= 2) k = value;
-    return old;
-  }
-  int* k = knob == 0 ? &g_fwd_maxpx : knob == 1 ? &g_bwd_maxpx : nullptr;
-  if (!k) return -1;
-  const int old = *k;
-  if (value == 256 || value == 512) *k = value;
-  return old;
-}
 
 int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift, int N,
                int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
-  if (dtype == XCP_BF16 && W <= 8) {
+  if (dtype == XCP_BF16 && W <= 8) {   // tiny frames (the 64^2 audio family's exit flow): dwframe.hip
     const int rc = xcp_internal_dw_fwd_small(act, X, Y, Wt, scale, shift, N, H, W, C, stream);
     if (rc != XCP_EUNSUPPORTED) return rc;
   }
-  if (dtype == XCP_BF16 && g_dw_frame) {
-    const int rc = xcp_internal_dw_fwd_frame(act, X, Y, Wt, scale, shift, N, H, W, C, stream);
-    if (rc != XCP_EUNSUPPORTED) return rc;
-  }
-  const int maxpx = g_fwd_maxpx;
-  DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, maxpx)};
-  if (g_dw_fwd_kernel == 2) {
-    if (dtype == XCP_BF16) return launch_fwd_lds<bf16>(act, a, stream);
-    if (dtype == XCP_F32) return launch_fwd_lds<float>(act, a, stream);
-    return XCP_EUNSUPPORTED;
-  }
-  if (g_dw_fwd_kernel == 0) {
-    if (dtype == XCP_BF16) return launch_fwd_row<bf16>(act, a, stream);
-    if (dtype == XCP_F32) return launch_fwd_row<float>(act, a, stream);
-    return XCP_EUNSUPPORTED;
-  }
-  if (dtype == XCP_BF16) return launch_fwd<bf16>(act, a, maxpx, stream);
-  if (dtype == XCP_F32) return launch_fwd<float>(act, a, maxpx, stream);
+  DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, FWD_MAXPX)};
+  if (dtype == XCP_BF16) return launch_fwd<bf16>(act, a, stream);
+  if (dtype == XCP_F32) return launch_fwd<float>(act, a, stream);
   return XCP_EUNSUPPORTED;
 }
 
-// number of partial rows (spatial workgroups) of the backward's slabs
+// number of partial rows (frame x 20-column groups) of the backward's slabs
 int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
+  (void)H;
   (void)C;
-  if (g_dw_bwd_kernel != 1) return N * ((W + RCOLS - 1) / RCOLS);
-  const TileGeo g = tile_geo(H, W, g_bwd_maxpx);
-  return N * g.nth * g.ntw;
+  return N * ((W + RCOLS - 1) / RCOLS);
 }
 
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
@@ -1295,26 +644,14 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
   if (bnpart && (act != ACT_BNRELU || !bmean || !binvstd)) return XCP_EINVAL;
-  const int maxpx = g_bwd_maxpx;
   DwBwdArgs a{};
   a.dY = dY; a.X = X; a.Wt = Wt; a.scale = scale; a.shift = shift; a.dRes = dRes; a.dSkip = dSkip;
   a.sOH = sOH; a.sOW = sOW; a.sS = sS > 0 ? sS : 1; a.dX = dX; a.dWpart = dWpart;
   a.bnpart = bnpart; a.bmean = bmean; a.binvstd = binvstd;
   a.N = N; a.H = H; a.W = W; a.C = C;
   a.ngroups = ngroups_for(C, dtype);
-  a.g = tile_geo(H, W, maxpx);
-  if (g_dw_bwd_kernel == 2) {
-    if (dtype == XCP_BF16) return launch_bwd_lds<bf16>(act, a, stream);
-    if (dtype == XCP_F32) return launch_bwd_lds<float>(act, a, stream);
-    return XCP_EUNSUPPORTED;
-  }
-  if (g_dw_bwd_kernel == 0) {
-    if (dtype == XCP_BF16) return launch_bwd_row<bf16>(act, a, stream);
-    if (dtype == XCP_F32) return launch_bwd_row<float>(act, a, stream);
-    return XCP_EUNSUPPORTED;
-  }
-  if (dtype == XCP_BF16) return launch_bwd<bf16>(act, a, maxpx, stream);
-  if (dtype == XCP_F32) return launch_bwd<float>(act, a, maxpx, stream);
+  if (dtype == XCP_BF16) return launch_bwd_lds<bf16>(act, a, stream);
+  if (dtype == XCP_F32) return launch_bwd_lds<float>(act, a, stream);
   return XCP_EUNSUPPORTED;
 }
 

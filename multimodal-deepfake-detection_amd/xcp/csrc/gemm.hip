@@ -316,93 +316,12 @@ __global__ __launch_bounds__(WMW * 128) void gemm_nt_kernel(NTArgs a) {
   }
 }
 
-constexpr int L_CP = 256 * 2 + 16;             // LDS-staged epilogue row pitch (bytes)
-
-// LDS-staged epilogue of the 256x256 kernels: acc[i][j][r] is C[row wr*128 + i*16 + fr]
-// [col wc*64 + j*16 + fg*4 + r]; rounded tile staged in LDS, written with coalesced 16-B
-// stores, BatchNorm partial sums per 128-row half ([ceil(M/128)][2][N] layout).
-template <int EPIV = 0>
-XCP_DEV void epilogue256(f32x4 (&acc)[8][4], char* smem, const NTArgs& a, int m0, int n0, int bm, int tid) {
-  const int lane = tid & 63, w = tid >> 6, wr = w >> 2, wc = w & 3, fr = lane & 15, fg = lane >> 4;
-  bf16* C = reinterpret_cast<bf16*>(a.C);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wr * 128 + i * 16 + fr, col = wc * 64 + j * 16 + fg * 4;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r];
-        VecIO<bf16, 4>::store(reinterpret_cast<bf16*>(smem + row * L_CP + col * 2), v);
-      }
-    __syncthreads();
-    const int c = tid & 31, rq = tid >> 5;
-    const int n = n0 + c * 8;
-    float t1[2][8], t2[2][8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) t1[h][e] = t2[h][e] = 0.f;
-    uint4 cv[16];
-#pragma unroll
-    for (int it = 0; it < 16; ++it) cv[it] = *reinterpret_cast<const uint4*>(smem + (rq + 16 * it) * L_CP + c * 16);
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int m = m0 + rq + 16 * it;
-      if (m < a.M && n < a.N) {
-        if (EPIV == 0 || a.M < 0) *reinterpret_cast<uint4*>(C + (long)m * a.ldc + n) = cv[it];
-        float f[8];
-        VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&cv[it]), f);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          t1[it >> 3][e] += f[e];
-          t2[it >> 3][e] = fmaf(f[e], f[e], t2[it >> 3][e]);
-        }
-      }
-    }
-    if (a.stats) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          t1[h][e] += __shfl_xor(t1[h][e], 32, 64);
-          t2[h][e] += __shfl_xor(t2[h][e], 32, 64);
-        }
-      float* red = reinterpret_cast<float*>(smem);   // [h][q][wave][256]
-      lds_barrier();
-      if (lane < 32) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            red[((h * 2 + 0) * 8 + w) * 256 + c * 8 + e] = t1[h][e];
-            red[((h * 2 + 1) * 8 + w) * 256 + c * 8 + e] = t2[h][e];
-          }
-      }
-      lds_barrier();
-      const int h = tid >> 8, col = tid & 255;
-      const int nn = n0 + col, srow = bm * 2 + h;
-      if (nn < a.N && srow < (a.M + 127) / 128) {
-        float u1 = 0.f, u2 = 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          u1 += red[((h * 2 + 0) * 8 + q) * 256 + col];
-          u2 += red[((h * 2 + 1) * 8 + q) * 256 + col];
-        }
-        a.stats[((long)srow * 2 + 0) * a.N + nn] = u1;
-        a.stats[((long)srow * 2 + 1) * a.N + nn] = u2;
-      }
-    }
-}
-
 // LDS-free epilogue of the 256x256 NT kernels (acc[i][j][r] = C[m0 + wr*128 + i*16 + fr]
 // [n0 + wc*64 + j*16 + fg*4 + r]): lanes fg / fg^1 (16 apart) swap 8-B pieces so each lane
 // stores 16 contiguous bytes (one store instruction = 16 rows x 64 B); the BatchNorm partial
 // sums of each 128-row half ([ceil(M/128)][2][N]) come from the rounded registers: sums over
 // the wave's 8 row fragments, then a 4-step reduce-scatter over the 16 row lanes (30
 // shuffles), after which lane fr holds 2 adjacent columns of one statistic.
-template <int EPIV = 0>
 XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n0, int wr, int wc, int fr, int fg) {
   bf16* C = reinterpret_cast<bf16*>(a.C);
   const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
@@ -442,11 +361,10 @@ XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n
     const uint4 st1 = odd ? make_uint4(rc1.x, rc1.y, pc[3].x, pc[3].y) : make_uint4(pc[2].x, pc[2].y, rc1.x, rc1.y);
     const int c0 = ncol + (odd ? 16 + (fg - 1) * 4 : fg * 4);
     bf16* crow = C + (long)m * a.ldc;
-    const bool wr_ok = (EPIV & 1) == 0 || a.M < 0;
-    if (wr_ok && mok && c0 < a.N) *reinterpret_cast<uint4*>(crow + c0) = st0;
-    if (wr_ok && mok && c0 + 32 < a.N) *reinterpret_cast<uint4*>(crow + c0 + 32) = st1;
+    if (mok && c0 < a.N) *reinterpret_cast<uint4*>(crow + c0) = st0;
+    if (mok && c0 + 32 < a.N) *reinterpret_cast<uint4*>(crow + c0 + 32) = st1;
   }
-  if (a.stats && ((EPIV & 2) == 0 || a.M < 0)) {
+  if (a.stats) {
     // reduce-scatter of v[32] = (s1[16], s2[16]) over the 16 row lanes
     float u[16], v8[8], v4[4], v2[2];
     const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
@@ -491,12 +409,9 @@ XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
   else wait_vmcnt<0>();
 }
 
-// EPIV: 0 = LDS-staged epilogue, 4 = LDS-free register epilogue (knob 3 = 11); measurement
-// only (knob 3 = 2 / 3): 1 = no C stores, 2 = no epilogue
-template <bool STAG, int EPIV = 0>
 __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
-  constexpr int RING = 2 * K_SLOT, EPI = 256 * L_CP;
-  __shared__ __attribute__((aligned(16))) char smem[RING > EPI ? RING : EPI];
+  constexpr bool STAG = true;   // wave group 1 runs one barrier behind group 0
+  __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
   const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
   const int id = xcd_remap(blockIdx.x, gridM * gridN);
   const int bn = id % gridN, bm = id / gridN;
@@ -621,248 +536,8 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
     sync_mfma(1, bl, 0);
   }
   if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
-  if constexpr (EPIV == 2) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-    if (a.M < 0) a.stats[tid] = t;
-  } else if constexpr (EPIV == 4) {
-    epilogue256_regs(acc, a, m0, n0, wr, wc, fr, fg);
-  } else {
-    epilogue256<EPIV>(acc, smem, a, m0, n0, bm, tid);
-  }
+  epilogue256_regs(acc, a, m0, n0, wr, wc, fr, fg);
 }
-
-// ---------------------------------------------------------------------------------
-// Persistent 256x256 bf16 NT kernel: the tile machinery of gemm_nt256k64_kernel (two
-// 64 KB LDS-DMA ring slots, 8 waves 2x4, four-phase quadrant schedule, staggered wave
-// groups, counted vmcnt), but one workgroup per CU walks a static list of tiles (tile =
-// round * grid + XCD-remapped workgroup id, so same-XCD workgroups hold neighbouring tiles
-// and share A rows in L2) and the K pipeline runs ACROSS tile boundaries: the last K-tile
-// of a tile prefetches K-tile 0 of the next one like any other stage, so no tile starts
-// with an exposed load.  That requires an epilogue that never touches LDS:
-//   * C stores: lanes fg / fg^1 (16 apart) swap 8-B pieces so every lane owns 16
-//     contiguous bytes; one store instruction writes 16 rows x 64 B.
-//   * BatchNorm partial sums of each 128-row half ([ceil(M/128)][2][N]) from the rounded
-//     registers: sums over the wave's 8 row fragments, then a 4-step reduce-scatter over
-//     the 16 row lanes (30 shuffles); lane fr ends with 2 adjacent columns of one statistic.
-// The epilogue's EPI_VM vector-memory ops per thread sit between A-bot(0) of the next tile
-// and the waits of that tile's first two phases; those waits allow for them, so the stores
-// drain under the next tile's MFMAs (the Q3 wait of K-tile 0 retires them).  A last K-tile
-// with <= 32 valid columns skips its second 32-deep MFMA step (K = 728: 736 instead of 768).
-constexpr int EPI_VM = 17;
-
-template <int N>
-XCP_DEV void wait_vm_imm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-XCP_DEV void wait_cnt_p(int n) {   // n in {0, 2, 4, E, E+2, E+4}
-  switch (n) {
-    case 0: wait_vm_imm<0>(); break;
-    case 2: wait_vm_imm<2>(); break;
-    case 4: wait_vm_imm<4>(); break;
-    case EPI_VM: wait_vm_imm<EPI_VM>(); break;
-    case EPI_VM + 2: wait_vm_imm<EPI_VM + 2>(); break;
-    default: wait_vm_imm<EPI_VM + 4>(); break;
-  }
-}
-
-template <bool STAG, int EPIV = 0>   // EPIV (measurement): 1 no C stores, 2 no stats, 3 neither
-__global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
-  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
-  const int tiles = gridM * gridN, G = gridDim.x;
-  // round r holds tiles [rG, rG+G): full rounds give each XCD a contiguous block of G/8 tiles;
-  // the last, partial round of R tiles goes to workgroups b < R (spread over all XCDs),
-  // again XCD-contiguous within it
-  const int full = tiles / G, R = tiles - full * G;
-  auto tile_of = [&](int r) { return r < full ? r * G + xcd_remap(blockIdx.x, G) : r * G + xcd_remap(blockIdx.x, R); };
-  const int my_tiles = full + ((int)blockIdx.x < R ? 1 : 0);
-  if (my_tiles == 0) return;            // uniform; before any barrier
-  int round = 0, tile = tile_of(0);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 2, wc = w & 3, fr = lane & 15, fg = lane >> 4;
-  const bf16* A = reinterpret_cast<const bf16*>(a.A);
-  const bf16* B = reinterpret_cast<const bf16*>(a.B);
-  bf16* C = reinterpret_cast<bf16*>(a.C);
-
-  // half-tile rows loaded by this wave (as gemm_nt256k64_kernel)
-  const int arow = (w < 4 ? 16 * w : 128 + 16 * (w - 4));
-  const int brow = 64 * (w >> 1) + 16 * (w & 1);
-  const int lr = lane >> 3;
-  // swizzled 16-B chunk column (in elements) of the row a load of half-tile h, piece i fills
-  auto kc8 = [&](int h, int i) {
-    const bool isA = (h == 0 || h == 3);
-    const int row = (isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0)) + i * 8 + lr;
-    return ((lane & 7) ^ ((row >> 1) & 7)) * 8;
-  };
-  const void* zero = g_zero16;
-  asm volatile("" : "+v"(zero));
-  auto glds = [](const void* p, char* dst) {
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
-                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-  };
-  // per-lane source element offsets (chunk column included; the host guarantees they fit
-  // 31 bits) of the tile the loads currently target: re-pointed to the next tile at the
-  // start of each tile's last K-tile
-  int src[4][2];
-  auto set_target = [&](int am0, int bn0) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const bool isA = (h == 0 || h == 3);
-        const int row = (isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0)) + i * 8 + lr;
-        src[h][i] = (isA ? min(am0 + row, a.M - 1) * (int)a.lda : min(bn0 + row, a.N - 1) * (int)a.ldb) + kc8(h, i);
-      }
-  };
-  // half-tile h (0 A-top, 1 B-left, 2 B-right, 3 A-bot) of K-tile kt of the target tile into ring slot sl
-  auto issue = [&](int h, int kt, int sl) {
-    const bool isA = (h == 0 || h == 3);
-    const int row0 = isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0);
-    char* d = smem + sl * K_SLOT + (isA ? 0 : K_OP) + row0 * 128;
-    const int kb = kt * 64;
-    const bf16* base = isA ? A : B;
-    if (kb + 64 <= a.K) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) glds(base + (src[h][i] + kb), d + i * 1024);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        glds(kb + kc8(h, i) < a.K ? (const void*)(base + (src[h][i] + kb)) : zero, d + i * 1024);
-    }
-  };
-
-  const int nk = (a.K + 63) / 64;
-  const bool half_tail = a.K - (nk - 1) * 64 <= 32;
-  set_target((tile / gridN) * 256, (tile % gridN) * 256);
-#pragma unroll
-  for (int h = 0; h < 4; ++h) issue(h, 0, 0);
-  wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-  if (STAG && wr == 1) __builtin_amdgcn_s_barrier();
-
-  f32x4 acc[8][4];
-  bf16x8 af[4][2], bl[2][2], br[2][2];   // [frag][k-step]
-  int slot = 0;
-  bool after_epi = false;
-  for (;;) {
-    const bool more = round + 1 < my_tiles;
-    const int next = more ? tile_of(round + 1) : tile;
-    const int cm0 = (tile / gridN) * 256, cn0 = (tile % gridN) * 256;
-    const int xm0 = (next / gridN) * 256, xn0 = (next % gridN) * 256;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool last = kt + 1 == nk;
-      const bool nxt = !last || more;
-      const int nkt = last ? 0 : kt + 1, nsl = slot ^ 1;
-      if (last && more) set_target(xm0, xn0);
-      const int e = (kt == 0 && after_epi) ? EPI_VM : 0;   // epilogue ops younger than this tile's loads
-      const bool one = last && half_tail;                  // only the first 32-deep step holds data
-      const char* sa = smem + slot * K_SLOT;
-      const char* sb = sa + K_OP;
-      auto mfma_q = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          if (ks == 1 && one) break;
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[ih * 4 + i][jh * 2 + j] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][ks], af[i][ks], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
-        }
-      };
-      auto sync_mfma = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
-        __builtin_amdgcn_s_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        mfma_q(ih, b, jh);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_s_barrier();
-      };
-      // Q0: A-top x B-left
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (ks == 1 && one) break;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          bl[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + j * 16 + fr, ks * 4 + fg));
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 16 + fr, ks * 4 + fg));
-      }
-      if (nxt) issue(0, nkt, nsl);
-      wait_cnt_p(2 + e + (nxt ? 2 : 0));   // B-right(kt) for Q1
-      sync_mfma(0, bl, 0);
-      // Q1: A-top x B-right
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (ks == 1 && one) break;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          br[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + 32 + j * 16 + fr, ks * 4 + fg));
-      }
-      if (nxt) issue(1, nkt, nsl);
-      wait_cnt_p(e + (nxt ? 4 : 0));       // A-bot(kt) for Q2
-      sync_mfma(0, br, 1);
-      // Q2: A-bot x B-right
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        if (ks == 1 && one) break;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
-      }
-      if (nxt) issue(2, nkt, nsl);
-      sync_mfma(1, br, 1);
-      // Q3: A-bot x B-left
-      if (nxt) {
-        issue(3, nkt, nsl);
-        wait_cnt_p(4);                     // A-top / B-left of the next K-tile (and the epilogue's stores)
-      }
-      sync_mfma(1, bl, 0);
-      slot = nsl;
-    }
-
-    epilogue256_regs<EPIV>(acc, a, cm0, cn0, wr, wc, fr, fg);
-    asm volatile("" ::: "memory");
-    if (!more) break;
-    tile = next;
-    ++round;
-    after_epi = true;
-  }
-  if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
-}
-
-// xcp_tune knob 6: 1 = 256x256 weight-gradient kernel (2-slot 64-row ring) for dense bf16
-// (default); 2 = the 4-slot 32-row ring (deeper prefetch measured no faster: 175 vs 168 us,
-// the loads are bandwidth- not latency-bound); 0 = 128x128
-int g_tn_cfg = 1;
-int g_tn_wgs = 256;    // xcp_tune knob 7: target workgroups (splits x tiles) of the 256x256 kernel
-bool tn_big(int dtype, int gmode, int N, int K) {
-  // (narrower outputs stream faster through the 128-tile kernel: 0.57 vs 0.95 ms at 5.5M x 128 x 128)
-  return g_tn_cfg >= 1 && dtype == XCP_BF16 && gmode == 0 && N >= 256 && K >= 256;
-}
-
-// xcp_tune knob 3: 11 = one tile per workgroup, staggered wave groups, LDS-free register
-// epilogue (default); 4 = the same with the LDS-staged epilogue; 1 = lockstep;
-// 0 / 7 = persistent kernel staggered / lockstep (measured slower: see DESIGN.md); 2 / 3 / 8-10 = ablations
-int g_nt256_var = 11;
-int g_num_cus = 256;   // set from the device at first use (xcp_gemm_nt)
-int g_nt_grid = 0;     // xcp_tune knob 10: persistent grid size (0 = one workgroup per CU)
-
-// xcp_tune knob 2: 0 = 128x128 tile / 2-stage ring, 1 = 256x128 / 3-stage,
-// 2 = auto (256x256 8-wave kernel for dense bf16 with >= 256 tiles and K >= 384, else 128x128),
-// 3 = 256x256 kernel for every dense bf16 call (tests)
-int g_nt_cfg = 2;
 
 // ---------------------------------------------------------------------------------
 // Weight gradient: P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]
@@ -1032,7 +707,6 @@ XCP_DEV int tswz(int m, int col) {             // byte offset of bf16 column col
   return m * 512 + ((((col >> 3) ^ ((m & 7) << 1))) << 4) + (col & 7) * 2;
 }
 
-template <int ABL>
 __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * T_SLOT];
   const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
@@ -1040,7 +714,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   const int id = xcd_remap(blockIdx.x, gridDim.x);   // one split's tiles share an XCD (its rows stay in L2)
   const int sp = id / tiles, t = id % tiles;
   const int n0 = (t / gridK) * 256, k0 = (t % gridK) * 256;
-  const int mbeg = ABL >= 3 ? 0 : sp * a.rows_per_split;   // ABL 3, 4 (measurement): every split reads split 0 rows
+  const int mbeg = sp * a.rows_per_split;
   const int mend = min(a.M, mbeg + a.rows_per_split);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 2, wc = w & 3;
@@ -1111,16 +785,11 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (ABL == 2 || ABL == 4) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(xf[i]), "v"(gf[i]));
-    } else {
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], gf[i], acc[ih * 4 + i][j], 0, 0, 0);
-    }
+      for (int j = 0; j < 4; ++j)
+        acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], gf[i], acc[ih * 4 + i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
@@ -1135,12 +804,12 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
       for (int j = 0; j < 4; ++j) xf[j] = frag(sx, ms, wc * 64 + j * 16);
 #pragma unroll
       for (int i = 0; i < 4; ++i) gf[i] = frag(sg, ms, wr * 128 + i * 16);
-      if (ABL != 1 && nxt) issue(2 * ms, kt + 1);
+      if (nxt) issue(2 * ms, kt + 1);
       sync_mfma(0);
       // n-bot
 #pragma unroll
       for (int i = 0; i < 4; ++i) gf[i] = frag(sg, ms, wr * 128 + 64 + i * 16);
-      if (ABL != 1 && nxt) {
+      if (nxt) {
         issue(2 * ms + 1, kt + 1);
         wait_vmcnt<4>();   // ms 0: m1 half-tiles of kt (for Q2); ms 1: m0 half-tiles of kt+1
       } else {
@@ -1164,147 +833,25 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------------
-// The same 256x256 weight-gradient tile with a deeper load pipeline.  Measured on the
-// 728x728 middle-flow shape, gemm_tn256_kernel is load-bound: 152 us per call, 79 us with
-// its LDS-DMA loads removed (MFMA + LDS reads alone), 148 us with its MFMAs removed.  Its
-// two 64-row K-tile slots give the loads of K-tile t+1 only the MFMAs of K-tile t to land
-// in.  Here a K-tile is 32 m-rows (one MFMA step; G and X slabs of 32 x 512 B = 32 KB per
-// slot) and the ring has 4 slots, so three K-tiles are in flight while one is consumed:
-//   phase A (n-top): reads X all + G n-top   issues G(t+3)
-//   phase B (n-bot): reads G n-bot           issues X(t+3), retires t+1 (counted vmcnt)
-// Slot (t+3)&3 = (t-1)&3 was last read in phase B of t-1, two barriers earlier.
-constexpr int R4_OP = 32 * 512;                // one operand, one slot (16 KB)
-constexpr int R4_SLOT = 2 * R4_OP;
+}  // namespace
 
-template <int N>
-XCP_DEV void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+namespace {
+// Tile selection (immutable): the 256x256 8-wave kernels run dense bf16 problems with enough
+// work (NT: >= 256 tiles and K >= 384, i.e. every 728 / 1024 / 1536-channel layer at
+// training batch sizes; TN: N, K >= 256); everything else runs the 128x128 kernels.  The
+// `tile` argument of the entry points (0 auto, 1 = 128x128, 2 = 256x256) overrides the choice
+// so tests can pin each kernel at small sizes.
+constexpr int TN_TARGET_WGS = 256;   // 256x256 weight-gradient workgroups (splits x tiles): one per CU
+
+bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
+  if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
+  return tile == 2 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
 }
 
-__global__ __launch_bounds__(512) void gemm_tn256r4_kernel(TNArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * R4_SLOT];
-  const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
-  const int tiles = gridN * gridK;
-  const int id = xcd_remap(blockIdx.x, gridDim.x);   // one split's tiles share an XCD (its rows stay in L2)
-  const int sp = id / tiles, t = id % tiles;
-  const int n0 = (t / gridK) * 256, k0 = (t % gridK) * 256;
-  const int mbeg = sp * a.rows_per_split;
-  const int mend = min(a.M, mbeg + a.rows_per_split);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 2, wc = w & 3;
-  const bf16* G = reinterpret_cast<const bf16*>(a.G);
-  const bf16* X = reinterpret_cast<const bf16*>(a.X);
-
-  // staging: a slab is 32 m-rows x 512 B; wave w loads rows 4w + 2i + (lane >> 5) (i = 0, 1),
-  // lane writes physical chunk lane & 31 = logical chunk lc
-  const int pc = lane & 31;
-  int rr[2], lc[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    rr[i] = 4 * w + 2 * i + (lane >> 5);
-    lc[i] = pc ^ ((rr[i] & 7) << 1);
-  }
-  const void* zero = g_zero16;
-  asm volatile("" : "+v"(zero));
-  auto glds = [](const void* p, char* dst) {
-    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
-                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-  };
-  // operand op (0: G, 1: X) of K-tile kt into slot kt & 3
-  auto issue = [&](int op, int kt) {
-    char* d = smem + (kt & 3) * R4_SLOT + op * R4_OP;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = mbeg + kt * 32 + rr[i];
-      const int col = (op == 0 ? n0 : k0) + lc[i] * 8;
-      const bool ok = m < mend && col < (op == 0 ? a.N : a.K);
-      const void* src = ok ? (op == 0 ? (const void*)(G + (long)m * a.ldg + col) : (const void*)(X + (long)m * a.ldx + col))
-                           : zero;
-      glds(src, d + (4 * w + 2 * i) * 512);   // 1 KB = slab rows 4w+2i, +1
-    }
-  };
-  // outstanding-load count after K-tile j's loads when waiting for them at the end of K-tile
-  // t (loads of K-tiles j+1 .. min(t+3, nk-1) may stay in flight; 4 per K-tile per thread)
-  auto wait_for = [&](int ahead) {
-    if (ahead >= 2) wait_vm<8>();
-    else if (ahead == 1) wait_vm<4>();
-    else wait_vm<0>();
-  };
-
-  f32x4 acc[8][4];   // [n-frag][k-frag]: lane holds P[n = .. + fr][k = .. + 4*fg + r]
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (mend - mbeg + 31) / 32;
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-    if (j < nk) {
-      issue(0, j);
-      issue(1, j);
-    }
-  wait_for(min(nk - 1, 2));   // K-tile 0 landed
-  __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();
-
-  const int fr = lane & 15, fg = lane >> 4;
-  const int q4 = fr >> 2, p4 = fr & 3;   // tr read: lane 4q+p reads slab row q, columns 4p..4p+3
-  // fragment of 16 columns at cb: k-slots of lane group fg are slab rows {4fg..4fg+3}
-  // (elements 0-3) and {16+4fg..} (4-7)
-  auto frag = [&](const char* slab, int cb) {
-    const int m0r = 4 * fg + q4;
-    const int col = cb + 4 * p4;
-    const bf16x4 lo = ds_read_tr(slab + tswz(m0r, col));
-    const bf16x4 hi = ds_read_tr(slab + tswz(m0r + 16, col));
-    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  };
-  bf16x8 gf[4], xf[4];
-  auto sync_mfma = [&](int ih) {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[j], gf[i], acc[ih * 4 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
-  };
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* sg = smem + (kt & 3) * R4_SLOT;
-    const char* sx = sg + R4_OP;
-    const bool nxt = kt + 3 < nk;
-    // phase A: n-top
-#pragma unroll
-    for (int j = 0; j < 4; ++j) xf[j] = frag(sx, wc * 64 + j * 16);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) gf[i] = frag(sg, wr * 128 + i * 16);
-    if (nxt) issue(0, kt + 3);
-    sync_mfma(0);
-    // phase B: n-bot
-#pragma unroll
-    for (int i = 0; i < 4; ++i) gf[i] = frag(sg, wr * 128 + 64 + i * 16);
-    if (nxt) issue(1, kt + 3);
-    if (kt + 1 < nk) wait_for(min(kt + 3, nk - 1) - (kt + 1));   // K-tile kt+1 landed (this wave)
-    sync_mfma(1);
-  }
-  if (wr == 0) __builtin_amdgcn_s_barrier();
-
-  float* P = a.P + (long)sp * a.N * a.K;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = n0 + wr * 128 + i * 16 + fr;
-    if (n >= a.N) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = k0 + wc * 64 + j * 16 + 4 * fg;
-      if (k < a.K) *reinterpret_cast<f32x4*>(P + (long)n * a.K + k) = acc[i][j];
-    }
-  }
+bool tn_big(int dtype, int gmode, int N, int K, int tile) {
+  // (narrower outputs stream faster through the 128-tile kernel: 0.57 vs 0.95 ms at 5.5M x 128 x 128)
+  if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
+  return tile == 2 || (N >= 256 && K >= 256);
 }
 }  // namespace
 
@@ -1312,50 +859,24 @@ extern "C" {
 
 // C[M,N] = A[M,K] . B[N,K]^T ; see include/xcp.h
 int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, hipStream_t stream) {
+                float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
+  if (tile < 0 || tile > 2) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
-  if (g_nt_cfg >= 2 && dtype == XCP_BF16 && gmode == 0) {
-    static const int cus = [] {
-      int d = 0, n = 0;
-      if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-        n = 0;
-      return n > 0 ? n : 256;
-    }();
-    g_num_cus = cus;
+  if (nt_big(dtype, gmode, M, N, K, tile)) {
     const int tiles = xcp_cdiv(M, 256) * xcp_cdiv(N, 256);
-    if ((tiles >= 256 && K >= 384) || g_nt_cfg == 3) {
-      const bool fits31 = (long)M * lda < (1L << 31) && (long)N * ldb < (1L << 31);
-      if ((g_nt256_var == 0 || (g_nt256_var >= 7 && g_nt256_var <= 10)) && fits31) {
-        const int cap = g_nt_grid > 0 ? g_nt_grid : g_num_cus;
-        const int grid = tiles < cap ? tiles : cap;
-        if (g_nt256_var == 7) hipLaunchKernelGGL((gemm_nt256p_kernel<false>), dim3(grid), dim3(512), 0, stream, a);
-        else if (g_nt256_var == 8) hipLaunchKernelGGL((gemm_nt256p_kernel<true, 1>), dim3(grid), dim3(512), 0, stream, a);
-        else if (g_nt256_var == 9) hipLaunchKernelGGL((gemm_nt256p_kernel<true, 2>), dim3(grid), dim3(512), 0, stream, a);
-        else if (g_nt256_var == 10) hipLaunchKernelGGL((gemm_nt256p_kernel<true, 3>), dim3(grid), dim3(512), 0, stream, a);
-        else hipLaunchKernelGGL((gemm_nt256p_kernel<true>), dim3(grid), dim3(512), 0, stream, a);
-      } else if (g_nt256_var == 1) hipLaunchKernelGGL((gemm_nt256k64_kernel<false>), dim3(tiles), dim3(512), 0, stream, a);
-      else if (g_nt256_var == 11) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 4>), dim3(tiles), dim3(512), 0, stream, a);
-      else if (g_nt256_var >= 7) hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);
-      else if (g_nt256_var == 2) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 1>), dim3(tiles), dim3(512), 0, stream, a);
-      else if (g_nt256_var == 3) hipLaunchKernelGGL((gemm_nt256k64_kernel<true, 2>), dim3(tiles), dim3(512), 0, stream, a);
-      else hipLaunchKernelGGL((gemm_nt256k64_kernel<true>), dim3(tiles), dim3(512), 0, stream, a);   // var 4
-      return (int)hipGetLastError();
-    }
+    hipLaunchKernelGGL(gemm_nt256k64_kernel, dim3(tiles), dim3(512), 0, stream, a);
+    return (int)hipGetLastError();
   }
-  const int wmw = g_nt_cfg == 1 ? 4 : 2;
-  const int grid = xcp_cdiv(M, 64 * wmw) * xcp_cdiv(N, NBN);
-#define XCP_NT_CFG(TT, GMV)                                                                                     \
-  if (wmw == 4) hipLaunchKernelGGL((gemm_nt_kernel<TT, GMV, 4, 3>), dim3(grid), dim3(512), 0, stream, a);        \
-  else hipLaunchKernelGGL((gemm_nt_kernel<TT, GMV, 2, 2>), dim3(grid), dim3(256), 0, stream, a);
-#define XCP_NT_LAUNCH(TT)                                                                                      \
-  switch (gmode) {                                                                                             \
-    case 0: XCP_NT_CFG(TT, 0) break;                                                                           \
-    case 1: XCP_NT_CFG(TT, 1) break;                                                                           \
-    case 2: XCP_NT_CFG(TT, 2) break;                                                                           \
-    default: XCP_NT_CFG(TT, 3) break;                                                                          \
+  const int grid = xcp_cdiv(M, 128) * xcp_cdiv(N, NBN);
+#define XCP_NT_LAUNCH(TT)                                                                                       \
+  switch (gmode) {                                                                                              \
+    case 0: hipLaunchKernelGGL((gemm_nt_kernel<TT, 0, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;     \
+    case 1: hipLaunchKernelGGL((gemm_nt_kernel<TT, 1, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;     \
+    case 2: hipLaunchKernelGGL((gemm_nt_kernel<TT, 2, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;     \
+    default: hipLaunchKernelGGL((gemm_nt_kernel<TT, 3, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;    \
   }
   if (dtype == XCP_BF16) {
     XCP_NT_LAUNCH(bf16)
@@ -1364,53 +885,23 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   } else {
     return XCP_EUNSUPPORTED;
   }
-#undef XCP_NT_CFG
 #undef XCP_NT_LAUNCH
   return (int)hipGetLastError();
 }
 
-// rows of the stats partial array gemm_nt writes ([rows][2][N])
-int xcp_gemm_nt_stat_rows(int M) { return xcp_cdiv(M, g_nt_cfg == 1 ? 256 : 128); }
-
-}  // extern "C"
-
-int xcp_internal_tn_tune(int knob, int v) {
-  int& k = knob == 6 ? g_tn_cfg : g_tn_wgs;
-  const int old = k;
-  if (knob == 6 && v >= 0 && v <= 2) k = v;
-  if (knob == 7 && v >= 8 && v <= 8192) k = v;
-  return old;
-}
-
-int xcp_internal_gemm_var(int v) {
-  const int old = g_nt256_var;
-  if (v >= 0 && v <= 13) g_nt256_var = v;
-  return old;
-}
-
-int xcp_internal_nt_grid(int v) {
-  const int old = g_nt_grid;
-  if (v >= 0 && v <= 4096) g_nt_grid = v;
-  return old;
-}
-
-int xcp_internal_gemm_tune(int cfg) {
-  const int old = g_nt_cfg;
-  if (cfg >= 0 && cfg <= 3) g_nt_cfg = cfg;
-  return old;
-}
-
-extern "C" {
+// rows of the stats partial array gemm_nt writes ([rows][2][N]): one per 128 output rows for
+// both tile sizes (the 256-row kernel writes one row per 128-row half)
+int xcp_gemm_nt_stat_rows(int M) { return xcp_cdiv(M, 128); }
 
 // Rows per split for xcp_gemm_tn (S = ceil(M / rows)): about one workgroup per CU for
 // the 256x256 kernel (each split's partial slab costs 4*N*K bytes of writes and
 // reads), ~1024 workgroups of the 128x128 kernel otherwise.
-int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K) {
+int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K, int tile) {
   if (M <= 0) return 64;
-  const bool big = tn_big(dtype, gmode, N, K);
-  const int tile = big ? 256 : 128, align = big ? 64 : 32;
-  const int tiles = xcp_cdiv(N, tile) * xcp_cdiv(K, tile);
-  const int target = big ? g_tn_wgs : 1024, min_rows = big ? 512 : 256;
+  const bool big = tn_big(dtype, gmode, N, K, tile);
+  const int tsz = big ? 256 : 128, align = big ? 64 : 32;
+  const int tiles = xcp_cdiv(N, tsz) * xcp_cdiv(K, tsz);
+  const int target = big ? TN_TARGET_WGS : 1024, min_rows = big ? 512 : 256;
   int S = target / (tiles > 0 ? tiles : 1);
   S = S < 1 ? 1 : S;
   const int smax = xcp_cdiv(M, min_rows);
@@ -1422,19 +913,17 @@ int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K) {
 
 // P[s][N][K] partial weight gradients; S splits of rows_per_split rows each.
 int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, float* P, int M, int N, int K, int S,
-                int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, hipStream_t stream) {
+                int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile,
+                hipStream_t stream) {
   if (N <= 0 || K <= 0 || S <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (ldg % 8) || (ldx % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 2 || (gmode == 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
+  if (tile < 0 || tile > 2) return XCP_EINVAL;
   TNArgs a{G, ldg, X, ldx, P, M, N, K, S, rows_per_split, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
-  if (tn_big(dtype, gmode, N, K)) {
+  if (tn_big(dtype, gmode, N, K, tile)) {
+    if (rows_per_split % 64) return XCP_EINVAL;
     const dim3 grid(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S);
-    if (g_nt256_var == 5) hipLaunchKernelGGL(gemm_tn256_kernel<1>, grid, dim3(512), 0, stream, a);
-    else if (g_nt256_var == 6) hipLaunchKernelGGL(gemm_tn256_kernel<2>, grid, dim3(512), 0, stream, a);
-    else if (g_nt256_var == 12) hipLaunchKernelGGL(gemm_tn256_kernel<3>, grid, dim3(512), 0, stream, a);
-    else if (g_nt256_var == 13) hipLaunchKernelGGL(gemm_tn256_kernel<4>, grid, dim3(512), 0, stream, a);
-    else if (g_tn_cfg == 1) hipLaunchKernelGGL(gemm_tn256_kernel<0>, grid, dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL(gemm_tn256r4_kernel, grid, dim3(512), 0, stream, a);
+    hipLaunchKernelGGL(gemm_tn256_kernel, grid, dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(N, 128) * xcp_cdiv(K, 128) * S;

@@ -438,35 +438,32 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(const float* __restr
   }
 }
 
-int g_lstm_kernel = 0;   // xcp_tune knob 9: 0 = register-resident / per-step kernels where H allows, 1 = generic
-
-bool lstm_reg(int H) { return g_lstm_kernel == 0 && (H == 128 || H == 64); }
+// Kernel choice (`kernel` argument: 0 = auto, 1 = the generic kernels, used by tests to pin
+// them at shapes the specialised kernels also cover).
+// register-resident: one 1024-thread workgroup per clip, W_hh slice in VGPRs
+bool lstm_reg(int H, int kernel) { return kernel == 0 && (H == 128 || H == 64); }
 // per-step kernels: H = 32 * KS for the instantiated KS, clips within the register partials
-bool lstm_step(int B, int H) {
+bool lstm_step(int B, int H, int kernel) {
   const size_t fwd_lds = ((size_t)B * 32 * (H / 32 + 4) + 8 * B) * sizeof(float);
   const size_t bwd_lds = ((size_t)8 * H + 2 * B) * sizeof(float);
-  return g_lstm_kernel == 0 && !lstm_reg(H) && (H == 256 || H == 512 || H == 1024) && B <= LS_MAXB &&
+  return kernel == 0 && !lstm_reg(H, kernel) && (H == 256 || H == 512 || H == 1024) && B <= LS_MAXB &&
          fwd_lds <= 65536 && bwd_lds <= 65536;
 }
 
 }  // namespace
 
-int xcp_internal_lstm_tune(int value) {
-  const int old = g_lstm_kernel;
-  if (value == 0 || value == 1) g_lstm_kernel = value;
-  return old;
-}
-
 
 extern "C" {
 
-// 1 when the recurrence runs on the generic kernels, which read the transposed W_hh
-int xcp_lstm_needs_whhT(int H) { return lstm_reg(H) || lstm_step(1, H) ? 0 : 1; }
+// 1 when xcp_lstm_fwd (same B, H, kernel) runs the generic kernel, which reads the transposed W_hh
+int xcp_lstm_needs_whhT(int B, int H, int kernel) { return lstm_reg(H, kernel) || lstm_step(B, H, kernel) ? 0 : 1; }
 
 int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
-                 float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, hipStream_t st) {
+                 float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, int kernel,
+                 hipStream_t st) {
   if (B <= 0 || T <= 0) return XCP_OK;
-  if (lstm_reg(H)) {
+  if (kernel < 0 || kernel > 1) return XCP_EINVAL;
+  if (lstm_reg(H, kernel)) {
     if (H == 128)
       hipLaunchKernelGGL(lstm_fwd_reg_kernel<128>, dim3(B), dim3(1024), 0, st, xproj, whh, bih, bhh, out, hprev, cst,
                          gates, hn, cn, T);
@@ -475,7 +472,7 @@ int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const 
                          gates, hn, cn, T);
     return (int)hipGetLastError();
   }
-  if (lstm_step(B, H)) {
+  if (lstm_step(B, H, kernel)) {
     const size_t smem = ((size_t)B * 32 * (H / 32 + 4) + 8 * B) * sizeof(float);
     for (int t = 0; t < T; ++t) {
       if (H == 256)
@@ -498,9 +495,10 @@ int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const 
 }
 
 int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const float* whh, const float* cst,
-                 const float* gates, float* dgates, float* work, int B, int T, int H, hipStream_t st) {
+                 const float* gates, float* dgates, float* work, int B, int T, int H, int kernel, hipStream_t st) {
   if (B <= 0 || T <= 0) return XCP_OK;
-  if (lstm_step(B, H)) {
+  if (kernel < 0 || kernel > 1) return XCP_EINVAL;
+  if (lstm_step(B, H, kernel)) {
     if (!work) return XCP_EINVAL;
     float* whhT = work + (long)B * H;
     hipLaunchKernelGGL(lstm_transpose_kernel, dim3(4 * H / 32, H / 32), dim3(256), 0, st, whh, whhT, H);
@@ -510,7 +508,7 @@ int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const fl
                          dgates, work, B, T, H, t);
     return (int)hipGetLastError();
   }
-  if (lstm_reg(H)) {
+  if (lstm_reg(H, kernel)) {
     if (H == 128)
       hipLaunchKernelGGL(lstm_bwd_reg_kernel<128>, dim3(B), dim3(1024), 0, st, dout, dhn, dcn, whh, cst, gates, dgates,
                          T);

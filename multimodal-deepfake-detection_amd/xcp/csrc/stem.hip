@@ -334,14 +334,9 @@ __global__ __launch_bounds__(256) void conv1_wgrad_tile_kernel(const float* __re
 }  // namespace
 
 namespace {
-int g_conv1_tile = 1;   // 1 = tiled conv1 kernels, 0 = per-pixel kernels (xcp_tune knob 8)
+// The tiled kernels stage input rows in LDS; frames wider than their 64 KB budget (IW > ~690)
+// fall back to the per-pixel kernels.
 constexpr int F1_TH = 4;
-}
-
-int xcp_internal_conv1_tune(int v) {
-  const int old = g_conv1_tile;
-  if (v == 0 || v == 1) g_conv1_tile = v;
-  return old;
 }
 
 extern "C" {
@@ -351,7 +346,7 @@ int xcp_conv1_fwd(int dtype, const float* X, const float* W, void* Y, int N, int
   const long total = (long)N * OH * OW * (C1 / 8);
   if (total <= 0) return XCP_OK;
   const size_t lds = ((size_t)3 * (2 * F1_TH + 1) * ((IW + 63) & ~63) + C1 * K1) * sizeof(float);
-  if (g_conv1_tile == 1 && lds <= 64 * 1024) {
+  if (lds <= 64 * 1024) {
     const unsigned blocks = (unsigned)(N * ((OH + F1_TH - 1) / F1_TH));
     if (dtype == XCP_BF16)
       hipLaunchKernelGGL((conv1_fwd_tile_kernel<bf16, F1_TH>), dim3(blocks), dim3(256), lds, st, X, W, (bf16*)Y, N, IH,
@@ -383,7 +378,7 @@ static size_t conv1_wgrad_lds(int dtype, int IW, int OW) {
 
 int xcp_conv1_wgrad_parts(int N, int IH, int IW) {
   const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
-  if (g_conv1_tile == 1 && conv1_wgrad_lds(XCP_F32, IW, OW) <= 64 * 1024) {
+  if (conv1_wgrad_lds(XCP_F32, IW, OW) <= 64 * 1024) {
     const int tiles = N * ((OH + W1_TH - 1) / W1_TH);
     return tiles < 1024 ? tiles : 1024;
   }
@@ -399,7 +394,7 @@ int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int 
   const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
   const long P = (long)N * OH * OW;
   const int blocks = xcp_conv1_wgrad_parts(N, IH, IW);
-  if (g_conv1_tile == 1 && conv1_wgrad_lds(XCP_F32, IW, OW) <= 64 * 1024) {
+  if (conv1_wgrad_lds(XCP_F32, IW, OW) <= 64 * 1024) {
     const size_t lds = conv1_wgrad_lds(dtype, IW, OW);
     if (dtype == XCP_BF16)
       hipLaunchKernelGGL(conv1_wgrad_tile_kernel<bf16>, dim3(blocks), dim3(256), lds, st, X, (const bf16*)dY, part, N, IH,

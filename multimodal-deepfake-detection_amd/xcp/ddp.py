@@ -9,89 +9,141 @@ of.  BatchNorm statistics stay per rank (the reference has no SyncBN); running
 buffers are broadcast from rank 0 before each forward (DDP ``broadcast_buffers``
 semantics).
 
-Buckets are launched asynchronously as soon as every gradient in them has been
-accumulated (post-accumulate-grad hooks): the head's (LSTM/FC) gradients arrive
-first, so their all-reduce runs on RCCL's stream while the fused backbone
-backward is still executing; the backbone buckets follow when the engine's
-backward returns.  Parameters are laid out in the flat buffer in reverse
-registration order so each bucket is contiguous.
+Overlap with backward.  Parameters sit in the flat buffer in reverse registration
+order, which is the order backward produces their gradients (head first, then the
+backbone from the exit flow down to the stem), and buckets are contiguous ranges of
+it.  A bucket's all-reduce is launched the moment its last gradient is final:
+
+* head parameters (LSTM / FC) report through post-accumulate-grad hooks;
+* backbone parameters report through the xcp engine's gradient sink
+  (``module=`` registers this object with every Xception engine inside the model):
+  the engine accumulates straight into the ``.grad`` views and calls ``ready`` after
+  each block, so the buckets of blocks 12 ... k are reduced while blocks k-1 ... 1
+  are still in backward.
+
+Which parameters take part is re-read at every ``zero()``: the reference trains with
+the backbone frozen for three epochs and then unfreezes it (train_visual.py:547-556);
+frozen parameters keep ``grad = None`` (so an optimiser skips them, as in the reference)
+and buckets only span parameters that require grad.
 """
 import torch
 import torch.distributed as dist
 
 
 class GradBuckets:
-    def __init__(self, params, bucket_bytes=64 << 20, world=None):
-        self.params = [p for p in params if p.requires_grad]
+    def __init__(self, params, bucket_bytes=25 << 20, world=None, module=None):
+        self.params = list(params)
+        if not self.params:
+            raise ValueError("GradBuckets: no parameters")
         self.world = world if world is not None else (dist.get_world_size() if dist.is_initialized() else 1)
+        self.bucket_elems = max(1, bucket_bytes // 4)
         dev = self.params[0].device
-        total = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
-        # reverse order: gradients of later layers are ready first
-        off = 0
+        self.flat = torch.zeros(sum(p.numel() for p in self.params), device=dev, dtype=torch.float32)
         self.views = {}
-        for p in reversed(self.params):
-            n = p.numel()
-            v = self.flat[off:off + n].view_as(p)
-            p.grad = v
-            self.views[p] = (off, n)
-            off += n
-        # contiguous buckets over the flat buffer
-        lim = max(1, bucket_bytes // 4)
-        self.buckets = []
-        start = 0
-        cur = 0
-        for p in reversed(self.params):
-            o, n = self.views[p]
-            if cur and cur + n > lim:
-                self.buckets.append((start, start + cur))
-                start, cur = o, 0
-            cur += n
-        if cur:
-            self.buckets.append((start, start + cur))
+        off = 0
+        for p in reversed(self.params):   # backward order
+            self.views[p] = (off, p.numel())
+            off += p.numel()
+        self.overlap = self.world > 1
+        self._active_key = None
         self._pending = []
-        self._left = []
-        self._bucket_of = {}
-        for bi, (a, b) in enumerate(self.buckets):
-            ps = [p for p in self.params if a <= self.views[p][0] < b]
-            self._left.append(len(ps))
+        self._hooked = set()
+        if module is not None:
+            self.attach(module)
+        self.zero()
+
+    # ------------------------------------------------------------ layout
+    def attach(self, module):
+        """Register as the gradient sink of every xcp Xception backbone inside ``module``."""
+        for m in module.modules():
+            if hasattr(m, "_xcp_grad_sink"):
+                m._xcp_grad_sink = self
+
+    def _layout(self):
+        """Buckets over the parameters that currently require grad: contiguous runs of the flat
+        buffer, split at bucket_elems."""
+        active = [p for p in reversed(self.params) if p.requires_grad]
+        self.active = active
+        self.buckets, self._bucket_of = [], {}
+        cur, start, end = [], None, None
+        for p in active:
+            o, n = self.views[p]
+            if cur and (o != end or end - start + n > self.bucket_elems):
+                self.buckets.append((start, end, cur))
+                cur = []
+            if not cur:
+                start = o
+            cur.append(p)
+            end = o + n
+        if cur:
+            self.buckets.append((start, end, cur))
+        for bi, (_, _, ps) in enumerate(self.buckets):
             for p in ps:
                 self._bucket_of[p] = bi
-        self._count = list(self._left)
-        self.overlap = self.world > 1
         if self.overlap:
-            for p in self.params:
-                p.register_post_accumulate_grad_hook(self._on_grad)
+            for p in active:
+                if p not in self._hooked:
+                    p.register_post_accumulate_grad_hook(self._on_grad)
+                    self._hooked.add(p)
+
+    # ------------------------------------------------------------ per step
+    def zero(self):
+        """Zero the flat gradient buffer, (re)attach the views and arm the buckets."""
+        key = tuple(p.requires_grad for p in self.params)
+        if key != self._active_key:
+            self._layout()
+            self._active_key = key
+        self.flat.zero_()
+        for p in self.params:
+            if not p.requires_grad:
+                p.grad = None
+                continue
+            o, n = self.views[p]
+            if p.grad is None or p.grad.data_ptr() != self.flat.data_ptr() + 4 * o:
+                p.grad = self.flat[o:o + n].view_as(p)
+        self._left = [len(ps) for _, _, ps in self.buckets]
+        self._done = set()
+        self._pending = []
+
+    def _launch(self, bi):
+        a, b, _ = self.buckets[bi]
+        self._pending.append(dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, async_op=True))
+
+    def ready(self, params, side_stream=None):
+        """Gradients of ``params`` are final (enqueued on the current stream, weight gradients
+        possibly on ``side_stream``).  Launches the all-reduce of every bucket this completes."""
+        if not self.overlap:
+            return
+        waited = False
+        for p in params:
+            if p in self._done or p not in self._bucket_of:
+                continue
+            self._done.add(p)
+            bi = self._bucket_of[p]
+            self._left[bi] -= 1
+            if self._left[bi] == 0:
+                if side_stream is not None and not waited:
+                    torch.cuda.current_stream().wait_stream(side_stream)
+                    waited = True
+                self._launch(bi)
 
     def _on_grad(self, p):
-        bi = self._bucket_of[p]
-        self._count[bi] -= 1
-        if self._count[bi] == 0:
-            a, b = self.buckets[bi]
-            self._pending.append(dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, async_op=True))
-
-    def zero(self):
-        self.flat.zero_()
-        self._count = list(self._left)
-        self._pending = []
-        for p in self.params:  # re-attach if an optimizer set grads to None
-            if p.grad is None or p.grad.data_ptr() != self.flat.data_ptr() + 4 * self.views[p][0]:
-                o, n = self.views[p]
-                p.grad = self.flat[o:o + n].view_as(p)
+        self.ready([p])
 
     def allreduce(self):
-        """Finish the gradient mean across ranks (no-op at world size 1).  Buckets whose
-        hooks did not fire (parameters without a gradient this step) are reduced here."""
+        """Finish the gradient mean across ranks (no-op at world size 1).  Buckets that did not
+        complete during backward (parameters without a gradient this step) are reduced here."""
         if self.world <= 1:
             return
-        for bi, (a, b) in enumerate(self.buckets):
-            if self._count[bi] != 0:
-                self._count[bi] = 0
-                self._pending.append(dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, async_op=True))
+        for bi in range(len(self.buckets)):
+            if self._left[bi] != 0:
+                self._left[bi] = 0
+                self._launch(bi)
         for w in self._pending:
             w.wait()
         self._pending = []
-        self.flat.mul_(1.0 / self.world)
+        for a, b, _ in self.buckets:
+            self.flat[a:b].mul_(1.0 / self.world)
 
 
 def broadcast_buffers(module, src=0):

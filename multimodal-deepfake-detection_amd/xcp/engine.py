@@ -15,6 +15,16 @@ kernels of ``libxcp.so`` and keeps activations NHWC in HBM:
 One engine serves one ``Xception`` module; it is driven through
 ``XceptionFunction`` so autograd sees a single node whose inputs are the frames and
 every backbone parameter.
+
+Gradient delivery has two modes:
+
+* default: the backward returns one fp32 gradient per parameter to autograd, which
+  accumulates it into ``param.grad`` (tensor hooks, post-accumulate-grad hooks,
+  ``torch.autograd.grad`` and ``backward(inputs=...)`` all behave as for any module);
+* gradient sink (``xcp.ddp.GradBuckets(..., module=model)`` registers one): the kernels
+  accumulate straight into the ``param.grad`` views of the sink's flat buffer and the
+  sink is told after each block which parameters are final, so it all-reduces a bucket
+  while the earlier blocks' backward is still running.
 """
 import os
 import math
@@ -118,6 +128,11 @@ class XceptionEngine:
         self._packed_bwd_key = None
         self._bufs = {}
         self._pack_fwd, self._pack_bwd = ops.PermuteBatch(), ops.PermuteBatch()
+
+    @property
+    def grad_sink(self):
+        """The gradient sink registered on the module (xcp.ddp.GradBuckets(module=...)), or None."""
+        return getattr(self.model, "_xcp_grad_sink", None)
 
     def _side_stream(self, dev):
         st = getattr(self, "_side", None)
@@ -231,6 +246,10 @@ class XceptionEngine:
         """x: [N,3,H,W] fp32 (NCHW, as XceptionLSTMV.extract_features feeds it).
         Returns (features [N,2048] fp32, saved-state dict for backward)."""
         ops.check_gpu(x)
+        with ops.device_guard(x):
+            return self._forward(x, train)
+
+    def _forward(self, x, train):
         self.device = x.device
         x = x.contiguous().float()
         N, C0, IH, IW = x.shape
@@ -320,21 +339,38 @@ class XceptionEngine:
         return out, OH, OW, bs
 
     # ------------------------------------------------------------ backward
-    def backward(self, S, dfeat):
-        """dfeat [N,2048] fp32 -> {param name: fp32 grad tensor} for every backbone parameter."""
+    def backward(self, S, dfeat, out=None, notify=None):
+        """dfeat [N,2048] fp32 -> backbone parameter gradients.
+
+        out None: returns {param name: fresh fp32 gradient}.  out {name: tensor}: the
+        gradients of those parameters are ADDED to the given tensors (param.grad views);
+        others are returned fresh.  notify(names, side_stream): called after the kernels
+        that produce the gradients of ``names`` are enqueued (side_stream: the stream the
+        weight gradients run on, or None)."""
         if not S["train"]:
             raise RuntimeError("xcp engine backward needs a train-mode forward (batch-stat BatchNorm)")
+        with ops.device_guard(dfeat):
+            return self._backward(S, dfeat, out, notify)
+
+    def _backward(self, S, dfeat, out, notify):
         pk = self.pack_bwd()
         m = self.model
         N = S["N"]
         dev = self.device
         grads = {}
         dfeat = dfeat.contiguous().float()
+        out = out or {}
+        pending = []
 
         def g(name, shape):
+            """(gradient tensor of parameter ``name``, accumulate into it?)"""
+            pending.append(name)
+            t = out.get(name)
+            if t is not None:
+                return t, True
             t = torch.empty(shape, device=dev, dtype=torch.float32)
             grads[name] = t
-            return t
+            return t, False
 
         # Pointwise weight gradients run on a side stream: they depend only on dY (and a saved
         # activation), nothing downstream waits for them until the backward returns, so they
@@ -342,40 +378,48 @@ class XceptionEngine:
         main = torch.cuda.current_stream(dev)
         side = self._side_stream(dev) if WGRAD_SIDE_STREAM else None
 
-        def wgrad(*args, **kw):
+        def wgrad(G, X, M, Nn, K, name, shape, **kw):
+            dst, acc = g(name, shape)
             if side is None:
-                ops.weight_grad(*args, **kw)
+                ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, **kw)
                 return
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                ops.weight_grad(*args, **kw)
-            for t in (args[0], args[1], args[5]):   # G, X, out: kept alive for the side stream
+                ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, **kw)
+            for t in (G, X, dst):   # kept alive for the side stream
                 t.record_stream(side)
 
-        def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False, pool=None):
+        def done():
+            """every gradient requested since the last call is enqueued: tell the sink"""
+            if notify is not None and pending:
+                notify(list(pending), side)
+            pending.clear()
+
+        def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
             dY = self._empty(rows * C)
             P = part[1] if part is not None else 0
-            ops.bn_backward(dZ, Y, rows, C, _bn_ref(bnmod), st, dY, g(name + ".weight", (C,)), g(name + ".bias", (C,)),
-                            part=part[0] if part is not None else None, R=P, relu=relu, pool=pool)
+            (gw, acc), (gb, acc_b) = g(name + ".weight", (C,)), g(name + ".bias", (C,))
+            if acc != acc_b:
+                raise NotImplementedError(f"xcp engine: {name}.weight and .bias must both (or neither) require grad")
+            ops.bn_backward(dZ, Y, rows, C, _bn_ref(bnmod), st, dY, gw, gb, part=part[0] if part is not None else None,
+                            R=P, relu=relu, accumulate=acc)
             return dY
 
-        def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None,
-                     pool=None):
+        def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None):
             """dZ: gradient w.r.t. this unit's BN output (``part``: its fused BN-backward
-            partial sums, if the producer emitted them; ``pool``: (dOut, amax, N, H, W) when
-            dZ is the max-pool backward of dOut, gathered on the fly).  Returns (gradient
-            w.r.t. the depthwise input after the activation mask (+ residual / skip terms),
-            and -- when ``prev_st`` is the Stats of the BN feeding this unit -- that BN's
-            backward partial sums)."""
+            partial sums, if the producer emitted them).  Returns (gradient w.r.t. the
+            depthwise input after the activation mask (+ residual / skip terms), and -- when
+            ``prev_st`` is the Stats of the BN feeding this unit -- that BN's backward partial
+            sums)."""
             M = N * H * W
-            dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part, pool=pool)
+            dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
             dD = self._empty(M * u.cin)
             ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, u.cin, u.cout)
-            wgrad(dY, rec["d"], M, u.cout, u.cin, g(u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1)))
+            wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
             dX = self._empty(M * u.cin)
-            bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX,
-                             g(u.name + ".conv1.weight", (u.cin, 1, 3, 3)), N, H, W, u.cin, dRes=dRes, dSkip=dSkip,
-                             skip_geom=skip_geom, bn_stats=prev_st)
+            dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
+            bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
+                             u.cin, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, bn_stats=prev_st, accumulate=acc)
             return dX, (bnp if prev_st is not None else None)
 
         # ---- exit flow
@@ -387,9 +431,11 @@ class XceptionEngine:
         ops.avgpool_bwd(dfeat, e4["y"], e4["st"].scale, e4["st"].shift, dZ4, N, H * W, 2048)
         dZ3, p3 = unit_bwd(u4, e4, dZ4, H, W, prev_st=e3["st"])
         dX, _ = unit_bwd(u3, e3, dZ3, H, W, part=p3)
+        done()
         # ---- blocks, last to first
         for b, bs in zip(reversed(self.blocks), reversed(S["blocks"])):
-            dX = self._block_bwd(b, bs, dX, N, pk, g, bn_bwd, unit_bwd, wgrad)
+            dX = self._block_bwd(b, bs, dX, N, pk, bn_bwd, unit_bwd, wgrad)
+            done()
         # ---- stem
         OH1, OW1, OH2, OW2 = S["OH1"], S["OW1"], S["OH2"], S["OW2"]
         rows1, rows2 = N * OH1 * OW1, N * OH2 * OW2
@@ -404,22 +450,28 @@ class XceptionEngine:
             ops.conv3x3_wgrad(dC2, S["a1"], w2g, N, OH1, OW1)
         else:
             ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
-        ops.permute3(w2g, g("conv2.weight", (64, 32, 3, 3)), 64, 9, 32, (0, 2, 1))
+        c2g, acc = g("conv2.weight", (64, 32, 3, 3))
+        if acc:
+            tmp = torch.empty_like(c2g)
+            ops.permute3(w2g, tmp, 64, 9, 32, (0, 2, 1))
+            c2g.add_(tmp)
+        else:
+            ops.permute3(w2g, c2g, 64, 9, 32, (0, 2, 1))
         dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], relu=True)   # relu (Xception.py:170) fused
-        ops.conv1_wgrad(S["x"], dC1, g("conv1.weight", (32, 3, 3, 3)), N, S["IH"], S["IW"])
+        c1g, acc = g("conv1.weight", (32, 3, 3, 3))
+        ops.conv1_wgrad(S["x"], dC1, c1g, N, S["IH"], S["IW"], accumulate=acc)
         if side is not None:
             main.wait_stream(side)
+        done()
         return grads
 
-    def _block_bwd(self, b, bs, dOut, N, pk, g, bn_bwd, unit_bwd, wgrad):
+    def _block_bwd(self, b, bs, dOut, N, pk, bn_bwd, unit_bwd, wgrad):
         H, W, OH, OW = bs["H"], bs["W"], bs["OH"], bs["OW"]
         Ms = N * OH * OW
         units = bs["units"]
         # pooled block: one pass materialises the max-pool gradient (per-quad gather) and
         # reduces it for the last unit's BN backward (1.50 vs 1.58 ms with a separate reduce
-        # at 147^2 x 128).  Gathering it inside the BN-backward kernels instead --
-        # ops.bn_backward(pool=...) -- measured slower: 1.83 / 1.88 ms.
-        pool = None
+        # at 147^2 x 128; gathering it inside the BN-backward kernels measured 1.83 / 1.88 ms)
         part = None
         if b.pool:
             dZ = self._empty(N * H * W * b.cout)
@@ -430,9 +482,8 @@ class XceptionEngine:
         skip_geom = (0, 0, 1)
         if b.skip is not None:
             dYs = bn_bwd(b.skipbn, b.name + ".skipbn", dOut, bs["ys"], Ms, b.cout, bs["sks"])
-            wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, g(b.name + ".skip.weight", (b.cout, b.cin, 1, 1)),
-                            gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0),
-                            ldx=b.cin)
+            wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1),
+                  gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0), ldx=b.cin)
             dXs = self._empty(Ms * b.cin)
             ops.gemm_nt(dYs, pk[b.name + ".skipT"], dXs, Ms, b.cin, b.cout)
             if b.stride != 1:
@@ -443,11 +494,10 @@ class XceptionEngine:
             dRes = dOut
         for i in range(len(b.units) - 1, -1, -1):
             u, rec = b.units[i], units[i]
-            src = pool if i == len(b.units) - 1 else None
             if i > 0:
-                dZ, part = unit_bwd(u, rec, dZ, H, W, part=part, prev_st=units[i - 1]["st"], pool=src)
+                dZ, part = unit_bwd(u, rec, dZ, H, W, part=part, prev_st=units[i - 1]["st"])
             else:
-                dZ, _ = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, part=part, pool=src)
+                dZ, _ = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, part=part)
         return dZ
 
 
@@ -467,25 +517,23 @@ class XceptionFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dfeat):
-        """Accumulates the backbone gradients into ``param.grad`` itself -- one fused
-        ``_foreach_add_`` for all of them (a parameter without a gradient takes the engine's
-        tensor) -- and returns None for the parameters, instead of handing ~170 tensors to
-        autograd's per-parameter accumulation (one add kernel each, ~0.8 ms per step).
-        Post-accumulate-grad hooks therefore do not fire for backbone parameters; xcp.ddp
-        reduces such buckets in ``GradBuckets.allreduce``."""
-        grads = ctx.engine.backward(ctx.S, dfeat)
-        ctx.S = None
-        acc, new = [], []
-        for n, need, p in zip(ctx.names, ctx.needs, ctx.params):
-            gt = grads.get(n) if need else None
-            if gt is None:
-                continue
-            if p.grad is None:
-                p.grad = gt
-            else:
-                acc.append(p.grad)
-                new.append(gt)
-        if acc:
-            torch._foreach_add_(acc, new)
-        ctx.params = None
+        eng = ctx.engine
+        sink = eng.grad_sink
+        need = {n for n, nd in zip(ctx.names, ctx.needs) if nd}
+        if sink is None:
+            # default: hand the gradients to autograd (hooks and autograd.grad behave as usual)
+            grads = eng.backward(ctx.S, dfeat)
+            ctx.S = ctx.params = None
+            return (None, None, None, *[grads.get(n) if n in need else None for n in ctx.names])
+        # gradient sink: accumulate straight into the sink's param.grad views, block by block
+        out = {}
+        for n, p in zip(ctx.names, ctx.params):
+            if n in need:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                out[n] = p.grad
+        by_name = dict(zip(ctx.names, ctx.params))
+        eng.backward(ctx.S, dfeat, out=out,
+                     notify=lambda names, side: sink.ready([by_name[n] for n in names if n in need], side))
+        ctx.S = ctx.params = None
         return (None, None, None, *([None] * len(ctx.names)))

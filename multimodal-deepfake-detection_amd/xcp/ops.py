@@ -19,7 +19,17 @@ def _p(t):
 
 
 def stream():
+    """The current HIP stream of the current device (callers enter ``device_guard`` first, so
+    that is the device of the tensors the call works on)."""
     return torch.cuda.current_stream().cuda_stream
+
+
+def device_guard(t):
+    """Sets (and restores) the current device to ``t``'s for the duration of a block of launches:
+    kernels are launched on the calling thread's current device and stream, and the reference
+    calls these ops from the autograd engine's per-device threads and from
+    nn.DataParallel.parallel_apply threads (train_audio.py:18, :38)."""
+    return torch.cuda.device(t.device)
 
 
 class KernelTimer:
@@ -78,49 +88,46 @@ def check_gpu(*ts):
 
 
 # ---------------------------------------------------------------- GEMM
-def gemm_nt(A, B, C, M, N, K, lda=None, ldb=None, ldc=None, stats=None, gather=(0, 0, 0, 0, 0, 1, 0)):
+def gemm_nt(A, B, C, M, N, K, lda=None, ldb=None, ldc=None, stats=None, gather=(0, 0, 0, 0, 0, 1, 0), tile=0):
+    """C[M,N] = A[M,K] B[N,K]^T (+ BN partial sums); tile 0 auto, 1 = 128x128, 2 = 256x256."""
     dt = DT[A.dtype]
     with _timed("gemm_nt", {"M": M, "N": N, "K": K, "stats": stats}):
         _lib.call("xcp_gemm_nt", dt, _p(A), lda or K, _p(B), ldb or K, _p(C), ldc or N, M, N, K, _p(stats), *gather,
-                  stream())
+                  tile, stream())
 
 
-def gemm_tn(G, X, P, M, N, K, S, rows_per_split, ldg=None, ldx=None, gather=(0, 0, 0, 0, 0, 1, 0)):
+def gemm_tn(G, X, P, M, N, K, S, rows_per_split, ldg=None, ldx=None, gather=(0, 0, 0, 0, 0, 1, 0), tile=0):
     dt = DT[G.dtype]
     _lib.call("xcp_gemm_tn", dt, _p(G), ldg or N, _p(X), ldx or K, _p(P), M, N, K, S, rows_per_split, *gather,
-              stream())
+              tile, stream())
 
 
 def nt_stat_rows(M):
     return _lib.call("xcp_gemm_nt_stat_rows", M)
 
 
-def colreduce_f64(inp, S, L, out, G):
-    _lib.call("xcp_colreduce_f64", _p(inp), S, L, _p(out), G, stream())
+def colreduce_f32(inp, S, L, out, G, accumulate=False):
+    _lib.call("xcp_colreduce_f32", _p(inp), S, L, _p(out), G, 1 if accumulate else 0, stream())
 
 
-def colreduce_f32(inp, S, L, out, G):
-    _lib.call("xcp_colreduce_f32", _p(inp), S, L, _p(out), G, stream())
-
-
-def reduce_slabs(P, S, L, out):
-    """out[L] = sum_s P[s][L] (fp32, deterministic, two levels when S is large)."""
+def reduce_slabs(P, S, L, out, accumulate=False):
+    """out[L] (+)= sum_s P[s][L] (fp32, deterministic, two levels when S is large)."""
     if S > 64:
         g = 32
         tmp = torch.empty(g * L, device=P.device, dtype=torch.float32)
         colreduce_f32(P, S, L, tmp, g)
-        colreduce_f32(tmp, g, L, out, 1)
+        colreduce_f32(tmp, g, L, out, 1, accumulate)
     else:
-        colreduce_f32(P, S, L, out, 1)
+        colreduce_f32(P, S, L, out, 1, accumulate)
 
 
-def weight_grad(G, X, M, N, K, out, gather=(0, 0, 0, 0, 0, 1, 0), ldg=None, ldx=None):
-    """out[N][K] (fp32) = G[M][N]^T X[M][K]."""
-    rps = _lib.call("xcp_gemm_tn_rows_per_split", DT[G.dtype], gather[0], M, N, K)
+def weight_grad(G, X, M, N, K, out, gather=(0, 0, 0, 0, 0, 1, 0), ldg=None, ldx=None, tile=0, accumulate=False):
+    """out[N][K] (fp32) (+)= G[M][N]^T X[M][K]."""
+    rps = _lib.call("xcp_gemm_tn_rows_per_split", DT[G.dtype], gather[0], M, N, K, tile)
     S = (M + rps - 1) // rps
     P = torch.empty(S * N * K, device=G.device, dtype=torch.float32)
-    gemm_tn(G, X, P, M, N, K, S, rps, ldg=ldg, ldx=ldx, gather=gather)
-    reduce_slabs(P, S, N * K, out)
+    gemm_tn(G, X, P, M, N, K, S, rps, ldg=ldg, ldx=ldx, gather=gather, tile=tile)
+    reduce_slabs(P, S, N * K, out, accumulate)
 
 
 # ---------------------------------------------------------------- depthwise
@@ -130,9 +137,10 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
 
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
-           bn_stats=None):
+           bn_stats=None, accumulate=False):
     """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
-    (that BN's Stats) is given, else (None, 0)."""
+    (that BN's Stats) is given, else (None, 0).  dW_out receives the weight gradient in the
+    nn.Conv2d [C][1][3][3] order (accumulate: added to it)."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
     bnpart = None
@@ -142,7 +150,7 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
               skip_geom[0], skip_geom[1], skip_geom[2], _p(dX), _p(part), _p(bnpart),
               _p(bn_stats["mean"]) if bn_stats is not None else 0,
               _p(bn_stats["invstd"]) if bn_stats is not None else 0, N, H, W, C, stream())
-    reduce_slabs(part, P, C * 9, dW_out)
+    reduce_slabs(part, P, C * 9, dW_out, accumulate)
     return bnpart, (P if bnpart is not None else 0)
 
 
@@ -193,41 +201,28 @@ def row_stats(X, rows, C):
     return part, R
 
 
-def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=False, pool=None):
-    """dY = BatchNorm2d backward (train-mode batch stats) of dZ; writes dgamma/dbeta.
+def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False):
+    """dY = BatchNorm2d backward (train-mode batch stats) of dZ; writes (accumulate: adds to)
+    dgamma/dbeta.
     ``part`` ([R][2][C] partial (sum dz, sum dz*zhat)) may come fused from the
     producer of dZ; otherwise it is reduced here.  relu=True: dZ is the gradient of
-    relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift).
-    pool=(dOut, amax, N, H, W): the gradient is the MaxPool2d(3,2,1) backward of dOut,
-    gathered inside the reduce kernel; with dZ None it is gathered again by the apply
-    kernel (never materialised), otherwise the reduce also stores it into dZ (an output
-    buffer) and the apply reads it back."""
+    relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift)."""
     ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
-    if pool is not None and (relu or part is not None):
-        raise ValueError("pool gradient source excludes part and relu")
     dev, dt = Y.device, Y.dtype
     if part is None:
         R = _lib.call("xcp_chanred_parts", rows, C)
         part = torch.empty(R * 2 * C, device=dev, dtype=torch.float32)
-        if pool is not None:
-            dOut, amax, N, H, W = pool
-            _lib.call("xcp_bn_bwd_reduce_pool", DT[dt], _p(dOut), _p(amax), _p(Y), _p(st["mean"]), _p(st["invstd"]),
-                      N, H, W, C, _p(part), _p(dZ), stream())
-        else:
-            _lib.call("xcp_bn_bwd_reduce", DT[dt], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), ms, mt, rows, C,
-                      _p(part), stream())
+        _lib.call("xcp_bn_bwd_reduce", DT[dt], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), ms, mt, rows, C,
+                  _p(part), stream())
     elif relu:
         raise ValueError("a fused partial cannot carry the ReLU mask")
     coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
     part, R = _fold(part, R, C)
     _lib.call("xcp_bn_bwd_finalize_part", _p(part), R, C, float(rows), _p(bn["weight"]), _p(st["mean"]),
-              _p(st["invstd"]), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta), stream())
-    if pool is not None and dZ is None:
-        _lib.call("xcp_bn_bwd_apply_pool", DT[dt], _p(dOut), _p(amax), _p(Y), _p(dY), _p(coef), _p(coef[C:]),
-                  _p(coef[2 * C:]), N, H, W, C, stream())
-    else:
-        _lib.call("xcp_bn_bwd_apply", DT[dt], _p(dZ), _p(Y), _p(dY), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), ms,
-                  mt, rows, C, stream())
+              _p(st["invstd"]), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta),
+              1 if accumulate else 0, stream())
+    _lib.call("xcp_bn_bwd_apply", DT[dt], _p(dZ), _p(Y), _p(dY), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), ms,
+              mt, rows, C, stream())
 
 
 def bn_act(X, Y, scale, shift, relu, rows, C):
@@ -270,11 +265,11 @@ def conv1_fwd(X, W, Y, N, IH, IW):
     _lib.call("xcp_conv1_fwd", DT[Y.dtype], _p(X), _p(W), _p(Y), N, IH, IW, stream())
 
 
-def conv1_wgrad(X, dY, out, N, IH, IW):
+def conv1_wgrad(X, dY, out, N, IH, IW, accumulate=False):
     R = _lib.call("xcp_conv1_wgrad_parts", N, IH, IW)
     part = torch.empty(R * 32 * 27, device=X.device, dtype=torch.float32)
     _lib.call("xcp_conv1_wgrad", DT[dY.dtype], _p(X), _p(dY), _p(part), N, IH, IW, stream())
-    reduce_slabs(part, R, 32 * 27, out)
+    reduce_slabs(part, R, 32 * 27, out, accumulate)
 
 
 def frames_u8_to_f32(frames, lengths, out):
@@ -363,17 +358,19 @@ class PermuteBatch:
 
 
 # ---------------------------------------------------------------- LSTM
-def lstm_needs_whhT(H):
-    return _lib.call("xcp_lstm_needs_whhT", H) != 0
+# kernel: 0 = automatic (register-resident for H 64 / 128, per-step kernels for H 256-1024),
+# 1 = the generic kernels (tests pin them at shapes the specialised kernels also cover)
+def lstm_needs_whhT(B, H, kernel=0):
+    return _lib.call("xcp_lstm_needs_whhT", B, H, kernel) != 0
 
 
-def lstm_fwd(xproj, whh, whhT, bih, bhh, out, hprev, cst, gates, hn, cn, B, T, H):
+def lstm_fwd(xproj, whh, whhT, bih, bhh, out, hprev, cst, gates, hn, cn, B, T, H, kernel=0):
     _lib.call("xcp_lstm_fwd", _p(xproj), _p(whh), _p(whhT), _p(bih), _p(bhh), _p(out), _p(hprev), _p(cst), _p(gates), _p(hn),
-              _p(cn), B, T, H, stream())
+              _p(cn), B, T, H, kernel, stream())
 
 
-def lstm_bwd(dout, dhn, dcn, whh, cst, gates, dgates, B, T, H):
+def lstm_bwd(dout, dhn, dcn, whh, cst, gates, dgates, B, T, H, kernel=0):
     # per-step kernels: cell-gradient carry [B][H] + W_hh^T [H][4H]
     work = torch.empty(B * H + 4 * H * H, device=whh.device, dtype=torch.float32)
     _lib.call("xcp_lstm_bwd", _p(dout), _p(dhn), _p(dcn), _p(whh), _p(cst), _p(gates), _p(dgates), _p(work), B, T, H,
-              stream())
+              kernel, stream())

@@ -1,11 +1,23 @@
-"""Fused gradient clipping + Adam for the training step (train_visual.py:575-577,
-train_audio.py:40-44): ``clip_grad_norm_(params, max_norm)`` followed by
+"""Fused gradient clipping + Adam for the training step (train_visual.py:533, :575-577;
+train_audio.py:21, :40-44): ``clip_grad_norm_(params, max_norm)`` followed by
 ``torch.optim.Adam(params, lr, betas, eps, weight_decay)`` in two HIP launches over a chunk
 table of every parameter (csrc/optim.hip), with the clip coefficient kept on the device.
 
-Same update as torch's Adam (L2 weight decay, bias correction, no amsgrad).  Differences:
-``param.grad`` keeps the unclipped gradient (clipping is applied inside the update), and
-``step()`` returns the pre-clip total norm as a 0-d device tensor, as clip_grad_norm_ does.
+A ``torch.optim.Optimizer``: ``param_groups`` (so ReduceLROnPlateau / OneCycleLR adjust
+``lr``), per-parameter ``state`` with torch Adam's keys (``step``, ``exp_avg``,
+``exp_avg_sq``; checkpoints interchange with torch.optim.Adam), ``zero_grad``,
+``state_dict`` / ``load_state_dict``, and ``GradScaler.step`` (which unscales the grads
+of ``param_groups`` before calling ``step``).  As torch Adam, parameters whose ``grad`` is
+None are skipped, so a backbone that is frozen when the optimiser is built (the
+reference's first three epochs, train_visual.py:547-553) starts training when it is
+unfrozen.
+
+Same update as torch's Adam (L2 weight decay, bias correction from each parameter's own
+step count, no amsgrad / maximize).  With ``max_norm`` the gradients are clipped to that
+total norm inside the update; ``param.grad`` keeps the unclipped gradient and ``step()``
+returns the pre-clip total norm as a fresh 0-d device tensor (clip_grad_norm_'s return).
+Without ``max_norm`` the script's own clip_grad_norm_ call does the clipping (as the
+reference scripts do) and ``step()`` returns None.
 """
 import math
 
@@ -16,54 +28,88 @@ from . import _lib, ops
 CHUNK = 16384
 
 
-class FusedAdamClip:
+class FusedAdamClip(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_norm=None):
-        self.params = [p for p in params if p.requires_grad]
-        for p in self.params:
-            if p.dtype != torch.float32 or not p.is_contiguous():
-                raise ValueError("FusedAdamClip: fp32 contiguous parameters only")
-        ops.check_gpu(*self.params)
-        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        if lr < 0.0 or eps < 0.0 or weight_decay < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError("FusedAdamClip: invalid hyper-parameter")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        for grp in self.param_groups:
+            for p in grp["params"]:
+                if p.dtype != torch.float32 or not p.is_contiguous():
+                    raise ValueError("FusedAdamClip: fp32 contiguous parameters only")
+                ops.check_gpu(p)
         self.max_norm = max_norm
-        self.t = 0
-        self.exp_avg = [torch.zeros_like(p) for p in self.params]
-        self.exp_avg_sq = [torch.zeros_like(p) for p in self.params]
-        dev = self.params[0].device
-        self._out = torch.zeros(2, device=dev, dtype=torch.float32)
-        self._key = None
-        self._tab = None
-        self._part = None
+        self._tables = {}
+        self._out = None
 
-    def _table(self):
-        key = tuple(p.grad.data_ptr() if p.grad is not None else 0 for p in self.params)
-        if key != self._key:
-            rows = []
-            for p, m, v in zip(self.params, self.exp_avg, self.exp_avg_sq):
-                if p.grad is None:
-                    continue
-                g = p.grad
+    def _state(self, p):
+        st = self.state[p]
+        if not st:
+            st["step"] = torch.tensor(0.0)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        return st
+
+    def _table(self, key, rows, dev):
+        """device chunk table for a list of (param, grad, exp_avg, exp_avg_sq), cached by pointers"""
+        tab = self._tables.get(key)
+        if tab is None:
+            r = []
+            for p, g, m, v in rows:
                 if g.dtype != torch.float32 or not g.is_contiguous():
                     raise ValueError("FusedAdamClip: fp32 contiguous gradients only")
                 n = p.numel()
                 for s in range(0, n, CHUNK):
-                    rows.append([p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), s, min(CHUNK, n - s)])
-            self._tab = torch.tensor(rows, dtype=torch.int64).to(self.params[0].device)
-            self._part = torch.empty(len(rows), device=self.params[0].device, dtype=torch.float32)
-            self._key = key
-        return self._tab
+                    r.append([p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), s, min(CHUNK, n - s)])
+            tab = torch.tensor(r, dtype=torch.int64).to(dev)
+            if len(self._tables) > 64:
+                self._tables.clear()
+            self._tables[key] = tab
+        return tab
 
     @torch.no_grad()
-    def step(self):
-        tab = self._table()
-        n = tab.shape[0]
-        s = ops.stream()
-        coef = 0
-        if self.max_norm is not None:
-            _lib.call("xcp_opt_sumsq", tab.data_ptr(), n, self._part.data_ptr(), float(self.max_norm),
-                      self._out.data_ptr(), s)
-            coef = self._out.data_ptr()
-        self.t += 1
-        b1, b2 = self.betas
-        _lib.call("xcp_opt_adam", tab.data_ptr(), n, coef, float(self.lr), float(b1), float(b2), float(self.eps),
-                  float(self.wd), float(1.0 - b1 ** self.t), float(math.sqrt(1.0 - b2 ** self.t)), s)
-        return self._out[1]
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        # parameters with a gradient, grouped by (param group, step count) for the bias corrections
+        launches, every = [], []
+        for gi, grp in enumerate(self.param_groups):
+            by_step = {}
+            for p in grp["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("FusedAdamClip does not support sparse gradients")
+                st = self._state(p)
+                st["step"] += 1
+                row = (p, p.grad, st["exp_avg"], st["exp_avg_sq"])
+                by_step.setdefault(int(st["step"].item()), []).append(row)
+                every.append(row)
+            for t, rows in by_step.items():
+                launches.append((grp, t, rows))
+        if not every:
+            return loss
+        dev = every[0][0].device
+        with ops.device_guard(every[0][0]):
+            s = ops.stream()
+            coef = 0
+            if self.max_norm is not None:
+                key = ("all",) + tuple(r[0].data_ptr() * 31 + r[1].data_ptr() for r in every)
+                tab = self._table(key, every, dev)
+                part = torch.empty(tab.shape[0], device=dev, dtype=torch.float32)
+                self._out = torch.empty(2, device=dev, dtype=torch.float32)
+                _lib.call("xcp_opt_sumsq", tab.data_ptr(), tab.shape[0], part.data_ptr(), float(self.max_norm),
+                          self._out.data_ptr(), s)
+                coef = self._out.data_ptr()
+            for grp, t, rows in launches:
+                key = ("grp",) + tuple(r[0].data_ptr() * 31 + r[1].data_ptr() for r in rows)
+                tab = self._table(key, rows, dev)
+                b1, b2 = grp["betas"]
+                _lib.call("xcp_opt_adam", tab.data_ptr(), tab.shape[0], coef, float(grp["lr"]), float(b1), float(b2),
+                          float(grp["eps"]), float(grp["weight_decay"]), float(1.0 - b1 ** t),
+                          float(math.sqrt(1.0 - b2 ** t)), s)
+        if loss is not None:
+            return loss
+        return self._out[1].clone() if self.max_norm is not None else None

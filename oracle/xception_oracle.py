@@ -153,10 +153,45 @@ def audio_frames(x):
     return F.interpolate(x.reshape(B * T, c, n, 1), size=(64, 64), mode="bilinear", align_corners=False)
 
 
-def clip_step(sd, clips, labels, unfrozen, audio=False):
+def clip_grad_norm(grads, max_norm):
+    """torch.nn.utils.clip_grad_norm_ (train_visual.py:575): total 2-norm of all gradients (a norm
+    of per-tensor norms, fp32), scale by min(1, max_norm / (total + 1e-6)).  Returns the total."""
+    gs = [g for g in grads if g is not None]
+    total = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g) for g in gs]))
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    for g in gs:
+        g.mul_(coef)
+    return total
+
+
+def adam_step(params, grads, state, lr, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+    """torch.optim.Adam (single-tensor form, L2 weight decay, no amsgrad) restated
+    (train_visual.py:533, :576; train_audio.py:21, :44).  params / grads / state are dicts keyed
+    by parameter name; parameters without a gradient are skipped, as torch does."""
+    b1, b2 = betas
+    with torch.no_grad():
+        for k, p in params.items():
+            g = grads.get(k)
+            if g is None:
+                continue
+            if weight_decay:
+                g = g.add(p, alpha=weight_decay)
+            st = state.setdefault(k, {"step": 0, "exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)})
+            st["step"] += 1
+            t = st["step"]
+            st["exp_avg"].lerp_(g, 1 - b1)
+            st["exp_avg_sq"].mul_(b2).addcmul_(g, g.conj(), value=1 - b2)
+            bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+            denom = (st["exp_avg_sq"].sqrt() / math.sqrt(bc2)).add_(eps)
+            p.addcdiv_(st["exp_avg"], denom, value=-lr / bc1)
+
+
+def clip_step(sd, clips, labels, unfrozen, audio=False, optim=None):
     """One train step of the clip model (train_audio.py:33-44 / train_visual.py BCE variant):
-    backbone in train mode, head dropout inactive, BCE loss, backward.
-    Returns dict(features, prob, logits, loss, grads{name: tensor}, stats{buffer: tensor})."""
+    backbone in train mode, head dropout inactive, BCE loss, backward; with ``optim`` =
+    dict(lr, weight_decay, max_norm (or None)) also clip_grad_norm_ + one Adam step.
+    Returns dict(features, prob, logits, loss, grads{name: tensor}, stats{buffer: tensor},
+    params{name: tensor after the step})."""
     params = {k: v.detach().clone() for k, v in sd.items()}
     train_keys = [k for k in params if k.startswith(("lstm.", "fc_layers.", "fc_out."))]
     if unfrozen:
@@ -172,8 +207,12 @@ def clip_step(sd, clips, labels, unfrozen, audio=False):
     loss = F.binary_cross_entropy(prob, labels)
     loss.backward()
     grads = {k: params[k].grad for k in train_keys}
+    if optim is not None:
+        if optim.get("max_norm") is not None:
+            clip_grad_norm(list(grads.values()), optim["max_norm"])
+        adam_step({k: params[k] for k in train_keys}, grads, {}, optim["lr"], weight_decay=optim.get("weight_decay", 0.0))
     return dict(features=feats.detach(), prob=prob.detach(), logits=logits.detach(), loss=loss.detach(),
-                grads=grads, stats=stats)
+                grads=grads, stats=stats, params=params)
 
 
 def kaiming_like_init(shape, out_channels, kh, kw, gen):

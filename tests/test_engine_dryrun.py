@@ -6,15 +6,28 @@ that every pointer argument addresses a live tensor large enough for the
 extents the call implies where cheap to infer.  This exercises the whole
 forward/backward call sequence of the XceptionLSTMV step on CPU in seconds.
 """
+import contextlib
 import ctypes
+import os
 
 import pytest
 import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
 import torch.nn as nn
 
+# value the fake kernels write into every gradient they produce (rank-dependent under gloo)
+FILL = {"v": 1.0}
 
-@pytest.fixture
-def fake_lib(monkeypatch):
+
+def _fill(ptr, n, acc):
+    """write (acc: add) FILL into n fp32 elements at a host address (dry-run tensors are CPU)"""
+    a = (ctypes.c_float * n).from_address(ptr)
+    for i in range(n):
+        a[i] = (a[i] if acc else 0.0) + FILL["v"]
+
+
+def install_fake_lib(monkeypatch):
     from xcp import _lib, ops
     calls = []
 
@@ -24,6 +37,13 @@ def fake_lib(monkeypatch):
         for a, t in zip(args, sig):
             t(a if a is not None else 0)  # raises on an unconvertible argument
         calls.append(name)
+        if name == "xcp_colreduce_f32":       # (in, S, L, out, G, accumulate, stream): gradient slabs
+            _fill(args[3], args[2] * args[4], args[5])
+        elif name == "xcp_bn_bwd_finalize_part" and args[10]:   # dgamma, dbeta (C each)
+            _fill(args[10], args[2], args[12])
+            _fill(args[11], args[2], args[12])
+        elif name == "xcp_permute3" and args[0] == 0:          # fp32 permute (stem conv2 gradient)
+            _fill(args[2], args[3] * args[4] * args[5], False)
         if name == "xcp_dw_bwd_chunks":
             return 7
         if name == "xcp_chanred_parts":
@@ -40,6 +60,7 @@ def fake_lib(monkeypatch):
 
     monkeypatch.setattr(_lib, "call", fake_call)
     monkeypatch.setattr(ops, "check_gpu", lambda *a: None)
+    monkeypatch.setattr(ops, "device_guard", lambda t: contextlib.nullcontext())
     from xcp import engine
     monkeypatch.setattr(engine, "WGRAD_SIDE_STREAM", False)   # no HIP streams on the CPU
 
@@ -47,11 +68,40 @@ def fake_lib(monkeypatch):
         cuda_stream = 0
 
     monkeypatch.setattr(torch.cuda, "current_stream", lambda *a, **k: _S())
+
+    # the LSTM custom op is registered for the GPU only: drive its Python bodies directly
+    from xcp import lstm as xl, torch_ops as T
+
+    class _LSTMFn(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w_ih, w_hh, b_ih, b_hh):
+            out, hn, cn, hprev, cst, gates = T.lstm._init_fn(x, w_ih, w_hh, b_ih, b_hh, 0)
+            ctx.save_for_backward(x, w_ih, w_hh, hprev, cst, gates)
+            return out, hn, cn
+
+        @staticmethod
+        def backward(ctx, dout, dhn, dcn):
+            x, w_ih, w_hh, hprev, cst, gates = ctx.saved_tensors
+            dx, dw_ih, dw_hh, db = T.lstm_backward._init_fn(dout, dhn, dcn, x, w_ih, w_hh, hprev, cst, gates, 0, False)
+            return None, dw_ih, dw_hh, db, db.clone()
+
+    def fake_forward(self, input, hx=None):
+        out, hn, cn = _LSTMFn.apply(input, self.weight_ih_l0, self.weight_hh_l0, self.bias_ih_l0, self.bias_hh_l0)
+        return out, (hn, cn)
+
+    monkeypatch.setattr(xl.LSTM, "forward", fake_forward)
     return calls
 
 
+@pytest.fixture
+def fake_lib(monkeypatch):
+    return install_fake_lib(monkeypatch)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp32"])
 @pytest.mark.parametrize("unfrozen", [False, True])
-def test_lstmv_step_call_sequence(fake_lib, unfrozen):
+def test_lstmv_step_call_sequence(fake_lib, unfrozen, prec):
+    import xcp
     from Models.XceptionLSTMV import XceptionLSTMV
     torch.manual_seed(0)
     m = XceptionLSTMV(128, pretrained=False)
@@ -59,16 +109,18 @@ def test_lstmv_step_call_sequence(fake_lib, unfrozen):
         for p in m.feature_extractor.parameters():
             p.requires_grad = True
     x = torch.rand(2, 3, 3, 71, 71)
-    feats = m.extract_features(x, "cpu")
-    assert feats.shape == (2, 3, 2048)
-    prob = m(feats)
-    loss = nn.BCELoss()(prob.clamp(1e-3, 1 - 1e-3), torch.tensor([[0.0], [1.0]]))
-    loss.backward()
+    with xcp.precision(prec):
+        feats = m.extract_features(x, "cpu")
+        assert feats.shape == (2, 3, 2048)
+        prob = m(feats)
+        loss = torch.nan_to_num(prob).sum()   # (the fake kernels leave their outputs uninitialised)
+        loss.backward()
     names = set(fake_lib)
     assert {"xcp_gemm_nt", "xcp_dw_fwd", "xcp_tail_fwd", "xcp_avgpool_fwd", "xcp_lstm_fwd", "xcp_lstm_bwd"} <= names
     if unfrozen:
-        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd_bnred", "xcp_conv1_wgrad",
-                "xcp_conv3x3", "xcp_conv3x3_wgrad"} <= names
+        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd_bnred", "xcp_conv1_wgrad"} <= names
+        # stem conv2: direct MFMA conv in bf16, im2col GEMM (gather modes 2 / 3) in fp32
+        assert ({"xcp_conv3x3", "xcp_conv3x3_wgrad"} <= names) == (prec == "bf16")
         for n, p in m.feature_extractor.named_parameters():
             assert p.grad is not None and p.grad.shape == p.shape, n
     else:
@@ -109,3 +161,77 @@ def test_no_cpu_fallback():
     m = xception(num_classes=1)
     with pytest.raises(RuntimeError, match="MI355X"):
         m(torch.zeros(1, 3, 64, 64))
+
+
+def test_default_mode_returns_gradients_to_autograd(fake_lib):
+    """Without a gradient sink the backbone node hands its gradients to autograd:
+    torch.autograd.grad works and post-accumulate-grad hooks fire for backbone parameters."""
+    from Models.Xception import xception
+    torch.manual_seed(0)
+    m = xception(num_classes=1)
+    m.fc = nn.Identity()
+    params = list(m.parameters())
+    fired = []
+    for p in params:
+        p.register_post_accumulate_grad_hook(lambda p: fired.append(p))
+    f = m(torch.rand(2, 3, 71, 71))
+    gr = torch.autograd.grad(f.sum(), [m.block4.rep[1].pointwise.weight, m.conv1.weight])
+    assert all(g is not None and torch.all(g == FILL["v"]) for g in gr)
+    assert m.block4.rep[1].pointwise.weight.grad is None      # autograd.grad leaves .grad alone
+    m(torch.rand(2, 3, 71, 71)).sum().backward()
+    assert len(fired) == len(params)
+
+
+def _sink_worker(rank, world, port, out):
+    """gloo rank: the engine's hook-less accumulation path with GradBuckets as its sink."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class _MP:   # minimal monkeypatch for a spawned process
+        def setattr(self, obj, name, val):
+            setattr(obj, name, val)
+
+    calls = install_fake_lib(_MP())
+    FILL["v"] = float(rank + 1)
+    from xcp import ddp
+    from Models.Xception import xception
+    torch.manual_seed(0)
+    m = xception(num_classes=1)
+    m.fc = nn.Identity()
+    params = list(m.parameters())
+    events = []
+    real = ddp.dist.all_reduce
+
+    def logged(t, *a, **k):
+        events.append(len(calls))
+        return real(t, *a, **k)
+
+    ddp.dist.all_reduce = logged
+    gb = ddp.GradBuckets(params, bucket_bytes=1 << 20, world=world, module=m)
+    for step in range(2):
+        gb.zero()
+        events.clear()
+        n0 = len(calls)
+        m(torch.rand(2, 3, 71, 71)).sum().backward()
+        last_dw = max(i for i, c in enumerate(calls) if c == "xcp_dw_bwd")
+        launched_during = sum(1 for e in events if e <= last_dw)
+        gb.allreduce()
+    out[rank] = {"grads": {n: p.grad.clone() for n, p in m.named_parameters()}, "during": launched_during,
+                 "buckets": len(gb.buckets), "nbwd": len(calls) - n0}
+    dist.destroy_process_group()
+
+
+def test_sink_allreduce_overlaps_backbone_backward():
+    """world 2 (gloo), fake kernels writing rank+1 into every gradient: the engine accumulates
+    into GradBuckets' views, buckets are all-reduced while the backbone backward is still
+    being enqueued, and every backbone gradient ends as the mean over ranks (1.5)."""
+    world, port = 2, 29600 + os.getpid() % 1000
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_sink_worker, args=(world, port, out), nprocs=world, join=True)
+    for rank in range(world):
+        r = out[rank]
+        assert r["buckets"] > 4
+        assert r["during"] >= r["buckets"] - 2, r   # all but the stem buckets launched inside backward
+        for n, gr in r["grads"].items():
+            assert torch.all(gr == 1.5), n

@@ -9,9 +9,13 @@ Stated tolerances:
               fp64 evaluation of the same graph by 1.7e-3 on bn1.bias),
               total gradient norm rel <= 1e-3.
   bf16 mode : feature cosine >= 0.999, logits abs <= 3e-2, loss rel <= 2e-2,
-              total gradient norm rel <= 5e-2, median per-parameter gradient-norm
-              rel error <= 3e-2 and max <= 0.3 (bf16 gradient storage through 40
-              BatchNorm layers; the fp32 mode carries the tight contract).
+              total gradient norm rel <= 5e-2, every conv / linear / LSTM
+              weight-gradient norm rel <= 5e-2, BatchNorm affine-gradient
+              norms: BF16_BN_TOL below.
+  after one optimiser step (Adam's first step moves every element by ~lr * sign(g)):
+              the parameter sums may differ from the reference's by 2 * lr per element
+              whose gradient sign differs; fp32 allows 0.2 % of the elements, bf16 (head
+              parameters only) 10 %.
 """
 import numpy as np
 import pytest
@@ -43,15 +47,57 @@ def bn_param_names(model):
     return names
 
 
-def check_gradnorms(errs, bn_names, f32):
-    """errs: {param: rel err of grad norm}."""
-    if f32:
-        for n, e in errs.items():
+# BatchNorm affine gradients in bf16: dgamma = sum(dz * zhat), dbeta = sum(dz) over B*T*H*W
+# pixels -- nearly cancelling sums that amplify the bf16 perturbation of the activations
+# they are taken over (up to 0.15 measured at bn1 / bn2, the 147^2 stem); PyTorch's own
+# bf16 autocast of the same graph shows the same spread (test_bf16_gradient_noise_vs_torch_
+# autocast asserts ours is no worse), so the bound is a property of bf16 on this graph.
+BF16_BN_TOL = 0.2
+
+
+def is_head(n):
+    return n.startswith(("lstm.", "fc_layers.", "fc_out."))
+
+
+def check_gradnorms(errs, bn_names, f32, skip_head=False):
+    """errs: {param: rel err of grad norm}.  skip_head (bf16): the LSTM / FC head is checked
+    against the oracle head on the GPU's own features instead (check_head_on_features): its
+    gradients react to the bf16 perturbation of the features through the head's ReLU masks
+    (a property of the random-init head at 2-4 clips, not of a kernel)."""
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:8]
+    print("\nworst gradient-norm errors:", [(n, round(e, 4)) for n, e in worst])
+    for n, e in errs.items():
+        if f32:
             assert e < (5e-3 if n in bn_names else 1e-3), (n, e)
-    else:
-        v = np.array(list(errs.values()))
-        assert np.median(v) < 3e-2, np.median(v)
-        assert v.max() < 0.3, max(errs.items(), key=lambda kv: kv[1])
+        elif not (skip_head and is_head(n)):
+            assert e < (BF16_BN_TOL if n in bn_names else 5e-2), (n, e)
+
+
+def check_head_on_features(m, feats, y, head_grads):
+    """The GPU head (xcp LSTM kernels + FC) against the oracle's fp32 CPU restatement of
+    XceptionLSTMV.forward (XceptionLSTMV.py:66-70) on the SAME features: gradients <= 1e-3."""
+    from oracle import xception_oracle as O
+    sd = {k: v.detach().cpu().clone().requires_grad_(is_head(k) and v.is_floating_point())
+          for k, v in m.state_dict().items()}
+    prob, _ = O.head_forward(feats.detach().float().cpu(), sd)
+    nn.BCELoss()(prob, y.cpu()).backward()
+    for n, gr in head_grads.items():
+        ref = sd[n].grad
+        assert relerr(gr.cpu(), ref) < 1e-3, (n, relerr(gr.cpu(), ref))
+
+
+def check_after_step(m, g, key, lr, frac, names=None):
+    """parameter sums after one optimiser step against the reference's (see module docstring)"""
+    bad = []
+    for n, p in m.named_parameters():
+        k = f"{key}/{n}/sum"
+        if k not in g or (names is not None and not names(n)):
+            continue
+        got = p.detach().double().sum().item()
+        tol = 2 * lr * max(frac * p.numel(), 2) + 1e-6 * abs(float(g[k])) + 1e-7   # >= 2 sign flips
+        if abs(got - float(g[k])) > tol:
+            bad.append((n, got, float(g[k]), tol))
+    assert not bad, bad[:5]
 
 
 def relerr(a, b):
@@ -142,7 +188,9 @@ def test_xceptionlstmv_train_step_vs_reference(gpu, golden, prec, mode):
             continue
         errs[n] = abs(p.grad.double().norm().item() - g[key]) / max(g[key], 1e-30)
         tot += (p.grad.double() ** 2).sum().item()
-    check_gradnorms(errs, bn_param_names(m), f32)
+    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not f32)
+    if not f32:
+        check_head_on_features(m, feats, y, {n: p.grad for n, p in m.named_parameters() if is_head(n)})
     np.testing.assert_allclose(tot ** 0.5, g[f"{mode}/total_gradnorm"], rtol=1e-3 if f32 else 5e-2)
 
 
@@ -208,6 +256,15 @@ def test_bf16_gradient_noise_vs_torch_autocast(gpu):
     print(f"median cos: xcp-bf16 {np.median(c16):.4f}  torch-autocast-bf16 {np.median(cau):.4f}; "
           f"min: {c16.min():.4f} / {cau.min():.4f}")
     assert np.median(c16) >= np.median(cau) - 0.02
+    # BatchNorm affine gradient norms (the BF16_BN_TOL contract): relative error against the
+    # fp32 gradients, ours vs PyTorch's bf16 autocast on the same graph
+    bn = [k for k in g32 if k.startswith("feature_extractor.") and g32[k].dim() == 1 and k in ga]
+    e16 = np.array([abs(g16[k].norm().item() - g32[k].norm().item()) / g32[k].norm().item() for k in bn])
+    eau = np.array([abs(ga[k].norm().item() - g32[k].norm().item()) / g32[k].norm().item() for k in bn])
+    print(f"BN affine grad-norm rel err: xcp-bf16 median {np.median(e16):.4f} max {e16.max():.4f} "
+          f"({bn[int(e16.argmax())]}); torch-autocast-bf16 median {np.median(eau):.4f} max {eau.max():.4f} "
+          f"({bn[int(eau.argmax())]})")
+    assert np.median(e16) <= np.median(eau) * 1.5 + 0.01
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
@@ -252,4 +309,97 @@ def test_xceptionlstma_step_vs_reference(gpu, golden, prec):
             assert key not in g, n
             continue
         errs[n] = abs(p.grad.double().norm().item() - g[key]) / max(g[key], 1e-30)
-    check_gradnorms(errs, bn_param_names(m), f32)
+    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not f32)
+    if not f32:
+        check_head_on_features(m, feats, y, {n: p.grad for n, p in m.named_parameters() if is_head(n)})
+
+
+def test_after_adam_and_buffers_b2t4(gpu, golden):
+    """The captured `after_adam/*` and `buf/*` entries of the B2T4 299^2 step (fp32): one
+    FusedAdamClip(lr 1e-4, no clipping) step after the BCE backward (capture_goldens.py
+    g_lstmv), and the BatchNorm running statistics after the train-mode forward."""
+    import xcp
+    from xcp.optim import FusedAdamClip
+    from Models.XceptionLSTMV import XceptionLSTMV
+    g = golden("lstmv_b2t4.npz")
+    B, T, S = int(g["B"]), int(g["T"]), int(g["S"])
+    for mode in ("frozen", "unfrozen"):
+        torch.manual_seed(0)
+        m = XceptionLSTMV(128, pretrained=False)
+        if mode == "unfrozen":
+            for p in m.feature_extractor.parameters():
+                p.requires_grad = True
+        m = m.to(gpu).train()
+        m.fc_layers.eval()
+        opt = FusedAdamClip(m.parameters(), lr=1e-4)
+        x = seeded_uniform((B, T, 3, S, S), 1234).to(gpu)
+        y = torch.tensor([[0.0], [1.0]], device=gpu)[:B]
+        with xcp.precision("fp32"):
+            nn.BCELoss()(m(m.extract_features(x, gpu)), y).backward()
+        assert opt.step() is None
+        torch.cuda.synchronize()
+        check_after_step(m, g, f"{mode}/after_adam", 1e-4, 2e-3)
+        for n, t in m.state_dict().items():
+            if "running_mean" in n or "running_var" in n:
+                np.testing.assert_allclose(t.double().sum().item(), g[f"{mode}/buf/{n}/sum"], rtol=1e-4, atol=1e-5,
+                                           err_msg=n)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_bench_size_step_vs_reference(gpu, golden, prec):
+    """XceptionLSTMV(128), unfrozen, at B*T = 64 frames of 299^2 (lstmv_b4t16.npz): the middle
+    flow's pointwise GEMMs have M = 23,104 rows, 273 output tiles of 256x256, so in bf16 the
+    bench's kernel set runs (the 256x256 NT / TN MFMA GEMMs), then one train_visual.py optimiser
+    step -- clip_grad_norm_(1.0) + Adam(lr 1e-5, weight_decay 1e-4) -- through FusedAdamClip."""
+    import xcp
+    from xcp.optim import FusedAdamClip
+    from Models.XceptionLSTMV import XceptionLSTMV
+    g = golden("lstmv_b4t16.npz")
+    B, T, S = int(g["B"]), int(g["T"]), int(g["S"])
+    M = B * T * 19 * 19
+    assert ((M + 255) // 256) * ((728 + 255) // 256) >= 256   # the 256x256 dispatch rule (gemm.hip nt_big)
+    torch.manual_seed(0)
+    m = XceptionLSTMV(128, pretrained=False)
+    for p in m.feature_extractor.parameters():
+        p.requires_grad = True
+    m = m.to(gpu).train()
+    m.fc_layers.eval()
+    opt = FusedAdamClip(m.parameters(), lr=1e-5, weight_decay=1e-4, max_norm=1.0)
+    logits = {}
+    m.fc_out.register_forward_hook(lambda mod, i, o: logits.__setitem__("v", o.detach()))
+    x = seeded_uniform((B, T, 3, S, S), 4242).to(gpu)
+    y = torch.tensor([[0.0], [1.0], [1.0], [0.0]], device=gpu)[:B]
+    with xcp.precision(prec):
+        feats = m.extract_features(x, gpu)
+        loss = nn.BCELoss()(m(feats), y)
+        loss.backward()
+    torch.cuda.synchronize()
+    f32 = prec == "fp32"
+    fv = feats.detach().double().reshape(-1).cpu().numpy()
+    samp = fv[g["features/idx"]]
+    if f32:
+        np.testing.assert_allclose(samp, g["features/val"], rtol=1e-4, atol=1e-5)
+    else:
+        assert cos(samp, g["features/val"]) > 0.999
+    np.testing.assert_allclose((fv * fv).sum(), g["features/sumsq"], rtol=1e-4 if f32 else 2e-2)
+    np.testing.assert_allclose(logits["v"].cpu().numpy(), g["logits"], atol=1e-4 if f32 else 3e-2, rtol=0)
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-5 if f32 else 2e-2)
+    errs = {n: abs(p.grad.double().norm().item() - g[f"gradnorm/{n}"]) / max(float(g[f"gradnorm/{n}"]), 1e-30)
+            for n, p in m.named_parameters()}
+    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not f32)
+    if not f32:
+        check_head_on_features(m, feats, y, {n: p.grad.clone() for n, p in m.named_parameters() if is_head(n)})
+    norm = opt.step()
+    np.testing.assert_allclose(norm.item(), g["total_gradnorm"], rtol=1e-3 if f32 else 5e-2)
+    torch.cuda.synchronize()
+    if f32:
+        check_after_step(m, g, "after_step", 1e-5, 2e-3)
+    else:   # backbone weights: Adam's sign(g) at bf16 gradient fidelity (cosine ~0.9 to fp32)
+        check_after_step(m, g, "after_step", 1e-5, 0.2)
+    for n, t in m.state_dict().items():
+        if "running_var" in n:
+            np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"], rtol=1e-4 if f32 else 2e-2,
+                                       err_msg=n)
+        elif "running_mean" in n:
+            np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"], rtol=1e-4 if f32 else 5e-2,
+                                       atol=1e-4 if f32 else 5e-2, err_msg=n)

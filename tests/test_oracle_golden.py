@@ -165,3 +165,24 @@ def test_audio_clip(golden):
     np.testing.assert_allclose(r["loss"].item(), g["loss"], rtol=1e-6)
     for k, gr in r["grads"].items():
         np.testing.assert_allclose(gr.double().norm().item(), g[f"gradnorm/{k}"], rtol=1e-3, err_msg=k)
+
+
+def test_oracle_optimizer_step_vs_reference(golden):
+    """oracle.clip_grad_norm + oracle.adam_step against the reference's own step at the bench
+    kernel-set size (lstmv_b4t16.npz: clip_grad_norm_(1.0) + Adam(lr 1e-5, wd 1e-4),
+    train_visual.py:533, :575-577), parameter sums after the step."""
+    g = golden("lstmv_b4t16.npz")
+    B, T, S = int(g["B"]), int(g["T"]), int(g["S"])
+    x = seeded_uniform((B, T, 3, S, S), 4242)
+    y = torch.tensor([[0.0], [1.0], [1.0], [0.0]])[:B]
+    torch.manual_seed(0)
+    sd = XceptionLSTMV(128, pretrained=False).state_dict()
+    r = O.clip_step(sd, x, y, unfrozen=True, optim=dict(lr=1e-5, weight_decay=1e-4, max_norm=1.0))
+    np.testing.assert_allclose(r["loss"].item(), g["loss"], rtol=1e-6)
+    for k, p in r["params"].items():
+        key = f"after_step/{k}/sum"
+        if key in g:
+            a = p.detach().double()
+            np.testing.assert_allclose(a.sum().item(), g[key], rtol=1e-6, atol=2e-5 * 1e-3 * a.numel() + 1e-6,
+                                       err_msg=k)
+            np.testing.assert_allclose((a * a).sum().item(), g[f"after_step/{k}/sumsq"], rtol=1e-5, err_msg=k)

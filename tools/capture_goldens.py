@@ -295,6 +295,192 @@ def g_audio(A, out_dir, B=2, T=6):
     np.savez_compressed(os.path.join(out_dir, "audio_b2t6.npz"), **out)
 
 
+def all_param_fp(out, prefix, module):
+    for name, p in module.named_parameters():
+        a = p.detach().double()
+        out[f"{prefix}/{name}/sum"] = a.sum().item()
+        out[f"{prefix}/{name}/sumsq"] = (a * a).sum().item()
+
+
+def g_lstmv_big(V, out_dir, B=4, T=16, S=299):
+    """The bench-size kernel set: XceptionLSTMV(128) unfrozen at B*T = 64 frames of 299^2
+    (M = 23,104 pixel rows in the middle flow, so the 256x256 MFMA GEMMs dispatch), one
+    train_visual.py optimiser step: BCE -> backward -> clip_grad_norm_(1.0) -> Adam(lr 1e-5,
+    weight_decay 1e-4) (train_visual.py:533, :575-577; BCE head as XceptionLSTMV.forward).
+    Stores fingerprints only (features, gradient norms, parameters after the step, buffers)."""
+    out = {"torch_version": torch.__version__, "B": B, "T": T, "S": S, "seed_w": 0, "seed_x": 4242,
+           "lr": 1e-5, "weight_decay": 1e-4, "max_norm": 1.0}
+    x = seeded_uniform((B, T, 3, S, S), 4242)
+    y = torch.tensor([[0.0], [1.0], [1.0], [0.0]])[:B]
+    torch.manual_seed(0)
+    m = V.XceptionLSTMV(128)
+    for p in m.feature_extractor.parameters():
+        p.requires_grad = True
+    m.train()
+    m.fc_layers.eval()
+    store = {}
+    m.fc_out.register_forward_hook(_logit_hook(store))
+    feats = m.extract_features(x, "cpu")
+    prob = m(feats)
+    loss = nn.BCELoss()(prob, y)
+    loss.backward()
+    put_fp(out, "features", feats)
+    out["logits"] = store["logits"].numpy()
+    out["loss"] = loss.item()
+    grad_norms(out, "gradnorm", m)
+    params = [p for p in m.parameters() if p.requires_grad]
+    out["total_gradnorm"] = torch.nn.utils.clip_grad_norm_(params, 1.0).item()
+    opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4)
+    opt.step()
+    all_param_fp(out, "after_step", m)
+    for name, t in m.state_dict().items():
+        if "running_mean" in name or "running_var" in name:
+            a = t.double()
+            out[f"buf/{name}/sum"] = a.sum().item()
+            out[f"buf/{name}/sumsq"] = (a * a).sum().item()
+    np.savez_compressed(os.path.join(out_dir, "lstmv_b4t16.npz"), **out)
+
+
+# ----------------------------------------------------------------------------- script-level defs
+def load_script_defs(fname, names, extra_globals=None):
+    """Executes ONLY the named top-level class / function definitions of a reference script
+    (the scripts themselves import modules absent from the snapshot, so they cannot be
+    imported whole; their definitions are self-contained).  Parsed with ``ast`` from the
+    read-only reference file; nothing is written there."""
+    import ast
+    import sklearn.metrics as skm
+    src = open(os.path.join(REF, fname)).read()
+    tree = ast.parse(src)
+    nodes = [n for n in tree.body if isinstance(n, (ast.ClassDef, ast.FunctionDef)) and n.name in names]
+    assert sorted(n.name for n in nodes) == sorted(names), (fname, [n.name for n in nodes])
+    ns = {"np": np, "torch": torch, "nn": nn, "F": F, "Optional": __import__("typing").Optional,
+          "roc_curve": skm.roc_curve, "roc_auc_score": skm.roc_auc_score, "auc": skm.auc, "sk_auc": skm.auc,
+          "average_precision_score": skm.average_precision_score}
+    ns.update(extra_globals or {})
+    exec(compile(ast.Module(body=nodes, type_ignores=[]), os.path.join(REF, fname), "exec"), ns)
+    return {n: ns[n] for n in names}
+
+
+def metric_cases():
+    """Seeded (labels, scores) sets: separable-ish, ties, heavy imbalance, and one class."""
+    rs = np.random.RandomState(11)
+    cases = []
+    y = rs.randint(0, 2, 200)
+    cases.append((y, np.clip(0.5 + 0.35 * (y - 0.5) + 0.25 * rs.randn(200), 0, 1)))
+    y = rs.randint(0, 2, 64)
+    cases.append((y, np.round(rs.rand(64), 1)))                       # many ties
+    y = (rs.rand(300) < 0.1).astype(int)
+    cases.append((y, rs.rand(300) * 0.5 + 0.4 * y))                    # 10 % positives
+    cases.append((np.array([0, 1, 0, 1, 1]), np.array([0.1, 0.9, 0.8, 0.3, 0.6])))
+    cases.append((np.zeros(10, int), rs.rand(10)))                     # single class
+    return cases
+
+
+def g_heads(out_dir):
+    """Heads, losses and metrics of the training / evaluation scripts:
+    ArcFaceHead (train_visual.py:455-474, m=0.5; train_au_face.py:423-442, m=0.30),
+    CBFocalLoss (train_au_face.py:445-458), compute_metrics (train_visual.py:476-487,
+    test_visual.py:515-565), compute_eer_auc / pick_threshold / compute_acc_ap_and_counts
+    (train_au_face.py:462-506) and _unwrap_state_dict (test_au_face.py:107-125)."""
+    out = {"torch_version": torch.__version__}
+    tv = load_script_defs("train_visual.py", ["ArcFaceHead", "compute_metrics"])
+    ta = load_script_defs("train_au_face.py", ["ArcFaceHead", "CBFocalLoss", "compute_eer_auc", "pick_threshold",
+                                               "compute_acc_ap_and_counts"])
+    te = load_script_defs("test_visual.py", ["compute_metrics"])
+    tf = load_script_defs("test_au_face.py", ["_unwrap_state_dict"])
+    for tag, cls, m_ in (("v", tv["ArcFaceHead"], 0.5), ("a", ta["ArcFaceHead"], 0.30)):
+        torch.manual_seed(21)
+        head = cls(128, 2, s=30.0, m=m_)
+        B = 16
+        f = seeded_normal((B, 128), 501).requires_grad_(True)
+        lab = torch.from_numpy(np.random.RandomState(502).randint(0, 2, B)).long()
+        with torch.no_grad():   # clamp edge: row 0 exactly along its class centre (cos = 1)
+            f[0] = head.weight[lab[0]] * 3.0
+        out[f"{tag}/weight"] = head.weight.detach().numpy()
+        out[f"{tag}/features"] = f.detach().numpy()
+        out[f"{tag}/labels"] = lab.numpy()
+        out[f"{tag}/logits_nolabel"] = head(f).detach().numpy()
+        logits = head(f, lab)
+        out[f"{tag}/logits"] = logits.detach().numpy()
+        if tag == "v":
+            loss = nn.CrossEntropyLoss()(logits, lab)
+        else:
+            cb = ta["CBFocalLoss"]([300, 1700], beta=0.9999, gamma=2.0)
+            out["a/class_weights"] = cb.class_weights.numpy()
+            loss = cb(logits, lab)
+        loss.backward()
+        out[f"{tag}/loss"] = loss.item()
+        out[f"{tag}/dfeatures"] = f.grad.numpy()
+        out[f"{tag}/dweight"] = head.weight.grad.numpy()
+    for i, (y, s) in enumerate(metric_cases()):
+        out[f"m{i}/labels"] = y
+        out[f"m{i}/scores"] = s
+        out[f"m{i}/train_visual"] = np.array(tv["compute_metrics"](y, s), dtype=np.float64)
+        r = te["compute_metrics"](y, s)
+        out[f"m{i}/test_visual_keys"] = np.array(sorted(r))
+        out[f"m{i}/test_visual"] = np.array([r[k] for k in sorted(r)], dtype=np.float64)
+        if len(np.unique(y)) > 1:
+            a_, p_, e_, _ = ta["compute_eer_auc"](y, s)
+            out[f"m{i}/eer_auc"] = np.array([a_, p_, e_])
+            for mode in ("youden", "fpr"):
+                thr = ta["pick_threshold"](y, s, mode=mode, fpr_target=0.05)
+                out[f"m{i}/thr_{mode}"] = np.array(thr)
+                out[f"m{i}/acc_{mode}"] = np.array(ta["compute_acc_ap_and_counts"](y, s, thr[0]), dtype=np.float64)
+    raw = {"model": {"module.conv.weight": torch.ones(2), "module.fc.bias": torch.zeros(3)}, "best_auc": 0.9,
+           "n_averaged": torch.tensor(4)}
+    out["unwrap/keys"] = np.array(sorted(tf["_unwrap_state_dict"](raw)))
+    raw2 = {"ema_state_dict": {"n_averaged": torch.tensor(3), "module.block.w": torch.ones(1)}}
+    out["unwrap2/keys"] = np.array(sorted(tf["_unwrap_state_dict"](raw2)))
+    np.savez_compressed(os.path.join(out_dir, "heads.npz"), **out)
+
+
+def g_arcface_step(V, out_dir, B=2, T=3):
+    """The active train_visual.py step (:563-577) on CPU fp32 (autocast("cuda") and GradScaler are
+    no-ops without CUDA): extract_features -> model.lstm(f)[0][:, -1] -> ArcFaceHead(128, 2, s=30,
+    m=0.5) -> CrossEntropyLoss -> backward -> clip_grad_norm_(1.0) -> Adam(lr 1e-5, wd 1e-4) over
+    model + head parameters, at the reference's own frame sizes 224^2 (train_visual.py:505) and
+    256^2 (video_dataloader.py:61), frozen (epochs < 3) and unfrozen (train_visual.py:547-556).
+    The shipped extract_features(x, seq_lengths) raises, so the device form is used."""
+    tv = load_script_defs("train_visual.py", ["ArcFaceHead"])
+    out = {"torch_version": torch.__version__, "B": B, "T": T}
+    for S, mode in ((224, "unfrozen"), (224, "frozen"), (256, "unfrozen")):
+        tag = f"s{S}_{mode}"
+        torch.manual_seed(0)
+        m = V.XceptionLSTMV(128)
+        torch.manual_seed(1)
+        head = tv["ArcFaceHead"](128, 2, s=30.0, m=0.5)
+        for p in m.feature_extractor.parameters():
+            p.requires_grad = mode == "unfrozen"
+        m.train()
+        head.train()
+        x = seeded_uniform((B, T, 3, S, S), 6000 + S)
+        lab = torch.tensor([0, 1])[:B]
+        params = list(m.parameters()) + list(head.parameters())
+        opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4)
+        opt.zero_grad()
+        feats = m.extract_features(x, "cpu")
+        emb = m.lstm(feats)[0][:, -1, :]
+        logits = head(emb, lab)
+        loss = nn.CrossEntropyLoss()(logits, lab)
+        loss.backward()
+        out[f"{tag}/logits"] = logits.detach().numpy()
+        out[f"{tag}/emb"] = emb.detach().numpy()
+        out[f"{tag}/loss"] = loss.item()
+        grad_norms(out, f"{tag}/gradnorm", m)
+        out[f"{tag}/gradnorm/head.weight"] = head.weight.grad.double().norm().item()
+        out[f"{tag}/total_gradnorm"] = torch.nn.utils.clip_grad_norm_(params, 1.0).item()
+        opt.step()
+        all_param_fp(out, f"{tag}/after_step", m)
+        out[f"{tag}/after_step/head.weight"] = head.weight.detach().numpy()
+    out["head_init"] = _head_init(tv, 1)
+    np.savez_compressed(os.path.join(out_dir, "arcface_step.npz"), **out)
+
+
+def _head_init(tv, seed):
+    torch.manual_seed(seed)
+    return tv["ArcFaceHead"](128, 2, s=30.0, m=0.5).weight.detach().numpy()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "tests", "golden"))
@@ -305,7 +491,8 @@ def main():
     jobs = {"init": lambda: g_init(X, V, A, args.out), "backbone64": lambda: g_backbone64(X, args.out),
             "lstm": lambda: g_lstm(args.out), "blocks": lambda: g_blocks(X, args.out),
             "sepconv": lambda: g_sepconv(X, args.out), "audio": lambda: g_audio(A, args.out),
-            "lstmv": lambda: g_lstmv(V, args.out)}
+            "lstmv": lambda: g_lstmv(V, args.out), "lstmv_big": lambda: g_lstmv_big(V, args.out),
+            "heads": lambda: g_heads(args.out), "arcface_step": lambda: g_arcface_step(V, args.out)}
     for k, fn in jobs.items():
         if args.only and k not in args.only.split(","):
             continue

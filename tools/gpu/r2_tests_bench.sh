@@ -1,0 +1,9 @@
+# GPU round-2 check: the full -m gpu suite, then the default bench (progress on stderr).
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf -s -p no:cacheprovider > gpurun_out/r2_t.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/r2_t.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py > gpurun_out/r2_b.json 2> gpurun_out/r2_b.err
