@@ -147,6 +147,35 @@ def head_forward(feats, sd, prefix=""):
     return torch.sigmoid(logits), logits
 
 
+def arcface_logits(features, weight, labels, s=30.0, m=0.5):
+    """ArcFaceHead.forward, train_visual.py:464-474 (m = 0.5) / train_au_face.py:432-442 (m = 0.30)."""
+    x = F.normalize(features)
+    W = F.normalize(weight)
+    cos = torch.matmul(x, W.t())
+    if labels is None:
+        return s * cos
+    theta = torch.acos(cos.clamp(-1 + 1e-7, 1 - 1e-7))
+    target = torch.cos(theta + m)
+    one_hot = F.one_hot(labels, num_classes=weight.shape[0]).float()
+    return s * (cos * (1 - one_hot) + target * one_hot)
+
+
+def cb_focal_loss(logits, labels, class_weights, gamma=2.0):
+    """CBFocalLoss.forward, train_au_face.py:455-458."""
+    ce = F.cross_entropy(logits, labels, reduction="none", weight=class_weights)
+    pt = torch.exp(-ce)
+    return ((1 - pt) ** gamma * ce).mean()
+
+
+def cb_class_weights(samples_per_cls, beta=0.9999):
+    """CBFocalLoss.__init__, train_au_face.py:447-451."""
+    import numpy as np
+    effective_num = 1.0 - np.power(beta, samples_per_cls)
+    weights = (1.0 - beta) / np.array(effective_num)
+    weights = weights / weights.sum() * len(samples_per_cls)
+    return torch.tensor(weights, dtype=torch.float32)
+
+
 def audio_frames(x):
     """XceptionLSTMA.extract_features front end, XceptionLSTMA.py:43-46."""
     B, T, c, n = x.shape
