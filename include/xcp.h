@@ -145,6 +145,14 @@ int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, in
 int xcp_frames_u8_to_f32(const unsigned char* in, const int* len, float* out, int B, int Tmax, int H, int W,
                          xcp_stream_t stream);
 
+/* ---- clip input, general form: the same x / 255, optionally resized and in the model's layout ----
+ * out = F.interpolate(x / 255, (OH, OW), mode="bilinear", align_corners=False) when (OH, OW) !=
+ * (H, W) (e.g. the dataset's 256^2 faces -> Xception's 299^2), else x / 255; dtype XCP_F32 or
+ * XCP_BF16 (round to nearest even); nhwc 0: [B][Tmax][3][OH][OW], 1: [B][Tmax][OH][OW][3]
+ * (channels_last).  Replaces video_dataloader.py:35 + :59-64 (+ the resize a 299^2 run adds). */
+int xcp_frames_prep(const unsigned char* in, const int* len, void* out, int B, int Tmax, int H, int W, int OH, int OW,
+                    int dtype, int nhwc, xcp_stream_t stream);
+
 /* ---- audio front end (XceptionLSTMA.py:44-46): F.interpolate(bilinear, align_corners=False) ----
  * out [NC][OH][OW] fp32 = bilinear resize of in [NC][IH][IW] fp32 (ATen's source-index and
  * weight formulas in fp32); MFCC frames [B*T*3][13][1] -> [B*T*3][64][64] */

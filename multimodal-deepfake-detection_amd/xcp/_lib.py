@@ -49,6 +49,7 @@ SIGNATURES = {
     "xcp_permute3_batch": [P, I, I, P],
     "xcp_frames_u8_to_f32": [P, P, P, I, I, I, I, P],
     "xcp_resize_bilinear": [P, P, I, I, I, I, I, P],
+    "xcp_frames_prep": [P, P, P, I, I, I, I, I, I, I, I, P],
     "xcp_opt_sumsq": [P, I, P, F, P, P],
     "xcp_opt_adam": [P, I, P, F, F, F, F, F, F, F, P],
     "xcp_conv3x3_parts": [I, I, I, I],

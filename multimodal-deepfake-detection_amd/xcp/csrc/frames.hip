@@ -84,9 +84,80 @@ __global__ __launch_bounds__(256) void resize_bilinear_kernel(const float* __res
   out[g] = t0 * lh0 + t1 * lh1;
 }
 
+// General clip preparation: uint8 frames -> x / 255, optionally bilinear-resized to OH x OW
+// (F.interpolate(x / 255, (OH, OW), mode="bilinear", align_corners=False) of the fp32 clip, as
+// lin_idx above), stored fp32 or bf16 (round to nearest even of that fp32 value), planar
+// [B][Tmax][3][OH][OW] or interleaved [B][Tmax][OH][OW][3].  One thread per output pixel
+// (3 channels); frames past a clip's length are zero.
+template <typename T, bool NHWC>
+__global__ __launch_bounds__(256) void frames_prep_kernel(const unsigned char* __restrict__ in,
+                                                          const int* __restrict__ len, T* __restrict__ out, int Tmax,
+                                                          int H, int W, int OH, int OW, float sh, float sw, long total) {
+#pragma clang fp contract(off)
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= total) return;
+  const long per_frame = (long)OH * OW;
+  const long frame = g / per_frame;
+  const int r = (int)(g - frame * per_frame), oh = r / OW, ow = r - oh * OW;
+  const int b = (int)(frame / Tmax), t = (int)(frame - (long)b * Tmax);
+  float v[3] = {0.f, 0.f, 0.f};
+  if (t < len[b]) {
+    const unsigned char* f = in + frame * H * W * 3;
+    if (OH == H && OW == W) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[c] = (float)f[((long)oh * W + ow) * 3 + c] / 255.f;
+    } else {
+      int h0, h1, w0, w1;
+      float lh0, lh1, lw0, lw1;
+      lin_idx(oh, H, sh, h0, h1, lh0, lh1);
+      lin_idx(ow, W, sw, w0, w1, lw0, lw1);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float a = (float)f[((long)h0 * W + w0) * 3 + c] / 255.f, bb = (float)f[((long)h0 * W + w1) * 3 + c] / 255.f;
+        const float cc = (float)f[((long)h1 * W + w0) * 3 + c] / 255.f, d = (float)f[((long)h1 * W + w1) * 3 + c] / 255.f;
+        const float t0 = a * lw0 + bb * lw1;
+        const float t1 = cc * lw0 + d * lw1;
+        v[c] = t0 * lh0 + t1 * lh1;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const long o = NHWC ? g * 3 + c : ((frame * 3 + c) * OH + oh) * OW + ow;
+    out[o] = (T)v[c];
+  }
+}
+
+template <typename T>
+void launch_prep(const unsigned char* in, const int* len, void* out, bool nhwc, int Tmax, int H, int W, int OH, int OW,
+                 long total, hipStream_t st) {
+  const dim3 grid((unsigned)((total + 255) / 256));
+  const float sh = (float)H / (float)OH, sw = (float)W / (float)OW;
+  if (nhwc)
+    hipLaunchKernelGGL((frames_prep_kernel<T, true>), grid, dim3(256), 0, st, in, len, (T*)out, Tmax, H, W, OH, OW, sh,
+                       sw, total);
+  else
+    hipLaunchKernelGGL((frames_prep_kernel<T, false>), grid, dim3(256), 0, st, in, len, (T*)out, Tmax, H, W, OH, OW, sh,
+                       sw, total);
+}
+
 }  // namespace
 
 extern "C" {
+
+// B clips of up to Tmax uint8 [H][W][3] frames (len: device int32 [B]) -> out at OH x OW:
+// dtype XCP_F32 / XCP_BF16, nhwc 0 = [B][Tmax][3][OH][OW], 1 = [B][Tmax][OH][OW][3]
+int xcp_frames_prep(const unsigned char* in, const int* len, void* out, int B, int Tmax, int H, int W, int OH, int OW,
+                    int dtype, int nhwc, hipStream_t st) {
+  if (B <= 0 || Tmax <= 0 || OH <= 0 || OW <= 0) return XCP_OK;
+  if (H <= 0 || W <= 0 || (dtype != XCP_F32 && dtype != XCP_BF16)) return XCP_EINVAL;
+  const long total = (long)B * Tmax * OH * OW;
+  if (dtype == XCP_F32)
+    launch_prep<float>(in, len, out, nhwc != 0, Tmax, H, W, OH, OW, total, st);
+  else
+    launch_prep<bf16>(in, len, out, nhwc != 0, Tmax, H, W, OH, OW, total, st);
+  return (int)hipGetLastError();
+}
 
 // B clips of up to Tmax frames (len: device int32 [B]); W must be a multiple of 4
 int xcp_frames_u8_to_f32(const unsigned char* in, const int* len, float* out, int B, int Tmax, int H, int W,

@@ -283,6 +283,26 @@ def frames_u8_to_f32(frames, lengths, out):
     _lib.call("xcp_frames_u8_to_f32", _p(frames), _p(lengths), _p(out), B, T, H, W, stream())
 
 
+def frames_prep(frames, lengths, size=None, dtype=torch.float32, channels_last=False):
+    """uint8 [B, T, H, W, 3] frames (device) + int32 [B] lengths -> the clip tensor
+    [B, T, 3, OH, OW] of ``dtype`` = F.interpolate(frames / 255, size, bilinear,
+    align_corners=False) (no resize when size is None or (H, W)); zero past each clip's length.
+    channels_last: the storage is [B, T, OH, OW, 3] (the returned tensor is its permuted view)."""
+    check_gpu(frames, lengths)
+    B, T, H, W, C = frames.shape
+    if C != 3 or frames.dtype != torch.uint8 or lengths.dtype != torch.int32 or dtype not in DT:
+        raise ValueError("frames_prep: expects uint8 [B,T,H,W,3], int32 [B], fp32 / bf16 output")
+    OH, OW = (H, W) if size is None else size
+    frames = frames.contiguous()
+    if channels_last:
+        out = torch.empty((B, T, OH, OW, 3), device=frames.device, dtype=dtype)
+    else:
+        out = torch.empty((B, T, 3, OH, OW), device=frames.device, dtype=dtype)
+    _lib.call("xcp_frames_prep", _p(frames), _p(lengths), _p(out), B, T, H, W, OH, OW, DT[dtype],
+              1 if channels_last else 0, stream())
+    return out.permute(0, 1, 4, 2, 3) if channels_last else out
+
+
 def resize_bilinear(x, size):
     """F.interpolate(x, size, mode="bilinear", align_corners=False) for fp32 NCHW x on the GPU
     (the XceptionLSTMA front end, XceptionLSTMA.py:46)."""

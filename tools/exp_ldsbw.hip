@@ -1,0 +1,88 @@
+// Microbenchmark (tools only, not product): per-CU fill bandwidth of LDS-DMA
+// (global_load_lds_dwordx4) by bytes in flight,
+// from an HBM-sized stream and from an L2-resident buffer.  One 512-thread workgroup per CU;
+// each step moves 8 KB (16 B per thread); DEPTH steps are kept in flight per thread with a
+// counted vmcnt (no barriers, no consumer).
+#include <hip/hip_runtime.h>
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if constexpr (N == 15) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+}
+
+template <int DEPTH, bool DMA>
+__global__ __launch_bounds__(512) void fill_kernel(const char* __restrict__ src, long wg_bytes, long wrap, int* out) {
+  __shared__ __attribute__((aligned(16))) char smem[DEPTH * 8192];
+  const int tid = threadIdx.x, w = tid >> 6;
+  const long base = ((long)blockIdx.x * wg_bytes) % wrap;
+  const int steps = (int)(wg_bytes / 8192);
+  int4 acc = {0, 0, 0, 0};
+  for (int s = 0; s < steps; ++s) {
+    const char* p = src + (base + (long)s * 8192) % wrap + tid * 16;
+    if constexpr (DMA) {
+      char* d = smem + (s % DEPTH) * 8192 + w * 1024;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                       (void __attribute__((address_space(3)))*)d, 16, 0, 0);
+    }
+    wait_vm<DEPTH - 1>();
+  }
+  wait_vm<0>();
+  if (DMA) acc.x = smem[tid];
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x7fffffff) out[0] = 1;
+}
+
+
+// register staging: DEPTH 16-B loads per thread in flight (unrolled ring), each stored to LDS
+// with ds_write_b128 when it lands.  MIX: waves 0-3 use this path, waves 4-7 LDS-DMA.
+template <int DEPTH, bool MIX>
+__global__ __launch_bounds__(512) void fill_reg_kernel(const char* __restrict__ src, long wg_bytes, long wrap, int* out) {
+  __shared__ __attribute__((aligned(16))) char smem[16 * 8192];
+  const int tid = threadIdx.x, w = tid >> 6;
+  const long base = ((long)blockIdx.x * wg_bytes) % wrap;
+  const int steps = (int)(wg_bytes / 8192);
+  if (MIX && w >= 4) {
+    for (int s = 0; s < steps; ++s) {
+      const char* p = src + (base + (long)s * 8192) % wrap + tid * 16;
+      char* d = smem + (s % 8) * 8192 + w * 1024;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                       (void __attribute__((address_space(3)))*)d, 16, 0, 0);
+      wait_vm<7>();
+    }
+    wait_vm<0>();
+    return;
+  }
+  int4 v[DEPTH];
+#pragma unroll
+  for (int j = 0; j < DEPTH; ++j) v[j] = *reinterpret_cast<const int4*>(src + (base + (long)j * 8192) % wrap + tid * 16);
+  for (int s = 0; s + DEPTH < steps; s += DEPTH) {
+#pragma unroll
+    for (int j = 0; j < DEPTH; ++j) {
+      *reinterpret_cast<int4*>(smem + ((s + j) % 16) * 8192 + tid * 16) = v[j];
+      v[j] = *reinterpret_cast<const int4*>(src + (base + (long)(s + j + DEPTH) * 8192) % wrap + tid * 16);
+    }
+  }
+  int4 acc = v[0];
+#pragma unroll
+  for (int j = 1; j < DEPTH; ++j) acc.x ^= v[j].x;
+  if (acc.x == 0x7fffffff) out[0] = smem[tid];
+}
+
+extern "C" int exp_fill(int depth, int dma, const void* src, long wg_bytes, long wrap, int* out, int grid,
+                        hipStream_t st) {
+#define L(D, M) hipLaunchKernelGGL((fill_kernel<D, M>), dim3(grid), dim3(512), 0, st, (const char*)src, wg_bytes, wrap, out)
+  if (dma) {
+    switch (depth) { case 1: L(1, true); break; case 2: L(2, true); break; case 4: L(4, true); break;
+                     case 8: L(8, true); break; case 16: L(16, true); break; default: return 1; }
+  } else if (dma == 0) {
+#define R(D, X) hipLaunchKernelGGL((fill_reg_kernel<D, X>), dim3(grid), dim3(512), 0, st, (const char*)src, wg_bytes, wrap, out)
+    switch (depth) { case 2: R(2, false); break; case 4: R(4, false); break; case 8: R(8, false); break; default: return 1; }
+  } else {
+    switch (depth) { case 2: R(2, true); break; case 4: R(4, true); break; case 8: R(8, true); break; default: return 1; }
+#undef R
+  }
+#undef L
+  return (int)hipGetLastError();
+}

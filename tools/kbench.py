@@ -79,6 +79,41 @@ def main():
         P = torch.empty(S * C * C, device=dev)
         rep(f"gemm_tn kernel only S={S}", timeit(lambda: ops.gemm_tn(D, X, P, M, C, C, S, rps)), flops=2.0 * M * C * C)
         rep(f"reduce_slabs S={S}", timeit(lambda: ops.reduce_slabs(P, S, C * C, out)), 4 * S * C * C)
+    if "ksweep" in sel:
+        # NT 256x256 kernel: N = 1024 (4 column tiles), M = 64 R row tiles -> exactly R rounds of
+        # 256 workgroups; time vs rounds and vs K separates the per-tile fixed cost (prologue
+        # fill + epilogue) from the per-K-tile main-loop cost
+        Kmax, Nn = 3072, 1024
+        Xk = torch.randn(256 * 64 * 4, Kmax, device=dev, generator=g).to(dt)
+        Wk = (torch.randn(Nn, Kmax, device=dev, generator=g) / 27).to(dt)
+        Yk = torch.empty(256 * 64 * 4, Nn, device=dev, dtype=dt)
+        for R in (1, 2, 4):
+            for K in (256, 768, 1536, 3072):
+                m = 256 * 64 * R
+                stk = torch.empty(ops.nt_stat_rows(m) * 2 * Nn, device=dev)
+                for stats in (stk, None):
+                    Xv = Xk[:m].narrow(1, 0, K)
+                    rep(f"nt R={R} K={K} stats={stats is not None}",
+                        timeit(lambda: ops.gemm_nt(Xv, Wk.narrow(1, 0, K), Yk[:m], m, Nn, K, stats=stats, lda=Kmax,
+                                                   ldb=Kmax)), flops=2.0 * m * Nn * K)
+        del Xk, Wk, Yk
+        # TN 256x256 kernel: 1024 x 1024 output (16 tiles) x 16 splits = 256 workgroups, rows per split swept
+        for rps in (512, 1024, 2048, 4096, 8192):
+            m = rps * 16
+            Gt = torch.randn(m, 1024, device=dev, generator=g).to(dt)
+            Xt = torch.randn(m, 1024, device=dev, generator=g).to(dt)
+            P = torch.empty(16 * 1024 * 1024, device=dev)
+            rep(f"tn rows/split={rps}", timeit(lambda: ops.gemm_tn(Gt, Xt, P, m, 1024, 1024, 16, rps)),
+                flops=2.0 * m * 1024 * 1024)
+            del Gt, Xt, P
+    if "nt_only" in sel:      # one kernel for the PMC passes
+        st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
+        rep("gemm_nt 728x728 +stats", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=st2)), flops=2.0 * M * C * C)
+    if "tn_only" in sel:
+        rps = ops._lib.call("xcp_gemm_tn_rows_per_split", 1, 0, M, C, C, 0)
+        S = (M + rps - 1) // rps
+        P = torch.empty(S * C * C, device=dev)
+        rep(f"gemm_tn kernel only S={S}", timeit(lambda: ops.gemm_tn(D, X, P, M, C, C, S, rps)), flops=2.0 * M * C * C)
     if "tnshape" in sel:   # the step's weight-gradient shapes on both tiles
         for (m, n, k) in ((5531904, 128, 128), (5531904, 128, 64), (1401856, 256, 256), (1401856, 256, 128),
                           (350464, 728, 256), (350464, 728, 728), (92416, 1024, 728), (25600, 2048, 1536)):
