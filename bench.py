@@ -14,6 +14,10 @@ Other configurations (secondary lines, BASELINE.json configs):
                      (BCEWithLogits, Adam) -> frames/s
   --model lstma    : C4, XceptionLSTMA(512) on MFCC clips [b, 120, 3, 13] resized to 64^2
                      on the GPU, frozen backbone as shipped, Adam lr 1e-4 (train_audio.py:33-44)
+  --model auface   : C5, the train_au_face.py step (xcp/auface.py) on the build-defined
+                     AUFaceCrossDetector: 32 clips/GPU x 75 face frames of 128^2 + 17 AU crops of
+                     64^2, autocast + GradScaler, accumulation 4, AdamW, OneCycleLR, averaged
+                     model; a step is one micro-batch (the optimizer steps on every 4th)
 
 Launch: ``python bench.py [--gpus N --steps K --warmup W]``.  Under torch.distributed.run
 (WORLD_SIZE set) one process drives one GPU; with --gpus N > 1 and no WORLD_SIZE this
@@ -42,7 +46,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", choices=["lstmv", "lstma", "xception"], default="lstmv")
+    ap.add_argument("--model", choices=["lstmv", "lstma", "xception", "auface"], default="lstmv")
+    ap.add_argument("--aus", type=int, default=17, help="auface: AU crops per clip")
+    ap.add_argument("--au-size", type=int, default=64, help="auface: AU crop size")
     ap.add_argument("--batch", type=int, default=None, help="clips (frames for xception) per GPU")
     ap.add_argument("--frames", type=int, default=None, help="frames per clip (default 16; 120 for lstma)")
     ap.add_argument("--size", type=int, default=299)
@@ -57,6 +63,11 @@ def parse():
                          "clip_grad_norm_ + torch.optim.Adam(fused=True)")
     a = ap.parse_args()
     audio = a.model == "lstma"
+    if a.model == "auface":
+        a.frames = a.frames or 75
+        a.batch = a.batch or 32
+        a.size = 128 if a.size == 299 else a.size
+        a.mode = a.mode or "unfrozen"
     a.frames = a.frames or (120 if audio else 16)
     a.batch = a.batch or (64 if a.model == "xception" else 16)
     a.mode = a.mode or ("frozen" if audio else "unfrozen" if a.model == "xception" else "both")
@@ -250,6 +261,20 @@ class Run:
         self.args, self.mode, self.world = args, mode, world
         torch.manual_seed(0)
         B, T, S = args.batch, args.frames, args.size
+        self.dev = dev
+        if args.model == "auface":
+            from Models.AUFaceModel import AUFaceCrossDetector
+            from xcp.auface import AUFaceTrainer
+            self.model = AUFaceCrossDetector(num_aus=max(17, args.aus)).to(dev)
+            self.trainer = AUFaceTrainer(self.model, samples_per_cls=(1000, 1000), steps_per_epoch=1 << 20)
+            self.trainer.train()
+            g = torch.Generator(device=dev).manual_seed(1234 + rank)
+            self.batch = (torch.rand((B, 3, T, S, S), generator=g, device=dev),
+                          torch.rand((B, args.aus, 3, args.au_size, args.au_size), generator=g, device=dev),
+                          torch.randint(0, 2, (B,), generator=g, device=dev),
+                          torch.ones(B, args.aus, device=dev), torch.rand((B, args.aus), generator=g, device=dev))
+            self.i = 0
+            return
         if args.model == "xception":
             from Models.Xception import xception
             model = xception(num_classes=1)
@@ -285,10 +310,13 @@ class Run:
             self.x = torch.rand((B, T, 3, S, S), generator=g, device=dev)
         gl = torch.Generator(device=dev).manual_seed(4321 + rank)
         self.y = torch.randint(0, 2, (B, 1), generator=gl, device=dev).float()
-        self.dev = dev
 
     def step(self):
         from xcp import ddp
+        if self.args.model == "auface":
+            loss, _, _ = self.trainer.micro_step(self.i, 1 << 30, self.batch)
+            self.i += 1
+            return loss
         self.buckets.zero()
         ddp.broadcast_buffers(self.model)
         if self.args.model == "xception":
@@ -351,7 +379,7 @@ def main():
     from xcp import ops
     xcp.set_compute_dtype(args.dtype)
     xcp.load_library()
-    audio, single = args.model == "lstma", args.model == "xception"
+    audio, single, fusion = args.model == "lstma", args.model == "xception", args.model == "auface"
     B, T, S = args.batch, args.frames, args.size
     frames = B if single else B * T
     modes = ["unfrozen", "frozen"] if args.mode == "both" else [args.mode]
@@ -362,7 +390,7 @@ def main():
             log(f"{args.model} {mode}: building model")
         run = Run(args, mode, dev, rank, world)
         timer = None
-        if not args.no_kernel_timing and mode == modes[0] and not audio:
+        if not args.no_kernel_timing and mode == modes[0] and not audio and not fusion:
             hm = middle_hw(S)
             timer = ops.KernelTimer({"pw_gemm_728": lambda name, a: name == "gemm_nt" and a["M"] == frames * hm * hm
                                      and a["N"] == 728 and a["K"] == 728 and a["stats"] is not None,
@@ -383,7 +411,7 @@ def main():
         hm = middle_hw(S)
         M = frames * hm * hm
         roof, extra = None, {}
-        traffic = {} if (audio or single) else pmc_traffic()   # the committed PMC passes are of the headline bench
+        traffic = {} if (audio or single or fusion) else pmc_traffic()   # the committed PMC passes are of the headline bench
         if timer is not None:
             pw_ms, dw_ms = timer.mean_ms("pw_gemm_728"), timer.mean_ms("dw_fwd_728")
             if pw_ms:
@@ -404,7 +432,7 @@ def main():
                                         "traffic_source": traffic.get("dw_fwd_kernel", (None, None))[1],
                                         "kernel": f"dw_fwd_kernel<bf16> (depthwise 3x3 C=728 @{hm}x{hm})",
                                         "bytes_per_launch": byts, "avg_launch_ms": round(dw_ms, 4)}
-        if not audio and args.dtype == "bf16":
+        if not audio and not fusion and args.dtype == "bf16":
             ideal, fl, by = step_roofline(S, frames, head == "unfrozen")
             ms = 1e3 * elapsed / steps
             extra["step_roofline"] = {"ideal_ms": round(ideal, 3), "ms_per_step": round(ms, 3),
@@ -420,7 +448,12 @@ def main():
                 ideal, _, _ = step_roofline(S, frames, False)
                 fz["step_roofline_frac"] = round(ideal / (1e3 * e2 / s2), 4)
             extra["frozen"] = fz
-        if audio:
+        if fusion:
+            metric = (f"clips/sec (node) AU+face fusion (build-defined AUFaceCrossDetector) {T}x{S}x{S} + "
+                      f"{args.aus} AU x {args.au_size}x{args.au_size} {args.dtype} train")
+            name, shape = "AUFaceCrossDetector(17, 512, 512, 256)", (f"{T} frames x 3x{S}x{S} + {args.aus} AU crops x "
+                                                                     f"3x{args.au_size}x{args.au_size}")
+        elif audio:
             metric = f"clips/sec (node) XceptionLSTMA MFCC {T}x3x13 (64x64) {args.dtype} train"
             name, shape = "XceptionLSTMA(hidden=512)", f"{T} MFCC frames x 3x13 -> 64x64"
         elif single:
@@ -436,14 +469,17 @@ def main():
                "data": f"synthetic (on-device {'N(0,1) MFCC' if audio else 'U[0,1)'} inputs, seeded per rank; "
                        "random-init weights, Xception.py:154-160 scheme)",
                "config": {"workload": f"{name} {head}-backbone train step, {B} {'frames' if single else 'clips'}/GPU x "
-                                      f"{shape}, {'BCEWithLogits' if single else 'BCE'} + clip 1.0 + Adam",
+                                      f"{shape}" + ("" if fusion else f", {'BCEWithLogits' if single else 'BCE'} + "
+                                                                      "clip 1.0 + Adam"),
                           "global_batch": B * world, "frames": 1 if single else T, "size": S, "mode": head,
-                          "optimizer": "clip 1.0 + Adam, " + ("xcp FusedAdamClip" if args.optim == "fused"
-                                                               else "torch fused Adam"),
+                          "optimizer": ("CB-focal(ArcFace) + align + temporal losses, autocast + GradScaler, "
+                                        "accumulation 4, clip 1.0, AdamW, OneCycleLR, averaged model (train_au_face.py)"
+                                        if fusion else "clip 1.0 + Adam, " + ("xcp FusedAdamClip" if args.optim == "fused"
+                                                                              else "torch fused Adam")),
                           "parallelism": f"dp{world}"},
                "roofline": roof, "loss": round(loss, 5)}
         out.update(extra)
-        if args.cpu_baseline == "on" and world == 1 and not single:
+        if args.cpu_baseline == "on" and world == 1 and not single and not fusion:
             out["cpu_baseline"] = cpu_baseline(args, T)
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -7,8 +7,8 @@ architecture is unknown.  This build defines one with the call contract the scri
     model = AUFaceCrossDetector(num_aus=17, face_dim=512, au_dim=512, lstm_hidden=256)
     logits, v_tokens, au_tokens = model(videos, au_patches, au_mask=None, au_weight=None)
 
-* ``videos``: [B, 3, T, H, W] (the layout train_au_face.py:643-644 normalises to) or
-  [B, T, 3, H, W]; ``au_patches``: [B, A, 3, h, w] (A <= num_aus AU crops per clip);
+* ``videos``: [B, 3, T, H, W] (the layout train_au_face.py:643-644 and test_au_face.py:161-162
+  normalise every batch to); ``au_patches``: [B, A, 3, h, w] (A <= num_aus AU crops per clip);
   ``au_mask`` [B, A] (> 0: present), ``au_weight`` [B, A] per-AU confidence.
 * ``v_tokens`` [B, T, face_dim]: per-frame face tokens, ``au_tokens`` [B, A, au_dim]: per-AU
   tokens (the harness pools both, train_au_face.py:659-661, and regularises their agreement
@@ -48,12 +48,10 @@ class AUFaceCrossDetector(nn.Module):
 
     @staticmethod
     def frames_first(videos):
-        """[B, 3, T, H, W] -> [B, T, 3, H, W] (a [B, T, 3, H, W] input passes through)."""
-        if videos.dim() != 5:
-            raise ValueError(f"videos must be 5-D, got {tuple(videos.shape)}")
-        if videos.size(1) == 3 and videos.size(2) != 3:
-            return videos.permute(0, 2, 1, 3, 4)
-        return videos
+        """[B, 3, T, H, W] -> [B, T, 3, H, W]."""
+        if videos.dim() != 5 or videos.size(1) != 3:
+            raise ValueError(f"videos must be [B, 3, T, H, W], got {tuple(videos.shape)}")
+        return videos.permute(0, 2, 1, 3, 4)
 
     def face_tokens(self, videos):
         v = self.frames_first(videos)

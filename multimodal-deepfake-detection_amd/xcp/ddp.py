@@ -45,6 +45,7 @@ class GradBuckets:
             self.views[p] = (off, p.numel())
             off += p.numel()
         self.overlap = self.world > 1
+        self.sync = True   # False: gradient accumulation micro-batch, no all-reduce launched
         self._active_key = None
         self._pending = []
         self._hooked = set()
@@ -112,7 +113,7 @@ class GradBuckets:
     def ready(self, params, side_stream=None):
         """Gradients of ``params`` are final (enqueued on the current stream, weight gradients
         possibly on ``side_stream``).  Launches the all-reduce of every bucket this completes."""
-        if not self.overlap:
+        if not self.overlap or not self.sync:
             return
         waited = False
         for p in params:

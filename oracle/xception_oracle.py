@@ -247,3 +247,30 @@ def clip_step(sd, clips, labels, unfrozen, audio=False, optim=None):
 def kaiming_like_init(shape, out_channels, kh, kw, gen):
     """Xception.py:154-158 init for a conv weight (N(0, sqrt(2/(kh*kw*out_channels))))."""
     return torch.randn(shape, generator=gen) * math.sqrt(2.0 / (kh * kw * out_channels))
+
+
+def auface_forward(videos, aus, sd, au_mask=None, au_weight=None, num_heads=8, train=True):
+    """Models/AUFaceModel.py AUFaceCrossDetector.forward (the build-defined C5 model; the
+    reference's AUFaceCrossDetector is absent) restated functionally.  ``videos`` [B,T,3,H,W],
+    ``aus`` [B,A,3,h,w]; returns (logits [B,2], v_tokens [B,T,Df], au_tokens [B,A,Da])."""
+    B, T = videos.shape[:2]
+    A = aus.shape[1]
+    f = backbone_forward(videos.reshape(B * T, *videos.shape[2:]), sd, train, None, prefix="face_backbone.")
+    v = F.linear(f, sd["face_proj.weight"], sd["face_proj.bias"]).view(B, T, -1)
+    a = backbone_forward(aus.reshape(B * A, *aus.shape[2:]), sd, train, None, prefix="au_backbone.")
+    au = F.linear(a, sd["au_proj.weight"], sd["au_proj.bias"]).view(B, A, -1) + sd["au_embed"][:A]
+    if au_weight is not None:
+        au = au * au_weight.unsqueeze(-1)
+    kpm = None
+    if au_mask is not None:
+        kpm = au_mask <= 0
+        kpm = kpm & ~kpm.all(dim=1, keepdim=True)
+    E = v.shape[-1]
+    fused = F.multi_head_attention_forward(
+        v.transpose(0, 1), au.transpose(0, 1), au.transpose(0, 1), E, num_heads, sd["cross.in_proj_weight"],
+        sd["cross.in_proj_bias"], None, None, False, 0.0, sd["cross.out_proj.weight"], sd["cross.out_proj.bias"],
+        training=train, key_padding_mask=kpm, need_weights=False)[0].transpose(0, 1)
+    out, _, _ = lstm_forward(v + fused, sd["temporal.weight_ih_l0"], sd["temporal.weight_hh_l0"],
+                             sd["temporal.bias_ih_l0"], sd["temporal.bias_hh_l0"])
+    logits = F.linear(torch.cat([out[:, -1], fused.mean(1)], dim=1), sd["classifier.weight"], sd["classifier.bias"])
+    return logits, v, au
