@@ -402,6 +402,16 @@ XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n
 // t+1, Q0 retires B-right, Q1 retires A-bot.  Wave group 1 runs one barrier behind
 // group 0 (its MFMA cluster overlaps group 0's reads and load issue).
 constexpr int K_OP = 256 * 128;                // one operand, one slot (32 KB)
+// raw buffer resources for LDS-DMA through buffer_load ... lds: SGPR base + one 32-bit VGPR
+// offset per lane (cheaper to form and issue than a 64-bit global address).  Lanes only ever
+// form in-range offsets or BUF_OOB (>= num_records: the load returns zeros).  num_records is
+// the 2 GB maximum rather than the operand's span: measured, the exact span made the NT
+// kernel ~10 % slower (tools/gemm_exp.py).  Used while every operand spans < 2 GB
+// (xcp_gemm_nt / xcp_gemm_tn check; the 64-bit global-address form otherwise).
+constexpr unsigned BUF_OOB = 0x80000000u;
+constexpr long BUF_LIMIT = 0x7fffffffL;
+constexpr int BUF_RECORDS = 0x7fffffff;
+constexpr int BUF_DWORD3 = 0x00020000;   // gfx9 raw buffer descriptor word 3
 constexpr int K_SLOT = 2 * K_OP;
 
 XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
@@ -410,6 +420,7 @@ XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
   else wait_vmcnt<0>();
 }
 
+template <bool BUF>
 __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   constexpr bool STAG = true;   // wave group 1 runs one barrier behind group 0
   __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
@@ -429,6 +440,7 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   const int brow = 64 * (w >> 1) + 16 * (w & 1);
   const int lr = lane >> 3;
   const bf16* src[4][2];   // [half-tile][i]
+  unsigned voff[4][2];     // BUF: byte offsets into the A / B buffer resources (OOB -> zeros)
   int kc8[4][2];
 #pragma unroll
   for (int h = 0; h < 4; ++h)
@@ -439,9 +451,17 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
       kc8[h][i] = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
       src[h][i] = isA ? A + (long)min(m0 + row, a.M - 1) * a.lda + kc8[h][i]
                       : B + (long)min(n0 + row, a.N - 1) * a.ldb + kc8[h][i];
+      const bool ok = isA ? m0 + row < a.M : n0 + row < a.N;
+      voff[h][i] = ok ? (unsigned)(isA ? ((long)(m0 + row) * a.lda + kc8[h][i]) * 2
+                                       : ((long)(n0 + row) * a.ldb + kc8[h][i]) * 2)
+                      : BUF_OOB;
     }
   const void* zero = g_zero16;
   asm volatile("" : "+v"(zero));
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
   auto glds = [](const void* p, char* dst) {
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
                                      (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
@@ -452,7 +472,14 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
     const int row0 = isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0);
     char* d = smem + (kt & 1) * K_SLOT + (isA ? 0 : K_OP) + row0 * 128;
     const int kb = kt * 64;
-    if (kb + 64 <= a.K) {
+    if constexpr (BUF) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const unsigned o = kb + kc8[h][i] < a.K ? voff[h][i] + kb * 2 : BUF_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, (__attribute__((address_space(3))) void*)(d + i * 1024),
+                                                 16, o, 0, 0, 0);
+      }
+    } else if (kb + 64 <= a.K) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) glds(src[h][i] + kb, d + i * 1024);
     } else {
@@ -733,6 +760,7 @@ XCP_DEV int tswz(int m, int col) {             // byte offset of bf16 column col
   return m * 512 + ((((col >> 3) ^ ((m & 7) << 1))) << 4) + (col & 7) * 2;
 }
 
+template <bool BUF>
 __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[T_RING * T_STEP];
   const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
@@ -762,6 +790,10 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
                                      (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
   };
+  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.G), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.X), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
   // operand isG of step st into ring slot sl
   auto issue = [&](bool isG, int st, int sl) {
     char* d = smem + sl * T_STEP + (isG ? 0 : T_HALF);
@@ -770,9 +802,17 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
       const int m = mbeg + st * 32 + rr[i];
       const int col = (isG ? n0 : k0) + lc[i] * 8;
       const bool ok = m < mend && col < (isG ? a.N : a.K);
-      const void* src = ok ? (isG ? (const void*)(G + (long)m * a.ldg + col) : (const void*)(X + (long)m * a.ldx + col))
-                           : zero;
-      glds(src, d + (4 * w + 2 * i) * 512);   // 1 KB = slab rows 4w+2i, +1
+      char* dst = d + (4 * w + 2 * i) * 512;   // 1 KB = slab rows 4w+2i, +1
+      if constexpr (BUF) {
+        const unsigned o = ok ? (unsigned)(((long)m * (isG ? a.ldg : a.ldx) + col) * 2) : BUF_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isG ? rG : rX, (__attribute__((address_space(3))) void*)dst, 16, o,
+                                                 0, 0, 0);
+      } else {
+        const void* src = ok ? (isG ? (const void*)(G + (long)m * a.ldg + col)
+                                    : (const void*)(X + (long)m * a.ldx + col))
+                             : zero;
+        glds(src, dst);
+      }
     }
   };
 
@@ -900,7 +940,11 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (nt_big(dtype, gmode, M, N, K, tile)) {
     const int tiles = xcp_cdiv(M, 256) * xcp_cdiv(N, 256);
-    hipLaunchKernelGGL(gemm_nt256k64_kernel, dim3(tiles), dim3(512), 0, stream, a);
+    const bool buf = ((long)(M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
+    if (buf)
+      hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(tiles), dim3(512), 0, stream, a);
+    else
+      hipLaunchKernelGGL(gemm_nt256k64_kernel<false>, dim3(tiles), dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(M, 128) * xcp_cdiv(N, NBN);
@@ -956,7 +1000,11 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
   if (tn_big(dtype, gmode, N, K, tile)) {
     if (rows_per_split % 32) return XCP_EINVAL;
     const dim3 grid(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S);
-    hipLaunchKernelGGL(gemm_tn256_kernel, grid, dim3(512), 0, stream, a);
+    const bool buf = ((long)(M - 1) * ldg + N) * 2 <= BUF_LIMIT && ((long)(M - 1) * ldx + K) * 2 <= BUF_LIMIT;
+    if (buf)
+      hipLaunchKernelGGL(gemm_tn256_kernel<true>, grid, dim3(512), 0, stream, a);
+    else
+      hipLaunchKernelGGL(gemm_tn256_kernel<false>, grid, dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(N, 128) * xcp_cdiv(K, 128) * S;

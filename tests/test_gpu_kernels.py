@@ -141,6 +141,31 @@ def test_gemm_tn(ops, gpu, dt, M, N, K, tile):
     assert rel_err(acc.view(N, K), ref + base.view(N, K)) < (1e-5 if dt == torch.float32 else 1e-3)
 
 
+def test_gemm_operands_over_2gb_global_address_path(ops, gpu):
+    """Operands spanning more than 2 GB take the 64-bit global-address LDS-DMA form of the
+    256x256 kernels (the 32-bit buffer-offset form covers the rest): NT and TN at
+    M = 1.5M rows x 728 channels (2.18 GB per operand) against fp32 torch on sampled rows /
+    the full weight gradient."""
+    M, C = 1_500_000, 728
+    g = torch.Generator(device=gpu).manual_seed(7)
+    X = (torch.rand(M, C, device=gpu, generator=g) - 0.5).to(torch.bfloat16)
+    W = ((torch.rand(C, C, device=gpu, generator=g) - 0.5) / 8).to(torch.bfloat16)
+    Y = torch.empty(M, C, device=gpu, dtype=torch.bfloat16)
+    ops.gemm_nt(X, W, Y, M, C, C, tile=2)
+    rows = torch.cat([torch.arange(0, 512, device=gpu), torch.arange(M - 512, M, device=gpu),
+                      torch.randint(0, M, (2048,), device=gpu, generator=g)])
+    ref = X[rows].float() @ W.float().t()
+    assert rel_err(Y[rows].float(), ref) < 1e-2
+    del Y
+    out = torch.empty(C * C, device=gpu)
+    ops.weight_grad(X, X, M, C, C, out, tile=2)
+    ref = torch.zeros(C, C, device=gpu)
+    for i in range(0, M, 250_000):
+        xs = X[i:i + 250_000].float()
+        ref += xs.t() @ xs
+    assert rel_err(out.view(C, C), ref) < 1e-3
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("act", [0, 1, 2])
 @pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9), (1, 64, 147), (2, 256, 74),

@@ -31,6 +31,10 @@ XCP_DEV void xcp_fake_glds(const void __attribute__((address_space(1)))* p, void
                            int, int, int) {
   asm volatile("" :: "v"(p));
 }
+XCP_DEV void xcp_fake_bload(__amdgpu_buffer_rsrc_t r, void __attribute__((address_space(3)))* d, int, unsigned o, int,
+                            int, int) {
+  asm volatile("" :: "v"(o));
+}
 
 namespace {
 
@@ -412,6 +416,16 @@ XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n
 // t+1, Q0 retires B-right, Q1 retires A-bot.  Wave group 1 runs one barrier behind
 // group 0 (its MFMA cluster overlaps group 0's reads and load issue).
 constexpr int K_OP = 256 * 128;                // one operand, one slot (32 KB)
+// raw buffer resources for LDS-DMA through buffer_load ... lds: SGPR base + one 32-bit VGPR
+// offset per lane (cheaper to form and issue than a 64-bit global address).  Lanes only ever
+// form in-range offsets or BUF_OOB (>= num_records: the load returns zeros).  num_records is
+// the 2 GB maximum rather than the operand's span: measured, the exact span made the NT
+// kernel ~10 % slower (tools/gemm_exp.py).  Used while every operand spans < 2 GB
+// (xcp_gemm_nt / xcp_gemm_tn check; the 64-bit global-address form otherwise).
+constexpr unsigned BUF_OOB = 0x80000000u;
+constexpr long BUF_LIMIT = 0x7fffffffL;
+constexpr int BUF_RECORDS = 0x7fffffff;
+constexpr int BUF_DWORD3 = 0x00020000;   // gfx9 raw buffer descriptor word 3
 constexpr int K_SLOT = 2 * K_OP;
 
 XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
@@ -420,6 +434,7 @@ XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
   else wait_vmcnt<0>();
 }
 
+template <bool BUF>
 __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   constexpr bool STAG = true;   // wave group 1 runs one barrier behind group 0
   __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
@@ -439,6 +454,7 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   const int brow = 64 * (w >> 1) + 16 * (w & 1);
   const int lr = lane >> 3;
   const bf16* src[4][2];   // [half-tile][i]
+  unsigned voff[4][2];     // BUF: byte offsets into the A / B buffer resources (OOB -> zeros)
   int kc8[4][2];
 #pragma unroll
   for (int h = 0; h < 4; ++h)
@@ -449,9 +465,17 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
       kc8[h][i] = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
       src[h][i] = isA ? A + (long)min(m0 + row, a.M - 1) * a.lda + kc8[h][i]
                       : B + (long)min(n0 + row, a.N - 1) * a.ldb + kc8[h][i];
+      const bool ok = isA ? m0 + row < a.M : n0 + row < a.N;
+      voff[h][i] = ok ? (unsigned)(isA ? ((long)(m0 + row) * a.lda + kc8[h][i]) * 2
+                                       : ((long)(n0 + row) * a.ldb + kc8[h][i]) * 2)
+                      : BUF_OOB;
     }
   const void* zero = g_zero16;
   asm volatile("" : "+v"(zero));
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
   auto glds = [](const void* p, char* dst) {
     xcp_fake_glds((const void __attribute__((address_space(1)))*)p,
                                      (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
@@ -462,7 +486,14 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
     const int row0 = isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0);
     char* d = smem + (kt & 1) * K_SLOT + (isA ? 0 : K_OP) + row0 * 128;
     const int kb = kt * 64;
-    if (kb + 64 <= a.K) {
+    if constexpr (BUF) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const unsigned o = kb + kc8[h][i] < a.K ? voff[h][i] + kb * 2 : BUF_OOB;
+        xcp_fake_bload(isA ? rA : rB, (__attribute__((address_space(3))) void*)(d + i * 1024),
+                                                 16, o, 0, 0, 0);
+      }
+    } else if (kb + 64 <= a.K) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) glds(src[h][i] + kb, d + i * 1024);
     } else {
@@ -547,160 +578,6 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
     sync_mfma(1, bl, 0);
   }
   if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
-  epilogue256_regs(acc, a, m0, n0, wr, wc, fr, fg);
-}
-
-// ---------------------------------------------------------------------------------
-// 256x256 NT kernel with a deeper A ring: A (activations, streamed from HBM) in 3 LDS slots,
-// B (weights, L2-resident) in 2, 160 KB in all.  Per K-tile t the four phases issue
-//   Q0: B-left(t+1)   Q1: B-right(t+1)   Q2: A-top(t+2)   Q3: A-bot(t+2)
-// so each A half-tile is issued 4-5 phases before its first read (3 in the 2-slot ring),
-// B 3 phases (it comes from L2).  Loads retire in issue order, so B(t+1) is issued before
-// A(t+2): Q3(t) retires A(t+1) and B-left(t+1) with vmcnt(6) leaving B-right(t+1) and A(t+2)
-// in flight; Q0(t) retires B-right(t).  WAR: A(t+2) reuses the slot of A(t-1) (last read in
-// Q2(t-1)), B(t+1) the slot of B(t-1) (last read in Q1(t-1)).
-constexpr int KA_SLOTS = 3, KB_SLOTS = 2;
-
-__global__ __launch_bounds__(512) void gemm_nt256a3_kernel(NTArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[(KA_SLOTS + KB_SLOTS) * K_OP];
-  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
-  const int id = xcd_remap(blockIdx.x, gridM * gridN);
-  const int bn = id % gridN, bm = id / gridN;
-  const int m0 = bm * 256, n0 = bn * 256;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 2, wc = w & 3;
-  const bf16* A = reinterpret_cast<const bf16*>(a.A);
-  const bf16* B = reinterpret_cast<const bf16*>(a.B);
-  char* const sA = smem;
-  char* const sB = smem + KA_SLOTS * K_OP;
-
-  const int arow = (w < 4 ? 16 * w : 128 + 16 * (w - 4));
-  const int brow = 64 * (w >> 1) + 16 * (w & 1);
-  const int lr = lane >> 3;
-  const bf16* src[4][2];   // [half-tile][i]: 0 A-top, 1 B-left, 2 B-right, 3 A-bot
-  int kc8[4][2];
-#pragma unroll
-  for (int h = 0; h < 4; ++h)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bool isA = (h == 0 || h == 3);
-      const int row = (isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0)) + i * 8 + lr;
-      kc8[h][i] = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
-      src[h][i] = isA ? A + (long)min(m0 + row, a.M - 1) * a.lda + kc8[h][i]
-                      : B + (long)min(n0 + row, a.N - 1) * a.ldb + kc8[h][i];
-    }
-  const void* zero = g_zero16;
-  asm volatile("" : "+v"(zero));
-  auto glds = [](const void* p, char* dst) {
-    xcp_fake_glds((const void __attribute__((address_space(1)))*)p,
-                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
-  };
-  auto issue = [&](int h, int kt) {
-    const bool isA = (h == 0 || h == 3);
-    const int row0 = isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0);
-    char* d = (isA ? sA + (kt % KA_SLOTS) * K_OP : sB + (kt & 1) * K_OP) + row0 * 128;
-    const int kb = kt * 64;
-    if (kb + 64 <= a.K) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) glds(src[h][i] + kb, d + i * 1024);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) glds(kb + kc8[h][i] < a.K ? (const void*)(src[h][i] + kb) : zero, d + i * 1024);
-    }
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (a.K + 63) / 64;
-  // prologue: A(0), B(0) retired, A(1) in flight
-  issue(0, 0);
-  issue(3, 0);
-  issue(1, 0);
-  issue(2, 0);
-  if (nk > 1) {
-    issue(0, 1);
-    issue(3, 1);
-    wait_vmcnt<4>();
-  } else {
-    wait_vmcnt<0>();
-  }
-  __builtin_amdgcn_s_barrier();
-  if (wr == 1) __builtin_amdgcn_s_barrier();
-
-  const int fr = lane & 15, fg = lane >> 4;
-  bf16x8 af[4][2], bl[2][2], br[2][2];
-  auto mfma_q = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[ih * 4 + i][jh * 2 + j] =
-              xcp_fake_mfma(b[j][ks], af[i][ks], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
-  };
-  auto sync_mfma = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
-    __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    mfma_q(ih, b, jh);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
-  };
-  int sa_slot = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* sa = sA + sa_slot * K_OP;
-    const char* sb = sB + (kt & 1) * K_OP;
-    const bool b1 = kt + 1 < nk, a2 = kt + 2 < nk;
-    // Q0: A-top x B-left
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bl[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + j * 16 + fr, ks * 4 + fg));
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 16 + fr, ks * 4 + fg));
-    }
-    if (b1) {
-      issue(1, kt + 1);
-      wait_vmcnt<6>();                    // B-right(kt) for Q1
-    } else {
-      wait_vmcnt<0>();
-    }
-    sync_mfma(0, bl, 0);
-    // Q1: A-top x B-right
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        br[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + 32 + j * 16 + fr, ks * 4 + fg));
-    if (b1) issue(2, kt + 1);
-    sync_mfma(0, br, 1);
-    // Q2: A-bot x B-right
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
-    if (a2) issue(0, kt + 2);
-    sync_mfma(1, br, 1);
-    // Q3: A-bot x B-left; retire A(kt+1) and B-left(kt+1) for Q0(kt+1)
-    if (a2) {
-      issue(3, kt + 2);
-      wait_vmcnt<6>();
-    } else if (b1) {
-      wait_vmcnt<2>();
-    }
-    sync_mfma(1, bl, 0);
-    sa_slot = sa_slot == KA_SLOTS - 1 ? 0 : sa_slot + 1;
-  }
-  if (wr == 0) __builtin_amdgcn_s_barrier();
   epilogue256_regs(acc, a, m0, n0, wr, wc, fr, fg);
 }
 
@@ -897,6 +774,7 @@ XCP_DEV int tswz(int m, int col) {             // byte offset of bf16 column col
   return m * 512 + ((((col >> 3) ^ ((m & 7) << 1))) << 4) + (col & 7) * 2;
 }
 
+template <bool BUF>
 __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[T_RING * T_STEP];
   const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
@@ -926,6 +804,10 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
     xcp_fake_glds((const void __attribute__((address_space(1)))*)p,
                                      (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
   };
+  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.G), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.X), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
   // operand isG of step st into ring slot sl
   auto issue = [&](bool isG, int st, int sl) {
     char* d = smem + sl * T_STEP + (isG ? 0 : T_HALF);
@@ -934,9 +816,17 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
       const int m = mbeg + st * 32 + rr[i];
       const int col = (isG ? n0 : k0) + lc[i] * 8;
       const bool ok = m < mend && col < (isG ? a.N : a.K);
-      const void* src = ok ? (isG ? (const void*)(G + (long)m * a.ldg + col) : (const void*)(X + (long)m * a.ldx + col))
-                           : zero;
-      glds(src, d + (4 * w + 2 * i) * 512);   // 1 KB = slab rows 4w+2i, +1
+      char* dst = d + (4 * w + 2 * i) * 512;   // 1 KB = slab rows 4w+2i, +1
+      if constexpr (BUF) {
+        const unsigned o = ok ? (unsigned)(((long)m * (isG ? a.ldg : a.ldx) + col) * 2) : BUF_OOB;
+        xcp_fake_bload(isG ? rG : rX, (__attribute__((address_space(3))) void*)dst, 16, o,
+                                                 0, 0, 0);
+      } else {
+        const void* src = ok ? (isG ? (const void*)(G + (long)m * a.ldg + col)
+                                    : (const void*)(X + (long)m * a.ldx + col))
+                             : zero;
+        glds(src, dst);
+      }
     }
   };
 
@@ -1060,17 +950,15 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
-  if (tile < 0 || tile > 3) return XCP_EINVAL;
+  if (tile < 0 || tile > 2) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
-  if (tile == 3) {
-    if (dtype != XCP_BF16 || gmode != 0) return XCP_EINVAL;
-    const int tiles = xcp_cdiv(M, 256) * xcp_cdiv(N, 256);
-    hipLaunchKernelGGL(gemm_nt256a3_kernel, dim3(tiles), dim3(512), 0, stream, a);
-    return (int)hipGetLastError();
-  }
   if (nt_big(dtype, gmode, M, N, K, tile)) {
     const int tiles = xcp_cdiv(M, 256) * xcp_cdiv(N, 256);
-    hipLaunchKernelGGL(gemm_nt256k64_kernel, dim3(tiles), dim3(512), 0, stream, a);
+    const bool buf = ((long)(M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
+    if (buf)
+      hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(tiles), dim3(512), 0, stream, a);
+    else
+      hipLaunchKernelGGL(gemm_nt256k64_kernel<false>, dim3(tiles), dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(M, 128) * xcp_cdiv(N, NBN);
@@ -1126,7 +1014,11 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
   if (tn_big(dtype, gmode, N, K, tile)) {
     if (rows_per_split % 32) return XCP_EINVAL;
     const dim3 grid(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S);
-    hipLaunchKernelGGL(gemm_tn256_kernel, grid, dim3(512), 0, stream, a);
+    const bool buf = ((long)(M - 1) * ldg + N) * 2 <= BUF_LIMIT && ((long)(M - 1) * ldx + K) * 2 <= BUF_LIMIT;
+    if (buf)
+      hipLaunchKernelGGL(gemm_tn256_kernel<true>, grid, dim3(512), 0, stream, a);
+    else
+      hipLaunchKernelGGL(gemm_tn256_kernel<false>, grid, dim3(512), 0, stream, a);
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(N, 128) * xcp_cdiv(K, 128) * S;

@@ -86,3 +86,32 @@ extern "C" int exp_fill(int depth, int dma, const void* src, long wg_bytes, long
 #undef L
   return (int)hipGetLastError();
 }
+
+// GEMM-like gather: each 1-KB DMA instruction moves 8 rows x 128 B of a row-major matrix with
+// row stride `ld` bytes (lane l: row l/8, 16-B chunk l%8), K-chunk k advancing along the rows.
+__global__ __launch_bounds__(512) void gather_kernel(const char* __restrict__ src, long ld, int rows_per_wg, int kchunks,
+                                                     long wrap_rows, int* out) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * 8192];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const long row0 = ((long)blockIdx.x * rows_per_wg) % wrap_rows;
+  int s = 0;
+  for (int rb = 0; rb < rows_per_wg; rb += 64) {          // 64 rows per step (8 waves x 8)
+    for (int k = 0; k < kchunks; ++k, ++s) {
+      const long row = (row0 + rb + w * 8 + (lane >> 3)) % wrap_rows;
+      const char* p = src + row * ld + (long)k * 128 + (lane & 7) * 16;
+      char* d = smem + (s % 8) * 8192 + w * 1024;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                       (void __attribute__((address_space(3)))*)d, 16, 0, 0);
+      wait_vm<7>();
+    }
+  }
+  wait_vm<0>();
+  if (smem[tid] == 0x7f && tid == 9999) out[0] = 1;
+}
+
+extern "C" int exp_gather(const void* src, long ld, int rows_per_wg, int kchunks, long wrap_rows, int* out, int grid,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(512), 0, st, (const char*)src, ld, rows_per_wg, kchunks,
+                     wrap_rows, out);
+  return (int)hipGetLastError();
+}

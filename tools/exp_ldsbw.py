@@ -22,9 +22,28 @@ else:
     out = torch.zeros(4, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     grid, wgb = 256, 8 << 20
-    for wrap_name, wrap in (("hbm", 2 << 30), ("mall", 64 << 20), ("l2", 2 << 20)):
-        for dma in (1, 0, 2):
-            for depth in ((1, 2, 4, 8, 16) if dma == 1 else (2, 4, 8)):
+    lib.exp_gather.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_long,
+                               ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    # GEMM-like gathers: rows of ld bytes, 11 128-B K-chunks each (1408 B of every row)
+    for ld in (1536, 1456):
+        for wname, wrap_rows in (("hbm", (2 << 30) // 1536 - 8), ("l2", 1024)):
+            rows = 4096
+            f = lambda: lib.exp_gather(buf.data_ptr(), ld, rows, 11, wrap_rows, out.data_ptr(), grid, st)
+            for _ in range(2):
+                f()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(5):
+                f()
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / 5
+            byts = grid * rows * 11 * 128
+            print(f"gather ld={ld} {wname:4s} {byts / ms / 1e6:8.1f} GB/s  {byts / ms / 1e6 / grid:6.1f} GB/s/CU", flush=True)
+    for wrap_name, wrap in (("hbm", 2 << 30), ("l2", 2 << 20)):
+        for dma in (1,):
+            for depth in (2, 8):
                 f = lambda: lib.exp_fill(depth, dma, buf.data_ptr(), wgb, wrap, out.data_ptr(), grid, st)
                 for _ in range(2):
                     f()

@@ -29,6 +29,10 @@ XCP_DEV void xcp_fake_glds(const void __attribute__((address_space(1)))* p, void
                            int, int, int) {
   asm volatile("" :: "v"(p));
 }
+XCP_DEV void xcp_fake_bload(__amdgpu_buffer_rsrc_t r, void __attribute__((address_space(3)))* d, int, unsigned o, int,
+                            int, int) {
+  asm volatile("" :: "v"(o));
+}
 '''
 VARIANTS = {"base": (), "nomfma": ("mfma",), "noload": ("load",), "nomfma_noload": ("mfma", "load")}
 
@@ -42,6 +46,7 @@ def patched(kinds):
         extra += FAKE_MFMA
     if "load" in kinds:
         s = s.replace("__builtin_amdgcn_global_load_lds(", "xcp_fake_glds(")
+        s = s.replace("__builtin_amdgcn_raw_ptr_buffer_load_lds(", "xcp_fake_bload(")
         extra += FAKE_GLDS
     s = s.replace(head, '#include "' + os.path.join(SRC, "common.h") + '"\n' + extra, 1)
     return s
