@@ -916,6 +916,16 @@ namespace {
 // so tests can pin each kernel at small sizes.
 constexpr int TN_TARGET_WGS = 256;   // 256x256 weight-gradient workgroups (splits x tiles): one per CU
 
+int gpu_cus() {   // compute units of the current device (256 on MI355X)
+  static const int cus = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      n = 0;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
   return tile == 2 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
@@ -939,12 +949,30 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (tile < 0 || tile > 2) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (nt_big(dtype, gmode, M, N, K, tile)) {
-    const int tiles = xcp_cdiv(M, 256) * xcp_cdiv(N, 256);
-    const bool buf = ((long)(M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
+    // One 256x256 tile per CU per round.  When the last round would be less than 3/4 full
+    // (1,083 tiles = 4.23 rounds in the middle flow), its rows go to the 128x128 kernel
+    // instead: four times as many, smaller tiles, one launch after the full rounds
+    // (tile == 0 only; tile == 2 pins the 256 kernel for every row).
+    const int gridN = xcp_cdiv(N, 256), gridM = xcp_cdiv(M, 256), tiles = gridM * gridN;
+    const int cus = gpu_cus();
+    int mb = gridM;
+    if (tile == 0 && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3) mb = (tiles / cus) * cus / gridN;
+    NTArgs big = a;
+    big.M = min(M, mb * 256);
+    const bool buf = ((long)(big.M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
     if (buf)
-      hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(tiles), dim3(512), 0, stream, a);
+      hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(mb * gridN), dim3(512), 0, stream, big);
     else
-      hipLaunchKernelGGL(gemm_nt256k64_kernel<false>, dim3(tiles), dim3(512), 0, stream, a);
+      hipLaunchKernelGGL(gemm_nt256k64_kernel<false>, dim3(mb * gridN), dim3(512), 0, stream, big);
+    if (big.M < M) {
+      NTArgs rest = a;
+      rest.M = M - big.M;
+      rest.A = reinterpret_cast<const bf16*>(A) + (long)big.M * lda;
+      rest.C = reinterpret_cast<bf16*>(C) + (long)big.M * ldc;
+      if (stats) rest.stats = stats + (long)(big.M / 128) * 2 * N;
+      hipLaunchKernelGGL((gemm_nt_kernel<bf16, 0, 2, 2>), dim3(xcp_cdiv(rest.M, 128) * xcp_cdiv(N, NBN)), dim3(256), 0,
+                         stream, rest);
+    }
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(M, 128) * xcp_cdiv(N, NBN);

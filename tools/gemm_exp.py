@@ -101,7 +101,7 @@ def run():
         S = (M + rps - 1) // rps
         P = torch.empty(S * C * C, device=dev)
         z = (0, 0, 0, 0, 0, 1, 0)
-        for tile in (2,):
+        for tile in (2, 0):
             t = timeit(lambda: lib.xcp_gemm_nt(1, X.data_ptr(), C, Wp.data_ptr(), C, Y.data_ptr(), C, M, C, C,
                                                st.data_ptr(), *z, tile, stream))
             print(f"{name:14s} nt tile={tile}  {t:8.1f} us  {2.0 * M * C * C / t / 1e6:7.1f} TFLOP/s", flush=True)

@@ -67,7 +67,7 @@ def main():
             4 * tensor_bytes)
     if "gemm" in sel:
         st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
-        for tile in (2, 1):
+        for tile in (0, 2, 1):
             rep(f"gemm_nt 728x728 +stats tile={tile}", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=st2, tile=tile)),
                 flops=2.0 * M * C * C)
         out = torch.empty(C * C, device=dev)
@@ -106,6 +106,11 @@ def main():
             rep(f"tn rows/split={rps}", timeit(lambda: ops.gemm_tn(Gt, Xt, P, m, 1024, 1024, 16, rps)),
                 flops=2.0 * m * 1024 * 1024)
             del Gt, Xt, P
+    if "dwf_only" in sel:     # one kernel for the PMC passes
+        rep("dw_fwd act=2", timeit(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
+    if "dwb_only" in sel:
+        rep("dw_bwd act=2 +bnsums", timeit(lambda: ops.dw_bwd(2, D, X, Wt, sc, sh, Y, dW, N, H, W, C, bn_stats=st)),
+            3 * tensor_bytes)
     if "nt_only" in sel:      # one kernel for the PMC passes
         st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
         rep("gemm_nt 728x728 +stats", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=st2)), flops=2.0 * M * C * C)
