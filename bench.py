@@ -370,9 +370,18 @@ def main():
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # XCP_BENCH_BACKEND=gloo (test only): ranks may share a GPU (device = local rank modulo the
+    # visible devices), which exercises the whole multi-rank path on a one-GPU box; the
+    # measured configuration is always RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("XCP_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     import xcp
