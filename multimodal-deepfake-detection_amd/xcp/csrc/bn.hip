@@ -364,7 +364,16 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const T* __restrict__ Y, 
       }
     }
 #pragma unroll
-    for (int j = 0; j < CPT; ++j) { o[j] = m[j]; amax[op * C + c0 + j] = am[j]; }
+    for (int j = 0; j < CPT; ++j) o[j] = m[j];
+    if constexpr (CPT == 8) {   // the 8 argmax bytes in one 8-B store (c0 is a multiple of 8)
+      unsigned long long pk = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pk |= (unsigned long long)am[j] << (8 * j);
+      *reinterpret_cast<unsigned long long*>(amax + op * C + c0) = pk;
+    } else {
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) amax[op * C + c0 + j] = am[j];
+    }
   } else {
     VecIO<T, CPT>::load(Y + op * C + c0, o);
 #pragma unroll

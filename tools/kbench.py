@@ -170,6 +170,18 @@ def main():
               "track": False}
         rep("bn_backward (reduce+apply)", timeit(lambda: ops.bn_backward(D, X, M, C, bn, st, Y, dgm, dbt)),
             4 * tensor_bytes)
+    if "tailpool" in sel:   # block1's pooled tail at 147^2 x 128 (the largest)
+        Hp, Cp = 147, 128
+        OHp = (Hp - 1) // 2 + 1
+        Yp = torch.randn(N * Hp * Hp * Cp, device=dev, generator=g).to(dt)
+        Sp = torch.randn(N * OHp * OHp * Cp, device=dev, generator=g).to(dt)
+        Op = torch.empty_like(Sp)
+        Ap = torch.empty(N * OHp * OHp * Cp, device=dev, dtype=torch.uint8)
+        sc2, sh2 = sc[:Cp].contiguous(), sh[:Cp].contiguous()
+        byts = 2 * (Yp.numel() + 2 * Sp.numel()) + Ap.numel()
+        rep("tail_fwd pooled 147^2x128", timeit(lambda: ops.tail_fwd(Yp, sc2, sh2, True, Sp, sc2, sh2, Op, Ap, N, Hp, Hp,
+                                                                     Cp)), byts)
+        del Yp, Sp, Op, Ap
     if "tail" in sel:
         rep("tail_fwd identity", timeit(lambda: ops.tail_fwd(X, sc, sh, False, D, None, None, Y, None, N, H, W, C)),
             3 * tensor_bytes)
