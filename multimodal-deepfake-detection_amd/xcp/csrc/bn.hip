@@ -393,6 +393,90 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const T* __restrict__ Y, 
   VecIO<T, CPT>::store(Out + op * C + c0, o);
 }
 
+// Pooled block tail per 2 x 2 quad of outputs (2a..2a+1, 2b..2b+1): their four 3 x 3 s2
+// windows cover the 5 x 5 input pixels (4a-1..4a+3, 4b-1..4b+3), each loaded once (25
+// loads for 4 outputs instead of 36).  Every output visits its window in (ky, kx) order
+// with the same first-max rule as tail_fwd_kernel, so out and amax are identical to it.
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict__ Y, const float* s1, const float* t1,
+                                                             const T* __restrict__ S, const float* s2, const float* t2,
+                                                             T* __restrict__ Out, unsigned char* __restrict__ amax,
+                                                             int N, int H, int W, int C, int OH, int OW) {
+  const int CV = C / CPT;
+  const int QH = (OH + 1) / 2, QW = (OW + 1) / 2;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long)N * QH * QW * CV) return;
+  const int c0 = (int)(g % CV) * CPT;
+  const long q = g / CV;
+  const int qb = (int)(q % QW);
+  const long t = q / QW;
+  const int qa = (int)(t % QH);
+  const int n = (int)(t / QH);
+  float sc[CPT], sh[CPT];
+  VecIO<float, CPT>::load(s1 + c0, sc);
+  VecIO<float, CPT>::load(t1 + c0, sh);
+  float m[4][CPT];
+  unsigned char am[4][CPT];
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      m[o][j] = -INFINITY;
+      am[o][j] = 0;
+    }
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int ih = 4 * qa - 1 + r;
+    if (ih < 0 || ih >= H) continue;
+#pragma unroll
+    for (int cc = 0; cc < 5; ++cc) {
+      const int iw = 4 * qb - 1 + cc;
+      if (iw < 0 || iw >= W) continue;
+      float v[CPT];
+      VecIO<T, CPT>::load(Y + (((long)n * H + ih) * W + iw) * C + c0, v);
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
+#pragma unroll
+      for (int oy = 0; oy < 2; ++oy) {
+        const int ky = r - 2 * oy;
+        if (ky < 0 || ky > 2) continue;
+#pragma unroll
+        for (int ox = 0; ox < 2; ++ox) {
+          const int kx = cc - 2 * ox;
+          if (kx < 0 || kx > 2) continue;
+          const int o = oy * 2 + ox;
+#pragma unroll
+          for (int j = 0; j < CPT; ++j)
+            if (v[j] > m[o][j] || (v[j] != v[j])) {
+              m[o][j] = v[j];
+              am[o][j] = (unsigned char)(ky * 3 + kx);
+            }
+        }
+      }
+    }
+  }
+  float a2[CPT], b2[CPT];
+  if (s2) {
+    VecIO<float, CPT>::load(s2 + c0, a2);
+    VecIO<float, CPT>::load(t2 + c0, b2);
+  }
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const int oh = 2 * qa + (o >> 1), ow = 2 * qb + (o & 1);
+    if (oh >= OH || ow >= OW) continue;
+    const long op = ((long)n * OH + oh) * OW + ow;
+    float sv[CPT], res[CPT];
+    VecIO<T, CPT>::load(S + op * C + c0, sv);
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) res[j] = m[o][j] + (s2 ? fmaf(sv[j], a2[j], b2[j]) : sv[j]);
+    VecIO<T, CPT>::store(Out + op * C + c0, res);
+    unsigned long long pk = 0;
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) pk |= (unsigned long long)am[o][j] << (8 * j);
+    *reinterpret_cast<unsigned long long*>(amax + op * C + c0) = pk;
+  }
+}
+
 // Max-pool backward by gather, per 2 x 2 quad of input pixels (2a..2a+1, 2b..2b+1): the quad
 // lies in windows (a..a+1, b..b+1), so each thread loads 4 windows' dOut / argmax once and
 // writes 4 pixels (a per-pixel gather loads 2.25 windows per pixel).
@@ -682,6 +766,18 @@ int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int
                  const float* t2, void* Out, unsigned char* amax, int N, int H, int W, int C, hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
   const int OH = pool ? (H - 1) / 2 + 1 : H, OW = pool ? (W - 1) / 2 + 1 : W;
+  if (pool) {   // one thread per 2 x 2 output quad x 8 channels
+    const unsigned gq = nblk((long)N * ((OH + 1) / 2) * ((OW + 1) / 2) * (C / 8));
+    if (dtype == XCP_BF16)
+      hipLaunchKernelGGL((tail_pool_quad_kernel<bf16, 8>), dim3(gq), dim3(256), 0, st, (const bf16*)Y, s1, t1,
+                         (const bf16*)S, s2, t2, (bf16*)Out, amax, N, H, W, C, OH, OW);
+    else if (dtype == XCP_F32)
+      hipLaunchKernelGGL((tail_pool_quad_kernel<float, 8>), dim3(gq), dim3(256), 0, st, (const float*)Y, s1, t1,
+                         (const float*)S, s2, t2, (float*)Out, amax, N, H, W, C, OH, OW);
+    else
+      return XCP_EUNSUPPORTED;
+    return (int)hipGetLastError();
+  }
   const unsigned g = nblk((long)N * OH * OW * (C / 8));
   if (dtype == XCP_BF16)
     hipLaunchKernelGGL((tail_fwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)Y, s1, t1, pool,
