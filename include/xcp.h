@@ -76,6 +76,8 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
 /* out[g][l] = sum over the g-th of G contiguous groups of slabs s of in[s][l] (fp64 sums, fp32 out);
  * accumulate = 1 (G = 1 only): out[l] += that sum (gradient accumulation into param.grad) */
 int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, int accumulate, xcp_stream_t stream);
+/* slab groups G for the first level of a two-level reduction of S slabs of L floats (0: one pass) */
+int xcp_colreduce_groups(int S, long L);
 int xcp_chanred_parts(long rows, int C);
 int xcp_row_stats(int dtype, const void* X, long rows, int C, float* part, xcp_stream_t stream);
 /* ms / mt (both null, or both set): scale / shift of the BN when dZ is the gradient of

@@ -27,6 +27,7 @@ SIGNATURES = {
     "xcp_dw_bwd_chunks": [I, I, I, I],
     "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_colreduce_f32": [P, I, L, P, I, I, P],
+    "xcp_colreduce_groups": [I, L],
     "xcp_chanred_parts": [L, I],
     "xcp_row_stats": [I, P, L, I, P, P],
     "xcp_bn_bwd_reduce": [I, P, P, P, P, P, P, L, I, P, P],
@@ -66,6 +67,7 @@ SIGNATURES = {
 
 # entry points that return a size, not a status
 SIZE_QUERIES = {"xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
+                "xcp_colreduce_groups",
                 "xcp_conv1_wgrad_parts", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
                 "xcp_maxpool_bwd_bnred_parts"}
 

@@ -15,23 +15,57 @@ namespace {
 
 // ---------------------------------------------------------------- column reduce
 // out[g][l] = sum_{s in group g} in[s][l]   (in: fp32 [S][L]; out: fp32 [G][L]; ACC: out +=)
-template <bool ACC>
+// Lane = VEC consecutive columns, wave w of 4 takes slabs w, w+4, ... of its group with four
+// loads in flight (the adds stay in slab order), the block folds the 4 waves in fp64.
+// The summation order depends only on (S, L, G), so the result is deterministic.
+template <bool ACC, int VEC>
 __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ in, int S, long L, float* __restrict__ out,
                                                         int G) {
-  __shared__ double red[4][64];
+  __shared__ double red[4][64 * VEC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long col = (long)blockIdx.x * 64 + lane;
+  const long col = ((long)blockIdx.x * 64 + lane) * VEC;
   const int g = blockIdx.y;
   const int spg = (S + G - 1) / G;
   const int s0 = g * spg, s1 = min(S, s0 + spg);
-  double acc = 0.0;
-  if (col < L)
-    for (int s = s0 + w; s < s1; s += 4) acc += (double)in[(long)s * L + col];
-  red[w][lane] = acc;
+  double acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.0;
+  if (col < L) {
+    const float* p = in + col;
+    int s = s0 + w;
+    for (; s + 12 < s1; s += 16) {
+      float v[4][VEC];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) VecIO<float, VEC>::load(p + (long)(s + 4 * u) * L, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] += (double)v[u][j];
+    }
+    for (; s < s1; s += 4) {
+      float v[VEC];
+      VecIO<float, VEC>::load(p + (long)s * L, v);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += (double)v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) red[w][lane * VEC + j] = acc[j];
   __syncthreads();
   if (w == 0 && col < L) {
-    const float v = (float)(red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
-    out[(long)g * L + col] = ACC ? out[(long)g * L + col] + v : v;
+    float v[VEC], o[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const int i = lane * VEC + j;
+      v[j] = (float)(red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+    }
+    float* q = out + (long)g * L + col;
+    if (ACC) {
+      VecIO<float, VEC>::load(q, o);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) v[j] += o[j];
+    }
+    VecIO<float, VEC>::store(q, v);
   }
 }
 
@@ -650,10 +684,29 @@ int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, int acc
   if (G > S) G = S;
   if (G < 1) G = 1;
   if (accumulate && G != 1) return XCP_EINVAL;
-  const dim3 grid((unsigned)((L + 63) / 64), G);
-  if (accumulate) hipLaunchKernelGGL(colreduce_kernel<true>, grid, dim3(256), 0, st, in, S, L, out, G);
-  else hipLaunchKernelGGL(colreduce_kernel<false>, grid, dim3(256), 0, st, in, S, L, out, G);
+  const bool v4 = L % 4 == 0 && ((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0;
+  const long cols_per_block = v4 ? 256 : 64;
+  const dim3 grid((unsigned)((L + cols_per_block - 1) / cols_per_block), G);
+  if (v4) {
+    if (accumulate) hipLaunchKernelGGL((colreduce_kernel<true, 4>), grid, dim3(256), 0, st, in, S, L, out, G);
+    else hipLaunchKernelGGL((colreduce_kernel<false, 4>), grid, dim3(256), 0, st, in, S, L, out, G);
+  } else {
+    if (accumulate) hipLaunchKernelGGL((colreduce_kernel<true, 1>), grid, dim3(256), 0, st, in, S, L, out, G);
+    else hipLaunchKernelGGL((colreduce_kernel<false, 1>), grid, dim3(256), 0, st, in, S, L, out, G);
+  }
   return (int)hipGetLastError();
+}
+
+// slab groups for the first level of a two-level reduction of S slabs of L floats
+// (0 = reduce in one pass): about 1024 workgroups, >= 8 slabs per group, <= 64 groups
+int xcp_colreduce_groups(int S, long L) {
+  const long blocks = (L + 255) / 256;
+  if (S <= 16 || blocks >= 512) return 0;
+  long G = 1024 / blocks;
+  const long gs = (S + 7) / 8;
+  if (G > gs) G = gs;
+  if (G > 64) G = 64;
+  return G <= 1 ? 0 : (int)G;
 }
 
 // number of partial rows the channel reductions below produce

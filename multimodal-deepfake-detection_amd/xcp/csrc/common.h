@@ -44,6 +44,8 @@ template <int N> struct VecIO<float, N> {
         float4 q = *reinterpret_cast<const float4*>(p + i);
         v[i] = q.x; v[i + 1] = q.y; v[i + 2] = q.z; v[i + 3] = q.w;
       }
+    } else if constexpr (N == 1) {
+      v[0] = *p;
     } else {
 #pragma unroll
       for (int i = 0; i < N; i += 2) {
@@ -57,6 +59,8 @@ template <int N> struct VecIO<float, N> {
 #pragma unroll
       for (int i = 0; i < N; i += 4)
         *reinterpret_cast<float4*>(p + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+    } else if constexpr (N == 1) {
+      *p = v[0];
     } else {
 #pragma unroll
       for (int i = 0; i < N; i += 2) *reinterpret_cast<float2*>(p + i) = make_float2(v[i], v[i + 1]);

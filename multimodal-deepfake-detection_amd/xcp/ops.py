@@ -111,9 +111,9 @@ def colreduce_f32(inp, S, L, out, G, accumulate=False):
 
 
 def reduce_slabs(P, S, L, out, accumulate=False):
-    """out[L] (+)= sum_s P[s][L] (fp32, deterministic, two levels when S is large)."""
-    if S > 64:
-        g = 32
+    """out[L] (+)= sum_s P[s][L] (fp32, deterministic; two levels when S is large and L small)."""
+    g = _lib.call("xcp_colreduce_groups", S, L)
+    if g:
         tmp = torch.empty(g * L, device=P.device, dtype=torch.float32)
         colreduce_f32(P, S, L, tmp, g)
         colreduce_f32(tmp, g, L, out, 1, accumulate)

@@ -144,6 +144,26 @@ def test_gemm_tn(ops, gpu, dt, M, N, K, tile):
     assert rel_err(acc.view(N, K), ref + base.view(N, K)) < (1e-5 if dt == torch.float32 else 1e-3)
 
 
+@pytest.mark.parametrize("S,L", [(1, 5), (3, 1001), (28, 728 * 728), (768, 728 * 9), (2560, 128 * 9), (40, 2304),
+                                 (17, 6), (300, 7)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_reduce_slabs(ops, gpu, S, L, accumulate):
+    """Slab reduction (one pass, and two levels when S is large and L small; float4 and
+    scalar lanes): fp64 sums rounded once, so it matches the fp64 column sum to fp32
+    rounding (once per level: atol grows with sqrt(S)); a second run is bit-identical
+    (deterministic order)."""
+    g = torch.Generator(device=gpu).manual_seed(S * 7 + L)
+    P = torch.randn(S, L, device=gpu, generator=g)
+    base = torch.randn(L, device=gpu, generator=g)
+    out = base.clone() if accumulate else torch.empty(L, device=gpu)
+    ops.reduce_slabs(P, S, L, out, accumulate)
+    ref = P.double().sum(0) + (base.double() if accumulate else 0)
+    torch.testing.assert_close(out.double(), ref, rtol=2e-6, atol=2e-6 * max(1.0, S ** 0.5))
+    again = base.clone() if accumulate else torch.empty(L, device=gpu)
+    ops.reduce_slabs(P, S, L, again, accumulate)
+    assert torch.equal(out, again)
+
+
 def test_gemm_operands_over_2gb_global_address_path(ops, gpu):
     """Operands spanning more than 2 GB take the 64-bit global-address LDS-DMA form of the
     256x256 kernels (the 32-bit buffer-offset form covers the rest): NT and TN at
