@@ -58,6 +58,17 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
                 int rows_per_split, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile,
                 xcp_stream_t stream);
 
+/* fused backward of one SeparableConv2d's pointwise conv + its BatchNorm2d (Xception.py:44-47
+ * then :56/:67/:73/:78 BN; replaces xcp_bn_bwd_apply + xcp_gemm_nt dgrad + xcp_gemm_tn wgrad for
+ * the unit): dY = alpha*G + (bcoef*Y + delta) (bf16-rounded, never stored),
+ * dD[M][CI] = dY Wt^T, P[s][CO][CI] = sum_{m in split s} dY[m][co] X[m][ci] (reduce with
+ * xcp_colreduce_f32).  Wt: [CI][CO].  bf16, CO = 128, CI = 64 or 128 only. */
+/* rows per split (S = ceil(M / rows)); 0: the shape is not supported */
+int xcp_unit_bwd_rows_per_split(int dtype, int M, int CO, int CI);
+int xcp_unit_bwd(int dtype, const void* G, const void* Y, const float* alpha, const float* bcoef, const float* delta,
+                 const void* Wt, const void* X, void* dD, float* P, int M, int CO, int CI, int S, int rows_per_split,
+                 xcp_stream_t stream);
+
 /* ---- depthwise 3x3 (SeparableConv2d.conv1, Xception.py:41,:45) ----
  * Y = dw3x3(act(X)); act per XCP_ACT_* (BN scale/shift for XCP_ACT_BNRELU);
  * Wt is the [9][C] fp32 tap-major packing of the [C,1,3,3] weight. */

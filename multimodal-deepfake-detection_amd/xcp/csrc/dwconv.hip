@@ -78,11 +78,11 @@ XCP_DEV float act1(float x, float s, float t) {
 // ([HP*WP][SLICE bytes]); with TRANSFORM the activation is applied.  All global
 // loads of a thread are issued before any is consumed (unconditional loads from a
 // clamped address, zero-selected afterwards).
-template <typename T, int ACT, bool TRANSFORM, int MAXPX>
+template <typename T, int ACT, bool TRANSFORM, int MAXPX, int FS = SLICE>
 XCP_DEV void stage(const T* __restrict__ src, char* dst, const TileGeo& g, long nbase, int th0, int tw0, int H, int W,
                    int C, int c0, const float* scale, const float* shift) {
   constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B chunk
-  constexpr int CPP = SLICE / 16;            // chunks per pixel slice
+  constexpr int CPP = FS / 16;               // chunks per pixel slice
   constexpr int MAXIT = MAXPX * CPP / 256;
   const int total = g.HP * g.WP * CPP;
   static_assert(256 % CPP == 0, "a thread's chunk column must be fixed");
@@ -128,7 +128,7 @@ XCP_DEV void stage(const T* __restrict__ src, char* dst, const TileGeo& g, long 
         VecIO<T, EPC>::store(reinterpret_cast<T*>(&u), f);
       }
     }
-    *reinterpret_cast<uint4*>(dst + p * SLICE + q * 16) = u;
+    *reinterpret_cast<uint4*>(dst + p * FS + q * 16) = u;
   }
 }
 
@@ -154,17 +154,21 @@ struct DwArgs {
   TileGeo g;
 };
 
-template <typename T, int ACT, int MAXPX>
+// FS: bytes of channels per pixel per workgroup (64, or 128 when the channel pitch is a
+// multiple of 128 B, so each pixel slice is one whole cache line)
+template <typename T, int ACT, int MAXPX, int FS>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
+  constexpr int LANES = FS / 4;           // dword lanes per row worker
+  constexpr int NWK = 256 / LANES;        // row workers per workgroup
   constexpr int EPT = DT<T>::EPT;
-  constexpr int CPG = SLICE / (int)sizeof(T);   // channels per group
-  __shared__ __attribute__((aligned(16))) char sA[MAXPX * SLICE];
+  constexpr int CPG = FS / (int)sizeof(T);      // channels per group
+  __shared__ __attribute__((aligned(16))) char sA[MAXPX * FS];
   const TileGeo& g = a.g;
   int grp, n, th0, tw0;
   block_coords(a.ngroups, g, grp, n, th0, tw0);
   const int c0 = grp * CPG;
   const long nbase = (long)n * a.H * a.W;
-  const int cl = threadIdx.x & 15, wk = threadIdx.x >> 4;
+  const int cl = threadIdx.x % LANES, wk = threadIdx.x / LANES;
   const int c = c0 + cl * EPT;
   const int cc = c < a.C ? c : a.C - EPT;
   float wt[9][EPT];
@@ -172,25 +176,25 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int e = 0; e < EPT; ++e) wt[t][e] = a.Wt[(long)t * a.C + cc + e];
-  stage<T, ACT, true, MAXPX>(reinterpret_cast<const T*>(a.X), sA, g, nbase, th0, tw0, a.H, a.W, a.C, c0, a.scale,
+  stage<T, ACT, true, MAXPX, FS>(reinterpret_cast<const T*>(a.X), sA, g, nbase, th0, tw0, a.H, a.W, a.C, c0, a.scale,
                              a.shift);
   __syncthreads();
   if (c >= a.C) return;
   T* Y = reinterpret_cast<T*>(a.Y);
   const int items = g.TH * g.nseg;
   const char* lbase = sA + cl * 4;
-  for (int it = wk; it < items; it += NW) {
+  for (int it = wk; it < items; it += NWK) {
     const int r = it / g.nseg, sg = it - r * g.nseg;
     const int oh = th0 + r;
     const int x0 = sg * SEGL;
     if (oh >= a.H) continue;
-    const char* base = lbase + (r * g.WP + x0) * SLICE;
+    const char* base = lbase + (r * g.WP + x0) * FS;
     float win[3][SEGL + 2][EPT];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
       for (int k = 0; k < SEGL + 2; ++k)
-        unpack(*reinterpret_cast<const unsigned*>(base + (ky * g.WP + k) * SLICE), win[ky][k], (T*)nullptr);
+        unpack(*reinterpret_cast<const unsigned*>(base + (ky * g.WP + k) * FS), win[ky][k], (T*)nullptr);
     T* yrow = Y + (nbase + (long)oh * a.W + tw0) * a.C + c;
 #pragma unroll
     for (int j = 0; j < SEGL; ++j) {
@@ -238,19 +242,27 @@ struct DwBwdArgs {
   int N, H, W, C, ngroups;
 };
 
-template <typename T>
+template <typename T, int P, int FS>
 int launch_fwd(int act, const DwArgs& a, hipStream_t st) {
   const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
-  constexpr int P = FWD_MAXPX;
-  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_NONE, P>), dim3(blocks), dim3(256), 0, st, a);
-  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_RELU, P>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_BNRELU, P>), dim3(blocks), dim3(256), 0, st, a);
+  if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_NONE, P, FS>), dim3(blocks), dim3(256), 0, st, a);
+  else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_RELU, P, FS>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_fwd_kernel<T, ACT_BNRELU, P, FS>), dim3(blocks), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
-inline int ngroups_for(int C, int dtype) {
-  const int cpg = SLICE / (dtype == XCP_BF16 ? 2 : 4);
+inline int ngroups_for(int C, int dtype, int slice = SLICE) {
+  const int cpg = slice / (dtype == XCP_BF16 ? 2 : 4);
   return (C + cpg - 1) / cpg;
+}
+
+// Forward slice bytes: 128 (whole cache lines, half the workgroups, twice the work each) for
+// small frames whose halo tile fits FWD_MAXPX128 pixels and whose pixel rows start on a line;
+// else 64.  Measured (tools/kbench.py dwshapes, 256 frames): 10^2 x 1536 / 2048 47.7 -> 36.7 /
+// 69.2 -> 52.6 us; at 19^2 and larger 128-B slices were 0-5 % slower (3 tiles per frame).
+constexpr int FWD_MAXPX128 = 256;   // halo pixels per staged 128-B-slice tile (32 KB)
+inline int fwd_slice_bytes(int C, int esz, int H, int W) {
+  return (C * esz) % 128 == 0 && (H + 2) * (W + 2) <= FWD_MAXPX128 ? 128 : 64;
 }
 
 
@@ -625,10 +637,15 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
     const int rc = xcp_internal_dw_fwd_small(act, X, Y, Wt, scale, shift, N, H, W, C, stream);
     if (rc != XCP_EUNSUPPORTED) return rc;
   }
+  if (dtype != XCP_BF16 && dtype != XCP_F32) return XCP_EUNSUPPORTED;
+  if (fwd_slice_bytes(C, dtype == XCP_BF16 ? 2 : 4, H, W) == 128) {
+    DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype, 128), tile_geo(H, W, FWD_MAXPX128)};
+    if (dtype == XCP_BF16) return launch_fwd<bf16, FWD_MAXPX128, 128>(act, a, stream);
+    return launch_fwd<float, FWD_MAXPX128, 128>(act, a, stream);
+  }
   DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, FWD_MAXPX)};
-  if (dtype == XCP_BF16) return launch_fwd<bf16>(act, a, stream);
-  if (dtype == XCP_F32) return launch_fwd<float>(act, a, stream);
-  return XCP_EUNSUPPORTED;
+  if (dtype == XCP_BF16) return launch_fwd<bf16, FWD_MAXPX, 64>(act, a, stream);
+  return launch_fwd<float, FWD_MAXPX, 64>(act, a, stream);
 }
 
 // number of partial rows (frame x 20-column groups) of the backward's slabs

@@ -1,0 +1,223 @@
+// Fused backward of one narrow SeparableConv2d + BatchNorm2d unit (the 147^2 entry-flow
+// units of block1: Xception.py:61-87 with 64 -> 128 and 128 -> 128 channels).
+//
+// Given, per pixel row m, the gradient G[m][co] w.r.t. the BN output, the BN input Y[m][co]
+// (= the pointwise output) and the BN-backward coefficients (alpha, bcoef, delta) of that BN
+// (from its finalised batch sums), one pass computes
+//   dY[m][co] = bf16(alpha[co] * G + (bcoef[co] * Y + delta[co]))   (as bn_bwd_apply_kernel)
+//   dD[m][ci] = sum_co dY[m][co] * W[co][ci]                           (pointwise dgrad)
+//   P[s][co][ci] = sum_{m in split s} dY[m][co] * X[m][ci]            (pointwise wgrad slabs)
+// so dY never goes to HBM: the unfused sequence (bn_bwd_apply, gemm_nt dgrad, gemm_tn wgrad)
+// reads G, Y once and dY twice, writes dY once; this reads G, Y, X and writes dD only.
+// HBM-bound: bytes per pixel row = 2*(2*CO + 2*CI) (bf16).
+//
+// Workgroup = 4 waves over one row split, 64-row tiles: the next tile's G / Y / X rows are
+// loaded into registers while the current tile's MFMAs run; dY and X are staged in LDS
+// ([m][c], 288-B class pitches so the transposed ds_read_b64_tr_b16 fragment reads of the
+// weight gradient are conflict-free), the weight W^T stays in LDS for the whole split, and
+// dD is transposed through LDS for 16-B stores.
+#include "common.h"
+
+namespace {
+
+constexpr int UB_CO = 128;                 // output channels of the unit (dY width)
+constexpr int UB_TM = 64;                  // pixel rows per tile
+constexpr int UB_DP = UB_CO * 2 + 32;      // sdY pitch (bytes)
+constexpr int UB_WP = UB_CO * 2 + 16;      // sW pitch (bytes): row-wise b128 reads
+constexpr int UB_SPLITS = 512;             // row splits (2 workgroups per CU)
+
+struct UnitBwdArgs {
+  const bf16* G;       // [M][CO] gradient w.r.t. the BN output
+  const bf16* Y;       // [M][CO] BN input (pointwise output)
+  const float* alpha;  // [CO]
+  const float* bcoef;  // [CO]
+  const float* delta;  // [CO]
+  const bf16* Wt;      // [CI][CO] pointwise weight, transposed (engine's pwT pack)
+  const bf16* X;       // [M][CI] pointwise input (depthwise output)
+  bf16* dD;            // [M][CI] gradient w.r.t. the pointwise input
+  float* P;            // [S][CO][CI] weight-gradient partial slabs
+  int M, S, rows_per_split;
+};
+
+template <int CI>
+__global__ __launch_bounds__(256, 2) void unit_bwd_kernel(UnitBwdArgs a) {
+  constexpr int CO = UB_CO, TM = UB_TM, DP = UB_DP, WP = UB_WP;
+  constexpr int XP = CI * 2 + 32;            // sX / sOut pitch (bytes)
+  constexpr int XCH = CI / 8;                // 16-B chunks per X row
+  constexpr int XLD = TM * XCH / 256;        // X chunks per thread per tile (4 or 2)
+  constexpr int WN = CI / 2;                 // wgrad wave tile: 64 co x WN ci
+  constexpr int NJ = WN / 16;
+  constexpr int DCI = CI / 4;                // dgrad wave tile: DCI ci x 64 m
+  constexpr int NDI = DCI / 16;
+  __shared__ __attribute__((aligned(16))) char sW[CI * WP];
+  __shared__ __attribute__((aligned(16))) char sD[TM * DP];
+  __shared__ __attribute__((aligned(16))) char sX[TM * XP];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4, q4 = fr >> 2, p4 = fr & 3;
+  const int s = blockIdx.x;
+  const long mbeg = (long)s * a.rows_per_split;
+  const long mend = min((long)a.M, mbeg + a.rows_per_split);
+  if (mbeg >= mend) return;   // (the host sizes S so that every split has rows)
+
+  // W^T -> LDS once
+  for (int q = tid; q < CI * (CO / 8); q += 256) {
+    const int r = q / (CO / 8), c = q % (CO / 8);
+    *reinterpret_cast<uint4*>(sW + r * WP + c * 16) = *reinterpret_cast<const uint4*>(a.Wt + (long)r * CO + c * 8);
+  }
+  // this thread's G / Y chunk column is fixed: channels 8*gc .. 8*gc+7
+  const int gc = tid & 15, grow = tid >> 4;   // rows grow + 16 i
+  float al[8], bc[8], de[8];
+  VecIO<float, 8>::load(a.alpha + gc * 8, al);
+  VecIO<float, 8>::load(a.bcoef + gc * 8, bc);
+  VecIO<float, 8>::load(a.delta + gc * 8, de);
+  const int xc = tid % XCH, xrow = tid / XCH;   // X rows xrow + (256 / XCH) i
+
+  uint4 rG[4], rY[4], rX[XLD];
+  auto load_tile = [&](long m0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long m = m0 + grow + 16 * i;
+      const long mm = m < mend ? m : mbeg;
+      rG[i] = *reinterpret_cast<const uint4*>(a.G + mm * CO + gc * 8);
+      rY[i] = *reinterpret_cast<const uint4*>(a.Y + mm * CO + gc * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) {
+      const long m = m0 + xrow + (256 / XCH) * i;
+      const long mm = m < mend ? m : mbeg;
+      rX[i] = *reinterpret_cast<const uint4*>(a.X + mm * CI + xc * 8);
+    }
+  };
+  auto stage_tile = [&](long m0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = grow + 16 * i;
+      float g[8], y[8];
+      VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&rG[i]), g);
+      VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&rY[i]), y);
+      const bool ok = m0 + r < mend;   // rows past the split: dY = 0 (not delta)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = ok ? fmaf(al[j], g[j], fmaf(bc[j], y[j], de[j])) : 0.f;
+      VecIO<bf16, 8>::store(reinterpret_cast<bf16*>(sD + r * DP + gc * 16), g);
+    }
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) {
+      const int r = xrow + (256 / XCH) * i;
+      *reinterpret_cast<uint4*>(sX + r * XP + xc * 16) = m0 + r < mend ? rX[i] : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  f32x4 accw[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) accw[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wm = w >> 1, wn = w & 1;   // wgrad wave tile: co wm*64.., ci wn*WN..
+
+  load_tile(mbeg);
+  for (long m0 = mbeg; m0 < mend; m0 += TM) {
+    lds_barrier();            // previous tile's readers of sD / sX (sOut) are done
+    stage_tile(m0);
+    lds_barrier();
+    if (m0 + TM < mend) load_tile(m0 + TM);
+
+    // weight gradient: accw += dY^T X over the tile's 64 rows (2 MFMA k-steps of 32 rows)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[NJ];
+#pragma unroll
+      for (int t4 = 0; t4 < 4; ++t4) {
+        const int ncol = wm * 64 + t4 * 16 + p4 * 4;
+        const bf16x4 a0 = ds_read_tr(sD + (32 * ks + 4 * fg + q4) * DP + ncol * 2);
+        const bf16x4 a1 = ds_read_tr(sD + (32 * ks + 16 + 4 * fg + q4) * DP + ncol * 2);
+        af[t4] = bf16x8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      }
+#pragma unroll
+      for (int t4 = 0; t4 < NJ; ++t4) {
+        const int kcol = wn * WN + t4 * 16 + p4 * 4;
+        const bf16x4 b0 = ds_read_tr(sX + (32 * ks + 4 * fg + q4) * XP + kcol * 2);
+        const bf16x4 b1 = ds_read_tr(sX + (32 * ks + 16 + 4 * fg + q4) * XP + kcol * 2);
+        bfr[t4] = bf16x8{b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) accw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], accw[i][j], 0, 0, 0);
+    }
+
+    // dgrad, transposed: dD^T[ci][m] = sum_co W^T[ci][co] dY[m][co]; wave w: ci w*DCI.., all 64 m
+    f32x4 accd[NDI][4];
+#pragma unroll
+    for (int i = 0; i < NDI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accd[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < CO; k0 += 32) {
+      bf16x8 wa[NDI], db[4];
+#pragma unroll
+      for (int i = 0; i < NDI; ++i)
+        wa[i] = *reinterpret_cast<const bf16x8*>(sW + (w * DCI + i * 16 + fr) * WP + (k0 + 8 * fg) * 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        db[j] = *reinterpret_cast<const bf16x8*>(sD + (j * 16 + fr) * DP + (k0 + 8 * fg) * 2);
+#pragma unroll
+      for (int i = 0; i < NDI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) accd[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i], db[j], accd[i][j], 0, 0, 0);
+    }
+    lds_barrier();            // every wave is done reading sX (weight gradient)
+    // accd[i][j][r] = dD[m = j*16 + fr][ci = w*DCI + i*16 + 4*fg + r] -> sOut (= sX) as bf16
+#pragma unroll
+    for (int i = 0; i < NDI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bf16x4 q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = (bf16)accd[i][j][r];
+        *reinterpret_cast<bf16x4*>(sX + (j * 16 + fr) * XP + (w * DCI + i * 16 + 4 * fg) * 2) = q;
+      }
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) {
+      const int r = xrow + (256 / XCH) * i;
+      if (m0 + r < mend)
+        *reinterpret_cast<uint4*>(a.dD + (m0 + r) * CI + xc * 8) = *reinterpret_cast<const uint4*>(sX + r * XP + xc * 16);
+    }
+  }
+  // weight-gradient slab: accw[i][j][r] = P[co = wm*64 + i*16 + 4*fg + r][ci = wn*WN + j*16 + fr]
+  float* P = a.P + (long)s * CO * CI;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) P[(long)(wm * 64 + i * 16 + 4 * fg + r) * CI + wn * WN + j * 16 + fr] = accw[i][j][r];
+}
+
+}  // namespace
+
+extern "C" {
+
+// rows per split of xcp_unit_bwd (0: shape not supported by the fused kernel)
+int xcp_unit_bwd_rows_per_split(int dtype, int M, int CO, int CI) {
+  if (dtype != XCP_BF16 || CO != UB_CO || (CI != 64 && CI != 128) || M <= 0) return 0;
+  const long per = ((long)M + UB_SPLITS - 1) / UB_SPLITS;
+  return (int)((per + UB_TM - 1) / UB_TM * UB_TM);
+}
+
+int xcp_unit_bwd(int dtype, const void* G, const void* Y, const float* alpha, const float* bcoef, const float* delta,
+                 const void* Wt, const void* X, void* dD, float* P, int M, int CO, int CI, int S, int rows_per_split,
+                 hipStream_t stream) {
+  if (M <= 0) return XCP_OK;
+  const int rps = xcp_unit_bwd_rows_per_split(dtype, M, CO, CI);
+  if (rps == 0) return XCP_EUNSUPPORTED;
+  if (rows_per_split != rps || S != (M + rps - 1) / rps) return XCP_EINVAL;
+  UnitBwdArgs a{(const bf16*)G, (const bf16*)Y, alpha, bcoef, delta, (const bf16*)Wt, (const bf16*)X, (bf16*)dD,
+                P, M, S, rows_per_split};
+  if (CI == 128) hipLaunchKernelGGL(unit_bwd_kernel<128>, dim3(S), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(unit_bwd_kernel<64>, dim3(S), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -106,6 +106,9 @@ class Stats:
 
 # pointwise weight gradients on a side stream (XCP_WGRAD_STREAM=0 keeps them in order)
 WGRAD_SIDE_STREAM = os.environ.get("XCP_WGRAD_STREAM", "1") != "0"
+# fused BN-apply + pointwise dgrad + wgrad for the narrow units (csrc/unitbwd.hip);
+# XCP_FUSED_UNIT_BWD=0 runs the three-kernel sequence (A/B and parity cross-checks)
+FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
 
 
 class XceptionEngine:
@@ -395,14 +398,19 @@ class XceptionEngine:
                 notify(list(pending), side)
             pending.clear()
 
-        def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
-            dY = self._empty(rows * C)
+        def bn_coef(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
+            """BN backward up to its coefficients (alpha, bcoef, delta); writes the affine grads"""
             P = part[1] if part is not None else 0
             (gw, acc), (gb, acc_b) = g(name + ".weight", (C,)), g(name + ".bias", (C,))
             if acc != acc_b:
                 raise NotImplementedError(f"xcp engine: {name}.weight and .bias must both (or neither) require grad")
-            ops.bn_backward(dZ, Y, rows, C, _bn_ref(bnmod), st, dY, gw, gb, part=part[0] if part is not None else None,
-                            R=P, relu=relu, accumulate=acc)
+            return ops.bn_backward_coef(dZ, Y, rows, C, _bn_ref(bnmod), st, gw, gb,
+                                        part=part[0] if part is not None else None, R=P, relu=relu, accumulate=acc)
+
+        def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
+            coef = bn_coef(bnmod, name, dZ, Y, rows, C, st, part, relu)
+            dY = self._empty(rows * C)
+            ops.bn_apply_coef(dZ, Y, dY, coef, st, rows, C, relu)
             return dY
 
         def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None):
@@ -412,10 +420,16 @@ class XceptionEngine:
             ``prev_st`` is the Stats of the BN feeding this unit -- that BN's backward partial
             sums)."""
             M = N * H * W
-            dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
             dD = self._empty(M * u.cin)
-            ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, u.cin, u.cout)
-            wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
+            if FUSED_UNIT_BWD and ops.unit_bwd_rows_per_split(dZ.dtype, M, u.cout, u.cin) > 0:
+                # narrow units: BN apply + pointwise dgrad + wgrad in one pass (dY stays on chip)
+                coef = bn_coef(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
+                dst, acc = g(u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
+                ops.unit_bwd(dZ, rec["y"], coef, pk[u.name + ".pwT"], rec["d"], dD, M, u.cout, u.cin, dst, acc)
+            else:
+                dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
+                ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, u.cin, u.cout)
+                wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
             dX = self._empty(M * u.cin)
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,

@@ -201,9 +201,10 @@ def row_stats(X, rows, C):
     return part, R
 
 
-def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False):
-    """dY = BatchNorm2d backward (train-mode batch stats) of dZ; writes (accumulate: adds to)
-    dgamma/dbeta.
+def bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False):
+    """BatchNorm2d backward (train-mode batch stats) up to the per-channel coefficients:
+    returns coef fp32 [3][C] (alpha, bcoef, delta: dY = alpha*dZ' + bcoef*Y + delta, dZ' the
+    ReLU-masked dZ when relu) and writes (accumulate: adds to) dgamma/dbeta.
     ``part`` ([R][2][C] partial (sum dz, sum dz*zhat)) may come fused from the
     producer of dZ; otherwise it is reduced here.  relu=True: dZ is the gradient of
     relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift)."""
@@ -221,8 +222,40 @@ def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=
     _lib.call("xcp_bn_bwd_finalize_part", _p(part), R, C, float(rows), _p(bn["weight"]), _p(st["mean"]),
               _p(st["invstd"]), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta),
               1 if accumulate else 0, stream())
-    _lib.call("xcp_bn_bwd_apply", DT[dt], _p(dZ), _p(Y), _p(dY), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), ms,
+    return coef
+
+
+def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False):
+    """dY = BatchNorm2d backward (train-mode batch stats) of dZ; writes (accumulate: adds to)
+    dgamma/dbeta (see bn_backward_coef)."""
+    coef = bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=part, R=R, relu=relu, accumulate=accumulate)
+    bn_apply_coef(dZ, Y, dY, coef, st, rows, C, relu)
+
+
+def bn_apply_coef(dZ, Y, dY, coef, st, rows, C, relu=False):
+    """dY = alpha*dZ' + bcoef*Y + delta (coef from bn_backward_coef; dZ' ReLU-masked when relu)"""
+    ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
+    _lib.call("xcp_bn_bwd_apply", DT[Y.dtype], _p(dZ), _p(Y), _p(dY), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), ms,
               mt, rows, C, stream())
+
+
+def unit_bwd_rows_per_split(dtype, M, CO, CI):
+    """rows per split of the fused pointwise + BN unit backward (0: shape not supported)"""
+    return _lib.call("xcp_unit_bwd_rows_per_split", DT[dtype], M, CO, CI)
+
+
+def unit_bwd(G, Y, coef, Wt, X, dD, M, CO, CI, dW_out, accumulate=False):
+    """Fused unit backward: dY = alpha*G + bcoef*Y + delta (coef from bn_backward_coef, never
+    stored), dD[M][CI] = dY Wt^T (Wt: [CI][CO]), dW_out[CO][CI] (+)= dY^T X."""
+    rps = unit_bwd_rows_per_split(G.dtype, M, CO, CI)
+    if rps <= 0:
+        raise ValueError(f"xcp.unit_bwd: unsupported shape M={M} CO={CO} CI={CI} dtype={G.dtype}")
+    S = (M + rps - 1) // rps
+    P = torch.empty(S * CO * CI, device=G.device, dtype=torch.float32)
+    with _timed("unit_bwd", {"M": M, "CO": CO, "CI": CI}):
+        _lib.call("xcp_unit_bwd", DT[G.dtype], _p(G), _p(Y), _p(coef), _p(coef[CO:]), _p(coef[2 * CO:]), _p(Wt),
+                  _p(X), _p(dD), _p(P), M, CO, CI, S, rps, stream())
+    reduce_slabs(P, S, CO * CI, dW_out, accumulate)
 
 
 def bn_act(X, Y, scale, shift, relu, rows, C):

@@ -164,6 +164,37 @@ def test_reduce_slabs(ops, gpu, S, L, accumulate):
     assert torch.equal(out, again)
 
 
+@pytest.mark.parametrize("CI", [128, 64])
+@pytest.mark.parametrize("M", [1000, 64 * 7 + 5, 150001, 5531904 // 16])
+def test_unit_bwd_fused(ops, gpu, M, CI):
+    """Fused BN-apply + pointwise dgrad + wgrad (csrc/unitbwd.hip) against the three-kernel
+    sequence it replaces (bn_bwd_apply -> dY, then dY Wt^T and dY^T X in fp32): ragged tiles and
+    splits; dD within bf16 output rounding, the weight gradient to fp32 summation order; the
+    accumulate form."""
+    CO = 128
+    g = torch.Generator(device=gpu).manual_seed(M + CI)
+    G = torch.randn(M, CO, device=gpu, generator=g).bfloat16()
+    Y = torch.randn(M, CO, device=gpu, generator=g).bfloat16()
+    coef = torch.randn(3 * CO, device=gpu, generator=g) * 0.5
+    Wt = (torch.randn(CI, CO, device=gpu, generator=g) / CO ** 0.5).bfloat16()
+    X = torch.randn(M, CI, device=gpu, generator=g).bfloat16()
+    dY = torch.empty(M, CO, device=gpu, dtype=torch.bfloat16)
+    ops.bn_apply_coef(G, Y, dY, coef, None, M, CO)
+    dD_ref = dY.float() @ Wt.float().t()
+    dW_ref = dY.float().t() @ X.float()
+    dD = torch.full((M, CI), float("nan"), device=gpu, dtype=torch.bfloat16)
+    dW = torch.empty(CO * CI, device=gpu)
+    ops.unit_bwd(G, Y, coef, Wt, X, dD, M, CO, CI, dW)
+    torch.cuda.synchronize()
+    assert rel_err(dD.float(), dD_ref) < 5e-3
+    assert (dD.float() - dD_ref).abs().max().item() <= 2e-2 * dD_ref.abs().max().item()
+    assert rel_err(dW.view(CO, CI), dW_ref) < 1e-5
+    base = torch.randn(CO * CI, device=gpu, generator=g)
+    acc = base.clone()
+    ops.unit_bwd(G, Y, coef, Wt, X, dD, M, CO, CI, acc, accumulate=True)
+    assert rel_err(acc.view(CO, CI), dW_ref + base.view(CO, CI)) < 1e-5
+
+
 def test_gemm_operands_over_2gb_global_address_path(ops, gpu):
     """Operands spanning more than 2 GB take the 64-bit global-address LDS-DMA form of the
     256x256 kernels (the 32-bit buffer-offset form covers the rest): NT and TN at

@@ -1,6 +1,7 @@
 # GPU: PMC passes on the isolated middle-flow depthwise kernels.
 set -o pipefail
 mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for k in dwf_only dwb_only; do
   timeout -s KILL 120 rocprofv3 --pmc TA_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_ta_$k -o p -- python tools/kbench.py $k > gpurun_out/pmc_ta_$k.log 2>&1 || exit $?

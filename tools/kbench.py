@@ -182,6 +182,65 @@ def main():
         rep("tail_fwd pooled 147^2x128", timeit(lambda: ops.tail_fwd(Yp, sc2, sh2, True, Sp, sc2, sh2, Op, Ap, N, Hp, Hp,
                                                                      Cp)), byts)
         del Yp, Sp, Op, Ap
+    if "pad" in sel:   # channel pitch 728 vs 736 (64-B aligned rows) vs 768 (128-B aligned) at 19^2 x 256
+        for Cp in (728, 736, 768):
+            Mp = N * H * W
+            Xp = torch.randn(Mp, Cp, device=dev, generator=g).to(dt)
+            Yp = torch.empty_like(Xp)
+            Dp = torch.randn(Mp, Cp, device=dev, generator=g).to(dt)
+            Wtp = torch.randn(9, Cp, device=dev, generator=g)
+            scp = torch.rand(Cp, device=dev, generator=g) + 0.5
+            shp = torch.randn(Cp, device=dev, generator=g)
+            dWp = torch.empty(Cp * 9, device=dev)
+            stp = {"mean": torch.zeros(Cp, device=dev), "invstd": torch.ones(Cp, device=dev)}
+            tb = Mp * Cp * 2
+            rep(f"C={Cp} dw_fwd act=2", timeit(lambda: ops.dw_fwd(2, Xp, Yp, Wtp, scp, shp, N, H, W, Cp)), 2 * tb)
+            rep(f"C={Cp} dw_bwd act=2 +bnsums", timeit(lambda: ops.dw_bwd(2, Dp, Xp, Wtp, scp, shp, Yp, dWp, N, H, W, Cp,
+                                                                           bn_stats=stp)), 3 * tb)
+            st2 = torch.empty(ops.nt_stat_rows(Mp) * 2 * C, device=dev)
+            Wq = torch.zeros(C, Cp, device=dev, dtype=dt)
+            Wq[:, :C] = Wp
+            rep(f"ld={Cp} gemm_nt 728x728 +stats", timeit(lambda: ops.gemm_nt(Xp, Wq, Yp, Mp, C, C, stats=st2, lda=Cp,
+                                                                               ldb=Cp, ldc=Cp)), flops=2.0 * Mp * C * C)
+            outp = torch.empty(C * C, device=dev)
+            rep(f"ld={Cp} weight_grad 728x728", timeit(lambda: ops.weight_grad(Dp, Xp, Mp, C, C, outp, ldg=Cp, ldx=Cp)),
+                flops=2.0 * Mp * C * C)
+            del Xp, Yp, Dp
+    if "dwshapes" in sel:   # depthwise forward at the step's shapes (256 frames)
+        for (Hs, Cs, act) in ((147, 64, 0), (147, 128, 2), (74, 128, 1), (74, 256, 2), (37, 256, 1), (37, 728, 2),
+                              (19, 728, 1), (19, 728, 2), (19, 1024, 2), (10, 1536, 0), (10, 2048, 2)):
+            Ms = N * Hs * Hs
+            Xs = torch.randn(Ms, Cs, device=dev, generator=g).to(dt)
+            Ys = torch.empty_like(Xs)
+            Wts = torch.randn(9, Cs, device=dev, generator=g)
+            scs = torch.rand(Cs, device=dev, generator=g) + 0.5
+            shs = torch.randn(Cs, device=dev, generator=g)
+            rep(f"dw_fwd {Hs}^2 x {Cs} act={act}", timeit(lambda: ops.dw_fwd(act, Xs, Ys, Wts, scs, shs, N, Hs, Hs, Cs)),
+                4 * Ms * Cs)
+            del Xs, Ys
+    if "unitbwd" in sel:   # block1's unit backward at 147^2 (256 frames): fused vs three kernels
+        Mu, CO = N * 147 * 147, 128
+        Gu = torch.randn(Mu, CO, device=dev, generator=g).to(dt)
+        Yu = torch.randn(Mu, CO, device=dev, generator=g).to(dt)
+        cu = torch.randn(3 * CO, device=dev, generator=g) * 0.5
+        dYu = torch.empty_like(Gu)
+        for CI in (128, 64):
+            Wu = (torch.randn(CI, CO, device=dev, generator=g) / 11).to(dt)
+            Xu = torch.randn(Mu, CI, device=dev, generator=g).to(dt)
+            dDu = torch.empty(Mu, CI, device=dev, dtype=dt)
+            dWu = torch.empty(CO * CI, device=dev)
+            byts = 2 * Mu * (2 * CO + 2 * CI)
+
+            def three():
+                ops.bn_apply_coef(Gu, Yu, dYu, cu, None, Mu, CO)
+                ops.gemm_nt(dYu, Wu, dDu, Mu, CI, CO)
+                ops.weight_grad(dYu, Xu, Mu, CO, CI, dWu)
+
+            rep(f"unit bwd 147^2 {CO}->{CI} three kernels", timeit(three, iters=10), byts)
+            rep(f"unit bwd 147^2 {CO}->{CI} fused", timeit(lambda: ops.unit_bwd(Gu, Yu, cu, Wu, Xu, dDu, Mu, CO, CI, dWu),
+                                                          iters=10), byts)
+            del Xu, dDu
+        del Gu, Yu, dYu
     if "tail" in sel:
         rep("tail_fwd identity", timeit(lambda: ops.tail_fwd(X, sc, sh, False, D, None, None, Y, None, N, H, W, C)),
             3 * tensor_bytes)
