@@ -62,7 +62,7 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
  * then :56/:67/:73/:78 BN; replaces xcp_bn_bwd_apply + xcp_gemm_nt dgrad + xcp_gemm_tn wgrad for
  * the unit): dY = alpha*G + (bcoef*Y + delta) (bf16-rounded, never stored),
  * dD[M][CI] = dY Wt^T, P[s][CO][CI] = sum_{m in split s} dY[m][co] X[m][ci] (reduce with
- * xcp_colreduce_f32).  Wt: [CI][CO].  bf16, CO = 128, CI = 64 or 128 only. */
+ * xcp_colreduce_f32).  Wt: [CI][CO].  bf16; (CO, CI) = (128, 64 | 128) or (256, 128 | 256) only. */
 /* rows per split (S = ceil(M / rows)); 0: the shape is not supported */
 int xcp_unit_bwd_rows_per_split(int dtype, int M, int CO, int CI);
 int xcp_unit_bwd(int dtype, const void* G, const void* Y, const float* alpha, const float* bcoef, const float* delta,

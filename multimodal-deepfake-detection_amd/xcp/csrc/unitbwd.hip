@@ -1,5 +1,6 @@
-// Fused backward of one narrow SeparableConv2d + BatchNorm2d unit (the 147^2 entry-flow
-// units of block1: Xception.py:61-87 with 64 -> 128 and 128 -> 128 channels).
+// Fused backward of one narrow SeparableConv2d + BatchNorm2d unit: the entry-flow units of
+// block1 (147^2: 64 -> 128, 128 -> 128 channels) and block2 (74^2: 128 -> 256, 256 -> 256),
+// Xception.py:61-87.
 //
 // Given, per pixel row m, the gradient G[m][co] w.r.t. the BN output, the BN input Y[m][co]
 // (= the pointwise output) and the BN-backward coefficients (alpha, bcoef, delta) of that BN
@@ -11,20 +12,17 @@
 // reads G, Y once and dY twice, writes dY once; this reads G, Y, X and writes dD only.
 // HBM-bound: bytes per pixel row = 2*(2*CO + 2*CI) (bf16).
 //
-// Workgroup = 4 waves over one row split, 64-row tiles: the next tile's G / Y / X rows are
-// loaded into registers while the current tile's MFMAs run; dY and X are staged in LDS
-// ([m][c], 288-B class pitches so the transposed ds_read_b64_tr_b16 fragment reads of the
-// weight gradient are conflict-free), the weight W^T stays in LDS for the whole split, and
-// dD is transposed through LDS for 16-B stores.
+// Workgroup = 4 or 8 waves over one row split (and one block of 128 input channels when
+// CI = 256), 64-row tiles: the next tile's G / Y / X rows are loaded into registers while the
+// current tile's MFMAs run; dY and X are staged in LDS ([m][c], 8 (mod 64)-dword pitches so the
+// transposed ds_read_b64_tr_b16 fragment reads of the weight gradient are conflict-free), the
+// block's rows of W^T stay in LDS for the whole split, and dD is transposed through LDS for
+// 16-B stores.
 #include "common.h"
 
 namespace {
 
-constexpr int UB_CO = 128;                 // output channels of the unit (dY width)
 constexpr int UB_TM = 64;                  // pixel rows per tile
-constexpr int UB_DP = UB_CO * 2 + 32;      // sdY pitch (bytes)
-constexpr int UB_WP = UB_CO * 2 + 16;      // sW pitch (bytes): row-wise b128 reads
-constexpr int UB_SPLITS = 512;             // row splits (2 workgroups per CU)
 
 struct UnitBwdArgs {
   const bf16* G;       // [M][CO] gradient w.r.t. the BN output
@@ -36,63 +34,78 @@ struct UnitBwdArgs {
   const bf16* X;       // [M][CI] pointwise input (depthwise output)
   bf16* dD;            // [M][CI] gradient w.r.t. the pointwise input
   float* P;            // [S][CO][CI] weight-gradient partial slabs
-  int M, S, rows_per_split;
+  int M, CI, S, rows_per_split;
 };
 
-template <int CI>
-__global__ __launch_bounds__(256, 2) void unit_bwd_kernel(UnitBwdArgs a) {
-  constexpr int CO = UB_CO, TM = UB_TM, DP = UB_DP, WP = UB_WP;
-  constexpr int XP = CI * 2 + 32;            // sX / sOut pitch (bytes)
-  constexpr int XCH = CI / 8;                // 16-B chunks per X row
-  constexpr int XLD = TM * XCH / 256;        // X chunks per thread per tile (4 or 2)
-  constexpr int WN = CI / 2;                 // wgrad wave tile: 64 co x WN ci
+// CO: unit output channels; CIW: input channels per workgroup (grid = S splits x CI / CIW
+// channel blocks: the blocks of one split are adjacent ids, so they run together on one XCD
+// and the second reads G / Y from L2); NTH: threads.
+template <int CO, int CIW, int NTH>
+__global__ __launch_bounds__(NTH, 512 / NTH) void unit_bwd_kernel(UnitBwdArgs a) {
+  constexpr int TM = UB_TM;
+  constexpr int NW = NTH / 64;               // waves
+  constexpr int DP = CO * 2 + 32;            // sD pitch (bytes): 8 (mod 64) dwords, conflict-free tr reads
+  constexpr int WP = CO * 2 + 16;            // sW pitch: 4 (mod 64) dwords, conflict-free b128 rows
+  constexpr int XP = CIW * 2 + 32;           // sX / sOut pitch
+  constexpr int GCH = CO / 8;                // 16-B chunks per G / Y row
+  constexpr int GLD = TM * GCH / NTH;        // G (and Y) chunks per thread per tile
+  constexpr int XCH = CIW / 8;               // 16-B chunks per X row (this block's channels)
+  constexpr int XLD = TM * XCH / NTH;        // X chunks per thread per tile
+  constexpr int WMS = CO / 64;               // wgrad: waves along co (64 each) ...
+  constexpr int WNS = NW / WMS;              // ... and along ci
+  constexpr int WN = CIW / WNS;              // wgrad wave tile: 64 co x WN ci
   constexpr int NJ = WN / 16;
-  constexpr int DCI = CI / 4;                // dgrad wave tile: DCI ci x 64 m
+  constexpr int DCI = CIW / NW;              // dgrad wave tile: DCI ci x 64 m
   constexpr int NDI = DCI / 16;
-  __shared__ __attribute__((aligned(16))) char sW[CI * WP];
+  static_assert(NTH % GCH == 0 && NTH % XCH == 0 && GLD >= 1 && XLD >= 1, "load mapping");
+  static_assert(WMS * WNS == NW && NJ >= 1 && NDI >= 1, "wave tiling");
+  __shared__ __attribute__((aligned(16))) char sW[CIW * WP];
   __shared__ __attribute__((aligned(16))) char sD[TM * DP];
   __shared__ __attribute__((aligned(16))) char sX[TM * XP];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4, q4 = fr >> 2, p4 = fr & 3;
-  const int s = blockIdx.x;
+  const int nblk = a.CI / CIW;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int s = id / nblk, c0 = (id % nblk) * CIW;   // split, first input channel of this block
   const long mbeg = (long)s * a.rows_per_split;
   const long mend = min((long)a.M, mbeg + a.rows_per_split);
   if (mbeg >= mend) return;   // (the host sizes S so that every split has rows)
 
-  // W^T -> LDS once
-  for (int q = tid; q < CI * (CO / 8); q += 256) {
-    const int r = q / (CO / 8), c = q % (CO / 8);
-    *reinterpret_cast<uint4*>(sW + r * WP + c * 16) = *reinterpret_cast<const uint4*>(a.Wt + (long)r * CO + c * 8);
+  // this block's rows of W^T -> LDS once
+  for (int q = tid; q < CIW * GCH; q += NTH) {
+    const int r = q / GCH, c = q % GCH;
+    *reinterpret_cast<uint4*>(sW + r * WP + c * 16) =
+        *reinterpret_cast<const uint4*>(a.Wt + (long)(c0 + r) * CO + c * 8);
   }
   // this thread's G / Y chunk column is fixed: channels 8*gc .. 8*gc+7
-  const int gc = tid & 15, grow = tid >> 4;   // rows grow + 16 i
+  const int gc = tid % GCH, grow = tid / GCH;   // rows grow + (NTH / GCH) i
   float al[8], bc[8], de[8];
   VecIO<float, 8>::load(a.alpha + gc * 8, al);
   VecIO<float, 8>::load(a.bcoef + gc * 8, bc);
   VecIO<float, 8>::load(a.delta + gc * 8, de);
-  const int xc = tid % XCH, xrow = tid / XCH;   // X rows xrow + (256 / XCH) i
+  const int xc = tid % XCH, xrow = tid / XCH;   // X rows xrow + (NTH / XCH) i
 
-  uint4 rG[4], rY[4], rX[XLD];
+  uint4 rG[GLD], rY[GLD], rX[XLD];
   auto load_tile = [&](long m0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const long m = m0 + grow + 16 * i;
+    for (int i = 0; i < GLD; ++i) {
+      const long m = m0 + grow + (NTH / GCH) * i;
       const long mm = m < mend ? m : mbeg;
       rG[i] = *reinterpret_cast<const uint4*>(a.G + mm * CO + gc * 8);
       rY[i] = *reinterpret_cast<const uint4*>(a.Y + mm * CO + gc * 8);
     }
 #pragma unroll
     for (int i = 0; i < XLD; ++i) {
-      const long m = m0 + xrow + (256 / XCH) * i;
+      const long m = m0 + xrow + (NTH / XCH) * i;
       const long mm = m < mend ? m : mbeg;
-      rX[i] = *reinterpret_cast<const uint4*>(a.X + mm * CI + xc * 8);
+      rX[i] = *reinterpret_cast<const uint4*>(a.X + mm * a.CI + c0 + xc * 8);
     }
   };
   auto stage_tile = [&](long m0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = grow + 16 * i;
+    for (int i = 0; i < GLD; ++i) {
+      const int r = grow + (NTH / GCH) * i;
       float g[8], y[8];
       VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&rG[i]), g);
       VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&rY[i]), y);
@@ -103,7 +116,7 @@ __global__ __launch_bounds__(256, 2) void unit_bwd_kernel(UnitBwdArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < XLD; ++i) {
-      const int r = xrow + (256 / XCH) * i;
+      const int r = xrow + (NTH / XCH) * i;
       *reinterpret_cast<uint4*>(sX + r * XP + xc * 16) = m0 + r < mend ? rX[i] : make_uint4(0, 0, 0, 0);
     }
   };
@@ -113,7 +126,7 @@ __global__ __launch_bounds__(256, 2) void unit_bwd_kernel(UnitBwdArgs a) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) accw[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int wm = w >> 1, wn = w & 1;   // wgrad wave tile: co wm*64.., ci wn*WN..
+  const int wm = w / WNS, wn = w % WNS;   // wgrad wave tile: co wm*64.., ci wn*WN..
 
   load_tile(mbeg);
   for (long m0 = mbeg; m0 < mend; m0 += TM) {
@@ -180,19 +193,38 @@ __global__ __launch_bounds__(256, 2) void unit_bwd_kernel(UnitBwdArgs a) {
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < XLD; ++i) {
-      const int r = xrow + (256 / XCH) * i;
+      const int r = xrow + (NTH / XCH) * i;
       if (m0 + r < mend)
-        *reinterpret_cast<uint4*>(a.dD + (m0 + r) * CI + xc * 8) = *reinterpret_cast<const uint4*>(sX + r * XP + xc * 16);
+        *reinterpret_cast<uint4*>(a.dD + (m0 + r) * a.CI + c0 + xc * 8) =
+            *reinterpret_cast<const uint4*>(sX + r * XP + xc * 16);
     }
   }
-  // weight-gradient slab: accw[i][j][r] = P[co = wm*64 + i*16 + 4*fg + r][ci = wn*WN + j*16 + fr]
-  float* P = a.P + (long)s * CO * CI;
+  // weight-gradient slab: accw[i][j][r] = P[co = wm*64 + i*16 + 4*fg + r][ci = c0 + wn*WN + j*16 + fr]
+  float* P = a.P + (long)s * CO * a.CI + c0;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) P[(long)(wm * 64 + i * 16 + 4 * fg + r) * CI + wn * WN + j * 16 + fr] = accw[i][j][r];
+      for (int j = 0; j < NJ; ++j)
+        P[(long)(wm * 64 + i * 16 + 4 * fg + r) * a.CI + wn * WN + j * 16 + fr] = accw[i][j][r];
+}
+
+// supported shapes: (CO, CI) -> input channels per block and target row splits
+// (CO 128: 2 workgroups of 256 threads per CU, 512 splits; CO 256: one of 512 per CU,
+// CI / 128 blocks per split, 256 workgroups)
+bool unit_cfg(int CO, int CI, int& ciw, int& splits) {
+  if (CO == 128 && (CI == 64 || CI == 128)) {
+    ciw = CI;
+    splits = 512;
+    return true;
+  }
+  if (CO == 256 && (CI == 128 || CI == 256)) {
+    ciw = 128;
+    splits = 256 / (CI / 128);
+    return true;
+  }
+  return false;
 }
 
 }  // namespace
@@ -201,8 +233,9 @@ extern "C" {
 
 // rows per split of xcp_unit_bwd (0: shape not supported by the fused kernel)
 int xcp_unit_bwd_rows_per_split(int dtype, int M, int CO, int CI) {
-  if (dtype != XCP_BF16 || CO != UB_CO || (CI != 64 && CI != 128) || M <= 0) return 0;
-  const long per = ((long)M + UB_SPLITS - 1) / UB_SPLITS;
+  int ciw, splits;
+  if (dtype != XCP_BF16 || M <= 0 || !unit_cfg(CO, CI, ciw, splits)) return 0;
+  const long per = ((long)M + splits - 1) / splits;
   return (int)((per + UB_TM - 1) / UB_TM * UB_TM);
 }
 
@@ -214,9 +247,11 @@ int xcp_unit_bwd(int dtype, const void* G, const void* Y, const float* alpha, co
   if (rps == 0) return XCP_EUNSUPPORTED;
   if (rows_per_split != rps || S != (M + rps - 1) / rps) return XCP_EINVAL;
   UnitBwdArgs a{(const bf16*)G, (const bf16*)Y, alpha, bcoef, delta, (const bf16*)Wt, (const bf16*)X, (bf16*)dD,
-                P, M, S, rows_per_split};
-  if (CI == 128) hipLaunchKernelGGL(unit_bwd_kernel<128>, dim3(S), dim3(256), 0, stream, a);
-  else hipLaunchKernelGGL(unit_bwd_kernel<64>, dim3(S), dim3(256), 0, stream, a);
+                P, M, CI, S, rows_per_split};
+  const dim3 grid(S * (CO == 256 ? CI / 128 : 1));
+  if (CO == 128 && CI == 128) hipLaunchKernelGGL((unit_bwd_kernel<128, 128, 256>), grid, dim3(256), 0, stream, a);
+  else if (CO == 128) hipLaunchKernelGGL((unit_bwd_kernel<128, 64, 256>), grid, dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL((unit_bwd_kernel<256, 128, 512>), grid, dim3(512), 0, stream, a);
   return (int)hipGetLastError();
 }
 

@@ -57,7 +57,8 @@ def install_fake_lib(monkeypatch):
         if name == "xcp_maxpool_bwd_bnred_parts":
             return 4
         if name == "xcp_unit_bwd_rows_per_split":   # (dtype, M, CO, CI): the fused narrow unit
-            return 64 if args[0] == 1 and args[2] == 128 and args[3] in (64, 128) else 0
+            ok = args[0] == 1 and (args[2], args[3]) in ((128, 64), (128, 128), (256, 128), (256, 256))
+            return 64 if ok else 0
         return 0
 
     monkeypatch.setattr(_lib, "call", fake_call)
@@ -123,8 +124,9 @@ def test_lstmv_step_call_sequence(fake_lib, unfrozen, prec):
         assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd_bnred", "xcp_conv1_wgrad"} <= names
         # stem conv2: direct MFMA conv in bf16, im2col GEMM (gather modes 2 / 3) in fp32
         assert ({"xcp_conv3x3", "xcp_conv3x3_wgrad"} <= names) == (prec == "bf16")
-        # block1's two units (64 -> 128, 128 -> 128): fused BN-apply + pointwise dgrad + wgrad in bf16
-        assert fake_lib.count("xcp_unit_bwd") == (2 if prec == "bf16" else 0)
+        # block1's and block2's units (64/128 -> 128, 128/256 -> 256): fused BN-apply + pointwise
+        # dgrad + wgrad in bf16
+        assert fake_lib.count("xcp_unit_bwd") == (4 if prec == "bf16" else 0)
         for n, p in m.feature_extractor.named_parameters():
             assert p.grad is not None and p.grad.shape == p.shape, n
     else:

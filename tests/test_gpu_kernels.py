@@ -164,15 +164,14 @@ def test_reduce_slabs(ops, gpu, S, L, accumulate):
     assert torch.equal(out, again)
 
 
-@pytest.mark.parametrize("CI", [128, 64])
+@pytest.mark.parametrize("CO,CI", [(128, 128), (128, 64), (256, 128), (256, 256)])
 @pytest.mark.parametrize("M", [1000, 64 * 7 + 5, 150001, 5531904 // 16])
-def test_unit_bwd_fused(ops, gpu, M, CI):
+def test_unit_bwd_fused(ops, gpu, M, CO, CI):
     """Fused BN-apply + pointwise dgrad + wgrad (csrc/unitbwd.hip) against the three-kernel
     sequence it replaces (bn_bwd_apply -> dY, then dY Wt^T and dY^T X in fp32): ragged tiles and
     splits; dD within bf16 output rounding, the weight gradient to fp32 summation order; the
     accumulate form."""
-    CO = 128
-    g = torch.Generator(device=gpu).manual_seed(M + CI)
+    g = torch.Generator(device=gpu).manual_seed(M + CO + CI)
     G = torch.randn(M, CO, device=gpu, generator=g).bfloat16()
     Y = torch.randn(M, CO, device=gpu, generator=g).bfloat16()
     coef = torch.randn(3 * CO, device=gpu, generator=g) * 0.5

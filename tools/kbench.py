@@ -218,13 +218,13 @@ def main():
             rep(f"dw_fwd {Hs}^2 x {Cs} act={act}", timeit(lambda: ops.dw_fwd(act, Xs, Ys, Wts, scs, shs, N, Hs, Hs, Cs)),
                 4 * Ms * Cs)
             del Xs, Ys
-    if "unitbwd" in sel:   # block1's unit backward at 147^2 (256 frames): fused vs three kernels
-        Mu, CO = N * 147 * 147, 128
-        Gu = torch.randn(Mu, CO, device=dev, generator=g).to(dt)
-        Yu = torch.randn(Mu, CO, device=dev, generator=g).to(dt)
-        cu = torch.randn(3 * CO, device=dev, generator=g) * 0.5
-        dYu = torch.empty_like(Gu)
-        for CI in (128, 64):
+    if "unitbwd" in sel:   # block1 / block2 unit backward (256 frames): fused vs three kernels
+        for (Hu, CO, CI) in ((147, 128, 128), (147, 128, 64), (74, 256, 256), (74, 256, 128)):
+            Mu = N * Hu * Hu
+            Gu = torch.randn(Mu, CO, device=dev, generator=g).to(dt)
+            Yu = torch.randn(Mu, CO, device=dev, generator=g).to(dt)
+            cu = torch.randn(3 * CO, device=dev, generator=g) * 0.5
+            dYu = torch.empty_like(Gu)
             Wu = (torch.randn(CI, CO, device=dev, generator=g) / 11).to(dt)
             Xu = torch.randn(Mu, CI, device=dev, generator=g).to(dt)
             dDu = torch.empty(Mu, CI, device=dev, dtype=dt)
@@ -236,11 +236,10 @@ def main():
                 ops.gemm_nt(dYu, Wu, dDu, Mu, CI, CO)
                 ops.weight_grad(dYu, Xu, Mu, CO, CI, dWu)
 
-            rep(f"unit bwd 147^2 {CO}->{CI} three kernels", timeit(three, iters=10), byts)
-            rep(f"unit bwd 147^2 {CO}->{CI} fused", timeit(lambda: ops.unit_bwd(Gu, Yu, cu, Wu, Xu, dDu, Mu, CO, CI, dWu),
-                                                          iters=10), byts)
-            del Xu, dDu
-        del Gu, Yu, dYu
+            rep(f"unit bwd {Hu}^2 {CO}->{CI} three kernels", timeit(three, iters=10), byts)
+            rep(f"unit bwd {Hu}^2 {CO}->{CI} fused", timeit(lambda: ops.unit_bwd(Gu, Yu, cu, Wu, Xu, dDu, Mu, CO, CI, dWu),
+                                                           iters=10), byts)
+            del Gu, Yu, dYu, Xu, dDu
     if "tail" in sel:
         rep("tail_fwd identity", timeit(lambda: ops.tail_fwd(X, sc, sh, False, D, None, None, Y, None, N, H, W, C)),
             3 * tensor_bytes)
