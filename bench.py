@@ -99,6 +99,10 @@ BLOCKS = [(64, 128, 2, 2, False, True), (128, 256, 2, 2, True, True), (256, 728,
     [(728, 728, 3, 1, True, True)] * 8 + [(728, 1024, 2, 2, True, False)]   # Xception.py:125-140
 
 
+# (cout, cin) of the units whose BN apply + pointwise dgrad + wgrad run fused in bf16
+FUSED_UNITS = {(128, 64), (128, 128), (256, 128), (256, 256)}
+
+
 def step_roofline(size, frames, unfrozen, s=2):
     """Ideal time of one backbone step of this design: sum over its kernels of
     max(flops / MFMA peak, bytes / HBM peak), with each kernel's algorithmic flops and the
@@ -127,9 +131,12 @@ def step_roofline(size, frames, unfrozen, s=2):
         op(2 * P * cin * cout, s * P * (cin + cout))            # pointwise (+BN stats epilogue)
         # BN backward: apply (read dz, y; write dy); its reduce comes fused from the consumer's
         # depthwise backward / the max-pool backward, except after a residual / the avg-pool
-        bwd.append((0, (5 if reduce else 3) * s * P * cout))
-        bwd.append((2 * P * cin * cout, s * P * (cin + cout)))  # pointwise dgrad
-        bwd.append((2 * P * cin * cout, s * P * (cin + cout)))  # pointwise wgrad
+        if s == 2 and (cout, cin) in FUSED_UNITS:   # apply + dgrad + wgrad in one pass (unitbwd.hip)
+            bwd.append((4 * P * cin * cout, s * P * (2 * cout + 2 * cin) + (2 * s * P * cout if reduce else 0)))
+        else:
+            bwd.append((0, (5 if reduce else 3) * s * P * cout))
+            bwd.append((2 * P * cin * cout, s * P * (cin + cout)))  # pointwise dgrad
+            bwd.append((2 * P * cin * cout, s * P * (cin + cout)))  # pointwise wgrad
         bwd.append((0, 3 * s * P * cin))                        # depthwise dgrad + wgrad (+BN partials)
 
     for cin, cout, reps, stride, _, grow in BLOCKS:
