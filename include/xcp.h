@@ -84,9 +84,10 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
                const float* bmean, const float* binvstd, int N, int H, int W, int C, xcp_stream_t stream);
 
 /* ---- BatchNorm2d (Xception.py:56,67,73,78,119,123,143,147), tails, pooling ---- */
-/* out[g][l] = sum over the g-th of G contiguous groups of slabs s of in[s][l] (fp64 sums, fp32 out);
- * accumulate = 1 (G = 1 only): out[l] += that sum (gradient accumulation into param.grad) */
-int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, int accumulate, xcp_stream_t stream);
+/* out[g][l] = sum over the g-th of G contiguous groups of slabs s of in[s*ld + l], l < L <= ld
+ * (fp64 sums, fp32 out); accumulate = 1 (G = 1 only): out[l] += that sum (gradient accumulation
+ * into param.grad) */
+int xcp_colreduce_f32(const float* in, int S, long L, long ld, float* out, int G, int accumulate, xcp_stream_t stream);
 /* slab groups G for the first level of a two-level reduction of S slabs of L floats (0: one pass) */
 int xcp_colreduce_groups(int S, long L);
 int xcp_chanred_parts(long rows, int C);
@@ -95,18 +96,21 @@ int xcp_row_stats(int dtype, const void* X, long rows, int C, float* part, xcp_s
  * relu(bn(Y)) -- the ReLU mask (Y*ms+mt > 0) is applied on the fly (replaces xcp_relu_bwd) */
 int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd,
                       const float* ms, const float* mt, long rows, int C, float* part, xcp_stream_t stream);
-/* train-mode finalize straight from fp32 partial rows part[R][2][C] (sum, sum of squares /
- * sum dz, sum dz*zhat); fp64 accumulation; replaces colreduce_f64 + the two entries below */
-int xcp_bn_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* beta,
+/* train-mode finalize straight from fp32 partial rows part[R][2][CP] (sum, sum of squares /
+ * sum dz, sum dz*zhat); fp64 accumulation.  C channels of a tensor with channel pitch CP >= C
+ * (the padded 736-channel layout of the 728-channel flow): gamma / beta / running stats /
+ * dgamma / dbeta have C entries, the per-channel outputs (mean .. shift, alpha .. delta) CP,
+ * zero for the padding channels */
+int xcp_bn_finalize_part(const float* part, int R, int C, int CP, double count, const float* gamma, const float* beta,
                          float* rmean, float* rvar, float momentum, float eps, float* mean_o, float* invstd_o,
                          float* scale_o, float* shift_o, xcp_stream_t stream);
 /* (dgamma, dbeta may be null; accumulate = 1 adds to them: gradient accumulation into param.grad) */
-int xcp_bn_bwd_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* mean,
-                             const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma,
-                             float* dbeta, int accumulate, xcp_stream_t stream);
-int xcp_bn_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* beta, float* rmean,
-                    float* rvar, float momentum, float eps, int train, float* mean, float* invstd, float* scale,
-                    float* shift, xcp_stream_t stream);
+int xcp_bn_bwd_finalize_part(const float* part, int R, int C, int CP, double count, const float* gamma,
+                             const float* mean, const float* invstd, float* alpha, float* bcoef, float* delta,
+                             float* dgamma, float* dbeta, int accumulate, xcp_stream_t stream);
+int xcp_bn_finalize(const double* part2, int G, int C, int CP, double count, const float* gamma, const float* beta,
+                    float* rmean, float* rvar, float momentum, float eps, int train, float* mean, float* invstd,
+                    float* scale, float* shift, xcp_stream_t stream);
 int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, long rows, int C,
                xcp_stream_t stream);
 int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const float* alpha, const float* bcoef,
@@ -180,8 +184,10 @@ int xcp_opt_sumsq(const long long* tab, int nchunks, float* part, float max_norm
 int xcp_opt_adam(const long long* tab, int nchunks, const float* coef, float lr, float b1, float b2, float eps, float wd,
                  float bc1, float bc2sqrt, xcp_stream_t stream);
 
-/* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][10] int64
- * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block), nblocks in total */
+/* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][12] int64
+ * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block, s0, s1), nblocks in
+ * total; output element (o0, o1, o2) goes to out[o0*s0 + o1*s1 + o2] (strides for the padded
+ * layouts; dense: s1 = od2, s0 = od1*od2) */
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream_t stream);
 
 /* ---- classification heads / losses of the training scripts (fp32) ----

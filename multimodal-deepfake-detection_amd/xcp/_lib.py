@@ -28,14 +28,14 @@ SIGNATURES = {
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
     "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, I, I, I, I, P],
-    "xcp_colreduce_f32": [P, I, L, P, I, I, P],
+    "xcp_colreduce_f32": [P, I, L, L, P, I, I, P],
     "xcp_colreduce_groups": [I, L],
     "xcp_chanred_parts": [L, I],
     "xcp_row_stats": [I, P, L, I, P, P],
     "xcp_bn_bwd_reduce": [I, P, P, P, P, P, P, L, I, P, P],
-    "xcp_bn_finalize_part": [P, I, I, D, P, P, P, P, F, F, P, P, P, P, P],
-    "xcp_bn_bwd_finalize_part": [P, I, I, D, P, P, P, P, P, P, P, P, I, P],
-    "xcp_bn_finalize": [P, I, I, D, P, P, P, P, F, F, I, P, P, P, P, P],
+    "xcp_bn_finalize_part": [P, I, I, I, D, P, P, P, P, F, F, P, P, P, P, P],
+    "xcp_bn_bwd_finalize_part": [P, I, I, I, D, P, P, P, P, P, P, P, P, I, P],
+    "xcp_bn_finalize": [P, I, I, I, D, P, P, P, P, F, F, I, P, P, P, P, P],
     "xcp_bn_act": [I, P, P, P, P, I, L, I, P],
     "xcp_bn_bwd_apply": [I, P, P, P, P, P, P, P, P, L, I, P],
     "xcp_relu_bwd": [I, P, P, L, I, P],

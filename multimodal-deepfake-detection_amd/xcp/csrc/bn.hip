@@ -14,13 +14,13 @@
 namespace {
 
 // ---------------------------------------------------------------- column reduce
-// out[g][l] = sum_{s in group g} in[s][l]   (in: fp32 [S][L]; out: fp32 [G][L]; ACC: out +=)
-// Lane = VEC consecutive columns, wave w of 4 takes slabs w, w+4, ... of its group with four
+// out[g][l] = sum_{s in group g} in[s][l]   (in: fp32 [S][ld], l < L <= ld; out: fp32 [G][L];
+// ACC: out +=).  Lane = VEC consecutive columns, wave w of 4 takes slabs w, w+4, ... of its group with four
 // loads in flight (the adds stay in slab order), the block folds the 4 waves in fp64.
 // The summation order depends only on (S, L, G), so the result is deterministic.
 template <bool ACC, int VEC>
-__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ in, int S, long L, float* __restrict__ out,
-                                                        int G) {
+__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ in, int S, long L, long ld,
+                                                        float* __restrict__ out, int G) {
   __shared__ double red[4][64 * VEC];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long col = ((long)blockIdx.x * 64 + lane) * VEC;
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict_
     for (; s + 12 < s1; s += 16) {
       float v[4][VEC];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) VecIO<float, VEC>::load(p + (long)(s + 4 * u) * L, v[u]);
+      for (int u = 0; u < 4; ++u) VecIO<float, VEC>::load(p + (long)(s + 4 * u) * ld, v[u]);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict_
     }
     for (; s < s1; s += 4) {
       float v[VEC];
-      VecIO<float, VEC>::load(p + (long)s * L, v);
+      VecIO<float, VEC>::load(p + (long)s * ld, v);
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc[j] += (double)v[j];
     }
@@ -180,17 +180,25 @@ __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av,
 }
 
 // ---------------------------------------------------------------- finalize
-__global__ void bn_finalize_kernel(const double* __restrict__ part2, int G, int C, double count, const float* gamma,
-                                   const float* beta, float* rmean, float* rvar, float momentum, float eps, int train,
-                                   float* mean_o, float* invstd_o, float* scale_o, float* shift_o) {
+// C channels of a tensor whose channel pitch is CP >= C: partial rows have CP entries per
+// statistic and the per-channel outputs get CP entries, zero for the padding channels (so a
+// BN-apply over the padded pitch leaves them zero).
+__global__ void bn_finalize_kernel(const double* __restrict__ part2, int G, int C, int CP, double count,
+                                   const float* gamma, const float* beta, float* rmean, float* rvar, float momentum,
+                                   float eps, int train, float* mean_o, float* invstd_o, float* scale_o,
+                                   float* shift_o) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  if (c >= CP) return;
+  if (c >= C) {
+    mean_o[c] = invstd_o[c] = scale_o[c] = shift_o[c] = 0.f;
+    return;
+  }
   double mean, var;
   if (train) {
     double s = 0.0, q = 0.0;
     for (int g = 0; g < G; ++g) {
-      s += part2[((long)g * 2 + 0) * C + c];
-      q += part2[((long)g * 2 + 1) * C + c];
+      s += part2[((long)g * 2 + 0) * CP + c];
+      q += part2[((long)g * 2 + 1) * CP + c];
     }
     mean = s / count;
     var = q / count - mean * mean;
@@ -218,19 +226,19 @@ __global__ void bn_finalize_kernel(const double* __restrict__ part2, int G, int 
 // many loads stay in flight), the 16 waves fold in LDS, and 32 threads finalize.
 constexpr int FIN_CH = 32, FIN_WAVES = 16;
 
-XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int c0, double (*red)[64], double& s0,
+XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, int c0, double (*red)[64], double& s0,
                         double& s1) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = c0 + (lane & 31), stat = lane >> 5;
   double a[4] = {0.0, 0.0, 0.0, 0.0};
   if (c < C) {
-    const float* col = part + (long)stat * C + c;
+    const float* col = part + (long)stat * CP + c;
     int r = w;
     for (; r + 3 * FIN_WAVES < R; r += 4 * FIN_WAVES) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] += (double)col[(long)(r + u * FIN_WAVES) * 2 * C];
+      for (int u = 0; u < 4; ++u) a[u] += (double)col[(long)(r + u * FIN_WAVES) * 2 * CP];
     }
-    for (; r < R; r += FIN_WAVES) a[0] += (double)col[(long)r * 2 * C];
+    for (; r < R; r += FIN_WAVES) a[0] += (double)col[(long)r * 2 * CP];
   }
   red[w][lane] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
@@ -244,7 +252,7 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int c0, do
   }
 }
 
-__global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C,
+__global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C, int CP,
                                                                 double count, const float* gamma, const float* beta,
                                                                 float* rmean, float* rvar, float momentum, float eps,
                                                                 float* mean_o, float* invstd_o, float* scale_o,
@@ -252,9 +260,13 @@ __global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __r
   __shared__ double red[FIN_WAVES][64];
   const int c0 = blockIdx.x * FIN_CH;
   double s, q;
-  fin_reduce(part, R, C, c0, red, s, q);
+  fin_reduce(part, R, C, CP, c0, red, s, q);
   const int c = c0 + threadIdx.x;
-  if (threadIdx.x >= FIN_CH || c >= C) return;
+  if (threadIdx.x >= FIN_CH || c >= CP) return;
+  if (c >= C) {   // padding channel
+    mean_o[c] = invstd_o[c] = scale_o[c] = shift_o[c] = 0.f;
+    return;
+  }
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -272,16 +284,20 @@ __global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __r
 }
 
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_part_kernel(const float* __restrict__ part, int R, int C,
-                                                                    double count, const float* gamma,
+                                                                    int CP, double count, const float* gamma,
                                                                     const float* mean, const float* invstd,
                                                                     float* alpha, float* bcoef, float* delta,
                                                                     float* dgamma, float* dbeta, int accumulate) {
   __shared__ double red[FIN_WAVES][64];
   const int c0 = blockIdx.x * FIN_CH;
   double sdz, sdzy;
-  fin_reduce(part, R, C, c0, red, sdz, sdzy);
+  fin_reduce(part, R, C, CP, c0, red, sdz, sdzy);
   const int c = c0 + threadIdx.x;
-  if (threadIdx.x >= FIN_CH || c >= C) return;
+  if (threadIdx.x >= FIN_CH || c >= CP) return;
+  if (c >= C) {   // padding channel: its gradient stays zero
+    alpha[c] = bcoef[c] = delta[c] = 0.f;
+    return;
+  }
   const double is = invstd[c], gm = gamma[c], mu = mean[c];
   const double a = gm * is;
   const double mdz = sdz / count, mdzy = sdzy / count;
@@ -679,20 +695,21 @@ inline PoolSrc pool_src(const void* dOut, const unsigned char* amax, int H, int 
 
 extern "C" {
 
-int xcp_colreduce_f32(const float* in, int S, long L, float* out, int G, int accumulate, hipStream_t st) {
+int xcp_colreduce_f32(const float* in, int S, long L, long ld, float* out, int G, int accumulate, hipStream_t st) {
   if (L <= 0) return XCP_OK;
+  if (ld < L) return XCP_EINVAL;
   if (G > S) G = S;
   if (G < 1) G = 1;
   if (accumulate && G != 1) return XCP_EINVAL;
-  const bool v4 = L % 4 == 0 && ((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0;
+  const bool v4 = L % 4 == 0 && ld % 4 == 0 && ((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0;
   const long cols_per_block = v4 ? 256 : 64;
   const dim3 grid((unsigned)((L + cols_per_block - 1) / cols_per_block), G);
   if (v4) {
-    if (accumulate) hipLaunchKernelGGL((colreduce_kernel<true, 4>), grid, dim3(256), 0, st, in, S, L, out, G);
-    else hipLaunchKernelGGL((colreduce_kernel<false, 4>), grid, dim3(256), 0, st, in, S, L, out, G);
+    if (accumulate) hipLaunchKernelGGL((colreduce_kernel<true, 4>), grid, dim3(256), 0, st, in, S, L, ld, out, G);
+    else hipLaunchKernelGGL((colreduce_kernel<false, 4>), grid, dim3(256), 0, st, in, S, L, ld, out, G);
   } else {
-    if (accumulate) hipLaunchKernelGGL((colreduce_kernel<true, 1>), grid, dim3(256), 0, st, in, S, L, out, G);
-    else hipLaunchKernelGGL((colreduce_kernel<false, 1>), grid, dim3(256), 0, st, in, S, L, out, G);
+    if (accumulate) hipLaunchKernelGGL((colreduce_kernel<true, 1>), grid, dim3(256), 0, st, in, S, L, ld, out, G);
+    else hipLaunchKernelGGL((colreduce_kernel<false, 1>), grid, dim3(256), 0, st, in, S, L, ld, out, G);
   }
   return (int)hipGetLastError();
 }
@@ -740,31 +757,33 @@ int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mea
 }
 
 // BatchNorm finalize straight from fp32 partial rows part[R][2][C] (train mode)
-int xcp_bn_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* beta,
+int xcp_bn_finalize_part(const float* part, int R, int C, int CP, double count, const float* gamma, const float* beta,
                          float* rmean, float* rvar, float momentum, float eps, float* mean_o, float* invstd_o,
                          float* scale_o, float* shift_o, hipStream_t st) {
   if (C <= 0) return XCP_OK;
-  if (R <= 0) return XCP_EINVAL;
-  hipLaunchKernelGGL(bn_finalize_part_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part, R, C,
-                     count, gamma, beta, rmean, rvar, momentum, eps, mean_o, invstd_o, scale_o, shift_o);
+  if (R <= 0 || CP < C) return XCP_EINVAL;
+  hipLaunchKernelGGL(bn_finalize_part_kernel, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part, R,
+                     C, CP, count, gamma, beta, rmean, rvar, momentum, eps, mean_o, invstd_o, scale_o, shift_o);
   return (int)hipGetLastError();
 }
 
-int xcp_bn_bwd_finalize_part(const float* part, int R, int C, double count, const float* gamma, const float* mean,
-                             const float* invstd, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
-                             int accumulate, hipStream_t st) {
+int xcp_bn_bwd_finalize_part(const float* part, int R, int C, int CP, double count, const float* gamma,
+                             const float* mean, const float* invstd, float* alpha, float* bcoef, float* delta,
+                             float* dgamma, float* dbeta, int accumulate, hipStream_t st) {
   if (C <= 0) return XCP_OK;
-  if (R <= 0) return XCP_EINVAL;
-  hipLaunchKernelGGL(bn_bwd_finalize_part_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part,
-                     R, C, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
+  if (R <= 0 || CP < C) return XCP_EINVAL;
+  hipLaunchKernelGGL(bn_bwd_finalize_part_kernel, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part,
+                     R, C, CP, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
   return (int)hipGetLastError();
 }
 
-int xcp_bn_finalize(const double* part2, int G, int C, double count, const float* gamma, const float* beta, float* rmean,
-                    float* rvar, float momentum, float eps, int train, float* mean, float* invstd, float* scale,
-                    float* shift, hipStream_t st) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part2, G, C, count, gamma, beta, rmean,
-                     rvar, momentum, eps, train, mean, invstd, scale, shift);
+int xcp_bn_finalize(const double* part2, int G, int C, int CP, double count, const float* gamma, const float* beta,
+                    float* rmean, float* rvar, float momentum, float eps, int train, float* mean, float* invstd,
+                    float* scale, float* shift, hipStream_t st) {
+  if (C <= 0) return XCP_OK;
+  if (CP < C) return XCP_EINVAL;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((CP + 255) / 256), dim3(256), 0, st, part2, G, C, CP, count, gamma, beta,
+                     rmean, rvar, momentum, eps, train, mean, invstd, scale, shift);
   return (int)hipGetLastError();
 }
 

@@ -121,17 +121,19 @@ __global__ __launch_bounds__(256) void permute3_kernel(const float* __restrict__
 }
 
 // Many permute3 jobs in one launch (the per-step weight packing of every layer).  jobs is a
-// device array of [njobs][10] int64: in, out, d0, d1, d2, p0, p1, p2, out dtype, first block.
+// device array of [njobs][12] int64: in, out, d0, d1, d2, p0, p1, p2, out dtype, first block,
+// s0, s1 (output strides of the first two output axes: padded layouts).
 // Workgroup b finds its job by binary search over the first-block column (uniform per block).
+constexpr int PJ = 12;
 __global__ __launch_bounds__(256) void permute3_batch_kernel(const long long* __restrict__ jobs, int njobs) {
   const int b = blockIdx.x;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (jobs[(long)mid * 10 + 9] <= b) lo = mid;
+    if (jobs[(long)mid * PJ + 9] <= b) lo = mid;
     else hi = mid - 1;
   }
-  const long long* j = jobs + (long)lo * 10;
+  const long long* j = jobs + (long)lo * PJ;
   const float* in = reinterpret_cast<const float*>(j[0]);
   const int d0 = (int)j[2], d1 = (int)j[3], d2 = (int)j[4], p0 = (int)j[5], p1 = (int)j[6], p2 = (int)j[7];
   const long total = (long)d0 * d1 * d2;
@@ -148,8 +150,9 @@ __global__ __launch_bounds__(256) void permute3_batch_kernel(const long long* __
   idx[p1] = o1;
   idx[p2] = o2;
   const float v = in[((long)idx[0] * d1 + idx[1]) * d2 + idx[2]];
-  if (j[8] == XCP_BF16) reinterpret_cast<bf16*>(j[1])[g] = (bf16)v;
-  else reinterpret_cast<float*>(j[1])[g] = v;
+  const long o = (long)o0 * j[10] + (long)o1 * j[11] + o2;
+  if (j[8] == XCP_BF16) reinterpret_cast<bf16*>(j[1])[o] = (bf16)v;
+  else reinterpret_cast<float*>(j[1])[o] = v;
 }
 
 // ---------------------------------------------------------------------------------
@@ -433,7 +436,7 @@ int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int 
   return (int)hipGetLastError();
 }
 
-// njobs permute3 jobs ([njobs][10] int64 on the device, see permute3_batch_kernel) covering
+// njobs permute3 jobs ([njobs][12] int64 on the device, see permute3_batch_kernel) covering
 // nblocks 256-element blocks in total; the host validates the permutations when it builds them
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, hipStream_t st) {
   if (njobs <= 0 || nblocks <= 0) return XCP_OK;

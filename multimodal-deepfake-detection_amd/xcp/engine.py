@@ -109,6 +109,16 @@ WGRAD_SIDE_STREAM = os.environ.get("XCP_WGRAD_STREAM", "1") != "0"
 # fused BN-apply + pointwise dgrad + wgrad for the narrow units (csrc/unitbwd.hip);
 # XCP_FUSED_UNIT_BWD=0 runs the three-kernel sequence (A/B and parity cross-checks)
 FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
+# Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
+# 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
+# columns in the packed weights, zero BN scale / shift / backward coefficients.  XCP_PAD_728=0
+# keeps the dense 728 pitch (A/B).
+PAD_PITCH = {728: 736} if os.environ.get("XCP_PAD_728", "1") != "0" else {}
+
+
+def pc(c):
+    """channel pitch of a c-channel activation"""
+    return PAD_PITCH.get(c, c)
 
 
 class XceptionEngine:
@@ -153,10 +163,10 @@ class XceptionEngine:
 
     def _buf(self, name, n, dtype, dev):
         """Persistent packed-weight buffer (re-used every step, so the batched pack's job
-        table stays valid)."""
+        table stays valid); zero-filled once, so the padding a padded pack skips stays zero."""
         t = self._bufs.get(name)
         if t is None or t.numel() != n or t.dtype != dtype or t.device != dev:
-            t = self._bufs[name] = torch.empty(n, device=dev, dtype=dtype)
+            t = self._bufs[name] = torch.zeros(n, device=dev, dtype=dtype)
         return t
 
     def pack(self):
@@ -169,19 +179,23 @@ class XceptionEngine:
         m = self.model
         dev = m.conv1.weight.device
 
-        def add(name, w, n_dtype, d0, d1, d2, perm):
-            out = self._buf(name, d0 * d1 * d2, n_dtype, dev)
-            jobs.append((w.detach(), out, d0, d1, d2, perm))
+        def add(name, w, n_dtype, d0, d1, d2, perm, rows=None, pitch=None):
+            """pack w permuted; rows x pitch: padded [rows][pitch] destination (2-D packs)"""
+            n = rows * pitch if rows else d0 * d1 * d2
+            out = self._buf(name, n, n_dtype, dev)
+            jobs.append((w.detach(), out, d0, d1, d2, perm, pitch))
             pk[name] = out
 
         for u in self._all_units():
             c = u.sep.conv1.in_channels
-            add(u.name + ".dw", u.sep.conv1.weight, torch.float32, c, 9, 1, (1, 0, 2))
+            add(u.name + ".dw", u.sep.conv1.weight, torch.float32, c, 9, 1, (1, 0, 2), 9, pc(c))
             pw = u.sep.pointwise
-            add(u.name + ".pw", pw.weight, dt, pw.out_channels, pw.in_channels, 1, (0, 1, 2))
+            co, ci = pw.out_channels, pw.in_channels
+            add(u.name + ".pw", pw.weight, dt, co, ci, 1, (0, 1, 2), pc(co), pc(ci))
         for b in self.blocks:
             if b.skip is not None:
-                add(b.name + ".skip", b.skip.weight, dt, b.skip.out_channels, b.skip.in_channels, 1, (0, 1, 2))
+                co, ci = b.skip.out_channels, b.skip.in_channels
+                add(b.name + ".skip", b.skip.weight, dt, co, ci, 1, (0, 1, 2), pc(co), pc(ci))
         add("conv2", m.conv2.weight, dt, 64, 32, 9, (0, 2, 1))   # [co][tap][ci]
         self._pack_fwd.run(jobs)
         self._packed, self._pack_key = pk, key
@@ -196,17 +210,20 @@ class XceptionEngine:
         dev = m.conv1.weight.device
         jobs = []
 
-        def add(name, w, d0, d1, d2, perm):
-            out = self._buf(name, d0 * d1 * d2, dt, dev)
-            jobs.append((w.detach(), out, d0, d1, d2, perm))
+        def add(name, w, d0, d1, d2, perm, rows=None, pitch=None):
+            n = rows * pitch if rows else d0 * d1 * d2
+            out = self._buf(name, n, dt, dev)
+            jobs.append((w.detach(), out, d0, d1, d2, perm, pitch))
             pk[name] = out
 
         for u in self._all_units():
             pw = u.sep.pointwise
-            add(u.name + ".pwT", pw.weight, pw.out_channels, pw.in_channels, 1, (1, 0, 2))
+            co, ci = pw.out_channels, pw.in_channels
+            add(u.name + ".pwT", pw.weight, co, ci, 1, (1, 0, 2), pc(ci), pc(co))
         for b in self.blocks:
             if b.skip is not None:
-                add(b.name + ".skipT", b.skip.weight, b.skip.out_channels, b.skip.in_channels, 1, (1, 0, 2))
+                co, ci = b.skip.out_channels, b.skip.in_channels
+                add(b.name + ".skipT", b.skip.weight, co, ci, 1, (1, 0, 2), pc(ci), pc(co))
         add("conv2T", m.conv2.weight, 64, 32, 9, (1, 2, 0))   # [ci][tap][co]
         self._pack_bwd.run(jobs)
         self._packed_bwd_key = self._pack_key
@@ -222,25 +239,29 @@ class XceptionEngine:
         return torch.empty(n, device=self.device, dtype=dtype or self.dtype)
 
     def _bn_stats(self, part, R, C, count, bnmod, train):
-        s = Stats(C, self.device)
+        """BN statistics of a C-channel tensor (partials and Stats at its channel pitch)"""
+        CP = pc(C)
+        s = Stats(CP, self.device)
         ref = _bn_ref(bnmod)
         if train:
             if ref["momentum"] is None:
                 ref["momentum"] = 1.0 / float(bnmod.num_batches_tracked.item() + 1)
-            ops.finalize_stats(part, R, C, count, ref, True, s)
+            ops.finalize_stats(part, R, C, count, ref, True, s, CP)
         else:
-            ops.eval_stats(C, ref, s, self.device)
+            ops.eval_stats(C, ref, s, self.device, CP)
         return s
 
     def _pw(self, A, Wp, M, cout, cin, train, bnmod, lda=None, gather=(0, 0, 0, 0, 0, 1, 0)):
-        Y = self._empty(M * cout)
+        """pointwise conv at the channel pitches (padded output channels come out zero)"""
+        cop, cip = pc(cout), pc(cin)
+        Y = self._empty(M * cop)
         if train:
             R = ops.nt_stat_rows(M)
-            part = self._empty(R * 2 * cout, torch.float32)
-            ops.gemm_nt(A, Wp, Y, M, cout, cin, lda=lda, stats=part, gather=gather)
+            part = self._empty(R * 2 * cop, torch.float32)
+            ops.gemm_nt(A, Wp, Y, M, cop, cip, lda=lda, stats=part, gather=gather)
             st = self._bn_stats(part, R, cout, M, bnmod, True)
         else:
-            ops.gemm_nt(A, Wp, Y, M, cout, cin, lda=lda, gather=gather)
+            ops.gemm_nt(A, Wp, Y, M, cop, cip, lda=lda, gather=gather)
             st = self._bn_stats(None, 0, cout, M, bnmod, False)
         return Y, st
 
@@ -298,8 +319,8 @@ class XceptionEngine:
         ex = []
         src, act, sc, sh = xc, ACT_NONE, None, None
         for u in self.exit_units:
-            d = self._empty(M * u.cin)
-            ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, u.cin)
+            d = self._empty(M * pc(u.cin))
+            ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, pc(u.cin))
             y, st = self._pw(d, pk[u.name + ".pw"], M, u.cout, u.cin, train, u.bn)
             ex.append({"src": src, "act": act, "sc": sc, "sh": sh, "d": d, "y": y, "st": st})
             src, act, sc, sh = y, ACT_BNRELU, st.scale, st.shift
@@ -318,8 +339,8 @@ class XceptionEngine:
         units = []
         src, act, sc, sh = x_in, (ACT_RELU if b.units[0].relu else ACT_NONE), None, None
         for u in b.units:
-            d = self._empty(M * u.cin)
-            ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, u.cin)
+            d = self._empty(M * pc(u.cin))
+            ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, pc(u.cin))
             y, st = self._pw(d, pk[u.name + ".pw"], M, u.cout, u.cin, train, u.bn)
             units.append({"src": src, "act": act, "sc": sc, "sh": sh, "d": d, "y": y, "st": st})
             src, act, sc, sh = y, ACT_BNRELU, st.scale, st.shift
@@ -330,14 +351,14 @@ class XceptionEngine:
         Ms = N * OH * OW
         ys = sks = None
         if b.skip is not None:
-            ys, sks = self._pw(x_in, pk[b.name + ".skip"], Ms, b.cout, b.cin, train, b.skipbn, lda=b.cin,
+            ys, sks = self._pw(x_in, pk[b.name + ".skip"], Ms, b.cout, b.cin, train, b.skipbn, lda=pc(b.cin),
                                gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
-        out = self._empty(Ms * b.cout)
-        amax = torch.empty(Ms * b.cout, device=self.device, dtype=torch.uint8) if b.pool else None
+        out = self._empty(Ms * pc(b.cout))
+        amax = torch.empty(Ms * pc(b.cout), device=self.device, dtype=torch.uint8) if b.pool else None
         st = units[-1]["st"]
         ops.tail_fwd(units[-1]["y"], st.scale, st.shift, b.pool, ys if ys is not None else x_in,
                      sks.scale if sks is not None else None, sks.shift if sks is not None else None, out, amax, N, H, W,
-                     b.cout)
+                     pc(b.cout))
         bs = {"x_in": x_in, "units": units, "ys": ys, "sks": sks, "amax": amax, "H": H, "W": W, "OH": OH, "OW": OW}
         return out, OH, OW, bs
 
@@ -382,6 +403,9 @@ class XceptionEngine:
         side = self._side_stream(dev) if WGRAD_SIDE_STREAM else None
 
         def wgrad(G, X, M, Nn, K, name, shape, **kw):
+            """dW[Nn][K] = G^T X (logical channels; G / X at their channel pitches)"""
+            kw.setdefault("ldg", pc(Nn))
+            kw.setdefault("ldx", pc(K))
             dst, acc = g(name, shape)
             if side is None:
                 ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, **kw)
@@ -399,18 +423,20 @@ class XceptionEngine:
             pending.clear()
 
         def bn_coef(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
-            """BN backward up to its coefficients (alpha, bcoef, delta); writes the affine grads"""
+            """BN backward up to its coefficients (alpha, bcoef, delta; at the channel pitch);
+            writes the affine grads"""
             P = part[1] if part is not None else 0
             (gw, acc), (gb, acc_b) = g(name + ".weight", (C,)), g(name + ".bias", (C,))
             if acc != acc_b:
                 raise NotImplementedError(f"xcp engine: {name}.weight and .bias must both (or neither) require grad")
             return ops.bn_backward_coef(dZ, Y, rows, C, _bn_ref(bnmod), st, gw, gb,
-                                        part=part[0] if part is not None else None, R=P, relu=relu, accumulate=acc)
+                                        part=part[0] if part is not None else None, R=P, relu=relu, accumulate=acc,
+                                        CP=pc(C))
 
         def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
             coef = bn_coef(bnmod, name, dZ, Y, rows, C, st, part, relu)
-            dY = self._empty(rows * C)
-            ops.bn_apply_coef(dZ, Y, dY, coef, st, rows, C, relu)
+            dY = self._empty(rows * pc(C))
+            ops.bn_apply_coef(dZ, Y, dY, coef, st, rows, pc(C), relu)
             return dY
 
         def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None):
@@ -420,7 +446,7 @@ class XceptionEngine:
             ``prev_st`` is the Stats of the BN feeding this unit -- that BN's backward partial
             sums)."""
             M = N * H * W
-            dD = self._empty(M * u.cin)
+            dD = self._empty(M * pc(u.cin))
             if FUSED_UNIT_BWD and ops.unit_bwd_rows_per_split(dZ.dtype, M, u.cout, u.cin) > 0:
                 # narrow units: BN apply + pointwise dgrad + wgrad in one pass (dY stays on chip)
                 coef = bn_coef(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
@@ -428,12 +454,13 @@ class XceptionEngine:
                 ops.unit_bwd(dZ, rec["y"], coef, pk[u.name + ".pwT"], rec["d"], dD, M, u.cout, u.cin, dst, acc)
             else:
                 dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
-                ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, u.cin, u.cout)
+                ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, pc(u.cin), pc(u.cout))
                 wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
-            dX = self._empty(M * u.cin)
+            dX = self._empty(M * pc(u.cin))
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
-                             u.cin, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, bn_stats=prev_st, accumulate=acc)
+                             pc(u.cin), dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, bn_stats=prev_st, accumulate=acc,
+                             Cw=u.cin)
             return dX, (bnp if prev_st is not None else None)
 
         # ---- exit flow
@@ -488,8 +515,8 @@ class XceptionEngine:
         # at 147^2 x 128; gathering it inside the BN-backward kernels measured 1.83 / 1.88 ms)
         part = None
         if b.pool:
-            dZ = self._empty(N * H * W * b.cout)
-            part = ops.maxpool_bwd_bnred(dOut, bs["amax"], dZ, units[-1]["y"], units[-1]["st"], N, H, W, b.cout)
+            dZ = self._empty(N * H * W * pc(b.cout))
+            part = ops.maxpool_bwd_bnred(dOut, bs["amax"], dZ, units[-1]["y"], units[-1]["st"], N, H, W, pc(b.cout))
         else:
             dZ = dOut
         dRes = dSkip = None
@@ -497,9 +524,9 @@ class XceptionEngine:
         if b.skip is not None:
             dYs = bn_bwd(b.skipbn, b.name + ".skipbn", dOut, bs["ys"], Ms, b.cout, bs["sks"])
             wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1),
-                  gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0), ldx=b.cin)
-            dXs = self._empty(Ms * b.cin)
-            ops.gemm_nt(dYs, pk[b.name + ".skipT"], dXs, Ms, b.cin, b.cout)
+                  gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
+            dXs = self._empty(Ms * pc(b.cin))
+            ops.gemm_nt(dYs, pk[b.name + ".skipT"], dXs, Ms, pc(b.cin), pc(b.cout))
             if b.stride != 1:
                 dSkip, skip_geom = dXs, (OH, OW, b.stride)
             else:

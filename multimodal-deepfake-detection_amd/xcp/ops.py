@@ -106,19 +106,20 @@ def nt_stat_rows(M):
     return _lib.call("xcp_gemm_nt_stat_rows", M)
 
 
-def colreduce_f32(inp, S, L, out, G, accumulate=False):
-    _lib.call("xcp_colreduce_f32", _p(inp), S, L, _p(out), G, 1 if accumulate else 0, stream())
+def colreduce_f32(inp, S, L, out, G, accumulate=False, ld=None):
+    _lib.call("xcp_colreduce_f32", _p(inp), S, L, ld or L, _p(out), G, 1 if accumulate else 0, stream())
 
 
-def reduce_slabs(P, S, L, out, accumulate=False):
-    """out[L] (+)= sum_s P[s][L] (fp32, deterministic; two levels when S is large and L small)."""
+def reduce_slabs(P, S, L, out, accumulate=False, ld=None):
+    """out[L] (+)= sum_s P[s*ld : s*ld + L] (fp32, deterministic; two levels when S is large and
+    L small).  ld (default L): slab stride, e.g. the padded channel pitch of depthwise partials."""
     g = _lib.call("xcp_colreduce_groups", S, L)
     if g:
         tmp = torch.empty(g * L, device=P.device, dtype=torch.float32)
-        colreduce_f32(P, S, L, tmp, g)
+        colreduce_f32(P, S, L, tmp, g, ld=ld)
         colreduce_f32(tmp, g, L, out, 1, accumulate)
     else:
-        colreduce_f32(P, S, L, out, 1, accumulate)
+        colreduce_f32(P, S, L, out, 1, accumulate, ld=ld)
 
 
 def weight_grad(G, X, M, N, K, out, gather=(0, 0, 0, 0, 0, 1, 0), ldg=None, ldx=None, tile=0, accumulate=False):
@@ -137,10 +138,11 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
 
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
-           bn_stats=None, accumulate=False):
+           bn_stats=None, accumulate=False, Cw=None):
     """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
     (that BN's Stats) is given, else (None, 0).  dW_out receives the weight gradient in the
-    nn.Conv2d [C][1][3][3] order (accumulate: added to it)."""
+    nn.Conv2d [C][1][3][3] order (accumulate: added to it); Cw (default C): channels of the
+    weight when C is a padded channel pitch."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
     bnpart = None
@@ -150,7 +152,7 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
               skip_geom[0], skip_geom[1], skip_geom[2], _p(dX), _p(part), _p(bnpart),
               _p(bn_stats["mean"]) if bn_stats is not None else 0,
               _p(bn_stats["invstd"]) if bn_stats is not None else 0, N, H, W, C, stream())
-    reduce_slabs(part, P, C * 9, dW_out, accumulate)
+    reduce_slabs(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
     return bnpart, (P if bnpart is not None else 0)
 
 
@@ -161,37 +163,39 @@ FIN_MAX_ROWS = 2048   # above this many partial rows, pre-reduce to FIN_GROUPS r
 FIN_GROUPS = 256
 
 
-def _fold(part, R, C):
+def _fold(part, R, CP):
     if R <= FIN_MAX_ROWS:
         return part, R
-    p2 = torch.empty(FIN_GROUPS * 2 * C, device=part.device, dtype=torch.float32)
-    colreduce_f32(part, R, 2 * C, p2, FIN_GROUPS)
+    p2 = torch.empty(FIN_GROUPS * 2 * CP, device=part.device, dtype=torch.float32)
+    colreduce_f32(part, R, 2 * CP, p2, FIN_GROUPS)
     return p2, FIN_GROUPS
 
 
-def finalize_stats(part, R, C, count, bn, train, out):
-    """part: fp32 [R][2][C] partial sums -> out dict of mean/invstd/scale/shift (fp32 [C]).
-    Updates bn running stats in place (train mode batch statistics)."""
+def finalize_stats(part, R, C, count, bn, train, out, CP=None):
+    """part: fp32 [R][2][CP] partial sums -> out dict of mean/invstd/scale/shift (fp32 [CP], zero
+    for the CP - C padding channels).  Updates bn running stats in place (train mode batch
+    statistics)."""
     if not train:
         raise ValueError("finalize_stats computes batch statistics (train mode); use eval_stats")
+    CP = CP or C
     track = bn["track"]
-    part, R = _fold(part, R, C)
-    _lib.call("xcp_bn_finalize_part", _p(part), R, C, float(count), _p(bn["weight"]), _p(bn["bias"]),
+    part, R = _fold(part, R, CP)
+    _lib.call("xcp_bn_finalize_part", _p(part), R, C, CP, float(count), _p(bn["weight"]), _p(bn["bias"]),
               _p(bn["running_mean"]) if track else 0, _p(bn["running_var"]) if track else 0, float(bn["momentum"]),
               float(bn["eps"]), _p(out["mean"]), _p(out["invstd"]), _p(out["scale"]), _p(out["shift"]), stream())
 
 
-def _bn_finalize(p2, G, C, count, bn, train, out):
+def _bn_finalize(p2, G, C, count, bn, train, out, CP=None):
     mom = bn["momentum"]
-    _lib.call("xcp_bn_finalize", _p(p2), G, C, float(count), _p(bn["weight"]), _p(bn["bias"]),
+    _lib.call("xcp_bn_finalize", _p(p2), G, C, CP or C, float(count), _p(bn["weight"]), _p(bn["bias"]),
               _p(bn["running_mean"]) if (train and bn["track"]) or not train else 0,
               _p(bn["running_var"]) if (train and bn["track"]) or not train else 0, float(mom), float(bn["eps"]),
               1 if train else 0, _p(out["mean"]), _p(out["invstd"]), _p(out["scale"]), _p(out["shift"]), stream())
 
 
-def eval_stats(C, bn, out, device):
-    p2 = torch.zeros(2 * C, device=device, dtype=torch.float64)
-    _bn_finalize(p2, 1, C, 1.0, bn, False, out)
+def eval_stats(C, bn, out, device, CP=None):
+    p2 = torch.zeros(2 * (CP or C), device=device, dtype=torch.float64)
+    _bn_finalize(p2, 1, C, 1.0, bn, False, out, CP)
 
 
 def row_stats(X, rows, C):
@@ -201,26 +205,28 @@ def row_stats(X, rows, C):
     return part, R
 
 
-def bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False):
+def bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False, CP=None):
     """BatchNorm2d backward (train-mode batch stats) up to the per-channel coefficients:
     returns coef fp32 [3][C] (alpha, bcoef, delta: dY = alpha*dZ' + bcoef*Y + delta, dZ' the
     ReLU-masked dZ when relu) and writes (accumulate: adds to) dgamma/dbeta.
-    ``part`` ([R][2][C] partial (sum dz, sum dz*zhat)) may come fused from the
+    ``part`` ([R][2][CP] partial (sum dz, sum dz*zhat)) may come fused from the
     producer of dZ; otherwise it is reduced here.  relu=True: dZ is the gradient of
-    relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift)."""
+    relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift).  CP (default C):
+    channel pitch of dZ / Y; coef then has CP entries per coefficient, zero for the padding."""
+    CP = CP or C
     ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
     dev, dt = Y.device, Y.dtype
     if part is None:
-        R = _lib.call("xcp_chanred_parts", rows, C)
-        part = torch.empty(R * 2 * C, device=dev, dtype=torch.float32)
-        _lib.call("xcp_bn_bwd_reduce", DT[dt], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), ms, mt, rows, C,
+        R = _lib.call("xcp_chanred_parts", rows, CP)
+        part = torch.empty(R * 2 * CP, device=dev, dtype=torch.float32)
+        _lib.call("xcp_bn_bwd_reduce", DT[dt], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), ms, mt, rows, CP,
                   _p(part), stream())
     elif relu:
         raise ValueError("a fused partial cannot carry the ReLU mask")
-    coef = torch.empty(3 * C, device=dev, dtype=torch.float32)
-    part, R = _fold(part, R, C)
-    _lib.call("xcp_bn_bwd_finalize_part", _p(part), R, C, float(rows), _p(bn["weight"]), _p(st["mean"]),
-              _p(st["invstd"]), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta),
+    coef = torch.empty(3 * CP, device=dev, dtype=torch.float32)
+    part, R = _fold(part, R, CP)
+    _lib.call("xcp_bn_bwd_finalize_part", _p(part), R, C, CP, float(rows), _p(bn["weight"]), _p(st["mean"]),
+              _p(st["invstd"]), _p(coef), _p(coef[CP:]), _p(coef[2 * CP:]), _p(dgamma), _p(dbeta),
               1 if accumulate else 0, stream())
     return coef
 
@@ -233,7 +239,8 @@ def bn_backward(dZ, Y, rows, C, bn, st, dY, dgamma, dbeta, part=None, R=0, relu=
 
 
 def bn_apply_coef(dZ, Y, dY, coef, st, rows, C, relu=False):
-    """dY = alpha*dZ' + bcoef*Y + delta (coef from bn_backward_coef; dZ' ReLU-masked when relu)"""
+    """dY = alpha*dZ' + bcoef*Y + delta (coef from bn_backward_coef; dZ' ReLU-masked when relu);
+    C: the channel pitch (coef has C entries per coefficient)"""
     ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
     _lib.call("xcp_bn_bwd_apply", DT[Y.dtype], _p(dZ), _p(Y), _p(dY), _p(coef), _p(coef[C:]), _p(coef[2 * C:]), ms,
               mt, rows, C, stream())
@@ -393,17 +400,25 @@ class PermuteBatch:
         self._nblocks = 0
 
     def run(self, jobs):
-        """jobs: list of (src fp32 tensor, dst tensor, d0, d1, d2, perm)."""
-        key = tuple((s.data_ptr(), d.data_ptr(), d0, d1, d2, tuple(pm), d.dtype) for s, d, d0, d1, d2, pm in jobs)
+        """jobs: list of (src fp32 tensor, dst tensor, d0, d1, d2, perm[, s0]): output element
+        (o0, o1, o2) of the permuted [od0][od1][od2] array goes to dst[o0*s0 + o1*od2 + o2]
+        (s0 default od1*od2; larger for a padded destination, whose padding is left alone)."""
+        jobs = [j if len(j) == 7 else (*j, None) for j in jobs]
+        key = tuple((s.data_ptr(), d.data_ptr(), d0, d1, d2, tuple(pm), d.dtype, s0)
+                    for s, d, d0, d1, d2, pm, s0 in jobs)
         if key != self._key:
             rows, blk = [], 0
-            for s, d, d0, d1, d2, pm in jobs:
+            for s, d, d0, d1, d2, pm, s0 in jobs:
                 n = d0 * d1 * d2
-                if sorted(pm) != [0, 1, 2] or s.numel() != n or d.numel() != n or s.dtype != torch.float32 \
-                        or not s.is_contiguous() or not d.is_contiguous():
+                dims = (d0, d1, d2)
+                od0, od1, od2 = dims[pm[0]], dims[pm[1]], dims[pm[2]]
+                s1 = od2
+                s0 = s0 or od1 * od2
+                if sorted(pm) != [0, 1, 2] or s.numel() != n or s0 < od1 * od2 or d.numel() < (od0 - 1) * s0 + od1 * od2 \
+                        or s.dtype != torch.float32 or not s.is_contiguous() or not d.is_contiguous():
                     raise ValueError("permute job: bad permutation, size, dtype or layout")
                 check_gpu(s, d)
-                rows.append([s.data_ptr(), d.data_ptr(), d0, d1, d2, pm[0], pm[1], pm[2], DT[d.dtype], blk])
+                rows.append([s.data_ptr(), d.data_ptr(), d0, d1, d2, pm[0], pm[1], pm[2], DT[d.dtype], blk, s0, s1])
                 blk += (n + 255) // 256
             self._table = torch.tensor(rows, dtype=torch.int64).to(jobs[0][1].device)
             self._nblocks, self._key = blk, key

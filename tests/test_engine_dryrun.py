@@ -37,11 +37,11 @@ def install_fake_lib(monkeypatch):
         for a, t in zip(args, sig):
             t(a if a is not None else 0)  # raises on an unconvertible argument
         calls.append(name)
-        if name == "xcp_colreduce_f32":       # (in, S, L, out, G, accumulate, stream): gradient slabs
-            _fill(args[3], args[2] * args[4], args[5])
-        elif name == "xcp_bn_bwd_finalize_part" and args[10]:   # dgamma, dbeta (C each)
-            _fill(args[10], args[2], args[12])
-            _fill(args[11], args[2], args[12])
+        if name == "xcp_colreduce_f32":       # (in, S, L, ld, out, G, accumulate, stream): gradient slabs
+            _fill(args[4], args[2] * args[5], args[6])
+        elif name == "xcp_bn_bwd_finalize_part" and args[11]:   # dgamma, dbeta (C each)
+            _fill(args[11], args[2], args[13])
+            _fill(args[12], args[2], args[13])
         elif name == "xcp_permute3" and args[0] == 0:          # fp32 permute (stem conv2 gradient)
             _fill(args[2], args[3] * args[4] * args[5], False)
         if name == "xcp_dw_bwd_chunks":

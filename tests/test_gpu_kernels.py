@@ -331,6 +331,45 @@ def test_bn_forward_backward(ops, gpu, dt, rows, C, relu):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+def test_bn_padded_channel_pitch(ops, gpu, dt):
+    """The 728-channel flow at its 736 pitch: statistics, running buffers and backward over
+    the padded rows equal the dense ones on the 728 real channels, and the padding channels get
+    zero scale / shift / backward coefficients (so they stay zero downstream)."""
+    from xcp.engine import Stats
+    rows, C, CP = 3 * 361, 728, 736
+    g = torch.Generator(device=gpu).manual_seed(7)
+    y = (torch.randn(rows, C, device=gpu, generator=g) * 2 + 0.7).to(dt)
+    dz = torch.randn(rows, C, device=gpu, generator=g).to(dt)
+    yp, dzp = torch.zeros(rows, CP, device=gpu, dtype=dt), torch.zeros(rows, CP, device=gpu, dtype=dt)
+    yp[:, :C], dzp[:, :C] = y, dz
+    gamma, beta = torch.rand(C, device=gpu, generator=g) + 0.5, torch.randn(C, device=gpu, generator=g) * 0.1
+    res = []
+    for (yy, dd, cp) in ((y, dz, C), (yp, dzp, CP)):
+        rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+        bn = {"weight": gamma, "bias": beta, "running_mean": rm, "running_var": rv, "eps": 1e-5, "momentum": 0.1,
+              "track": True}
+        part, R = ops.row_stats(yy, rows, cp)
+        st = Stats(cp, gpu)
+        ops.finalize_stats(part, R, C, rows, bn, True, st, cp)
+        dY = torch.full((rows, cp), float("nan"), device=gpu, dtype=dt)
+        dg, db = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+        coef = ops.bn_backward_coef(dd, yy, rows, C, bn, st, dg, db, CP=cp)
+        ops.bn_apply_coef(dd, yy, dY, coef, st, rows, cp)
+        res.append((st, rm, rv, dY, dg, db, coef))
+    (s0, rm0, rv0, d0, g0, b0, _), (s1, rm1, rv1, d1, g1, b1, c1) = res
+    for k in ("mean", "invstd", "scale", "shift"):
+        torch.testing.assert_close(s1[k][:C], s0[k], rtol=1e-6, atol=1e-6)
+        assert torch.all(s1[k][C:] == 0), k
+    torch.testing.assert_close(rm1, rm0, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(rv1, rv0, rtol=1e-6, atol=1e-7)
+    assert torch.all(c1.view(3, CP)[:, C:] == 0)
+    assert torch.all(d1[:, C:] == 0)
+    assert rel_err(d1[:, :C].float(), d0.float()) < 1e-5
+    torch.testing.assert_close(g1, g0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(b1, b0, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("H", [147, 37, 19, 20])
 def test_tail_maxpool_fwd_bwd(ops, gpu, dt, H):
     N, C = 2, 128
