@@ -112,8 +112,11 @@ FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
 # columns in the packed weights, zero BN scale / shift / backward coefficients.  XCP_PAD_728=0
-# keeps the dense 728 pitch (A/B).
-PAD_PITCH = {728: 736} if os.environ.get("XCP_PAD_728", "1") != "0" else {}
+# keeps the dense 728 pitch, XCP_PAD_728=<pitch> (a multiple of 8 above 728) sets another (A/B).
+_pad = os.environ.get("XCP_PAD_728", "736")
+PAD_PITCH = {} if _pad == "0" else {728: int(_pad)}
+if PAD_PITCH and (PAD_PITCH[728] < 728 or PAD_PITCH[728] % 8):
+    raise ValueError("XCP_PAD_728 must be 0 or a multiple of 8 >= 728")
 
 
 def pc(c):
