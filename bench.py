@@ -392,7 +392,7 @@ def main():
     dev = torch.device("cuda", local)
 
     import xcp
-    from xcp import ops
+    from xcp import engine, ops
     xcp.set_compute_dtype(args.dtype)
     xcp.load_library()
     audio, single, fusion = args.model == "lstma", args.model == "xception", args.model == "auface"
@@ -408,9 +408,10 @@ def main():
         timer = None
         if not args.no_kernel_timing and mode == modes[0] and not audio and not fusion:
             hm = middle_hw(S)
+            cp = engine.pc(728)   # the 728-channel flow's channel pitch (736: padded rows)
             timer = ops.KernelTimer({"pw_gemm_728": lambda name, a: name == "gemm_nt" and a["M"] == frames * hm * hm
-                                     and a["N"] == 728 and a["K"] == 728 and a["stats"] is not None,
-                                     "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == 728 and a["H"] == hm})
+                                     and a["N"] == cp and a["K"] == cp and a["stats"] is not None,
+                                     "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == cp and a["H"] == hm})
         steps = args.steps if mode == modes[0] else max(3, args.steps // 2)
         elapsed, loss = timed(run, steps, args.warmup, world, timer)
         results[mode] = (elapsed, steps, loss, timer)
@@ -437,7 +438,8 @@ def main():
                         "frac": round(ach / PEAK_BF16_TFLOPS, 4),
                         "traffic": traffic.get("gemm_nt", (None,))[0],
                         "traffic_source": traffic.get("gemm_nt", (None, None))[1],
-                        "kernel": f"gemm_nt256k64_kernel (bf16 pointwise 1x1 728->728 @{hm}x{hm}, middle flow)",
+                        "kernel": f"gemm_nt256k64_kernel (bf16 pointwise 1x1 728->728 @{hm}x{hm}, middle flow; "
+                                  f"channel pitch {engine.pc(728)}, flops counted for the 728 real channels)",
                         "flops_per_launch": flops, "avg_launch_ms": round(pw_ms, 4), "launches": timer.count("pw_gemm_728")}
             if dw_ms:
                 byts = 2.0 * (2 * M * 728) + 4 * 9 * 728
@@ -446,7 +448,8 @@ def main():
                                         "frac": round(gbs / PEAK_HBM_GBS, 4),
                                         "traffic": traffic.get("dw_fwd_kernel", (None,))[0],
                                         "traffic_source": traffic.get("dw_fwd_kernel", (None, None))[1],
-                                        "kernel": f"dw_fwd_kernel<bf16> (depthwise 3x3 C=728 @{hm}x{hm})",
+                                        "kernel": f"dw_fwd_kernel<bf16> (depthwise 3x3 C=728 @{hm}x{hm}; channel pitch "
+                                                  f"{engine.pc(728)}, bytes counted for the 728 real channels)",
                                         "bytes_per_launch": byts, "avg_launch_ms": round(dw_ms, 4)}
         if not audio and not fusion and args.dtype == "bf16":
             ideal, fl, by = step_roofline(S, frames, head == "unfrozen")

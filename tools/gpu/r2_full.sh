@@ -1,4 +1,4 @@
-# GPU: full -m gpu suite, the default bench, then the GEMM ablation timings.
+# GPU: full -m gpu suite, smoke(), then the default bench (with its CPU baseline).
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -7,5 +7,5 @@ timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-m
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/r2_t.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py > gpurun_out/r2_b.json 2> gpurun_out/r2_b.err || exit $?
-timeout -k 10 300 python -u tools/gemm_exp.py run > gpurun_out/r2_exp.log 2>&1
+timeout -k 10 170 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r2_smoke.log 2>&1 || exit $?
+timeout -k 10 600 python bench.py > gpurun_out/r2_b.json 2> gpurun_out/r2_b.err
