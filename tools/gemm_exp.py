@@ -6,7 +6,9 @@ travel to the GPU box) and timed at the middle-flow shape (M = 256 x 19 x 19, 72
   python tools/gemm_exp.py run          # on the GPU box
 
 Variants: base (unpatched), nomfma (MFMAs replaced by a register sink that keeps the
-fragment reads alive), noload (LDS-DMA issues removed: LDS holds stale data), nomfma+noload.
+fragment reads alive), noload (LDS-DMA issues removed: LDS holds stale data), nomfma+noload,
+nobar2 / noload_nobar2 (timing only: the barrier after each MFMA cluster removed).
+GEMM_EXP_VARIANTS=a,b selects a subset.
 """
 import ctypes
 import os
@@ -34,7 +36,9 @@ XCP_DEV void xcp_fake_bload(__amdgpu_buffer_rsrc_t r, void __attribute__((addres
   asm volatile("" :: "v"(o));
 }
 '''
-VARIANTS = {"base": (), "nomfma": ("mfma",), "noload": ("load",), "nomfma_noload": ("mfma", "load")}
+VARIANTS = {"base": (), "nomfma": ("mfma",), "noload": ("load",), "nomfma_noload": ("mfma", "load"),
+            "nobar2": ("bar2",), "noload_nobar2": ("load", "bar2")}
+SEL = os.environ.get("GEMM_EXP_VARIANTS")   # comma-separated subset to build / run
 
 
 def patched(kinds):
@@ -44,6 +48,10 @@ def patched(kinds):
     if "mfma" in kinds:
         s = s.replace("__builtin_amdgcn_mfma_f32_16x16x32_bf16(", "xcp_fake_mfma(")
         extra += FAKE_MFMA
+    if "bar2" in kinds:   # timing only: NT256 phases without the barrier after each MFMA cluster
+        old = "    mfma_q(ih, b, jh);\n    __builtin_amdgcn_s_setprio(0);\n    __builtin_amdgcn_s_barrier();\n"
+        assert old in s
+        s = s.replace(old, "    mfma_q(ih, b, jh);\n    __builtin_amdgcn_s_setprio(0);\n")
     if "load" in kinds:
         s = s.replace("__builtin_amdgcn_global_load_lds(", "xcp_fake_glds(")
         s = s.replace("__builtin_amdgcn_raw_ptr_buffer_load_lds(", "xcp_fake_bload(")
@@ -55,6 +63,8 @@ def patched(kinds):
 def build():
     os.makedirs(OUT, exist_ok=True)
     for name, kinds in VARIANTS.items():
+        if SEL and name not in SEL.split(","):
+            continue
         src = os.path.join(OUT, f"gemm_{name}.hip")
         open(src, "w").write(patched(kinds))
         so = os.path.join(OUT, f"libgemm_{name}.so")
@@ -93,6 +103,8 @@ def run():
         return s.elapsed_time(e) / iters * 1e3
 
     for name in VARIANTS:
+        if SEL and name not in SEL.split(","):
+            continue
         lib = ctypes.CDLL(os.path.join(OUT, f"libgemm_{name}.so"))
         for fn in ("xcp_gemm_nt", "xcp_gemm_tn", "xcp_gemm_tn_rows_per_split"):
             getattr(lib, fn).argtypes = _lib.SIGNATURES[fn]
