@@ -7,7 +7,8 @@ travel to the GPU box) and timed at the middle-flow shape (M = 256 x 19 x 19, 72
 
 Variants: base (unpatched), nomfma (MFMAs replaced by a register sink that keeps the
 fragment reads alive), noload (LDS-DMA issues removed: LDS holds stale data), nomfma+noload,
-nobar2 / noload_nobar2 (timing only: the barrier after each MFMA cluster removed).
+nobar2 / noload_nobar2 (timing only: the barrier after each MFMA cluster removed), noepi /
+noload_noepi (timing only: the epilogue replaced by a register sink).
 GEMM_EXP_VARIANTS=a,b selects a subset.
 """
 import ctypes
@@ -37,7 +38,7 @@ XCP_DEV void xcp_fake_bload(__amdgpu_buffer_rsrc_t r, void __attribute__((addres
 }
 '''
 VARIANTS = {"base": (), "nomfma": ("mfma",), "noload": ("load",), "nomfma_noload": ("mfma", "load"),
-            "nobar2": ("bar2",), "noload_nobar2": ("load", "bar2")}
+            "nobar2": ("bar2",), "noload_nobar2": ("load", "bar2"), "noepi": ("epi",), "noload_noepi": ("load", "epi")}
 SEL = os.environ.get("GEMM_EXP_VARIANTS")   # comma-separated subset to build / run
 
 
@@ -52,6 +53,16 @@ def patched(kinds):
         old = "    mfma_q(ih, b, jh);\n    __builtin_amdgcn_s_setprio(0);\n    __builtin_amdgcn_s_barrier();\n"
         assert old in s
         s = s.replace(old, "    mfma_q(ih, b, jh);\n    __builtin_amdgcn_s_setprio(0);\n")
+    if "epi" in kinds:    # timing only: NT256 epilogue replaced by a sink that keeps every MFMA alive
+        old = "  epilogue256_regs(acc, a, m0, n0, wr, wc, fr, fg);\n}"
+        assert old in s
+        s = s.replace(old, """  float sink = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sink += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+  if (sink == 1234.5f) reinterpret_cast<float*>(a.stats)[threadIdx.x] = sink;
+}""")
     if "load" in kinds:
         s = s.replace("__builtin_amdgcn_global_load_lds(", "xcp_fake_glds(")
         s = s.replace("__builtin_amdgcn_raw_ptr_buffer_load_lds(", "xcp_fake_bload(")
