@@ -222,10 +222,12 @@ def test_gemm_operands_over_2gb_global_address_path(ops, gpu):
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("act", [0, 1, 2])
 @pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9), (1, 64, 147), (2, 256, 74),
-                                   (5, 728, 3), (2, 200, 1), (3, 728, 7), (4, 1024, 3)])
+                                   (5, 728, 3), (2, 200, 1), (3, 728, 7), (4, 1024, 3), (301, 728, 19),
+                                   (2600, 64, 9)])
 def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
     """Tile forward (LDS halo tile), tiny-frame forward (W <= 8, bf16: the (7, 8), (3, 4),
-    (1, 2) frames), and the fused LDS row-walk backward (dgrad + wgrad + BN partial sums)."""
+    (1, 2) frames), and the fused LDS row-walk backward (dgrad + wgrad + BN partial sums).
+    N = 301 / 2600: grids of more than one round of resident workgroups / waves."""
     W = H + 1
     g = torch.Generator(device=gpu).manual_seed(C + H + act)
     x = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
@@ -275,8 +277,10 @@ def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-def test_dw_bwd_residual_and_skip(ops, gpu, dt):
-    N, C, H, W = 2, 128, 15, 15
+@pytest.mark.parametrize("N", [2, 701])
+def test_dw_bwd_residual_and_skip(ops, gpu, dt, N):
+    """Residual and strided-skip gradient adds (N = 701: several rounds of resident waves)."""
+    C, H, W = 128, 15, 15
     x = torch.randn(N, C, H, W, device=gpu).to(dt)
     w = torch.randn(C, 1, 3, 3, device=gpu) / 3
     Wt = w.reshape(C, 9).t().contiguous()

@@ -207,8 +207,8 @@ def main():
                 flops=2.0 * Mp * C * C)
             del Xp, Yp, Dp
     if "dwshapes" in sel:   # depthwise forward at the step's shapes (256 frames)
-        for (Hs, Cs, act) in ((147, 64, 0), (147, 128, 2), (74, 128, 1), (74, 256, 2), (37, 256, 1), (37, 728, 2),
-                              (19, 728, 1), (19, 728, 2), (19, 1024, 2), (10, 1536, 0), (10, 2048, 2)):
+        for (Hs, Cs, act) in ((147, 64, 0), (147, 128, 2), (74, 128, 1), (74, 256, 2), (37, 256, 1), (37, 736, 2),
+                              (19, 736, 1), (19, 736, 2), (19, 1024, 2), (10, 1536, 0), (10, 2048, 2)):
             Ms = N * Hs * Hs
             Xs = torch.randn(Ms, Cs, device=dev, generator=g).to(dt)
             Ys = torch.empty_like(Xs)
@@ -218,6 +218,23 @@ def main():
             rep(f"dw_fwd {Hs}^2 x {Cs} act={act}", timeit(lambda: ops.dw_fwd(act, Xs, Ys, Wts, scs, shs, N, Hs, Hs, Cs)),
                 4 * Ms * Cs)
             del Xs, Ys
+    if "dwbshapes" in sel:   # depthwise backward at the step's shapes (256 frames)
+        for (Hs, Cs, act, res) in ((147, 64, 0, False), (147, 128, 2, False), (74, 128, 1, True), (74, 256, 2, False),
+                                   (37, 256, 1, True), (37, 736, 2, False), (19, 736, 1, True), (19, 736, 2, False),
+                                   (10, 1024, 2, False), (10, 1536, 0, False)):
+            Ms = N * Hs * Hs
+            Xs = torch.randn(Ms, Cs, device=dev, generator=g).to(dt)
+            Ds = torch.randn(Ms, Cs, device=dev, generator=g).to(dt)
+            Ys = torch.empty_like(Xs)
+            Wts = torch.randn(9, Cs, device=dev, generator=g)
+            scs = torch.rand(Cs, device=dev, generator=g) + 0.5
+            shs = torch.randn(Cs, device=dev, generator=g)
+            dWs = torch.empty(Cs * 9, device=dev)
+            sts = {"mean": torch.zeros(Cs, device=dev), "invstd": torch.ones(Cs, device=dev)} if act == 2 else None
+            rep(f"dw_bwd {Hs}^2 x {Cs} act={act}{' +res' if res else ''}",
+                timeit(lambda: ops.dw_bwd(act, Ds, Xs, Wts, scs, shs, Ys, dWs, N, Hs, Hs, Cs, bn_stats=sts,
+                                          dRes=Ds if res else None)), (4 if res else 3) * Ms * Cs * 2)
+            del Xs, Ds, Ys
     if "unitbwd" in sel:   # block1 / block2 unit backward (256 frames): fused vs three kernels
         for (Hu, CO, CI) in ((147, 128, 128), (147, 128, 64), (74, 256, 256), (74, 256, 128)):
             Mu = N * Hu * Hu
