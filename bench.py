@@ -58,6 +58,12 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--small-batch", type=int, default=4,
+                    help="lstmv: also time the unfrozen step at this many clips/GPU (train_visual.py:545 uses 4; "
+                         "0: off)")
+    ap.add_argument("--measured-peaks", choices=["on", "off"], default="on",
+                    help="time a bf16 GEMM (torch.matmul -> hipBLASLt, 8192^3) and a device copy after the timed "
+                         "region and report the roofline fractions against them too")
     ap.add_argument("--optim", choices=["fused", "torch"], default="fused",
                     help="fused: xcp.optim.FusedAdamClip (clip + Adam in two HIP launches); torch: "
                          "clip_grad_norm_ + torch.optim.Adam(fused=True)")
@@ -339,6 +345,37 @@ class Run:
         return loss
 
 
+def measured_peaks(dev):
+    """Live peaks on this GPU, after the timed region (report the fraction of a
+    measured GEMM peak and of a measured stream-copy peak beside the spec peaks)."""
+    import torch
+    a = torch.randn(8192, 8192, device=dev).to(torch.bfloat16)
+    c = torch.empty_like(a)
+    x = torch.empty(256 << 20, device=dev, dtype=torch.bfloat16)   # 512 MB: twice the Infinity Cache
+    y = torch.empty_like(x)
+
+    def best(fn, reps=10):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps * 1e-3
+
+    t_mm = best(lambda: torch.matmul(a, a, out=c))
+    t_cp = best(lambda: y.copy_(x))
+    out = {"gemm_bf16_tflops": round(2.0 * 8192 ** 3 / t_mm / 1e12, 1),
+           "gemm_source": "torch.matmul (hipBLASLt) bf16 8192x8192x8192, mean of 10",
+           "copy_gbs": round(2.0 * x.numel() * 2 / t_cp / 1e9, 1),
+           "copy_source": "device copy of 512 MB (read + write bytes), mean of 10"}
+    del a, c, x, y
+    torch.cuda.empty_cache()
+    return out
+
+
 def timed(run, steps, warmup, world, timer=None):
     import torch
     import torch.distributed as dist
@@ -417,6 +454,19 @@ def main():
         results[mode] = (elapsed, steps, loss, timer)
         if rank == 0:
             log(f"{args.model} {mode}: {1e3 * elapsed / steps:.2f} ms/step")
+        del run
+        torch.cuda.empty_cache()
+    small = None
+    if args.model == "lstmv" and args.small_batch and args.small_batch != B:
+        # the script's own batch (train_visual.py:545), unfrozen, on every rank (the step all-reduces)
+        import copy
+        a4 = copy.copy(args)
+        a4.batch = args.small_batch
+        run = Run(a4, "unfrozen", dev, rank, world)
+        s4 = max(5, args.steps // 2)
+        e4, l4 = timed(run, s4, max(2, args.warmup), world)
+        small = {"batch": a4.batch, "value": round(a4.batch * world * s4 / e4, 3), "ms_per_step": round(1e3 * e4 / s4, 3),
+                 "steps": s4, "loss": round(l4, 5), "mode": "unfrozen"}
         del run
         torch.cuda.empty_cache()
 
@@ -498,6 +548,15 @@ def main():
                           "parallelism": f"dp{world}"},
                "roofline": roof, "loss": round(loss, 5)}
         out.update(extra)
+        if small is not None:
+            out["small_batch"] = small
+        if args.measured_peaks == "on" and not audio and not fusion:
+            mp = measured_peaks(dev)
+            out["measured_peaks"] = mp
+            if out.get("roofline"):
+                out["roofline"]["frac_of_measured_peak"] = round(out["roofline"]["achieved"] / mp["gemm_bf16_tflops"], 4)
+            if out.get("roofline_dw"):
+                out["roofline_dw"]["frac_of_measured_peak"] = round(out["roofline_dw"]["achieved"] / mp["copy_gbs"], 4)
         if args.cpu_baseline == "on" and world == 1 and not single and not fusion:
             out["cpu_baseline"] = cpu_baseline(args, T)
         print(json.dumps(out), flush=True)
