@@ -155,8 +155,5 @@ def broadcast_buffers(module, src=0):
         return
     flat = torch.cat([b.reshape(-1) for b in bufs])
     dist.broadcast(flat, src)
-    off = 0
-    for b in bufs:
-        n = b.numel()
-        b.copy_(flat[off:off + n].view_as(b))
-        off += n
+    # one multi-tensor launch instead of a copy kernel per BN buffer (~80 per step)
+    torch._foreach_copy_(bufs, [v.view_as(b) for v, b in zip(flat.split([b.numel() for b in bufs]), bufs)])
