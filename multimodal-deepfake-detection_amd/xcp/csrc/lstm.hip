@@ -286,7 +286,8 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(const float* __restr
                                                             float* __restrict__ hn, float* __restrict__ cn, int B, int T,
                                                             int t) {
   constexpr int H = KS * 32, G4 = 4 * H, PS = KS + 4;   // LDS slice pitch (floats)
-  extern __shared__ float sm[];                          // h_{t-1} [B][32][PS], then pre [8][B]
+  constexpr int RP = 33;                                // pitch of a (row, clip) partial row
+  extern __shared__ float sm[];   // h_{t-1} [B][32][PS] (then the partials [8][B][RP]), then pre [8][B]
   float* sh = sm;
   float* spre = sm + B * 32 * PS;
   const int tid = threadIdx.x, u0 = blockIdx.x * LS_UPW;
@@ -299,26 +300,59 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(const float* __restr
     const float4 v = *reinterpret_cast<const float4*>(whh + (long)j * H + s * KS + i);
     w[i] = v.x; w[i + 1] = v.y; w[i + 2] = v.z; w[i + 3] = v.w;
   }
-  // stage h_{t-1} (zero at t = 0)
-  for (int e = tid; e < B * H / 4; e += 256) {
-    const int b = e / (H / 4), k4 = (e - b * (H / 4)) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (t > 0) v = *reinterpret_cast<const float4*>(out + ((long)b * T + t - 1) * H + k4);
-    *reinterpret_cast<float4*>(sh + (b * 32 + k4 / KS) * PS + (k4 % KS)) = v;
+  // stage h_{t-1} (zero at t = 0): 8 loads in flight per thread
+  const int n4 = B * H / 4;
+  for (int e0 = tid; e0 < n4; e0 += 8 * 256) {
+    float4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = e0 + i * 256;
+      const int b = e / (H / 4), k4 = (e - b * (H / 4)) * 4;
+      v[i] = (t > 0 && e < n4) ? *reinterpret_cast<const float4*>(out + ((long)b * T + t - 1) * H + k4)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = e0 + i * 256;
+      const int b = e / (H / 4), k4 = (e - b * (H / 4)) * 4;
+      if (e < n4) *reinterpret_cast<float4*>(sh + (b * 32 + k4 / KS) * PS + (k4 % KS)) = v[i];
+    }
   }
   __syncthreads();
-  for (int b = 0; b < B; ++b) {
-    const float* hb = sh + (b * 32 + s) * PS;
-    float a0 = 0.f, a1 = 0.f;
+  // every clip's partial dot of this thread's row slice, independent chains (no per-clip
+  // cross-lane reduction on the critical path)
+  float acc[LS_MAXB];
 #pragma unroll
-    for (int i = 0; i < KS; i += 2) {
-      a0 = fmaf(w[i], hb[i], a0);
-      a1 = fmaf(w[i + 1], hb[i + 1], a1);
+  for (int b = 0; b < LS_MAXB; ++b) {
+    acc[b] = 0.f;
+    if (b < B) {
+      const float* hb = sh + (b * 32 + s) * PS;
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < KS; i += 2) {
+        a0 = fmaf(w[i], hb[i], a0);
+        a1 = fmaf(w[i + 1], hb[i + 1], a1);
+      }
+      acc[b] = a0 + a1;
     }
-    float acc = a0 + a1;
+  }
+  __syncthreads();   // h_{t-1} no longer read: its space takes the partials
+  float* red = sm;
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) acc += __shfl_xor(acc, o, 64);
-    if (s == 0) spre[r * B + b] = acc;
+  for (int b = 0; b < LS_MAXB; ++b)
+    if (b < B) red[(r * B + b) * RP + s] = acc[b];
+  __syncthreads();
+  // (row, clip) threads sum the 32 slices in the pairwise order of a 5-level xor butterfly
+  if (tid < 8 * B) {
+    const float* pr = red + tid * RP;
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = pr[i];
+#pragma unroll
+    for (int w2 = 1; w2 < 32; w2 <<= 1)
+#pragma unroll
+      for (int i = 0; i < 32; i += 2 * w2) v[i] = v[i] + v[i + w2];
+    spre[tid] = v[0];   // tid = row * B + clip
   }
   __syncthreads();
   if (tid < B * LS_UPW) {
@@ -337,7 +371,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(const float* __restr
     const float h = og * tanhf(c);
     float* gt = gates + ((long)b * T + t) * G4;
     gt[k] = ig; gt[H + k] = fg; gt[2 * H + k] = gg; gt[3 * H + k] = og;
-    hprev[ob + k] = t > 0 ? sh[(b * 32 + k / KS) * PS + k % KS] : 0.f;
+    hprev[ob + k] = t > 0 ? out[ob - H + k] : 0.f;
     cst[ob + k] = c;
     out[ob + k] = h;
     if (t == T - 1) {

@@ -235,6 +235,22 @@ def main():
                 timeit(lambda: ops.dw_bwd(act, Ds, Xs, Wts, scs, shs, Ys, dWs, N, Hs, Hs, Cs, bn_stats=sts,
                                           dRes=Ds if res else None)), (4 if res else 3) * Ms * Cs * 2)
             del Xs, Ds, Ys
+    if "dwloc" in sel:   # same bytes, different channel counts: channel slicing vs frame size at 19^2 and 147^2
+        for (Hs, Cs, Ns) in ((19, 736, 256), (19, 128, 1472), (19, 64, 2944), (147, 128, 256), (147, 736, 44)):
+            Ms = Ns * Hs * Hs
+            Xs = torch.randn(Ms, Cs, device=dev, generator=g).to(dt)
+            Ds = torch.randn(Ms, Cs, device=dev, generator=g).to(dt)
+            Ys = torch.empty_like(Xs)
+            Wts = torch.randn(9, Cs, device=dev, generator=g)
+            scs = torch.rand(Cs, device=dev, generator=g) + 0.5
+            shs = torch.randn(Cs, device=dev, generator=g)
+            dWs = torch.empty(Cs * 9, device=dev)
+            sts = {"mean": torch.zeros(Cs, device=dev), "invstd": torch.ones(Cs, device=dev)}
+            rep(f"dw_fwd {Hs}^2 x {Cs} N={Ns} act=2", timeit(lambda: ops.dw_fwd(2, Xs, Ys, Wts, scs, shs, Ns, Hs, Hs, Cs)),
+                4 * Ms * Cs)
+            rep(f"dw_bwd {Hs}^2 x {Cs} N={Ns} act=2", timeit(lambda: ops.dw_bwd(2, Ds, Xs, Wts, scs, shs, Ys, dWs, Ns, Hs,
+                                                                                 Hs, Cs, bn_stats=sts)), 6 * Ms * Cs)
+            del Xs, Ds, Ys
     if "unitbwd" in sel:   # block1 / block2 unit backward (256 frames): fused vs three kernels
         for (Hu, CO, CI) in ((147, 128, 128), (147, 128, 64), (74, 256, 256), (74, 256, 128)):
             Mu = N * Hu * Hu
