@@ -41,10 +41,8 @@ typedef void* xcp_stream_t; /* hipStream_t */
  * (sum, sum^2) of the stored C columns (BatchNorm batch statistics).
  * gmode: 0 dense rows, 1 strided (skip conv, stride gS), 2 im2col 3x3 p0,
  *        3 transposed im2col (conv input gradient); gC = channels per tap.
- * tile: 0 = automatic (256x368 8-wave kernel for dense bf16 with 368 < N <= 736, K >= 384 and
- *       >= 256 tiles -- the 736-pitch 728-channel flow; else 256x256 for >= 256 output tiles and
- *       K >= 384; else 128x128), 1 = force 128x128, 2 = force 256x256, 3 = force 256x368
- *       (2 and 3: dense bf16 only). */
+ * tile: 0 = automatic (256x256 8-wave kernel for dense bf16 with >= 256 output tiles and
+ *       K >= 384, else 128x128), 1 = force 128x128, 2 = force 256x256 (dense bf16 only). */
 int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                 float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, xcp_stream_t stream);
 /* number of partial rows in gemm_nt's stats array for M rows */

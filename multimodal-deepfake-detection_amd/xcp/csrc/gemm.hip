@@ -568,200 +568,6 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
-// 256 x 368 bf16 NT kernel for the 728-channel flow at its 736-channel pitch (N = 736 =
-// 2 x 368: no padded column tile; the 256 x 256 kernel covers 736 with 768).  8 waves, wave w
-// owns output rows 32w .. 32w+31 (2 m-fragments) x all 23 n-fragments of the tile (acc = 184
-// registers).  K-tiles of 64 in a 2-slot LDS ring (A 32 KB + B 46 KB per slot, 156 KB) filled
-// by LDS-DMA through buffer resources one K-tile ahead: 78 KB of fill per 12 MFLOP against
-// 64 KB per 8.4 MFLOP for the 256 x 256 tile (0.85x the fill bytes per flop, the resource the
-// middle-flow GEMMs are bound by, §5.3), and 722 tiles (2.8 rounds of 256 CUs) instead of
-// 1,083 (4.2 rounds).  Epilogue: 16-B stores through lane-pair exchange (n-fragment pairs,
-// fragment 22 with 8-B stores), BatchNorm partial sums reduce-scattered over the 16 row lanes
-// then summed over the 4 waves of each 128-row half in LDS.
-constexpr int N3 = 368, N3F = 23;
-constexpr int N3_AOP = 256 * 128, N3_BOP = N3 * 128, N3_SLOT = N3_AOP + N3_BOP;
-constexpr int N3_PIECES = (N3_AOP + N3_BOP) / 1024;   // 78 LDS-DMA wave-instructions per K-tile
-
-__global__ __launch_bounds__(512) void gemm_nt368_kernel(NTArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * N3_SLOT];
-  const int gridN = (a.N + N3 - 1) / N3, gridM = (a.M + 255) / 256;
-  const int id = xcd_remap(blockIdx.x, gridM * gridN);
-  const int bn = id % gridN, bm = id / gridN;
-  const int m0 = bm * 256, n0 = bn * N3;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // fill: piece p = w + 8i (i < 4: A rows 8p.., else B rows 8(p-32)..), lane = (row lane>>3,
-  // physical chunk lane&7 holding logical chunk (lane&7) ^ ((row>>1)&7))
-  // (row >> 1) & 7 = (4p + (lane >> 4)) & 7 and 4p = 4w (mod 8): one logical chunk for all pieces
-  const int kc = ((lane & 7) ^ ((4 * w + (lane >> 4)) & 7)) * 8;
-  unsigned voff[10];
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const bool isA = i < 4;
-    const int p = w + 8 * i;
-    const int row = (isA ? p : p - 32) * 8 + (lane >> 3);
-    const bool ok = p < N3_PIECES && (isA ? m0 + row < a.M : n0 + row < a.N);
-    voff[i] = ok ? (unsigned)(isA ? ((long)(m0 + row) * a.lda + kc) * 2 : ((long)(n0 + row) * a.ldb + kc) * 2)
-                 : BUF_OOB;
-  }
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
-                                                                       BUF_DWORD3);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
-                                                                       BUF_DWORD3);
-  auto issue = [&](int kt, int slot) {
-    const int kb = kt * 64;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      const int p = w + 8 * i;
-      if (i < 9 || p < N3_PIECES) {
-        char* d = smem + slot * N3_SLOT + p * 1024;
-        const unsigned o = kb + kc < a.K ? voff[i] + kb * 2 : BUF_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 4 ? rA : rB, (__attribute__((address_space(3))) void*)d, 16, o, 0,
-                                                 0, 0);
-      }
-    }
-  };
-
-  f32x4 acc[2][N3F];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < N3F; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (a.K + 63) / 64;
-  issue(0, 0);
-  wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-  const int fr = lane & 15, fg = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int slot = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, slot ^ 1);
-    const char* sa = smem + slot * N3_SLOT;
-    const char* sb = sa + N3_AOP;
-    const int nks = kt * 64 + 32 >= a.K ? 1 : 2;   // the second 32-deep step is past K
-    for (int ks = 0; ks < nks; ++ks) {
-      auto rdb = [&](int j) { return *reinterpret_cast<const bf16x8*>(sb + swz(16 * j + fr, ks * 4 + fg)); };
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(sa + swz(32 * w + fr, ks * 4 + fg));
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(sa + swz(32 * w + 16 + fr, ks * 4 + fg));
-      // B fragments in a 4-register ring, read 3 ahead of their MFMA pair
-      bf16x8 bq[4];
-      bq[0] = rdb(0);
-      bq[1] = rdb(1);
-      bq[2] = rdb(2);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < N3F; ++j) {
-        if (j + 3 < N3F) bq[(j + 3) & 3] = rdb(j + 3);
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j & 3], a0, acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[j & 3], a1, acc[1][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);   // A fragments + the first 3 B reads
-#pragma unroll
-      for (int j = 0; j < N3F; ++j) {
-        if (j + 3 < N3F) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      }
-      __builtin_amdgcn_s_setprio(0);
-    }
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-  }
-
-  // ---- epilogue: lane holds C[m0 + 32w + 16i + fr][n0 + 16j + 4fg + r].  Fragment-pair major,
-  // so accumulators retire as the statistics' first reduce-scatter level (xor 8 over the row
-  // lanes: lanes with fr & 8 keep the sums of squares, the others the sums) takes their columns.
-  bf16* C = reinterpret_cast<bf16*>(a.C);
-  const bool odd = fg & 1;
-  const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2;
-  const int m_0 = m0 + 32 * w + fr, m_1 = m_0 + 16;
-  const bool mok0 = m_0 < a.M, mok1 = m_1 < a.M;
-  bf16* crow0 = C + (long)m_0 * a.ldc;
-  bf16* crow1 = C + (long)m_1 * a.ldc;
-  constexpr int V2 = N3F * 4, V4 = V2 / 2, V8 = V4 / 2;   // 92, 46, 23
-  float u[V2];   // column 4j + r: (b3 ? sum of squares : sum) over the 2 x 2 rows of lanes fr, fr ^ 8
-  auto frag = [&](int j, uint2& p0, uint2& p1) {
-    bf16x4 q0, q1;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      q0[r] = (bf16)acc[0][j][r];
-      q1[r] = (bf16)acc[1][j][r];
-    }
-    p0 = __builtin_bit_cast(uint2, q0);
-    p1 = __builtin_bit_cast(uint2, q1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float f0 = mok0 ? (float)q0[r] : 0.f, f1 = mok1 ? (float)q1[r] : 0.f;
-      const float t1 = f0 + f1, t2 = fmaf(f1, f1, f0 * f0);
-      u[4 * j + r] = (b3 ? t2 : t1) + __shfl_xor(b3 ? t1 : t2, 8, 64);
-    }
-  };
-#pragma unroll
-  for (int jp = 0; jp < N3F / 2; ++jp) {   // fragment pairs (2jp, 2jp+1): 16-B stores
-    uint2 e0, e1, o0, o1;   // [fragment 2jp / 2jp+1][row 0 / 1]
-    frag(2 * jp, e0, e1);
-    frag(2 * jp + 1, o0, o1);
-    const int c0 = n0 + 32 * jp + (odd ? 16 + (fg - 1) * 4 : fg * 4);
-    {
-      const uint2 snd = odd ? e0 : o0;
-      uint2 rc;
-      rc.x = __shfl_xor(snd.x, 16, 64);
-      rc.y = __shfl_xor(snd.y, 16, 64);
-      const uint4 st = odd ? make_uint4(rc.x, rc.y, o0.x, o0.y) : make_uint4(e0.x, e0.y, rc.x, rc.y);
-      if (mok0 && c0 < a.N) *reinterpret_cast<uint4*>(crow0 + c0) = st;
-    }
-    {
-      const uint2 snd = odd ? e1 : o1;
-      uint2 rc;
-      rc.x = __shfl_xor(snd.x, 16, 64);
-      rc.y = __shfl_xor(snd.y, 16, 64);
-      const uint4 st = odd ? make_uint4(rc.x, rc.y, o1.x, o1.y) : make_uint4(e1.x, e1.y, rc.x, rc.y);
-      if (mok1 && c0 < a.N) *reinterpret_cast<uint4*>(crow1 + c0) = st;
-    }
-  }
-  {   // fragment 22: 8-B stores
-    uint2 p0, p1;
-    frag(N3F - 1, p0, p1);
-    const int c0 = n0 + 16 * (N3F - 1) + 4 * fg;
-    if (mok0 && c0 < a.N) *reinterpret_cast<uint2*>(crow0 + c0) = p0;
-    if (mok1 && c0 < a.N) *reinterpret_cast<uint2*>(crow1 + c0) = p1;
-  }
-  if (!a.stats) return;
-  // remaining reduce-scatter levels (xor 4, 2) and a full add over xor 1: lane fr then holds the
-  // 23 sums of statistic b3 for columns cl = (b2 ? 46 : 0) + (b1 ? 23 : 0) + t
-  float x4[V4], x8[V8];
-#pragma unroll
-  for (int q = 0; q < V4; ++q) x4[q] = (b2 ? u[V4 + q] : u[q]) + __shfl_xor(b2 ? u[q] : u[V4 + q], 4, 64);
-#pragma unroll
-  for (int q = 0; q < V8; ++q) {
-    x8[q] = (b1 ? x4[V8 + q] : x4[q]) + __shfl_xor(b1 ? x4[q] : x4[V8 + q], 2, 64);
-    x8[q] += __shfl_xor(x8[q], 1, 64);
-  }
-  // LDS: red[half][wave in half][stat][N3] (23.5 KB; the ring is no longer read)
-  float* red = reinterpret_cast<float*>(smem);
-  const int half = w >> 2, wq = w & 3;
-  if ((fr & 1) == 0) {
-    const int stat = b3 ? 1 : 0, base = (b2 ? V4 : 0) + (b1 ? V8 : 0);
-#pragma unroll
-    for (int t = 0; t < V8; ++t) {
-      const int cl = base + t;   // 4j + r
-      const int col = 16 * (cl >> 2) + 4 * fg + (cl & 3);
-      red[((half * 4 + wq) * 2 + stat) * N3 + col] = x8[t];
-    }
-  }
-  lds_barrier();   // not __syncthreads(): the C stores above must not be waited for
-  const int stat_rows = (a.M + 127) / 128;
-  for (int e = tid; e < 2 * 2 * N3; e += 512) {
-    const int hf = e / (2 * N3), rem = e - hf * (2 * N3), stat = rem / N3, col = rem - stat * N3;
-    const int srow = bm * 2 + hf, n = n0 + col;
-    if (srow < stat_rows && n < a.N) {
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) t += red[((hf * 4 + q) * 2 + stat) * N3 + col];
-      a.stats[((long)srow * 2 + stat) * a.N + n] = t;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------
 // Weight gradient: P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]
 // G: [M][ldg] (output-gradient pixel rows), X: [M][ldx] (layer-input pixel rows).
 // Both operands are pixel-major, so the reduction index m is the slow memory
@@ -1125,14 +931,6 @@ bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   return tile == 2 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
 }
 
-// 256 x 368 tiles: N in (368, 736] (the 736-pitch 728 flow: two whole column tiles), enough
-// tiles for >= 1 round, operands addressable by 32-bit buffer offsets; tile == 3 forces it
-bool nt368(int dtype, int gmode, int M, int N, int K, long lda, long ldb, int tile) {
-  if (dtype != XCP_BF16 || gmode != 0 || (tile != 0 && tile != 3)) return false;
-  if (((long)(M - 1) * lda + K) * 2 > BUF_LIMIT || ((long)(N - 1) * ldb + K) * 2 > BUF_LIMIT) return false;
-  return tile == 3 || (N > N3 && N <= 2 * N3 && K >= 384 && (long)xcp_cdiv(M, 256) * xcp_cdiv(N, N3) >= 256);
-}
-
 bool tn_big(int dtype, int gmode, int N, int K, int tile) {
   // (narrower outputs stream faster through the 128-tile kernel: 0.57 vs 0.95 ms at 5.5M x 128 x 128)
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
@@ -1148,13 +946,8 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
-  if (tile < 0 || tile > 3) return XCP_EINVAL;
+  if (tile < 0 || tile > 2) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
-  if (nt368(dtype, gmode, M, N, K, lda, ldb, tile)) {
-    hipLaunchKernelGGL(gemm_nt368_kernel, dim3(xcp_cdiv(M, 256) * xcp_cdiv(N, N3)), dim3(512), 0, stream, a);
-    return (int)hipGetLastError();
-  }
-  if (tile == 3) tile = 2;   // (operands past the 32-bit offset range: the 256 x 256 kernel)
   if (nt_big(dtype, gmode, M, N, K, tile)) {
     // One 256x256 tile per CU per round.  When the last round would be less than 3/4 full
     // (1,083 tiles = 4.23 rounds in the middle flow), its rows go to the 128x128 kernel
