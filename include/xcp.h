@@ -74,14 +74,17 @@ int xcp_unit_bwd(int dtype, const void* G, const void* Y, const float* alpha, co
  * Wt is the [9][C] fp32 tap-major packing of the [C,1,3,3] weight. */
 int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift, int N,
                int H, int W, int C, xcp_stream_t stream);
-/* fused backward: dX = act'(X) * dgrad(dY) + dRes + scatter_stride(dSkip);
+/* fused backward: dX = act'(X) * dgrad(dY) + dRes + scatter_stride(dSkip) (skip_pre = 0), or
+ * act'(X) * (dgrad(dY) + scatter_stride(dSkip)) + dRes (skip_pre = 1: the strided skip conv read the
+ * same activation act(X), so its gradient passes the mask and enters the BN partial sums);
  * dWpart[P][C][9] workgroup partials of the weight gradient, P = xcp_dw_bwd_chunks();
  * optional bnpart[P][2][C] = (sum dX, sum dX*(X-bmean)*binvstd): the backward
  * partial sums of the BatchNorm that produced X (XCP_ACT_BNRELU only). */
 int xcp_dw_bwd_chunks(int N, int H, int W, int C);
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
-               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, float* bnpart,
-               const float* bmean, const float* binvstd, int N, int H, int W, int C, xcp_stream_t stream);
+               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre, void* dX, float* dWpart,
+               float* bnpart, const float* bmean, const float* binvstd, int N, int H, int W, int C,
+               xcp_stream_t stream);
 
 /* ---- BatchNorm2d (Xception.py:56,67,73,78,119,123,143,147), tails, pooling ---- */
 /* out[g][l] = sum over the g-th of G contiguous groups of slabs s of in[s*ld + l], l < L <= ld
@@ -113,6 +116,11 @@ int xcp_bn_finalize(const double* part2, int G, int C, int CP, double count, con
                     float* scale, float* shift, xcp_stream_t stream);
 int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, long rows, int C,
                xcp_stream_t stream);
+/* Y[n][oh][ow][c] = act(X[n][oh*S][ow*S][c] * scale[c] + shift[c]) (relu: max(., 0)): the activated
+ * input of a stride-S 1x1 conv (Block.skip, Xception.py:55) when the full-resolution activation is
+ * never materialised (its other consumer applies the BN + ReLU on load). */
+int xcp_bn_act_strided(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, int N, int H,
+                       int W, int OH, int OW, int S, int C, xcp_stream_t stream);
 int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const float* alpha, const float* bcoef,
                      const float* delta, const float* ms, const float* mt, long rows, int C, xcp_stream_t stream);
 int xcp_relu_bwd(int dtype, void* dX, const void* X, long rows, int C, xcp_stream_t stream);

@@ -27,7 +27,7 @@ SIGNATURES = {
     "xcp_unit_bwd": [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
-    "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, P, P, P, P, P, I, I, I, I, P],
+    "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_colreduce_f32": [P, I, L, L, P, I, I, P],
     "xcp_colreduce_groups": [I, L],
     "xcp_chanred_parts": [L, I],
@@ -37,6 +37,7 @@ SIGNATURES = {
     "xcp_bn_bwd_finalize_part": [P, I, I, I, D, P, P, P, P, P, P, P, P, I, P],
     "xcp_bn_finalize": [P, I, I, I, D, P, P, P, P, F, F, I, P, P, P, P, P],
     "xcp_bn_act": [I, P, P, P, P, I, L, I, P],
+    "xcp_bn_act_strided": [I, P, P, P, P, I, I, I, I, I, I, I, I, P],
     "xcp_bn_bwd_apply": [I, P, P, P, P, P, P, P, P, L, I, P],
     "xcp_relu_bwd": [I, P, P, L, I, P],
     "xcp_tail_fwd": [I, P, P, P, I, P, P, P, P, P, I, I, I, I, P],

@@ -331,6 +331,33 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ X, T*
   VecIO<T, CPT>::store(Y + p * C + c0, v);
 }
 
+// y[n][oh][ow] = act(x[n][oh*S][ow*S] * scale + shift): the activated input of a stride-S 1x1
+// conv (Block.skip, Xception.py:55) when the consumers of the full-resolution activation
+// apply the BN + ReLU on load themselves
+template <typename T, int CPT>
+__global__ __launch_bounds__(256) void bn_act_strided_kernel(const T* __restrict__ X, T* __restrict__ Y, const float* scale,
+                                                             const float* shift, int relu, int H, int W, int OH, int OW,
+                                                             int S, long rows, int C) {
+  const int CV = C / CPT;
+  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= rows * CV) return;
+  const int c0 = (int)(g % CV) * CPT;
+  const long p = g / CV;
+  const long n = p / ((long)OH * OW);
+  const int rem = (int)(p - n * OH * OW), oh = rem / OW, ow = rem - oh * OW;
+  const long q = (n * H + (long)oh * S) * W + (long)ow * S;
+  float v[CPT], s[CPT], t[CPT];
+  VecIO<T, CPT>::load(X + q * C + c0, v);
+  VecIO<float, CPT>::load(scale + c0, s);
+  VecIO<float, CPT>::load(shift + c0, t);
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    v[j] = fmaf(v[j], s[j], t[j]);
+    if (relu) v[j] = fmaxf(v[j], 0.f);
+  }
+  VecIO<T, CPT>::store(Y + p * C + c0, v);
+}
+
 // dy = alpha*dz + bcoef*y + delta   (dbeta = sum dz, dgamma = sum dz*yhat come from the finalize)
 template <typename T, int CPT, bool MASK>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dZ, const T* __restrict__ Yv, T* dY,
@@ -797,6 +824,23 @@ int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const floa
   else if (dtype == XCP_F32)
     hipLaunchKernelGGL((bn_act_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)X, (float*)Y, scale, shift,
                        relu, rows, C);
+  else
+    return XCP_EUNSUPPORTED;
+  return (int)hipGetLastError();
+}
+
+int xcp_bn_act_strided(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, int N, int H,
+                       int W, int OH, int OW, int S, int C, hipStream_t st) {
+  if (C % 8 || S < 1 || (OH - 1) * S >= H || (OW - 1) * S >= W) return XCP_EINVAL;
+  const long rows = (long)N * OH * OW;
+  if (rows <= 0) return XCP_OK;
+  const unsigned g = nblk(rows * (C / 8));
+  if (dtype == XCP_BF16)
+    hipLaunchKernelGGL((bn_act_strided_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)X, (bf16*)Y, scale,
+                       shift, relu, H, W, OH, OW, S, rows, C);
+  else if (dtype == XCP_F32)
+    hipLaunchKernelGGL((bn_act_strided_kernel<float, 8>), dim3(g), dim3(256), 0, st, (const float*)X, (float*)Y, scale,
+                       shift, relu, H, W, OH, OW, S, rows, C);
   else
     return XCP_EUNSUPPORTED;
   return (int)hipGetLastError();

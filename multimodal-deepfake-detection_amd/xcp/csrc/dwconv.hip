@@ -234,6 +234,8 @@ struct DwBwdArgs {
   const void* dRes;
   const void* dSkip;
   int sOH, sOW, sS;
+  int skip_pre;           // 1: the skip term is a gradient of the same activation (added before the
+                          // activation mask and the BN partial sums), 0: added after them
   void* dX;
   float* dWpart;          // [P][C][9]
   float* bnpart;          // [P][2][C] or null
@@ -540,6 +542,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
 #pragma unroll
     for (int j = 0; j < RS; ++j) {
       V s = sj[j];
+      if (skip_row && a.skip_pre) s += R::unpack(pskp[j]);
       if constexpr (ACT != ACT_NONE) {
         const V ctr = xa[j + 1];
         if constexpr (EPT == 2) {
@@ -556,7 +559,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
         bs2 = vfma(dz, (R::unpack(xr[j]) - mu) * is, bs2);
       }
       if constexpr (RES) s += R::unpack(pres[j]);
-      if (skip_row) s += R::unpack(pskp[j]);
+      if (skip_row && !a.skip_pre) s += R::unpack(pskp[j]);
       *reinterpret_cast<unsigned*>(stg + (sg * RS + j) * SLICE + cl * 4) = R::pack(s);
     }
     store_row<T>(dX, h, a.W, a.C, rl_st, stg, lane);
@@ -656,14 +659,14 @@ int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
 }
 
 int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
-               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, void* dX, float* dWpart, float* bnpart,
-               const float* bmean, const float* binvstd, int N, int H, int W, int C, hipStream_t stream) {
+               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre, void* dX, float* dWpart,
+               float* bnpart, const float* bmean, const float* binvstd, int N, int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
   if (bnpart && (act != ACT_BNRELU || !bmean || !binvstd)) return XCP_EINVAL;
   DwBwdArgs a{};
   a.dY = dY; a.X = X; a.Wt = Wt; a.scale = scale; a.shift = shift; a.dRes = dRes; a.dSkip = dSkip;
-  a.sOH = sOH; a.sOW = sOW; a.sS = sS > 0 ? sS : 1; a.dX = dX; a.dWpart = dWpart;
+  a.sOH = sOH; a.sOW = sOW; a.sS = sS > 0 ? sS : 1; a.skip_pre = skip_pre != 0; a.dX = dX; a.dWpart = dWpart;
   a.bnpart = bnpart; a.bmean = bmean; a.binvstd = binvstd;
   a.N = N; a.H = H; a.W = W; a.C = C;
   a.ngroups = ngroups_for(C, dtype);

@@ -109,6 +109,9 @@ WGRAD_SIDE_STREAM = os.environ.get("XCP_WGRAD_STREAM", "1") != "0"
 # fused BN-apply + pointwise dgrad + wgrad for the narrow units (csrc/unitbwd.hip);
 # XCP_FUSED_UNIT_BWD=0 runs the three-kernel sequence (A/B and parity cross-checks)
 FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
+# XCP_STEM_FUSED=0 materialises relu(bn2(conv2)) at full resolution for block1 (A/B and parity
+# cross-checks); by default block1's first depthwise conv applies BN2 + ReLU on load
+STEM_FUSED = os.environ.get("XCP_STEM_FUSED", "1") != "0"
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
 # columns in the packed weights, zero BN scale / shift / backward coefficients.  XCP_PAD_728=0
@@ -308,13 +311,25 @@ class XceptionEngine:
         else:        # implicit GEMM (im2col gather)
             c2, s2 = self._pw(a1, pk["conv2"], rows2, 64, 288, train, m.bn2, lda=32,
                               gather=(2, OH1, OW1, OH2, OW2, 1, 32))
-        sout = self._empty(rows2 * 64)
-        ops.bn_act(c2, sout, s2.scale, s2.shift, True, rows2, 64)
-        S.update(c1=c1, s1=s1, a1=a1, c2=c2, s2=s2, sout=sout, OH1=OH1, OW1=OW1, OH2=OH2, OW2=OW2)
+        S.update(c1=c1, s1=s1, a1=a1, c2=c2, s2=s2, OH1=OH1, OW1=OW1, OH2=OH2, OW2=OW2)
         # ---- blocks (Xception.py:176-187)
-        xc, H, W = sout, OH2, OW2
         S["blocks"] = []
-        for b in self.blocks:
+        b0 = self.blocks[0]
+        if STEM_FUSED and not b0.units[0].relu and b0.skip is not None and b0.stride != 1:
+            # block1 (start_with_relu=False, stride-2 skip conv): x = relu(bn2(conv2)) is never
+            # materialised at 147^2 -- the first depthwise conv applies BN2 + ReLU on load and the
+            # skip conv reads only the stride-2 pixels, activated by one small pass
+            OHs, OWs = (OH2 - 1) // b0.stride + 1, (OW2 - 1) // b0.stride + 1
+            skip_x = self._empty(N * OHs * OWs * 64)
+            ops.bn_act_strided(c2, skip_x, s2.scale, s2.shift, True, N, OH2, OW2, OHs, OWs, b0.stride, 64)
+            xc, H, W, bs = self._block_fwd(b0, c2, N, OH2, OW2, pk, train, pre_bn=s2, skip_x=skip_x)
+            S["blocks"].append(bs)
+            rest = self.blocks[1:]
+        else:
+            xc = self._empty(rows2 * 64)
+            ops.bn_act(c2, xc, s2.scale, s2.shift, True, rows2, 64)
+            H, W, rest = OH2, OW2, self.blocks
+        for b in rest:
             xc, H, W, bs = self._block_fwd(b, xc, N, H, W, pk, train)
             S["blocks"].append(bs)
         # ---- exit flow (Xception.py:189-198)
@@ -337,10 +352,14 @@ class XceptionEngine:
                 torch._foreach_add_(nbt, 1)
         return feats, S
 
-    def _block_fwd(self, b, x_in, N, H, W, pk, train):
+    def _block_fwd(self, b, x_in, N, H, W, pk, train, pre_bn=None, skip_x=None):
+        """pre_bn: Stats of a BN + ReLU the block's input still needs (applied on load by the first
+        depthwise conv); skip_x: the skip conv's input, already strided and activated"""
         M = N * H * W
         units = []
         src, act, sc, sh = x_in, (ACT_RELU if b.units[0].relu else ACT_NONE), None, None
+        if pre_bn is not None:
+            act, sc, sh = ACT_BNRELU, pre_bn.scale, pre_bn.shift
         for u in b.units:
             d = self._empty(M * pc(u.cin))
             ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, pc(u.cin))
@@ -353,7 +372,9 @@ class XceptionEngine:
             OH, OW = H, W
         Ms = N * OH * OW
         ys = sks = None
-        if b.skip is not None:
+        if b.skip is not None and skip_x is not None:
+            ys, sks = self._pw(skip_x, pk[b.name + ".skip"], Ms, b.cout, b.cin, train, b.skipbn, lda=pc(b.cin))
+        elif b.skip is not None:
             ys, sks = self._pw(x_in, pk[b.name + ".skip"], Ms, b.cout, b.cin, train, b.skipbn, lda=pc(b.cin),
                                gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
         out = self._empty(Ms * pc(b.cout))
@@ -362,7 +383,8 @@ class XceptionEngine:
         ops.tail_fwd(units[-1]["y"], st.scale, st.shift, b.pool, ys if ys is not None else x_in,
                      sks.scale if sks is not None else None, sks.shift if sks is not None else None, out, amax, N, H, W,
                      pc(b.cout))
-        bs = {"x_in": x_in, "units": units, "ys": ys, "sks": sks, "amax": amax, "H": H, "W": W, "OH": OH, "OW": OW}
+        bs = {"x_in": x_in, "units": units, "ys": ys, "sks": sks, "amax": amax, "H": H, "W": W, "OH": OH, "OW": OW,
+              "pre_bn": pre_bn, "skip_x": skip_x}
         return out, OH, OW, bs
 
     # ------------------------------------------------------------ backward
@@ -442,7 +464,8 @@ class XceptionEngine:
             ops.bn_apply_coef(dZ, Y, dY, coef, st, rows, pc(C), relu)
             return dY
 
-        def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None):
+        def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None,
+                     skip_pre=False):
             """dZ: gradient w.r.t. this unit's BN output (``part``: its fused BN-backward
             partial sums, if the producer emitted them).  Returns (gradient w.r.t. the
             depthwise input after the activation mask (+ residual / skip terms), and -- when
@@ -463,7 +486,7 @@ class XceptionEngine:
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
                              pc(u.cin), dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, bn_stats=prev_st, accumulate=acc,
-                             Cw=u.cin)
+                             Cw=u.cin, skip_pre=skip_pre)
             return dX, (bnp if prev_st is not None else None)
 
         # ---- exit flow
@@ -477,13 +500,17 @@ class XceptionEngine:
         dX, _ = unit_bwd(u3, e3, dZ3, H, W, part=p3)
         done()
         # ---- blocks, last to first
+        pre_part = None
         for b, bs in zip(reversed(self.blocks), reversed(S["blocks"])):
-            dX = self._block_bwd(b, bs, dX, N, pk, bn_bwd, unit_bwd, wgrad)
+            dX, pre_part = self._block_bwd(b, bs, dX, N, pk, bn_bwd, unit_bwd, wgrad)
             done()
         # ---- stem
         OH1, OW1, OH2, OW2 = S["OH1"], S["OW1"], S["OH2"], S["OW2"]
         rows1, rows2 = N * OH1 * OW1, N * OH2 * OW2
-        dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"], relu=True)   # relu (Xception.py:174) fused
+        if pre_part is not None:   # block1 applied BN2 + ReLU on load: dX is masked, its BN2 sums came along
+            dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"], part=pre_part)
+        else:
+            dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"], relu=True)   # relu (Xception.py:174) fused
         dA1 = self._empty(rows1 * 32)
         if self.dtype == torch.bfloat16 and ops.conv3x3_parts(1, N, OH2, OW2) > 0:
             ops.conv3x3(1, dC2, pk["conv2T"], dA1, None, N, OH2, OW2)
@@ -526,8 +553,11 @@ class XceptionEngine:
         skip_geom = (0, 0, 1)
         if b.skip is not None:
             dYs = bn_bwd(b.skipbn, b.name + ".skipbn", dOut, bs["ys"], Ms, b.cout, bs["sks"])
-            wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1),
-                  gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
+            if bs["skip_x"] is not None:
+                wgrad(dYs, bs["skip_x"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1))
+            else:
+                wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1),
+                      gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
             dXs = self._empty(Ms * pc(b.cin))
             ops.gemm_nt(dYs, pk[b.name + ".skipT"], dXs, Ms, pc(b.cin), pc(b.cout))
             if b.stride != 1:
@@ -541,8 +571,10 @@ class XceptionEngine:
             if i > 0:
                 dZ, part = unit_bwd(u, rec, dZ, H, W, part=part, prev_st=units[i - 1]["st"])
             else:
-                dZ, _ = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, part=part)
-        return dZ
+                pre = bs["pre_bn"]
+                dZ, pre_part = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, part=part,
+                                        prev_st=pre, skip_pre=pre is not None)
+        return dZ, pre_part
 
 
 class XceptionFunction(torch.autograd.Function):

@@ -138,18 +138,19 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
 
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
-           bn_stats=None, accumulate=False, Cw=None):
+           bn_stats=None, accumulate=False, Cw=None, skip_pre=False):
     """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
     (that BN's Stats) is given, else (None, 0).  dW_out receives the weight gradient in the
     nn.Conv2d [C][1][3][3] order (accumulate: added to it); Cw (default C): channels of the
-    weight when C is a padded channel pitch."""
+    weight when C is a padded channel pitch.  skip_pre: dSkip is a gradient of the same
+    activation act(X) (it passes the activation mask and enters the BN partial sums)."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
     bnpart = None
     if bn_stats is not None:
         bnpart = torch.empty(P * 2 * C, device=dY.device, dtype=torch.float32)
     _lib.call("xcp_dw_bwd", DT[dY.dtype], act, _p(dY), _p(X), _p(Wt), _p(scale), _p(shift), _p(dRes), _p(dSkip),
-              skip_geom[0], skip_geom[1], skip_geom[2], _p(dX), _p(part), _p(bnpart),
+              skip_geom[0], skip_geom[1], skip_geom[2], int(skip_pre), _p(dX), _p(part), _p(bnpart),
               _p(bn_stats["mean"]) if bn_stats is not None else 0,
               _p(bn_stats["invstd"]) if bn_stats is not None else 0, N, H, W, C, stream())
     reduce_slabs(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
@@ -267,6 +268,12 @@ def unit_bwd(G, Y, coef, Wt, X, dD, M, CO, CI, dW_out, accumulate=False):
 
 def bn_act(X, Y, scale, shift, relu, rows, C):
     _lib.call("xcp_bn_act", DT[X.dtype], _p(X), _p(Y), _p(scale), _p(shift), 1 if relu else 0, rows, C, stream())
+
+
+def bn_act_strided(X, Y, scale, shift, relu, N, H, W, OH, OW, S, C):
+    """Y[n,oh,ow] = act(X[n, oh*S, ow*S] * scale + shift) (NHWC pixel rows of C channels)."""
+    _lib.call("xcp_bn_act_strided", DT[X.dtype], _p(X), _p(Y), _p(scale), _p(shift), int(relu), N, H, W, OH, OW, S, C,
+              stream())
 
 
 def relu_bwd(dX, X, rows, C):

@@ -299,6 +299,47 @@ def test_dw_bwd_residual_and_skip(ops, gpu, dt, N):
     assert rel_err(nchw(out.view(N, H, W, C)).float(), want) < (1e-6 if dt == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("N,H", [(3, 15), (256, 147)])
+def test_dw_bwd_skip_pre_bnrelu(ops, gpu, dt, N, H):
+    """Block1 with the stem's BN2 + ReLU applied on load (engine): the rep's depthwise conv and
+    the stride-2 skip conv both read a = relu(bn(x)), so the skip gradient passes the same ReLU
+    mask and enters the BN partial sums (skip_pre); the skip's input is the strided activation
+    (xcp_bn_act_strided).  Against torch autograd through relu(x*sc+sh) in fp32."""
+    C, W = 64, H
+    g = torch.Generator(device=gpu).manual_seed(N + H)
+    x = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
+    w = torch.randn(C, 1, 3, 3, device=gpu, generator=g) / 3
+    Wt = w.reshape(C, 9).t().contiguous()
+    sc = torch.rand(C, device=gpu, generator=g) + 0.5
+    sh = torch.randn(C, device=gpu, generator=g) * 0.2
+    OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    # strided activation
+    xs = torch.empty(N * OH * OW, C, device=gpu, dtype=dt)
+    ops.bn_act_strided(nhwc(x), xs, sc, sh, True, N, H, W, OH, OW, 2, C)
+    # z rounded once, as the kernels' fma (x*sc + sh in fp32 rounds twice and flips ReLU masks)
+    z = (x.double() * sc.double().view(1, C, 1, 1) + sh.double().view(1, C, 1, 1)).float()
+    want_s = F.relu(z)[:, :, ::2, ::2].to(dt).float()
+    assert rel_err(nchw(xs.view(N, OH, OW, C)).float(), want_s) < 1e-6
+    # backward with the skip gradient before the mask
+    zr = z.clone().requires_grad_(True)
+    a = F.relu(zr)
+    dy = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
+    dsk = torch.randn(N, C, OH, OW, device=gpu, generator=g).to(dt)
+    ((F.conv2d(a, w, None, 1, 1, 1, C) * dy.float()).sum() + (a[:, :, ::2, ::2] * dsk.float()).sum()).backward()
+    st = {"mean": torch.randn(C, device=gpu, generator=g) * 0.1, "invstd": torch.rand(C, device=gpu, generator=g) + 0.5}
+    dX = torch.empty(N * H * W, C, device=gpu, dtype=dt)
+    dW = torch.empty(C * 9, device=gpu)
+    bnpart, P = ops.dw_bwd(2, nhwc(dy), nhwc(x), Wt, sc, sh, dX, dW, N, H, W, C, dSkip=nhwc(dsk), skip_geom=(OH, OW, 2),
+                           bn_stats=st, skip_pre=True)
+    dXn = nchw(dX.view(N, H, W, C)).float()
+    assert rel_err(dXn, zr.grad) < (1e-6 if dt == torch.float32 else 1e-2)
+    sums = bnpart.view(P, 2, C).double().sum(0)
+    zhat = (x.float() - st["mean"].view(1, C, 1, 1)) * st["invstd"].view(1, C, 1, 1)
+    torch.testing.assert_close(sums[0], dXn.double().sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(sums[1], (dXn * zhat).double().sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+
+
 @pytest.mark.parametrize("relu", [False, True])
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("rows,C", [(100000, 128), (3 * 361, 728), (50, 2048)])
