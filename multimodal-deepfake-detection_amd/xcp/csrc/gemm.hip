@@ -914,7 +914,11 @@ namespace {
 // training batch sizes; TN: N, K >= 256); everything else runs the 128x128 kernels.  The
 // `tile` argument of the entry points (0 auto, 1 = 128x128, 2 = 256x256) overrides the choice
 // so tests can pin each kernel at small sizes.
-constexpr int TN_TARGET_WGS = 256;   // 256x256 weight-gradient workgroups (splits x tiles): one per CU
+// 256x256 weight-gradient workgroups (splits x tiles): about half the CUs.  The engine runs the
+// weight gradients on a side stream beside the main stream's dgrad GEMMs and depthwise backward;
+// one 160 KB-LDS workgroup on every CU left those no room, half the CUs (and half the split-K
+// slabs) measured 1.0-1.8 % faster per step for targets 64-192 (profiles/r02_tn_target_sweep.txt).
+constexpr int TN_TARGET_WGS = 128;
 
 int gpu_cus() {   // compute units of the current device (256 on MI355X)
   static const int cus = [] {
