@@ -26,6 +26,7 @@ Gradient delivery has two modes:
   sink is told after each block which parameters are final, so it all-reduces a bucket
   while the earlier blocks' backward is still running.
 """
+import contextlib
 import os
 import math
 
@@ -112,6 +113,7 @@ FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
 # XCP_STEM_FUSED=0 materialises relu(bn2(conv2)) at full resolution for block1 (A/B and parity
 # cross-checks); by default block1's first depthwise conv applies BN2 + ReLU on load
 STEM_FUSED = os.environ.get("XCP_STEM_FUSED", "1") != "0"
+STEM_WGRAD_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_STEM_WGRAD_SIDE", "1") != "0"
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
 # columns in the packed weights, zero BN scale / shift / backward coefficients.  XCP_PAD_728=0
@@ -516,18 +518,27 @@ class XceptionEngine:
             ops.conv3x3(1, dC2, pk["conv2T"], dA1, None, N, OH2, OW2)
         else:
             ops.gemm_nt(dC2, pk["conv2T"], dA1, rows1, 32, 576, lda=64, gather=(3, OH1, OW1, OH2, OW2, 1, 64))
-        w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
-        if self.dtype == torch.bfloat16 and ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0:
-            ops.conv3x3_wgrad(dC2, S["a1"], w2g, N, OH1, OW1)
-        else:
-            ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
-        c2g, acc = g("conv2.weight", (64, 32, 3, 3))
-        if acc:
-            tmp = torch.empty_like(c2g)
-            ops.permute3(w2g, tmp, 64, 9, 32, (0, 2, 1))
-            c2g.add_(tmp)
-        else:
-            ops.permute3(w2g, c2g, 64, 9, 32, (0, 2, 1))
+        # conv2's weight gradient on the weight-gradient stream, beside the dgrad chain below
+        st2 = side if STEM_WGRAD_SIDE else None
+        if st2 is not None:
+            st2.wait_stream(main)
+        with torch.cuda.stream(st2) if st2 is not None else contextlib.nullcontext():
+            w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
+            if self.dtype == torch.bfloat16 and ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0:
+                ops.conv3x3_wgrad(dC2, S["a1"], w2g, N, OH1, OW1)
+            else:
+                ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
+            c2g, acc = g("conv2.weight", (64, 32, 3, 3))
+            if acc:
+                tmp = torch.empty_like(c2g)
+                ops.permute3(w2g, tmp, 64, 9, 32, (0, 2, 1))
+                c2g.add_(tmp)
+            else:
+                ops.permute3(w2g, c2g, 64, 9, 32, (0, 2, 1))
+        if st2 is not None:
+            for t in (dC2, S["a1"]):
+                t.record_stream(st2)
+            c2g.record_stream(main)
         dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], relu=True)   # relu (Xception.py:170) fused
         c1g, acc = g("conv1.weight", (32, 3, 3, 3))
         ops.conv1_wgrad(S["x"], dC1, c1g, N, S["IH"], S["IW"], accumulate=acc)
