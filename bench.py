@@ -127,7 +127,8 @@ def step_roofline(size, frames, unfrozen, s=2):
     op(2 * 27 * 32 * p1, 4 * 3 * n * size * size + s * 32 * p1)                  # conv1
     op(0, s * 32 * p1 * 3)                                                      # bn1 stats + apply
     op(2 * 288 * 64 * p2, s * (32 * p1 + 64 * p2))                              # conv2 (+stats)
-    op(0, s * 64 * p2 * 2)                                                      # bn2 apply
+    ps1 = n * ((oh2 - 1) // 2 + 1) ** 2
+    op(0, s * 64 * ps1 * 2)           # bn2 + ReLU at block1's skip stride only (the depthwise applies it on load)
     bwd = []
     h = oh2
 
@@ -166,7 +167,7 @@ def step_roofline(size, frames, unfrozen, s=2):
     op(0, s * n * h * h * 2048)                                                 # bn4 + ReLU + avgpool
     if unfrozen:
         bwd.append((0, 2 * s * n * h * h * 2048))                               # avgpool backward
-        bwd.append((0, 5 * s * 64 * p2))                                        # bn2 backward
+        bwd.append((0, 3 * s * 64 * p2))                   # bn2 backward apply (reduce fused: block1 depthwise)
         bwd.append((2 * 576 * 32 * p1, s * (64 * p2 + 32 * p1)))               # conv2 dgrad
         bwd.append((2 * 288 * 64 * p2, s * (64 * p2 + 32 * p1)))                # conv2 wgrad
         bwd.append((0, 5 * s * 32 * p1))                                        # bn1 backward
