@@ -251,6 +251,15 @@ def main():
             rep(f"dw_bwd {Hs}^2 x {Cs} N={Ns} act=2", timeit(lambda: ops.dw_bwd(2, Ds, Xs, Wts, scs, shs, Ys, dWs, Ns, Hs,
                                                                                  Hs, Cs, bn_stats=sts)), 6 * Ms * Cs)
             del Xs, Ds, Ys
+    if "conv1" in sel:   # stem conv1 3->32 3x3 s2 at 256 frames of 299^2 (fp32 NCHW in, bf16 NHWC out)
+        Xc = torch.rand(N, 3, 299, 299, device=dev, generator=g)
+        Wc = torch.randn(32, 3, 3, 3, device=dev, generator=g) / 5
+        Yc = torch.empty(N * 149 * 149, 32, device=dev, dtype=dt)
+        byts = Xc.numel() * 4 + Yc.numel() * 2
+        rep("conv1 fwd 299^2 -> 149^2 x 32", timeit(lambda: ops.conv1_fwd(Xc, Wc, Yc, N, 299, 299), iters=10), byts)
+        dWc = torch.empty(32 * 27, device=dev)
+        rep("conv1 wgrad", timeit(lambda: ops.conv1_wgrad(Xc, Yc, dWc, N, 299, 299), iters=10), byts)
+        del Xc, Yc
     if "unitbwd" in sel:   # block1 / block2 unit backward (256 frames): fused vs three kernels
         for (Hu, CO, CI) in ((147, 128, 128), (147, 128, 64), (74, 256, 256), (74, 256, 128)):
             Mu = N * Hu * Hu
