@@ -114,6 +114,9 @@ FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
 # cross-checks); by default block1's first depthwise conv applies BN2 + ReLU on load
 STEM_FUSED = os.environ.get("XCP_STEM_FUSED", "1") != "0"
 STEM_WGRAD_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_STEM_WGRAD_SIDE", "1") != "0"
+# depthwise weight-gradient slab reductions on the weight-gradient stream (XCP_DW_REDUCE_SIDE=0:
+# on the main stream right after each depthwise backward)
+DW_REDUCE_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_DW_REDUCE_SIDE", "1") != "0"
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
 # columns in the packed weights, zero BN scale / shift / backward coefficients.  XCP_PAD_728=0
@@ -488,7 +491,7 @@ class XceptionEngine:
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
                              pc(u.cin), dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, bn_stats=prev_st, accumulate=acc,
-                             Cw=u.cin, skip_pre=skip_pre)
+                             Cw=u.cin, skip_pre=skip_pre, reduce_stream=side if DW_REDUCE_SIDE else None)
             return dX, (bnp if prev_st is not None else None)
 
         # ---- exit flow

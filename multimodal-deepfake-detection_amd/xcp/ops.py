@@ -138,12 +138,13 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
 
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
-           bn_stats=None, accumulate=False, Cw=None, skip_pre=False):
+           bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None):
     """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
     (that BN's Stats) is given, else (None, 0).  dW_out receives the weight gradient in the
     nn.Conv2d [C][1][3][3] order (accumulate: added to it); Cw (default C): channels of the
     weight when C is a padded channel pitch.  skip_pre: dSkip is a gradient of the same
-    activation act(X) (it passes the activation mask and enters the BN partial sums)."""
+    activation act(X) (it passes the activation mask and enters the BN partial sums).
+    reduce_stream: run the weight-gradient slab reduction there (ordered after this launch)."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
     bnpart = None
@@ -153,7 +154,14 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
               skip_geom[0], skip_geom[1], skip_geom[2], int(skip_pre), _p(dX), _p(part), _p(bnpart),
               _p(bn_stats["mean"]) if bn_stats is not None else 0,
               _p(bn_stats["invstd"]) if bn_stats is not None else 0, N, H, W, C, stream())
-    reduce_slabs(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
+    if reduce_stream is None:
+        reduce_slabs(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
+    else:
+        reduce_stream.wait_stream(torch.cuda.current_stream(dY.device))
+        with torch.cuda.stream(reduce_stream):
+            reduce_slabs(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
+        part.record_stream(reduce_stream)
+        dW_out.record_stream(reduce_stream)
     return bnpart, (P if bnpart is not None else 0)
 
 
