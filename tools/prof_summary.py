@@ -96,6 +96,32 @@ def main():
         lab = labels.get(k, k[0])
         print(f"{lab[:44]:44s} {str(k[1]):>10s} {str(k[2]):>4s} {c:6d} {t / 1e6:10.3f} {t / c / 1e3:9.1f} "
               f"{100 * t / total:6.2f}")
+    if path.endswith(".csv"):
+        contention(path)
+
+
+# the roofline kernels of bench.py, (kernel base name, grid) at the bench's middle-flow shape
+ROOF = (("gemm_nt256k64_kernel", 523776), ("dw_fwd_kernel", 1507328))
+
+
+def contention(path):
+    """Launches of the roofline kernels split by whether another stream ran a kernel during them
+    (the side-stream weight gradients of the backward): bench.py times the op's forward launches,
+    which never overlap one, so its live average is the 'alone' column here (plus, for the
+    pointwise GEMM, the op's second launch: the sparse last round on the 128x128 kernel)."""
+    with open(path) as f:
+        rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Stream_Id"),
+                 int(r.get("Grid_Size_X") or 0)) for r in csv.DictReader(f)]
+    print("
+roofline kernels: launches alone on the GPU vs overlapping another stream's kernels")
+    for name, grid in ROOF:
+        sel = [r for r in rows if base(r[0]) == name and r[4] == grid]
+        alone, shared = [], []
+        for r in sel:
+            ov = any(o[3] != r[3] and o[1] < r[2] and o[2] > r[1] for o in rows if o is not r)
+            (shared if ov else alone).append((r[2] - r[1]) / 1e3)
+        f = lambda v: f"{len(v):5d} x {sum(v) / len(v):7.1f} us" if v else "    0"
+        print(f"{name:28s} grid {grid:>8d}  all {f(alone + shared)}  alone {f(alone)}  overlapped {f(shared)}")
 
 
 if __name__ == "__main__":
