@@ -112,8 +112,7 @@ def contention(path):
     with open(path) as f:
         rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Stream_Id"),
                  int(r.get("Grid_Size_X") or 0)) for r in csv.DictReader(f)]
-    print("
-roofline kernels: launches alone on the GPU vs overlapping another stream's kernels")
+    print("\nroofline kernels: launches alone on the GPU vs overlapping another stream's kernels")
     for name, grid in ROOF:
         sel = [r for r in rows if base(r[0]) == name and r[4] == grid]
         alone, shared = [], []
