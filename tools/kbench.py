@@ -170,6 +170,32 @@ def main():
               "track": False}
         rep("bn_backward (reduce+apply)", timeit(lambda: ops.bn_backward(D, X, M, C, bn, st, Y, dgm, dbt)),
             4 * tensor_bytes)
+    if "chanred" in sel:   # per-channel reductions: BN forward stats (1 tensor), BN backward sums (2 tensors)
+        R = ops._lib.call("xcp_chanred_parts", M, C)
+        part = torch.empty(R * 2 * C, device=dev)
+        rep("row_stats 19^2 x 728 (1 tensor)", timeit(lambda: ops._lib.call("xcp_row_stats", 1, ops._p(X), M, C,
+                                                                            ops._p(part), ops.stream())), tensor_bytes)
+        rep("bn_bwd_reduce 19^2 x 728 (2 tensors)",
+            timeit(lambda: ops._lib.call("xcp_bn_bwd_reduce", 1, ops._p(D), ops._p(X), ops._p(st["mean"]),
+                                         ops._p(st["invstd"]), 0, 0, M, C, ops._p(part), ops.stream())),
+            2 * tensor_bytes)
+    if "dwgeom" in sel:   # depthwise backward, ~92k pixels x 736 channels: walk length vs frame width
+        for (Ng, Hg, Wg) in ((256, 19, 19), (33, 147, 19), (33, 19, 147), (4, 147, 147)):
+            Mg = Ng * Hg * Wg
+            Xg = torch.randn(Mg, 736, device=dev, generator=g).to(dt)
+            Dg = torch.randn(Mg, 736, device=dev, generator=g).to(dt)
+            Yg = torch.empty_like(Xg)
+            Wtg = torch.randn(9, 736, device=dev, generator=g)
+            scg = torch.rand(736, device=dev, generator=g) + 0.5
+            shg = torch.randn(736, device=dev, generator=g)
+            dWg = torch.empty(736 * 9, device=dev)
+            stg = {"mean": torch.zeros(736, device=dev), "invstd": torch.ones(736, device=dev)}
+            rep(f"dw_bwd N={Ng} {Hg}x{Wg} x 736 act=2", timeit(lambda: ops.dw_bwd(2, Dg, Xg, Wtg, scg, shg, Yg, dWg, Ng, Hg,
+                                                                                   Wg, 736, bn_stats=stg)),
+                6 * Mg * 736)
+            rep(f"dw_fwd N={Ng} {Hg}x{Wg} x 736 act=2", timeit(lambda: ops.dw_fwd(2, Xg, Yg, Wtg, scg, shg, Ng, Hg, Wg,
+                                                                                   736)), 4 * Mg * 736)
+            del Xg, Dg, Yg
     if "tailpool" in sel:   # block1's pooled tail at 147^2 x 128 (the largest)
         Hp, Cp = 147, 128
         OHp = (Hp - 1) // 2 + 1
