@@ -360,6 +360,8 @@ class XceptionEngine:
     def _block_fwd(self, b, x_in, N, H, W, pk, train, pre_bn=None, skip_x=None):
         """pre_bn: Stats of a BN + ReLU the block's input still needs (applied on load by the first
         depthwise conv); skip_x: the skip conv's input, already strided and activated"""
+        if pre_bn is not None and (b.skip is None or b.stride == 1 or b.units[0].relu):
+            raise ValueError("pre_bn: only a block without a leading ReLU and with a strided skip conv")
         M = N * H * W
         units = []
         src, act, sc, sh = x_in, (ACT_RELU if b.units[0].relu else ACT_NONE), None, None
