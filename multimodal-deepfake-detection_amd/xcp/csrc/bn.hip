@@ -492,6 +492,17 @@ __global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict
   float sc[CPT], sh[CPT];
   VecIO<float, CPT>::load(s1 + c0, sc);
   VecIO<float, CPT>::load(t1 + c0, sh);
+  // Branch-free loads: out-of-range rows / columns read a clamped (valid) pixel and are masked to
+  // -inf, which the strict first-max rule below never selects -- the same result as skipping them,
+  // but without a branch per load all 25 loads (and the 4 skip loads) can be in flight at once
+  // (with a branch each, every load was its own round trip).
+  const int oh0 = 2 * qa, ow0 = 2 * qb;
+  float sv[4][CPT];
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const int oh = min(oh0 + (o >> 1), OH - 1), ow = min(ow0 + (o & 1), OW - 1);
+    VecIO<T, CPT>::load(S + (((long)n * OH + oh) * OW + ow) * C + c0, sv[o]);
+  }
   float m[4][CPT];
   unsigned char am[4][CPT];
 #pragma unroll
@@ -503,16 +514,18 @@ __global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict
     }
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    const int ih = 4 * qa - 1 + r;
-    if (ih < 0 || ih >= H) continue;
+    const int ihr = 4 * qa - 1 + r;
+    const bool rok = ihr >= 0 && ihr < H;
+    const int ih = min(max(ihr, 0), H - 1);
 #pragma unroll
     for (int cc = 0; cc < 5; ++cc) {
-      const int iw = 4 * qb - 1 + cc;
-      if (iw < 0 || iw >= W) continue;
+      const int iwr = 4 * qb - 1 + cc;
+      const bool ok = rok && iwr >= 0 && iwr < W;
+      const int iw = min(max(iwr, 0), W - 1);
       float v[CPT];
       VecIO<T, CPT>::load(Y + (((long)n * H + ih) * W + iw) * C + c0, v);
 #pragma unroll
-      for (int j = 0; j < CPT; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
+      for (int j = 0; j < CPT; ++j) v[j] = ok ? fmaf(v[j], sc[j], sh[j]) : -INFINITY;
 #pragma unroll
       for (int oy = 0; oy < 2; ++oy) {
         const int ky = r - 2 * oy;
@@ -542,10 +555,9 @@ __global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict
     const int oh = 2 * qa + (o >> 1), ow = 2 * qb + (o & 1);
     if (oh >= OH || ow >= OW) continue;
     const long op = ((long)n * OH + oh) * OW + ow;
-    float sv[CPT], res[CPT];
-    VecIO<T, CPT>::load(S + op * C + c0, sv);
+    float res[CPT];
 #pragma unroll
-    for (int j = 0; j < CPT; ++j) res[j] = m[o][j] + (s2 ? fmaf(sv[j], a2[j], b2[j]) : sv[j]);
+    for (int j = 0; j < CPT; ++j) res[j] = m[o][j] + (s2 ? fmaf(sv[o][j], a2[j], b2[j]) : sv[o][j]);
     VecIO<T, CPT>::store(Out + op * C + c0, res);
     unsigned long long pk = 0;
 #pragma unroll
