@@ -43,16 +43,21 @@ __global__ __launch_bounds__(256) void dw_fwd_small_kernel(const bf16* __restric
   }
   const bf16* Xn = X + (long)n * H * W * C + c0;
   bf16* Yn = Y + (long)n * H * W * C + c0;
+  // Row h's raw pixels are fetched one step ahead of their use (fetch_row issues all W loads
+  // with no branch between them and nothing waits on them until the next step's act_row), so
+  // the loads of row r + 2 are in flight while row r is computed.
+  uint2 nx[W];
+  auto fetch_row = [&](int h) {
+#pragma unroll
+    for (int x = 0; x < W; ++x) nx[x] = *reinterpret_cast<const uint2*>(Xn + ((long)h * W + x) * C);
+  };
   // row h as W + 2 activated columns (zero padding at both ends and outside the frame)
-  auto load_row = [&](int h, f2 (&o)[W + 2][2]) {
+  auto act_row = [&](int h, f2 (&o)[W + 2][2]) {
+    const bool ok = h < H;   // h >= 0 here
     o[0][0] = o[0][1] = o[W + 1][0] = o[W + 1][1] = f2(0.f);
 #pragma unroll
     for (int x = 0; x < W; ++x) {
-      if (h < 0 || h >= H) {
-        o[x + 1][0] = o[x + 1][1] = f2(0.f);
-        continue;
-      }
-      const uint2 u = *reinterpret_cast<const uint2*>(Xn + ((long)h * W + x) * C);
+      const uint2 u = nx[x];
       f2 v0 = f2{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u)};
       f2 v1 = f2{__uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
       if constexpr (ACT == ACT_BNRELU) {
@@ -62,12 +67,13 @@ __global__ __launch_bounds__(256) void dw_fwd_small_kernel(const bf16* __restric
         v0 = max0(v0);
         v1 = max0(v1);
       }
-      o[x + 1][0] = v0;
-      o[x + 1][1] = v1;
+      o[x + 1][0] = ok ? v0 : f2(0.f);
+      o[x + 1][1] = ok ? v1 : f2(0.f);
     }
   };
   auto step = [&](int r, const f2 (&ra)[W + 2][2], const f2 (&rb)[W + 2][2], f2 (&rc)[W + 2][2]) {
-    load_row(r + 1, rc);
+    act_row(r + 1, rc);
+    if (r + 2 < H) fetch_row(r + 2);   // uniform: r and H are the same for every thread
 #pragma unroll
     for (int x = 0; x < W; ++x) {
       f2 o[2];
@@ -93,8 +99,11 @@ __global__ __launch_bounds__(256) void dw_fwd_small_kernel(const bf16* __restric
     }
   };
   f2 w0[W + 2][2], w1[W + 2][2], w2[W + 2][2];
-  load_row(-1, w0);
-  load_row(0, w1);
+#pragma unroll
+  for (int x = 0; x < W + 2; ++x) w0[x][0] = w0[x][1] = f2(0.f);   // row -1: padding
+  fetch_row(0);
+  act_row(0, w1);
+  if (1 < H) fetch_row(1);
   for (int r = 0; r < H; r += 3) {
     step(r, w0, w1, w2);
     if (r + 1 < H) step(r + 1, w1, w2, w0);

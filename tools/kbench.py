@@ -196,18 +196,30 @@ def main():
             rep(f"dw_fwd N={Ng} {Hg}x{Wg} x 736 act=2", timeit(lambda: ops.dw_fwd(2, Xg, Yg, Wtg, scg, shg, Ng, Hg, Wg,
                                                                                    736)), 4 * Mg * 736)
             del Xg, Dg, Yg
-    if "tailpool" in sel:   # block1's pooled tail at 147^2 x 128 (the largest)
-        Hp, Cp = 147, 128
-        OHp = (Hp - 1) // 2 + 1
-        Yp = torch.randn(N * Hp * Hp * Cp, device=dev, generator=g).to(dt)
-        Sp = torch.randn(N * OHp * OHp * Cp, device=dev, generator=g).to(dt)
-        Op = torch.empty_like(Sp)
-        Ap = torch.empty(N * OHp * OHp * Cp, device=dev, dtype=torch.uint8)
-        sc2, sh2 = sc[:Cp].contiguous(), sh[:Cp].contiguous()
-        byts = 2 * (Yp.numel() + 2 * Sp.numel()) + Ap.numel()
-        rep("tail_fwd pooled 147^2x128", timeit(lambda: ops.tail_fwd(Yp, sc2, sh2, True, Sp, sc2, sh2, Op, Ap, N, Hp, Hp,
-                                                                     Cp)), byts)
-        del Yp, Sp, Op, Ap
+    if "dwsmall" in sel:   # tiny-frame depthwise forward at the XceptionLSTMA shapes (1920 64^2 frames)
+        for Hs, Cs in ((4, 736), (8, 736), (8, 256)):
+            Ms = 1920 * Hs * Hs
+            Xs = torch.randn(Ms, Cs, device=dev, generator=g).to(dt)
+            Ys = torch.empty_like(Xs)
+            Wts = torch.randn(9, Cs, device=dev, generator=g)
+            scs = torch.rand(Cs, device=dev, generator=g) + 0.5
+            shs = torch.randn(Cs, device=dev, generator=g)
+            rep(f"dw_fwd small 1920x{Hs}^2x{Cs} act=2", timeit(lambda: ops.dw_fwd(2, Xs, Ys, Wts, scs, shs, 1920, Hs, Hs,
+                                                                                   Cs)), 4 * Ms * Cs)
+            del Xs, Ys
+    if "tailpool" in sel:   # the three pooled block tails of the entry flow (blocks 1-3)
+        for Hp, Cp in ((147, 128), (74, 256), (37, 736)):
+            OHp = (Hp - 1) // 2 + 1
+            Yp = torch.randn(N * Hp * Hp * Cp, device=dev, generator=g).to(dt)
+            Sp = torch.randn(N * OHp * OHp * Cp, device=dev, generator=g).to(dt)
+            Op = torch.empty_like(Sp)
+            Ap = torch.empty(N * OHp * OHp * Cp, device=dev, dtype=torch.uint8)
+            sc2 = (torch.rand(Cp, device=dev, generator=g) + 0.5)
+            sh2 = torch.randn(Cp, device=dev, generator=g)
+            byts = 2 * (Yp.numel() + 2 * Sp.numel()) + Ap.numel()
+            rep(f"tail_fwd pooled {Hp}^2x{Cp}", timeit(lambda: ops.tail_fwd(Yp, sc2, sh2, True, Sp, sc2, sh2, Op, Ap, N, Hp,
+                                                                            Hp, Cp)), byts)
+            del Yp, Sp, Op, Ap
     if "pad" in sel:   # channel pitch 728 vs 736 (64-B aligned rows) vs 768 (128-B aligned) at 19^2 x 256
         for Cp in (728, 736, 768):
             Mp = N * H * W
