@@ -359,18 +359,26 @@ __global__ __launch_bounds__(256) void bn_act_strided_kernel(const T* __restrict
 }
 
 // dy = alpha*dz + bcoef*y + delta   (dbeta = sum dz, dgamma = sum dz*yhat come from the finalize)
-template <typename T, int CPT, bool MASK>
+// A thread owns one chunk of CPT channels in RPT rows p0 + k * ceil(rows / RPT) (each k a
+// contiguous stream across the grid): the 3-5 per-channel coefficient vectors are loaded once
+// for RPT rows, and all 2 * RPT data loads are issued back to back (clamped rows, guarded stores).
+template <typename T, int CPT, bool MASK, int RPT>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dZ, const T* __restrict__ Yv, T* dY,
                                                            const float* alpha, const float* bcoef, const float* delta,
                                                            const float* ms, const float* mt, long rows, int C) {
   const int CV = C / CPT;
+  const long rq = (rows + RPT - 1) / RPT;
   const long g = (long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= rows * CV) return;
+  if (g >= rq * CV) return;
   const int c0 = (int)(g % CV) * CPT;
-  const long p = g / CV;
-  float dz[CPT], y[CPT], al[CPT], bc[CPT], de[CPT];
-  VecIO<T, CPT>::load(dZ + p * C + c0, dz);
-  VecIO<T, CPT>::load(Yv + p * C + c0, y);
+  const long p0 = g / CV;
+  float dz[RPT][CPT], y[RPT][CPT], al[CPT], bc[CPT], de[CPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const long p = min(p0 + k * rq, rows - 1);
+    VecIO<T, CPT>::load(dZ + p * C + c0, dz[k]);
+    VecIO<T, CPT>::load(Yv + p * C + c0, y[k]);
+  }
   VecIO<float, CPT>::load(alpha + c0, al);
   VecIO<float, CPT>::load(bcoef + c0, bc);
   VecIO<float, CPT>::load(delta + c0, de);
@@ -379,11 +387,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     VecIO<float, CPT>::load(ms + c0, sm);
     VecIO<float, CPT>::load(mt + c0, tm);
 #pragma unroll
-    for (int j = 0; j < CPT; ++j) dz[j] = fmaf(y[j], sm[j], tm[j]) > 0.f ? dz[j] : 0.f;
+    for (int k = 0; k < RPT; ++k)
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) dz[k][j] = fmaf(y[k][j], sm[j], tm[j]) > 0.f ? dz[k][j] : 0.f;
   }
 #pragma unroll
-  for (int j = 0; j < CPT; ++j) dz[j] = fmaf(al[j], dz[j], fmaf(bc[j], y[j], de[j]));
-  VecIO<T, CPT>::store(dY + p * C + c0, dz);
+  for (int k = 0; k < RPT; ++k) {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) dz[k][j] = fmaf(al[j], dz[k][j], fmaf(bc[j], y[k][j], de[j]));
+    const long p = p0 + k * rq;
+    if (p < rows) VecIO<T, CPT>::store(dY + p * C + c0, dz[k]);
+  }
 }
 
 // dx *= (x > 0)
@@ -862,10 +876,13 @@ int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const f
                      const float* delta, const float* ms, const float* mt, long rows, int C, hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
   if ((ms == nullptr) != (mt == nullptr)) return XCP_EINVAL;
-  const unsigned g = nblk(rows * (C / 8));
-#define XCP_APPLY(TT, MK)                                                                                      \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, 8, MK>), dim3(g), dim3(256), 0, st, (const TT*)dZ, (const TT*)Y,  \
-                     (TT*)dY, alpha, bcoef, delta, ms, mt, rows, C)
+  if (rows <= 0) return XCP_OK;
+  // rows per thread: 4 with the mask (5 coefficient vectors), 2 without (3); at 92,416 x 736 bf16
+  // 91.5 -> 74 us and 71 -> 71 us against one row per thread (profiles/r02_bnapply_ab.txt)
+  const long rq4 = (rows + 3) / 4, rq2 = (rows + 1) / 2;
+#define XCP_APPLY(TT, MK)                                                                                       \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<TT, 8, MK, MK ? 4 : 2>), dim3(nblk((MK ? rq4 : rq2) * (C / 8))),    \
+                     dim3(256), 0, st, (const TT*)dZ, (const TT*)Y, (TT*)dY, alpha, bcoef, delta, ms, mt, rows, C)
   if (dtype == XCP_BF16) {
     if (ms) XCP_APPLY(bf16, true);
     else XCP_APPLY(bf16, false);

@@ -196,6 +196,17 @@ def main():
             rep(f"dw_fwd N={Ng} {Hg}x{Wg} x 736 act=2", timeit(lambda: ops.dw_fwd(2, Xg, Yg, Wtg, scg, shg, Ng, Hg, Wg,
                                                                                    736)), 4 * Mg * 736)
             del Xg, Dg, Yg
+    if "bnapply" in sel:   # BN-backward apply at the middle-flow shape (92,416 rows x 736), without / with the mask
+        Ma, Ca = N * H * W, 736
+        dZa = torch.randn(Ma, Ca, device=dev, generator=g).to(dt)
+        Ya = torch.randn(Ma, Ca, device=dev, generator=g).to(dt)
+        dYa = torch.empty_like(Ya)
+        coef = torch.randn(3 * Ca, device=dev, generator=g)
+        sta = {"scale": torch.rand(Ca, device=dev, generator=g) + 0.5, "shift": torch.randn(Ca, device=dev, generator=g)}
+        for relu in (False, True):
+            rep(f"bn_bwd_apply {Ma}x{Ca} mask={int(relu)}",
+                timeit(lambda: ops.bn_apply_coef(dZa, Ya, dYa, coef, sta, Ma, Ca, relu)), 3 * 2 * Ma * Ca)
+        del dZa, Ya, dYa
     if "dwsmall" in sel:   # tiny-frame depthwise forward at the XceptionLSTMA shapes (1920 64^2 frames)
         for Hs, Cs in ((4, 736), (8, 736), (8, 256)):
             Ms = 1920 * Hs * Hs
