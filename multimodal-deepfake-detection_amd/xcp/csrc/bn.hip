@@ -583,25 +583,10 @@ __global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict
 // Max-pool backward by gather, per 2 x 2 quad of input pixels (2a..2a+1, 2b..2b+1): the quad
 // lies in windows (a..a+1, b..b+1), so each thread loads 4 windows' dOut / argmax once and
 // writes 4 pixels (a per-pixel gather loads 2.25 windows per pixel).
-// quad q = (n, a, b): fill g[py*2+px][j] with the gradient of input pixel (2a+py, 2b+px)
-// (rounded to T; pixels past H / W are left out by the callers)
+// pool_combine: g[py*2+px][j] = the gradient of input pixel (2a+py, 2b+px) from the 4 windows'
+// dOut d[k] and argmax bytes am[k] (0xff: window k absent), rounded to T.
 template <typename T, int CPT>
-XCP_DEV void pool_quad(const PoolSrc& ps, unsigned n, unsigned a, unsigned b, int C, unsigned c0,
-                       float (&g)[4][CPT]) {
-  const T* dOut = reinterpret_cast<const T*>(ps.dOut);
-  const bool hb = b + 1 < (unsigned)ps.OW, ha = a + 1 < (unsigned)ps.OH;
-  float d[4][CPT];
-  unsigned am[4][2];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const bool ok = (k & 1 ? hb : true) && (k & 2 ? ha : true);
-    const unsigned oh = a + (k >> 1), ow = b + (k & 1);
-    const long op = ((long)(n * ps.OH + (ok ? oh : a)) * ps.OW + (ok ? ow : b)) * C + c0;
-    VecIO<T, CPT>::load(dOut + op, d[k]);
-    const uint2 m = *reinterpret_cast<const uint2*>(ps.amax + op);
-    am[k][0] = ok ? m.x : 0xffffffffu;   // 0xff never matches a tap
-    am[k][1] = ok ? m.y : 0xffffffffu;
-  }
+XCP_DEV void pool_combine(const float (&d)[4][CPT], const unsigned (&am)[4][2], float (&g)[4][CPT]) {
   auto tap = [&](int k, int j) { return (am[k][j >> 2] >> (8 * (j & 3))) & 0xffu; };
   // pixel (py, px) of the quad: its windows in (oh, ow) order and the tap it has in each
   //   (0,0): w00 t4          (0,1): w00 t5, w01 t3
@@ -619,6 +604,35 @@ XCP_DEV void pool_quad(const PoolSrc& ps, unsigned n, unsigned a, unsigned b, in
         if (py && px && tap(3, j) == 0u) s += d[3][j];
         g[py * 2 + px][j] = rnd<T>(s);
       }
+}
+
+// window k (= dy*2 + dx: (a+dy, b+dx)) of quad (n, a, b): present, and its element offset
+// (an absent window maps to window (a, b), so the address is always valid)
+XCP_DEV bool pool_win(const PoolSrc& ps, unsigned n, unsigned a, unsigned b, int C, unsigned c0, int k, long& op) {
+  const bool ok = (k & 1 ? b + 1 < (unsigned)ps.OW : true) && (k & 2 ? a + 1 < (unsigned)ps.OH : true);
+  const unsigned oh = a + (k >> 1), ow = b + (k & 1);
+  op = ((long)(n * ps.OH + (ok ? oh : a)) * ps.OW + (ok ? ow : b)) * C + c0;
+  return ok;
+}
+
+// quad q = (n, a, b): fill g (pool_combine) from dOut / amax (pixels past H / W are left out by
+// the callers)
+template <typename T, int CPT>
+XCP_DEV void pool_quad(const PoolSrc& ps, unsigned n, unsigned a, unsigned b, int C, unsigned c0,
+                       float (&g)[4][CPT]) {
+  const T* dOut = reinterpret_cast<const T*>(ps.dOut);
+  float d[4][CPT];
+  unsigned am[4][2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    long op;
+    const bool ok = pool_win(ps, n, a, b, C, c0, k, op);
+    VecIO<T, CPT>::load(dOut + op, d[k]);
+    const uint2 m = *reinterpret_cast<const uint2*>(ps.amax + op);
+    am[k][0] = ok ? m.x : 0xffffffffu;   // 0xff never matches a tap
+    am[k][1] = ok ? m.y : 0xffffffffu;
+  }
+  pool_combine<T, CPT>(d, am, g);
 }
 
 // dZ = max-pool backward of dOut (one thread per input quad and 8 channels)
@@ -645,11 +659,21 @@ __global__ __launch_bounds__(256) void maxpool_bwd_quad_kernel(PoolSrc ps, T* __
 
 // The same, fused with the BatchNorm-backward reduce of the BN that precedes the pool:
 // part[P][2][C] = per-chunk (sum dz, sum dz*(y-mean)*invstd) over the stored dz (chanred
-// layout, ChanRed over quads).
+// layout, ChanRed over quads).  Software-pipelined: the next quad's raw Y / dOut / argmax words
+// (clamped to the chunk, so unconditional) are loaded before the current quad is combined, so a
+// slot's quads are not one dependent round trip each.
+template <typename T, int CPT>
+struct QuadRaw {
+  static constexpr int NQ = CPT * (int)sizeof(T) / 16;   // 16-B words per CPT channels
+  uint4 y[4][NQ], d[4][NQ];
+  uint2 am[4];
+};
+
 template <typename T, int CPT>
 __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc ps, T* __restrict__ dZ,
                                                               const T* __restrict__ Y, const float* mean,
                                                               const float* invstd, float* part) {
+  using Q = QuadRaw<T, CPT>;
   const int cchunk = blockIdx.x % r.nch, pchunk = blockIdx.x / r.nch;
   const int lcv = threadIdx.x % r.CVB, slot = threadIdx.x / r.CVB;
   const int cv = cchunk * r.CVB + lcv;
@@ -661,19 +685,53 @@ __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc
     float mu[CPT], is[CPT];
     VecIO<float, CPT>::load(mean + c0, mu);
     VecIO<float, CPT>::load(invstd + c0, is);
+    const T* dOut = reinterpret_cast<const T*>(ps.dOut);
     const long rb = (long)pchunk * r.rows_per_chunk, re = min(r.rows, rb + r.rows_per_chunk);
-    for (long p = rb + slot; p < re; p += r.SPB) {
+    auto coords = [&](long p, unsigned& n, unsigned& a, unsigned& b) {
       const unsigned q = (unsigned)p;
-      const unsigned t = q / (unsigned)ps.OW, b = q - t * ps.OW;
-      const unsigned n = t / (unsigned)ps.OH, a = t - n * ps.OH;
-      float y[4][CPT];
+      const unsigned t = q / (unsigned)ps.OW;
+      b = q - t * ps.OW;
+      n = t / (unsigned)ps.OH;
+      a = t - n * ps.OH;
+    };
+    auto fetch = [&](long p, Q& in) {
+      unsigned n, a, b;
+      coords(p, n, a, b);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const unsigned h = min(2 * a + (k >> 1), (unsigned)ps.H - 1), w = min(2 * b + (k & 1), (unsigned)ps.W - 1);
-        VecIO<T, CPT>::load(Y + ((long)(n * ps.H + h) * ps.W + w) * r.C + c0, y[k]);
+        const uint4* src = reinterpret_cast<const uint4*>(Y + ((long)(n * ps.H + h) * ps.W + w) * r.C + c0);
+#pragma unroll
+        for (int i = 0; i < Q::NQ; ++i) in.y[k][i] = src[i];
+        long op;
+        pool_win(ps, n, a, b, r.C, (unsigned)c0, k, op);
+        const uint4* dsrc = reinterpret_cast<const uint4*>(dOut + op);
+#pragma unroll
+        for (int i = 0; i < Q::NQ; ++i) in.d[k][i] = dsrc[i];
+        in.am[k] = *reinterpret_cast<const uint2*>(ps.amax + op);
+      }
+    };
+    Q cur;
+    long p = rb + slot;
+    if (p < re) fetch(p, cur);
+    for (; p < re; p += r.SPB) {
+      Q nxt;
+      fetch(min(p + r.SPB, re - 1), nxt);
+      unsigned n, a, b;
+      coords(p, n, a, b);
+      float d[4][CPT], y[4][CPT];
+      unsigned am[4][2];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        long op;
+        const bool ok = pool_win(ps, n, a, b, r.C, (unsigned)c0, k, op);
+        VecIO<T, CPT>::load(reinterpret_cast<const T*>(cur.d[k]), d[k]);
+        VecIO<T, CPT>::load(reinterpret_cast<const T*>(cur.y[k]), y[k]);
+        am[k][0] = ok ? cur.am[k].x : 0xffffffffu;   // 0xff never matches a tap
+        am[k][1] = ok ? cur.am[k].y : 0xffffffffu;
       }
       float g[4][CPT];
-      pool_quad<T, CPT>(ps, n, a, b, r.C, (unsigned)c0, g);
+      pool_combine<T, CPT>(d, am, g);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const unsigned h = 2 * a + (k >> 1), w = 2 * b + (k & 1);
@@ -685,6 +743,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc
           acc[1][j] = fmaf(g[k][j], (y[k][j] - mu[j]) * is[j], acc[1][j]);
         }
       }
+      cur = nxt;
     }
   }
   chanred_finish<CPT>(r, acc, part, cchunk, pchunk, lcv, slot);

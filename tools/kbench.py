@@ -196,6 +196,19 @@ def main():
             rep(f"dw_fwd N={Ng} {Hg}x{Wg} x 736 act=2", timeit(lambda: ops.dw_fwd(2, Xg, Yg, Wtg, scg, shg, Ng, Hg, Wg,
                                                                                    736)), 4 * Mg * 736)
             del Xg, Dg, Yg
+    if "poolbwd" in sel:   # max-pool backward + BN reduce of blocks 2 / 3 (74^2 x 256, 37^2 x 736)
+        from xcp.engine import Stats
+        for Hb, Cb in ((74, 256), (37, 736)):
+            OHb = (Hb - 1) // 2 + 1
+            Yb = torch.randn(N * Hb * Hb * Cb, device=dev, generator=g).to(dt)
+            dOb = torch.randn(N * OHb * OHb * Cb, device=dev, generator=g).to(dt)
+            amb = torch.randint(0, 9, (N * OHb * OHb * Cb,), device=dev, generator=g, dtype=torch.uint8)
+            dzb = torch.empty_like(Yb)
+            stb = Stats(Cb, dev)
+            byts = 2 * (2 * Yb.numel() + dOb.numel()) + amb.numel()
+            rep(f"maxpool_bwd_bnred {Hb}^2x{Cb}", timeit(lambda: ops.maxpool_bwd_bnred(dOb, amb, dzb, Yb, stb, N, Hb, Hb,
+                                                                                      Cb)), byts)
+            del Yb, dOb, amb, dzb
     if "bnapply" in sel:   # BN-backward apply at the middle-flow shape (92,416 rows x 736), without / with the mask
         Ma, Ca = N * H * W, 736
         dZa = torch.randn(Ma, Ca, device=dev, generator=g).to(dt)
