@@ -300,22 +300,26 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(const float* __restr
     const float4 v = *reinterpret_cast<const float4*>(whh + (long)j * H + s * KS + i);
     w[i] = v.x; w[i + 1] = v.y; w[i + 2] = v.z; w[i + 3] = v.w;
   }
-  // stage h_{t-1} (zero at t = 0): 8 loads in flight per thread
+  // stage h_{t-1} (zero at t = 0): 8 loads in flight per thread -- unconditional (clamped index;
+  // t = 0 reads step 0's slot as a stand-in and selects zero), since a load under a condition is
+  // issued and waited for on its own
   const int n4 = B * H / 4;
+  const int tp = t > 0 ? t - 1 : 0;
   for (int e0 = tid; e0 < n4; e0 += 8 * 256) {
     float4 v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int e = e0 + i * 256;
+      const int e = min(e0 + i * 256, n4 - 1);
       const int b = e / (H / 4), k4 = (e - b * (H / 4)) * 4;
-      v[i] = (t > 0 && e < n4) ? *reinterpret_cast<const float4*>(out + ((long)b * T + t - 1) * H + k4)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[i] = *reinterpret_cast<const float4*>(out + ((long)b * T + tp) * H + k4);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int e = e0 + i * 256;
       const int b = e / (H / 4), k4 = (e - b * (H / 4)) * 4;
-      if (e < n4) *reinterpret_cast<float4*>(sh + (b * 32 + k4 / KS) * PS + (k4 % KS)) = v[i];
+      if (e < n4)
+        *reinterpret_cast<float4*>(sh + (b * 32 + k4 / KS) * PS + (k4 % KS)) =
+            t > 0 ? v[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
   __syncthreads();
@@ -366,12 +370,14 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(const float* __restr
     }
     const float ig = sigm(pre[0]), fg = sigm(pre[1]), gg = tanhf(pre[2]), og = sigm(pre[3]);
     const long ob = ((long)b * T + t) * H;
-    const float cp = t > 0 ? cst[ob - H + k] : 0.f;
+    const long op = t > 0 ? ob - H + k : ob + k;   // t = 0: a valid stand-in, selected away
+    const float vcp = cst[op], vhp = out[op];
+    const float cp = t > 0 ? vcp : 0.f;
     const float c = fmaf(fg, cp, ig * gg);
     const float h = og * tanhf(c);
     float* gt = gates + ((long)b * T + t) * G4;
     gt[k] = ig; gt[H + k] = fg; gt[2 * H + k] = gg; gt[3 * H + k] = og;
-    hprev[ob + k] = t > 0 ? out[ob - H + k] : 0.f;
+    hprev[ob + k] = t > 0 ? vhp : 0.f;
     cst[ob + k] = c;
     out[ob + k] = h;
     if (t == T - 1) {
@@ -402,37 +408,62 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(const float* __restr
                                                             const float* __restrict__ cst, const float* __restrict__ gates,
                                                             float* __restrict__ dgates, float* __restrict__ dcw, int B,
                                                             int T, int H, int t) {
-  extern __shared__ float sm[];   // W columns [4H][2], dh [B][2]
+  extern __shared__ float sm[];   // W columns [16 slices][SP] ([4H / 16][2] each), dh [B][2]
   const int G4 = 4 * H;
+  const int per = G4 / 16, SP = 2 * per + 4;   // slice pitch: +4 floats, so the 16 slices of a
+                                               // half-wave start on 16 different 4-bank groups
   float* swc = sm;
-  float* sdh = sm + G4 * 2;
+  float* sdh = sm + 16 * SP;
   const int tid = threadIdx.x, u0 = blockIdx.x * LS_UPW;
   if (t < T - 1) {
-    for (int jj = tid; jj < G4; jj += 256) {   // rows u0, u0+1 of W_hh^T (contiguous)
-      swc[2 * jj] = whhT[(long)u0 * G4 + jj];
-      swc[2 * jj + 1] = whhT[(long)(u0 + 1) * G4 + jj];
+    // rows u0, u0+1 of W_hh^T (contiguous), interleaved into swc[j][2]: 16-B loads, up to 4 per
+    // row per thread issued before any store (clamped indices; a loop of dependent scalar loads
+    // was ~8 L2 round trips a step at H = 512)
+    const int n4 = G4 / 4;
+    const float4* r0 = reinterpret_cast<const float4*>(whhT + (long)u0 * G4);
+    const float4* r1 = reinterpret_cast<const float4*>(whhT + (long)(u0 + 1) * G4);
+    for (int e0 = tid; e0 < n4; e0 += 4 * 256) {
+      float4 x0[4], x1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = min(e0 + i * 256, n4 - 1);
+        x0[i] = r0[e];
+        x1[i] = r1[e];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = e0 + i * 256;
+        if (e < n4) {   // jj = 4e..4e+3, all in slice 4e / per
+          float4* d = reinterpret_cast<float4*>(swc + (4 * e / per) * SP + 2 * (4 * e % per));
+          d[0] = make_float4(x0[i].x, x1[i].x, x0[i].y, x1[i].y);
+          d[1] = make_float4(x0[i].z, x1[i].z, x0[i].w, x1[i].w);
+        }
+      }
     }
     __syncthreads();
-    const int per = G4 / 16;
     for (int b0 = 0; b0 < B; b0 += 16) {
       const int b = b0 + (tid >> 4), sl = tid & 15;
       float a0 = 0.f, a1 = 0.f;
       if (b < B) {
         const float* dg = dgates + ((long)b * T + t + 1) * G4 + sl * per;
-        const float* wc = swc + 2 * sl * per;
-        // 8 independent 16-B loads in flight per batch (the loop is L2-latency-bound otherwise)
-        for (int i0 = 0; i0 < per; i0 += 32) {
-          float4 g4[8];
+        const float* wc = swc + sl * SP;
+        // 16 independent 16-B loads in flight per batch (the loop is L2-latency-bound otherwise)
+        for (int i0 = 0; i0 < per; i0 += 64) {
+          float4 g4[16];
 #pragma unroll
-          for (int q = 0; q < 8; ++q) g4[q] = *reinterpret_cast<const float4*>(dg + i0 + 4 * q);
+          for (int q = 0; q < 16; ++q) g4[q] = *reinterpret_cast<const float4*>(dg + i0 + 4 * q);
 #pragma unroll
-          for (int q = 0; q < 8; ++q) {
+          for (int q = 0; q < 16; ++q) {
             const float gv[4] = {g4[q].x, g4[q].y, g4[q].z, g4[q].w};
+            // (W[i][0], W[i][1], W[i+1][0], W[i+1][1]) as one ds_read_b128: banks (a/4) % 64, the
+            // 16 slices 4 banks apart (pitch SP), so a lane group's reads never collide
+            const float4* w4 = reinterpret_cast<const float4*>(wc + 2 * (i0 + 4 * q));
+            const float4 wa = w4[0], wb = w4[1];
+            const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const int i = i0 + 4 * q + e;
-              a0 = fmaf(gv[e], wc[2 * i], a0);
-              a1 = fmaf(gv[e], wc[2 * i + 1], a1);
+              a0 = fmaf(gv[e], wv[2 * e], a0);
+              a1 = fmaf(gv[e], wv[2 * e + 1], a1);
             }
           }
         }
@@ -451,19 +482,27 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(const float* __restr
   }
   if (tid < B * LS_UPW) {
     const int b = tid / LS_UPW, v = tid - b * LS_UPW, k = u0 + v;
-    const long ob = ((long)b * T + t) * H;
-    const float dhr = t < T - 1 ? sdh[b * 2 + v] : (dhn ? dhn[(long)b * H + k] : 0.f);
-    const float dcr = t < T - 1 ? dcw[(long)b * H + k] : (dcn ? dcn[(long)b * H + k] : 0.f);
-    const float dh = dhr + (dout ? dout[ob + k] : 0.f);
-    const float c = cst[ob + k];
-    const float cp = t > 0 ? cst[ob - H + k] : 0.f;
+    const long ob = ((long)b * T + t) * H, bk = (long)b * H + k;
+    // every global load unconditional (absent operands read a valid stand-in address and are
+    // selected away), so they go out together instead of one round trip per branch
+    const bool last = t == T - 1;
+    const float* pc = cst + ob + k;
+    const float vhn = *(last && dhn ? dhn + bk : pc);
+    const float vcw = *(!last ? dcw + bk : (dcn ? dcn + bk : pc));
+    const float vdo = *(dout ? dout + ob + k : pc);
+    const float vcp = *(t > 0 ? pc - H : pc);
+    const float c = *pc;
     const float* gt = gates + ((long)b * T + t) * G4;
     const float ig = gt[k], fg = gt[H + k], gg = gt[2 * H + k], og = gt[3 * H + k];
+    const float dhr = !last ? sdh[b * 2 + v] : (dhn ? vhn : 0.f);
+    const float dcr = !last || dcn ? vcw : 0.f;
+    const float dh = dhr + (dout ? vdo : 0.f);
+    const float cp = t > 0 ? vcp : 0.f;
     const float tc = tanhf(c);
     const float dO = dh * tc;
     const float dc = dcr + dh * og * (1.f - tc * tc);
     const float dI = dc * gg, dG = dc * ig, dF = dc * cp;
-    dcw[(long)b * H + k] = dc * fg;
+    dcw[bk] = dc * fg;
     float* dg = dgates + ((long)b * T + t) * G4;
     dg[k] = dI * ig * (1.f - ig);
     dg[H + k] = dF * fg * (1.f - fg);
@@ -479,7 +518,7 @@ bool lstm_reg(int H, int kernel) { return kernel == 0 && (H == 128 || H == 64); 
 // per-step kernels: H = 32 * KS for the instantiated KS, clips within the register partials
 bool lstm_step(int B, int H, int kernel) {
   const size_t fwd_lds = ((size_t)B * 32 * (H / 32 + 4) + 8 * B) * sizeof(float);
-  const size_t bwd_lds = ((size_t)8 * H + 2 * B) * sizeof(float);
+  const size_t bwd_lds = ((size_t)8 * H + 64 + 2 * B) * sizeof(float);
   return kernel == 0 && !lstm_reg(H, kernel) && (H == 256 || H == 512 || H == 1024) && B <= LS_MAXB &&
          fwd_lds <= 65536 && bwd_lds <= 65536;
 }
@@ -536,7 +575,7 @@ int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const fl
     if (!work) return XCP_EINVAL;
     float* whhT = work + (long)B * H;
     hipLaunchKernelGGL(lstm_transpose_kernel, dim3(4 * H / 32, H / 32), dim3(256), 0, st, whh, whhT, H);
-    const size_t smem = ((size_t)8 * H + 2 * B) * sizeof(float);
+    const size_t smem = ((size_t)8 * H + 64 + 2 * B) * sizeof(float);
     for (int t = T - 1; t >= 0; --t)
       hipLaunchKernelGGL(lstm_bwd_step_kernel, dim3(H / LS_UPW), dim3(256), smem, st, dout, dhn, dcn, whhT, cst, gates,
                          dgates, work, B, T, H, t);
