@@ -330,12 +330,18 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(const float* __restr
   for (int b = 0; b < LS_MAXB; ++b) {
     acc[b] = 0.f;
     if (b < B) {
-      const float* hb = sh + (b * 32 + s) * PS;
+      // 16-B reads (ds_read_b128, banks (a/4) % 64): the slices' pitch PS = KS + 4 puts every
+      // lane group's 16 slices on distinct 4-bank slots (as 2-dword reads, banks mod 32, the same
+      // pitch was a 4-way conflict: 71 % of this kernel's LDS cycles)
+      const float4* hb = reinterpret_cast<const float4*>(sh + (b * 32 + s) * PS);
       float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-      for (int i = 0; i < KS; i += 2) {
-        a0 = fmaf(w[i], hb[i], a0);
-        a1 = fmaf(w[i + 1], hb[i + 1], a1);
+      for (int i = 0; i < KS; i += 4) {
+        const float4 h4 = hb[i / 4];
+        a0 = fmaf(w[i], h4.x, a0);
+        a1 = fmaf(w[i + 1], h4.y, a1);
+        a0 = fmaf(w[i + 2], h4.z, a0);
+        a1 = fmaf(w[i + 3], h4.w, a1);
       }
       acc[b] = a0 + a1;
     }

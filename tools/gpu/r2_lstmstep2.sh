@@ -1,5 +1,5 @@
-# GPU: per-step LSTM backward with bank-spread W column slices (ds_read_b128) + unconditional loads:
-# LSTM parity tests, rocprofv3 kernel traces (current vs tools/exp/lstmold), XceptionLSTMA line.
+# GPU: per-step LSTM kernels (bank-spread LDS reads): LSTM parity tests,
+# rocprofv3 kernel traces (current vs tools/exp/lstmold), XceptionLSTMA line.
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
