@@ -64,6 +64,10 @@ def parse():
     ap.add_argument("--measured-peaks", choices=["on", "off"], default="on",
                     help="time a bf16 GEMM (torch.matmul -> hipBLASLt, 8192^3) and a device copy after the timed "
                          "region and report the roofline fractions against them too")
+    ap.add_argument("--diag", choices=["on", "off"], default="on",
+                    help="per-step / forward / backward device times, allocator counters over the timed region, "
+                         "the MFMA-load clock before and after it, and (lstmv) the unfrozen step with the weight "
+                         "gradients on the main stream")
     ap.add_argument("--optim", choices=["fused", "torch"], default="fused",
                     help="fused: xcp.optim.FusedAdamClip (clip + Adam in two HIP launches); torch: "
                          "clip_grad_norm_ + torch.optim.Adam(fused=True)")
@@ -74,6 +78,12 @@ def parse():
         a.batch = a.batch or 32
         a.size = 128 if a.size == 299 else a.size
         a.mode = a.mode or "unfrozen"
+        # whole accumulation cycles (train_au_face.py: accumulation 4): the warm-up covers at least
+        # one, so the first optimizer step (state allocation, the first averaged-model update) is
+        # outside the timed region, and the timed window is a whole number of cycles
+        acc = 4
+        a.warmup = max(acc, -(-a.warmup // acc) * acc)
+        a.steps = max(acc, -(-a.steps // acc) * acc)
     a.frames = a.frames or (120 if audio else 16)
     a.batch = a.batch or (64 if a.model == "xception" else 16)
     a.mode = a.mode or ("frozen" if audio else "unfrozen" if a.model == "xception" else "both")
@@ -325,11 +335,19 @@ class Run:
         gl = torch.Generator(device=dev).manual_seed(4321 + rank)
         self.y = torch.randint(0, 2, (B, 1), generator=gl, device=dev).float()
 
-    def step(self):
+    def step(self, ev=None):
+        """One training step.  ev: 4 timing events recorded on the current stream at the step's
+        phase boundaries (start, after the loss, after backward, after all-reduce + optimizer)
+        -- event records only, no host synchronisation."""
         from xcp import ddp
+        if ev is not None:
+            ev[0].record()
         if self.args.model == "auface":
             loss, _, _ = self.trainer.micro_step(self.i, 1 << 30, self.batch)
             self.i += 1
+            if ev is not None:
+                for e in ev[1:]:
+                    e.record()
             return loss
         self.buckets.zero()
         ddp.broadcast_buffers(self.model)
@@ -338,11 +356,17 @@ class Run:
         else:
             out = self.model(self.model.extract_features(self.x, self.dev))
         loss = self.crit(out, self.y)
+        if ev is not None:
+            ev[1].record()
         loss.backward()
+        if ev is not None:
+            ev[2].record()
         self.buckets.allreduce()
         if self.args.optim == "torch":
             self.torch.nn.utils.clip_grad_norm_([p for p in self.params if p.grad is not None], 1.0)
         self.opt.step()   # (the fused optimiser clips to norm 1.0 inside)
+        if ev is not None:
+            ev[3].record()
         return loss
 
 
@@ -366,18 +390,37 @@ def measured_peaks(dev):
         torch.cuda.synchronize()
         return s.elapsed_time(e) / reps * 1e-3
 
+    from xcp import _lib, ops
     t_mm = best(lambda: torch.matmul(a, a, out=c))
-    t_cp = best(lambda: y.copy_(x))
+    n16 = x.numel() * 2 // 16
+    t_cp = best(lambda: _lib.call("xcp_stream_copy", x.data_ptr(), y.data_ptr(), n16, ops.stream()))
+    t_tc = best(lambda: y.copy_(x))
     out = {"gemm_bf16_tflops": round(2.0 * 8192 ** 3 / t_mm / 1e12, 1),
            "gemm_source": "torch.matmul (hipBLASLt) bf16 8192x8192x8192, mean of 10",
            "copy_gbs": round(2.0 * x.numel() * 2 / t_cp / 1e9, 1),
-           "copy_source": "device copy of 512 MB (read + write bytes), mean of 10"}
+           "copy_source": "streaming copy of 512 MB, 16 B per lane, 4 loads in flight per thread (xcp_stream_copy; "
+                          "read + write bytes), mean of 10",
+           "torch_copy_gbs": round(2.0 * x.numel() * 2 / t_tc / 1e9, 1)}
     del a, c, x, y
     torch.cuda.empty_cache()
     return out
 
 
-def timed(run, steps, warmup, world, timer=None):
+MEM_KEYS = ("num_alloc_retries", "num_device_alloc", "num_device_free", "num_ooms")
+
+
+def mem_counters(dev):
+    import torch
+    st = torch.cuda.memory_stats(dev)
+    return {k: int(st.get(k, 0)) for k in MEM_KEYS}
+
+
+def timed(run, steps, warmup, world, timer=None, diag=None):
+    """Warm-up, then exactly ``steps`` timed steps between barrier + synchronize (host clock,
+    max over ranks).  diag (dict): filled with per-step / per-phase device times from events
+    recorded at the step's phase boundaries, and the caching allocator's counters over the
+    timed region (device allocations or retries inside it would be host-synchronising work
+    the warm-up did not absorb)."""
     import torch
     import torch.distributed as dist
     from xcp import ops
@@ -388,12 +431,14 @@ def timed(run, steps, warmup, world, timer=None):
         dist.barrier()
     if timer is not None:
         ops.set_kernel_timer(timer)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)] if diag is not None else None
+    m0 = mem_counters(run.dev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        loss = run.step()
+    for i in range(steps):
+        loss = run.step(evs[i] if evs is not None else None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -403,6 +448,18 @@ def timed(run, steps, warmup, world, timer=None):
         e = torch.tensor([elapsed], device=run.dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = e.item()
+    if diag is not None:
+        m1 = mem_counters(run.dev)
+        st = torch.cuda.memory_stats(run.dev)
+        step_ms = [evs[i][0].elapsed_time(evs[i + 1][0]) for i in range(steps - 1)] + \
+                  [evs[-1][0].elapsed_time(evs[-1][3])]
+        ph = [[ev[k].elapsed_time(ev[k + 1]) for ev in evs] for k in range(3)]
+        mean = lambda v: round(sum(v) / len(v), 3)   # noqa: E731
+        diag.update({"step_ms": [round(v, 2) for v in step_ms],
+                     "fwd_ms": mean(ph[0]), "bwd_ms": mean(ph[1]), "opt_ms": mean(ph[2]),
+                     "alloc_in_timed_region": {k: m1[k] - m0[k] for k in MEM_KEYS},
+                     "reserved_peak_gb": round(st.get("reserved_bytes.all.peak", 0) / 2 ** 30, 2),
+                     "allocated_peak_gb": round(st.get("allocated_bytes.all.peak", 0) / 2 ** 30, 2)})
     return elapsed, float(loss.item())
 
 
@@ -439,6 +496,9 @@ def main():
     modes = ["unfrozen", "frozen"] if args.mode == "both" else [args.mode]
 
     results = {}
+    diag = {"device": torch.cuda.get_device_name(dev)} if args.diag == "on" else None
+    if diag is not None:
+        diag["clock_mhz_idle"] = round(ops.clock_probe(dev), 1)
     for mode in modes:
         if rank == 0:
             log(f"{args.model} {mode}: building model")
@@ -451,10 +511,25 @@ def main():
                                      and a["N"] == cp and a["K"] == cp and a["stats"] is not None,
                                      "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == cp and a["H"] == hm})
         steps = args.steps if mode == modes[0] else max(3, args.steps // 2)
-        elapsed, loss = timed(run, steps, args.warmup, world, timer)
+        dg = {} if diag is not None else None
+        elapsed, loss = timed(run, steps, args.warmup, world, timer, dg)
+        if dg is not None:
+            if mode == modes[0]:
+                dg["clock_mhz_after"] = round(ops.clock_probe(dev), 1)
+            diag[mode] = dg
         results[mode] = (elapsed, steps, loss, timer)
         if rank == 0:
             log(f"{args.model} {mode}: {1e3 * elapsed / steps:.2f} ms/step")
+        if diag is not None and mode == "unfrozen" and args.model == "lstmv" and not fusion:
+            # the same step with the weight gradients on the main stream (no side-stream overlap)
+            engine.WGRAD_SIDE_STREAM = False
+            try:
+                s2 = max(3, args.steps // 2)
+                e2, _ = timed(run, s2, 2, world)
+                diag["unfrozen"]["wgrad_main_stream_ms"] = round(1e3 * e2 / s2, 3)
+                log(f"{args.model} {mode}, weight gradients on the main stream: {1e3 * e2 / s2:.2f} ms/step")
+            finally:
+                engine.WGRAD_SIDE_STREAM = True
         del run
         torch.cuda.empty_cache()
     small = None
@@ -551,6 +626,8 @@ def main():
         out.update(extra)
         if small is not None:
             out["small_batch"] = small
+        if diag is not None:
+            out["diag"] = diag
         if args.measured_peaks == "on" and not audio and not fusion:
             mp = measured_peaks(dev)
             out["measured_peaks"] = mp

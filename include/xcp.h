@@ -226,6 +226,15 @@ int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const 
 int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const float* whh, const float* cst,
                  const float* gates, float* dgates, float* work, int B, int T, int H, int kernel, xcp_stream_t stream);
 
+/* ---- diagnostic (bench.py only; no reference counterpart) ----
+ * blocks workgroups (one per CU) each run `iters` x 4 back-to-back bf16 MFMAs; out: DEVICE int64
+ * [2 * blocks + 256]: out[2b] = shader cycles of block b's loop, out[2b + 1] = 100 MHz real-time
+ * ticks of it (clock = cycles / ticks * 100 MHz). */
+int xcp_clock_probe(long long* out, int blocks, int iters, xcp_stream_t stream);
+/* out[i] = in[i] for n16 16-byte units (a multiple of 1024): the streaming-copy rate bench.py
+ * quotes the depthwise kernels against (the guide's float4 copy) */
+int xcp_stream_copy(const void* in, void* out, long n16, xcp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

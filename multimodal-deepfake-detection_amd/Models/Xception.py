@@ -137,9 +137,22 @@ class Xception(nn.Module):
         from xcp.engine import XceptionEngine
         dt = compute_dtype()
         eng = self._xcp_engines.get(dt)
-        if eng is None:
+        if eng is None or eng.model is not self:
+            # (a shallow copy of this module -- e.g. an nn.DataParallel replica made before
+            # _replicate_for_data_parallel below existed -- never drives another module's engine)
+            if eng is not None:
+                self._xcp_engines = {}
             eng = self._xcp_engines[dt] = XceptionEngine(self, dt)
         return eng
+
+    def _replicate_for_data_parallel(self):
+        """nn.DataParallel replica (train_audio.py:16-18): its own engine cache (an engine holds
+        the module it packs weights from) and no gradient sink -- a replica's gradients reach
+        the original parameters through DataParallel's autograd broadcast."""
+        r = super()._replicate_for_data_parallel()
+        r._xcp_engines = {}
+        r._xcp_grad_sink = None
+        return r
 
     def features(self, x):
         """Backbone up to the global average pool: [N,3,H,W] fp32 -> [N,2048] fp32."""

@@ -66,6 +66,8 @@ SIGNATURES = {
     "xcp_lstm_needs_whhT": [I, I, I],
     "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_lstm_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "xcp_clock_probe": [P, I, I, P],
+    "xcp_stream_copy": [P, P, L, P],
 }
 
 # entry points that return a size, not a status

@@ -106,8 +106,39 @@ class GradBuckets:
         self._done = set()
         self._pending = []
 
+    def _is_view(self, p):
+        o, _ = self.views[p]
+        g = p.grad
+        return g is not None and g.data_ptr() == self.flat.data_ptr() + 4 * o and g.shape == p.shape
+
+    def grad_view(self, p):
+        """``p.grad`` as this sink's flat view, for a producer that accumulates into it (the xcp
+        engine's gradient sink).  After ``optimizer.zero_grad()`` (set_to_none, the reference's
+        per-step call, train_visual.py:566) ``p.grad`` is None: the view is zeroed and re-attached.
+        A gradient tensor of the caller's own is copied into the view first.  A parameter this
+        sink does not hold keeps (or gets a zeroed) gradient tensor of its own."""
+        if p not in self.views:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            return p.grad
+        if not self._is_view(p):
+            self._adopt(p)
+        return p.grad
+
+    def _adopt(self, p):
+        o, n = self.views[p]
+        v = self.flat[o:o + n].view_as(p)
+        if p.grad is None:
+            v.zero_()
+        else:
+            v.copy_(p.grad)
+        p.grad = v
+
     def _launch(self, bi):
-        a, b, _ = self.buckets[bi]
+        a, b, ps = self.buckets[bi]
+        for p in ps:   # a gradient autograd created after zero_grad(set_to_none) joins the flat buffer
+            if not self._is_view(p):
+                self._adopt(p)
         self._pending.append(dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, async_op=True))
 
     def ready(self, params, side_stream=None):

@@ -166,7 +166,18 @@ class XceptionEngine:
 
     # ------------------------------------------------------------ parameters
     def named_params(self):
-        """Backbone parameters in a fixed order (the autograd inputs)."""
+        """Backbone parameters in a fixed order (the autograd inputs).  On an nn.DataParallel
+        replica the parameters are the broadcast copies DataParallel set as plain attributes
+        (``_former_parameters``, same names and order): gradients w.r.t. them flow back to the
+        original parameters through DataParallel's broadcast."""
+        if getattr(self.model, "_is_replica", False):
+            out = []
+            for mn, mod in self.model.named_modules():
+                for k, t in getattr(mod, "_former_parameters", {}).items():
+                    n = f"{mn}.{k}" if mn else k
+                    if t is not None and not n.startswith("fc."):
+                        out.append((n, t))
+            return out
         return [(n, p) for n, p in self.model.named_parameters() if not n.startswith("fc.")]
 
     def _version_key(self):
@@ -433,6 +444,14 @@ class XceptionEngine:
         # overlap the dgrad GEMMs and depthwise backward kernels of the main stream.
         main = torch.cuda.current_stream(dev)
         side = self._side_stream(dev) if WGRAD_SIDE_STREAM else None
+        # Main-stream tensors the side stream reads are kept referenced here until the main
+        # stream has waited for the side stream (end of this backward); freeing them after that
+        # point is stream-ordered, so the caching allocator may hand them out again at once.
+        # (record_stream instead defers their reuse until the side stream's work has actually
+        # run on the GPU; with the host a step or more ahead of the GPU that kept every step's
+        # backward temporaries unusable and the allocator mapped fresh device memory every step:
+        # 140-170 hipMallocs in 20 timed steps and 149 GB reserved for 25.6 GB in use.)
+        keep = []
 
         def wgrad(G, X, M, Nn, K, name, shape, **kw):
             """dW[Nn][K] = G^T X (logical channels; G / X at their channel pitches)"""
@@ -445,8 +464,7 @@ class XceptionEngine:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, **kw)
-            for t in (G, X, dst):   # kept alive for the side stream
-                t.record_stream(side)
+            keep.extend((G, X))   # dst: a gradient, referenced by the caller until the end
 
         def done():
             """every gradient requested since the last call is enqueued: tell the sink"""
@@ -493,7 +511,8 @@ class XceptionEngine:
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
                              pc(u.cin), dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, bn_stats=prev_st, accumulate=acc,
-                             Cw=u.cin, skip_pre=skip_pre, reduce_stream=side if DW_REDUCE_SIDE else None)
+                             Cw=u.cin, skip_pre=skip_pre, reduce_stream=side if DW_REDUCE_SIDE else None,
+                             keep=keep)
             return dX, (bnp if prev_st is not None else None)
 
         # ---- exit flow
@@ -527,13 +546,13 @@ class XceptionEngine:
         st2 = side if STEM_WGRAD_SIDE else None
         if st2 is not None:
             st2.wait_stream(main)
+        c2g, acc = g("conv2.weight", (64, 32, 3, 3))   # (allocated on the main stream)
         with torch.cuda.stream(st2) if st2 is not None else contextlib.nullcontext():
             w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
             if self.dtype == torch.bfloat16 and ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0:
                 ops.conv3x3_wgrad(dC2, S["a1"], w2g, N, OH1, OW1)
             else:
                 ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
-            c2g, acc = g("conv2.weight", (64, 32, 3, 3))
             if acc:
                 tmp = torch.empty_like(c2g)
                 ops.permute3(w2g, tmp, 64, 9, 32, (0, 2, 1))
@@ -541,14 +560,13 @@ class XceptionEngine:
             else:
                 ops.permute3(w2g, c2g, 64, 9, 32, (0, 2, 1))
         if st2 is not None:
-            for t in (dC2, S["a1"]):
-                t.record_stream(st2)
-            c2g.record_stream(main)
+            keep.append(dC2)
         dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], relu=True)   # relu (Xception.py:170) fused
         c1g, acc = g("conv1.weight", (32, 3, 3, 3))
         ops.conv1_wgrad(S["x"], dC1, c1g, N, S["IH"], S["IW"], accumulate=acc)
         if side is not None:
             main.wait_stream(side)
+        keep.clear()   # after the wait: reuse of these blocks is ordered behind the side stream
         done()
         return grads
 
@@ -621,9 +639,9 @@ class XceptionFunction(torch.autograd.Function):
         out = {}
         for n, p in zip(ctx.names, ctx.params):
             if n in need:
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
-                out[n] = p.grad
+                # the sink's flat view (re-attached, zeroed, after optimizer.zero_grad() set it to
+                # None), so what the kernels add is what the bucket all-reduce sees
+                out[n] = sink.grad_view(p)
         by_name = dict(zip(ctx.names, ctx.params))
         eng.backward(ctx.S, dfeat, out=out,
                      notify=lambda names, side: sink.ready([by_name[n] for n in names if n in need], side))

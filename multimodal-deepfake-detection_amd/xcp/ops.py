@@ -138,13 +138,15 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
 
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
-           bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None):
+           bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None, keep=None):
     """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
     (that BN's Stats) is given, else (None, 0).  dW_out receives the weight gradient in the
     nn.Conv2d [C][1][3][3] order (accumulate: added to it); Cw (default C): channels of the
     weight when C is a padded channel pitch.  skip_pre: dSkip is a gradient of the same
     activation act(X) (it passes the activation mask and enters the BN partial sums).
-    reduce_stream: run the weight-gradient slab reduction there (ordered after this launch)."""
+    reduce_stream: run the weight-gradient slab reduction there (ordered after this launch);
+    keep: a list that receives the scratch the reduce stream reads, for a caller that holds it
+    until its stream has waited for the reduce stream (otherwise it is record_stream'ed)."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
     bnpart = None
@@ -160,8 +162,11 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
         reduce_stream.wait_stream(torch.cuda.current_stream(dY.device))
         with torch.cuda.stream(reduce_stream):
             reduce_slabs(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
-        part.record_stream(reduce_stream)
-        dW_out.record_stream(reduce_stream)
+        if keep is not None:
+            keep.append(part)
+        else:
+            part.record_stream(reduce_stream)
+            dW_out.record_stream(reduce_stream)
     return bnpart, (P if bnpart is not None else 0)
 
 
@@ -438,6 +443,21 @@ class PermuteBatch:
             self._table = torch.tensor(rows, dtype=torch.int64).to(jobs[0][1].device)
             self._nblocks, self._key = blk, key
         _lib.call("xcp_permute3_batch", _p(self._table), len(jobs), self._nblocks, stream())
+
+
+# ---------------------------------------------------------------- diagnostics
+def clock_probe(device, launches=8, iters=40000):
+    """Shader clock (MHz) the chip holds under a bf16 MFMA load: ``launches`` back-to-back
+    probe launches (one workgroup per CU, ~0.6 ms each), median over the last launch's
+    workgroups of cycles / real-time ticks x 100 MHz (MI355X_MICROARCH.md, DVFS item 6)."""
+    blocks = torch.cuda.get_device_properties(device).multi_processor_count
+    out = torch.zeros(2 * blocks + 256, device=device, dtype=torch.int64)
+    with torch.cuda.device(device):
+        for _ in range(launches):
+            _lib.call("xcp_clock_probe", out.data_ptr(), blocks, iters, stream())
+        v = out[:2 * blocks].view(blocks, 2).cpu()
+    mhz = (v[:, 0].double() / v[:, 1].double().clamp(min=1)) * 100.0
+    return float(mhz.median())
 
 
 # ---------------------------------------------------------------- LSTM

@@ -50,6 +50,18 @@ class FusedAdamClip(torch.optim.Optimizer):
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         return st
 
+    @staticmethod
+    def _key(kind, rows):
+        """cache key of a chunk table: every pointer a row of it holds (param, grad and both
+        moment buffers), so a replaced state tensor (load_state_dict, a re-zeroed moment) or a
+        re-attached gradient can never reuse a table that points at the old storage"""
+        return (kind,) + tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel())
+                               for p, g, m, v in rows)
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._tables.clear()   # the moment buffers were replaced
+
     def _table(self, key, rows, dev):
         """device chunk table for a list of (param, grad, exp_avg, exp_avg_sq), cached by pointers"""
         tab = self._tables.get(key)
@@ -96,16 +108,14 @@ class FusedAdamClip(torch.optim.Optimizer):
             s = ops.stream()
             coef = 0
             if self.max_norm is not None:
-                key = ("all",) + tuple(r[0].data_ptr() * 31 + r[1].data_ptr() for r in every)
-                tab = self._table(key, every, dev)
+                tab = self._table(self._key("all", every), every, dev)
                 part = torch.empty(tab.shape[0], device=dev, dtype=torch.float32)
                 self._out = torch.empty(2, device=dev, dtype=torch.float32)
                 _lib.call("xcp_opt_sumsq", tab.data_ptr(), tab.shape[0], part.data_ptr(), float(self.max_norm),
                           self._out.data_ptr(), s)
                 coef = self._out.data_ptr()
             for grp, t, rows in launches:
-                key = ("grp",) + tuple(r[0].data_ptr() * 31 + r[1].data_ptr() for r in rows)
-                tab = self._table(key, rows, dev)
+                tab = self._table(self._key("grp", rows), rows, dev)
                 b1, b2 = grp["betas"]
                 _lib.call("xcp_opt_adam", tab.data_ptr(), tab.shape[0], coef, float(grp["lr"]), float(b1), float(b2),
                           float(grp["eps"]), float(grp["weight_decay"]), float(1.0 - b1 ** t),

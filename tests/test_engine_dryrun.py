@@ -216,6 +216,9 @@ def _sink_worker(rank, world, port, out):
     gb = ddp.GradBuckets(params, bucket_bytes=1 << 20, world=world, module=m)
     for step in range(2):
         gb.zero()
+        if step == 1:   # optimizer.zero_grad() (set_to_none) after zero(): the sink re-attaches its views
+            for p in params:
+                p.grad = None
         events.clear()
         n0 = len(calls)
         m(torch.rand(2, 3, 71, 71)).sum().backward()
@@ -241,3 +244,84 @@ def test_sink_allreduce_overlaps_backbone_backward():
         assert r["during"] >= r["buckets"] - 2, r   # all but the stem buckets launched inside backward
         for n, gr in r["grads"].items():
             assert torch.all(gr == 1.5), n
+
+
+def _cpu_replicate(net):
+    """torch.nn.parallel.replicate for one replica, on the CPU (the real one broadcasts over
+    CUDA devices): every module through _replicate_for_data_parallel, parameters as non-leaf
+    copies set as plain attributes (and in _former_parameters), buffers cloned."""
+    from collections import OrderedDict
+    modules = list(net.modules())
+    idx = {m: i for i, m in enumerate(modules)}
+    copies = [m._replicate_for_data_parallel() for m in modules]
+    pcopy = {p: p * 1.0 for p in net.parameters()}
+    for m, r in zip(modules, copies):
+        r._former_parameters = OrderedDict()
+        for k, child in m._modules.items():
+            if child is None:
+                r._modules[k] = None
+            else:
+                setattr(r, k, copies[idx[child]])
+        for k, p in m._parameters.items():
+            if p is None:
+                r._parameters[k] = None
+            else:
+                setattr(r, k, pcopy[p])
+                r._former_parameters[k] = pcopy[p]
+        for k, b in m._buffers.items():
+            setattr(r, k, None if b is None else b.clone())
+    return copies[0]
+
+
+def test_dataparallel_replica_gets_own_engine(fake_lib):
+    """nn.DataParallel (train_audio.py:16-18) replicates with a shallow __dict__ copy: a replica
+    must not drive the original's engine (bound to the original's parameters on cuda:0), must
+    not feed its gradient sink, and its backbone gradients must reach the original parameters
+    through the broadcast copies."""
+    from xcp import ddp
+    from Models.Xception import xception
+    torch.manual_seed(0)
+    m = xception(num_classes=1)
+    m.fc = nn.Identity()
+    gb = ddp.GradBuckets(list(m.parameters()), module=m)
+    m(torch.rand(2, 3, 71, 71))                     # the original's engine exists now
+    eng0 = m._engine()
+    r = _cpu_replicate(m)
+    assert r._xcp_engines is not m._xcp_engines and not r._xcp_engines
+    assert r._xcp_grad_sink is None and m._xcp_grad_sink is gb
+    er = r._engine()
+    assert er is not eng0 and er.model is r and eng0.model is m
+    names0 = [n for n, _ in eng0.named_params()]
+    namesr = [n for n, _ in er.named_params()]
+    assert names0 == namesr and len(namesr) == len(list(m.parameters()))
+    assert all(t is getattr(r.get_submodule(n.rsplit(".", 1)[0]) if "." in n else r, n.rsplit(".", 1)[-1])
+               for n, t in er.named_params())
+    for p in m.parameters():
+        p.grad = None
+    r(torch.rand(2, 3, 71, 71)).sum().backward()
+    for n, p in m.named_parameters():              # through the copies, not the sink
+        assert p.grad is not None and torch.all(p.grad == FILL["v"]), n
+    # a plain shallow copy (no _replicate_for_data_parallel) still gets an engine of its own
+    import copy as _copy
+    s = _copy.copy(m)
+    assert s._engine().model is s and m._engine() is eng0
+
+
+def test_sink_reattaches_after_zero_grad_set_to_none(fake_lib):
+    """optimizer.zero_grad() (set_to_none, the reference's per-step call, train_visual.py:566)
+    between GradBuckets.zero() steps: the engine's gradient sink re-attaches the zeroed flat
+    views instead of accumulating into fresh tensors the all-reduce never sees."""
+    from xcp import ddp
+    from Models.Xception import xception
+    torch.manual_seed(0)
+    m = xception(num_classes=1)
+    m.fc = nn.Identity()
+    params = list(m.parameters())
+    gb = ddp.GradBuckets(params, world=1, module=m)
+    for step in range(2):
+        for p in params:
+            p.grad = None                            # optimizer.zero_grad()
+        m(torch.rand(2, 3, 71, 71)).sum().backward()
+        for p in params:
+            assert gb._is_view(p)
+            assert torch.all(p.grad == FILL["v"])    # zeroed before accumulation, not stale

@@ -659,3 +659,50 @@ def test_fused_adam_clip_vs_torch(ops, gpu, max_norm):
         opt_b.step()
         for p, q in zip(a, b):
             torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_fused_adam_clip_load_state_dict_resume(ops, gpu):
+    """step -> load_state_dict(torch.optim.Adam's state_dict) -> step against torch.optim.Adam
+    with the gradient tensors kept in place (the GradBuckets pattern: param.grad views of one flat
+    buffer whose pointers never change), so a chunk table cached before the load would still
+    point at the replaced moment buffers (the cache key holds every row pointer and
+    load_state_dict drops the tables)."""
+    from xcp.optim import FusedAdamClip
+    g = torch.Generator(device=gpu).manual_seed(12)
+    shapes = [(5,), (64, 33), (20000,)]
+    a = [torch.randn(s, device=gpu, generator=g).requires_grad_(True) for s in shapes]
+    b = [t.detach().clone().requires_grad_(True) for t in a]
+    for p in a + b:
+        p.grad = torch.zeros_like(p)
+    opt_a = FusedAdamClip(a, lr=1e-2, weight_decay=1e-2, max_norm=1.0)
+    opt_b = torch.optim.Adam(b, lr=1e-2, weight_decay=1e-2)
+
+    def step(k):
+        for p, q in zip(a, b):
+            gr = torch.randn(p.shape, device=gpu, generator=g) * (1.0 + k)
+            p.grad.copy_(gr)
+            q.grad.copy_(gr)
+        opt_a.step()
+        torch.nn.utils.clip_grad_norm_(b, 1.0)
+        opt_b.step()
+
+    for k in range(2):
+        step(k)
+    # a different trajectory's state (torch's, after extra steps) replaces both optimisers' state
+    for k in range(2, 4):
+        for q in b:
+            q.grad.copy_(torch.randn(q.shape, device=gpu, generator=g))
+        torch.nn.utils.clip_grad_norm_(b, 1.0)
+        opt_b.step()
+    import copy
+    sd = copy.deepcopy(opt_b.state_dict())   # a checkpoint's copy (state_dict() returns the live tensors)
+    opt_a.load_state_dict(sd)
+    with torch.no_grad():
+        for p, q in zip(a, b):
+            p.copy_(q)
+    for k in range(4, 6):
+        step(k)
+    for p, q in zip(a, b):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+    for p, q in zip(a, b):
+        torch.testing.assert_close(opt_a.state[p]["exp_avg"], opt_b.state[q]["exp_avg"], rtol=1e-5, atol=1e-7)

@@ -403,3 +403,33 @@ def test_bench_size_step_vs_reference(gpu, golden, prec):
         elif "running_mean" in n:
             np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"], rtol=1e-4 if f32 else 5e-2,
                                        atol=1e-4 if f32 else 5e-2, err_msg=n)
+
+
+def test_dataparallel_replica_matches_module(gpu):
+    """An nn.DataParallel replica (torch.nn.parallel.replicate, the mechanism behind
+    train_audio.py:16-18, :38) of an xcp Xception runs on its own engine over the broadcast
+    parameter copies: features and the original parameters' gradients equal those of the module
+    run directly (fp32), and the original's engine stays bound to the original."""
+    import xcp
+    from Models.Xception import xception
+    torch.manual_seed(0)
+    m = xception(num_classes=1)
+    m.fc = nn.Identity()
+    m = m.to(gpu).train()
+    x = seeded_uniform((2, 3, 64, 64), 7).to(gpu)
+    r = seeded_normal((2, 2048), 8).to(gpu)
+    with xcp.precision("fp32"):
+        f0 = m(x)
+        (f0 * r).sum().backward()
+        g0 = {n: p.grad.clone() for n, p in m.named_parameters()}
+        eng0 = m._engine()
+        for p in m.parameters():
+            p.grad = None
+        rep = torch.nn.parallel.replicate(m, [gpu.index or 0])[0]
+        f1 = rep(x)
+        (f1 * r).sum().backward()
+    assert rep._engine() is not eng0 and m._engine() is eng0 and eng0.model is m
+    torch.testing.assert_close(f1, f0, rtol=1e-5, atol=1e-6)
+    for n, p in m.named_parameters():
+        assert p.grad is not None, n
+        torch.testing.assert_close(p.grad, g0[n], rtol=1e-4, atol=1e-6)

@@ -1,0 +1,9 @@
+# Round 3: the driver's bench command as the FIRST GPU process on a fresh box, then again as a
+# second process, then the GPU suite (progress under gpurun_out/).
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r3_b1.json 2> gpurun_out/r3_b1.err || exit $?
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-baseline off > gpurun_out/r3_b2.json 2> gpurun_out/r3_b2.err || exit $?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_t.log 2>&1
+echo "pytest rc=$?" >> gpurun_out/r3_t.log
