@@ -244,6 +244,25 @@ def clip_step(sd, clips, labels, unfrozen, audio=False, optim=None):
                 grads=grads, stats=stats, params=params)
 
 
+def frame_step(sd, frames, labels, optim=None):
+    """Configs C1 / C2: ``xception(num_classes=1)`` trained per frame (Xception.py:205-213; the
+    backbone of Xception.py:167-201 with its own ``fc``), train-mode BatchNorm,
+    BCEWithLogitsLoss, backward; with ``optim`` = dict(lr, weight_decay) one Adam step.
+    Returns dict(logits, loss, grads{name: tensor}, params{name: tensor after the step})."""
+    params = {k: v.detach().clone() for k, v in sd.items()}
+    keys = [k for k in params if "running" not in k and "num_batches" not in k]
+    for k in keys:
+        params[k].requires_grad_(True)
+    feats = backbone_forward(frames, params, True, {})
+    logits = F.linear(feats, params["fc.weight"], params["fc.bias"])
+    loss = F.binary_cross_entropy_with_logits(logits, labels)
+    loss.backward()
+    grads = {k: params[k].grad for k in keys}
+    if optim is not None:
+        adam_step({k: params[k] for k in keys}, grads, {}, optim["lr"], weight_decay=optim.get("weight_decay", 0.0))
+    return dict(logits=logits.detach(), loss=loss.detach(), grads=grads, params=params)
+
+
 def kaiming_like_init(shape, out_channels, kh, kw, gen):
     """Xception.py:154-158 init for a conv weight (N(0, sqrt(2/(kh*kw*out_channels))))."""
     return torch.randn(shape, generator=gen) * math.sqrt(2.0 / (kh * kw * out_channels))

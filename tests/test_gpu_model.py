@@ -345,16 +345,34 @@ def test_after_adam_and_buffers_b2t4(gpu, golden):
                                            err_msg=n)
 
 
+# bf16 head gradients against the reference's fp32 goldens (SURVEY 8c's 5e-2 for every weight
+# gradient); at 2-4 clips the random-init head's ReLU masks flip under the bf16 feature
+# perturbation, so below BENCH_HEAD_MIN_CLIPS clips the head is checked against the oracle head on
+# the GPU's own features only (check_head_on_features)
+BENCH_HEAD_MIN_CLIPS = 16
+
+
+def bn_errors_report(errs, bn_names, tol=5e-2):
+    """bf16 BatchNorm affine gradient-norm errors above SURVEY 8c's 5e-2, printed per parameter"""
+    over = sorted(((n, e) for n, e in errs.items() if n in bn_names and e > tol), key=lambda kv: -kv[1])
+    print(f"\nBN affine grad-norm errors > {tol}: {len(over)} of {len(bn_names)}:",
+          [(n, round(e, 4)) for n, e in over])
+    return over
+
+
+@pytest.mark.parametrize("fname", ["lstmv_b4t16.npz", "lstmv_b16t16.npz"])
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-def test_bench_size_step_vs_reference(gpu, golden, prec):
-    """XceptionLSTMV(128), unfrozen, at B*T = 64 frames of 299^2 (lstmv_b4t16.npz): the middle
-    flow's pointwise GEMMs have M = 23,104 rows, 273 output tiles of 256x256, so in bf16 the
-    bench's kernel set runs (the 256x256 NT / TN MFMA GEMMs), then one train_visual.py optimiser
-    step -- clip_grad_norm_(1.0) + Adam(lr 1e-5, weight_decay 1e-4) -- through FusedAdamClip."""
+def test_bench_size_step_vs_reference(gpu, golden, prec, fname):
+    """XceptionLSTMV(128), unfrozen, at B*T frames of 299^2: lstmv_b4t16.npz (64 frames; the
+    middle flow's pointwise GEMMs have M = 23,104 rows, 273 output tiles of 256x256, so in bf16
+    the bench's kernel set runs) and lstmv_b16t16.npz (256 frames: the bench configuration
+    itself, M = 92,416, 1,083 tiles, the sparse last round, the largest split-K slabs), then one
+    train_visual.py optimiser step -- clip_grad_norm_(1.0) + Adam(lr 1e-5, weight_decay 1e-4) --
+    through FusedAdamClip."""
     import xcp
     from xcp.optim import FusedAdamClip
     from Models.XceptionLSTMV import XceptionLSTMV
-    g = golden("lstmv_b4t16.npz")
+    g = golden(fname)
     B, T, S = int(g["B"]), int(g["T"]), int(g["S"])
     M = B * T * 19 * 19
     assert ((M + 255) // 256) * ((728 + 255) // 256) >= 256   # the 256x256 dispatch rule (gemm.hip nt_big)
@@ -368,9 +386,11 @@ def test_bench_size_step_vs_reference(gpu, golden, prec):
     logits = {}
     m.fc_out.register_forward_hook(lambda mod, i, o: logits.__setitem__("v", o.detach()))
     x = seeded_uniform((B, T, 3, S, S), 4242).to(gpu)
-    y = torch.tensor([[0.0], [1.0], [1.0], [0.0]], device=gpu)[:B]
+    labels = g["labels"] if "labels" in g else np.array([0.0, 1.0, 1.0, 0.0])[:B]
+    y = torch.tensor(labels, dtype=torch.float32, device=gpu).view(B, 1)
     with xcp.precision(prec):
         feats = m.extract_features(x, gpu)
+        del x
         loss = nn.BCELoss()(m(feats), y)
         loss.backward()
     torch.cuda.synchronize()
@@ -386,8 +406,14 @@ def test_bench_size_step_vs_reference(gpu, golden, prec):
     np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-5 if f32 else 2e-2)
     errs = {n: abs(p.grad.double().norm().item() - g[f"gradnorm/{n}"]) / max(float(g[f"gradnorm/{n}"]), 1e-30)
             for n, p in m.named_parameters()}
-    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not f32)
+    head_vs_ref = f32 or B >= BENCH_HEAD_MIN_CLIPS
+    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not head_vs_ref)
     if not f32:
+        bn_errors_report(errs, bn_param_names(m))
+        if head_vs_ref:   # the head's gradients against the reference's own
+            for n in ("lstm.bias_ih_l0", "fc_out.weight", "fc_out.bias"):
+                if f"grad/{n}" in g:
+                    assert relerr(dict(m.named_parameters())[n].grad.cpu(), g[f"grad/{n}"]) < 5e-2, n
         check_head_on_features(m, feats, y, {n: p.grad.clone() for n, p in m.named_parameters() if is_head(n)})
     norm = opt.step()
     np.testing.assert_allclose(norm.item(), g["total_gradnorm"], rtol=1e-3 if f32 else 5e-2)
@@ -396,6 +422,52 @@ def test_bench_size_step_vs_reference(gpu, golden, prec):
         check_after_step(m, g, "after_step", 1e-5, 2e-3)
     else:   # backbone weights: Adam's sign(g) at bf16 gradient fidelity (cosine ~0.9 to fp32)
         check_after_step(m, g, "after_step", 1e-5, 0.2)
+    for n, t in m.state_dict().items():
+        if "running_var" in n:
+            np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"], rtol=1e-4 if f32 else 2e-2,
+                                       err_msg=n)
+        elif "running_mean" in n:
+            np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"], rtol=1e-4 if f32 else 5e-2,
+                                       atol=1e-4 if f32 else 5e-2, err_msg=n)
+
+
+@pytest.mark.parametrize("fname,prec", [("xception_c1_b4.npz", "fp32"), ("xception_c1_b4.npz", "bf16"),
+                                        ("xception_c2_b64.npz", "bf16"), ("xception_c2_b64.npz", "fp32")])
+def test_xception_frame_step_vs_reference(gpu, golden, fname, prec):
+    """BASELINE configs C1 / C2: xception(num_classes=1) trained per frame (Xception.py:205-213)
+    at B = 4 / 64 frames of 299^2 -- logits, BCEWithLogits loss, every gradient norm, one
+    Adam(lr 1e-5, weight_decay 1e-4) step (FusedAdamClip, no clipping) and the BatchNorm buffers
+    against the reference's CPU step (capture_goldens.py g_xception_frames)."""
+    import xcp
+    from xcp.optim import FusedAdamClip
+    from Models.Xception import xception
+    g = golden(fname)
+    B, S = int(g["B"]), int(g["S"])
+    torch.manual_seed(0)
+    m = xception(num_classes=1).to(gpu).train()
+    opt = FusedAdamClip(m.parameters(), lr=1e-5, weight_decay=1e-4)
+    x = seeded_uniform((B, 3, S, S), int(g["seed_x"])).to(gpu)
+    y = (torch.arange(B, device=gpu) % 3 == 0).float().view(B, 1)
+    with xcp.precision(prec):
+        out = m(x)
+        loss = nn.BCEWithLogitsLoss()(out, y)
+        loss.backward()
+    torch.cuda.synchronize()
+    f32 = prec == "fp32"
+    np.testing.assert_allclose(out.detach().cpu().numpy(), g["logits"], atol=1e-4 if f32 else 3e-2, rtol=0)
+    np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-5 if f32 else 2e-2)
+    errs = {n: abs(p.grad.double().norm().item() - g[f"gradnorm/{n}"]) / max(float(g[f"gradnorm/{n}"]), 1e-30)
+            for n, p in m.named_parameters()}
+    check_gradnorms(errs, bn_param_names(m), f32)
+    if not f32:
+        bn_errors_report(errs, bn_param_names(m))
+    for n in ("fc.weight", "fc.bias"):
+        assert relerr(dict(m.named_parameters())[n].grad.cpu(), g[f"grad/{n}"]) < (1e-3 if f32 else 5e-2), n
+    tot = sum((p.grad.double() ** 2).sum().item() for p in m.parameters()) ** 0.5
+    np.testing.assert_allclose(tot, g["total_gradnorm"], rtol=1e-3 if f32 else 5e-2)
+    assert opt.step() is None
+    torch.cuda.synchronize()
+    check_after_step(m, g, "after_step", 1e-5, 2e-3 if f32 else 0.2)
     for n, t in m.state_dict().items():
         if "running_var" in n:
             np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"], rtol=1e-4 if f32 else 2e-2,

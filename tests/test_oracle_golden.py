@@ -186,3 +186,23 @@ def test_oracle_optimizer_step_vs_reference(golden):
             np.testing.assert_allclose(a.sum().item(), g[key], rtol=1e-6, atol=2e-5 * 1e-3 * a.numel() + 1e-6,
                                        err_msg=k)
             np.testing.assert_allclose((a * a).sum().item(), g[f"after_step/{k}/sumsq"], rtol=1e-5, err_msg=k)
+
+
+def test_frame_step_c1(golden):
+    """Config C1 (xception(num_classes=1), B = 4 frames of 299^2, BCEWithLogits + Adam): the
+    oracle's frame_step against the reference's own step (xception_c1_b4.npz)."""
+    g = golden("xception_c1_b4.npz")
+    B, S = int(g["B"]), int(g["S"])
+    torch.manual_seed(0)
+    sd = {k: v.clone() for k, v in xception(num_classes=1).state_dict().items()}
+    x = seeded_uniform((B, 3, S, S), int(g["seed_x"]))
+    y = (torch.arange(B) % 3 == 0).float().view(B, 1)
+    r = O.frame_step(sd, x, y, optim=dict(lr=float(g["lr"]), weight_decay=float(g["weight_decay"])))
+    np.testing.assert_allclose(r["logits"].numpy(), g["logits"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(r["loss"].item(), g["loss"], rtol=1e-6)
+    for n, gr in r["grads"].items():
+        np.testing.assert_allclose(gr.double().norm().item(), g[f"gradnorm/{n}"], rtol=1e-4, err_msg=n)
+    for n, p in r["params"].items():
+        if f"after_step/{n}/sum" in g:
+            np.testing.assert_allclose(p.detach().double().sum().item(), g[f"after_step/{n}/sum"], rtol=1e-6,
+                                       atol=1e-6, err_msg=n)

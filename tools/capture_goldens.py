@@ -302,43 +302,102 @@ def all_param_fp(out, prefix, module):
         out[f"{prefix}/{name}/sumsq"] = (a * a).sum().item()
 
 
-def g_lstmv_big(V, out_dir, B=4, T=16, S=299):
-    """The bench-size kernel set: XceptionLSTMV(128) unfrozen at B*T = 64 frames of 299^2
-    (M = 23,104 pixel rows in the middle flow, so the 256x256 MFMA GEMMs dispatch), one
-    train_visual.py optimiser step: BCE -> backward -> clip_grad_norm_(1.0) -> Adam(lr 1e-5,
-    weight_decay 1e-4) (train_visual.py:533, :575-577; BCE head as XceptionLSTMV.forward).
-    Stores fingerprints only (features, gradient norms, parameters after the step, buffers)."""
+def _checkpoint_blocks(xc):
+    """Recompute each Xception block in backward (torch.utils.checkpoint, non-reentrant) so a
+    256-frame 299^2 step fits in the capture container's memory (the reference's autograd
+    saves ~0.31 GB per frame).  The recompute runs the same CPU ops on the same inputs, so the
+    gradients are those of the plain step; it re-runs the blocks' train-mode BatchNorms, so the
+    running buffers are recorded before backward."""
+    import torch.utils.checkpoint as cp
+    for i in range(1, 13):
+        blk = getattr(xc, f"block{i}")
+        fwd = blk.forward
+        blk.forward = (lambda f: (lambda inp: cp.checkpoint(f, inp, use_reentrant=False)))(fwd)
+
+
+def g_lstmv_big(V, out_dir, B=4, T=16, S=299, labels=(0.0, 1.0, 1.0, 0.0), name="lstmv_b4t16.npz", ckpt=False):
+    """The bench-size kernel set: XceptionLSTMV(128) unfrozen at B*T frames of 299^2 (B4T16:
+    M = 23,104 pixel rows in the middle flow, so the 256x256 MFMA GEMMs dispatch; B16T16: the
+    bench configuration itself, 256 frames, M = 92,416), one train_visual.py optimiser step:
+    BCE -> backward -> clip_grad_norm_(1.0) -> Adam(lr 1e-5, weight_decay 1e-4)
+    (train_visual.py:533, :575-577; BCE head as XceptionLSTMV.forward).  Stores fingerprints
+    only (features, gradient norms, parameters after the step, buffers)."""
     out = {"torch_version": torch.__version__, "B": B, "T": T, "S": S, "seed_w": 0, "seed_x": 4242,
-           "lr": 1e-5, "weight_decay": 1e-4, "max_norm": 1.0}
+           "lr": 1e-5, "weight_decay": 1e-4, "max_norm": 1.0, "labels": np.array(labels[:B])}
     x = seeded_uniform((B, T, 3, S, S), 4242)
-    y = torch.tensor([[0.0], [1.0], [1.0], [0.0]])[:B]
+    y = torch.tensor([[v] for v in labels[:B]])
     torch.manual_seed(0)
     m = V.XceptionLSTMV(128)
     for p in m.feature_extractor.parameters():
         p.requires_grad = True
     m.train()
     m.fc_layers.eval()
+    if ckpt:
+        _checkpoint_blocks(m.feature_extractor)
     store = {}
     m.fc_out.register_forward_hook(_logit_hook(store))
     feats = m.extract_features(x, "cpu")
+    del x
     prob = m(feats)
     loss = nn.BCELoss()(prob, y)
+    bufs = {}
+    for bname, t in m.state_dict().items():
+        if "running_mean" in bname or "running_var" in bname:
+            a = t.double()
+            bufs[f"buf/{bname}/sum"] = a.sum().item()
+            bufs[f"buf/{bname}/sumsq"] = (a * a).sum().item()
     loss.backward()
     put_fp(out, "features", feats)
     out["logits"] = store["logits"].numpy()
     out["loss"] = loss.item()
     grad_norms(out, "gradnorm", m)
+    for hn, p in m.named_parameters():   # head gradients in full (small), for the bf16 head check
+        if hn.startswith(("lstm.bias", "fc_out.")) and p.grad is not None:
+            out[f"grad/{hn}"] = p.grad.numpy()
     params = [p for p in m.parameters() if p.requires_grad]
     out["total_gradnorm"] = torch.nn.utils.clip_grad_norm_(params, 1.0).item()
     opt = torch.optim.Adam(params, lr=1e-5, weight_decay=1e-4)
     opt.step()
     all_param_fp(out, "after_step", m)
-    for name, t in m.state_dict().items():
-        if "running_mean" in name or "running_var" in name:
+    out.update(bufs)
+    np.savez_compressed(os.path.join(out_dir, name), **out)
+
+
+def g_xception_frames(X, out_dir, B, name, ckpt=False):
+    """Configs C1 / C2 (BASELINE.json configs[0], [1]): xception(num_classes=1) trained per frame
+    (Xception.py:205-213), B frames of 299^2, BCEWithLogitsLoss on the logits, Adam(lr 1e-5,
+    weight_decay 1e-4) (the optimiser of train_visual.py:533), no clipping.  Full logits, loss,
+    every gradient norm, every parameter after the step, BatchNorm buffers."""
+    S = 299
+    out = {"torch_version": torch.__version__, "B": B, "S": S, "seed_w": 0, "seed_x": 5151 + B,
+           "lr": 1e-5, "weight_decay": 1e-4}
+    x = seeded_uniform((B, 3, S, S), 5151 + B)
+    y = (torch.arange(B) % 3 == 0).float().view(B, 1)
+    torch.manual_seed(0)
+    m = X.xception(num_classes=1)
+    m.train()
+    if ckpt:
+        _checkpoint_blocks(m)
+    logits = m(x)
+    loss = nn.BCEWithLogitsLoss()(logits, y)
+    bufs = {}
+    for bname, t in m.state_dict().items():
+        if "running_mean" in bname or "running_var" in bname:
             a = t.double()
-            out[f"buf/{name}/sum"] = a.sum().item()
-            out[f"buf/{name}/sumsq"] = (a * a).sum().item()
-    np.savez_compressed(os.path.join(out_dir, "lstmv_b4t16.npz"), **out)
+            bufs[f"buf/{bname}/sum"] = a.sum().item()
+            bufs[f"buf/{bname}/sumsq"] = (a * a).sum().item()
+    loss.backward()
+    out["logits"] = logits.detach().numpy()
+    out["loss"] = loss.item()
+    grad_norms(out, "gradnorm", m)
+    out["grad/fc.weight"] = m.fc.weight.grad.numpy()
+    out["grad/fc.bias"] = m.fc.bias.grad.numpy()
+    out["total_gradnorm"] = torch.sqrt(sum((p.grad.double() ** 2).sum() for p in m.parameters())).item()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-5, weight_decay=1e-4)
+    opt.step()
+    all_param_fp(out, "after_step", m)
+    out.update(bufs)
+    np.savez_compressed(os.path.join(out_dir, name), **out)
 
 
 # ----------------------------------------------------------------------------- script-level defs
@@ -492,6 +551,10 @@ def main():
             "lstm": lambda: g_lstm(args.out), "blocks": lambda: g_blocks(X, args.out),
             "sepconv": lambda: g_sepconv(X, args.out), "audio": lambda: g_audio(A, args.out),
             "lstmv": lambda: g_lstmv(V, args.out), "lstmv_big": lambda: g_lstmv_big(V, args.out),
+            "lstmv_b16t16": lambda: g_lstmv_big(V, args.out, B=16, T=16, labels=tuple(float(i % 2) for i in range(16)),
+                                                name="lstmv_b16t16.npz", ckpt=True),
+            "c1": lambda: g_xception_frames(X, args.out, 4, "xception_c1_b4.npz"),
+            "c2": lambda: g_xception_frames(X, args.out, 64, "xception_c2_b64.npz", ckpt=True),
             "heads": lambda: g_heads(args.out), "arcface_step": lambda: g_arcface_step(V, args.out)}
     for k, fn in jobs.items():
         if args.only and k not in args.only.split(","):
