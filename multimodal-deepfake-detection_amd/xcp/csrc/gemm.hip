@@ -568,6 +568,250 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+// Persistent 256x256 NT kernel: the main loop of gemm_nt256k64_kernel, one workgroup per CU
+// walking its tiles (round r: tile r * grid + its XCD-remapped slot, so each round keeps the
+// A-row sharing of the one-shot kernel).  Per tile the one-shot kernel pays a fixed cost of
+// ~8-15 us at K = 736 (tools/gemm_probe.py: launch boundary, the first K-tile's fill latency and
+// the epilogue's 128 KB of stores, all CUs storing at once) against ~1.55 us per 64-deep
+// K-tile.  Here the next tile's first K-tile is issued BEFORE this tile's epilogue, so its fill
+// runs under the epilogue's conversion and store issue, and the stores drain under the next
+// tile's first K-tile: the counted waits of that K-tile allow the S epilogue stores (issued
+// after the prefetch, before the K-tile-1 loads) to stay in flight; the first wait that needs
+// a K-tile-1 load (phase Q3) retires them.  Every epilogue store is a buffer store whose masked
+// lanes get an out-of-range offset, so each wave issues exactly S store instructions and the
+// counts are exact (a skipped, fully masked store would make a count one short: a race).
+XCP_DEV void vm_wait(int n) {   // s_waitcnt vmcnt(n), n in [0, 31] (folds when n is constant)
+  switch (n < 0 ? 0 : n > 31 ? 31 : n) {
+#define XCP_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    XCP_VMW(0) XCP_VMW(1) XCP_VMW(2) XCP_VMW(3) XCP_VMW(4) XCP_VMW(5) XCP_VMW(6) XCP_VMW(7)
+    XCP_VMW(8) XCP_VMW(9) XCP_VMW(10) XCP_VMW(11) XCP_VMW(12) XCP_VMW(13) XCP_VMW(14) XCP_VMW(15)
+    XCP_VMW(16) XCP_VMW(17) XCP_VMW(18) XCP_VMW(19) XCP_VMW(20) XCP_VMW(21) XCP_VMW(22) XCP_VMW(23)
+    XCP_VMW(24) XCP_VMW(25) XCP_VMW(26) XCP_VMW(27) XCP_VMW(28) XCP_VMW(29) XCP_VMW(30) XCP_VMW(31)
+#undef XCP_VMW
+  }
+}
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+// epilogue256_regs with buffer stores (always issued; OOB offset for masked lanes):
+// 16 C stores per lane, + 1 statistics store when STATS
+template <bool STATS>
+XCP_DEV void epilogue256_buf(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffer_rsrc_t rC,
+                             __amdgpu_buffer_rsrc_t rS, int m0, int n0, int wr, int wc, int fr, int fg) {
+  const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
+  const int mrow = m0 + wr * 128 + fr;
+  const int ncol = n0 + wc * 64;
+  const bool odd = fg & 1;
+  float s1[16], s2[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) s1[q] = s2[q] = 0.f;
+  const int c0 = ncol + (odd ? 16 + (fg - 1) * 4 : fg * 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mrow + i * 16;
+    const bool mok = m < a.M;
+    uint2 pc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x4 q;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) q[r] = (bf16)acc[i][j][r];
+      pc[j] = __builtin_bit_cast(uint2, q);
+      if constexpr (STATS) {   // (branch-free: rows past M add zero)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float f = mok ? (float)q[r] : 0.f;
+          s1[j * 4 + r] += f;
+          s2[j * 4 + r] = fmaf(f, f, s2[j * 4 + r]);
+        }
+      }
+    }
+    const uint2 snd0 = odd ? pc[0] : pc[1], snd1 = odd ? pc[2] : pc[3];
+    uint2 rc0, rc1;
+    rc0.x = __shfl_xor(snd0.x, 16, 64);
+    rc0.y = __shfl_xor(snd0.y, 16, 64);
+    rc1.x = __shfl_xor(snd1.x, 16, 64);
+    rc1.y = __shfl_xor(snd1.y, 16, 64);
+    const uint4 st0 = odd ? make_uint4(rc0.x, rc0.y, pc[1].x, pc[1].y) : make_uint4(pc[0].x, pc[0].y, rc0.x, rc0.y);
+    const uint4 st1 = odd ? make_uint4(rc1.x, rc1.y, pc[3].x, pc[3].y) : make_uint4(pc[2].x, pc[2].y, rc1.x, rc1.y);
+    const unsigned rowb = (unsigned)((long)m * a.ldc * 2);
+    const unsigned o0 = (mok && c0 < a.N) ? rowb + (unsigned)c0 * 2 : BUF_OOB;
+    const unsigned o1 = (mok && c0 + 32 < a.N) ? rowb + (unsigned)(c0 + 32) * 2 : BUF_OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 0);
+  }
+  if constexpr (STATS) {
+    float u[16], v8[8], v4[4], v2[2];
+    const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u[q] = (b3 ? s2[q] : s1[q]) + __shfl_xor(b3 ? s1[q] : s2[q], 8, 64);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v8[q] = (b2 ? u[8 + q] : u[q]) + __shfl_xor(b2 ? u[q] : u[8 + q], 4, 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v4[q] = (b1 ? v8[4 + q] : v8[q]) + __shfl_xor(b1 ? v8[q] : v8[4 + q], 2, 64);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) v2[q] = (b0 ? v4[2 + q] : v4[q]) + __shfl_xor(b0 ? v4[q] : v4[2 + q], 1, 64);
+    const int col = ncol + ((fr & 7) >> 1) * 16 + fg * 4 + (fr & 1) * 2;
+    const int srow = bm * 2 + wr;
+    const unsigned so = (srow < stat_rows && col < a.N) ? (unsigned)((((long)srow * 2 + (fr >> 3)) * a.N + col) * 4)
+                                                        : BUF_OOB;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_float2(v2[0], v2[1])), rS, (int)so, 0, 0);
+  }
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
+  constexpr int S_ST = 16 + (STATS ? 1 : 0);   // store instructions per wave per epilogue
+  __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
+  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
+  const int tiles = gridM * gridN, nwg = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, nwg);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int arow = (w < 4 ? 16 * w : 128 + 16 * (w - 4));
+  const int brow = 64 * (w >> 1) + 16 * (w & 1);
+  const int lr = lane >> 3;
+  int rowt[4][2], kc8[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool isA = (h == 0 || h == 3);
+      rowt[h][i] = (isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0)) + i * 8 + lr;
+      kc8[h][i] = ((lane & 7) ^ ((rowt[h][i] >> 1) & 7)) * 8;
+    }
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, BUF_RECORDS, BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(STATS ? (void*)a.stats : a.C, (short)0,
+                                                                       BUF_RECORDS, BUF_DWORD3);
+  unsigned voff[4][2];
+  auto set_tile = [&](int m0, int n0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool isA = (h == 0 || h == 3);
+        const int r = (isA ? m0 : n0) + rowt[h][i];
+        const bool ok = isA ? r < a.M : r < a.N;
+        voff[h][i] = ok ? (unsigned)(((long)r * (isA ? a.lda : a.ldb) + kc8[h][i]) * 2) : BUF_OOB;
+      }
+  };
+  auto issue = [&](int h, int kt) {
+    const bool isA = (h == 0 || h == 3);
+    const int row0 = isA ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0);
+    char* d = smem + (kt & 1) * K_SLOT + (isA ? 0 : K_OP) + row0 * 128;
+    const int kb = kt * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const unsigned o = kb + kc8[h][i] < a.K ? voff[h][i] + kb * 2 : BUF_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, (__attribute__((address_space(3))) void*)(d + i * 1024),
+                                               16, o, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+  const int nk = (a.K + 63) / 64;
+  const int fr = lane & 15, fg = lane >> 4;
+  bf16x8 af[4][2], bl[2][2], br[2][2];
+  auto mfma_q = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ih * 4 + i][jh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][ks], af[i][ks], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+  };
+  auto sync_mfma = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfma_q(ih, b, jh);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  int t = slot;
+  if (t >= tiles) return;
+  int m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
+  set_tile(m0, n0);
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue(h, 0);
+  int extra = 0;   // epilogue stores of the previous tile still allowed in flight during K-tile 0
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (extra) vm_wait(S_ST);   // K-tile 0 landed (the previous epilogue's stores may still drain)
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+    // one 64-deep K-tile; FIRST (kt == 0): its data was retired by the wait above, so the two
+    // in-tile waits are skipped (they would otherwise also wait for the previous epilogue's stores)
+    auto ktile = [&](int kt, auto first) {
+      const char* sa = smem + (kt & 1) * K_SLOT;
+      const char* sb = sa + K_OP;
+      const bool nxt = kt + 1 < nk;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bl[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + j * 16 + fr, ks * 4 + fg));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 16 + fr, ks * 4 + fg));
+      }
+      if (nxt) issue(0, kt + 1);
+      if constexpr (!decltype(first)::value) wait_cnt(2 + (nxt ? 2 : 0));   // B-right(kt) for Q1
+      sync_mfma(0, bl, 0);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          br[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + 32 + j * 16 + fr, ks * 4 + fg));
+      if (nxt) issue(1, kt + 1);
+      if constexpr (!decltype(first)::value) wait_cnt(nxt ? 4 : 0);         // A-bot(kt) for Q2
+      sync_mfma(0, br, 1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
+      if (nxt) issue(2, kt + 1);
+      sync_mfma(1, br, 1);
+      if (nxt) {
+        issue(3, kt + 1);
+        wait_cnt(4);   // A-top / B-left(kt+1) for Q0(kt+1); also retires the previous epilogue's stores
+      }
+      sync_mfma(1, bl, 0);
+    };
+    ktile(0, IC<1>{});
+    for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
+    if (wr == 0) __builtin_amdgcn_s_barrier();   // every wave is done reading both ring slots
+    const int cm0 = m0, cn0 = n0;
+    t += nwg;
+    const bool more = t < tiles;
+    if (more) {   // the next tile's first K-tile, ahead of this tile's stores
+      m0 = (t / gridN) * 256;
+      n0 = (t % gridN) * 256;
+      set_tile(m0, n0);
+#pragma unroll
+      for (int h = 0; h < 4; ++h) issue(h, 0);
+    }
+    epilogue256_buf<STATS>(acc, a, rC, rS, cm0, cn0, wr, wc, fr, fg);
+    if (!more) break;
+    extra = S_ST;
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // Weight gradient: P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]
 // G: [M][ldg] (output-gradient pixel rows), X: [M][ldx] (layer-input pixel rows).
 // Both operands are pixel-major, so the reduction index m is the slow memory
@@ -932,7 +1176,7 @@ int gpu_cus() {   // compute units of the current device (256 on MI355X)
 
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
-  return tile == 2 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
+  return tile >= 2 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
 }
 
 bool tn_big(int dtype, int gmode, int N, int K, int tile) {
@@ -950,7 +1194,7 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
-  if (tile < 0 || tile > 2) return XCP_EINVAL;
+  if (tile < 0 || tile > 3) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (nt_big(dtype, gmode, M, N, K, tile)) {
     // One 256x256 tile per CU per round.  When the last round would be less than 3/4 full
@@ -960,11 +1204,19 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     const int gridN = xcp_cdiv(N, 256), gridM = xcp_cdiv(M, 256), tiles = gridM * gridN;
     const int cus = gpu_cus();
     int mb = gridM;
-    if (tile == 0 && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3) mb = (tiles / cus) * cus / gridN;
+    if ((tile == 0 || tile == 3) && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3)
+      mb = (tiles / cus) * cus / gridN;
     NTArgs big = a;
     big.M = min(M, mb * 256);
     const bool buf = ((long)(big.M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
-    if (buf)
+    const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
+    if (tile == 3 && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
+      const int grid = min(mb * gridN, cus);
+      if (stats)
+        hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
+      else
+        hipLaunchKernelGGL(gemm_nt256p_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
+    } else if (buf)
       hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(mb * gridN), dim3(512), 0, stream, big);
     else
       hipLaunchKernelGGL(gemm_nt256k64_kernel<false>, dim3(mb * gridN), dim3(512), 0, stream, big);

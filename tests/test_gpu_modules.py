@@ -96,12 +96,17 @@ def test_block_module(gpu, golden, prec):
         torch.cuda.synchronize()
         check_fp(g, f"{name}/out", y.float(), f32)
         check_fp(g, f"{name}/dx", x.grad.float(), f32, rtol=1e-3, min_cos=0.99, flips=0.02 if s != 1 else 0.0)
+        errs = {}
         for n, p in blk.named_parameters():
             key = f"{name}/gradnorm/{n}"
             if key in g:
                 e = abs(p.grad.double().norm().item() - g[key]) / g[key]
-                bn = p.dim() == 1
-                assert e < ((5e-3 if bn else 1e-3) if f32 else (0.2 if bn else 5e-2)), (name, n, e)
+                errs[n] = e
+                if f32:
+                    assert e < (5e-3 if p.dim() == 1 else 1e-3), (name, n, e)
+        if not f32:   # SURVEY 8c's 5e-2 with the measured exceptions (tests/bf16_contract.py)
+            import bf16_contract
+            bf16_contract.check(f"blocks_{name}", errs)
         for n, t in blk.state_dict().items():
             if "running" in n:
                 np.testing.assert_allclose(t.double().sum().item(), g[f"{name}/buf/{n}/sum"],

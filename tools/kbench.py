@@ -67,7 +67,7 @@ def main():
             4 * tensor_bytes)
     if "gemm" in sel:
         st2 = torch.empty(ops.nt_stat_rows(M) * 2 * C, device=dev)
-        for tile in (0, 2, 1):
+        for tile in (0, 2, 3, 1):
             rep(f"gemm_nt 728x728 +stats tile={tile}", timeit(lambda: ops.gemm_nt(X, Wp, Y, M, C, C, stats=st2, tile=tile)),
                 flops=2.0 * M * C * C)
         out = torch.empty(C * C, device=dev)
