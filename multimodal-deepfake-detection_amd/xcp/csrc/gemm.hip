@@ -667,7 +667,7 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
   const int tiles = gridM * gridN, nwg = gridDim.x;
   const int slot = xcd_remap(blockIdx.x, nwg);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: LDS-DMA destinations (M0) from SGPRs
   const int wr = w >> 2, wc = w & 3;
   const int arow = (w < 4 ? 16 * w : 128 + 16 * (w - 4));
   const int brow = 64 * (w >> 1) + 16 * (w & 1);
