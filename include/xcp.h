@@ -91,6 +91,10 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
  * (fp64 sums, fp32 out); accumulate = 1 (G = 1 only): out[l] += that sum (gradient accumulation
  * into param.grad) */
 int xcp_colreduce_f32(const float* in, int S, long L, long ld, float* out, int G, int accumulate, xcp_stream_t stream);
+/* up to 16 column reductions in one launch: jobs = HOST int64 [njobs][7] = (in, out, S, L, ld, G,
+ * accumulate), each as xcp_colreduce_f32 (bitwise the same outputs); L, ld multiples of 4, in /
+ * out 16-B aligned (the backbone backward batches one block's weight-gradient slab reductions) */
+int xcp_colreduce_multi(const long long* jobs, int njobs, xcp_stream_t stream);
 /* slab groups G for the first level of a two-level reduction of S slabs of L floats (0: one pass) */
 int xcp_colreduce_groups(int S, long L);
 int xcp_chanred_parts(long rows, int C);

@@ -30,6 +30,7 @@ SIGNATURES = {
     "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_colreduce_f32": [P, I, L, L, P, I, I, P],
     "xcp_colreduce_groups": [I, L],
+    "xcp_colreduce_multi": [P, I, P],
     "xcp_chanred_parts": [L, I],
     "xcp_row_stats": [I, P, L, I, P, P],
     "xcp_bn_bwd_reduce": [I, P, P, P, P, P, P, L, I, P, P],

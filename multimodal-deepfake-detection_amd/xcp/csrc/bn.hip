@@ -69,6 +69,74 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict_
   }
 }
 
+// Several independent column reductions in one launch (the weight-gradient slab reductions of
+// one backbone block: its pointwise split-K slabs and depthwise partials), jobs passed by value
+// in the kernel arguments.  Each job runs colreduce_kernel's arithmetic (VEC = 4) on its own
+// blocks, so every output is bitwise what the single-job launch gives.
+constexpr int CR_MAXJ = 16;
+struct CRJob {
+  const float* in;
+  float* out;
+  long L, ld;
+  int S, G, acc, blk0, nbx;
+};
+struct CRMulti {
+  CRJob j[CR_MAXJ];
+  int njobs;
+};
+
+__global__ __launch_bounds__(256) void colreduce_multi_kernel(CRMulti m) {
+  __shared__ double red[4][64 * 4];
+  int k = 0;
+#pragma unroll 1
+  while (k + 1 < m.njobs && (int)blockIdx.x >= m.j[k + 1].blk0) ++k;
+  const CRJob jb = m.j[k];
+  const int local = blockIdx.x - jb.blk0;
+  const int g = local / jb.nbx, bx = local - g * jb.nbx;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long col = ((long)bx * 64 + lane) * 4;
+  const int spg = (jb.S + jb.G - 1) / jb.G;
+  const int s0 = g * spg, s1 = min(jb.S, s0 + spg);
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (col < jb.L) {
+    const float* p = jb.in + col;
+    int s = s0 + w;
+    for (; s + 12 < s1; s += 16) {
+      float v[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) VecIO<float, 4>::load(p + (long)(s + 4 * u) * jb.ld, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += (double)v[u][q];
+    }
+    for (; s < s1; s += 4) {
+      float v[4];
+      VecIO<float, 4>::load(p + (long)s * jb.ld, v);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] += (double)v[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[w][lane * 4 + q] = acc[q];
+  __syncthreads();
+  if (w == 0 && col < jb.L) {
+    float v[4], o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = lane * 4 + q;
+      v[q] = (float)(red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+    }
+    float* dst = jb.out + (long)g * jb.L + col;
+    if (jb.acc) {
+      VecIO<float, 4>::load(dst, o);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += o[q];
+    }
+    VecIO<float, 4>::store(dst, v);
+  }
+}
+
 // ---------------------------------------------------------------- per-channel reductions
 // Generic channel-reduction skeleton: block = nch channel chunks x P row chunks;
 // thread (lcv, slot) accumulates CPT channels over rows slot, slot+SPB, ... of its
@@ -823,6 +891,34 @@ int xcp_colreduce_f32(const float* in, int S, long L, long ld, float* out, int G
     if (accumulate) hipLaunchKernelGGL((colreduce_kernel<true, 1>), grid, dim3(256), 0, st, in, S, L, ld, out, G);
     else hipLaunchKernelGGL((colreduce_kernel<false, 1>), grid, dim3(256), 0, st, in, S, L, ld, out, G);
   }
+  return (int)hipGetLastError();
+}
+
+// jobs: HOST int64 [njobs][7] = (in, out, S, L, ld, G, accumulate) -- njobs <= 16 column
+// reductions (each as xcp_colreduce_f32) in one launch; every job needs L % 4 == 0, ld % 4 == 0
+// and 16-B aligned in / out
+int xcp_colreduce_multi(const long long* jobs, int njobs, hipStream_t st) {
+  if (njobs <= 0) return XCP_OK;
+  if (njobs > CR_MAXJ) return XCP_EINVAL;
+  CRMulti m{};
+  int blk = 0, n = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const long long* r = jobs + 7L * i;
+    CRJob j{reinterpret_cast<const float*>(r[0]), reinterpret_cast<float*>(r[1]), (long)r[3], (long)r[4], (int)r[2],
+            (int)r[5], (int)r[6], 0, 0};
+    if (j.L <= 0) continue;
+    if (j.ld < j.L || j.L % 4 || j.ld % 4 || ((uintptr_t)j.in % 16) || ((uintptr_t)j.out % 16)) return XCP_EINVAL;
+    if (j.G > j.S) j.G = j.S;
+    if (j.G < 1) j.G = 1;
+    if (j.acc && j.G != 1) return XCP_EINVAL;
+    j.nbx = (int)((j.L + 255) / 256);
+    j.blk0 = blk;
+    blk += j.nbx * j.G;
+    m.j[n++] = j;
+  }
+  m.njobs = n;
+  if (n == 0) return XCP_OK;
+  hipLaunchKernelGGL(colreduce_multi_kernel, dim3(blk), dim3(256), 0, st, m);
   return (int)hipGetLastError();
 }
 

@@ -117,6 +117,9 @@ STEM_WGRAD_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_STEM_WGRAD_SIDE", "1
 # depthwise weight-gradient slab reductions on the weight-gradient stream (XCP_DW_REDUCE_SIDE=0:
 # on the main stream right after each depthwise backward)
 DW_REDUCE_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_DW_REDUCE_SIDE", "1") != "0"
+# one block's weight-gradient slab reductions batched into one or two launches (XCP_REDUCE_BATCH=0:
+# one launch per weight, as they are produced)
+REDUCE_BATCH = os.environ.get("XCP_REDUCE_BATCH", "1") != "0"
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
 # columns in the packed weights, zero BN scale / shift / backward coefficients.  XCP_PAD_728=0
@@ -452,6 +455,9 @@ class XceptionEngine:
         # backward temporaries unusable and the allocator mapped fresh device memory every step:
         # 140-170 hipMallocs in 20 timed steps and 149 GB reserved for 25.6 GB in use.)
         keep = []
+        # the weight-gradient slab reductions of one block (pointwise split-K slabs, depthwise
+        # partials) go out together in one or two launches when the block is done (REDUCE_BATCH)
+        rbatch = ops.ReduceBatch() if REDUCE_BATCH else None
 
         def wgrad(G, X, M, Nn, K, name, shape, **kw):
             """dW[Nn][K] = G^T X (logical channels; G / X at their channel pitches)"""
@@ -459,15 +465,23 @@ class XceptionEngine:
             kw.setdefault("ldx", pc(K))
             dst, acc = g(name, shape)
             if side is None:
-                ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, **kw)
+                ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, batch=rbatch, **kw)
                 return
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, **kw)
+                ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, batch=rbatch, **kw)
             keep.extend((G, X))   # dst: a gradient, referenced by the caller until the end
 
         def done():
-            """every gradient requested since the last call is enqueued: tell the sink"""
+            """every gradient requested since the last call is enqueued: reduce the block's slabs,
+            tell the sink"""
+            if rbatch is not None and rbatch.jobs:
+                if side is not None:
+                    side.wait_stream(main)   # the depthwise partials come from the main stream
+                    with torch.cuda.stream(side):
+                        rbatch.flush()
+                else:
+                    rbatch.flush()
             if notify is not None and pending:
                 notify(list(pending), side)
             pending.clear()
@@ -512,7 +526,7 @@ class XceptionEngine:
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
                              pc(u.cin), dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, bn_stats=prev_st, accumulate=acc,
                              Cw=u.cin, skip_pre=skip_pre, reduce_stream=side if DW_REDUCE_SIDE else None,
-                             keep=keep)
+                             keep=keep, batch=rbatch)
             return dX, (bnp if prev_st is not None else None)
 
         # ---- exit flow

@@ -122,13 +122,55 @@ def reduce_slabs(P, S, L, out, accumulate=False, ld=None):
         colreduce_f32(P, S, L, out, 1, accumulate, ld=ld)
 
 
-def weight_grad(G, X, M, N, K, out, gather=(0, 0, 0, 0, 0, 1, 0), ldg=None, ldx=None, tile=0, accumulate=False):
-    """out[N][K] (fp32) (+)= G[M][N]^T X[M][K]."""
+class ReduceBatch:
+    """Slab reductions collected and issued together (xcp_colreduce_multi, <= 16 jobs per launch):
+    the engine batches one backbone block's weight-gradient reductions (pointwise split-K slabs,
+    depthwise partials) into one or two launches instead of one or two per weight.  A job that
+    reduce_slabs would split into two levels has its first level in the first launch and its
+    second in the next; outputs are bitwise those of reduce_slabs."""
+
+    def __init__(self):
+        self.jobs = []
+
+    def add(self, P, S, L, out, accumulate=False, ld=None):
+        self.jobs.append((P, S, L, ld or L, out, bool(accumulate)))
+
+    def flush(self):
+        """enqueue every collected reduction on the current stream"""
+        import ctypes
+        if not self.jobs:
+            return
+        dev = self.jobs[0][0].device
+        first, second = [], []
+        for P, S, L, ld, out, acc in self.jobs:
+            g = _lib.call("xcp_colreduce_groups", S, L)
+            if g:
+                tmp = torch.empty(g * L, device=dev, dtype=torch.float32)
+                first.append((P, tmp, S, L, ld, g, 0))
+                second.append((tmp, out, g, L, L, 1, int(acc)))
+            else:
+                first.append((P, out, S, L, ld, 1, int(acc)))
+        for level in (first, second):
+            for i in range(0, len(level), 16):
+                chunk = level[i:i + 16]
+                vals = [v for a, b, S, L, ld, G, acc in chunk for v in (a.data_ptr(), b.data_ptr(), S, L, ld, G, acc)]
+                arr = (ctypes.c_longlong * len(vals))(*vals)
+                _lib.call("xcp_colreduce_multi", ctypes.addressof(arr), len(chunk), stream())
+        self.jobs = []
+
+
+def weight_grad(G, X, M, N, K, out, gather=(0, 0, 0, 0, 0, 1, 0), ldg=None, ldx=None, tile=0, accumulate=False,
+                batch=None):
+    """out[N][K] (fp32) (+)= G[M][N]^T X[M][K].  batch (ReduceBatch): the slab reduction is added
+    to it instead of launched here (the caller flushes it on this stream or one ordered after)."""
     rps = _lib.call("xcp_gemm_tn_rows_per_split", DT[G.dtype], gather[0], M, N, K, tile)
     S = (M + rps - 1) // rps
     P = torch.empty(S * N * K, device=G.device, dtype=torch.float32)
     gemm_tn(G, X, P, M, N, K, S, rps, ldg=ldg, ldx=ldx, gather=gather, tile=tile)
-    reduce_slabs(P, S, N * K, out, accumulate)
+    if batch is not None:
+        batch.add(P, S, N * K, out, accumulate)
+    else:
+        reduce_slabs(P, S, N * K, out, accumulate)
 
 
 # ---------------------------------------------------------------- depthwise
@@ -138,7 +180,7 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
 
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
-           bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None, keep=None):
+           bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None, keep=None, batch=None):
     """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
     (that BN's Stats) is given, else (None, 0).  dW_out receives the weight gradient in the
     nn.Conv2d [C][1][3][3] order (accumulate: added to it); Cw (default C): channels of the
@@ -146,7 +188,9 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
     activation act(X) (it passes the activation mask and enters the BN partial sums).
     reduce_stream: run the weight-gradient slab reduction there (ordered after this launch);
     keep: a list that receives the scratch the reduce stream reads, for a caller that holds it
-    until its stream has waited for the reduce stream (otherwise it is record_stream'ed)."""
+    until its stream has waited for the reduce stream (otherwise it is record_stream'ed);
+    batch (ReduceBatch): the slab reduction is added to it instead (the caller flushes it after
+    ordering its stream behind this launch, and keeps the scratch alive through ``keep``)."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
     bnpart = None
@@ -156,7 +200,11 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
               skip_geom[0], skip_geom[1], skip_geom[2], int(skip_pre), _p(dX), _p(part), _p(bnpart),
               _p(bn_stats["mean"]) if bn_stats is not None else 0,
               _p(bn_stats["invstd"]) if bn_stats is not None else 0, N, H, W, C, stream())
-    if reduce_stream is None:
+    if batch is not None:
+        batch.add(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
+        if keep is not None:
+            keep.append(part)
+    elif reduce_stream is None:
         reduce_slabs(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
     else:
         reduce_stream.wait_stream(torch.cuda.current_stream(dY.device))

@@ -39,6 +39,11 @@ def install_fake_lib(monkeypatch):
         calls.append(name)
         if name == "xcp_colreduce_f32":       # (in, S, L, ld, out, G, accumulate, stream): gradient slabs
             _fill(args[4], args[2] * args[5], args[6])
+        elif name == "xcp_colreduce_multi":   # (jobs [n][7] = in, out, S, L, ld, G, acc; n; stream)
+            jobs = (ctypes.c_longlong * (7 * args[1])).from_address(args[0])
+            for i in range(args[1]):
+                _, out, _, L, _, G, acc = jobs[7 * i:7 * i + 7]
+                _fill(out, L * G, acc)
         elif name == "xcp_bn_bwd_finalize_part" and args[11]:   # dgamma, dbeta (C each)
             _fill(args[11], args[2], args[13])
             _fill(args[12], args[2], args[13])
