@@ -143,6 +143,9 @@ class ReduceBatch:
         dev = self.jobs[0][0].device
         first, second = [], []
         for P, S, L, ld, out, acc in self.jobs:
+            if L % 4 or ld % 4 or P.data_ptr() % 16 or out.data_ptr() % 16:
+                reduce_slabs(P, S, L, out, acc, ld=ld)   # (float4 lanes only in the batched kernel)
+                continue
             g = _lib.call("xcp_colreduce_groups", S, L)
             if g:
                 tmp = torch.empty(g * L, device=dev, dtype=torch.float32)

@@ -735,15 +735,20 @@ def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref):
 def test_reduce_batch_bitwise(ops, gpu):
     """ReduceBatch (xcp_colreduce_multi: up to 16 reductions per launch, two-level jobs split over
     two launches) gives bitwise reduce_slabs' outputs, for one-level and two-level shapes, a slab
-    pitch wider than L, the accumulate form, and more than 16 jobs."""
+    pitch wider than L, the accumulate form, an output off the 16-B grid (reduced on its own),
+    and more than 16 jobs."""
     g = torch.Generator(device=gpu).manual_seed(5)
     shapes = [(14, 736 * 736, None), (300, 728 * 9, 736 * 9), (40, 128 * 9, None), (3, 64, None), (129, 256 * 9, None)]
     shapes = shapes * 4   # 20 jobs: two launches per level
     jobs = []
     for i, (S, L, ld) in enumerate(shapes):
         P = torch.randn(S * (ld or L), device=gpu, generator=g)
-        o0 = torch.randn(L, device=gpu, generator=g)
+        o0 = torch.randn(L + 1, device=gpu, generator=g)
         o1 = o0.clone()
+        if i % 5 == 4:   # an output view off the 16-B grid (a parameter gradient view of a flat buffer)
+            o0, o1 = o0[1:], o1[1:]
+        else:
+            o0, o1 = o0[:L], o1[:L]
         jobs.append((P, S, L, ld, o0, o1, i % 3 == 0))
     rb = ops.ReduceBatch()
     for P, S, L, ld, o0, o1, acc in jobs:
