@@ -132,7 +132,7 @@ __global__ __launch_bounds__(WMW * 128) void gemm_nt_kernel(NTArgs a) {
   const int id = xcd_remap(blockIdx.x, gridM * gridN);
   const int bn = id % gridN, bm = id / gridN;
   const int m0 = bm * BMT, n0 = bn * NBN;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: LDS-DMA destinations (M0) from SGPRs
   const int wm = w >> 1, wn = w & 1;
   const T* A = reinterpret_cast<const T*>(a.A);
   const T* B = reinterpret_cast<const T*>(a.B);
@@ -428,7 +428,7 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   const int id = xcd_remap(blockIdx.x, gridM * gridN);
   const int bn = id % gridN, bm = id / gridN;
   const int m0 = bm * 256, n0 = bn * 256;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: LDS-DMA destinations (M0) from SGPRs
   const int wr = w >> 2, wc = w & 3;
   const bf16* A = reinterpret_cast<const bf16*>(a.A);
   const bf16* B = reinterpret_cast<const bf16*>(a.B);
@@ -1014,7 +1014,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   const int n0 = (t / gridK) * 256, k0 = (t % gridK) * 256;
   const int mbeg = sp * a.rows_per_split;
   const int mend = min(a.M, mbeg + a.rows_per_split);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: LDS-DMA destinations (M0) from SGPRs
   const int wr = w >> 2, wc = w & 3;
   const bf16* G = reinterpret_cast<const bf16*>(a.G);
   const bf16* X = reinterpret_cast<const bf16*>(a.X);
@@ -1176,7 +1176,7 @@ int gpu_cus() {   // compute units of the current device (256 on MI355X)
 
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
-  return tile >= 2 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
+  return tile == 2 || tile == 3 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
 }
 
 bool tn_big(int dtype, int gmode, int N, int K, int tile) {
@@ -1194,9 +1194,12 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
-  if (tile < 0 || tile > 3) return XCP_EINVAL;
+  if (tile < 0 || tile > 4) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (nt_big(dtype, gmode, M, N, K, tile)) {
+    // automatic choice (tile 0): the persistent kernel; tile 4: the automatic choice with the
+    // one-shot kernel (A/B)
+    const bool persist = tile == 3 || tile == 0;
     // One 256x256 tile per CU per round.  When the last round would be less than 3/4 full
     // (1,083 tiles = 4.23 rounds in the middle flow), its rows go to the 128x128 kernel
     // instead: four times as many, smaller tiles, one launch after the full rounds
@@ -1204,13 +1207,13 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     const int gridN = xcp_cdiv(N, 256), gridM = xcp_cdiv(M, 256), tiles = gridM * gridN;
     const int cus = gpu_cus();
     int mb = gridM;
-    if ((tile == 0 || tile == 3) && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3)
+    if (tile != 2 && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3)
       mb = (tiles / cus) * cus / gridN;
     NTArgs big = a;
     big.M = min(M, mb * 256);
     const bool buf = ((long)(big.M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
     const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
-    if (tile == 3 && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
+    if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
       const int grid = min(mb * gridN, cus);
       if (stats)
         hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);

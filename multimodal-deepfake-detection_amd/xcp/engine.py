@@ -120,6 +120,9 @@ DW_REDUCE_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_DW_REDUCE_SIDE", "1")
 # one block's weight-gradient slab reductions batched into one or two launches (XCP_REDUCE_BATCH=0:
 # one launch per weight, as they are produced)
 REDUCE_BATCH = os.environ.get("XCP_REDUCE_BATCH", "1") != "0"
+# XCP_NT_ONESHOT=1: the big pointwise GEMMs on the one-shot 256x256 kernel instead of its
+# persistent form (gemm.hip tile 4 vs 0; A/B)
+NT_TILE = 4 if os.environ.get("XCP_NT_ONESHOT", "0") == "1" else 0
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
 # columns in the packed weights, zero BN scale / shift / backward coefficients.  XCP_PAD_728=0
@@ -283,10 +286,10 @@ class XceptionEngine:
         if train:
             R = ops.nt_stat_rows(M)
             part = self._empty(R * 2 * cop, torch.float32)
-            ops.gemm_nt(A, Wp, Y, M, cop, cip, lda=lda, stats=part, gather=gather)
+            ops.gemm_nt(A, Wp, Y, M, cop, cip, lda=lda, stats=part, gather=gather, tile=NT_TILE)
             st = self._bn_stats(part, R, cout, M, bnmod, True)
         else:
-            ops.gemm_nt(A, Wp, Y, M, cop, cip, lda=lda, gather=gather)
+            ops.gemm_nt(A, Wp, Y, M, cop, cip, lda=lda, gather=gather, tile=NT_TILE)
             st = self._bn_stats(None, 0, cout, M, bnmod, False)
         return Y, st
 
@@ -519,7 +522,7 @@ class XceptionEngine:
                 ops.unit_bwd(dZ, rec["y"], coef, pk[u.name + ".pwT"], rec["d"], dD, M, u.cout, u.cin, dst, acc)
             else:
                 dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
-                ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, pc(u.cin), pc(u.cout))
+                ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, pc(u.cin), pc(u.cout), tile=NT_TILE)
                 wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
             dX = self._empty(M * pc(u.cin))
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
@@ -607,7 +610,7 @@ class XceptionEngine:
                 wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1),
                       gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
             dXs = self._empty(Ms * pc(b.cin))
-            ops.gemm_nt(dYs, pk[b.name + ".skipT"], dXs, Ms, pc(b.cin), pc(b.cout))
+            ops.gemm_nt(dYs, pk[b.name + ".skipT"], dXs, Ms, pc(b.cin), pc(b.cout), tile=NT_TILE)
             if b.stride != 1:
                 dSkip, skip_geom = dXs, (OH, OW, b.stride)
             else:

@@ -1,6 +1,6 @@
 """Interleaved A/B of the NT GEMM variants at the middle-flow shape (M = 256 frames x 19 x 19,
 736-channel pitch, bf16): tile 0 (automatic: one-shot 256x256 + sparse round on 128x128),
-tile 2 (one-shot 256x256 for every row), tile 3 (persistent 256x256 + sparse round), with and
+tile 2 (one-shot 256x256 for every row), tile 3 (persistent 256x256 + sparse round; tile 0 is now this), tile 4 (the automatic choice with the one-shot kernel), with and
 without the BN-statistics epilogue.  Rounds alternate variants in one process (rule 24).
 
 usage (GPU box): python tools/gemm_ab.py [rounds]
@@ -40,7 +40,7 @@ def main():
     C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     st = torch.empty(ops.nt_stat_rows(M) * 2 * N, device=dev)
     fl = 2.0 * M * 728 * 728
-    variants = {f"tile{t}{'+stats' if s else ''}": (t, s) for t in (0, 2, 3) for s in (True, False)}
+    variants = {f"tile{t}{'+stats' if s else ''}": (t, s) for t in (0, 4, 2, 3) for s in (True, False)}
     res = {k: [] for k in variants}
     for _ in range(rounds):
         for k, (t, s) in variants.items():

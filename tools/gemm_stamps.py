@@ -66,7 +66,7 @@ def run():
     lib.xcp_gemm_nt.argtypes = _lib.SIGNATURES["xcp_gemm_nt"]
     lib.xcp_gemm_nt.restype = ctypes.c_int
     lib.xcp_set_stamps.argtypes = [ctypes.c_void_p]
-    M, C = 256 * 361, 736
+    M, C = int(os.environ.get("STAMP_M", 256 * 361)), 736
     g = torch.Generator(device=dev).manual_seed(0)
     A = torch.randn(M, C, device=dev, generator=g).bfloat16()
     B = (torch.randn(C, C, device=dev, generator=g) / 27).bfloat16()
