@@ -812,6 +812,152 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+// 4-wave 256x256 NT kernel: one wave per SIMD, wave tile 128x128 (8 x 8 MFMA 16x16x32 tiles,
+// 256 fp32 accumulators per lane, held in AGPRs).  Against the 8-wave kernel (wave tile
+// 128x64): 2/3 of the LDS fragment bytes per flop (128 vs 192 KB per 64-deep K-tile per CU)
+// and one barrier per K-tile instead of eight.  The wave has no SIMD partner to hide its LDS
+// latency, so its reads run ahead of the MFMAs: a K-tile is 16 groups g = (k-step, m-fragment)
+// of 8 MFMAs; the A fragment of group g is read two groups ahead, the 8 B fragments of the next
+// k-step one per group during the current one (registers: 2 x 8 B fragments + 3 A fragments).
+// LDS: A(kt) in slot kt mod 3 of an A ring, B(kt) in slot kt mod 2 of a B ring (5 x 32 KB).
+// One barrier per K-tile, between its two k-steps: before it every wave has read all of B(kt)
+// and A(kt-1) (lgkmcnt(0)) and holds A(kt+1) / B(kt+1) (vmcnt(0): they were issued one K-tile
+// earlier); after it A(kt+2) / B(kt+2) are issued into those two freed slots.
+constexpr int NT4_SLOT = 256 * 128;
+
+// v_mfma_f32_16x16x32_bf16 with the accumulator pinned to AGPRs (an inline-asm operand
+// constraint): with 256 accumulators per lane the register allocator otherwise splits them over
+// VGPRs and AGPRs and copies them around the loop.  srcA = b, srcB = a, as the builtin calls above.
+XCP_DEV void mfma_agpr(f32x4& c, const bf16x8& b, const bf16x8& a) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(b), "v"(a));
+}
+
+
+template <int EARLY>
+__global__ __launch_bounds__(256) void gemm_nt4w_kernel(NTArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[5 * NT4_SLOT];   // A ring: slots 0-2, B ring: 3-4
+  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
+  const int id = xcd_remap(blockIdx.x, gridM * gridN);
+  const int bn = id % gridN, bm = id / gridN;
+  const int m0 = bm * 256, n0 = bn * 256;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  // LDS-DMA: an operand tile is 256 rows x 128 B; instruction i of wave w fills rows (4i + w) * 8
+  // + [0, 8), lane l the 16-B physical chunk l & 7 of row (4i + w) * 8 + (l >> 3), i.e. logical
+  // chunk (l & 7) ^ ((row >> 1) & 7) -- the same for every i
+  const int lrow = w * 8 + (lane >> 3);
+  const int kc8 = ((lane & 7) ^ ((lrow >> 1) & 7)) * 8;
+  unsigned voA[8], voB[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = lrow + 32 * i;
+    voA[i] = m0 + row < a.M ? (unsigned)(((long)(m0 + row) * a.lda + kc8) * 2) : BUF_OOB;
+    voB[i] = n0 + row < a.N ? (unsigned)(((long)(n0 + row) * a.ldb + kc8) * 2) : BUF_OOB;
+  }
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  auto slotA = [&](int kt) { return smem + (kt % 3) * NT4_SLOT; };
+  auto slotB = [&](int kt) { return smem + (3 + (kt & 1)) * NT4_SLOT; };
+  // LDS-DMA instructions i0, i0 + 1 of operand op (0: A, 1: B) of K-tile kt; past the last
+  // K-tile the offsets are out of range and the slot (free by then) is zero-filled
+  auto issue_part = [&](int op, int kt, int i0) {
+    char* d = (op ? slotB(kt) : slotA(kt)) + w * 1024;
+    const int kb = kt * 64;
+    const unsigned lim = kb + kc8 < a.K ? 0u : BUF_OOB;   // columns past K: out of range (zeros)
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i) {
+      const unsigned o = ((op ? voB[i] : voA[i]) + kb * 2) | lim;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? rB : rA, (__attribute__((address_space(3))) void*)(d + i * 4096),
+                                               16, o, 0, 0, 0);
+    }
+  };
+  auto issue = [&](int op, int kt) {
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) issue_part(op, kt, i);
+  };
+
+  f32x4 acc[2][8][4];   // [n half][m frag][n frag]: C[m0 + wr*128 + 16i + fr][n0 + wc*128 + 64h + 16j + 4fg + r]
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  // fragment (row r of a 128-row wave half, k-step ks) of an operand slot
+  const int aoff = wr * 128 * 128, boff = wc * 128 * 128;
+  auto frag = [&](const char* s, int off, int i, int ks) {
+    return *reinterpret_cast<const bf16x8*>(s + off + swz(i * 16 + fr, ks * 4 + fg));
+  };
+
+  const int nk = (a.K + 63) / 64;
+  issue(0, 0);
+  issue(1, 0);
+  issue(0, 1);
+  issue(1, 1);
+  vm_wait(16);   // A(0), B(0) landed
+  __builtin_amdgcn_s_barrier();
+  bf16x8 fb0[8], fa_n0, fa_n1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb0[j] = frag(slotB(0), boff, j, 0);
+  fa_n0 = frag(slotA(0), aoff, 0, 0);
+  fa_n1 = frag(slotA(0), aoff, 1, 0);
+  // group order is fixed with sched_barrier: each group's reads are issued before the MFMAs of the
+  // group two (A) / one (B) behind them, so the waits the compiler inserts are counted ones
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* sa = slotA(kt);
+    const char* sb = slotB(kt);
+    bf16x8 fa[18], fb1[8];
+    fa[0] = fa_n0;
+    fa[1] = fa_n1;
+    // k-step 0: MFMAs on fb0; B fragments of k-step 1 and A fragments two groups ahead
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      fa[g + 2] = frag(sa, aoff, (g + 2) & 7, (g + 2) >> 3);
+      fb1[g] = frag(sb, boff, g, 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mfma_agpr(acc[j >> 2][g][j & 3], fb0[j], fa[g]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // B(kt) and A(kt-1) fully read by this wave
+    wait_vmcnt<0>();                                     // A(kt+1), B(kt+1) landed
+    __builtin_amdgcn_s_barrier();
+    if constexpr (EARLY) {
+      issue(0, kt + 2);
+      issue(1, kt + 2);
+    }
+    // k-step 1: MFMAs on fb1; the LDS-DMA issues of A(kt+2) / B(kt+2) (two per group), B fragments
+    // of K-tile kt+1's k-step 0, and A fragments two groups ahead (the last two from A(kt+1))
+    const char* sa1 = slotA(kt + 1);
+    const char* sb1 = slotB(kt + 1);
+#pragma unroll
+    for (int g = 8; g < 16; ++g) {
+      if constexpr (!EARLY) issue_part(g < 12 ? 0 : 1, kt + 2, (g & 3) * 2);
+      fa[g + 2] = g + 2 < 16 ? frag(sa, aoff, (g + 2) & 7, 1) : frag(sa1, aoff, g - 14, 0);
+      fb0[g - 8] = frag(sb1, boff, g - 8, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mfma_agpr(acc[j >> 2][g - 8][j & 3], fb1[j], fa[g]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    fa_n0 = fa[16];
+    fa_n1 = fa[17];
+    // a real s_waitcnt (not inline asm), so the compiler's wait counting starts the next K-tile
+    // from zero reads in flight instead of a full drain after its first group's reads
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+  }
+  wait_vmcnt<0>();   // the zero-filling issues past the last K-tile
+  // the epilogue's accumulator reads follow inline-asm MFMAs the hazard recognizer cannot see:
+  // cover the last MFMA's passes explicitly
+  asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
+  epilogue256_regs(acc[0], a, m0, n0, wr, wc * 2, fr, fg);
+  epilogue256_regs(acc[1], a, m0, n0, wr, wc * 2 + 1, fr, fg);
+}
+
+// ---------------------------------------------------------------------------------
 // Weight gradient: P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]
 // G: [M][ldg] (output-gradient pixel rows), X: [M][ldx] (layer-input pixel rows).
 // Both operands are pixel-major, so the reduction index m is the slow memory
@@ -1176,7 +1322,7 @@ int gpu_cus() {   // compute units of the current device (256 on MI355X)
 
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
-  return tile == 2 || tile == 3 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
+  return tile == 2 || tile == 3 || tile >= 5 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
 }
 
 bool tn_big(int dtype, int gmode, int N, int K, int tile) {
@@ -1194,7 +1340,7 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
-  if (tile < 0 || tile > 4) return XCP_EINVAL;
+  if (tile < 0 || tile > 6) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (nt_big(dtype, gmode, M, N, K, tile)) {
     // automatic choice (tile 0): the persistent kernel; tile 4: the automatic choice with the
@@ -1213,7 +1359,9 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     big.M = min(M, mb * 256);
     const bool buf = ((long)(big.M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
     const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
-    if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
+    if (tile >= 5 && buf)   // 4-wave kernel, one wave per SIMD
+      hipLaunchKernelGGL(tile == 5 ? gemm_nt4w_kernel<1> : gemm_nt4w_kernel<0>, dim3(mb * gridN), dim3(256), 0, stream, big);
+    else if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
       const int grid = min(mb * gridN, cus);
       if (stats)
         hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
