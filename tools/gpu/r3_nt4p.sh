@@ -1,0 +1,11 @@
+# Round 3: the 4-wave persistent NT kernel (tile 5): GEMM parity tests (incl. bitwise vs the
+# one-shot kernel), the interleaved A/B at the middle-flow shape, the fixed-cost probe.
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  -k "gemm_nt256 or persistent_bitwise or gemm_nt_stats" > gpurun_out/nt4p_t.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/nt4p_t.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 300 python -u tools/gemm_ab.py 5 > gpurun_out/nt4p_ab.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/gemm_probe.py 2 5 > gpurun_out/nt4p_probe.log 2>&1
