@@ -343,12 +343,10 @@ XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n
   float s1[16], s2[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) s1[q] = s2[q] = 0.f;
-  // FULL: every row of the tile is below M (all but the last row tile), so no row mask is formed
-  auto rows = [&](auto FULL) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = mrow + i * 16;
-    const bool mok = FULL ? true : m < a.M;
+    const bool mok = m < a.M;
     uint2 pc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -378,9 +376,6 @@ XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n
     if (mok && c0 < a.N) *reinterpret_cast<uint4*>(crow + c0) = st0;
     if (mok && c0 + 32 < a.N) *reinterpret_cast<uint4*>(crow + c0 + 32) = st1;
   }
-  };
-  if (m0 + 256 <= a.M) rows(IC<1>{});
-  else rows(IC<0>{});
   if (a.stats) {
     // reduce-scatter of v[32] = (s1[16], s2[16]) over the 16 row lanes
     float u[16], v8[8], v4[4], v2[2];
@@ -616,7 +611,7 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // epilogue256_regs with buffer stores (always issued; OOB offset for masked lanes):
 // 16 C stores per lane, + 1 statistics store when STATS
-template <bool STATS, typename Get>
+template <bool STATS, bool SPLIT = false, typename Get>
 XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC, __amdgpu_buffer_rsrc_t rS, int m0,
                              int n0, int wr, int wc, int fr, int fg) {
   const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
@@ -627,7 +622,8 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
 #pragma unroll
   for (int q = 0; q < 16; ++q) s1[q] = s2[q] = 0.f;
   const int c0 = ncol + (odd ? 16 + (fg - 1) * 4 : fg * 4);
-  // FULL: every row of the tile is below M (all but the last row tile), so no row mask is formed
+  // SPLIT (4-wave kernel): a FULL copy for row tiles wholly below M, which forms no row mask (in
+  // the 8-wave kernels the second copy costs spilled registers)
   auto rows = [&](auto FULL) {
   static_for<0, 8>([&](auto i) {   // (compile-time indices: the 4-wave kernel's acc() names AGPRs)
     const int m = mrow + i * 16;
@@ -661,7 +657,7 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 0);
   });
   };
-  if (m0 + 256 <= a.M) rows(IC<1>{});
+  if (SPLIT && m0 + 256 <= a.M) rows(IC<SPLIT>{});
   else rows(IC<0>{});
   if constexpr (STATS) {
     float u[16], v8[8], v4[4], v2[2];
@@ -1405,8 +1401,8 @@ __global__ __launch_bounds__(256) void gemm_nt4p_kernel(NTArgs a) {
                           decltype(r)::value>();
         };
       };
-      epilogue256_get<STATS>(rd(IC<0>{}), a, rC, rS, m0, n0, wr, wc * 2, fr, fg);
-      epilogue256_get<STATS>(rd(IC<1>{}), a, rC, rS, m0, n0, wr, wc * 2 + 1, fr, fg);
+      epilogue256_get<STATS, true>(rd(IC<0>{}), a, rC, rS, m0, n0, wr, wc * 2, fr, fg);
+      epilogue256_get<STATS, true>(rd(IC<1>{}), a, rC, rS, m0, n0, wr, wc * 2 + 1, fr, fg);
       kt = 0;
       t += nwg;
       m0 = (t / gridN) * 256;

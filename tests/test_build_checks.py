@@ -17,3 +17,11 @@ def test_nt4p_accumulators_stay_in_named_agprs():
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "check_nt4p_regs.py")], capture_output=True,
                        text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc") and not shutil.which("hipcc"), reason="hipcc absent")
+def test_hot_kernels_do_not_spill():
+    """No scratch (spilled registers) in the hot kernels: GEMMs, depthwise, fused unit backward,
+    BN-backward apply (tools/check_spills.py)."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "check_spills.py")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -1,0 +1,56 @@
+"""Register-spill census of every kernel in csrc/*.hip (gfx950): compiles each source with
+-Rpass-analysis=kernel-resource-usage and lists kernels with scratch use.  A spill in a hot kernel
+is a silent slowdown (an epilogue change once added 44 spilled VGPRs to the persistent NT kernel);
+tests/test_build_checks.py asserts that the kernels listed in HOT have none.
+
+usage: python tools/check_spills.py
+"""
+import concurrent.futures as cf
+import os
+import re
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(HERE), "multimodal-deepfake-detection_amd", "xcp", "csrc")
+HOT = ("gemm_nt256k64_kernel", "gemm_nt256p_kernel", "gemm_nt4p_kernel", "gemm_tn256_kernel", "gemm_nt_kernel",
+       "dw_fwd_kernel", "dw_bwd_lds_kernel", "unit_bwd_kernel", "bn_bwd_apply_kernel")
+
+
+def census(src):
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
+                        "-S", src, "-o", os.devnull, "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True)
+    out = {}
+    name = None
+    for line in r.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            out[name] = {}
+            continue
+        m = re.search(r"remark:\s+(VGPRs Spill|ScratchSize \[bytes/lane\]|VGPRs|AGPRs): (\d+)", line)
+        if m and name:
+            out[name][m.group(1)] = int(m.group(2))
+    return out
+
+
+def main():
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    with cf.ThreadPoolExecutor(8) as ex:
+        res = {}
+        for d in ex.map(census, srcs):
+            res.update(d)
+    bad = []
+    for k, v in sorted(res.items()):
+        sc = v.get("ScratchSize [bytes/lane]", 0)
+        if sc:
+            hot = any(h in k for h in HOT)
+            print(f"{'HOT ' if hot else '    '}{k[:90]:90s} VGPRs {v.get('VGPRs')} spill {v.get('VGPRs Spill')} scratch {sc}")
+            if hot:
+                bad.append(k)
+    print(f"{len(res)} kernels, {len(bad)} hot kernels with scratch")
+    return not bad
+
+
+if __name__ == "__main__":
+    sys.exit(0 if main() else 1)
