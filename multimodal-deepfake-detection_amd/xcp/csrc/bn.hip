@@ -298,17 +298,22 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, in
                         double& s1) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = c0 + (lane & 31), stat = lane >> 5;
-  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  // rows w, w + 16, ... in chunks of FIN_U: every load of a chunk is issued before the first is
+  // added (clamped row, zero-selected past R), so a lane waits ceil(R / (16 FIN_U)) memory round
+  // trips, not one per 4 rows (722 partial rows of the middle flow: 3 instead of 12)
+  constexpr int FIN_U = 16;
+  double a = 0.0;
   if (c < C) {
     const float* col = part + (long)stat * CP + c;
-    int r = w;
-    for (; r + 3 * FIN_WAVES < R; r += 4 * FIN_WAVES) {
+    for (int r0 = w; r0 < R; r0 += FIN_U * FIN_WAVES) {
+      float v[FIN_U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] += (double)col[(long)(r + u * FIN_WAVES) * 2 * CP];
+      for (int u = 0; u < FIN_U; ++u) v[u] = col[(long)min(r0 + u * FIN_WAVES, R - 1) * 2 * CP];
+#pragma unroll
+      for (int u = 0; u < FIN_U; ++u) a += r0 + u * FIN_WAVES < R ? (double)v[u] : 0.0;
     }
-    for (; r < R; r += FIN_WAVES) a[0] += (double)col[(long)r * 2 * CP];
   }
-  red[w][lane] = (a[0] + a[1]) + (a[2] + a[3]);
+  red[w][lane] = a;
   __syncthreads();
   s0 = s1 = 0.0;
   if (threadIdx.x < FIN_CH) {

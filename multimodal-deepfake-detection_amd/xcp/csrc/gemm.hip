@@ -611,7 +611,7 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // epilogue256_regs with buffer stores (always issued; OOB offset for masked lanes):
 // 16 C stores per lane, + 1 statistics store when STATS
-template <bool STATS, bool SPLIT = false, typename Get>
+template <bool STATS, typename Get>
 XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC, __amdgpu_buffer_rsrc_t rS, int m0,
                              int n0, int wr, int wc, int fr, int fg) {
   const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
@@ -622,12 +622,9 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
 #pragma unroll
   for (int q = 0; q < 16; ++q) s1[q] = s2[q] = 0.f;
   const int c0 = ncol + (odd ? 16 + (fg - 1) * 4 : fg * 4);
-  // SPLIT (4-wave kernel): a FULL copy for row tiles wholly below M, which forms no row mask (in
-  // the 8-wave kernels the second copy costs spilled registers)
-  auto rows = [&](auto FULL) {
-  static_for<0, 8>([&](auto i) {   // (compile-time indices: the 4-wave kernel's acc() names AGPRs)
+  static_for<0, 8>([&](auto i) {
     const int m = mrow + i * 16;
-    const bool mok = FULL ? true : m < a.M;
+    const bool mok = m < a.M;
     uint2 pc[4];
     static_for<0, 4>([&](auto j) {
       bf16x4 q;
@@ -656,9 +653,6 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 0);
   });
-  };
-  if (SPLIT && m0 + 256 <= a.M) rows(IC<SPLIT>{});
-  else rows(IC<0>{});
   if constexpr (STATS) {
     float u[16], v8[8], v4[4], v2[2];
     const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
@@ -833,589 +827,6 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
     if (!more) break;
     extra = S_ST;
   }
-}
-
-// ---------------------------------------------------------------------------------
-// 4-wave persistent 256x256 NT kernel: one wave per SIMD, wave tile 128x128 (8 x 8 MFMA 16x16x32
-// tiles, 256 fp32 accumulators per lane, held in AGPRs), one workgroup per CU walking its tiles.
-// Against the 8-wave kernel (wave tile 128x64): 2/3 of the LDS fragment bytes per flop and one
-// barrier per K-tile instead of eight; measured in-kernel (tools/gemm_stamps4.py) its K-loop does
-// not slow down when every CU fills at once, so what is left per tile is the fill of the first
-// K-tile and the epilogue's stores -- both taken off the critical path here:
-//  * the LDS-DMA stream is continuous across tiles: K-tiles are counted per workgroup (G), A(G)
-//    lives in slot G mod 3 of an A ring and B(G) in slot G mod 2 of a B ring (5 x 32 KB), and the
-//    issues of K-tile kt+2 past the tile's last K-tile fetch the next tile's first two K-tiles;
-//  * the epilogue's 32 (+2 statistics) buffer stores are always issued (out-of-range offsets for
-//    masked lanes), so the next tile's first middle wait counts them exactly (vmcnt(S)) and they
-//    drain under its first K-tile; the accumulators restart from the MFMA's zero C operand.
-// A K-tile is 16 groups g = (k-step, m-fragment) of 8 MFMAs; the A fragment of group g is read two
-// groups ahead, the 8 B fragments of the next k-step one per group during the current one.  The
-// barrier between its two k-steps is the only one: before it every wave has read B(G) and A(G-1)
-// (lgkmcnt(0)) and holds A(G+1) / B(G+1); after it the A(G+2) / B(G+2) issues overwrite those two
-// freed slots, one LDS-DMA instruction per 4 MFMAs.  Needs K > 64 (two K-tiles per tile).
-constexpr int NT4_SLOT = 256 * 128;
-
-// The 4-wave kernel's 256 accumulators per lane live in fixed AGPRs a0-a255 (tile T = 32h + 4i + j
-// in a[4T : 4T+3]), named in the inline-asm MFMAs and reads below (with the registers as clobbers,
-// which is also how the kernel's AGPR count is accounted).  As C++ values of an asm "a" operand the
-// register allocator kept copies of them in VGPRs around the tile loop and spilled; named registers
-// take them out of its hands.  The compiler's own code must then never need an AGPR: the kernel
-// keeps its VGPR use far below 256 (no VGPR -> AGPR spill), checked at build time
-// (tools/check_nt4p_regs.py).  ZERO: C = 0 (a tile's first k-step) instead of the accumulator.
-template <bool ZERO, int t>
-XCP_DEV void mfma_fixed(const bf16x8& b, const bf16x8& a) {
-  if constexpr (ZERO) {
-    switch (t) {
-      case 0: asm volatile("v_mfma_f32_16x16x32_bf16 a[0:3], %0, %1, 0" :: "v"(b), "v"(a) : "a0", "a1", "a2", "a3"); break;
-      case 1: asm volatile("v_mfma_f32_16x16x32_bf16 a[4:7], %0, %1, 0" :: "v"(b), "v"(a) : "a4", "a5", "a6", "a7"); break;
-      case 2: asm volatile("v_mfma_f32_16x16x32_bf16 a[8:11], %0, %1, 0" :: "v"(b), "v"(a) : "a8", "a9", "a10", "a11"); break;
-      case 3: asm volatile("v_mfma_f32_16x16x32_bf16 a[12:15], %0, %1, 0" :: "v"(b), "v"(a) : "a12", "a13", "a14", "a15"); break;
-      case 4: asm volatile("v_mfma_f32_16x16x32_bf16 a[16:19], %0, %1, 0" :: "v"(b), "v"(a) : "a16", "a17", "a18", "a19"); break;
-      case 5: asm volatile("v_mfma_f32_16x16x32_bf16 a[20:23], %0, %1, 0" :: "v"(b), "v"(a) : "a20", "a21", "a22", "a23"); break;
-      case 6: asm volatile("v_mfma_f32_16x16x32_bf16 a[24:27], %0, %1, 0" :: "v"(b), "v"(a) : "a24", "a25", "a26", "a27"); break;
-      case 7: asm volatile("v_mfma_f32_16x16x32_bf16 a[28:31], %0, %1, 0" :: "v"(b), "v"(a) : "a28", "a29", "a30", "a31"); break;
-      case 8: asm volatile("v_mfma_f32_16x16x32_bf16 a[32:35], %0, %1, 0" :: "v"(b), "v"(a) : "a32", "a33", "a34", "a35"); break;
-      case 9: asm volatile("v_mfma_f32_16x16x32_bf16 a[36:39], %0, %1, 0" :: "v"(b), "v"(a) : "a36", "a37", "a38", "a39"); break;
-      case 10: asm volatile("v_mfma_f32_16x16x32_bf16 a[40:43], %0, %1, 0" :: "v"(b), "v"(a) : "a40", "a41", "a42", "a43"); break;
-      case 11: asm volatile("v_mfma_f32_16x16x32_bf16 a[44:47], %0, %1, 0" :: "v"(b), "v"(a) : "a44", "a45", "a46", "a47"); break;
-      case 12: asm volatile("v_mfma_f32_16x16x32_bf16 a[48:51], %0, %1, 0" :: "v"(b), "v"(a) : "a48", "a49", "a50", "a51"); break;
-      case 13: asm volatile("v_mfma_f32_16x16x32_bf16 a[52:55], %0, %1, 0" :: "v"(b), "v"(a) : "a52", "a53", "a54", "a55"); break;
-      case 14: asm volatile("v_mfma_f32_16x16x32_bf16 a[56:59], %0, %1, 0" :: "v"(b), "v"(a) : "a56", "a57", "a58", "a59"); break;
-      case 15: asm volatile("v_mfma_f32_16x16x32_bf16 a[60:63], %0, %1, 0" :: "v"(b), "v"(a) : "a60", "a61", "a62", "a63"); break;
-      case 16: asm volatile("v_mfma_f32_16x16x32_bf16 a[64:67], %0, %1, 0" :: "v"(b), "v"(a) : "a64", "a65", "a66", "a67"); break;
-      case 17: asm volatile("v_mfma_f32_16x16x32_bf16 a[68:71], %0, %1, 0" :: "v"(b), "v"(a) : "a68", "a69", "a70", "a71"); break;
-      case 18: asm volatile("v_mfma_f32_16x16x32_bf16 a[72:75], %0, %1, 0" :: "v"(b), "v"(a) : "a72", "a73", "a74", "a75"); break;
-      case 19: asm volatile("v_mfma_f32_16x16x32_bf16 a[76:79], %0, %1, 0" :: "v"(b), "v"(a) : "a76", "a77", "a78", "a79"); break;
-      case 20: asm volatile("v_mfma_f32_16x16x32_bf16 a[80:83], %0, %1, 0" :: "v"(b), "v"(a) : "a80", "a81", "a82", "a83"); break;
-      case 21: asm volatile("v_mfma_f32_16x16x32_bf16 a[84:87], %0, %1, 0" :: "v"(b), "v"(a) : "a84", "a85", "a86", "a87"); break;
-      case 22: asm volatile("v_mfma_f32_16x16x32_bf16 a[88:91], %0, %1, 0" :: "v"(b), "v"(a) : "a88", "a89", "a90", "a91"); break;
-      case 23: asm volatile("v_mfma_f32_16x16x32_bf16 a[92:95], %0, %1, 0" :: "v"(b), "v"(a) : "a92", "a93", "a94", "a95"); break;
-      case 24: asm volatile("v_mfma_f32_16x16x32_bf16 a[96:99], %0, %1, 0" :: "v"(b), "v"(a) : "a96", "a97", "a98", "a99"); break;
-      case 25: asm volatile("v_mfma_f32_16x16x32_bf16 a[100:103], %0, %1, 0" :: "v"(b), "v"(a) : "a100", "a101", "a102", "a103"); break;
-      case 26: asm volatile("v_mfma_f32_16x16x32_bf16 a[104:107], %0, %1, 0" :: "v"(b), "v"(a) : "a104", "a105", "a106", "a107"); break;
-      case 27: asm volatile("v_mfma_f32_16x16x32_bf16 a[108:111], %0, %1, 0" :: "v"(b), "v"(a) : "a108", "a109", "a110", "a111"); break;
-      case 28: asm volatile("v_mfma_f32_16x16x32_bf16 a[112:115], %0, %1, 0" :: "v"(b), "v"(a) : "a112", "a113", "a114", "a115"); break;
-      case 29: asm volatile("v_mfma_f32_16x16x32_bf16 a[116:119], %0, %1, 0" :: "v"(b), "v"(a) : "a116", "a117", "a118", "a119"); break;
-      case 30: asm volatile("v_mfma_f32_16x16x32_bf16 a[120:123], %0, %1, 0" :: "v"(b), "v"(a) : "a120", "a121", "a122", "a123"); break;
-      case 31: asm volatile("v_mfma_f32_16x16x32_bf16 a[124:127], %0, %1, 0" :: "v"(b), "v"(a) : "a124", "a125", "a126", "a127"); break;
-      case 32: asm volatile("v_mfma_f32_16x16x32_bf16 a[128:131], %0, %1, 0" :: "v"(b), "v"(a) : "a128", "a129", "a130", "a131"); break;
-      case 33: asm volatile("v_mfma_f32_16x16x32_bf16 a[132:135], %0, %1, 0" :: "v"(b), "v"(a) : "a132", "a133", "a134", "a135"); break;
-      case 34: asm volatile("v_mfma_f32_16x16x32_bf16 a[136:139], %0, %1, 0" :: "v"(b), "v"(a) : "a136", "a137", "a138", "a139"); break;
-      case 35: asm volatile("v_mfma_f32_16x16x32_bf16 a[140:143], %0, %1, 0" :: "v"(b), "v"(a) : "a140", "a141", "a142", "a143"); break;
-      case 36: asm volatile("v_mfma_f32_16x16x32_bf16 a[144:147], %0, %1, 0" :: "v"(b), "v"(a) : "a144", "a145", "a146", "a147"); break;
-      case 37: asm volatile("v_mfma_f32_16x16x32_bf16 a[148:151], %0, %1, 0" :: "v"(b), "v"(a) : "a148", "a149", "a150", "a151"); break;
-      case 38: asm volatile("v_mfma_f32_16x16x32_bf16 a[152:155], %0, %1, 0" :: "v"(b), "v"(a) : "a152", "a153", "a154", "a155"); break;
-      case 39: asm volatile("v_mfma_f32_16x16x32_bf16 a[156:159], %0, %1, 0" :: "v"(b), "v"(a) : "a156", "a157", "a158", "a159"); break;
-      case 40: asm volatile("v_mfma_f32_16x16x32_bf16 a[160:163], %0, %1, 0" :: "v"(b), "v"(a) : "a160", "a161", "a162", "a163"); break;
-      case 41: asm volatile("v_mfma_f32_16x16x32_bf16 a[164:167], %0, %1, 0" :: "v"(b), "v"(a) : "a164", "a165", "a166", "a167"); break;
-      case 42: asm volatile("v_mfma_f32_16x16x32_bf16 a[168:171], %0, %1, 0" :: "v"(b), "v"(a) : "a168", "a169", "a170", "a171"); break;
-      case 43: asm volatile("v_mfma_f32_16x16x32_bf16 a[172:175], %0, %1, 0" :: "v"(b), "v"(a) : "a172", "a173", "a174", "a175"); break;
-      case 44: asm volatile("v_mfma_f32_16x16x32_bf16 a[176:179], %0, %1, 0" :: "v"(b), "v"(a) : "a176", "a177", "a178", "a179"); break;
-      case 45: asm volatile("v_mfma_f32_16x16x32_bf16 a[180:183], %0, %1, 0" :: "v"(b), "v"(a) : "a180", "a181", "a182", "a183"); break;
-      case 46: asm volatile("v_mfma_f32_16x16x32_bf16 a[184:187], %0, %1, 0" :: "v"(b), "v"(a) : "a184", "a185", "a186", "a187"); break;
-      case 47: asm volatile("v_mfma_f32_16x16x32_bf16 a[188:191], %0, %1, 0" :: "v"(b), "v"(a) : "a188", "a189", "a190", "a191"); break;
-      case 48: asm volatile("v_mfma_f32_16x16x32_bf16 a[192:195], %0, %1, 0" :: "v"(b), "v"(a) : "a192", "a193", "a194", "a195"); break;
-      case 49: asm volatile("v_mfma_f32_16x16x32_bf16 a[196:199], %0, %1, 0" :: "v"(b), "v"(a) : "a196", "a197", "a198", "a199"); break;
-      case 50: asm volatile("v_mfma_f32_16x16x32_bf16 a[200:203], %0, %1, 0" :: "v"(b), "v"(a) : "a200", "a201", "a202", "a203"); break;
-      case 51: asm volatile("v_mfma_f32_16x16x32_bf16 a[204:207], %0, %1, 0" :: "v"(b), "v"(a) : "a204", "a205", "a206", "a207"); break;
-      case 52: asm volatile("v_mfma_f32_16x16x32_bf16 a[208:211], %0, %1, 0" :: "v"(b), "v"(a) : "a208", "a209", "a210", "a211"); break;
-      case 53: asm volatile("v_mfma_f32_16x16x32_bf16 a[212:215], %0, %1, 0" :: "v"(b), "v"(a) : "a212", "a213", "a214", "a215"); break;
-      case 54: asm volatile("v_mfma_f32_16x16x32_bf16 a[216:219], %0, %1, 0" :: "v"(b), "v"(a) : "a216", "a217", "a218", "a219"); break;
-      case 55: asm volatile("v_mfma_f32_16x16x32_bf16 a[220:223], %0, %1, 0" :: "v"(b), "v"(a) : "a220", "a221", "a222", "a223"); break;
-      case 56: asm volatile("v_mfma_f32_16x16x32_bf16 a[224:227], %0, %1, 0" :: "v"(b), "v"(a) : "a224", "a225", "a226", "a227"); break;
-      case 57: asm volatile("v_mfma_f32_16x16x32_bf16 a[228:231], %0, %1, 0" :: "v"(b), "v"(a) : "a228", "a229", "a230", "a231"); break;
-      case 58: asm volatile("v_mfma_f32_16x16x32_bf16 a[232:235], %0, %1, 0" :: "v"(b), "v"(a) : "a232", "a233", "a234", "a235"); break;
-      case 59: asm volatile("v_mfma_f32_16x16x32_bf16 a[236:239], %0, %1, 0" :: "v"(b), "v"(a) : "a236", "a237", "a238", "a239"); break;
-      case 60: asm volatile("v_mfma_f32_16x16x32_bf16 a[240:243], %0, %1, 0" :: "v"(b), "v"(a) : "a240", "a241", "a242", "a243"); break;
-      case 61: asm volatile("v_mfma_f32_16x16x32_bf16 a[244:247], %0, %1, 0" :: "v"(b), "v"(a) : "a244", "a245", "a246", "a247"); break;
-      case 62: asm volatile("v_mfma_f32_16x16x32_bf16 a[248:251], %0, %1, 0" :: "v"(b), "v"(a) : "a248", "a249", "a250", "a251"); break;
-      case 63: asm volatile("v_mfma_f32_16x16x32_bf16 a[252:255], %0, %1, 0" :: "v"(b), "v"(a) : "a252", "a253", "a254", "a255"); break;
-    }
-  } else {
-    switch (t) {
-      case 0: asm volatile("v_mfma_f32_16x16x32_bf16 a[0:3], %0, %1, a[0:3]" :: "v"(b), "v"(a) : "a0", "a1", "a2", "a3"); break;
-      case 1: asm volatile("v_mfma_f32_16x16x32_bf16 a[4:7], %0, %1, a[4:7]" :: "v"(b), "v"(a) : "a4", "a5", "a6", "a7"); break;
-      case 2: asm volatile("v_mfma_f32_16x16x32_bf16 a[8:11], %0, %1, a[8:11]" :: "v"(b), "v"(a) : "a8", "a9", "a10", "a11"); break;
-      case 3: asm volatile("v_mfma_f32_16x16x32_bf16 a[12:15], %0, %1, a[12:15]" :: "v"(b), "v"(a) : "a12", "a13", "a14", "a15"); break;
-      case 4: asm volatile("v_mfma_f32_16x16x32_bf16 a[16:19], %0, %1, a[16:19]" :: "v"(b), "v"(a) : "a16", "a17", "a18", "a19"); break;
-      case 5: asm volatile("v_mfma_f32_16x16x32_bf16 a[20:23], %0, %1, a[20:23]" :: "v"(b), "v"(a) : "a20", "a21", "a22", "a23"); break;
-      case 6: asm volatile("v_mfma_f32_16x16x32_bf16 a[24:27], %0, %1, a[24:27]" :: "v"(b), "v"(a) : "a24", "a25", "a26", "a27"); break;
-      case 7: asm volatile("v_mfma_f32_16x16x32_bf16 a[28:31], %0, %1, a[28:31]" :: "v"(b), "v"(a) : "a28", "a29", "a30", "a31"); break;
-      case 8: asm volatile("v_mfma_f32_16x16x32_bf16 a[32:35], %0, %1, a[32:35]" :: "v"(b), "v"(a) : "a32", "a33", "a34", "a35"); break;
-      case 9: asm volatile("v_mfma_f32_16x16x32_bf16 a[36:39], %0, %1, a[36:39]" :: "v"(b), "v"(a) : "a36", "a37", "a38", "a39"); break;
-      case 10: asm volatile("v_mfma_f32_16x16x32_bf16 a[40:43], %0, %1, a[40:43]" :: "v"(b), "v"(a) : "a40", "a41", "a42", "a43"); break;
-      case 11: asm volatile("v_mfma_f32_16x16x32_bf16 a[44:47], %0, %1, a[44:47]" :: "v"(b), "v"(a) : "a44", "a45", "a46", "a47"); break;
-      case 12: asm volatile("v_mfma_f32_16x16x32_bf16 a[48:51], %0, %1, a[48:51]" :: "v"(b), "v"(a) : "a48", "a49", "a50", "a51"); break;
-      case 13: asm volatile("v_mfma_f32_16x16x32_bf16 a[52:55], %0, %1, a[52:55]" :: "v"(b), "v"(a) : "a52", "a53", "a54", "a55"); break;
-      case 14: asm volatile("v_mfma_f32_16x16x32_bf16 a[56:59], %0, %1, a[56:59]" :: "v"(b), "v"(a) : "a56", "a57", "a58", "a59"); break;
-      case 15: asm volatile("v_mfma_f32_16x16x32_bf16 a[60:63], %0, %1, a[60:63]" :: "v"(b), "v"(a) : "a60", "a61", "a62", "a63"); break;
-      case 16: asm volatile("v_mfma_f32_16x16x32_bf16 a[64:67], %0, %1, a[64:67]" :: "v"(b), "v"(a) : "a64", "a65", "a66", "a67"); break;
-      case 17: asm volatile("v_mfma_f32_16x16x32_bf16 a[68:71], %0, %1, a[68:71]" :: "v"(b), "v"(a) : "a68", "a69", "a70", "a71"); break;
-      case 18: asm volatile("v_mfma_f32_16x16x32_bf16 a[72:75], %0, %1, a[72:75]" :: "v"(b), "v"(a) : "a72", "a73", "a74", "a75"); break;
-      case 19: asm volatile("v_mfma_f32_16x16x32_bf16 a[76:79], %0, %1, a[76:79]" :: "v"(b), "v"(a) : "a76", "a77", "a78", "a79"); break;
-      case 20: asm volatile("v_mfma_f32_16x16x32_bf16 a[80:83], %0, %1, a[80:83]" :: "v"(b), "v"(a) : "a80", "a81", "a82", "a83"); break;
-      case 21: asm volatile("v_mfma_f32_16x16x32_bf16 a[84:87], %0, %1, a[84:87]" :: "v"(b), "v"(a) : "a84", "a85", "a86", "a87"); break;
-      case 22: asm volatile("v_mfma_f32_16x16x32_bf16 a[88:91], %0, %1, a[88:91]" :: "v"(b), "v"(a) : "a88", "a89", "a90", "a91"); break;
-      case 23: asm volatile("v_mfma_f32_16x16x32_bf16 a[92:95], %0, %1, a[92:95]" :: "v"(b), "v"(a) : "a92", "a93", "a94", "a95"); break;
-      case 24: asm volatile("v_mfma_f32_16x16x32_bf16 a[96:99], %0, %1, a[96:99]" :: "v"(b), "v"(a) : "a96", "a97", "a98", "a99"); break;
-      case 25: asm volatile("v_mfma_f32_16x16x32_bf16 a[100:103], %0, %1, a[100:103]" :: "v"(b), "v"(a) : "a100", "a101", "a102", "a103"); break;
-      case 26: asm volatile("v_mfma_f32_16x16x32_bf16 a[104:107], %0, %1, a[104:107]" :: "v"(b), "v"(a) : "a104", "a105", "a106", "a107"); break;
-      case 27: asm volatile("v_mfma_f32_16x16x32_bf16 a[108:111], %0, %1, a[108:111]" :: "v"(b), "v"(a) : "a108", "a109", "a110", "a111"); break;
-      case 28: asm volatile("v_mfma_f32_16x16x32_bf16 a[112:115], %0, %1, a[112:115]" :: "v"(b), "v"(a) : "a112", "a113", "a114", "a115"); break;
-      case 29: asm volatile("v_mfma_f32_16x16x32_bf16 a[116:119], %0, %1, a[116:119]" :: "v"(b), "v"(a) : "a116", "a117", "a118", "a119"); break;
-      case 30: asm volatile("v_mfma_f32_16x16x32_bf16 a[120:123], %0, %1, a[120:123]" :: "v"(b), "v"(a) : "a120", "a121", "a122", "a123"); break;
-      case 31: asm volatile("v_mfma_f32_16x16x32_bf16 a[124:127], %0, %1, a[124:127]" :: "v"(b), "v"(a) : "a124", "a125", "a126", "a127"); break;
-      case 32: asm volatile("v_mfma_f32_16x16x32_bf16 a[128:131], %0, %1, a[128:131]" :: "v"(b), "v"(a) : "a128", "a129", "a130", "a131"); break;
-      case 33: asm volatile("v_mfma_f32_16x16x32_bf16 a[132:135], %0, %1, a[132:135]" :: "v"(b), "v"(a) : "a132", "a133", "a134", "a135"); break;
-      case 34: asm volatile("v_mfma_f32_16x16x32_bf16 a[136:139], %0, %1, a[136:139]" :: "v"(b), "v"(a) : "a136", "a137", "a138", "a139"); break;
-      case 35: asm volatile("v_mfma_f32_16x16x32_bf16 a[140:143], %0, %1, a[140:143]" :: "v"(b), "v"(a) : "a140", "a141", "a142", "a143"); break;
-      case 36: asm volatile("v_mfma_f32_16x16x32_bf16 a[144:147], %0, %1, a[144:147]" :: "v"(b), "v"(a) : "a144", "a145", "a146", "a147"); break;
-      case 37: asm volatile("v_mfma_f32_16x16x32_bf16 a[148:151], %0, %1, a[148:151]" :: "v"(b), "v"(a) : "a148", "a149", "a150", "a151"); break;
-      case 38: asm volatile("v_mfma_f32_16x16x32_bf16 a[152:155], %0, %1, a[152:155]" :: "v"(b), "v"(a) : "a152", "a153", "a154", "a155"); break;
-      case 39: asm volatile("v_mfma_f32_16x16x32_bf16 a[156:159], %0, %1, a[156:159]" :: "v"(b), "v"(a) : "a156", "a157", "a158", "a159"); break;
-      case 40: asm volatile("v_mfma_f32_16x16x32_bf16 a[160:163], %0, %1, a[160:163]" :: "v"(b), "v"(a) : "a160", "a161", "a162", "a163"); break;
-      case 41: asm volatile("v_mfma_f32_16x16x32_bf16 a[164:167], %0, %1, a[164:167]" :: "v"(b), "v"(a) : "a164", "a165", "a166", "a167"); break;
-      case 42: asm volatile("v_mfma_f32_16x16x32_bf16 a[168:171], %0, %1, a[168:171]" :: "v"(b), "v"(a) : "a168", "a169", "a170", "a171"); break;
-      case 43: asm volatile("v_mfma_f32_16x16x32_bf16 a[172:175], %0, %1, a[172:175]" :: "v"(b), "v"(a) : "a172", "a173", "a174", "a175"); break;
-      case 44: asm volatile("v_mfma_f32_16x16x32_bf16 a[176:179], %0, %1, a[176:179]" :: "v"(b), "v"(a) : "a176", "a177", "a178", "a179"); break;
-      case 45: asm volatile("v_mfma_f32_16x16x32_bf16 a[180:183], %0, %1, a[180:183]" :: "v"(b), "v"(a) : "a180", "a181", "a182", "a183"); break;
-      case 46: asm volatile("v_mfma_f32_16x16x32_bf16 a[184:187], %0, %1, a[184:187]" :: "v"(b), "v"(a) : "a184", "a185", "a186", "a187"); break;
-      case 47: asm volatile("v_mfma_f32_16x16x32_bf16 a[188:191], %0, %1, a[188:191]" :: "v"(b), "v"(a) : "a188", "a189", "a190", "a191"); break;
-      case 48: asm volatile("v_mfma_f32_16x16x32_bf16 a[192:195], %0, %1, a[192:195]" :: "v"(b), "v"(a) : "a192", "a193", "a194", "a195"); break;
-      case 49: asm volatile("v_mfma_f32_16x16x32_bf16 a[196:199], %0, %1, a[196:199]" :: "v"(b), "v"(a) : "a196", "a197", "a198", "a199"); break;
-      case 50: asm volatile("v_mfma_f32_16x16x32_bf16 a[200:203], %0, %1, a[200:203]" :: "v"(b), "v"(a) : "a200", "a201", "a202", "a203"); break;
-      case 51: asm volatile("v_mfma_f32_16x16x32_bf16 a[204:207], %0, %1, a[204:207]" :: "v"(b), "v"(a) : "a204", "a205", "a206", "a207"); break;
-      case 52: asm volatile("v_mfma_f32_16x16x32_bf16 a[208:211], %0, %1, a[208:211]" :: "v"(b), "v"(a) : "a208", "a209", "a210", "a211"); break;
-      case 53: asm volatile("v_mfma_f32_16x16x32_bf16 a[212:215], %0, %1, a[212:215]" :: "v"(b), "v"(a) : "a212", "a213", "a214", "a215"); break;
-      case 54: asm volatile("v_mfma_f32_16x16x32_bf16 a[216:219], %0, %1, a[216:219]" :: "v"(b), "v"(a) : "a216", "a217", "a218", "a219"); break;
-      case 55: asm volatile("v_mfma_f32_16x16x32_bf16 a[220:223], %0, %1, a[220:223]" :: "v"(b), "v"(a) : "a220", "a221", "a222", "a223"); break;
-      case 56: asm volatile("v_mfma_f32_16x16x32_bf16 a[224:227], %0, %1, a[224:227]" :: "v"(b), "v"(a) : "a224", "a225", "a226", "a227"); break;
-      case 57: asm volatile("v_mfma_f32_16x16x32_bf16 a[228:231], %0, %1, a[228:231]" :: "v"(b), "v"(a) : "a228", "a229", "a230", "a231"); break;
-      case 58: asm volatile("v_mfma_f32_16x16x32_bf16 a[232:235], %0, %1, a[232:235]" :: "v"(b), "v"(a) : "a232", "a233", "a234", "a235"); break;
-      case 59: asm volatile("v_mfma_f32_16x16x32_bf16 a[236:239], %0, %1, a[236:239]" :: "v"(b), "v"(a) : "a236", "a237", "a238", "a239"); break;
-      case 60: asm volatile("v_mfma_f32_16x16x32_bf16 a[240:243], %0, %1, a[240:243]" :: "v"(b), "v"(a) : "a240", "a241", "a242", "a243"); break;
-      case 61: asm volatile("v_mfma_f32_16x16x32_bf16 a[244:247], %0, %1, a[244:247]" :: "v"(b), "v"(a) : "a244", "a245", "a246", "a247"); break;
-      case 62: asm volatile("v_mfma_f32_16x16x32_bf16 a[248:251], %0, %1, a[248:251]" :: "v"(b), "v"(a) : "a248", "a249", "a250", "a251"); break;
-      case 63: asm volatile("v_mfma_f32_16x16x32_bf16 a[252:255], %0, %1, a[252:255]" :: "v"(b), "v"(a) : "a252", "a253", "a254", "a255"); break;
-    }
-  }
-}
-template <int n>
-XCP_DEV float acc_read() {
-  float v = 0.f;
-  switch (n) {
-    case 0: asm volatile("v_accvgpr_read_b32 %0, a0" : "=v"(v)); break;
-    case 1: asm volatile("v_accvgpr_read_b32 %0, a1" : "=v"(v)); break;
-    case 2: asm volatile("v_accvgpr_read_b32 %0, a2" : "=v"(v)); break;
-    case 3: asm volatile("v_accvgpr_read_b32 %0, a3" : "=v"(v)); break;
-    case 4: asm volatile("v_accvgpr_read_b32 %0, a4" : "=v"(v)); break;
-    case 5: asm volatile("v_accvgpr_read_b32 %0, a5" : "=v"(v)); break;
-    case 6: asm volatile("v_accvgpr_read_b32 %0, a6" : "=v"(v)); break;
-    case 7: asm volatile("v_accvgpr_read_b32 %0, a7" : "=v"(v)); break;
-    case 8: asm volatile("v_accvgpr_read_b32 %0, a8" : "=v"(v)); break;
-    case 9: asm volatile("v_accvgpr_read_b32 %0, a9" : "=v"(v)); break;
-    case 10: asm volatile("v_accvgpr_read_b32 %0, a10" : "=v"(v)); break;
-    case 11: asm volatile("v_accvgpr_read_b32 %0, a11" : "=v"(v)); break;
-    case 12: asm volatile("v_accvgpr_read_b32 %0, a12" : "=v"(v)); break;
-    case 13: asm volatile("v_accvgpr_read_b32 %0, a13" : "=v"(v)); break;
-    case 14: asm volatile("v_accvgpr_read_b32 %0, a14" : "=v"(v)); break;
-    case 15: asm volatile("v_accvgpr_read_b32 %0, a15" : "=v"(v)); break;
-    case 16: asm volatile("v_accvgpr_read_b32 %0, a16" : "=v"(v)); break;
-    case 17: asm volatile("v_accvgpr_read_b32 %0, a17" : "=v"(v)); break;
-    case 18: asm volatile("v_accvgpr_read_b32 %0, a18" : "=v"(v)); break;
-    case 19: asm volatile("v_accvgpr_read_b32 %0, a19" : "=v"(v)); break;
-    case 20: asm volatile("v_accvgpr_read_b32 %0, a20" : "=v"(v)); break;
-    case 21: asm volatile("v_accvgpr_read_b32 %0, a21" : "=v"(v)); break;
-    case 22: asm volatile("v_accvgpr_read_b32 %0, a22" : "=v"(v)); break;
-    case 23: asm volatile("v_accvgpr_read_b32 %0, a23" : "=v"(v)); break;
-    case 24: asm volatile("v_accvgpr_read_b32 %0, a24" : "=v"(v)); break;
-    case 25: asm volatile("v_accvgpr_read_b32 %0, a25" : "=v"(v)); break;
-    case 26: asm volatile("v_accvgpr_read_b32 %0, a26" : "=v"(v)); break;
-    case 27: asm volatile("v_accvgpr_read_b32 %0, a27" : "=v"(v)); break;
-    case 28: asm volatile("v_accvgpr_read_b32 %0, a28" : "=v"(v)); break;
-    case 29: asm volatile("v_accvgpr_read_b32 %0, a29" : "=v"(v)); break;
-    case 30: asm volatile("v_accvgpr_read_b32 %0, a30" : "=v"(v)); break;
-    case 31: asm volatile("v_accvgpr_read_b32 %0, a31" : "=v"(v)); break;
-    case 32: asm volatile("v_accvgpr_read_b32 %0, a32" : "=v"(v)); break;
-    case 33: asm volatile("v_accvgpr_read_b32 %0, a33" : "=v"(v)); break;
-    case 34: asm volatile("v_accvgpr_read_b32 %0, a34" : "=v"(v)); break;
-    case 35: asm volatile("v_accvgpr_read_b32 %0, a35" : "=v"(v)); break;
-    case 36: asm volatile("v_accvgpr_read_b32 %0, a36" : "=v"(v)); break;
-    case 37: asm volatile("v_accvgpr_read_b32 %0, a37" : "=v"(v)); break;
-    case 38: asm volatile("v_accvgpr_read_b32 %0, a38" : "=v"(v)); break;
-    case 39: asm volatile("v_accvgpr_read_b32 %0, a39" : "=v"(v)); break;
-    case 40: asm volatile("v_accvgpr_read_b32 %0, a40" : "=v"(v)); break;
-    case 41: asm volatile("v_accvgpr_read_b32 %0, a41" : "=v"(v)); break;
-    case 42: asm volatile("v_accvgpr_read_b32 %0, a42" : "=v"(v)); break;
-    case 43: asm volatile("v_accvgpr_read_b32 %0, a43" : "=v"(v)); break;
-    case 44: asm volatile("v_accvgpr_read_b32 %0, a44" : "=v"(v)); break;
-    case 45: asm volatile("v_accvgpr_read_b32 %0, a45" : "=v"(v)); break;
-    case 46: asm volatile("v_accvgpr_read_b32 %0, a46" : "=v"(v)); break;
-    case 47: asm volatile("v_accvgpr_read_b32 %0, a47" : "=v"(v)); break;
-    case 48: asm volatile("v_accvgpr_read_b32 %0, a48" : "=v"(v)); break;
-    case 49: asm volatile("v_accvgpr_read_b32 %0, a49" : "=v"(v)); break;
-    case 50: asm volatile("v_accvgpr_read_b32 %0, a50" : "=v"(v)); break;
-    case 51: asm volatile("v_accvgpr_read_b32 %0, a51" : "=v"(v)); break;
-    case 52: asm volatile("v_accvgpr_read_b32 %0, a52" : "=v"(v)); break;
-    case 53: asm volatile("v_accvgpr_read_b32 %0, a53" : "=v"(v)); break;
-    case 54: asm volatile("v_accvgpr_read_b32 %0, a54" : "=v"(v)); break;
-    case 55: asm volatile("v_accvgpr_read_b32 %0, a55" : "=v"(v)); break;
-    case 56: asm volatile("v_accvgpr_read_b32 %0, a56" : "=v"(v)); break;
-    case 57: asm volatile("v_accvgpr_read_b32 %0, a57" : "=v"(v)); break;
-    case 58: asm volatile("v_accvgpr_read_b32 %0, a58" : "=v"(v)); break;
-    case 59: asm volatile("v_accvgpr_read_b32 %0, a59" : "=v"(v)); break;
-    case 60: asm volatile("v_accvgpr_read_b32 %0, a60" : "=v"(v)); break;
-    case 61: asm volatile("v_accvgpr_read_b32 %0, a61" : "=v"(v)); break;
-    case 62: asm volatile("v_accvgpr_read_b32 %0, a62" : "=v"(v)); break;
-    case 63: asm volatile("v_accvgpr_read_b32 %0, a63" : "=v"(v)); break;
-    case 64: asm volatile("v_accvgpr_read_b32 %0, a64" : "=v"(v)); break;
-    case 65: asm volatile("v_accvgpr_read_b32 %0, a65" : "=v"(v)); break;
-    case 66: asm volatile("v_accvgpr_read_b32 %0, a66" : "=v"(v)); break;
-    case 67: asm volatile("v_accvgpr_read_b32 %0, a67" : "=v"(v)); break;
-    case 68: asm volatile("v_accvgpr_read_b32 %0, a68" : "=v"(v)); break;
-    case 69: asm volatile("v_accvgpr_read_b32 %0, a69" : "=v"(v)); break;
-    case 70: asm volatile("v_accvgpr_read_b32 %0, a70" : "=v"(v)); break;
-    case 71: asm volatile("v_accvgpr_read_b32 %0, a71" : "=v"(v)); break;
-    case 72: asm volatile("v_accvgpr_read_b32 %0, a72" : "=v"(v)); break;
-    case 73: asm volatile("v_accvgpr_read_b32 %0, a73" : "=v"(v)); break;
-    case 74: asm volatile("v_accvgpr_read_b32 %0, a74" : "=v"(v)); break;
-    case 75: asm volatile("v_accvgpr_read_b32 %0, a75" : "=v"(v)); break;
-    case 76: asm volatile("v_accvgpr_read_b32 %0, a76" : "=v"(v)); break;
-    case 77: asm volatile("v_accvgpr_read_b32 %0, a77" : "=v"(v)); break;
-    case 78: asm volatile("v_accvgpr_read_b32 %0, a78" : "=v"(v)); break;
-    case 79: asm volatile("v_accvgpr_read_b32 %0, a79" : "=v"(v)); break;
-    case 80: asm volatile("v_accvgpr_read_b32 %0, a80" : "=v"(v)); break;
-    case 81: asm volatile("v_accvgpr_read_b32 %0, a81" : "=v"(v)); break;
-    case 82: asm volatile("v_accvgpr_read_b32 %0, a82" : "=v"(v)); break;
-    case 83: asm volatile("v_accvgpr_read_b32 %0, a83" : "=v"(v)); break;
-    case 84: asm volatile("v_accvgpr_read_b32 %0, a84" : "=v"(v)); break;
-    case 85: asm volatile("v_accvgpr_read_b32 %0, a85" : "=v"(v)); break;
-    case 86: asm volatile("v_accvgpr_read_b32 %0, a86" : "=v"(v)); break;
-    case 87: asm volatile("v_accvgpr_read_b32 %0, a87" : "=v"(v)); break;
-    case 88: asm volatile("v_accvgpr_read_b32 %0, a88" : "=v"(v)); break;
-    case 89: asm volatile("v_accvgpr_read_b32 %0, a89" : "=v"(v)); break;
-    case 90: asm volatile("v_accvgpr_read_b32 %0, a90" : "=v"(v)); break;
-    case 91: asm volatile("v_accvgpr_read_b32 %0, a91" : "=v"(v)); break;
-    case 92: asm volatile("v_accvgpr_read_b32 %0, a92" : "=v"(v)); break;
-    case 93: asm volatile("v_accvgpr_read_b32 %0, a93" : "=v"(v)); break;
-    case 94: asm volatile("v_accvgpr_read_b32 %0, a94" : "=v"(v)); break;
-    case 95: asm volatile("v_accvgpr_read_b32 %0, a95" : "=v"(v)); break;
-    case 96: asm volatile("v_accvgpr_read_b32 %0, a96" : "=v"(v)); break;
-    case 97: asm volatile("v_accvgpr_read_b32 %0, a97" : "=v"(v)); break;
-    case 98: asm volatile("v_accvgpr_read_b32 %0, a98" : "=v"(v)); break;
-    case 99: asm volatile("v_accvgpr_read_b32 %0, a99" : "=v"(v)); break;
-    case 100: asm volatile("v_accvgpr_read_b32 %0, a100" : "=v"(v)); break;
-    case 101: asm volatile("v_accvgpr_read_b32 %0, a101" : "=v"(v)); break;
-    case 102: asm volatile("v_accvgpr_read_b32 %0, a102" : "=v"(v)); break;
-    case 103: asm volatile("v_accvgpr_read_b32 %0, a103" : "=v"(v)); break;
-    case 104: asm volatile("v_accvgpr_read_b32 %0, a104" : "=v"(v)); break;
-    case 105: asm volatile("v_accvgpr_read_b32 %0, a105" : "=v"(v)); break;
-    case 106: asm volatile("v_accvgpr_read_b32 %0, a106" : "=v"(v)); break;
-    case 107: asm volatile("v_accvgpr_read_b32 %0, a107" : "=v"(v)); break;
-    case 108: asm volatile("v_accvgpr_read_b32 %0, a108" : "=v"(v)); break;
-    case 109: asm volatile("v_accvgpr_read_b32 %0, a109" : "=v"(v)); break;
-    case 110: asm volatile("v_accvgpr_read_b32 %0, a110" : "=v"(v)); break;
-    case 111: asm volatile("v_accvgpr_read_b32 %0, a111" : "=v"(v)); break;
-    case 112: asm volatile("v_accvgpr_read_b32 %0, a112" : "=v"(v)); break;
-    case 113: asm volatile("v_accvgpr_read_b32 %0, a113" : "=v"(v)); break;
-    case 114: asm volatile("v_accvgpr_read_b32 %0, a114" : "=v"(v)); break;
-    case 115: asm volatile("v_accvgpr_read_b32 %0, a115" : "=v"(v)); break;
-    case 116: asm volatile("v_accvgpr_read_b32 %0, a116" : "=v"(v)); break;
-    case 117: asm volatile("v_accvgpr_read_b32 %0, a117" : "=v"(v)); break;
-    case 118: asm volatile("v_accvgpr_read_b32 %0, a118" : "=v"(v)); break;
-    case 119: asm volatile("v_accvgpr_read_b32 %0, a119" : "=v"(v)); break;
-    case 120: asm volatile("v_accvgpr_read_b32 %0, a120" : "=v"(v)); break;
-    case 121: asm volatile("v_accvgpr_read_b32 %0, a121" : "=v"(v)); break;
-    case 122: asm volatile("v_accvgpr_read_b32 %0, a122" : "=v"(v)); break;
-    case 123: asm volatile("v_accvgpr_read_b32 %0, a123" : "=v"(v)); break;
-    case 124: asm volatile("v_accvgpr_read_b32 %0, a124" : "=v"(v)); break;
-    case 125: asm volatile("v_accvgpr_read_b32 %0, a125" : "=v"(v)); break;
-    case 126: asm volatile("v_accvgpr_read_b32 %0, a126" : "=v"(v)); break;
-    case 127: asm volatile("v_accvgpr_read_b32 %0, a127" : "=v"(v)); break;
-    case 128: asm volatile("v_accvgpr_read_b32 %0, a128" : "=v"(v)); break;
-    case 129: asm volatile("v_accvgpr_read_b32 %0, a129" : "=v"(v)); break;
-    case 130: asm volatile("v_accvgpr_read_b32 %0, a130" : "=v"(v)); break;
-    case 131: asm volatile("v_accvgpr_read_b32 %0, a131" : "=v"(v)); break;
-    case 132: asm volatile("v_accvgpr_read_b32 %0, a132" : "=v"(v)); break;
-    case 133: asm volatile("v_accvgpr_read_b32 %0, a133" : "=v"(v)); break;
-    case 134: asm volatile("v_accvgpr_read_b32 %0, a134" : "=v"(v)); break;
-    case 135: asm volatile("v_accvgpr_read_b32 %0, a135" : "=v"(v)); break;
-    case 136: asm volatile("v_accvgpr_read_b32 %0, a136" : "=v"(v)); break;
-    case 137: asm volatile("v_accvgpr_read_b32 %0, a137" : "=v"(v)); break;
-    case 138: asm volatile("v_accvgpr_read_b32 %0, a138" : "=v"(v)); break;
-    case 139: asm volatile("v_accvgpr_read_b32 %0, a139" : "=v"(v)); break;
-    case 140: asm volatile("v_accvgpr_read_b32 %0, a140" : "=v"(v)); break;
-    case 141: asm volatile("v_accvgpr_read_b32 %0, a141" : "=v"(v)); break;
-    case 142: asm volatile("v_accvgpr_read_b32 %0, a142" : "=v"(v)); break;
-    case 143: asm volatile("v_accvgpr_read_b32 %0, a143" : "=v"(v)); break;
-    case 144: asm volatile("v_accvgpr_read_b32 %0, a144" : "=v"(v)); break;
-    case 145: asm volatile("v_accvgpr_read_b32 %0, a145" : "=v"(v)); break;
-    case 146: asm volatile("v_accvgpr_read_b32 %0, a146" : "=v"(v)); break;
-    case 147: asm volatile("v_accvgpr_read_b32 %0, a147" : "=v"(v)); break;
-    case 148: asm volatile("v_accvgpr_read_b32 %0, a148" : "=v"(v)); break;
-    case 149: asm volatile("v_accvgpr_read_b32 %0, a149" : "=v"(v)); break;
-    case 150: asm volatile("v_accvgpr_read_b32 %0, a150" : "=v"(v)); break;
-    case 151: asm volatile("v_accvgpr_read_b32 %0, a151" : "=v"(v)); break;
-    case 152: asm volatile("v_accvgpr_read_b32 %0, a152" : "=v"(v)); break;
-    case 153: asm volatile("v_accvgpr_read_b32 %0, a153" : "=v"(v)); break;
-    case 154: asm volatile("v_accvgpr_read_b32 %0, a154" : "=v"(v)); break;
-    case 155: asm volatile("v_accvgpr_read_b32 %0, a155" : "=v"(v)); break;
-    case 156: asm volatile("v_accvgpr_read_b32 %0, a156" : "=v"(v)); break;
-    case 157: asm volatile("v_accvgpr_read_b32 %0, a157" : "=v"(v)); break;
-    case 158: asm volatile("v_accvgpr_read_b32 %0, a158" : "=v"(v)); break;
-    case 159: asm volatile("v_accvgpr_read_b32 %0, a159" : "=v"(v)); break;
-    case 160: asm volatile("v_accvgpr_read_b32 %0, a160" : "=v"(v)); break;
-    case 161: asm volatile("v_accvgpr_read_b32 %0, a161" : "=v"(v)); break;
-    case 162: asm volatile("v_accvgpr_read_b32 %0, a162" : "=v"(v)); break;
-    case 163: asm volatile("v_accvgpr_read_b32 %0, a163" : "=v"(v)); break;
-    case 164: asm volatile("v_accvgpr_read_b32 %0, a164" : "=v"(v)); break;
-    case 165: asm volatile("v_accvgpr_read_b32 %0, a165" : "=v"(v)); break;
-    case 166: asm volatile("v_accvgpr_read_b32 %0, a166" : "=v"(v)); break;
-    case 167: asm volatile("v_accvgpr_read_b32 %0, a167" : "=v"(v)); break;
-    case 168: asm volatile("v_accvgpr_read_b32 %0, a168" : "=v"(v)); break;
-    case 169: asm volatile("v_accvgpr_read_b32 %0, a169" : "=v"(v)); break;
-    case 170: asm volatile("v_accvgpr_read_b32 %0, a170" : "=v"(v)); break;
-    case 171: asm volatile("v_accvgpr_read_b32 %0, a171" : "=v"(v)); break;
-    case 172: asm volatile("v_accvgpr_read_b32 %0, a172" : "=v"(v)); break;
-    case 173: asm volatile("v_accvgpr_read_b32 %0, a173" : "=v"(v)); break;
-    case 174: asm volatile("v_accvgpr_read_b32 %0, a174" : "=v"(v)); break;
-    case 175: asm volatile("v_accvgpr_read_b32 %0, a175" : "=v"(v)); break;
-    case 176: asm volatile("v_accvgpr_read_b32 %0, a176" : "=v"(v)); break;
-    case 177: asm volatile("v_accvgpr_read_b32 %0, a177" : "=v"(v)); break;
-    case 178: asm volatile("v_accvgpr_read_b32 %0, a178" : "=v"(v)); break;
-    case 179: asm volatile("v_accvgpr_read_b32 %0, a179" : "=v"(v)); break;
-    case 180: asm volatile("v_accvgpr_read_b32 %0, a180" : "=v"(v)); break;
-    case 181: asm volatile("v_accvgpr_read_b32 %0, a181" : "=v"(v)); break;
-    case 182: asm volatile("v_accvgpr_read_b32 %0, a182" : "=v"(v)); break;
-    case 183: asm volatile("v_accvgpr_read_b32 %0, a183" : "=v"(v)); break;
-    case 184: asm volatile("v_accvgpr_read_b32 %0, a184" : "=v"(v)); break;
-    case 185: asm volatile("v_accvgpr_read_b32 %0, a185" : "=v"(v)); break;
-    case 186: asm volatile("v_accvgpr_read_b32 %0, a186" : "=v"(v)); break;
-    case 187: asm volatile("v_accvgpr_read_b32 %0, a187" : "=v"(v)); break;
-    case 188: asm volatile("v_accvgpr_read_b32 %0, a188" : "=v"(v)); break;
-    case 189: asm volatile("v_accvgpr_read_b32 %0, a189" : "=v"(v)); break;
-    case 190: asm volatile("v_accvgpr_read_b32 %0, a190" : "=v"(v)); break;
-    case 191: asm volatile("v_accvgpr_read_b32 %0, a191" : "=v"(v)); break;
-    case 192: asm volatile("v_accvgpr_read_b32 %0, a192" : "=v"(v)); break;
-    case 193: asm volatile("v_accvgpr_read_b32 %0, a193" : "=v"(v)); break;
-    case 194: asm volatile("v_accvgpr_read_b32 %0, a194" : "=v"(v)); break;
-    case 195: asm volatile("v_accvgpr_read_b32 %0, a195" : "=v"(v)); break;
-    case 196: asm volatile("v_accvgpr_read_b32 %0, a196" : "=v"(v)); break;
-    case 197: asm volatile("v_accvgpr_read_b32 %0, a197" : "=v"(v)); break;
-    case 198: asm volatile("v_accvgpr_read_b32 %0, a198" : "=v"(v)); break;
-    case 199: asm volatile("v_accvgpr_read_b32 %0, a199" : "=v"(v)); break;
-    case 200: asm volatile("v_accvgpr_read_b32 %0, a200" : "=v"(v)); break;
-    case 201: asm volatile("v_accvgpr_read_b32 %0, a201" : "=v"(v)); break;
-    case 202: asm volatile("v_accvgpr_read_b32 %0, a202" : "=v"(v)); break;
-    case 203: asm volatile("v_accvgpr_read_b32 %0, a203" : "=v"(v)); break;
-    case 204: asm volatile("v_accvgpr_read_b32 %0, a204" : "=v"(v)); break;
-    case 205: asm volatile("v_accvgpr_read_b32 %0, a205" : "=v"(v)); break;
-    case 206: asm volatile("v_accvgpr_read_b32 %0, a206" : "=v"(v)); break;
-    case 207: asm volatile("v_accvgpr_read_b32 %0, a207" : "=v"(v)); break;
-    case 208: asm volatile("v_accvgpr_read_b32 %0, a208" : "=v"(v)); break;
-    case 209: asm volatile("v_accvgpr_read_b32 %0, a209" : "=v"(v)); break;
-    case 210: asm volatile("v_accvgpr_read_b32 %0, a210" : "=v"(v)); break;
-    case 211: asm volatile("v_accvgpr_read_b32 %0, a211" : "=v"(v)); break;
-    case 212: asm volatile("v_accvgpr_read_b32 %0, a212" : "=v"(v)); break;
-    case 213: asm volatile("v_accvgpr_read_b32 %0, a213" : "=v"(v)); break;
-    case 214: asm volatile("v_accvgpr_read_b32 %0, a214" : "=v"(v)); break;
-    case 215: asm volatile("v_accvgpr_read_b32 %0, a215" : "=v"(v)); break;
-    case 216: asm volatile("v_accvgpr_read_b32 %0, a216" : "=v"(v)); break;
-    case 217: asm volatile("v_accvgpr_read_b32 %0, a217" : "=v"(v)); break;
-    case 218: asm volatile("v_accvgpr_read_b32 %0, a218" : "=v"(v)); break;
-    case 219: asm volatile("v_accvgpr_read_b32 %0, a219" : "=v"(v)); break;
-    case 220: asm volatile("v_accvgpr_read_b32 %0, a220" : "=v"(v)); break;
-    case 221: asm volatile("v_accvgpr_read_b32 %0, a221" : "=v"(v)); break;
-    case 222: asm volatile("v_accvgpr_read_b32 %0, a222" : "=v"(v)); break;
-    case 223: asm volatile("v_accvgpr_read_b32 %0, a223" : "=v"(v)); break;
-    case 224: asm volatile("v_accvgpr_read_b32 %0, a224" : "=v"(v)); break;
-    case 225: asm volatile("v_accvgpr_read_b32 %0, a225" : "=v"(v)); break;
-    case 226: asm volatile("v_accvgpr_read_b32 %0, a226" : "=v"(v)); break;
-    case 227: asm volatile("v_accvgpr_read_b32 %0, a227" : "=v"(v)); break;
-    case 228: asm volatile("v_accvgpr_read_b32 %0, a228" : "=v"(v)); break;
-    case 229: asm volatile("v_accvgpr_read_b32 %0, a229" : "=v"(v)); break;
-    case 230: asm volatile("v_accvgpr_read_b32 %0, a230" : "=v"(v)); break;
-    case 231: asm volatile("v_accvgpr_read_b32 %0, a231" : "=v"(v)); break;
-    case 232: asm volatile("v_accvgpr_read_b32 %0, a232" : "=v"(v)); break;
-    case 233: asm volatile("v_accvgpr_read_b32 %0, a233" : "=v"(v)); break;
-    case 234: asm volatile("v_accvgpr_read_b32 %0, a234" : "=v"(v)); break;
-    case 235: asm volatile("v_accvgpr_read_b32 %0, a235" : "=v"(v)); break;
-    case 236: asm volatile("v_accvgpr_read_b32 %0, a236" : "=v"(v)); break;
-    case 237: asm volatile("v_accvgpr_read_b32 %0, a237" : "=v"(v)); break;
-    case 238: asm volatile("v_accvgpr_read_b32 %0, a238" : "=v"(v)); break;
-    case 239: asm volatile("v_accvgpr_read_b32 %0, a239" : "=v"(v)); break;
-    case 240: asm volatile("v_accvgpr_read_b32 %0, a240" : "=v"(v)); break;
-    case 241: asm volatile("v_accvgpr_read_b32 %0, a241" : "=v"(v)); break;
-    case 242: asm volatile("v_accvgpr_read_b32 %0, a242" : "=v"(v)); break;
-    case 243: asm volatile("v_accvgpr_read_b32 %0, a243" : "=v"(v)); break;
-    case 244: asm volatile("v_accvgpr_read_b32 %0, a244" : "=v"(v)); break;
-    case 245: asm volatile("v_accvgpr_read_b32 %0, a245" : "=v"(v)); break;
-    case 246: asm volatile("v_accvgpr_read_b32 %0, a246" : "=v"(v)); break;
-    case 247: asm volatile("v_accvgpr_read_b32 %0, a247" : "=v"(v)); break;
-    case 248: asm volatile("v_accvgpr_read_b32 %0, a248" : "=v"(v)); break;
-    case 249: asm volatile("v_accvgpr_read_b32 %0, a249" : "=v"(v)); break;
-    case 250: asm volatile("v_accvgpr_read_b32 %0, a250" : "=v"(v)); break;
-    case 251: asm volatile("v_accvgpr_read_b32 %0, a251" : "=v"(v)); break;
-    case 252: asm volatile("v_accvgpr_read_b32 %0, a252" : "=v"(v)); break;
-    case 253: asm volatile("v_accvgpr_read_b32 %0, a253" : "=v"(v)); break;
-    case 254: asm volatile("v_accvgpr_read_b32 %0, a254" : "=v"(v)); break;
-    case 255: asm volatile("v_accvgpr_read_b32 %0, a255" : "=v"(v)); break;
-  }
-  return v;
-}
-
-template <bool STATS>
-__global__ __launch_bounds__(256) void gemm_nt4p_kernel(NTArgs a) {
-  constexpr int S_ST = 32 + (STATS ? 2 : 0);   // epilogue store instructions per wave
-  __shared__ __attribute__((aligned(16))) char smem[5 * NT4_SLOT];   // A ring: slots 0-2, B ring: 3-4
-  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
-  const int tiles = gridM * gridN, nwg = gridDim.x;
-  int t = xcd_remap(blockIdx.x, nwg);
-  if (t >= tiles) return;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = w >> 1, wc = w & 1;
-  // LDS-DMA: an operand tile is 256 rows x 128 B; instruction i of wave w fills rows (4i + w) * 8
-  // + [0, 8), lane l the 16-B physical chunk l & 7 of row (4i + w) * 8 + (l >> 3), i.e. logical
-  // chunk (l & 7) ^ ((row >> 1) & 7) -- the same for every i
-  const int lrow = w * 8 + (lane >> 3);
-  const int kc8 = ((lane & 7) ^ ((lrow >> 1) & 7)) * 8;
-  unsigned voA[8], voB[8], vnA[8], vnB[8];   // this tile's / the next tile's row offsets (bytes)
-  auto set_offsets = [&](int tt, unsigned (&oa)[8], unsigned (&ob)[8]) {
-    const int tm = (tt / gridN) * 256, tn = (tt % gridN) * 256;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = lrow + 32 * i;
-      oa[i] = tt < tiles && tm + row < a.M ? (unsigned)(((long)(tm + row) * a.lda + kc8) * 2) : BUF_OOB;
-      ob[i] = tt < tiles && tn + row < a.N ? (unsigned)(((long)(tn + row) * a.ldb + kc8) * 2) : BUF_OOB;
-    }
-  };
-  set_offsets(t, voA, voB);
-  set_offsets(t + nwg, vnA, vnB);
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
-                                                                       BUF_DWORD3);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
-                                                                       BUF_DWORD3);
-  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, BUF_RECORDS, BUF_DWORD3);
-  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(STATS ? (void*)a.stats : a.C, (short)0,
-                                                                       BUF_RECORDS, BUF_DWORD3);
-  const int nk = (a.K + 63) / 64;
-  __builtin_assume(nk >= 2);
-  auto slotA = [&](int g) { return smem + (g % 3) * NT4_SLOT; };
-  auto slotB = [&](int g) { return smem + (3 + (g & 1)) * NT4_SLOT; };
-  // LDS-DMA instruction i of operand op (0: A, 1: B) for the workgroup's K-tile G, which is K-tile
-  // k of this tile (nxt = 0) or of the next one (nxt = 1; out-of-range offsets past the last tile).
-  // The column offset rides in soffset; columns past K get an out-of-range lane offset (zeros).
-  auto issue1 = [&](int op, int G, int k, bool nxt, int i) {
-    char* d = (op ? slotB(G) : slotA(G)) + w * 1024 + i * 4096;
-    const unsigned lim = k * 64 + kc8 < a.K ? 0u : BUF_OOB;
-    const unsigned o = (op ? (nxt ? vnB[i] : voB[i]) : (nxt ? vnA[i] : voA[i])) | lim;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(op ? rB : rA, (__attribute__((address_space(3))) void*)d, 16, o, k * 128,
-                                             0, 0);
-  };
-
-  // accumulator tile (n half h, m fragment i, n fragment j) = C[m0 + wr*128 + 16i + fr]
-  // [n0 + wc*128 + 64h + 16j + 4fg + r] in a[4T + r], T = 32h + 4i + j (mfma_fixed, acc_read)
-  const int fr = lane & 15, fg = lane >> 4;
-  const int aoff = wr * 128 * 128, boff = wc * 128 * 128;
-  auto frag = [&](const char* s, int off, int i, int ks) {
-    return *reinterpret_cast<const bf16x8*>(s + off + swz(i * 16 + fr, ks * 4 + fg));
-  };
-
-#pragma unroll
-  for (int i = 0; i < 8; ++i) issue1(0, 0, 0, false, i);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) issue1(1, 0, 0, false, i);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) issue1(0, 1, 1, false, i);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) issue1(1, 1, 1, false, i);
-  vm_wait(16);   // A(0), B(0) landed
-  __builtin_amdgcn_s_barrier();
-  bf16x8 fb0[8], fa_n0, fa_n1;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) fb0[j] = frag(slotB(0), boff, j, 0);
-  fa_n0 = frag(slotA(0), aoff, 0, 0);
-  fa_n1 = frag(slotA(0), aoff, 1, 0);
-  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), as a real s_waitcnt (see the loop's end)
-
-  // one flat loop over the workgroup's K-tiles (G), tile by tile: the epilogue runs inside it after
-  // a tile's last K-tile (a nested tile loop made the register allocator spill the accumulators)
-  const int total = ((tiles - t + nwg - 1) / nwg) * nk;
-  int kt = 0, m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
-  for (int G = 0; G < total; ++G) {
-    const char* sa = slotA(G);
-    const char* sb = slotB(G);
-    bf16x8 fa[18], fb1[8];
-    fa[0] = fa_n0;
-    fa[1] = fa_n1;
-    // k-step 0: MFMAs on fb0 (the first of a tile from a zero C); B fragments of k-step 1 and A
-    // fragments two groups ahead.  Group order is fixed with sched_barrier, so the waits the
-    // compiler inserts before each group are counted ones.
-    const bool first = kt == 0;
-    static_for<0, 8>([&](auto g) {
-      fa[g + 2] = frag(sa, aoff, (g + 2) & 7, (g + 2) >> 3);
-      fb1[g] = frag(sb, boff, g, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (first)
-        static_for<0, 8>([&](auto j) { mfma_fixed<true, (j >> 2) * 32 + g * 4 + (j & 3)>(fb0[j], fa[g]); });
-      else
-        static_for<0, 8>([&](auto j) { mfma_fixed<false, (j >> 2) * 32 + g * 4 + (j & 3)>(fb0[j], fa[g]); });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // B(G) and A(G-1) fully read by this wave
-    if (kt == 0 && G > 0) vm_wait(S_ST);                 // A(G+1), B(G+1) landed; the previous
-    else wait_vmcnt<0>();                                // tile's stores, issued after, may drain
-    __builtin_amdgcn_s_barrier();
-    // k-step 1: MFMAs on fb1; one LDS-DMA issue per 4 MFMAs (A(G+2) in groups 8-11, B(G+2) in
-    // 12-15), B fragments of K-tile G+1's k-step 0 and A fragments two groups ahead (the last
-    // two from A(G+1))
-    const bool nx = kt + 2 >= nk;
-    const int k2 = nx ? kt + 2 - nk : kt + 2;
-    const char* sa1 = slotA(G + 1);
-    const char* sb1 = slotB(G + 1);
-    static_for<8, 16>([&](auto g) {
-      constexpr int op = g < 12 ? 0 : 1, i0 = (g & 3) * 2;
-      issue1(op, G + 2, k2, nx, i0);
-      fa[g + 2] = g + 2 < 16 ? frag(sa, aoff, (g + 2) & 7, 1) : frag(sa1, aoff, g - 14, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      static_for<0, 4>([&](auto j) { mfma_fixed<false, (g - 8) * 4 + j>(fb1[j], fa[g]); });
-      __builtin_amdgcn_sched_barrier(0);
-      issue1(op, G + 2, k2, nx, i0 + 1);
-      fb0[g - 8] = frag(sb1, boff, g - 8, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      static_for<4, 8>([&](auto j) { mfma_fixed<false, 32 + (g - 8) * 4 + (j - 4)>(fb1[j + 0], fa[g]); });
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    fa_n0 = fa[16];
-    fa_n1 = fa[17];
-    // a real s_waitcnt (not inline asm), so the compiler's wait counting starts the next K-tile
-    // from zero reads in flight instead of a full drain after its first group's reads
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-    if (++kt == nk) {
-      // the epilogue's accumulator reads follow inline-asm MFMAs the hazard recognizer cannot
-      // see: cover the last MFMA's passes explicitly
-      asm volatile("s_nop 7\n s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
-      auto rd = [](auto h) {
-        return [](auto i, auto j, auto r) {
-          return acc_read<decltype(h)::value * 128 + (decltype(i)::value * 4 + decltype(j)::value) * 4 +
-                          decltype(r)::value>();
-        };
-      };
-      epilogue256_get<STATS, true>(rd(IC<0>{}), a, rC, rS, m0, n0, wr, wc * 2, fr, fg);
-      epilogue256_get<STATS, true>(rd(IC<1>{}), a, rC, rS, m0, n0, wr, wc * 2 + 1, fr, fg);
-      kt = 0;
-      t += nwg;
-      m0 = (t / gridN) * 256;
-      n0 = (t % gridN) * 256;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        voA[i] = vnA[i];
-        voB[i] = vnB[i];
-      }
-      set_offsets(t + nwg, vnA, vnB);
-    }
-  }
-  wait_vmcnt<0>();   // the last stores and the zero-filling issues for the (absent) next tile
 }
 
 // ---------------------------------------------------------------------------------
@@ -1783,7 +1194,7 @@ int gpu_cus() {   // compute units of the current device (256 on MI355X)
 
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
-  return tile == 2 || tile == 3 || tile == 5 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
+  return tile == 2 || tile == 3 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
 }
 
 bool tn_big(int dtype, int gmode, int N, int K, int tile) {
@@ -1801,7 +1212,7 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
-  if (tile < 0 || tile > 5) return XCP_EINVAL;
+  if (tile < 0 || tile > 4) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (nt_big(dtype, gmode, M, N, K, tile)) {
     // automatic choice (tile 0): the persistent kernel; tile 4: the automatic choice with the
@@ -1820,13 +1231,7 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     big.M = min(M, mb * 256);
     const bool buf = ((long)(big.M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
     const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
-    if (tile == 5 && buf && cbuf && K > 64) {   // 4-wave persistent kernel, one wave per SIMD
-      const int grid = min(mb * gridN, cus);
-      if (stats)
-        hipLaunchKernelGGL(gemm_nt4p_kernel<true>, dim3(grid), dim3(256), 0, stream, big);
-      else
-        hipLaunchKernelGGL(gemm_nt4p_kernel<false>, dim3(grid), dim3(256), 0, stream, big);
-    } else if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
+    if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
       const int grid = min(mb * gridN, cus);
       if (stats)
         hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);

@@ -121,8 +121,8 @@ DW_REDUCE_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_DW_REDUCE_SIDE", "1")
 # one launch per weight, as they are produced)
 REDUCE_BATCH = os.environ.get("XCP_REDUCE_BATCH", "1") != "0"
 # XCP_NT_ONESHOT=1: the big pointwise GEMMs on the one-shot 256x256 kernel instead of its
-# persistent form (gemm.hip tile 4 vs 0; A/B)
-NT_TILE = 4 if os.environ.get("XCP_NT_ONESHOT", "0") == "1" else 0
+# persistent form (gemm.hip tile 4 vs 0; A/B); XCP_NT_TILE=<t> pins any gemm.hip tile choice for them
+NT_TILE = int(os.environ.get("XCP_NT_TILE", "4" if os.environ.get("XCP_NT_ONESHOT", "0") == "1" else "0"))
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
 # columns in the packed weights, zero BN scale / shift / backward coefficients.  XCP_PAD_728=0

@@ -58,12 +58,11 @@ def test_gemm_nt_stats(ops, gpu, dt, M, N, K):
                                        (77, 64, 288, 288), (513, 264, 40, 40), (92416 // 8, 728, 728, 736),
                                        (4100, 1024, 728, 1456), (46208, 728, 728, 736), (77073, 264, 40, 40),
                                        (92416, 728, 728, 728)])
-@pytest.mark.parametrize("tile", [2, 0, 3, 5])
+@pytest.mark.parametrize("tile", [2, 0, 3])
 def test_gemm_nt256_stats(ops, gpu, M, N, K, lda, tile):
     """The 256x256 8-wave bf16 kernel (tile 2: forced for every size; tile 3: its persistent form,
     one workgroup per CU walking the tiles with the next tile's first K-tile prefetched under the
-    epilogue; tile 5: the 4-wave kernel, one wave per SIMD with 128x128 wave tiles; tile 0:
-    automatic choice, so the large shapes take it and the small ones the 128x128
+    epilogue; tile 0: automatic choice, so the large shapes take it and the small ones the 128x128
     kernel, and a sparse
     last round of 256 tiles -- 46208 and 92416 rows x 728 -- goes to the 128x128 kernel with
     its rows, output and stats rows offset): ragged M / N,
@@ -713,12 +712,12 @@ def test_fused_adam_clip_load_state_dict_resume(ops, gpu):
 
 @pytest.mark.parametrize("M,N,K,ref", [(92416, 736, 736, 0), (5120 * 9, 1024, 736, 0), (2048 * 7 + 256, 512, 64, 2),
                                        (256 * 506 + 77, 256, 200, 2), (256 * 600 + 77, 256, 448, 0)])
-@pytest.mark.parametrize("tile", [3, 5])
-def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref, tile):
-    """The persistent 256x256 kernel (tile 3) and the 4-wave kernel (tile 5) compute every tile
-    with the one-shot kernel's MFMA order: identical output and statistics bits (against tile 0
-    where all send a sparse last round to the 128x128 kernel, tile 2 otherwise), across several
-    tiles per workgroup (the prefetch / epilogue overlap must not change a value)."""
+def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref):
+    """The persistent 256x256 kernel (tile 3) computes every tile with the one-shot kernel's
+    MFMA order: identical output and statistics bits (against tile 0 where both send a sparse
+    last round to the 128x128 kernel, tile 2 otherwise), across several tiles per workgroup
+    (the prefetch / epilogue overlap must not change a value)."""
+    tile = 3
     g = torch.Generator(device=gpu).manual_seed(M + N)
     A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
     B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()

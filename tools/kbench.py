@@ -344,6 +344,22 @@ def main():
             rep(f"unit bwd {Hu}^2 {CO}->{CI} fused", timeit(lambda: ops.unit_bwd(Gu, Yu, cu, Wu, Xu, dDu, Mu, CO, CI, dWu),
                                                            iters=10), byts)
             del Gu, Yu, dYu, Xu, dDu
+    if "fin" in sel:   # BN finalize from the GEMM epilogue's partial rows (forward) and the backward's
+        CP = 736
+        for R in (722, 2888, 90):
+            part = torch.rand(R * 2 * CP, device=dev, generator=g)
+            bnp = {"weight": torch.ones(CP, device=dev), "bias": torch.zeros(CP, device=dev), "track": True,
+                   "running_mean": torch.zeros(CP, device=dev), "running_var": torch.ones(CP, device=dev),
+                   "momentum": 0.1, "eps": 1e-3}
+            out = {k: torch.empty(CP, device=dev) for k in ("mean", "invstd", "scale", "shift")}
+            rep(f"bn finalize R={R} C=728/{CP}", timeit(lambda: ops.finalize_stats(part, R, 728, float(R * 128), bnp, True, out, CP),
+                                                       iters=50), R * 2 * CP * 4)
+            stt = {"mean": torch.zeros(CP, device=dev), "invstd": torch.ones(CP, device=dev)}
+            dg, db = torch.zeros(CP, device=dev), torch.zeros(CP, device=dev)
+            Yd = torch.empty(1, device=dev, dtype=dt)
+            rep(f"bn bwd finalize R={R}", timeit(lambda: ops.bn_backward_coef(None, Yd, R * 128, 728, bnp, stt, dg, db,
+                                                                              part=part, R=R, CP=CP), iters=50),
+                R * 2 * CP * 4)
     if "tail" in sel:
         rep("tail_fwd identity", timeit(lambda: ops.tail_fwd(X, sc, sh, False, D, None, None, Y, None, N, H, W, C)),
             3 * tensor_bytes)
