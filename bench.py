@@ -253,13 +253,14 @@ def cpu_baseline(args, frames):
 
 
 def pmc_traffic():
-    """HBM bytes per launch of the two roofline kernels, from the newest committed
-    ``profiles/*_traffic.json`` (tools/pmc_traffic.py over separate FETCH_SIZE / WRITE_SIZE
-    rocprofv3 passes of this bench, FETCH_SIZE x2 gfx950 correction).  The middle-flow
-    shape is the most frequent dispatch of each kernel, so it is the group with most launches.
-    Returns ({kernel base: (bytes, source)}) or {} when no file exists."""
+    """HBM bytes per launch of the two roofline ops, from the newest committed
+    ``profiles/*_optraffic.json``: separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    (tools/pmc_traffic.py, FETCH_SIZE x2 gfx950 correction) over ``tools/kbench.py roof_ops``, which
+    runs exactly the bench's two timed ops at the step's shape (the pointwise op is the persistent
+    256x256 launch plus the sparse last round on the 128x128 kernel: its bytes are summed over both,
+    as the live timing covers both).  Returns {kernel base: (bytes, source)} or {} when absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_optraffic.json")))
     if not files:
         return {}
     data = json.load(open(files[-1]))
@@ -267,9 +268,11 @@ def pmc_traffic():
     for b in ("gemm_nt", "dw_fwd_kernel"):
         cand = [v for v in data.values() if v.get("base", "").startswith(b)]
         if cand:
-            v = max(cand, key=lambda v: v["launches"])
-            out[b] = (v["traffic_bytes"], f"{os.path.relpath(files[-1], REPO)}: {v['kernel']} grid={v['grid']}, "
-                                          f"2*FETCH_SIZE+WRITE_SIZE mean over {v['launches']} launches")
+            n = max(v["launches"] for v in cand)
+            parts = [v for v in cand if v["launches"] == n]
+            out[b] = (sum(v["traffic_bytes"] for v in parts),
+                      f"{os.path.relpath(files[-1], REPO)}: " + " + ".join(f"{v['kernel']} grid={v['grid']}" for v in parts)
+                      + f", 2*FETCH_SIZE+WRITE_SIZE per op, mean over {n} launches (tools/kbench.py roof_ops)")
     return out
 
 
@@ -554,7 +557,7 @@ def main():
         hm = middle_hw(S)
         M = frames * hm * hm
         roof, extra = None, {}
-        traffic = {} if (audio or single or fusion) else pmc_traffic()   # the committed PMC passes are of the headline bench
+        traffic = {} if (audio or single or fusion) else pmc_traffic()   # the committed PMC passes are of the headline ops
         if timer is not None:
             pw_ms, dw_ms = timer.mean_ms("pw_gemm_728"), timer.mean_ms("dw_fwd_728")
             if pw_ms:

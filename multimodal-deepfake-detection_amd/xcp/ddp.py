@@ -38,12 +38,17 @@ class GradBuckets:
         self.world = world if world is not None else (dist.get_world_size() if dist.is_initialized() else 1)
         self.bucket_elems = max(1, bucket_bytes // 4)
         dev = self.params[0].device
-        self.flat = torch.zeros(sum(p.numel() for p in self.params), device=dev, dtype=torch.float32)
+        # every view starts on a 16-B boundary (slots padded to 4 floats, the padding stays zero):
+        # the batched slab reductions write float4 lanes straight into the .grad views
+        slot = lambda n: (n + 3) // 4 * 4   # noqa: E731
+        self.flat = torch.zeros(sum(slot(p.numel()) for p in self.params), device=dev, dtype=torch.float32)
         self.views = {}
+        self._slot = {}
         off = 0
         for p in reversed(self.params):   # backward order
             self.views[p] = (off, p.numel())
-            off += p.numel()
+            self._slot[p] = slot(p.numel())
+            off += self._slot[p]
         self.overlap = self.world > 1
         self.sync = True   # False: gradient accumulation micro-batch, no all-reduce launched
         self._active_key = None
@@ -68,7 +73,8 @@ class GradBuckets:
         self.buckets, self._bucket_of = [], {}
         cur, start, end = [], None, None
         for p in active:
-            o, n = self.views[p]
+            o, _ = self.views[p]
+            n = self._slot[p]
             if cur and (o != end or end - start + n > self.bucket_elems):
                 self.buckets.append((start, end, cur))
                 cur = []

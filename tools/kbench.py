@@ -106,6 +106,22 @@ def main():
             rep(f"tn rows/split={rps}", timeit(lambda: ops.gemm_tn(Gt, Xt, P, m, 1024, 1024, 16, rps)),
                 flops=2.0 * m * 1024 * 1024)
             del Gt, Xt, P
+    if "roof_ops" in sel:   # the bench's two roofline ops at the step's shape (736 pitch), for the PMC passes
+        CP = 736
+        Xp = torch.zeros(M, CP, device=dev, dtype=dt)
+        Xp[:, :C] = X
+        Yp = torch.empty_like(Xp)
+        Wpp = torch.zeros(CP, CP, device=dev, dtype=dt)
+        Wpp[:C, :C] = Wp
+        Wtp = torch.zeros(9, CP, device=dev)
+        Wtp[:, :C] = Wt
+        scp, shp = torch.zeros(CP, device=dev), torch.zeros(CP, device=dev)
+        scp[:C], shp[:C] = sc, sh
+        stp = torch.empty(ops.nt_stat_rows(M) * 2 * CP, device=dev)
+        rep("roofline op: gemm_nt 736 pitch +stats", timeit(lambda: ops.gemm_nt(Xp, Wpp, Yp, M, CP, CP, stats=stp)),
+            flops=2.0 * M * C * C)
+        rep("roofline op: dw_fwd 736 pitch act=2", timeit(lambda: ops.dw_fwd(2, Xp, Yp, Wtp, scp, shp, N, H, W, CP)),
+            2 * (2 * M * C) + 36 * C)
     if "dwf_only" in sel:     # one kernel for the PMC passes
         rep("dw_fwd act=2", timeit(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
     if "dwb_only" in sel:
