@@ -567,7 +567,8 @@ def main():
                         "frac": round(ach / PEAK_BF16_TFLOPS, 4),
                         "traffic": traffic.get("gemm_nt", (None,))[0],
                         "traffic_source": traffic.get("gemm_nt", (None, None))[1],
-                        "kernel": f"gemm_nt256k64_kernel (bf16 pointwise 1x1 728->728 @{hm}x{hm}, middle flow; "
+                        "kernel": f"gemm_nt256p_kernel + sparse last round on gemm_nt_kernel (the xcp_gemm_nt op: "
+                                  f"bf16 pointwise 1x1 728->728 @{hm}x{hm} with the BN-statistics epilogue, middle flow; "
                                   f"channel pitch {engine.pc(728)}, flops counted for the 728 real channels)",
                         "flops_per_launch": flops, "avg_launch_ms": round(pw_ms, 4), "launches": timer.count("pw_gemm_728")}
             if dw_ms:

@@ -114,6 +114,9 @@ FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
 # cross-checks); by default block1's first depthwise conv applies BN2 + ReLU on load
 STEM_FUSED = os.environ.get("XCP_STEM_FUSED", "1") != "0"
 STEM_WGRAD_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_STEM_WGRAD_SIDE", "1") != "0"
+# BN1's backward coefficients before the side-stream conv2 weight gradient is launched
+# (XCP_STEM_BN1_FIRST=0: after it, the round-2 order; A/B)
+STEM_BN1_FIRST = os.environ.get("XCP_STEM_BN1_FIRST", "1") != "0"
 # depthwise weight-gradient slab reductions on the weight-gradient stream (XCP_DW_REDUCE_SIDE=0:
 # on the main stream right after each depthwise backward)
 DW_REDUCE_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_DW_REDUCE_SIDE", "1") != "0"
@@ -559,7 +562,13 @@ class XceptionEngine:
             ops.conv3x3(1, dC2, pk["conv2T"], dA1, None, N, OH2, OW2)
         else:
             ops.gemm_nt(dC2, pk["conv2T"], dA1, rows1, 32, 576, lda=64, gather=(3, OH1, OW1, OH2, OW2, 1, 64))
-        # conv2's weight gradient on the weight-gradient stream, beside the dgrad chain below
+        # BN1's backward coefficients first (per-channel reduce + finalize on the main stream), then
+        # conv2's weight gradient on the weight-gradient stream beside the rest of the chain (BN1
+        # apply, conv1's weight gradient).  Launched the other way round, the finalize's one
+        # 1024-thread workgroup waited for the side stream's conv2 weight gradient to leave the CUs:
+        # 356 us per step on the main stream (profiles/r03_v3_kernels.txt)
+        if STEM_BN1_FIRST:
+            coef1 = bn_coef(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], None, True)   # relu (Xception.py:170)
         st2 = side if STEM_WGRAD_SIDE else None
         if st2 is not None:
             st2.wait_stream(main)
@@ -578,7 +587,10 @@ class XceptionEngine:
                 ops.permute3(w2g, c2g, 64, 9, 32, (0, 2, 1))
         if st2 is not None:
             keep.append(dC2)
-        dC1 = bn_bwd(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], relu=True)   # relu (Xception.py:170) fused
+        if not STEM_BN1_FIRST:
+            coef1 = bn_coef(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], None, True)
+        dC1 = self._empty(rows1 * pc(32))
+        ops.bn_apply_coef(dA1, S["c1"], dC1, coef1, S["s1"], rows1, pc(32), relu=True)
         c1g, acc = g("conv1.weight", (32, 3, 3, 3))
         ops.conv1_wgrad(S["x"], dC1, c1g, N, S["IH"], S["IW"], accumulate=acc)
         if side is not None:
