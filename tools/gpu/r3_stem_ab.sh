@@ -20,3 +20,4 @@ print(f"{sys.argv[1]:8s} round {sys.argv[2]}: {d['value']:.1f} clips/s  {d['ms_p
 PY
   done
 done
+timeout -k 10 120 python -u tools/kbench.py chanred fin > gpurun_out/sab_kbench.log 2>&1
