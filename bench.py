@@ -502,6 +502,7 @@ def main():
     diag = {"device": torch.cuda.get_device_name(dev)} if args.diag == "on" else None
     if diag is not None:
         diag["clock_mhz_idle"] = round(ops.clock_probe(dev), 1)
+        diag["stream_priority_range"] = list(torch.cuda.Stream.priority_range())
     for mode in modes:
         if rank == 0:
             log(f"{args.model} {mode}: building model")
@@ -515,7 +516,14 @@ def main():
                                      "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == cp and a["H"] == hm})
         steps = args.steps if mode == modes[0] else max(3, args.steps // 2)
         dg = {} if diag is not None else None
-        elapsed, loss = timed(run, steps, args.warmup, world, timer, dg)
+        if os.environ.get("XCP_BENCH_STREAM") == "high":   # A/B: the step on a high-priority stream
+            hs = torch.cuda.Stream(dev, priority=torch.cuda.Stream.priority_range()[1])
+            hs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(hs):
+                elapsed, loss = timed(run, steps, args.warmup, world, timer, dg)
+            torch.cuda.current_stream().wait_stream(hs)
+        else:
+            elapsed, loss = timed(run, steps, args.warmup, world, timer, dg)
         if dg is not None:
             if mode == modes[0]:
                 dg["clock_mhz_after"] = round(ops.clock_probe(dev), 1)

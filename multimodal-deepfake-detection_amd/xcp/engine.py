@@ -114,6 +114,7 @@ FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
 # cross-checks); by default block1's first depthwise conv applies BN2 + ReLU on load
 STEM_FUSED = os.environ.get("XCP_STEM_FUSED", "1") != "0"
 STEM_WGRAD_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_STEM_WGRAD_SIDE", "1") != "0"
+SIDE_PRIO_LOW = os.environ.get("XCP_SIDE_PRIO", "") == "low"
 # BN1's backward coefficients before the side-stream conv2 weight gradient is launched
 # (XCP_STEM_BN1_FIRST=0: after it, the round-2 order; A/B)
 STEM_BN1_FIRST = os.environ.get("XCP_STEM_BN1_FIRST", "1") != "0"
@@ -170,7 +171,11 @@ class XceptionEngine:
     def _side_stream(self, dev):
         st = getattr(self, "_side", None)
         if st is None or st.device != dev:
-            st = self._side = torch.cuda.Stream(dev)
+            # XCP_SIDE_PRIO=low: the weight-gradient stream at the least priority the device offers
+            # (below the default stream's when the range has one), so the dispatcher prefers the
+            # main stream's workgroups (A/B; the default creates it at the default priority)
+            prio = torch.cuda.Stream.priority_range()[0] if SIDE_PRIO_LOW else 0
+            st = self._side = torch.cuda.Stream(dev, priority=prio)
         return st
 
     # ------------------------------------------------------------ parameters
