@@ -19,6 +19,7 @@
 // fully unrolled 3 x (SEGL+2) register window.  FWD_MAXPX (halo pixels per staged
 // tile) trades halo re-reads against workgroups per CU (512: 5 workgroups per CU).
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -408,15 +409,22 @@ XCP_DEV void store_row(T* frame, int h, int W, int C, const RowLanes& rl, const 
   }
 }
 
-template <typename T, int ACT, bool RES>
-__global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
+// Without a residual input (ROLL = false) the three dY rows a step needs (h-1, h, h+1) are read
+// from the LDS ring one row at a time and consumed at once (dgrad and wgrad FMAs of that row), so
+// only one 7-column window is live instead of three rolling ones: 177 -> 140-152 VGPRs, three
+// waves per SIMD instead of two (the dY ring keeps BD + 3 slots: rows h-1 .. h+1 being read, h+2
+// landed, h+3 staged).  With the residual (ROLL = true) the extra ring slots would cost a
+// workgroup per CU (LDS), so the rolling register windows stay: measured 125.2 vs 138.6 us
+// without, 148.1 vs 142.3 us with the residual at 19^2 x 736 (profiles/r03_dwb_ab.txt).
+template <typename T, int ACT, bool RES, bool ROLL>
+__global__ __launch_bounds__(256, ROLL ? 2 : 3) void dw_bwd_lds_kernel(DwBwdArgs a) {
   typedef RV<T> R;
   typedef typename R::V V;
   constexpr int EPT = R::EPT, CPG = 16 * EPT;
-  constexpr int NT_ = RES ? 3 : 2;                       // staged tensors: X, dY (, dRes)
   constexpr int BD = 2;                                  // rows of look-ahead per staged tensor
-  constexpr int NS = BD + 1;
-  __shared__ __attribute__((aligned(16))) char sm[4][NS * NT_ * LROW];
+  constexpr int NS = BD + 1;                             // X / dRes ring slots
+  constexpr int NSG = ROLL ? NS : BD + 3;                // dY ring slots
+  __shared__ __attribute__((aligned(16))) char sm[4][(NS + NSG + (RES ? NS : 0)) * LROW];
   __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];   // output staging (separate object)
   const int ncg = (a.W + RCOLS - 1) / RCOLS;
   const RowMap mp = row_map(a.N, ncg, a.ngroups);
@@ -424,8 +432,8 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
   char* ring = sm[threadIdx.x >> 6];
   char* rx = ring;                  // X rows, slot r % NS
-  char* rg = ring + NS * LROW;      // dY rows, slot r % NS
-  char* rres = ring + 2 * NS * LROW;   // dRes rows (RES)
+  char* rg = ring + NS * LROW;      // dY rows, slot r % NSG
+  char* rres = rg + NSG * LROW;     // dRes rows (RES), slot r % NS
   char* stg = so[threadIdx.x >> 6];
   const int c0 = mp.grp * CPG;
   const int c = c0 + cl * EPT;
@@ -468,7 +476,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
     for (int k = 0; k < RS + 2; ++k) gy[k] = R::unpack(rd(row, k));   // staged zero padding
   };
   auto sx = [&](int r) { return rx + (r % NS) * LROW; };
-  auto sgs = [&](int r) { return rg + (r % NS) * LROW; };
+  auto sgs = [&](int r) { return rg + ((r + NSG) % NSG) * LROW; };   // (r >= -1)
   auto sr = [&](int r) { return rres + (r % NS) * LROW; };
   // VMEM per step h: loads X h+BD, dY h+1+BD (, dRes h+BD) = L, then 2 stores of row h.
   // At step h the rows issued at step h-BD+1 ... are not needed yet; the step-h rows
@@ -477,7 +485,6 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
   constexpr int L = RES ? 6 : 4;
   auto step = [&](int h, const V (&g0)[RS + 2], const V (&g1)[RS + 2], V (&g2)[RS + 2]) {
     char* sxh = sx(h);
-    char* sgn = sgs(h + 1);
     char* srh = sr(h);
     vmwait<2 + (BD - 1) * (L + 2)>();
     // strided-skip gradient terms of this row: plain loads issued before this step's
@@ -511,7 +518,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
       xa[k] = v;
       if (k >= 1 && k <= RS) xr[k - 1] = u;
     }
-    cvtg(sgn, g2);   // dY row h+1
+    if constexpr (ROLL) cvtg(sgs(h + 1), g2);   // dY row h+1
     unsigned pres[RS];
     if constexpr (RES) {
 #pragma unroll
@@ -520,25 +527,47 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
     stage_row<T>(X, h + BD, a.H, a.W, a.C, rl_ld, sx(h + BD), lane);          // slot of X row h-1
     stage_row<T>(G, h + 1 + BD, a.H, a.W, a.C, rl_ld, sgs(h + 1 + BD), lane);   // slot of dY row h
     if constexpr (RES) stage_row<T>(dRes, h + BD, a.H, a.W, a.C, rl_ld, sr(h + BD), lane);
-    // independent accumulation chains: consecutive packed FMAs never depend on each other
+    // dY rows h+1, h, h-1 (ky = 0, 1, 2; row -1 is the zero padding above the frame), one 7-column
+    // window at a time; independent accumulation chains: consecutive packed FMAs never depend on
+    // each other
     V sj[RS];
 #pragma unroll
     for (int j = 0; j < RS; ++j) sj[j] = V(0.f);
+    if constexpr (ROLL) {
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx)
+      for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int j = 0; j < RS; ++j)
+            sj[j] = vfma((ky == 0 ? g2 : ky == 1 ? g1 : g0)[j + 2 - kx], wt[ky * 3 + kx], sj[j]);
+#pragma unroll
+      for (int j = 0; j < RS; ++j)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          dw[kx] = vfma(g2[j + 1], xa[j + kx], dw[kx]);
+          dw[3 + kx] = vfma(g1[j + 1], xa[j + kx], dw[3 + kx]);
+          dw[6 + kx] = vfma(g0[j + 1], xa[j + kx], dw[6 + kx]);
+        }
+    } else {
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        V gw[RS + 2];
+        cvtg(sgs(h + 1 - ky), gw);
+        if (ky == 2 && h == 0) {
+#pragma unroll
+          for (int k = 0; k < RS + 2; ++k) gw[k] = V(0.f);
+        }
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int j = 0; j < RS; ++j) sj[j] = vfma(gw[j + 2 - kx], wt[ky * 3 + kx], sj[j]);
 #pragma unroll
         for (int j = 0; j < RS; ++j)
-          sj[j] = vfma((ky == 0 ? g2 : ky == 1 ? g1 : g0)[j + 2 - kx], wt[ky * 3 + kx], sj[j]);
 #pragma unroll
-    for (int j = 0; j < RS; ++j)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        dw[kx] = vfma(g2[j + 1], xa[j + kx], dw[kx]);
-        dw[3 + kx] = vfma(g1[j + 1], xa[j + kx], dw[3 + kx]);
-        dw[6 + kx] = vfma(g0[j + 1], xa[j + kx], dw[6 + kx]);
+          for (int kx = 0; kx < 3; ++kx) dw[ky * 3 + kx] = vfma(gw[j + 1], xa[j + kx], dw[ky * 3 + kx]);
       }
+    }
 #pragma unroll
     for (int j = 0; j < RS; ++j) {
       V s = sj[j];
@@ -564,9 +593,6 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
     }
     store_row<T>(dX, h, a.W, a.C, rl_st, stg, lane);
   };
-  V g0[RS + 2], g1[RS + 2], g2[RS + 2];
-#pragma unroll
-  for (int k = 0; k < RS + 2; ++k) g0[k] = V(0.f);
   // prologue: X rows 0 .. BD-1, dY rows 0 .. BD, dRes rows 0 .. BD-1
 #pragma unroll
   for (int r = 0; r <= BD; ++r) {
@@ -576,11 +602,19 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
       if (r < BD) stage_row<T>(dRes, r, a.H, a.W, a.C, rl_ld, sr(r), lane);
   }
   vmwait<0>();
-  cvtg(sgs(0), g1);
-  for (int h = 0; h < a.H; h += 3) {
-    step(h, g0, g1, g2);
-    if (h + 1 < a.H) step(h + 1, g1, g2, g0);
-    if (h + 2 < a.H) step(h + 2, g2, g0, g1);
+  if constexpr (ROLL) {
+    V g0[RS + 2], g1[RS + 2], g2[RS + 2];
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) g0[k] = V(0.f);
+    cvtg(sgs(0), g1);
+    for (int h = 0; h < a.H; h += 3) {
+      step(h, g0, g1, g2);
+      if (h + 1 < a.H) step(h + 1, g1, g2, g0);
+      if (h + 2 < a.H) step(h + 2, g2, g0, g1);
+    }
+  } else {
+    V gx[RS + 2];   // (unused by the streaming step)
+    for (int h = 0; h < a.H; ++h) step(h, gx, gx, gx);
   }
   // reduce the 4 lane segments (lanes cl, cl+16, cl+32, cl+48) and write the partials
   float red[EPT][11];
@@ -609,10 +643,20 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_lds_kernel(DwBwdArgs a) {
   }
 }
 
+// XCP_DW_BWD_ROLL=1: the rolling-window form for every variant (the round-2 kernel; A/B)
+bool dw_bwd_roll_all() {
+  static const bool v = [] {
+    const char* e = getenv("XCP_DW_BWD_ROLL");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 template <typename T, int ACT>
 void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true>), dim3(blocks), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false>), dim3(blocks), dim3(256), 0, st, a);
+  if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true>), dim3(blocks), dim3(256), 0, st, a);
+  else if (dw_bwd_roll_all()) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, true>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false>), dim3(blocks), dim3(256), 0, st, a);
 }
 
 template <typename T>
