@@ -21,6 +21,7 @@
 // LDS rows are 128 B (one 64-deep bf16 / 32-deep fp32 K-stage), 16-B chunks
 // XOR-swizzled with (row>>1)&7 so a 16-lane ds_read_b128 group is conflict-free.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -1180,7 +1181,15 @@ namespace {
 // weight gradients on a side stream beside the main stream's dgrad GEMMs and depthwise backward;
 // one 160 KB-LDS workgroup on every CU left those no room, half the CUs (and half the split-K
 // slabs) measured 1.0-1.8 % faster per step for targets 64-192 (profiles/r02_tn_target_sweep.txt).
-constexpr int TN_TARGET_WGS = 128;
+constexpr int TN_TARGET_WGS_DEFAULT = 128;
+int tn_target_wgs() {   // XCP_TN_TARGET_WGS=<n> overrides the default (A/B of the side-stream share)
+  static const int v = [] {
+    const char* e = getenv("XCP_TN_TARGET_WGS");
+    const int n = e ? atoi(e) : 0;
+    return n > 0 ? n : TN_TARGET_WGS_DEFAULT;
+  }();
+  return v;
+}
 
 int gpu_cus() {   // compute units of the current device (256 on MI355X)
   static const int cus = [] {
@@ -1283,7 +1292,7 @@ int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K, int ti
   const bool big = tn_big(dtype, gmode, N, K, tile);
   const int tsz = big ? 256 : 128, align = big ? 64 : 32;
   const int tiles = xcp_cdiv(N, tsz) * xcp_cdiv(K, tsz);
-  const int target = big ? TN_TARGET_WGS : 1024, min_rows = big ? 512 : 256;
+  const int target = big ? tn_target_wgs() : 1024, min_rows = big ? 512 : 256;
   int S = target / (tiles > 0 ? tiles : 1);
   S = S < 1 ? 1 : S;
   const int smax = xcp_cdiv(M, min_rows);
