@@ -35,12 +35,12 @@ struct TileGeo {
   int TH, TW, HP, WP, nth, ntw, nseg;
 };
 
-inline TileGeo tile_geo(int H, int W, int maxpx) {
+inline TileGeo tile_geo(int H, int W, int maxpx, int segl = SEGL) {
   TileGeo g;
   g.ntw = (W + 39) / 40;
   g.TW = (W + g.ntw - 1) / g.ntw;
-  g.nseg = (g.TW + SEGL - 1) / SEGL;
-  g.WP = g.nseg * SEGL + 2;
+  g.nseg = (g.TW + segl - 1) / segl;
+  g.WP = g.nseg * segl + 2;
   int thmax = maxpx / g.WP - 2;
   if (thmax < 1) thmax = 1;
   g.nth = (H + thmax - 1) / thmax;
@@ -215,6 +215,78 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
       if (x < g.TW && tw0 + x < a.W) *reinterpret_cast<unsigned*>(yrow + (long)x * a.C) = pack(o, (T*)nullptr);
     }
   }
+}
+
+// The same forward with two channel dwords (4 bf16 channels) per lane: 8 lanes per 64-B pixel
+// slice, 32 row workers of SG-pixel segments, one 8-B store per output pixel and lane (half the
+// store instructions of dw_fwd_kernel's 4-B stores); the per-channel fma chain is the same, so
+// the outputs are bitwise those of dw_fwd_kernel.
+template <int ACT, int MAXPX, int SG>
+__global__ __launch_bounds__(256) void dw_fwd_w2_kernel(DwArgs a) {
+  constexpr int FS = SLICE, LANES = FS / 8, NWK = 256 / LANES, CPL = 4;
+  __shared__ __attribute__((aligned(16))) char sA[MAXPX * FS];
+  const TileGeo& g = a.g;
+  int grp, n, th0, tw0;
+  block_coords(a.ngroups, g, grp, n, th0, tw0);
+  const int c0 = grp * (FS / 2);
+  const long nbase = (long)n * a.H * a.W;
+  const int cl = threadIdx.x % LANES, wk = threadIdx.x / LANES;
+  const int c = c0 + cl * CPL;
+  const int cc = c < a.C ? c : a.C - CPL;
+  float wt[9][CPL];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) VecIO<float, CPL>::load(a.Wt + (long)t * a.C + cc, wt[t]);
+  stage<bf16, ACT, true, MAXPX, FS>(reinterpret_cast<const bf16*>(a.X), sA, g, nbase, th0, tw0, a.H, a.W, a.C, c0, a.scale,
+                                    a.shift);
+  __syncthreads();
+  if (c >= a.C) return;
+  bf16* Y = reinterpret_cast<bf16*>(a.Y);
+  const int items = g.TH * g.nseg;
+  const char* lbase = sA + cl * 8;
+  for (int it = wk; it < items; it += NWK) {
+    const int r = it / g.nseg, sg = it - r * g.nseg;
+    const int oh = th0 + r;
+    const int x0 = sg * SG;
+    if (oh >= a.H) continue;
+    const char* base = lbase + (r * g.WP + x0) * FS;
+    float win[3][SG + 2][CPL];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int k = 0; k < SG + 2; ++k) {
+        const uint2 u = *reinterpret_cast<const uint2*>(base + (ky * g.WP + k) * FS);
+        unpack(u.x, win[ky][k], (bf16*)nullptr);
+        unpack(u.y, win[ky][k] + 2, (bf16*)nullptr);
+      }
+    bf16* yrow = Y + (nbase + (long)oh * a.W + tw0) * a.C + c;
+#pragma unroll
+    for (int j = 0; j < SG; ++j) {
+      float o[CPL];
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
+        float s = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
+        o[e] = s;
+      }
+      const int x = x0 + j;
+      if (x < g.TW && tw0 + x < a.W)
+        *reinterpret_cast<uint2*>(yrow + (long)x * a.C) = make_uint2(pack(o, (bf16*)nullptr), pack(o + 2, (bf16*)nullptr));
+    }
+  }
+}
+
+// XCP_DW_FWD_W2=<SG>: bf16 64-B-slice forwards through dw_fwd_w2_kernel with SG-pixel segments
+// (4 or 5; A/B)
+int dw_fwd_w2() {
+  static const int v = [] {
+    const char* e = getenv("XCP_DW_FWD_W2");
+    const int k = e ? atoi(e) : 0;
+    return k == 4 || k == 5 ? k : 0;
+  }();
+  return v;
 }
 
 // ---------------------------------------------------------------------------------
@@ -416,12 +488,12 @@ XCP_DEV void store_row(T* frame, int h, int W, int C, const RowLanes& rl, const 
 // landed, h+3 staged).  With the residual (ROLL = true) the extra ring slots would cost a
 // workgroup per CU (LDS), so the rolling register windows stay: measured 125.2 vs 138.6 us
 // without, 148.1 vs 142.3 us with the residual at 19^2 x 736 (profiles/r03_dwb_ab.txt).
-template <typename T, int ACT, bool RES, bool ROLL>
-__global__ __launch_bounds__(256, ROLL ? 2 : 3) void dw_bwd_lds_kernel(DwBwdArgs a) {
+template <typename T, int ACT, bool RES, bool ROLL, int BDV = 2, int MINW = (ROLL ? 2 : 3), bool SKIP = true>
+__global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   typedef RV<T> R;
   typedef typename R::V V;
   constexpr int EPT = R::EPT, CPG = 16 * EPT;
-  constexpr int BD = 2;                                  // rows of look-ahead per staged tensor
+  constexpr int BD = BDV;                                // rows of look-ahead per staged tensor
   constexpr int NS = BD + 1;                             // X / dRes ring slots
   constexpr int NSG = ROLL ? NS : BD + 3;                // dY ring slots
   __shared__ __attribute__((aligned(16))) char sm[4][(NS + NSG + (RES ? NS : 0)) * LROW];
@@ -489,7 +561,7 @@ __global__ __launch_bounds__(256, ROLL ? 2 : 3) void dw_bwd_lds_kernel(DwBwdArgs
     vmwait<2 + (BD - 1) * (L + 2)>();
     // strided-skip gradient terms of this row: plain loads issued before this step's
     // LDS-DMA, so waiting for them never waits for the prefetch
-    const bool skip_row = dSkip && (h % a.sS) == 0 && h / a.sS < a.sOH;
+    const bool skip_row = SKIP && dSkip && (h % a.sS) == 0 && h / a.sS < a.sOH;
     unsigned pskp[RS];
 #pragma unroll
     for (int j = 0; j < RS; ++j) pskp[j] = 0u;
@@ -503,8 +575,10 @@ __global__ __launch_bounds__(256, ROLL ? 2 : 3) void dw_bwd_lds_kernel(DwBwdArgs
       }
     }
     // activated X row h (slot sxh; zero padded after the activation), raw centre values
+    // (at four waves per SIMD the raw centre values are re-read from LDS where the BN sums use them)
+    constexpr bool KEEP_XR = MINW < 4;
     V xa[RS + 2];
-    unsigned xr[RS];
+    unsigned xr[KEEP_XR ? RS : 1];
 #pragma unroll
     for (int k = 0; k < RS + 2; ++k) {
       const unsigned u = rd(sxh, k);
@@ -516,7 +590,8 @@ __global__ __launch_bounds__(256, ROLL ? 2 : 3) void dw_bwd_lds_kernel(DwBwdArgs
         v = vmax0(v);
       }
       xa[k] = v;
-      if (k >= 1 && k <= RS) xr[k - 1] = u;
+      if constexpr (KEEP_XR)
+        if (k >= 1 && k <= RS) xr[k - 1] = u;
     }
     if constexpr (ROLL) cvtg(sgs(h + 1), g2);   // dY row h+1
     unsigned pres[RS];
@@ -585,7 +660,8 @@ __global__ __launch_bounds__(256, ROLL ? 2 : 3) void dw_bwd_lds_kernel(DwBwdArgs
         const bool valid = cok && x0 + j < a.W;
         const V dz = valid ? R::unpack(R::pack(s)) : V(0.f);   // the stored (rounded) dz
         bs1 += dz;
-        bs2 = vfma(dz, (R::unpack(xr[j]) - mu) * is, bs2);
+        const unsigned xraw = KEEP_XR ? xr[KEEP_XR ? j : 0] : rd(sxh, j + 1);
+        bs2 = vfma(dz, (R::unpack(xraw) - mu) * is, bs2);
       }
       if constexpr (RES) s += R::unpack(pres[j]);
       if (skip_row && !a.skip_pre) s += R::unpack(pskp[j]);
@@ -651,11 +727,24 @@ bool dw_bwd_roll_all() {
   }();
   return v;
 }
+// XCP_DW_BWD_OCC4=1: the streaming form with one row of look-ahead (6 ring rows per wave,
+// 39 KB per workgroup) at four waves per SIMD (A/B)
+bool dw_bwd_occ4() {
+  static const bool v = [] {
+    const char* e = getenv("XCP_DW_BWD_OCC4");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 
 template <typename T, int ACT>
 void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true>), dim3(blocks), dim3(256), 0, st, a);
+  if (a.dRes && dw_bwd_occ4() && !a.dSkip)
+    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, false, 1, 3, false>), dim3(blocks), dim3(256), 0, st, a);
+  else if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (dw_bwd_roll_all()) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, true>), dim3(blocks), dim3(256), 0, st, a);
+  else if (dw_bwd_occ4() && !a.dSkip)
+    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 4, false>), dim3(blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false>), dim3(blocks), dim3(256), 0, st, a);
 }
 
@@ -691,6 +780,18 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
     return launch_fwd<float, FWD_MAXPX128, 128>(act, a, stream);
   }
   DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, FWD_MAXPX)};
+  if (dtype == XCP_BF16 && dw_fwd_w2()) {
+    const int sg = dw_fwd_w2();
+    a.g = tile_geo(H, W, FWD_MAXPX, sg);
+    const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
+#define XCP_W2(SGV)                                                                                                  \
+    if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_w2_kernel<ACT_NONE, FWD_MAXPX, SGV>), dim3(blocks), dim3(256), 0, stream, a); \
+    else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_w2_kernel<ACT_RELU, FWD_MAXPX, SGV>), dim3(blocks), dim3(256), 0, stream, a); \
+    else hipLaunchKernelGGL((dw_fwd_w2_kernel<ACT_BNRELU, FWD_MAXPX, SGV>), dim3(blocks), dim3(256), 0, stream, a);
+    if (sg == 4) { XCP_W2(4) } else { XCP_W2(5) }
+#undef XCP_W2
+    return (int)hipGetLastError();
+  }
   if (dtype == XCP_BF16) return launch_fwd<bf16, FWD_MAXPX, 64>(act, a, stream);
   return launch_fwd<float, FWD_MAXPX, 64>(act, a, stream);
 }
