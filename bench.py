@@ -265,7 +265,7 @@ def pmc_traffic():
         return {}
     data = json.load(open(files[-1]))
     out = {}
-    for b in ("gemm_nt", "dw_fwd_kernel"):
+    for b in ("gemm_nt", "dw_fwd"):
         cand = [v for v in data.values() if v.get("base", "").startswith(b)]
         if cand:
             n = max(v["launches"] for v in cand)
@@ -584,9 +584,9 @@ def main():
                 gbs = byts / (dw_ms * 1e-3) / 1e9
                 extra["roofline_dw"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                                         "frac": round(gbs / PEAK_HBM_GBS, 4),
-                                        "traffic": traffic.get("dw_fwd_kernel", (None,))[0],
-                                        "traffic_source": traffic.get("dw_fwd_kernel", (None, None))[1],
-                                        "kernel": f"dw_fwd_kernel<bf16> (depthwise 3x3 C=728 @{hm}x{hm}; channel pitch "
+                                        "traffic": traffic.get("dw_fwd", (None,))[0],
+                                        "traffic_source": traffic.get("dw_fwd", (None, None))[1],
+                                        "kernel": f"dw_fwd_w2_kernel (depthwise 3x3 C=728 @{hm}x{hm}; channel pitch "
                                                   f"{engine.pc(728)}, bytes counted for the 728 real channels)",
                                         "bytes_per_launch": byts, "avg_launch_ms": round(dw_ms, 4)}
         if not audio and not fusion and args.dtype == "bf16":

@@ -278,12 +278,14 @@ __global__ __launch_bounds__(256) void dw_fwd_w2_kernel(DwArgs a) {
   }
 }
 
-// XCP_DW_FWD_W2=<SG>: bf16 64-B-slice forwards through dw_fwd_w2_kernel with SG-pixel segments
-// (4 or 5; A/B)
+// bf16 64-B-slice forwards run dw_fwd_w2_kernel with 5-pixel segments by default: 67 -> 64.5 us
+// at 19^2 x 736, 262 -> 246 at 37^2, 766 -> 733 at 147^2 x 128, bitwise-equal outputs
+// (tools/kbench.py dwshapes fingerprints, profiles/r03_dw_fwd_w2_ab.txt).  XCP_DW_FWD_W2=0 selects
+// dw_fwd_kernel, =4 4-pixel segments (A/B).
 int dw_fwd_w2() {
   static const int v = [] {
     const char* e = getenv("XCP_DW_FWD_W2");
-    const int k = e ? atoi(e) : 0;
+    const int k = e ? atoi(e) : 5;
     return k == 4 || k == 5 ? k : 0;
   }();
   return v;
@@ -727,12 +729,16 @@ bool dw_bwd_roll_all() {
   }();
   return v;
 }
-// XCP_DW_BWD_OCC4=1: the streaming form with one row of look-ahead (6 ring rows per wave,
-// 39 KB per workgroup) at four waves per SIMD (A/B)
+// Default for calls without a strided-skip input: the streaming form with one row of look-ahead
+// (6 ring rows per wave, 39 KB per workgroup, 112-122 VGPRs: four waves per SIMD; with a residual
+// 8 rows, 50 KB, three).  Against the BD = 2 forms at the step's shapes (tools/dw_ab.py,
+// profiles/r03_dw_occ4_ab.txt): 137.0 -> 119.4 us at 19^2 x 736, 154.2 -> 144.0 with the residual,
+// 426 -> 398 at 37^2, 113 -> 96 at 10^2 x 1536; outputs bitwise equal except the residual form's dX
+// (bf16 rounding of the reordered window sum).  XCP_DW_BWD_OCC4=0 keeps the BD = 2 forms (A/B).
 bool dw_bwd_occ4() {
   static const bool v = [] {
     const char* e = getenv("XCP_DW_BWD_OCC4");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }

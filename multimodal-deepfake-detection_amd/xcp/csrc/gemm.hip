@@ -1182,10 +1182,10 @@ namespace {
 // one 160 KB-LDS workgroup on every CU left those no room, half the CUs (and half the split-K
 // slabs) measured 1.0-1.8 % faster per step for targets 64-192 (profiles/r02_tn_target_sweep.txt).
 constexpr int TN_TARGET_WGS_DEFAULT = 128;
-bool tn_xcd_splits() {
+bool tn_xcd_splits() {   // XCP_TN_XCD_SPLITS=1 (A/B; measured -0.3 % in the step, off)
   static const bool v = [] {
     const char* e = getenv("XCP_TN_XCD_SPLITS");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return v;
 }
@@ -1302,10 +1302,10 @@ int xcp_gemm_tn_rows_per_split(int dtype, int gmode, int M, int N, int K, int ti
   const int target = big ? tn_target_wgs() : 1024, min_rows = big ? 512 : 256;
   int S = target / (tiles > 0 ? tiles : 1);
   S = S < 1 ? 1 : S;
-  // 256x256 kernel with few output tiles: a multiple of 8 splits, so that with the kernel's XCD
-  // remap every XCD holds whole splits and a split's row panels are shared by all of its tiles
-  // in one L2 (9 tiles x 14 splits = 126 workgroups put most splits across two XCDs).
-  // XCP_TN_XCD_SPLITS=0 keeps the plain count (A/B).
+  // XCP_TN_XCD_SPLITS=1: for few output tiles a multiple of 8 splits, so that with the kernel's
+  // XCD remap every XCD holds whole splits and a split's row panels are shared by all of its tiles
+  // in one L2 (9 tiles x 14 splits = 126 workgroups put most splits across two XCDs).  Measured in
+  // the step: 399.6-400.4 vs 400.7-401.3 clips/s with the plain count (profiles/r03_ab3.txt): off.
   if (big && tiles <= 16 && S >= 4 && tn_xcd_splits()) S = (S + 4) / 8 * 8;
   const int smax = xcp_cdiv(M, min_rows);
   S = S < smax ? S : smax;

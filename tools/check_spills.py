@@ -14,7 +14,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "multimodal-deepfake-detection_amd", "xcp", "csrc")
 HOT = ("gemm_nt256k64_kernel", "gemm_nt256p_kernel", "gemm_tn256_kernel", "gemm_nt_kernel",
-       "dw_fwd_kernel", "dw_bwd_lds_kernel", "unit_bwd_kernel", "bn_bwd_apply_kernel")
+       "dw_fwd_kernel", "dw_fwd_w2_kernel", "dw_bwd_lds_kernel", "unit_bwd_kernel", "bn_bwd_apply_kernel")
 
 
 def census(src):

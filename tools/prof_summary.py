@@ -101,7 +101,7 @@ def main():
 
 
 # the roofline kernels of bench.py, (kernel base name, grid) at the bench's middle-flow shape
-ROOF = (("gemm_nt256k64_kernel", 523776), ("dw_fwd_kernel", 1507328))
+ROOF = (("gemm_nt256p_kernel", 131072), ("dw_fwd_w2_kernel", 1507328))
 
 
 def contention(path):
