@@ -300,6 +300,18 @@ def main():
             pos = torch.arange(raw.numel(), device=dev).view(raw.shape) % 1000003
             print(f"  fingerprint {int((raw * pos).sum())} {int(raw.sum())}", flush=True)
             del Xs, Ys, raw, pos
+    if "entrygemm" in sel:   # entry-flow forward pointwise GEMMs (+BN stats) on each tile kernel
+        for (Me, Ne, Ke) in ((5531904, 128, 64), (5531904, 128, 128), (1401856, 256, 128), (1401856, 256, 256),
+                             (350464, 736, 256), (350464, 736, 736)):
+            Ae = torch.randn(Me, Ke, device=dev, generator=g).to(dt)
+            Be = (torch.randn(Ne, Ke, device=dev, generator=g) / Ke ** 0.5).to(dt)
+            Ce = torch.empty(Me, Ne, device=dev, dtype=dt)
+            ste = torch.empty(ops.nt_stat_rows(Me), 2, Ne, device=dev)
+            for tl in (1, 2, 3, 0):
+                rep(f"gemm_nt {Me}x{Ne}x{Ke} +stats tile {tl}", timeit(lambda: ops.gemm_nt(Ae, Be, Ce, Me, Ne, Ke, stats=ste,
+                                                                                       tile=tl), iters=10),
+                    2 * Me * (Ke + Ne), flops=2.0 * Me * Ne * Ke)
+            del Ae, Be, Ce, ste
     if "dwbshapes" in sel:   # depthwise backward at the step's shapes (256 frames)
         for (Hs, Cs, act, res) in ((147, 64, 0, False), (147, 128, 2, False), (74, 128, 1, True), (74, 256, 2, False),
                                    (37, 256, 1, True), (37, 736, 2, False), (19, 736, 1, True), (19, 736, 2, False),
