@@ -1208,9 +1208,18 @@ int gpu_cus() {   // compute units of the current device (256 on MI355X)
   return cus;
 }
 
+int nt_big_min_k() {   // XCP_NT_BIG_MINK=<k>: smallest K the automatic choice gives the 256x256 kernel (A/B)
+  static const int v = [] {
+    const char* e = getenv("XCP_NT_BIG_MINK");
+    const int k = e ? atoi(e) : 0;
+    return k > 0 ? k : 384;
+  }();
+  return v;
+}
+
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
-  return tile == 2 || tile == 3 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= 384);
+  return tile == 2 || tile == 3 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= nt_big_min_k());
 }
 
 bool tn_big(int dtype, int gmode, int N, int K, int tile) {
