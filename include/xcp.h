@@ -87,6 +87,14 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
                const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre, void* dX, float* dWpart,
                float* bnpart, const float* bmean, const float* binvstd, int N, int H, int W, int C,
                xcp_stream_t stream);
+/* The same backward with a residual input dRes (no skip input) whose BatchNorm partial sums are
+ * those of the BN whose OUTPUT gradient is the final dX = act'(X) * dA + dRes (an identity-skip block
+ * boundary, Xception.py:95-99: the previous block's last BN feeds both this block's first ReLU and its
+ * residual add): bnpart[P][2][C] = (sum dX, sum dX * (Yb - bmean) * binvstd), dX as stored, Yb that
+ * BN's input.  Replaces the separate per-channel reduce of the backward for that BN. */
+int xcp_dw_bwd_resbn(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
+                     const float* shift, const void* dRes, void* dX, float* dWpart, float* bnpart, const float* bmean,
+                     const float* binvstd, const void* Yb, int N, int H, int W, int C, xcp_stream_t stream);
 
 /* ---- BatchNorm2d (Xception.py:56,67,73,78,119,123,143,147), tails, pooling ---- */
 /* out[g][l] = sum over the g-th of G contiguous groups of slabs s of in[s*ld + l], l < L <= ld

@@ -28,6 +28,7 @@ SIGNATURES = {
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
     "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, I, I, P],
+    "xcp_dw_bwd_resbn": [I, I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_colreduce_f32": [P, I, L, L, P, I, I, P],
     "xcp_colreduce_groups": [I, L],
     "xcp_colreduce_multi": [P, I, P],

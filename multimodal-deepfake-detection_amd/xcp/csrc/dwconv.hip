@@ -314,6 +314,8 @@ struct DwBwdArgs {
   void* dX;
   float* dWpart;          // [P][C][9]
   float* bnpart;          // [P][2][C] or null
+  const void* Yb;         // with dRes: the sums are those of the BN whose output gradient is the final dX
+                          // (after the residual add), zhat = (Yb - mean) * invstd (xcp_dw_bwd_resbn)
   const float* bmean;
   const float* binvstd;
   int N, H, W, C, ngroups;
@@ -517,6 +519,8 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const RowLanes rl_ld = row_lanes_load<T>(a.W, a.C, x0w, c0, lane);
   const RowLanes rl_st = row_lanes_store<T>(a.W, a.C, x0w, c0, lane);
   const bool bnsum = a.bnpart != nullptr;
+  const bool bnres = RES && bnsum && a.Yb != nullptr;   // sums over the final dX against Yb
+  const bool bnx = bnsum && !bnres;                     // sums over the masked dz against X
   V wt[9], dw[9], sc = V(1.f), sh = V(0.f), bs1 = V(0.f), bs2 = V(0.f), mu = V(0.f), is = V(0.f);
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
@@ -567,6 +571,14 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     unsigned pskp[RS];
 #pragma unroll
     for (int j = 0; j < RS; ++j) pskp[j] = 0u;
+    unsigned pyb[RES ? RS : 1];
+    if constexpr (RES) {
+      if (bnres) {   // raw values of the BN input at this row's output pixels (clamped column, masked below)
+        const T* yrow = reinterpret_cast<const T*>(a.Yb) + fbase + (long)h * a.W * a.C + cc;
+#pragma unroll
+        for (int j = 0; j < RS; ++j) pyb[j] = *reinterpret_cast<const unsigned*>(yrow + (long)min(x0 + j, a.W - 1) * a.C);
+      }
+    }
     if (skip_row) {
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
@@ -658,7 +670,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
           s = ctr > 0.f ? s : 0.f;
         }
       }
-      if (bnsum) {
+      if (bnx) {
         const bool valid = cok && x0 + j < a.W;
         const V dz = valid ? R::unpack(R::pack(s)) : V(0.f);   // the stored (rounded) dz
         bs1 += dz;
@@ -667,6 +679,14 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
       }
       if constexpr (RES) s += R::unpack(pres[j]);
       if (skip_row && !a.skip_pre) s += R::unpack(pskp[j]);
+      if constexpr (RES) {
+        if (bnres) {
+          const bool valid = cok && x0 + j < a.W;
+          const V dz = valid ? R::unpack(R::pack(s)) : V(0.f);   // the stored (rounded) dX
+          bs1 += dz;
+          bs2 = vfma(dz, (R::unpack(pyb[j]) - mu) * is, bs2);
+        }
+      }
       *reinterpret_cast<unsigned*>(stg + (sg * RS + j) * SLICE + cl * 4) = R::pack(s);
     }
     store_row<T>(dX, h, a.W, a.C, rl_st, stg, lane);
@@ -809,21 +829,40 @@ int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
   return N * ((W + RCOLS - 1) / RCOLS);
 }
 
-int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
-               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre, void* dX, float* dWpart,
-               float* bnpart, const float* bmean, const float* binvstd, int N, int H, int W, int C, hipStream_t stream) {
+static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
+                       const float* shift, const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre,
+                       void* dX, float* dWpart, float* bnpart, const float* bmean, const float* binvstd, const void* Yb,
+                       int N, int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
-  if (bnpart && (act != ACT_BNRELU || !bmean || !binvstd)) return XCP_EINVAL;
+  if (Yb) {   // sums over the final dX: needs the residual input, no skip input, and the BN's statistics
+    if (!dRes || dSkip || !bnpart || !bmean || !binvstd) return XCP_EINVAL;
+  } else if (bnpart && (act != ACT_BNRELU || !bmean || !binvstd)) {
+    return XCP_EINVAL;
+  }
   DwBwdArgs a{};
   a.dY = dY; a.X = X; a.Wt = Wt; a.scale = scale; a.shift = shift; a.dRes = dRes; a.dSkip = dSkip;
   a.sOH = sOH; a.sOW = sOW; a.sS = sS > 0 ? sS : 1; a.skip_pre = skip_pre != 0; a.dX = dX; a.dWpart = dWpart;
-  a.bnpart = bnpart; a.bmean = bmean; a.binvstd = binvstd;
+  a.bnpart = bnpart; a.bmean = bmean; a.binvstd = binvstd; a.Yb = Yb;
   a.N = N; a.H = H; a.W = W; a.C = C;
   a.ngroups = ngroups_for(C, dtype);
   if (dtype == XCP_BF16) return launch_bwd_lds<bf16>(act, a, stream);
   if (dtype == XCP_F32) return launch_bwd_lds<float>(act, a, stream);
   return XCP_EUNSUPPORTED;
+}
+
+int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale, const float* shift,
+               const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre, void* dX, float* dWpart,
+               float* bnpart, const float* bmean, const float* binvstd, int N, int H, int W, int C, hipStream_t stream) {
+  return dw_bwd_impl(dtype, act, dY, X, Wt, scale, shift, dRes, dSkip, sOH, sOW, sS, skip_pre, dX, dWpart, bnpart, bmean,
+                     binvstd, nullptr, N, H, W, C, stream);
+}
+
+int xcp_dw_bwd_resbn(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
+                     const float* shift, const void* dRes, void* dX, float* dWpart, float* bnpart, const float* bmean,
+                     const float* binvstd, const void* Yb, int N, int H, int W, int C, hipStream_t stream) {
+  return dw_bwd_impl(dtype, act, dY, X, Wt, scale, shift, dRes, nullptr, 0, 0, 1, 0, dX, dWpart, bnpart, bmean, binvstd, Yb,
+                     N, H, W, C, stream);
 }
 
 }  // extern "C"

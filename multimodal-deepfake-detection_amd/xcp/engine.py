@@ -113,6 +113,9 @@ FUSED_UNIT_BWD = os.environ.get("XCP_FUSED_UNIT_BWD", "1") != "0"
 # XCP_STEM_FUSED=0 materialises relu(bn2(conv2)) at full resolution for block1 (A/B and parity
 # cross-checks); by default block1's first depthwise conv applies BN2 + ReLU on load
 STEM_FUSED = os.environ.get("XCP_STEM_FUSED", "1") != "0"
+# an identity-skip block boundary's BN partial sums from the next block's first depthwise backward
+# (xcp_dw_bwd_resbn) instead of a per-channel reduce pass (XCP_RESBN=1; default off until measured)
+RESBN = os.environ.get("XCP_RESBN", "0") == "1"
 STEM_WGRAD_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_STEM_WGRAD_SIDE", "1") != "0"
 SIDE_PRIO_LOW = os.environ.get("XCP_SIDE_PRIO", "") == "low"
 # BN1's backward coefficients before the side-stream conv2 weight gradient is launched
@@ -515,7 +518,7 @@ class XceptionEngine:
             return dY
 
         def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None,
-                     skip_pre=False):
+                     skip_pre=False, res_bn=None):
             """dZ: gradient w.r.t. this unit's BN output (``part``: its fused BN-backward
             partial sums, if the producer emitted them).  Returns (gradient w.r.t. the
             depthwise input after the activation mask (+ residual / skip terms), and -- when
@@ -535,10 +538,11 @@ class XceptionEngine:
             dX = self._empty(M * pc(u.cin))
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
-                             pc(u.cin), dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, bn_stats=prev_st, accumulate=acc,
+                             pc(u.cin), dRes=dRes, dSkip=dSkip, skip_geom=skip_geom,
+                             bn_stats=res_bn[1] if res_bn is not None else prev_st, accumulate=acc,
                              Cw=u.cin, skip_pre=skip_pre, reduce_stream=side if DW_REDUCE_SIDE else None,
-                             keep=keep, batch=rbatch)
-            return dX, (bnp if prev_st is not None else None)
+                             keep=keep, batch=rbatch, res_bn_input=res_bn[0] if res_bn is not None else None)
+            return dX, (bnp if prev_st is not None or res_bn is not None else None)
 
         # ---- exit flow
         H, W = S["xH"], S["xW"]
@@ -551,9 +555,11 @@ class XceptionEngine:
         dX, _ = unit_bwd(u3, e3, dZ3, H, W, part=p3)
         done()
         # ---- blocks, last to first
-        pre_part = None
-        for b, bs in zip(reversed(self.blocks), reversed(S["blocks"])):
-            dX, pre_part = self._block_bwd(b, bs, dX, N, pk, bn_bwd, unit_bwd, wgrad)
+        pre_part = part_in = None
+        for k in range(len(self.blocks) - 1, -1, -1):
+            prev = (self.blocks[k - 1], S["blocks"][k - 1]) if k > 0 else None
+            dX, pre_part, part_in = self._block_bwd(self.blocks[k], S["blocks"][k], dX, N, pk, bn_bwd, unit_bwd,
+                                                    wgrad, part_in, prev)
             done()
         # ---- stem
         OH1, OW1, OH2, OW2 = S["OH1"], S["OW1"], S["OH2"], S["OW2"]
@@ -604,14 +610,18 @@ class XceptionEngine:
         done()
         return grads
 
-    def _block_bwd(self, b, bs, dOut, N, pk, bn_bwd, unit_bwd, wgrad):
+    def _block_bwd(self, b, bs, dOut, N, pk, bn_bwd, unit_bwd, wgrad, part_in=None, prev=None):
+        """part_in: partial sums of this block's last BN (whose output gradient is dOut), produced by
+        the next block's first depthwise backward; prev: (block, forward state) of the block before.
+        Returns (gradient w.r.t. the block input, the stem BN2 partials (block1 only), the partial sums
+        of prev's last BN when this block's first depthwise backward produced them)."""
         H, W, OH, OW = bs["H"], bs["W"], bs["OH"], bs["OW"]
         Ms = N * OH * OW
         units = bs["units"]
         # pooled block: one pass materialises the max-pool gradient (per-quad gather) and
         # reduces it for the last unit's BN backward (1.50 vs 1.58 ms with a separate reduce
         # at 147^2 x 128; gathering it inside the BN-backward kernels measured 1.83 / 1.88 ms)
-        part = None
+        part = None if b.pool else part_in   # (a pooled tail's backward reduces its last BN itself)
         if b.pool:
             dZ = self._empty(N * H * W * pc(b.cout))
             part = ops.maxpool_bwd_bnred(dOut, bs["amax"], dZ, units[-1]["y"], units[-1]["st"], N, H, W, pc(b.cout))
@@ -640,9 +650,18 @@ class XceptionEngine:
                 dZ, part = unit_bwd(u, rec, dZ, H, W, part=part, prev_st=units[i - 1]["st"])
             else:
                 pre = bs["pre_bn"]
-                dZ, pre_part = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, part=part,
-                                        prev_st=pre, skip_pre=pre is not None)
-        return dZ, pre_part
+                # identity-skip boundary: prev's output is BN(y) + its input (no pool after the BN), so
+                # this unit's final dX is the gradient w.r.t. that BN's output
+                res_bn = None
+                if (RESBN and pre is None and dRes is not None and dSkip is None and prev is not None
+                        and not prev[0].pool):
+                    last = prev[1]["units"][-1]
+                    res_bn = (last["y"], last["st"])
+                dZ, out_part = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, part=part,
+                                        prev_st=pre, skip_pre=pre is not None, res_bn=res_bn)
+                pre_part = out_part if pre is not None else None
+                prev_part = out_part if res_bn is not None else None
+        return dZ, pre_part, prev_part
 
 
 class XceptionFunction(torch.autograd.Function):

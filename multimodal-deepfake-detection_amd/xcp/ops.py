@@ -183,7 +183,8 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
 
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
-           bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None, keep=None, batch=None):
+           bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None, keep=None, batch=None,
+           res_bn_input=None):
     """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
     (that BN's Stats) is given, else (None, 0).  dW_out receives the weight gradient in the
     nn.Conv2d [C][1][3][3] order (accumulate: added to it); Cw (default C): channels of the
@@ -193,16 +194,26 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
     keep: a list that receives the scratch the reduce stream reads, for a caller that holds it
     until its stream has waited for the reduce stream (otherwise it is record_stream'ed);
     batch (ReduceBatch): the slab reduction is added to it instead (the caller flushes it after
-    ordering its stream behind this launch, and keeps the scratch alive through ``keep``)."""
+    ordering its stream behind this launch, and keeps the scratch alive through ``keep``).
+    res_bn_input (with dRes, no dSkip; bn_stats then the Stats of that BN): the partial sums are
+    those of the BN whose output gradient is the final dX (after the residual add) and whose input
+    is res_bn_input -- an identity-skip block boundary (xcp_dw_bwd_resbn)."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
     bnpart = None
     if bn_stats is not None:
         bnpart = torch.empty(P * 2 * C, device=dY.device, dtype=torch.float32)
-    _lib.call("xcp_dw_bwd", DT[dY.dtype], act, _p(dY), _p(X), _p(Wt), _p(scale), _p(shift), _p(dRes), _p(dSkip),
-              skip_geom[0], skip_geom[1], skip_geom[2], int(skip_pre), _p(dX), _p(part), _p(bnpart),
-              _p(bn_stats["mean"]) if bn_stats is not None else 0,
-              _p(bn_stats["invstd"]) if bn_stats is not None else 0, N, H, W, C, stream())
+    if res_bn_input is not None:
+        if dRes is None or dSkip is not None or bn_stats is None:
+            raise ValueError("xcp.dw_bwd: res_bn_input needs dRes, no dSkip and the BN's bn_stats")
+        _lib.call("xcp_dw_bwd_resbn", DT[dY.dtype], act, _p(dY), _p(X), _p(Wt), _p(scale), _p(shift), _p(dRes),
+                  _p(dX), _p(part), _p(bnpart), _p(bn_stats["mean"]), _p(bn_stats["invstd"]), _p(res_bn_input),
+                  N, H, W, C, stream())
+    else:
+        _lib.call("xcp_dw_bwd", DT[dY.dtype], act, _p(dY), _p(X), _p(Wt), _p(scale), _p(shift), _p(dRes), _p(dSkip),
+                  skip_geom[0], skip_geom[1], skip_geom[2], int(skip_pre), _p(dX), _p(part), _p(bnpart),
+                  _p(bn_stats["mean"]) if bn_stats is not None else 0,
+                  _p(bn_stats["invstd"]) if bn_stats is not None else 0, N, H, W, C, stream())
     if batch is not None:
         batch.add(part, P, (Cw or C) * 9, dW_out, accumulate, ld=C * 9)
         if keep is not None:

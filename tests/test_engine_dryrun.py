@@ -108,9 +108,12 @@ def fake_lib(monkeypatch):
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])
 @pytest.mark.parametrize("unfrozen", [False, True])
-def test_lstmv_step_call_sequence(fake_lib, unfrozen, prec):
+@pytest.mark.parametrize("resbn", [False, True])
+def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn):
     import xcp
+    from xcp import engine as engine_mod
     from Models.XceptionLSTMV import XceptionLSTMV
+    monkeypatch.setattr(engine_mod, "RESBN", resbn)
     torch.manual_seed(0)
     m = XceptionLSTMV(128, pretrained=False)
     if unfrozen:
@@ -132,6 +135,9 @@ def test_lstmv_step_call_sequence(fake_lib, unfrozen, prec):
         # block1's and block2's units (64/128 -> 128, 128/256 -> 256): fused BN-apply + pointwise
         # dgrad + wgrad in bf16
         assert fake_lib.count("xcp_unit_bwd") == (4 if prec == "bf16" else 0)
+        # identity-skip boundaries (blocks 5-11 after an unpooled block): the previous block's last BN
+        # sums come from the first depthwise backward, not from a per-channel reduce
+        assert fake_lib.count("xcp_dw_bwd_resbn") == (7 if resbn else 0)
         for n, p in m.feature_extractor.named_parameters():
             assert p.grad is not None and p.grad.shape == p.shape, n
     else:

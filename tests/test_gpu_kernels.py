@@ -302,6 +302,42 @@ def test_dw_bwd_residual_and_skip(ops, gpu, dt, N):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("N,C,H", [(3, 128, 15), (701, 64, 19), (256, 736, 19), (4, 200, 7)])
+def test_dw_bwd_resbn(ops, gpu, dt, act, N, C, H):
+    """Identity-skip block boundary (xcp_dw_bwd_resbn): the BN partial sums are taken over the final
+    dX (after the residual add, as stored) against zhat = (Yb - mean) * invstd of the BN that produced
+    the previous block's output; dX and dW equal the plain residual backward's."""
+    W = H
+    g = torch.Generator(device=gpu).manual_seed(N + C + H + act)
+    x = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
+    w = torch.randn(C, 1, 3, 3, device=gpu, generator=g) / 3
+    Wt = w.reshape(C, 9).t().contiguous()
+    sc = torch.rand(C, device=gpu, generator=g) + 0.5
+    sh = torch.randn(C, device=gpu, generator=g) * 0.2
+    dy = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
+    res = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
+    yb = torch.randn(N, C, H, W, device=gpu, generator=g).to(dt)
+    st = {"mean": torch.randn(C, device=gpu, generator=g) * 0.1, "invstd": torch.rand(C, device=gpu, generator=g) + 0.5}
+    base = torch.empty(N * H * W, C, device=gpu, dtype=dt)
+    dW0 = torch.empty(C * 9, device=gpu)
+    ops.dw_bwd(act, nhwc(dy), nhwc(x), Wt, sc, sh, base, dW0, N, H, W, C, dRes=nhwc(res))
+    out = torch.empty_like(base)
+    dW = torch.empty(C * 9, device=gpu)
+    bnpart, P = ops.dw_bwd(act, nhwc(dy), nhwc(x), Wt, sc, sh, out, dW, N, H, W, C, dRes=nhwc(res), bn_stats=st,
+                           res_bn_input=nhwc(yb))
+    assert torch.equal(out, base)
+    torch.testing.assert_close(dW, dW0, rtol=0, atol=0)
+    sums = bnpart.view(P, 2, C).double().sum(0)
+    dX = out.view(N, H, W, C).double()
+    zhat = (yb.permute(0, 2, 3, 1).double() - st["mean"].double()) * st["invstd"].double()
+    torch.testing.assert_close(sums[0], dX.sum((0, 1, 2)), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(sums[1], (dX * zhat).sum((0, 1, 2)), rtol=1e-4, atol=1e-3)
+    with pytest.raises(Exception):   # needs the residual input
+        ops.dw_bwd(act, nhwc(dy), nhwc(x), Wt, sc, sh, out, dW, N, H, W, C, bn_stats=st, res_bn_input=nhwc(yb))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("N,H", [(3, 15), (256, 147)])
 def test_dw_bwd_skip_pre_bnrelu(ops, gpu, dt, N, H):
     """Block1 with the stem's BN2 + ReLU applied on load (engine): the rep's depthwise conv and
