@@ -89,7 +89,7 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
                xcp_stream_t stream);
 /* The same backward with a residual input dRes (no skip input) whose BatchNorm partial sums are
  * those of the BN whose OUTPUT gradient is the final dX = act'(X) * dA + dRes (an identity-skip block
- * boundary, Xception.py:95-99: the previous block's last BN feeds both this block's first ReLU and its
+ * boundary, Xception.py:89-99 (skip = inp, x += skip at :96-98): the previous block's last BN feeds both this block's first ReLU and its
  * residual add): bnpart[P][2][C] = (sum dX, sum dX * (Yb - bmean) * binvstd), dX as stored, Yb that
  * BN's input.  Replaces the separate per-channel reduce of the backward for that BN. */
 int xcp_dw_bwd_resbn(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
