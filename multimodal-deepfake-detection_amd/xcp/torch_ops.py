@@ -226,9 +226,10 @@ def batch_norm_backward(grad: Tensor, x: Tensor, weight: Tensor, mean: Tensor, i
             p = torch.empty(P * 2 * C, device=x.device, dtype=torch.float32)
             ops._lib.call("xcp_bn_bwd_reduce", ops.DT[xc.dtype], gc.data_ptr(), xc.data_ptr(), mean.data_ptr(),
                           invstd.data_ptr(), 0, 0, rows, C, p.data_ptr(), ops.stream())
-            s = p.view(P, 2, C).double().sum(0)
-            db.copy_(s[0])
-            dg.copy_(s[1])
+            s = torch.empty(2 * C, device=x.device, dtype=torch.float32)
+            ops.reduce_slabs(p, P, 2 * C, s)   # colreduce: fp64 sums over the partial rows
+            db.copy_(s[:C])
+            dg.copy_(s[C:])
             scale = (weight.detach().float() * invstd).contiguous()
             ops.bn_act(gc, dx, scale, torch.zeros_like(scale), False, rows, C)
         return dx, dg, db

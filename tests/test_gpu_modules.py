@@ -167,3 +167,33 @@ def test_opcheck_xcp_ops(gpu):
     ]
     for op, args in cases:
         torch.library.opcheck(op, args, test_utils=("test_schema", "test_faketensor", "test_autograd_registration"))
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_batchnorm_module_backward(gpu, training):
+    """xcp.modules.BatchNorm2d (Xception.py:56 and every rep BN) forward + backward against
+    nn.BatchNorm2d in fp32, in training (batch statistics) and eval mode (running statistics: the
+    input gradient is the affine map, dgamma / dbeta from the BN reduce and the colreduce slab sum)."""
+    from xcp.modules import BatchNorm2d
+    torch.manual_seed(3)
+    C = 40
+    ref = nn.BatchNorm2d(C).to(gpu)
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5)
+        ref.bias.normal_()
+        ref.running_mean.normal_()
+        ref.running_var.uniform_(0.5, 2.0)
+    mine = BatchNorm2d(C).to(gpu)
+    mine.load_state_dict(ref.state_dict())
+    ref.train(training)
+    mine.train(training)
+    x = torch.randn(3, C, 9, 11, device=gpu)
+    dy = torch.randn(3, C, 9, 11, device=gpu)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya, yb = ref(xa), mine(xb)
+    ya.backward(dy)
+    yb.backward(dy)
+    torch.testing.assert_close(yb, ya, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(xb.grad, xa.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(mine.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(mine.bias.grad, ref.bias.grad, rtol=1e-4, atol=1e-4)
