@@ -1217,9 +1217,24 @@ int nt_big_min_k() {   // XCP_NT_BIG_MINK=<k>: smallest K the automatic choice g
   return v;
 }
 
+// Outputs at least 256 wide also take the 256x256 kernel from K = 128 (entry-flow forward GEMMs,
+// tools/kbench.py entrygemm, profiles/r03_entrygemm.txt: 1,401,856 x 256 x 128 / 256 297 -> 241 /
+// 400 -> 318 us, 350,464 x 736 x 256 303 -> 219 us); 128-wide outputs stay on the 128x128 kernel
+// (5,531,904 x 128 x 64 / 128: 459 / 567 us there against 552 / 680 on the 256x256 one).
+// XCP_NT_BIG_N256=0 restores the K >= 384 rule alone (A/B).
+bool nt_big_n256() {
+  static const bool v = [] {
+    const char* e = getenv("XCP_NT_BIG_N256");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
-  return tile == 2 || tile == 3 || (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) >= 256 && K >= nt_big_min_k());
+  if (tile == 2 || tile == 3) return true;
+  if (xcp_cdiv(M, 256) * xcp_cdiv(N, 256) < 256) return false;
+  return K >= nt_big_min_k() || (nt_big_n256() && N >= 256 && K >= 128);
 }
 
 bool tn_big(int dtype, int gmode, int N, int K, int tile) {

@@ -21,3 +21,14 @@ timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcoh_fetch -o p -- python tools/kbench.py roof_ops > gpurun_out/h_pmco_f.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcoh_write -o p -- python tools/kbench.py roof_ops > gpurun_out/h_pmco_w.log 2>&1 || exit $?
 python tools/pmc_traffic.py $(find gpurun_out/pmcoh_fetch -name "*counter_collection.csv" | head -1) $(find gpurun_out/pmcoh_write -name "*counter_collection.csv" | head -1) gpurun_out/optraffic_h.json > gpurun_out/h_pmco.log 2>&1
+B="python bench.py --cpu-baseline off --mode unfrozen --small-batch 0 --measured-peaks off --steps 10 --warmup 3 --diag off"
+for r in 1 2 3; do
+  for v in 1 0; do
+    XCP_NT_BIG_N256=$v timeout -k 10 240 $B > gpurun_out/h_n256_${v}_${r}.json 2> gpurun_out/h_n256_${v}_${r}.err || exit $?
+    python - "$v" "$r" <<'PY'
+import json, sys
+d = json.loads(open(f"gpurun_out/h_n256_{sys.argv[1]}_{sys.argv[2]}.json").read().strip().splitlines()[-1])
+print(f"XCP_NT_BIG_N256={sys.argv[1]} round {sys.argv[2]}: {d['value']:.1f} clips/s  {d['ms_per_step']:.2f} ms", flush=True)
+PY
+  done
+done
