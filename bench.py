@@ -533,6 +533,7 @@ def main():
             log(f"{args.model} {mode}: {1e3 * elapsed / steps:.2f} ms/step")
         if diag is not None and mode == "unfrozen" and args.model == "lstmv" and not fusion:
             # the same step with the weight gradients on the main stream (no side-stream overlap)
+            prev_side = engine.WGRAD_SIDE_STREAM
             engine.WGRAD_SIDE_STREAM = False
             try:
                 s2 = max(3, args.steps // 2)
@@ -540,7 +541,7 @@ def main():
                 diag["unfrozen"]["wgrad_main_stream_ms"] = round(1e3 * e2 / s2, 3)
                 log(f"{args.model} {mode}, weight gradients on the main stream: {1e3 * e2 / s2:.2f} ms/step")
             finally:
-                engine.WGRAD_SIDE_STREAM = True
+                engine.WGRAD_SIDE_STREAM = prev_side
         del run
         torch.cuda.empty_cache()
     small = None

@@ -42,9 +42,11 @@ typedef void* xcp_stream_t; /* hipStream_t */
  * gmode: 0 dense rows, 1 strided (skip conv, stride gS), 2 im2col 3x3 p0,
  *        3 transposed im2col (conv input gradient); gC = channels per tap.
  * tile: 0 = automatic (256x256 8-wave kernel for dense bf16 with >= 256 output tiles and
- *       K >= 384 -- its persistent form, one workgroup per CU walking the tiles -- else 128x128),
- *       1 = force 128x128, 2 = force the one-shot 256x256, 3 = force the persistent 256x256
- *       (dense bf16 only), 4 = automatic with the one-shot 256x256 kernel. */
+ *       K >= 384, or outputs >= 256 wide and K >= 128 -- its persistent form, one workgroup
+ *       per CU walking the tiles, with a less than 3/4 full last round of tiles sent to the
+ *       128x128 kernel -- else 128x128), 1 = force 128x128, 2 = force the one-shot 256x256
+ *       for every row, 3 = force the persistent 256x256 for every row (dense bf16 only),
+ *       4 = automatic with the one-shot 256x256 kernel. */
 int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
                 float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, xcp_stream_t stream);
 /* number of partial rows in gemm_nt's stats array for M rows */

@@ -1261,11 +1261,11 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     // One 256x256 tile per CU per round.  When the last round would be less than 3/4 full
     // (1,083 tiles = 4.23 rounds in the middle flow), its rows go to the 128x128 kernel
     // instead: four times as many, smaller tiles, one launch after the full rounds
-    // (tile == 0 only; tile == 2 pins the 256 kernel for every row).
+    // (tile 0 / 4 only; tile 2 pins the one-shot 256 kernel for every row, tile 3 the persistent one).
     const int gridN = xcp_cdiv(N, 256), gridM = xcp_cdiv(M, 256), tiles = gridM * gridN;
     const int cus = gpu_cus();
     int mb = gridM;
-    if (tile != 2 && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3)
+    if ((tile == 0 || tile == 4) && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3)
       mb = (tiles / cus) * cus / gridN;
     NTArgs big = a;
     big.M = min(M, mb * 256);

@@ -21,6 +21,15 @@ it.  A bucket's all-reduce is launched the moment its last gradient is final:
   each block, so the buckets of blocks 12 ... k are reduced while blocks k-1 ... 1
   are still in backward.
 
+Streams.  A bucket's gradients are written by the main (backward) stream and, for the
+pointwise weight gradients, by the engine's weight-gradient side stream.  The all-reduces are
+launched from a dedicated communication stream that waits on both; the main stream never
+waits on the side stream or on a collective before the backward has been enqueued
+(``allreduce()`` makes it wait for the collectives, the engine for its side stream at the
+end of its backward).  Making the main stream wait on the side stream at every completed
+bucket instead would drain the side stream's queued weight-gradient GEMMs mid-backward, about
+once per 25 MB bucket, and give back the overlap the side stream exists for.
+
 Which parameters take part is re-read at every ``zero()``: the reference trains with
 the backbone frozen for three epochs and then unfreezes it (train_visual.py:547-556);
 frozen parameters keep ``grad = None`` (so an optimiser skips them, as in the reference)
@@ -54,6 +63,8 @@ class GradBuckets:
         self._active_key = None
         self._pending = []
         self._hooked = set()
+        self._comm = None
+        self.use_streams = dev.type == "cuda"
         if module is not None:
             self.attach(module)
         self.zero()
@@ -147,12 +158,35 @@ class GradBuckets:
                 self._adopt(p)
         self._pending.append(dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, async_op=True))
 
+    def comm_stream(self):
+        """The stream the bucket all-reduces are launched from (created on first use)."""
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(self.flat.device)
+        return self._comm
+
+    def _launch_from_comm(self, bis, side_stream=None):
+        """All-reduce buckets ``bis`` once the work enqueued so far on the current stream (and on
+        ``side_stream``) is done, without making the current stream wait for anything."""
+        if not bis:
+            return
+        if not self.use_streams:
+            for bi in bis:   # CPU tensors (gloo): no streams
+                self._launch(bi)
+            return
+        comm = self.comm_stream()
+        comm.wait_stream(torch.cuda.current_stream(self.flat.device))
+        if side_stream is not None:
+            comm.wait_stream(side_stream)
+        with torch.cuda.stream(comm):
+            for bi in bis:
+                self._launch(bi)
+
     def ready(self, params, side_stream=None):
         """Gradients of ``params`` are final (enqueued on the current stream, weight gradients
         possibly on ``side_stream``).  Launches the all-reduce of every bucket this completes."""
         if not self.overlap or not self.sync:
             return
-        waited = False
+        full = []
         for p in params:
             if p in self._done or p not in self._bucket_of:
                 continue
@@ -160,10 +194,8 @@ class GradBuckets:
             bi = self._bucket_of[p]
             self._left[bi] -= 1
             if self._left[bi] == 0:
-                if side_stream is not None and not waited:
-                    torch.cuda.current_stream().wait_stream(side_stream)
-                    waited = True
-                self._launch(bi)
+                full.append(bi)
+        self._launch_from_comm(full, side_stream)
 
     def _on_grad(self, p):
         self.ready([p])
@@ -173,11 +205,13 @@ class GradBuckets:
         complete during backward (parameters without a gradient this step) are reduced here."""
         if self.world <= 1:
             return
+        rest = []
         for bi in range(len(self.buckets)):
             if self._left[bi] != 0:
                 self._left[bi] = 0
-                self._launch(bi)
-        for w in self._pending:
+                rest.append(bi)
+        self._launch_from_comm(rest)
+        for w in self._pending:   # the current (main) stream waits for the collectives
             w.wait()
         self._pending = []
         for a, b, _ in self.buckets:

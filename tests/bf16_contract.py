@@ -1,112 +1,110 @@
-"""The bf16 gradient-norm contract of SURVEY.md §8(c) and its measured exceptions.
+"""The bf16 gradient contract of SURVEY.md §8(c), bounded by PyTorch's own bf16 noise.
 
-Contract: in bf16 mode every parameter's gradient norm is within 5e-2 (relative) of the
-reference's fp32 CPU value (tests/golden, captured from the reference itself).
+Contract: in bf16 mode every parameter's gradient norm is within TOL = 5e-2 (relative) of
+the reference's fp32 CPU value (tests/golden, captured from the reference itself) -- or, where
+bf16 arithmetic itself cannot get that close, within K_AUTO x the worst error of R_AUTO
+realizations of PyTorch's own bf16 autocast of the same graph on the same inputs, computed in
+the same test process:
 
-Exceptions: the parameters listed in OVER exceed it, each with the error measured on the
-MI355X (the engine is deterministic: the same inputs give the same bits on every run and
-box) and the bound asserted for it (1.25 x the measured error).  They are the BatchNorm
-affine gradients of the stem and of the first blocks -- dgamma = sum(dz * zhat), dbeta =
-sum(dz) over up to 256 x 147^2 pixels, nearly cancelling sums of bf16 gradients -- and, at the
-16-clip batch, the last head layers, whose ReLU masks flip under the bf16 perturbation of the
-features (the head is also checked against the oracle head on the GPU's own features at
-1e-3).  PyTorch's own bf16 autocast of the same graph shows the same spread
-(test_bf16_gradient_noise_vs_torch_autocast).
+    bound(p) = max(TOL, K_AUTO * max_r err_autocast_r(p))
 
-XCP_BF16_RECORD=1 prints every parameter above 5e-2 per tag without asserting (how the table
-below was measured).
+Why an ensemble and not one autocast run: the error of a bf16 gradient norm is rounding
+noise with a per-parameter scale (largest for the BatchNorm affine gradients of the stem and
+the first blocks -- dgamma = sum(dz * zhat), dbeta = sum(dz) over up to 256 x 147^2 pixels,
+nearly cancelling sums -- and for head layers whose ReLU masks flip under the feature noise).
+Two single draws of the same noise differ by more than 1.5x in 37 % of the cases, so a
+one-sample bound fails on noise; against the worst of 6 draws, an equally noisy path exceeds
+2.5x with probability 0.7 % per parameter (3 % if it were 1.5x noisier), while a real defect
+(an error many times the noise) does not pass.
+
+The realizations are decorrelated without changing the answer: the input clip is scaled by c
+(SCALES) and conv1's weight by 1/c inside the graph (scaled_input). conv1 is linear and has no
+bias, so in exact arithmetic its output, every later activation, the loss and every gradient
+(including conv1's, through the 1/c) are independent of c -- fp64 agrees to 1e-15, fp32 to its
+own rounding noise (<= 1.1e-3 on BN affine sums; test_bf16_contract_cpu.py) -- while every bf16 rounding from the input on falls
+differently.  (Scaling the input alone relies on bn1's scale invariance, which its eps breaks by
+up to 2 % on nearly cancelling BN gradients: not used.)
+
+The autocast graph is the oracle's functional restatement of the reference
+(oracle/xception_oracle.py) run on the GPU under torch.autocast("cuda", bfloat16) -- MIOpen /
+hipBLASLt convolutions in bf16, BatchNorm in fp32 -- with the head / loss in fp32 as in the xcp
+path.  It is test infrastructure (the checker); the path under test never calls it.
+
+XCP_BF16_RECORD=1 prints every parameter above TOL with its bound and does not assert.
 """
 import os
 
+import numpy as np
+import torch
+
 TOL = 5e-2
+K_AUTO = 2.5
+R_AUTO = 6
+# input scales of the autocast realizations (none a power of two apart)
+SCALES = (1.0, 1.0905, 0.8377, 1.2613, 0.9311, 1.1779, 0.7457, 1.3573)
 RECORD = os.environ.get("XCP_BF16_RECORD") == "1"
 
-# tag -> {parameter: bound}; bound = 1.25 x the measured error (round 3, MI355X)
-OVER = {
-    'backbone64': {
-        'bn1.weight': 0.161,
-        'block2.rep.5.bias': 0.11,
-        'block2.skipbn.bias': 0.11,
-        'block1.rep.4.weight': 0.093,
-        'block1.rep.1.weight': 0.089,
-        'block2.rep.5.weight': 0.084,
-        'bn2.weight': 0.077,
-        'bn2.bias': 0.07,
-        'block2.skipbn.weight': 0.068,
-        'block1.skipbn.bias': 0.066,
-        'block1.rep.4.bias': 0.065,
-        'block1.rep.1.bias': 0.064,
-    },
-    'lstmv_b2t4_unfrozen': {
-        'feature_extractor.bn2.bias': 0.132,
-        'feature_extractor.block1.rep.4.weight': 0.114,
-        'feature_extractor.bn2.weight': 0.095,
-        'feature_extractor.bn1.weight': 0.092,
-        'feature_extractor.block9.rep.2.weight': 0.082,
-        'feature_extractor.block2.rep.2.bias': 0.082,
-        'feature_extractor.block10.rep.2.weight': 0.081,
-        'feature_extractor.block6.rep.2.bias': 0.071,
-        'feature_extractor.block1.rep.1.weight': 0.069,
-    },
-    'lstmv_b4t16': {
-        'feature_extractor.bn2.weight': 0.16,
-        'feature_extractor.bn2.bias': 0.103,
-        'feature_extractor.bn1.bias': 0.097,
-        'feature_extractor.block7.rep.5.bias': 0.086,
-        'feature_extractor.block1.rep.4.weight': 0.08,
-        'feature_extractor.block5.rep.8.bias': 0.065,
-        'feature_extractor.block6.rep.8.bias': 0.064,
-        'feature_extractor.block2.rep.2.weight': 0.064,
-    },
-    'lstmv_b16t16': {
-        'feature_extractor.bn1.weight': 0.285,
-        'feature_extractor.bn2.weight': 0.11,
-        'feature_extractor.block1.skipbn.weight': 0.093,
-        'fc_layers.9.bias': 0.089,
-        'feature_extractor.block3.rep.2.bias': 0.086,
-        'fc_layers.9.weight': 0.079,
-        'feature_extractor.block2.rep.5.weight': 0.074,
-        'feature_extractor.bn1.bias': 0.069,
-        'feature_extractor.block2.rep.2.weight': 0.067,
-        'feature_extractor.block5.rep.2.weight': 0.067,
-        'feature_extractor.block8.rep.8.weight': 0.067,
-        'feature_extractor.block4.rep.2.bias': 0.065,
-        'grad/lstm.bias_ih_l0': 0.527,
-        'grad/fc_out.weight': 0.114,
-    },
-    'xception_c1_b4': {
-        'bn2.weight': 0.349,
-        'block1.rep.4.bias': 0.169,
-        'block1.skipbn.bias': 0.169,
-        'bn1.weight': 0.122,
-        'bn2.bias': 0.117,
-        'block1.rep.1.bias': 0.086,
-        'block8.rep.5.bias': 0.078,
-        'block1.skipbn.weight': 0.069,
-        'grad/fc.weight': 0.137,
-    },
-    'xception_c2_b64': {
-        'bn1.bias': 0.523,
-        'bn1.weight': 0.165,
-        'block1.rep.1.bias': 0.138,
-        'block1.rep.1.weight': 0.097,
-        'block2.skipbn.weight': 0.083,
-        'bn2.weight': 0.075,
-        'block4.rep.2.weight': 0.071,
-        'conv1.weight': 0.063,
-        'block3.rep.5.bias': 0.063,
-        'block3.skipbn.bias': 0.063,
-    },
-}
+
+def relerr(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def check(tag, errs, skip=()):
-    """errs: {parameter: relative gradient-norm error vs the reference}; skip: names checked
-    elsewhere.  Asserts the contract with this tag's exceptions."""
-    over = sorted(((n, e) for n, e in errs.items() if e > TOL and n not in skip), key=lambda kv: -kv[1])
-    print(f"\nbf16 gradient norms above {TOL} [{tag}]: {{" + ", ".join(f"{n!r}: {e:.4f}" for n, e in over) + "}")
+def autocast_errors(sd, loss_fn, ref_norms, ref_elem=None, trainable=None, R=R_AUTO):
+    """PyTorch bf16 autocast realizations of the oracle graph.
+
+    sd: {state_dict key: tensor on the GPU} (the initial state of the model under test);
+    loss_fn(params, scale) -> scalar loss, the graph with its backbone under autocast and the
+    input scaled by `scale`; ref_norms: {param: reference fp32 gradient norm};
+    ref_elem: {param: reference fp32 gradient array} for element-wise checks; trainable:
+    names that get gradients (default: the keys of ref_norms).
+    Returns ({param: [norm rel err per realization]}, {param: [element-wise rel err ...]})."""
+    trainable = set(ref_norms if trainable is None else trainable)
+    norms = {n: [] for n in ref_norms}
+    elem = {n: [] for n in (ref_elem or {})}
+    for c in SCALES[:R]:
+        params = {k: (v.detach().clone().requires_grad_(True) if k in trainable else v.detach().clone())
+                  for k, v in sd.items()}
+        loss_fn(params, c).backward()
+        for n in norms:
+            gn = params[n].grad.double().norm().item()
+            norms[n].append(abs(gn - float(ref_norms[n])) / max(float(ref_norms[n]), 1e-30))
+        for n in elem:
+            elem[n].append(relerr(params[n].grad.cpu(), ref_elem[n]))
+        del params
+    torch.cuda.synchronize()
+    return norms, elem
+
+
+def scaled_input(params, x, c, prefix=""):
+    """(params with conv1.weight -> conv1.weight / c, x * c): the same function of the leaves,
+    different bf16 roundings."""
+    q = dict(params)
+    q[prefix + "conv1.weight"] = params[prefix + "conv1.weight"] / c
+    return q, x * c
+
+
+def bound(name, auto):
+    """max(TOL, K_AUTO x the worst autocast error of `name`) (TOL when auto has no entry)."""
+    if not auto or name not in auto or not auto[name]:
+        return TOL
+    return max(TOL, K_AUTO * max(auto[name]))
+
+
+def check(tag, errs, auto=None, skip=()):
+    """errs: {parameter: relative gradient-norm (or element-wise) error vs the reference};
+    auto: autocast_errors' per-parameter realizations (None: TOL for every parameter);
+    skip: names checked elsewhere."""
+    rows = sorted(((n, e, bound(n, auto)) for n, e in errs.items() if n not in skip), key=lambda r: -r[1])
+    over = [r for r in rows if r[1] > TOL]
+    print(f"\nbf16 errors above {TOL} [{tag}] (name, xcp, bound, autocast worst): {{"
+          + ", ".join(f"{n!r}: ({e:.4f}, {b:.4f}, {max(auto[n]) if auto and n in auto else float('nan'):.4f})"
+                      for n, e, b in over) + "}")
+    if auto:
+        ratio = sorted(((n, e / max(max(auto[n]), 1e-12)) for n, e, _ in rows if n in auto and e > TOL),
+                       key=lambda r: -r[1])[:5]
+        print(f"largest xcp / autocast-worst ratios among those [{tag}]:", [(n, round(x, 2)) for n, x in ratio])
     if RECORD:
         return
-    table = OVER.get(tag, {})
-    bad = [(n, round(e, 4), table.get(n, TOL)) for n, e in errs.items() if n not in skip and e > table.get(n, TOL)]
-    assert not bad, f"bf16 gradient norms outside the contract [{tag}]: {bad}"
+    bad = [(n, round(e, 4), round(b, 4)) for n, e, b in rows if e > b]
+    assert not bad, f"bf16 errors outside the contract [{tag}]: {bad}"

@@ -257,6 +257,98 @@ def test_sink_allreduce_overlaps_backbone_backward():
             assert torch.all(gr == 1.5), n
 
 
+class _FakeStream:
+    """A recording stand-in for torch.cuda.Stream on the CPU: wait_stream logs
+    (waiter, waited-on, number of library calls enqueued so far)."""
+    log, calls, current, n = [], None, None, 0
+
+    def __init__(self, device=None, priority=0, name=None):
+        _FakeStream.n += 1
+        self.device, self.name, self.cuda_stream = device, name or f"s{_FakeStream.n}", 0
+
+    def wait_stream(self, other):
+        _FakeStream.log.append((self.name, other.name, len(_FakeStream.calls)))
+
+
+def _install_fake_streams(calls):
+    _FakeStream.log, _FakeStream.calls = [], calls
+    _FakeStream.current = _FakeStream(name="main")
+
+    @contextlib.contextmanager
+    def stream(s):
+        prev, _FakeStream.current = _FakeStream.current, s
+        try:
+            yield
+        finally:
+            _FakeStream.current = prev
+
+    torch.cuda.Stream = _FakeStream
+    torch.cuda.stream = stream
+    torch.cuda.current_stream = lambda *a, **k: _FakeStream.current
+
+
+def _streams_worker(rank, world, port, out):
+    """gloo rank: the engine with its weight-gradient side stream (recording fake streams) and
+    GradBuckets launching bucket all-reduces from its communication stream."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class _MP:
+        def setattr(self, obj, name, val):
+            setattr(obj, name, val)
+
+    calls = install_fake_lib(_MP())
+    FILL["v"] = float(rank + 1)
+    from xcp import ddp, engine
+    engine.WGRAD_SIDE_STREAM = True
+    _install_fake_streams(calls)
+    from Models.Xception import xception
+    torch.manual_seed(0)
+    m = xception(num_classes=1)
+    m.fc = nn.Identity()
+    params = list(m.parameters())
+    launched = []
+    real = ddp.dist.all_reduce
+
+    def logged(t, *a, **k):
+        launched.append((len(calls), _FakeStream.current.name))
+        return real(t, *a, **k)
+
+    ddp.dist.all_reduce = logged
+    gb = ddp.GradBuckets(params, bucket_bytes=1 << 20, world=world, module=m)
+    gb.use_streams = True
+    gb.zero()
+    m(torch.rand(2, 3, 71, 71)).sum().backward()
+    last_dw = max(i for i, c in enumerate(calls) if c == "xcp_dw_bwd")
+    gb.allreduce()
+    comm = gb.comm_stream().name
+    out[rank] = {"log": list(_FakeStream.log), "launched": launched, "last_dw": last_dw, "comm": comm,
+                 "buckets": len(gb.buckets), "grads_ok": all(torch.all(p.grad == 1.5).item() for p in params)}
+    dist.destroy_process_group()
+
+
+def test_bucket_allreduce_does_not_stall_main_stream():
+    """world 2 (gloo), fake kernels, recording fake streams: every bucket
+    all-reduce is launched from GradBuckets' communication stream, which waits on the main and
+    the weight-gradient side stream; the main stream is never made to wait on the side stream
+    before the backbone backward has been enqueued (only the engine's own wait at its end), and
+    every backbone gradient is the mean over ranks."""
+    world, port = 2, 29700 + os.getpid() % 1000
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_streams_worker, args=(world, port, out), nprocs=world, join=True)
+    for rank in range(world):
+        r = out[rank]
+        assert r["grads_ok"]
+        assert all(st == r["comm"] for _, st in r["launched"]), r["launched"]
+        during = [n for n, _ in r["launched"] if n <= r["last_dw"]]
+        assert len(during) >= r["buckets"] - 2, r
+        main_waits_side = [n for w, o, n in r["log"] if w == "main" and o not in ("main", r["comm"])]
+        assert all(n > r["last_dw"] for n in main_waits_side), (main_waits_side, r["last_dw"])
+        comm_waits = {o for w, o, n in r["log"] if w == r["comm"]}
+        assert "main" in comm_waits and len(comm_waits) == 2, comm_waits   # main + the side stream
+
+
 def _cpu_replicate(net):
     """torch.nn.parallel.replicate for one replica, on the CPU (the real one broadcasts over
     CUDA devices): every module through _replicate_for_data_parallel, parameters as non-leaf

@@ -88,6 +88,53 @@ def test_gemm_nt256_stats(ops, gpu, M, N, K, lda, tile):
     torch.testing.assert_close(part[r, 0].double(), Cs[128 * r:].sum(0), rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,N,K,lda", [(1_401_856, 256, 128, 128), (1_401_856, 256, 256, 256),
+                                       (350_464, 736, 256, 256), (5_531_904 // 4, 128, 128, 128)])
+def test_gemm_nt_entry_flow_shapes_vs_fp64(ops, gpu, M, N, K, lda):
+    """The entry-flow forward pointwise GEMMs of the bench step (256 frames: 74^2 x 128->256,
+    74^2 x 256->256, 37^2 x 256->736 pitch; and a 147^2 x 128->128 slice) under the automatic
+    tile choice (tile 0: since round 3 the persistent 256x256 kernel + the sparse-round 128x128
+    tail for outputs >= 256 wide) and pinned to the 128x128 kernel (tile 1), against an fp64
+    product of the same bf16 operands:
+      C: every element is one of the two bf16 neighbours of the fp64 value (fp32 accumulation
+         error is far below a bf16 ulp), and >= 99 % are the round-to-nearest one;
+      BN partial sums (the epilogue's per-128-row sum / sum of squares of the stored bf16 C):
+         equal to an fp64 sum of the stored C to fp32 summation error, and the two tiles' column
+         sums agree with each other and with the fp64 product's to bf16 rounding noise."""
+    g = torch.Generator(device=gpu).manual_seed(M + N + K)
+    A = (torch.rand(M, lda, device=gpu, generator=g) - 0.25).bfloat16()   # post-ReLU-like, nonzero mean
+    B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
+    ref = A[:, :K].double() @ B.double().t()
+    rb = ref.to(torch.bfloat16).double()
+    # bf16 spacing at |ref|, plus a rigorous fp32 accumulation bound (K u32 sum|a||b|) for the
+    # elements whose value nearly cancels
+    lim = (ref.abs().clamp_min(1e-30).log2().floor() - 7).exp2()
+    lim += (A[:, :K].float().abs() @ B.float().abs().t()).double() * (K * 2.0 ** -24)
+    R = ops.nt_stat_rows(M)
+    sums = {}
+    for tile in (0, 1):
+        C = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        part = torch.full((R, 2, N), float("nan"), device=gpu)
+        ops.gemm_nt(A, B, C, M, N, K, lda=lda, stats=part, tile=tile)
+        torch.cuda.synchronize()
+        Cd = C.double()
+        assert not torch.isnan(Cd).any()
+        d = (Cd - ref).abs()
+        assert (d <= lim * 1.0001).all(), (tile, (d / lim).max().item())
+        nearest = (Cd == rb).double().mean().item()
+        assert nearest >= 0.99, (tile, nearest)
+        s = part.double().sum(0)
+        torch.testing.assert_close(s[0], Cd.sum(0), rtol=1e-5, atol=1e-5 * Cd.abs().sum(0).max().item())
+        torch.testing.assert_close(s[1], (Cd * Cd).sum(0), rtol=1e-5, atol=1e-3)
+        sums[tile] = s
+        del C, part, Cd, d
+    # the stats of the two kernels: same stored values up to the 1 % of elements rounded the other way
+    scale0 = (ref.abs().sum(0) * 2.0 ** -8)
+    assert ((sums[0][0] - sums[1][0]).abs() <= scale0 * 0.05 + 1e-6).all()
+    assert ((sums[0][0] - ref.sum(0)).abs() <= scale0 * 0.05 + 1e-6).all()
+    torch.testing.assert_close(sums[0][1], (ref * ref).sum(0), rtol=2e-3, atol=0)
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 def test_gemm_nt_strided_gather(ops, gpu, dt):
     N, H, W, Cin, Cout = 3, 37, 37, 256, 728

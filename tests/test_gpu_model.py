@@ -9,10 +9,10 @@ Stated tolerances:
               fp64 evaluation of the same graph by 1.7e-3 on bn1.bias),
               total gradient norm rel <= 1e-3.
   bf16 mode : feature cosine >= 0.999, logits abs <= 3e-2, loss rel <= 2e-2,
-              total gradient norm rel <= 5e-2, every conv / linear / LSTM
-              weight-gradient norm rel <= 5e-2, BatchNorm affine gradient
-              norms too, except the parameters tests/bf16_contract.py lists with their
-              measured errors.
+              total gradient norm rel <= 5e-2, every gradient norm rel <=
+              max(5e-2, 2.5 x the worst of 6 realizations of PyTorch's own
+              bf16 autocast of the same graph on the same inputs, computed in the test:
+              tests/bf16_contract.py).
   after one optimiser step (Adam's first step moves every element by ~lr * sign(g)):
               the parameter sums may differ from the reference's by 2 * lr per element
               whose gradient sign differs; fp32 allows 0.2 % of the elements, bf16 (head
@@ -52,10 +52,10 @@ def is_head(n):
     return n.startswith(("lstm.", "fc_layers.", "fc_out."))
 
 
-def check_gradnorms(errs, bn_names, f32, skip_head=False, tag=None):
+def check_gradnorms(errs, bn_names, f32, skip_head=False, tag=None, auto=None):
     """errs: {param: rel err of grad norm}.  fp32: 1e-3 (BatchNorm affine 5e-3).  bf16: the
-    SURVEY 8c contract of 5e-2 with the measured exceptions of tests/bf16_contract.py under
-    ``tag``.  skip_head (bf16): the LSTM / FC head is checked against the oracle head on the
+    SURVEY 8c contract of 5e-2, or K x the worst of the autocast realizations ``auto``
+    (tests/bf16_contract.py).  skip_head (bf16): the LSTM / FC head is checked against the oracle head on the
     GPU's own features instead (check_head_on_features): at 2-4 clips its gradients react to
     the bf16 perturbation of the features through the head's ReLU masks (a property of the
     random-init head at a few clips, not of a kernel)."""
@@ -66,7 +66,35 @@ def check_gradnorms(errs, bn_names, f32, skip_head=False, tag=None):
             assert e < (5e-3 if n in bn_names else 1e-3), (n, e)
         return
     import bf16_contract
-    bf16_contract.check(tag, errs, skip=[n for n in errs if skip_head and is_head(n)])
+    bf16_contract.check(tag, errs, auto, skip=[n for n in errs if skip_head and is_head(n)])
+
+
+def autocast_backbone_errors(sd, x, tail, ref_norms, ref_elem=None, prefix=""):
+    """bf16_contract.autocast_errors for a graph = the oracle backbone on the frames ``x``
+    ([N,3,H,W]; x * c and conv1.weight / c per realization) under torch.autocast(bfloat16), then ``tail(feats fp32,
+    params) -> loss`` in fp32 (the head, as the xcp path runs it)."""
+    import bf16_contract
+    from oracle import xception_oracle as O
+
+    def loss_fn(params, c):
+        q, xc = bf16_contract.scaled_input(params, x, c, prefix)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            f = O.backbone_forward(xc, q, True, {}, prefix=prefix)
+        return tail(f.float(), params)
+    return bf16_contract.autocast_errors(sd, loss_fn, ref_norms, ref_elem)
+
+
+def lstmv_tail(B, T, y):
+    from oracle import xception_oracle as O
+
+    def tail(f, params):
+        prob, _ = O.head_forward(f.view(B, T, -1), params)
+        return nn.BCELoss()(prob, y)
+    return tail
+
+
+def snapshot(m):
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
 
 
 def check_head_on_features(m, feats, y, head_grads):
@@ -110,6 +138,7 @@ def test_backbone64_vs_reference(gpu, golden, prec):
     m = xception(num_classes=1000)
     m.fc = nn.Identity()
     m = m.to(gpu).train()
+    sd0 = snapshot(m)
     x = seeded_uniform((4, 3, 64, 64), 1234).to(gpu)
     with xcp.precision(prec):
         f = m(x)
@@ -126,7 +155,11 @@ def test_backbone64_vs_reference(gpu, golden, prec):
             key = f"gradnorm/{n}"
             if key in g:
                 errs[n] = abs(p.grad.double().norm().item() - g[key]) / max(g[key], 1e-30)
-        check_gradnorms(errs, bn_param_names(m), prec == "fp32", tag="backbone64")
+        auto = None
+        if prec != "fp32":
+            auto, _ = autocast_backbone_errors(sd0, x, lambda f, p: (f * r).sum(),
+                                               {n: g[f"gradnorm/{n}"] for n in errs})
+        check_gradnorms(errs, bn_param_names(m), prec == "fp32", tag="backbone64", auto=auto)
         for n, t in m.state_dict().items():
             if "running_var" in n:
                 np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"],
@@ -158,6 +191,7 @@ def test_xceptionlstmv_train_step_vs_reference(gpu, golden, prec, mode):
             p.requires_grad = True
     m = m.to(gpu).train()
     m.fc_layers.eval()
+    sd0 = snapshot(m)
     logits = {}
     m.fc_out.register_forward_hook(lambda mod, i, o: logits.__setitem__("v", o.detach()))
     x = seeded_uniform((B, T, 3, S, S), 1234).to(gpu)
@@ -184,7 +218,12 @@ def test_xceptionlstmv_train_step_vs_reference(gpu, golden, prec, mode):
             continue
         errs[n] = abs(p.grad.double().norm().item() - g[key]) / max(g[key], 1e-30)
         tot += (p.grad.double() ** 2).sum().item()
-    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not f32, tag=f"lstmv_b2t4_{mode}")
+    auto = None
+    if not f32 and mode == "unfrozen":
+        auto, _ = autocast_backbone_errors(sd0, x.reshape(B * T, 3, S, S), lstmv_tail(B, T, y),
+                                           {n: g[f"{mode}/gradnorm/{n}"] for n in errs if not is_head(n)},
+                                           prefix="feature_extractor.")
+    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not f32, tag=f"lstmv_b2t4_{mode}", auto=auto)
     if not f32:
         check_head_on_features(m, feats, y, {n: p.grad for n, p in m.named_parameters() if is_head(n)})
     np.testing.assert_allclose(tot ** 0.5, g[f"{mode}/total_gradnorm"], rtol=1e-3 if f32 else 5e-2)
@@ -370,6 +409,7 @@ def test_bench_size_step_vs_reference(gpu, golden, prec, fname):
         p.requires_grad = True
     m = m.to(gpu).train()
     m.fc_layers.eval()
+    sd0 = snapshot(m)
     opt = FusedAdamClip(m.parameters(), lr=1e-5, weight_decay=1e-4, max_norm=1.0)
     logits = {}
     m.fc_out.register_forward_hook(lambda mod, i, o: logits.__setitem__("v", o.detach()))
@@ -395,15 +435,21 @@ def test_bench_size_step_vs_reference(gpu, golden, prec, fname):
     errs = {n: abs(p.grad.double().norm().item() - g[f"gradnorm/{n}"]) / max(float(g[f"gradnorm/{n}"]), 1e-30)
             for n, p in m.named_parameters()}
     head_vs_ref = f32 or B >= BENCH_HEAD_MIN_CLIPS
-    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not head_vs_ref, tag=fname[:-4])
+    auto = None
+    if not f32:
+        import bf16_contract
+        elem_names = [n for n in ("lstm.bias_ih_l0", "fc_out.weight", "fc_out.bias") if head_vs_ref and f"grad/{n}" in g]
+        xa = seeded_uniform((B * T, 3, S, S), 4242).to(gpu)   # the same clip batch, as frames
+        auto, eauto = autocast_backbone_errors(
+            sd0, xa, lstmv_tail(B, T, y),
+            {n: g[f"gradnorm/{n}"] for n in errs if head_vs_ref or not is_head(n)},
+            {n: g[f"grad/{n}"] for n in elem_names}, prefix="feature_extractor.")
+        del xa
+    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not head_vs_ref, tag=fname[:-4], auto=auto)
     if not f32:
         if head_vs_ref:   # the head's gradients against the reference's own, element-wise
-            import bf16_contract
-            for n in ("lstm.bias_ih_l0", "fc_out.weight", "fc_out.bias"):
-                if f"grad/{n}" in g:
-                    e = relerr(dict(m.named_parameters())[n].grad.cpu(), g[f"grad/{n}"])
-                    print(f"head gradient {n}: rel err {e:.4f}")
-                    assert bf16_contract.RECORD or e < bf16_contract.OVER.get(fname[:-4], {}).get(f"grad/{n}", 5e-2), n
+            eerrs = {f"grad/{n}": relerr(dict(m.named_parameters())[n].grad.cpu(), g[f"grad/{n}"]) for n in elem_names}
+            bf16_contract.check(fname[:-4] + " head elements", eerrs, {f"grad/{n}": v for n, v in eauto.items()})
         check_head_on_features(m, feats, y, {n: p.grad.clone() for n, p in m.named_parameters() if is_head(n)})
     norm = opt.step()
     np.testing.assert_allclose(norm.item(), g["total_gradnorm"], rtol=1e-3 if f32 else 5e-2)
@@ -435,6 +481,7 @@ def test_xception_frame_step_vs_reference(gpu, golden, fname, prec):
     B, S = int(g["B"]), int(g["S"])
     torch.manual_seed(0)
     m = xception(num_classes=1).to(gpu).train()
+    sd0 = snapshot(m)
     opt = FusedAdamClip(m.parameters(), lr=1e-5, weight_decay=1e-4)
     x = seeded_uniform((B, 3, S, S), int(g["seed_x"])).to(gpu)
     y = (torch.arange(B, device=gpu) % 3 == 0).float().view(B, 1)
@@ -448,15 +495,23 @@ def test_xception_frame_step_vs_reference(gpu, golden, fname, prec):
     np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-5 if f32 else 2e-2)
     errs = {n: abs(p.grad.double().norm().item() - g[f"gradnorm/{n}"]) / max(float(g[f"gradnorm/{n}"]), 1e-30)
             for n, p in m.named_parameters()}
-    check_gradnorms(errs, bn_param_names(m), f32, tag=fname[:-4])
+    auto = eauto = None
+    if not f32:
+        def tail(f, params):
+            return nn.BCEWithLogitsLoss()(torch.nn.functional.linear(f, params["fc.weight"], params["fc.bias"]), y)
+        auto, eauto = autocast_backbone_errors(sd0, x, tail, {n: g[f"gradnorm/{n}"] for n in errs},
+                                               {n: g[f"grad/{n}"] for n in ("fc.weight", "fc.bias")})
+    check_gradnorms(errs, bn_param_names(m), f32, tag=fname[:-4], auto=auto)
     import bf16_contract
+    eerrs = {}
     for n in ("fc.weight", "fc.bias"):   # the head's gradients against the reference's own, element-wise
         e = relerr(dict(m.named_parameters())[n].grad.cpu(), g[f"grad/{n}"])
         print(f"head gradient {n}: rel err {e:.4f}")
         if f32:
             assert e < 1e-3, n
-        else:
-            assert bf16_contract.RECORD or e < bf16_contract.OVER.get(fname[:-4], {}).get(f"grad/{n}", 5e-2), n
+        eerrs[f"grad/{n}"] = e
+    if not f32:
+        bf16_contract.check(fname[:-4] + " head elements", eerrs, {f"grad/{n}": v for n, v in eauto.items()})
     tot = sum((p.grad.double() ** 2).sum().item() for p in m.parameters()) ** 0.5
     np.testing.assert_allclose(tot, g["total_gradnorm"], rtol=1e-3 if f32 else 5e-2)
     assert opt.step() is None
