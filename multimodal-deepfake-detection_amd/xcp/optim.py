@@ -22,6 +22,7 @@ reference scripts do) and ``step()`` returns None.
 import math
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib, ops
 
@@ -120,6 +121,10 @@ class FusedAdamClip(torch.optim.Optimizer):
                 _lib.call("xcp_opt_adam", tab.data_ptr(), tab.shape[0], coef, float(grp["lr"]), float(b1), float(b2),
                           float(grp["eps"]), float(grp["weight_decay"]), float(1.0 - b1 ** t),
                           float(math.sqrt(1.0 - b2 ** t)), s)
+        # the kernels wrote the parameters through raw pointers: bump their autograd version
+        # counters as an in-place torch op would, so that consumers keyed on them (the xcp
+        # engine's packed-weight cache, engine.pack) see the update
+        increment_version([row[0] for row in every])
         if loss is not None:
             return loss
         return self._out[1].clone() if self.max_norm is not None else None

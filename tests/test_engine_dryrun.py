@@ -148,6 +148,32 @@ def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn):
     assert fake_lib.count("xcp_tail_fwd") == 12
 
 
+def test_weights_repacked_after_fused_optimizer_step(fake_lib):
+    """FusedAdamClip writes the parameters through raw pointers; it bumps their version counters,
+    so the next forward repacks the kernel-layout weights (one batched permute launch per
+    direction) instead of running on the pre-step copies."""
+    from xcp import ops, optim
+    from Models.Xception import xception
+    ops_check = ops.check_gpu
+    try:
+        ops.check_gpu = lambda *a: None   # (the optimiser checks its parameters at construction)
+        torch.manual_seed(0)
+        m = xception(num_classes=1)
+        opt = optim.FusedAdamClip(m.parameters(), lr=1e-3, max_norm=1.0)
+    finally:
+        ops.check_gpu = ops_check
+    packs = []
+    for _ in range(3):
+        n0 = len(fake_lib)
+        m(torch.rand(2, 3, 71, 71)).sum().backward()
+        packs.append(fake_lib[n0:].count("xcp_permute3_batch"))
+        v0 = m.conv1.weight._version
+        opt.step()
+        assert m.conv1.weight._version == v0 + 1
+        opt.zero_grad()
+    assert packs == [2, 2, 2], packs   # forward + backward layouts, every step
+
+
 def test_header_matches_binding():
     """include/xcp.h declares exactly the entry points _lib.py binds, with the same arity."""
     import os

@@ -176,3 +176,35 @@ def test_train_visual_step_autocast_gradscaler(gpu):
         if abs(got - want) > tol:
             bad.append((n, got, want, tol))
     assert not bad, bad[:5]
+
+
+def test_second_step_forward_uses_updated_weights(gpu):
+    """Two FusedAdamClip training steps (fp32): the second forward runs on the weights the first
+    step wrote (the engine repacks its kernel-layout copies when the optimiser bumps the parameter
+    versions) -- its output equals that of a fresh model loaded with the post-step state_dict, and
+    differs from the first forward's."""
+    import xcp
+    from xcp.optim import FusedAdamClip
+    from Models.Xception import xception
+    torch.manual_seed(0)
+    m = xception(num_classes=1).to(gpu).train()
+    opt = FusedAdamClip(m.parameters(), lr=1e-2, max_norm=1.0)
+    x = seeded_uniform((2, 3, 96, 96), 77).to(gpu)
+    outs = []
+    with xcp.precision("fp32"):
+        for _ in range(2):
+            out = m(x)
+            outs.append(out.detach().clone())
+            out.sum().backward()
+            opt.step()
+            opt.zero_grad()
+        sd = {k: v.clone() for k, v in m.state_dict().items()}
+        m.eval()
+        got = m(x).detach()
+        fresh = xception(num_classes=1).to(gpu)
+        fresh.load_state_dict(sd)
+        fresh.eval()
+        want = fresh(x).detach()
+    torch.cuda.synchronize()
+    assert not torch.equal(outs[0], outs[1])
+    torch.testing.assert_close(got, want, rtol=0, atol=0)
