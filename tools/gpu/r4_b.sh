@@ -10,6 +10,6 @@ XCP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 $S > gpurun_ou
 timeout -k 10 300 python bench.py $S > gpurun_out/b_g1.json 2> gpurun_out/b_g1.err || exit $?
 B="python bench.py --cpu-baseline off --mode unfrozen --steps 5 --warmup 2 --small-batch 0 --measured-peaks off --diag off"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r4b -o kt -- $B > gpurun_out/b_prof.log 2>&1 || exit $?
-python tools/stream_timeline.py gpurun_out/prof_r4b/kt_kernel_trace.csv 40 > gpurun_out/b_timeline.txt 2>&1
+python tools/stream_timeline.py "$(find gpurun_out/prof_r4b -name "*kernel_trace.csv" | head -1)" 40 > gpurun_out/b_timeline.txt 2>&1
 python tools/prof_summary.py gpurun_out/prof_r4b 60 > gpurun_out/b_kernels.txt 2>&1
 echo ok
