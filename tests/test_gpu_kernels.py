@@ -793,13 +793,13 @@ def test_fused_adam_clip_load_state_dict_resume(ops, gpu):
         torch.testing.assert_close(opt_a.state[p]["exp_avg"], opt_b.state[q]["exp_avg"], rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize("M,N,K,ref", [(92416, 736, 736, 0), (5120 * 9, 1024, 736, 0), (2048 * 7 + 256, 512, 64, 2),
-                                       (256 * 506 + 77, 256, 200, 2), (256 * 600 + 77, 256, 448, 0)])
+@pytest.mark.parametrize("M,N,K,ref", [(92416, 736, 736, 2), (5120 * 9, 1024, 736, 2), (2048 * 7 + 256, 512, 64, 2),
+                                       (256 * 506 + 77, 256, 200, 2), (256 * 600 + 77, 256, 448, 2)])
 def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref):
-    """The persistent 256x256 kernel (tile 3) computes every tile with the one-shot kernel's
-    MFMA order: identical output and statistics bits (against tile 0 where both send a sparse
-    last round to the 128x128 kernel, tile 2 otherwise), across several tiles per workgroup
-    (the prefetch / epilogue overlap must not change a value)."""
+    """The persistent 256x256 kernel (tile 3, every row on it) computes every tile with the
+    one-shot kernel's MFMA order: identical output and statistics bits against tile 2 (the
+    one-shot kernel for every row), across several tiles per workgroup (the prefetch / epilogue
+    overlap must not change a value)."""
     tile = 3
     g = torch.Generator(device=gpu).manual_seed(M + N)
     A = torch.randn(M, K, device=gpu, generator=g).bfloat16()

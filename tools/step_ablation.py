@@ -2,7 +2,9 @@
 (XceptionLSTMV, 16 clips x 16 x 299^2, unfrozen, bf16) with chosen C-ABI launches dropped, to
 price what each kernel class costs the STEP (its marginal cost, contention included) rather
 than what it costs alone.  Not part of the product path: the skip is a monkeypatch of
-xcp._lib.call applied in this process only.
+xcp._lib.call applied in this process only; GEMMs of fewer than 4096 rows (the LSTM input
+projection) are never dropped, and the loss is fed sanitised probabilities (torch's BCE asserts
+0 <= p <= 1 on the device, and a dropped launch leaves garbage behind it).
 
   python tools/step_ablation.py [--steps 8] [--rounds 2] set1 set2 ...
 
@@ -32,7 +34,9 @@ def matcher(spec):
             return False
         if n == "xcp_gemm_nt" and flt:
             stats = args[10]
-            N, K = args[8], args[9]
+            M, N, K = args[7], args[8], args[9]
+            if M < 4096:   # the LSTM input projection and other head-size GEMMs are never dropped
+                return False
             if "728" in flt and not (N == 736 and K == 736):
                 return False
             if flt.endswith("fwd") and not stats:
@@ -61,6 +65,10 @@ def main():
     args = bench.parse()
     args.mode = "unfrozen"
     run = bench.Run(args, "unfrozen", dev, 0, 1)
+    # dropped launches leave garbage (possibly NaN / inf) in their outputs; torch's BCE asserts
+    # 0 <= p <= 1 on the device (an assert is a GPU trap), so the loss sees sanitised probabilities
+    bce = torch.nn.functional.binary_cross_entropy
+    run.crit = lambda out, y: bce(torch.nan_to_num(out.float(), nan=0.5, posinf=1.0, neginf=0.0).clamp(0.0, 1.0), y)
     real = _lib.call
     active = []
     skipped = {"n": 0}
