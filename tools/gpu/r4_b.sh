@@ -12,4 +12,5 @@ B="python bench.py --cpu-baseline off --mode unfrozen --steps 5 --warmup 2 --sma
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r4b -o kt -- $B > gpurun_out/b_prof.log 2>&1 || exit $?
 python tools/stream_timeline.py "$(find gpurun_out/prof_r4b -name "*kernel_trace.csv" | head -1)" 40 > gpurun_out/b_timeline.txt 2>&1
 python tools/prof_summary.py gpurun_out/prof_r4b 60 > gpurun_out/b_kernels.txt 2>&1
-echo ok
+
+timeout -k 10 300 python -u tools/step_ablation.py --rounds 3 gemm_tn gemm_nt:728fwd gemm_nt:728dgrad gemm_nt:dgrad gemm_nt:fwd dw_bwd dw_fwd bn_bwd_apply colreduce_multi bn_bwd_reduce unit_bwd bn_finalize_part+bn_bwd_finalize_part maxpool_bwd_bnred > gpurun_out/b_ablation.log 2>&1
