@@ -319,6 +319,7 @@ struct DwBwdArgs {
   const float* bmean;
   const float* binvstd;
   int N, H, W, C, ngroups;
+  int nbands, bandH;      // row bands per frame (one wave walks rows [band*bandH, +bandH))
 };
 
 template <typename T, int P, int FS>
@@ -384,17 +385,19 @@ template <typename V> XCP_DEV V vfma(V a, V b, V c) { return __builtin_elementwi
 template <typename V> XCP_DEV V vmax0(V a) { return __builtin_elementwise_max(a, V(0.f)); }
 
 struct RowMap {
-  int n, cg, grp, unit;
+  int n, cg, grp, unit, band;
   bool live;
 };
-XCP_DEV RowMap row_map(int N, int ncg, int ngroups) {
+XCP_DEV RowMap row_map(int N, int ncg, int ngroups, int nbands = 1) {
   RowMap m;
   const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  m.live = gw < N * ncg * ngroups;
+  m.live = gw < N * ncg * nbands * ngroups;
   m.grp = gw % ngroups;
-  m.unit = gw / ngroups;   // (frame, column group)
-  m.cg = m.unit % ncg;
-  m.n = m.unit / ncg;
+  m.unit = gw / ngroups;   // (frame, column group, row band): the partial-sum row
+  m.band = m.unit % nbands;
+  const int fc = m.unit / nbands;
+  m.cg = fc % ncg;
+  m.n = fc / ncg;
   return m;
 }
 
@@ -503,8 +506,12 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   __shared__ __attribute__((aligned(16))) char sm[4][(NS + NSG + (RES ? NS : 0)) * LROW];
   __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];   // output staging (separate object)
   const int ncg = (a.W + RCOLS - 1) / RCOLS;
-  const RowMap mp = row_map(a.N, ncg, a.ngroups);
+  const RowMap mp = row_map(a.N, ncg, a.ngroups, a.nbands);
   if (!mp.live) return;
+  // this wave's rows [r0, r1); it reads X rows r0 .. r1-1 and dY rows r0-1 .. r1 (rows past
+  // those are staged from the zero line: never read)
+  const int r0 = mp.band * a.bandH, r1 = min(a.H, r0 + a.bandH);
+  const int hx = r1, hg = min(a.H, r1 + 1);
   const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
   char* ring = sm[threadIdx.x >> 6];
   char* rx = ring;                  // X rows, slot r % NS
@@ -613,9 +620,9 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
 #pragma unroll
       for (int j = 0; j < RS; ++j) pres[j] = rd(srh, j + 1);
     }
-    stage_row<T>(X, h + BD, a.H, a.W, a.C, rl_ld, sx(h + BD), lane);          // slot of X row h-1
-    stage_row<T>(G, h + 1 + BD, a.H, a.W, a.C, rl_ld, sgs(h + 1 + BD), lane);   // slot of dY row h
-    if constexpr (RES) stage_row<T>(dRes, h + BD, a.H, a.W, a.C, rl_ld, sr(h + BD), lane);
+    stage_row<T>(X, h + BD, hx, a.W, a.C, rl_ld, sx(h + BD), lane);          // slot of X row h-1
+    stage_row<T>(G, h + 1 + BD, hg, a.W, a.C, rl_ld, sgs(h + 1 + BD), lane);   // slot of dY row h
+    if constexpr (RES) stage_row<T>(dRes, h + BD, hx, a.W, a.C, rl_ld, sr(h + BD), lane);
     // dY rows h+1, h, h-1 (ky = 0, 1, 2; row -1 is the zero padding above the frame), one 7-column
     // window at a time; independent accumulation chains: consecutive packed FMAs never depend on
     // each other
@@ -691,28 +698,39 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     }
     store_row<T>(dX, h, a.W, a.C, rl_st, stg, lane);
   };
-  // prologue: X rows 0 .. BD-1, dY rows 0 .. BD, dRes rows 0 .. BD-1
+  // prologue: X rows r0 .. r0+BD-1, dY rows r0 .. r0+BD, dRes rows r0 .. r0+BD-1; dY row r0-1
+  // (zero above the frame) first, into the register window (rolling form) or its ring slot
+  V gup[ROLL ? RS + 2 : 1];
+  if (r0 > 0) {
+    stage_row<T>(G, r0 - 1, a.H, a.W, a.C, rl_ld, sgs(r0 - 1), lane);
+    if constexpr (ROLL) {
+      vmwait<0>();
+      cvtg(sgs(r0 - 1), gup);
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the row is in registers before its slot is refilled
+    }
+  } else if constexpr (ROLL) {
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) gup[k] = V(0.f);
+  }
 #pragma unroll
   for (int r = 0; r <= BD; ++r) {
-    if (r < BD) stage_row<T>(X, r, a.H, a.W, a.C, rl_ld, sx(r), lane);
-    stage_row<T>(G, r, a.H, a.W, a.C, rl_ld, sgs(r), lane);
+    if (r < BD) stage_row<T>(X, r0 + r, hx, a.W, a.C, rl_ld, sx(r0 + r), lane);
+    stage_row<T>(G, r0 + r, hg, a.W, a.C, rl_ld, sgs(r0 + r), lane);
     if constexpr (RES)
-      if (r < BD) stage_row<T>(dRes, r, a.H, a.W, a.C, rl_ld, sr(r), lane);
+      if (r < BD) stage_row<T>(dRes, r0 + r, hx, a.W, a.C, rl_ld, sr(r0 + r), lane);
   }
   vmwait<0>();
   if constexpr (ROLL) {
-    V g0[RS + 2], g1[RS + 2], g2[RS + 2];
-#pragma unroll
-    for (int k = 0; k < RS + 2; ++k) g0[k] = V(0.f);
-    cvtg(sgs(0), g1);
-    for (int h = 0; h < a.H; h += 3) {
-      step(h, g0, g1, g2);
-      if (h + 1 < a.H) step(h + 1, g1, g2, g0);
-      if (h + 2 < a.H) step(h + 2, g2, g0, g1);
+    V g1[RS + 2], g2[RS + 2];
+    cvtg(sgs(r0), g1);
+    for (int h = r0; h < r1; h += 3) {
+      step(h, gup, g1, g2);
+      if (h + 1 < r1) step(h + 1, g1, g2, gup);
+      if (h + 2 < r1) step(h + 2, g2, gup, g1);
     }
   } else {
     V gx[RS + 2];   // (unused by the streaming step)
-    for (int h = 0; h < a.H; ++h) step(h, gx, gx, gx);
+    for (int h = r0; h < r1; ++h) step(h, gx, gx, gx);
   }
   // reduce the 4 lane segments (lanes cl, cl+16, cl+32, cl+48) and write the partials
   float red[EPT][11];
@@ -763,6 +781,17 @@ bool dw_bwd_occ4() {
   return v;
 }
 
+// Row bands per frame: XCP_DW_BWD_BANDS=<b> splits every frame's row walk into b bands of
+// ceil(H / b) rows (one wave each; a band re-reads the dY rows just above and below it), so that
+// a launch has more, shorter waves.  Frames under 2 b rows keep one band.  (Read per call, so a
+// test can compare band counts in one process.)
+int dw_bwd_bands(int H) {
+  const char* e = getenv("XCP_DW_BWD_BANDS");
+  int v = e ? atoi(e) : 1;
+  v = v >= 1 && v <= 8 ? v : 1;
+  return H >= 2 * v ? v : 1;
+}
+
 template <typename T, int ACT>
 void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
   if (a.dRes && dw_bwd_occ4() && !a.dSkip)
@@ -776,7 +805,7 @@ void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
 
 template <typename T>
 int launch_bwd_lds(int act, const DwBwdArgs& a, hipStream_t st) {
-  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.ngroups;
+  const long waves = (long)a.N * ((a.W + RCOLS - 1) / RCOLS) * a.nbands * a.ngroups;
   const int blocks = (int)((waves + 3) / 4);
   if (act == ACT_NONE) launch_bwd_act<T, ACT_NONE>(a, blocks, st);
   else if (act == ACT_RELU) launch_bwd_act<T, ACT_RELU>(a, blocks, st);
@@ -822,11 +851,10 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
   return launch_fwd<float, FWD_MAXPX, 64>(act, a, stream);
 }
 
-// number of partial rows (frame x 20-column groups) of the backward's slabs
+// number of partial rows (frame x 20-column group x row band) of the backward's slabs
 int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
-  (void)H;
   (void)C;
-  return N * ((W + RCOLS - 1) / RCOLS);
+  return N * ((W + RCOLS - 1) / RCOLS) * dw_bwd_bands(H);
 }
 
 static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
@@ -846,6 +874,8 @@ static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const 
   a.bnpart = bnpart; a.bmean = bmean; a.binvstd = binvstd; a.Yb = Yb;
   a.N = N; a.H = H; a.W = W; a.C = C;
   a.ngroups = ngroups_for(C, dtype);
+  a.nbands = dw_bwd_bands(H);
+  a.bandH = (H + a.nbands - 1) / a.nbands;
   if (dtype == XCP_BF16) return launch_bwd_lds<bf16>(act, a, stream);
   if (dtype == XCP_F32) return launch_bwd_lds<float>(act, a, stream);
   return XCP_EUNSUPPORTED;

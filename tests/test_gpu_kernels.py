@@ -325,6 +325,44 @@ def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
         torch.testing.assert_close(sums[1], (dXn * zhat).double().sum((0, 2, 3)), rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("bands", [2, 3])
+@pytest.mark.parametrize("N,C,H,act,res,skip", [(64, 736, 19, 2, False, False), (64, 736, 19, 1, True, False),
+                                                (16, 256, 37, 2, False, False), (8, 128, 15, 1, True, True),
+                                                (32, 1536, 10, 0, False, False), (5, 64, 7, 2, False, False)])
+def test_dw_bwd_row_bands(ops, gpu, monkeypatch, bands, N, C, H, act, res, skip):
+    """The backward's row walk split into row bands (XCP_DW_BWD_BANDS; a band re-reads the dY
+    rows above and below it): dX bitwise equal to the one-band walk (the same per-pixel sums), the
+    weight gradient and the BN partial sums equal to fp32 summation order (more partial rows)."""
+    W = H
+    g = torch.Generator(device=gpu).manual_seed(N + C + H)
+    dt = torch.bfloat16
+    x = torch.randn(N * H * W, C, device=gpu, generator=g).to(dt)
+    dy = torch.randn(N * H * W, C, device=gpu, generator=g).to(dt)
+    Wt = torch.randn(9, C, device=gpu, generator=g) / 3
+    sc = torch.rand(C, device=gpu, generator=g) + 0.5
+    sh = torch.randn(C, device=gpu, generator=g) * 0.2
+    dR = torch.randn(N * H * W, C, device=gpu, generator=g).to(dt) if res else None
+    OH = (H - 1) // 2 + 1
+    dS = torch.randn(N * OH * OH, C, device=gpu, generator=g).to(dt) if skip else None
+    st = {"mean": torch.randn(C, device=gpu, generator=g) * 0.1,
+          "invstd": torch.rand(C, device=gpu, generator=g) + 0.5} if act == 2 else None
+    outs = []
+    for b in (1, bands):
+        monkeypatch.setenv("XCP_DW_BWD_BANDS", str(b))
+        dX = torch.full((N * H * W, C), float("nan"), device=gpu, dtype=dt)
+        dW = torch.empty(C * 9, device=gpu)
+        bnpart, P = ops.dw_bwd(act, dy, x, Wt, sc, sh, dX, dW, N, H, W, C, dRes=dR, dSkip=dS,
+                               skip_geom=(OH, OH, 2) if skip else (0, 0, 1), bn_stats=st)
+        torch.cuda.synchronize()
+        sums = bnpart.view(P, 2, C).double().sum(0) if bnpart is not None else None
+        outs.append((dX, dW, sums, P))
+    assert outs[1][3] == outs[0][3] * bands
+    assert torch.equal(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-5)
+    if act == 2:
+        torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-6, atol=1e-4)
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("N", [2, 701])
 def test_dw_bwd_residual_and_skip(ops, gpu, dt, N):

@@ -1,0 +1,58 @@
+"""Depthwise backward row bands (XCP_DW_BWD_BANDS): launch time at the step's shapes (256 frames,
+bf16) for 1, 2 and 3 bands, interleaved rounds, median; HIP events on the launch stream.
+
+  python tools/dw_bands.py      # GPU box
+"""
+import os
+import statistics
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "multimodal-deepfake-detection_amd"), REPO]
+
+from xcp import ops  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    ops._lib.load()
+    g = torch.Generator(device=dev).manual_seed(0)
+    shapes = [(256, 19, 736, 2, False), (256, 19, 736, 1, True), (256, 37, 736, 2, False), (256, 74, 256, 2, False),
+              (256, 147, 128, 2, False), (256, 10, 1536, 2, False)]
+    for N, H, C, act, res in shapes:
+        W = H
+        M = N * H * W
+        dy = torch.randn(M, C, device=dev, generator=g).bfloat16()
+        x = torch.randn(M, C, device=dev, generator=g).bfloat16()
+        dR = torch.randn(M, C, device=dev, generator=g).bfloat16() if res else None
+        Wt = torch.randn(9, C, device=dev, generator=g) / 3
+        sc = torch.rand(C, device=dev, generator=g) + 0.5
+        sh = torch.randn(C, device=dev, generator=g) * 0.2
+        st = {"mean": torch.zeros(C, device=dev), "invstd": torch.ones(C, device=dev)} if act == 2 else None
+        dX = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+        dW = torch.empty(C * 9, device=dev)
+        times = {b: [] for b in (1, 2, 3)}
+        for _ in range(5):
+            for b in times:
+                os.environ["XCP_DW_BWD_BANDS"] = str(b)
+                for _ in range(2):
+                    ops.dw_bwd(act, dy, x, Wt, sc, sh, dX, dW, N, H, W, C, dRes=dR, bn_stats=st)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(10):
+                    ops.dw_bwd(act, dy, x, Wt, sc, sh, dX, dW, N, H, W, C, dRes=dR, bn_stats=st)
+                e.record()
+                torch.cuda.synchronize()
+                times[b].append(s.elapsed_time(e) / 10 * 1e3)
+        byts = (3 + (1 if res else 0)) * M * C * 2
+        line = " ".join(f"bands={b}: {statistics.median(v):7.1f} us ({byts / statistics.median(v) / 1e6:6.0f} GB/s)"
+                        for b, v in times.items())
+        print(f"{N}x{H}^2x{C} act={act} res={res} (op incl. slab reduce): {line}", flush=True)
+        del dy, x, dR, dX
+    os.environ.pop("XCP_DW_BWD_BANDS", None)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,11 @@
+# Round 4 (c): depthwise backward row bands (kernel times, in-step A/B), the 2-rank gloo path at 4
+# clips/rank against world 1 at 4 clips (ranks share cuda:0: gloo, not RCCL)
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 python -u tools/dw_bands.py > gpurun_out/c_bands.log 2>&1 || exit $?
+for b in 2 1 2 1; do XCP_DW_BWD_BANDS=$b timeout -k 10 200 python bench.py --cpu-baseline off --mode unfrozen --small-batch 0 --measured-peaks off --diag off --no-kernel-timing > gpurun_out/c_step_bands$b.json 2>> gpurun_out/c_step_bands.err || exit $?; cat gpurun_out/c_step_bands$b.json >> gpurun_out/c_step_bands.log; done
+S="--steps 4 --warmup 2 --batch 4 --mode unfrozen --cpu-baseline off --small-batch 0 --measured-peaks off --no-kernel-timing"
+XCP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 $S > gpurun_out/c_g2.json 2> gpurun_out/c_g2.err || exit $?
+timeout -k 10 300 python bench.py $S > gpurun_out/c_g1.json 2> gpurun_out/c_g1.err || exit $?
