@@ -9,3 +9,10 @@ for b in 2 1 2 1; do XCP_DW_BWD_BANDS=$b timeout -k 10 200 python bench.py --cpu
 S="--steps 4 --warmup 2 --batch 4 --mode unfrozen --cpu-baseline off --small-batch 0 --measured-peaks off --no-kernel-timing"
 XCP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 $S > gpurun_out/c_g2.json 2> gpurun_out/c_g2.err || exit $?
 timeout -k 10 300 python bench.py $S > gpurun_out/c_g1.json 2> gpurun_out/c_g1.err || exit $?
+# weight-gradient split layout in the step: XCD-whole splits (S a multiple of 8) at targets 72 / 144 vs default
+Q="--cpu-baseline off --mode unfrozen --small-batch 0 --measured-peaks off --diag off --no-kernel-timing"
+for v in base xcd72 xcd144 base xcd72 xcd144; do
+  case $v in base) E="";; xcd72) E="XCP_TN_XCD_SPLITS=1 XCP_TN_TARGET_WGS=72";; xcd144) E="XCP_TN_XCD_SPLITS=1 XCP_TN_TARGET_WGS=144";; esac
+  env $E timeout -k 10 200 python bench.py $Q > gpurun_out/c_tn_$v.json 2>> gpurun_out/c_tn.err || exit $?
+  echo "$v $(cat gpurun_out/c_tn_$v.json)" >> gpurun_out/c_tn.log
+done
