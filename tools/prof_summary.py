@@ -32,10 +32,15 @@ def decode(name):
     if rest.startswith("I"):
         body = rest[1:]
         while body and not body.startswith("EE") and not body.startswith("Ev"):
-            mm = re.match(r"Li(-?\d+)E|(DF16b|f|d|h|i)", body)
+            mm = re.match(r"Li(-?\d+)E|Lb([01])E|(DF16b|f|d|h|i)", body)
             if not mm:
                 break
-            args.append(mm.group(1) if mm.group(1) is not None else _TYPES[mm.group(2)])
+            if mm.group(1) is not None:
+                args.append(mm.group(1))
+            elif mm.group(2) is not None:   # bool template argument (e.g. the NT GEMM's BN-statistics epilogue)
+                args.append("true" if mm.group(2) == "1" else "false")
+            else:
+                args.append(_TYPES[mm.group(3)])
             body = body[mm.end():]
     return f"{ident}<{', '.join(args)}>" if args else ident
 
@@ -71,18 +76,20 @@ def main():
             glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
         path = cands[0]
     rows = load(path)
+    # instances: (base name, grid, workgroup, LDS, VGPRs) refined by the decoded template arguments
+    # where rocprofv3 kept the mangled name (so e.g. gemm_nt256p_kernel<true> -- the forward, with the
+    # BN-statistics epilogue -- and <false> -- the input gradient -- are separate rows)
     labels = {}
-    for name, _, key in rows:
-        d = decode(name)
-        if d:
-            labels[(base(name),) + key] = d
     by_base = defaultdict(lambda: [0, 0])
     by_inst = defaultdict(lambda: [0, 0])
     for name, dur, key in rows:
         b = base(name)
         by_base[b][0] += dur
         by_base[b][1] += 1
-        ik = (b,) + key
+        d = decode(name)
+        ik = (b,) + key + ((d,) if d and "<" in d else ())
+        if d:
+            labels[ik] = d
         by_inst[ik][0] += dur
         by_inst[ik][1] += 1
     total = sum(t for t, _ in by_base.values())
@@ -115,12 +122,15 @@ def contention(path):
     print("\nroofline kernels: launches alone on the GPU vs overlapping another stream's kernels")
     for name, grid in ROOF:
         sel = [r for r in rows if base(r[0]) == name and r[4] == grid]
-        alone, shared = [], []
-        for r in sel:
-            ov = any(o[3] != r[3] and o[1] < r[2] and o[2] > r[1] for o in rows if o is not r)
-            (shared if ov else alone).append((r[2] - r[1]) / 1e3)
-        f = lambda v: f"{len(v):5d} x {sum(v) / len(v):7.1f} us" if v else "    0"
-        print(f"{name:28s} grid {grid:>8d}  all {f(alone + shared)}  alone {f(alone)}  overlapped {f(shared)}")
+        for role in sorted({decode(r[0]) or name for r in sel}):
+            alone, shared = [], []
+            for r in sel:
+                if (decode(r[0]) or name) != role:
+                    continue
+                ov = any(o[3] != r[3] and o[1] < r[2] and o[2] > r[1] for o in rows if o is not r)
+                (shared if ov else alone).append((r[2] - r[1]) / 1e3)
+            f = lambda v: f"{len(v):5d} x {sum(v) / len(v):7.1f} us" if v else "    0"   # noqa: E731
+            print(f"{role[:34]:34s} grid {grid:>8d}  all {f(alone + shared)}  alone {f(alone)}  overlapped {f(shared)}")
 
 
 if __name__ == "__main__":
