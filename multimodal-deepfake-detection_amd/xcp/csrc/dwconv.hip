@@ -320,6 +320,7 @@ struct DwBwdArgs {
   const float* binvstd;
   int N, H, W, C, ngroups;
   int nbands, bandH;      // row bands per frame (one wave walks rows [band*bandH, +bandH))
+  int xcd;                // 1: consecutive workgroups of the walk on one XCD (xcd_remap)
 };
 
 template <typename T, int P, int FS>
@@ -388,9 +389,13 @@ struct RowMap {
   int n, cg, grp, unit, band;
   bool live;
 };
-XCP_DEV RowMap row_map(int N, int ncg, int ngroups, int nbands = 1) {
+XCP_DEV RowMap row_map(int N, int ncg, int ngroups, int nbands = 1, bool xcd = false) {
   RowMap m;
-  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  // xcd: the workgroups holding consecutive channel slices of a pixel row run on one XCD, so the
+  // 128-B lines two of them share (every odd pixel of a 1,472-B row starts mid-line) are fetched
+  // into one L2 instead of two
+  const int wg = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int gw = __builtin_amdgcn_readfirstlane(wg * 4 + (threadIdx.x >> 6));
   m.live = gw < N * ncg * nbands * ngroups;
   m.grp = gw % ngroups;
   m.unit = gw / ngroups;   // (frame, column group, row band): the partial-sum row
@@ -506,7 +511,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   __shared__ __attribute__((aligned(16))) char sm[4][(NS + NSG + (RES ? NS : 0)) * LROW];
   __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];   // output staging (separate object)
   const int ncg = (a.W + RCOLS - 1) / RCOLS;
-  const RowMap mp = row_map(a.N, ncg, a.ngroups, a.nbands);
+  const RowMap mp = row_map(a.N, ncg, a.ngroups, a.nbands, a.xcd != 0);
   if (!mp.live) return;
   // this wave's rows [r0, r1); it reads X rows r0 .. r1-1 and dY rows r0-1 .. r1 (rows past
   // those are staged from the zero line: never read)
@@ -792,6 +797,12 @@ int dw_bwd_bands(int H) {
   return H >= 2 * v ? v : 1;
 }
 
+// XCP_DW_BWD_XCD=1: XCD-aware workgroup order for the backward walk (A/B; read per call)
+int dw_bwd_xcd() {
+  const char* e = getenv("XCP_DW_BWD_XCD");
+  return e && e[0] == '1' ? 1 : 0;
+}
+
 template <typename T, int ACT>
 void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
   if (a.dRes && dw_bwd_occ4() && !a.dSkip)
@@ -875,6 +886,7 @@ static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const 
   a.N = N; a.H = H; a.W = W; a.C = C;
   a.ngroups = ngroups_for(C, dtype);
   a.nbands = dw_bwd_bands(H);
+  a.xcd = dw_bwd_xcd();
   a.bandH = (H + a.nbands - 1) / a.nbands;
   if (dtype == XCP_BF16) return launch_bwd_lds<bf16>(act, a, stream);
   if (dtype == XCP_F32) return launch_bwd_lds<float>(act, a, stream);

@@ -332,7 +332,8 @@ def test_dw_fwd_bwd(ops, gpu, dt, act, N, C, H):
 def test_dw_bwd_row_bands(ops, gpu, monkeypatch, bands, N, C, H, act, res, skip):
     """The backward's row walk split into row bands (XCP_DW_BWD_BANDS; a band re-reads the dY
     rows above and below it): dX bitwise equal to the one-band walk (the same per-pixel sums), the
-    weight gradient and the BN partial sums equal to fp32 summation order (more partial rows)."""
+    weight gradient and the BN partial sums equal to fp32 summation order (more partial rows); the
+    XCD-aware workgroup order (XCP_DW_BWD_XCD) changes nothing but placement: bitwise equal."""
     W = H
     g = torch.Generator(device=gpu).manual_seed(N + C + H)
     dt = torch.bfloat16
@@ -347,8 +348,9 @@ def test_dw_bwd_row_bands(ops, gpu, monkeypatch, bands, N, C, H, act, res, skip)
     st = {"mean": torch.randn(C, device=gpu, generator=g) * 0.1,
           "invstd": torch.rand(C, device=gpu, generator=g) + 0.5} if act == 2 else None
     outs = []
-    for b in (1, bands):
+    for b, xcd in ((1, "0"), (bands, "0"), (bands, "1")):
         monkeypatch.setenv("XCP_DW_BWD_BANDS", str(b))
+        monkeypatch.setenv("XCP_DW_BWD_XCD", xcd)
         dX = torch.full((N * H * W, C), float("nan"), device=gpu, dtype=dt)
         dW = torch.empty(C * 9, device=gpu)
         bnpart, P = ops.dw_bwd(act, dy, x, Wt, sc, sh, dX, dW, N, H, W, C, dRes=dR, dSkip=dS,
@@ -361,6 +363,10 @@ def test_dw_bwd_row_bands(ops, gpu, monkeypatch, bands, N, C, H, act, res, skip)
     torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-5)
     if act == 2:
         torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-6, atol=1e-4)
+    # the XCD-aware walk order is a permutation of the same waves: every output bitwise equal
+    assert torch.equal(outs[2][0], outs[1][0]) and torch.equal(outs[2][1], outs[1][1])
+    if act == 2:
+        assert torch.equal(outs[2][2], outs[1][2])
 
 
 @pytest.mark.parametrize("dt", DTYPES)

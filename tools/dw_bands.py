@@ -1,5 +1,6 @@
-"""Depthwise backward row bands (XCP_DW_BWD_BANDS): launch time at the step's shapes (256 frames,
-bf16) for 1, 2 and 3 bands, interleaved rounds, median; HIP events on the launch stream.
+"""Depthwise backward variants read per call -- row bands (XCP_DW_BWD_BANDS) and the XCD-aware
+workgroup order (XCP_DW_BWD_XCD) -- timed at the step's shapes (256 frames, bf16), interleaved rounds,
+median; HIP events on the launch stream.
 
   python tools/dw_bands.py      # GPU box
 """
@@ -33,10 +34,11 @@ def main():
         st = {"mean": torch.zeros(C, device=dev), "invstd": torch.ones(C, device=dev)} if act == 2 else None
         dX = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
         dW = torch.empty(C * 9, device=dev)
-        times = {b: [] for b in (1, 2, 3)}
+        times = {v: [] for v in ((1, 0), (1, 1), (2, 0), (2, 1), (3, 1))}
         for _ in range(5):
             for b in times:
-                os.environ["XCP_DW_BWD_BANDS"] = str(b)
+                os.environ["XCP_DW_BWD_BANDS"] = str(b[0])
+                os.environ["XCP_DW_BWD_XCD"] = str(b[1])
                 for _ in range(2):
                     ops.dw_bwd(act, dy, x, Wt, sc, sh, dX, dW, N, H, W, C, dRes=dR, bn_stats=st)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -47,11 +49,12 @@ def main():
                 torch.cuda.synchronize()
                 times[b].append(s.elapsed_time(e) / 10 * 1e3)
         byts = (3 + (1 if res else 0)) * M * C * 2
-        line = " ".join(f"bands={b}: {statistics.median(v):7.1f} us ({byts / statistics.median(v) / 1e6:6.0f} GB/s)"
+        line = " ".join(f"b{b[0]}x{b[1]}: {statistics.median(v):7.1f} us ({byts / statistics.median(v) / 1e6:5.0f} GB/s)"
                         for b, v in times.items())
         print(f"{N}x{H}^2x{C} act={act} res={res} (op incl. slab reduce): {line}", flush=True)
         del dy, x, dR, dX
     os.environ.pop("XCP_DW_BWD_BANDS", None)
+    os.environ.pop("XCP_DW_BWD_XCD", None)
 
 
 if __name__ == "__main__":

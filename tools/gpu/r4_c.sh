@@ -5,7 +5,11 @@ mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 python -u tools/dw_bands.py > gpurun_out/c_bands.log 2>&1 || exit $?
-for b in 2 1 2 1; do XCP_DW_BWD_BANDS=$b timeout -k 10 200 python bench.py --cpu-baseline off --mode unfrozen --small-batch 0 --measured-peaks off --diag off --no-kernel-timing > gpurun_out/c_step_bands$b.json 2>> gpurun_out/c_step_bands.err || exit $?; cat gpurun_out/c_step_bands$b.json >> gpurun_out/c_step_bands.log; done
+Q="--cpu-baseline off --mode unfrozen --small-batch 0 --measured-peaks off --diag off --no-kernel-timing"
+for v in 1x0 2x0 1x1 2x1 1x0 2x0 1x1 2x1; do
+  XCP_DW_BWD_BANDS=${v%x*} XCP_DW_BWD_XCD=${v#*x} timeout -k 10 200 python bench.py $Q > gpurun_out/c_step_dw$v.json 2>> gpurun_out/c_step_dw.err || exit $?
+  echo "$v $(cat gpurun_out/c_step_dw$v.json)" >> gpurun_out/c_step_dw.log
+done
 S="--steps 4 --warmup 2 --batch 4 --mode unfrozen --cpu-baseline off --small-batch 0 --measured-peaks off --no-kernel-timing"
 XCP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 $S > gpurun_out/c_g2.json 2> gpurun_out/c_g2.err || exit $?
 timeout -k 10 300 python bench.py $S > gpurun_out/c_g1.json 2> gpurun_out/c_g1.err || exit $?
