@@ -273,6 +273,17 @@ def pmc_traffic():
             out[b] = (sum(v["traffic_bytes"] for v in parts),
                       f"{os.path.relpath(files[-1], REPO)}: " + " + ".join(f"{v['kernel']} grid={v['grid']}" for v in parts)
                       + f", 2*FETCH_SIZE+WRITE_SIZE per op, mean over {n} launches (tools/kbench.py roof_ops)")
+    # the weight-gradient GEMM: from the newest whole-step passes (the middle-flow launches: the grid
+    # with the most launches)
+    steps = sorted(glob.glob(os.path.join(REPO, "profiles", "*_step_traffic.json")))
+    if steps:
+        data = json.load(open(steps[-1]))
+        cand = [v for v in data.values() if isinstance(v, dict) and v.get("base") == "gemm_tn256_kernel"]
+        if cand:
+            v = max(cand, key=lambda v: v["launches"])
+            out["gemm_tn"] = (v["traffic_bytes"], f"{os.path.relpath(steps[-1], REPO)}: {v['kernel']} grid={v['grid']}, "
+                                                  f"2*FETCH_SIZE+WRITE_SIZE, mean over {v['launches']} launches "
+                                                  f"in the step (incl. its fp32 slab writes)")
     return out
 
 
@@ -513,7 +524,9 @@ def main():
             cp = engine.pc(728)   # the 728-channel flow's channel pitch (736: padded rows)
             timer = ops.KernelTimer({"pw_gemm_728": lambda name, a: name == "gemm_nt" and a["M"] == frames * hm * hm
                                      and a["N"] == cp and a["K"] == cp and a["stats"] is not None,
-                                     "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == cp and a["H"] == hm})
+                                     "dw_fwd_728": lambda name, a: name == "dw_fwd" and a["C"] == cp and a["H"] == hm,
+                                     "tn_728": lambda name, a: name == "gemm_tn" and a["M"] == frames * hm * hm
+                                     and a["N"] == 728 and a["K"] == 728})
         steps = args.steps if mode == modes[0] else max(3, args.steps // 2)
         dg = {} if diag is not None else None
         if os.environ.get("XCP_BENCH_STREAM") == "high":   # A/B: the step on a high-priority stream
@@ -590,6 +603,17 @@ def main():
                                         "kernel": f"dw_fwd_w2_kernel (depthwise 3x3 C=728 @{hm}x{hm}; channel pitch "
                                                   f"{engine.pc(728)}, bytes counted for the 728 real channels)",
                                         "bytes_per_launch": byts, "avg_launch_ms": round(dw_ms, 4)}
+            tn_ms = timer.mean_ms("tn_728")
+            if tn_ms:   # the weight-gradient GEMM (side stream, the largest kernel by time): in-step, contended
+                flops = 2.0 * M * 728 * 728
+                ach = flops / (tn_ms * 1e-3) / 1e12
+                extra["roofline_wgrad"] = {
+                    "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic.get("gemm_tn", (None,))[0],
+                    "traffic_source": traffic.get("gemm_tn", (None, None))[1],
+                    "kernel": f"gemm_tn256_kernel (split-K weight gradient dW = dY^T X of the 728->728 pointwise @{hm}x{hm}, "
+                              f"side stream beside the backward's main stream; slab reduction not included)",
+                    "flops_per_launch": flops, "avg_launch_ms": round(tn_ms, 4), "launches": timer.count("tn_728")}
         if not audio and not fusion and args.dtype == "bf16":
             ideal, fl, by = step_roofline(S, frames, head == "unfrozen")
             ms = 1e3 * elapsed / steps

@@ -98,8 +98,9 @@ def gemm_nt(A, B, C, M, N, K, lda=None, ldb=None, ldc=None, stats=None, gather=(
 
 def gemm_tn(G, X, P, M, N, K, S, rows_per_split, ldg=None, ldx=None, gather=(0, 0, 0, 0, 0, 1, 0), tile=0):
     dt = DT[G.dtype]
-    _lib.call("xcp_gemm_tn", dt, _p(G), ldg or N, _p(X), ldx or K, _p(P), M, N, K, S, rows_per_split, *gather,
-              tile, stream())
+    with _timed("gemm_tn", {"M": M, "N": N, "K": K, "ldg": ldg or N}):
+        _lib.call("xcp_gemm_tn", dt, _p(G), ldg or N, _p(X), ldx or K, _p(P), M, N, K, S, rows_per_split, *gather,
+                  tile, stream())
 
 
 def nt_stat_rows(M):
