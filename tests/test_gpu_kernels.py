@@ -360,9 +360,9 @@ def test_dw_bwd_row_bands(ops, gpu, monkeypatch, bands, N, C, H, act, res, skip)
         outs.append((dX, dW, sums, P))
     assert outs[1][3] == outs[0][3] * bands
     assert torch.equal(outs[0][0], outs[1][0])
-    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-5, atol=1e-5)
+    assert rel_err(outs[1][1], outs[0][1]) < 1e-5   # fp32 sums over more, shorter partial rows
     if act == 2:
-        torch.testing.assert_close(outs[1][2], outs[0][2], rtol=1e-6, atol=1e-4)
+        assert rel_err(outs[1][2], outs[0][2]) < 1e-5
     # the XCD-aware walk order is a permutation of the same waves: every output bitwise equal
     assert torch.equal(outs[2][0], outs[1][0]) and torch.equal(outs[2][1], outs[1][1])
     if act == 2:
