@@ -209,9 +209,11 @@ int xcp_opt_adam(const long long* tab, int nchunks, const float* coef, float lr,
                  float bc1, float bc2sqrt, xcp_stream_t stream);
 
 /* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][12] int64
- * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first 256-element block, s0, s1), nblocks in
+ * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first workgroup, s0, s1), nblocks workgroups in
  * total; output element (o0, o1, o2) goes to out[o0*s0 + o1*s1 + o2] (strides for the padded
- * layouts; dense: s1 = od2, s0 = od1*od2) */
+ * layouts; dense: s1 = od2, s0 = od1*od2).  A job takes xcp_permute3_blocks(...) workgroups
+ * (copies and 2-D transposes run as 32 x 32 tiles, other permutations one element per thread). */
+int xcp_permute3_blocks(int d0, int d1, int d2, int p0, int p1, int p2, long s0, long s1);
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, xcp_stream_t stream);
 
 /* ---- classification heads / losses of the training scripts (fp32) ----

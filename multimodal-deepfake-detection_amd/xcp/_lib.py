@@ -52,6 +52,7 @@ SIGNATURES = {
     "xcp_conv1_wgrad_parts": [I, I, I],
     "xcp_conv1_wgrad": [I, P, P, P, I, I, I, P],
     "xcp_permute3": [I, P, P, I, I, I, I, I, I, P],
+    "xcp_permute3_blocks": [I, I, I, I, I, I, L, L],
     "xcp_permute3_batch": [P, I, I, P],
     "xcp_frames_u8_to_f32": [P, P, P, I, I, I, I, P],
     "xcp_resize_bilinear": [P, P, I, I, I, I, I, P],
@@ -73,7 +74,7 @@ SIGNATURES = {
 }
 
 # entry points that return a size, not a status
-SIZE_QUERIES = {"xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
+SIZE_QUERIES = {"xcp_permute3_blocks", "xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
                 "xcp_colreduce_groups", "xcp_unit_bwd_rows_per_split",
                 "xcp_conv1_wgrad_parts", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
                 "xcp_maxpool_bwd_bnred_parts"}

@@ -122,10 +122,47 @@ __global__ __launch_bounds__(256) void permute3_kernel(const float* __restrict__
 
 // Many permute3 jobs in one launch (the per-step weight packing of every layer).  jobs is a
 // device array of [njobs][12] int64: in, out, d0, d1, d2, p0, p1, p2, out dtype, first block,
-// s0, s1 (output strides of the first two output axes: padded layouts).
-// Workgroup b finds its job by binary search over the first-block column (uniform per block).
+// s0, s1 (output strides of the first two output axes: padded layouts).  Workgroup b finds its
+// job by binary search over the first-block column (uniform per block).
+//
+// Every permutation the packs use is a copy or a (batched) 2-D transpose of rows of a
+// contiguous fp32 array: those run as 32 x 32 tiles (coalesced reads and writes, the transpose
+// through LDS), with the index arithmetic once per workgroup; anything else falls back to one
+// element per thread.  A per-element form with 64-bit division for every element took 114 us
+// per pack of the 21 M parameters (two per step).
 constexpr int PJ = 12;
+
+struct PermPlan {
+  int mode;                  // 0 copy, 1 transpose, 2 per element
+  int B, R, Cc;              // batch of [R][Cc] fp32 input rows
+  long ib, ob, ors;          // input batch stride, output batch stride, output row stride
+  int tiles() const { return B * ((R + 31) / 32) * ((Cc + 31) / 32); }
+};
+
+__host__ __device__ inline PermPlan perm_plan(int d0, int d1, int d2, int p0, int p1, int p2, long s0, long s1) {
+  PermPlan q{2, 1, 0, 0, 0, 0, 0};
+  const int od1 = p1 == 0 ? d0 : p1 == 1 ? d1 : d2, od2 = p2 == 0 ? d0 : p2 == 1 ? d1 : d2;
+  if (s1 != od2) return q;
+  if (p0 == 0 && p1 == 1 && p2 == 2) {   // out[i0][i1 i2] (row pitch s0)
+    q = PermPlan{0, 1, d0, d1 * d2, 0, 0, s0};
+  } else if (p0 == 1 && p1 == 0 && p2 == 2 && d2 == 1) {   // out[i1][i0]
+    q = PermPlan{1, 1, d0, d1, 0, 0, s0};
+  } else if (p0 == 0 && p1 == 2 && p2 == 1) {   // out[i0][i2][i1]: d0 transposes of [d1][d2]
+    q = PermPlan{1, d0, d1, d2, (long)d1 * d2, s0, s1};
+  } else if (p0 == 1 && p1 == 2 && p2 == 0 && s0 == (long)od1 * od2) {   // out[i1 i2][i0]
+    q = PermPlan{1, 1, d0, d1 * d2, 0, 0, d0};
+  }
+  (void)od1;
+  return q;
+}
+
+XCP_DEV inline void store_as(int dtype, void* out, long o, float v) {
+  if (dtype == XCP_BF16) reinterpret_cast<bf16*>(out)[o] = (bf16)v;
+  else reinterpret_cast<float*>(out)[o] = v;
+}
+
 __global__ __launch_bounds__(256) void permute3_batch_kernel(const long long* __restrict__ jobs, int njobs) {
+  __shared__ float tile[32][33];
   const int b = blockIdx.x;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
@@ -135,24 +172,53 @@ __global__ __launch_bounds__(256) void permute3_batch_kernel(const long long* __
   }
   const long long* j = jobs + (long)lo * PJ;
   const float* in = reinterpret_cast<const float*>(j[0]);
+  void* out = reinterpret_cast<void*>(j[1]);
   const int d0 = (int)j[2], d1 = (int)j[3], d2 = (int)j[4], p0 = (int)j[5], p1 = (int)j[6], p2 = (int)j[7];
-  const long total = (long)d0 * d1 * d2;
-  const long g = (long)(b - (int)j[9]) * 256 + threadIdx.x;
-  if (g >= total) return;
-  const int dims[3] = {d0, d1, d2};
-  const int od1 = dims[p1], od2 = dims[p2];
-  const int o2 = (int)(g % od2);
-  const long t = g / od2;
-  const int o1 = (int)(t % od1);
-  const int o0 = (int)(t / od1);
-  int idx[3];
-  idx[p0] = o0;
-  idx[p1] = o1;
-  idx[p2] = o2;
-  const float v = in[((long)idx[0] * d1 + idx[1]) * d2 + idx[2]];
-  const long o = (long)o0 * j[10] + (long)o1 * j[11] + o2;
-  if (j[8] == XCP_BF16) reinterpret_cast<bf16*>(j[1])[o] = (bf16)v;
-  else reinterpret_cast<float*>(j[1])[o] = v;
+  const int dtype = (int)j[8];
+  const PermPlan q = perm_plan(d0, d1, d2, p0, p1, p2, j[10], j[11]);
+  const int lb = b - (int)j[9];
+  if (q.mode == 2) {   // per element
+    const long total = (long)d0 * d1 * d2;
+    const long g = (long)lb * 256 + threadIdx.x;
+    if (g >= total) return;
+    const int dims[3] = {d0, d1, d2};
+    const int od1 = dims[p1], od2 = dims[p2];
+    const int o2 = (int)(g % od2);
+    const long t = g / od2;
+    const int o1 = (int)(t % od1);
+    const int o0 = (int)(t / od1);
+    int idx[3];
+    idx[p0] = o0;
+    idx[p1] = o1;
+    idx[p2] = o2;
+    store_as(dtype, out, (long)o0 * j[10] + (long)o1 * j[11] + o2, in[((long)idx[0] * d1 + idx[1]) * d2 + idx[2]]);
+    return;
+  }
+  const int ntr = (q.R + 31) / 32, ntc = (q.Cc + 31) / 32;
+  const int bb = lb / (ntr * ntc), rem = lb - bb * (ntr * ntc), tr = rem / ntc, tc = rem - tr * ntc;
+  const float* src = in + bb * q.ib;
+  const long obase = bb * q.ob;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = tc * 32 + tx;
+  if (q.mode == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = tr * 32 + ty + 8 * k;
+      if (r < q.R && c < q.Cc) store_as(dtype, out, obase + r * q.ors + c, src[(long)r * q.Cc + c]);
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = tr * 32 + ty + 8 * k;
+    tile[ty + 8 * k][tx] = (r < q.R && c < q.Cc) ? src[(long)r * q.Cc + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int oc = tc * 32 + ty + 8 * k, orow = tr * 32 + tx;   // output row = input column
+    if (oc < q.Cc && orow < q.R) store_as(dtype, out, obase + oc * q.ors + orow, tile[tx][ty + 8 * k]);
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -436,8 +502,15 @@ int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int 
   return (int)hipGetLastError();
 }
 
+// workgroups xcp_permute3_batch gives one job (the job table's first-block column advances by it)
+int xcp_permute3_blocks(int d0, int d1, int d2, int p0, int p1, int p2, long s0, long s1) {
+  const PermPlan q = perm_plan(d0, d1, d2, p0, p1, p2, s0, s1);
+  if (q.mode == 2) return (int)(((long)d0 * d1 * d2 + 255) / 256);
+  return q.tiles();
+}
+
 // njobs permute3 jobs ([njobs][12] int64 on the device, see permute3_batch_kernel) covering
-// nblocks 256-element blocks in total; the host validates the permutations when it builds them
+// nblocks workgroups in total; the host validates the permutations when it builds them
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, hipStream_t st) {
   if (njobs <= 0 || nblocks <= 0) return XCP_OK;
   hipLaunchKernelGGL(permute3_batch_kernel, dim3(nblocks), dim3(256), 0, st, jobs, njobs);

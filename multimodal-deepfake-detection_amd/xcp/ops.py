@@ -502,7 +502,7 @@ class PermuteBatch:
                     raise ValueError("permute job: bad permutation, size, dtype or layout")
                 check_gpu(s, d)
                 rows.append([s.data_ptr(), d.data_ptr(), d0, d1, d2, pm[0], pm[1], pm[2], DT[d.dtype], blk, s0, s1])
-                blk += (n + 255) // 256
+                blk += _lib.call("xcp_permute3_blocks", d0, d1, d2, pm[0], pm[1], pm[2], s0, s1)
             self._table = torch.tensor(rows, dtype=torch.int64).to(jobs[0][1].device)
             self._nblocks, self._key = blk, key
         _lib.call("xcp_permute3_batch", _p(self._table), len(jobs), self._nblocks, stream())

@@ -886,3 +886,33 @@ def test_reduce_batch_bitwise(ops, gpu):
     torch.cuda.synchronize()
     for P, S, L, ld, o0, o1, acc in jobs:
         assert torch.equal(o0, o1), (S, L, ld, acc)
+
+
+def test_permute_batch_plans(ops, gpu):
+    """The batched weight pack (xcp_permute3_batch): every job type the engine packs -- row copy
+    into a padded pitch, 2-D transpose into a padded pitch, batched transposes (conv2 [co][tap][ci]),
+    the (1, 2, 0) transpose (conv2T) -- plus a permutation outside those forms (per-element path),
+    in one launch, bf16 and fp32 destinations, against torch.permute (exact: a cast of fp32 values)."""
+    g = torch.Generator(device=gpu).manual_seed(3)
+    specs = [((728, 728, 1), (0, 1, 2), 736, torch.bfloat16), ((728, 728, 1), (1, 0, 2), 736, torch.bfloat16),
+             ((1024, 728, 1), (1, 0, 2), 1024, torch.bfloat16), ((736, 9, 1), (1, 0, 2), 736, torch.float32),
+             ((64, 32, 9), (0, 2, 1), None, torch.bfloat16), ((64, 32, 9), (1, 2, 0), None, torch.bfloat16),
+             ((5, 7, 3), (2, 0, 1), None, torch.float32), ((33, 65, 1), (0, 1, 2), 72, torch.float32)]
+    jobs, want = [], []
+    for (d0, d1, d2), pm, pitch, dt in specs:
+        src = torch.randn(d0, d1, d2, device=gpu, generator=g)
+        ref = src.permute(*pm).contiguous()
+        od = ref.shape
+        if pitch is None:
+            dst = torch.full((ref.numel(),), float("nan"), device=gpu, dtype=dt)
+            want.append((dst, ref.to(dt).reshape(-1), None))
+        else:   # padded [od0][pitch] destination, the padding left alone (zeros here)
+            dst = torch.zeros(od[0] * pitch, device=gpu, dtype=dt)
+            full = torch.zeros(od[0], pitch, device=gpu, dtype=dt)
+            full[:, :od[1] * od[2]] = ref.reshape(od[0], -1).to(dt)
+            want.append((dst, full.reshape(-1), None))
+        jobs.append((src.reshape(-1), dst, d0, d1, d2, pm, pitch))
+    ops.PermuteBatch().run(jobs)
+    torch.cuda.synchronize()
+    for dst, ref, _ in want:
+        assert torch.equal(dst, ref)
