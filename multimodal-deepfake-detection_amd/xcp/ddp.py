@@ -35,8 +35,14 @@ the backbone frozen for three epochs and then unfreezes it (train_visual.py:547-
 frozen parameters keep ``grad = None`` (so an optimiser skips them, as in the reference)
 and buckets only span parameters that require grad.
 """
+import os
+
 import torch
 import torch.distributed as dist
+
+# XCP_DDP_COMM_STREAM=0: launch the bucket all-reduces from the current stream after making it wait
+# on the weight-gradient stream (the round-3 behaviour; A/B)
+COMM_STREAM = os.environ.get("XCP_DDP_COMM_STREAM", "1") != "0"
 
 
 class GradBuckets:
@@ -171,6 +177,12 @@ class GradBuckets:
             return
         if not self.use_streams:
             for bi in bis:   # CPU tensors (gloo): no streams
+                self._launch(bi)
+            return
+        if not COMM_STREAM:
+            if side_stream is not None:
+                torch.cuda.current_stream(self.flat.device).wait_stream(side_stream)
+            for bi in bis:
                 self._launch(bi)
             return
         comm = self.comm_stream()
