@@ -22,13 +22,15 @@ it.  A bucket's all-reduce is launched the moment its last gradient is final:
   are still in backward.
 
 Streams.  A bucket's gradients are written by the main (backward) stream and, for the
-pointwise weight gradients, by the engine's weight-gradient side stream.  The all-reduces are
-launched from a dedicated communication stream that waits on both; the main stream never
-waits on the side stream or on a collective before the backward has been enqueued
-(``allreduce()`` makes it wait for the collectives, the engine for its side stream at the
-end of its backward).  Making the main stream wait on the side stream at every completed
-bucket instead would drain the side stream's queued weight-gradient GEMMs mid-backward, about
-once per 25 MB bucket, and give back the overlap the side stream exists for.
+pointwise weight gradients, by the engine's weight-gradient side stream.  A completed bucket's
+all-reduce is launched from the side stream after it waits on the main stream (which it is
+normally behind already): the collective then follows every gradient of the bucket, and the main
+stream never waits on the side stream or on a collective before the backward has been enqueued
+(``allreduce()`` makes it wait for the collectives, the engine for its side stream at the end of
+its backward).  Making the main stream wait on the side stream at every completed bucket instead
+(round 3) would drain the side stream's queued weight-gradient GEMMs mid-backward, about once per
+25 MB bucket, and give back the overlap the side stream exists for.  A third, dedicated
+communication stream waiting on both was measured and dropped (XCP_DDP_LAUNCH above).
 
 Which parameters take part is re-read at every ``zero()``: the reference trains with
 the backbone frozen for three epochs and then unfreezes it (train_visual.py:547-556);
@@ -40,9 +42,14 @@ import os
 import torch
 import torch.distributed as dist
 
-# XCP_DDP_COMM_STREAM=0: launch the bucket all-reduces from the current stream after making it wait
-# on the weight-gradient stream (the round-3 behaviour; A/B)
-COMM_STREAM = os.environ.get("XCP_DDP_COMM_STREAM", "1") != "0"
+# Where a bucket's all-reduce is launched from (XCP_DDP_LAUNCH):
+#   side (default): the engine's weight-gradient stream, after it waits on the current stream;
+#   comm: a communication stream of its own that waits on both (measured: the 2-rank gloo path ran
+#         13-17x slower per step this way, 944 vs 74 ms at 4 clips per rank, profiles/r04_ddp_ab.txt);
+#   main: the current stream after it waits on the weight-gradient stream (the round-3 order).
+DDP_LAUNCH = os.environ.get("XCP_DDP_LAUNCH", "side")
+if DDP_LAUNCH not in ("side", "comm", "main"):
+    raise ValueError("XCP_DDP_LAUNCH must be side, comm or main")
 
 
 class GradBuckets:
@@ -179,14 +186,21 @@ class GradBuckets:
             for bi in bis:   # CPU tensors (gloo): no streams
                 self._launch(bi)
             return
-        if not COMM_STREAM:
+        cur = torch.cuda.current_stream(self.flat.device)
+        if DDP_LAUNCH == "main" or (DDP_LAUNCH == "side" and side_stream is None):
             if side_stream is not None:
-                torch.cuda.current_stream(self.flat.device).wait_stream(side_stream)
+                cur.wait_stream(side_stream)
             for bi in bis:
                 self._launch(bi)
             return
+        if DDP_LAUNCH == "side":
+            side_stream.wait_stream(cur)
+            with torch.cuda.stream(side_stream):
+                for bi in bis:
+                    self._launch(bi)
+            return
         comm = self.comm_stream()
-        comm.wait_stream(torch.cuda.current_stream(self.flat.device))
+        comm.wait_stream(cur)
         if side_stream is not None:
             comm.wait_stream(side_stream)
         with torch.cuda.stream(comm):

@@ -11,3 +11,10 @@ for v in 0 2 4 0 2 4; do
   XCP_DW_BWD_XCD=1 XCP_DW_FWD_P=$v timeout -k 10 200 python bench.py $Q > gpurun_out/e_step_p$v.json 2>> gpurun_out/e_step.err || exit $?
   echo "$v $(cat gpurun_out/e_step_p$v.json)" >> gpurun_out/e_step.log
 done
+# the 2-rank gloo path (ranks share cuda:0): collectives launched from the side stream (default),
+# the main stream (round 3) or a communication stream
+S="--steps 3 --warmup 2 --batch 4 --mode unfrozen --cpu-baseline off --small-batch 0 --measured-peaks off --no-kernel-timing --diag off"
+for v in side main comm; do
+  XCP_DDP_LAUNCH=$v XCP_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 $S > gpurun_out/e_g2_$v.json 2> gpurun_out/e_g2_$v.err || exit $?
+done
+timeout -k 10 300 python -u -m pytest -p no:cacheprovider --timeout 300 --timeout-method thread -rf tests/test_gpu_ddp.py -q > gpurun_out/e_ddp_tests.log 2>&1 || exit $?
