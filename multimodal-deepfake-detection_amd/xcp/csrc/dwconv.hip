@@ -278,162 +278,6 @@ __global__ __launch_bounds__(256) void dw_fwd_w2_kernel(DwArgs a) {
   }
 }
 
-// Persistent form of dw_fwd_w2_kernel: grid = a few workgroups per CU, each walking tiles
-// t = L, L + G, ... (L = its XCD-remapped index, so the tiles in flight on an XCD are neighbouring
-// channel slices that share lines).  The halo of the NEXT tile is brought into the other half of a
-// double LDS buffer by LDS-DMA (raw bf16, no registers) while this tile is transformed in place
-// (activation, zero padding), computed and stored, so the loads of one tile overlap the work of the
-// previous one inside a workgroup.  The activation is rounded to bf16 in LDS as the staging of
-// dw_fwd_w2_kernel does, and the per-channel fma chain is the same: outputs are bitwise equal.
-__device__ __attribute__((aligned(64))) uint4 g_fzero[4];
-
-template <int ACT, int MAXPX, int SG>
-__global__ __launch_bounds__(256) void dw_fwd_p_kernel(DwArgs a, int ntiles) {
-  constexpr int FS = SLICE, LANES = FS / 8, NWK = 256 / LANES, CPL = 4;
-  constexpr int BUFB = MAXPX * FS;
-  __shared__ __attribute__((aligned(16))) char sA[2 * BUFB];
-  const TileGeo& g = a.g;
-  const int G = gridDim.x;
-  const int L = xcd_remap(blockIdx.x, G);
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int cl = threadIdx.x % LANES, wk = threadIdx.x / LANES;
-  const int npx = g.HP * g.WP, nchunk = npx * 4, ninst = (nchunk + 63) / 64;
-  const int ntl = g.nth * g.ntw;
-  const bf16* X = reinterpret_cast<const bf16*>(a.X);
-  bf16* Y = reinterpret_cast<bf16*>(a.Y);
-  auto coords = [&](int t, int& grp, long& nbase, int& th0, int& tw0) {
-    grp = t % a.ngroups;
-    const int sp = t / a.ngroups, tile = sp % ntl, n = sp / ntl;
-    nbase = (long)n * a.H * a.W;
-    th0 = (tile / g.ntw) * g.TH;
-    tw0 = (tile % g.ntw) * g.TW;
-  };
-  // LDS-DMA of tile t's halo (16-B chunk i = pixel i/4, part i%4 lands at byte 16 i of the buffer;
-  // chunks outside the frame / channels read a zero line)
-  auto issue = [&](int t, int buf) {
-    int grp, th0, tw0;
-    long nbase;
-    coords(t, grp, nbase, th0, tw0);
-    const int c0 = grp * (FS / 2);
-    for (int k = w; k < ninst; k += 4) {
-      const int i = k * 64 + lane, p = i >> 2, q = i & 3;
-      const int hy = p / g.WP, hx = p - hy * g.WP;
-      const int h = th0 - 1 + hy, x = tw0 - 1 + hx, c = c0 + q * 8;
-      const bool ok = i < nchunk && h >= 0 && h < a.H && x >= 0 && x < a.W && c < a.C;
-      const void* src = ok ? (const void*)(X + (nbase + (long)h * a.W + x) * a.C + c) : (const void*)g_fzero;
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                       (void __attribute__((address_space(3)))*)(sA + buf * BUFB + k * 1024), 16, 0,
-                                       0);
-    }
-  };
-  int t = L;
-  if (t >= ntiles) return;
-  issue(t, 0);
-  int buf = 0;
-  for (; t < ntiles; t += G) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's DMA of tile t landed (and its stores left)
-    __syncthreads();                      // every wave's DMA landed; every wave done with the other buffer
-    if (t + G < ntiles) issue(t + G, buf ^ 1);
-    int grp, th0, tw0;
-    long nbase;
-    coords(t, grp, nbase, th0, tw0);
-    const int c0 = grp * (FS / 2);
-    char* sb = sA + buf * BUFB;
-    if constexpr (ACT != ACT_NONE) {   // in place: activation, rounded to bf16; zero outside the frame
-      const int q = threadIdx.x & 3;   // fixed for this thread (256 chunks per pass)
-      float sc[8], sh[8];
-      if constexpr (ACT == ACT_BNRELU) {
-        const int cq = min(c0 + q * 8, a.C - 8);
-        VecIO<float, 8>::load(a.scale + cq, sc);
-        VecIO<float, 8>::load(a.shift + cq, sh);
-      }
-      for (int i = threadIdx.x; i < nchunk; i += 256) {
-        const int p = i >> 2, hy = p / g.WP, hx = p - hy * g.WP;
-        const int h = th0 - 1 + hy, x = tw0 - 1 + hx, c = c0 + q * 8;
-        const bool ok = h >= 0 && h < a.H && x >= 0 && x < a.W && c < a.C;
-        uint4 u = *reinterpret_cast<const uint4*>(sb + i * 16);
-        if (ok) {
-          float f[8];
-          VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&u), f);
-          typedef float p2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-          for (int j = 0; j < 8; j += 2) {
-            p2 v = p2{f[j], f[j + 1]};
-            if constexpr (ACT == ACT_BNRELU) v = __builtin_elementwise_fma(v, p2{sc[j], sc[j + 1]}, p2{sh[j], sh[j + 1]});
-            v = __builtin_elementwise_max(v, p2(0.f));
-            f[j] = v[0];
-            f[j + 1] = v[1];
-          }
-          VecIO<bf16, 8>::store(reinterpret_cast<bf16*>(&u), f);
-        } else {
-          u = make_uint4(0, 0, 0, 0);
-        }
-        *reinterpret_cast<uint4*>(sb + i * 16) = u;
-      }
-      __syncthreads();
-    }
-    const int c = c0 + cl * CPL;
-    if (c < a.C) {
-      float wt[9][CPL];
-#pragma unroll
-      for (int tp = 0; tp < 9; ++tp) VecIO<float, CPL>::load(a.Wt + (long)tp * a.C + c, wt[tp]);
-      const int items = g.TH * g.nseg;
-      const char* lbase = sb + cl * 8;
-      for (int it = wk; it < items; it += NWK) {
-        const int r = it / g.nseg, sgi = it - r * g.nseg;
-        const int oh = th0 + r, x0 = sgi * SG;
-        if (oh >= a.H) continue;
-        const char* base = lbase + (r * g.WP + x0) * FS;
-        float win[3][SG + 2][CPL];
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int k = 0; k < SG + 2; ++k) {
-            const uint2 u = *reinterpret_cast<const uint2*>(base + (ky * g.WP + k) * FS);
-            unpack(u.x, win[ky][k], (bf16*)nullptr);
-            unpack(u.y, win[ky][k] + 2, (bf16*)nullptr);
-          }
-        bf16* yrow = Y + (nbase + (long)oh * a.W + tw0) * a.C + c;
-#pragma unroll
-        for (int j = 0; j < SG; ++j) {
-          float o[CPL];
-#pragma unroll
-          for (int e = 0; e < CPL; ++e) {
-            float s = 0.f;
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-              for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
-            o[e] = s;
-          }
-          const int x = x0 + j;
-          if (x < g.TW && tw0 + x < a.W)
-            *reinterpret_cast<uint2*>(yrow + (long)x * a.C) = make_uint2(pack(o, (bf16*)nullptr), pack(o + 2, (bf16*)nullptr));
-        }
-      }
-    }
-    buf ^= 1;
-  }
-}
-
-// XCP_DW_FWD_P=<n>: the persistent double-buffered forward with n workgroups per CU (2: 512-pixel
-// tiles, 64 KB of LDS each; 4: 256-pixel tiles); 0 or unset: dw_fwd_w2_kernel (read per call, A/B)
-int dw_fwd_persistent() {
-  const char* e = getenv("XCP_DW_FWD_P");
-  const int v = e ? atoi(e) : 0;
-  return v == 2 || v == 4 ? v : 0;
-}
-
-int dw_gpu_cus() {
-  static const int cus = [] {
-    int d = 0, n = 0;
-    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-      n = 0;
-    return n > 0 ? n : 256;
-  }();
-  return cus;
-}
-
 // bf16 64-B-slice forwards run dw_fwd_w2_kernel with 5-pixel segments by default: 67 -> 64.5 us
 // at 19^2 x 736, 262 -> 246 at 37^2, 766 -> 733 at 147^2 x 128, bitwise-equal outputs
 // (tools/kbench.py dwshapes fingerprints, profiles/r03_dw_fwd_w2_ab.txt).  XCP_DW_FWD_W2=0 selects
@@ -942,21 +786,25 @@ bool dw_bwd_occ4() {
   return v;
 }
 
-// Row bands per frame: XCP_DW_BWD_BANDS=<b> splits every frame's row walk into b bands of
-// ceil(H / b) rows (one wave each; a band re-reads the dY rows just above and below it), so that
-// a launch has more, shorter waves.  Frames under 2 b rows keep one band.  (Read per call, so a
-// test can compare band counts in one process.)
+// Row bands per frame: the row walk of a frame split into b bands of ceil(H / b) rows (one wave
+// each; a band re-reads the dY rows just above and below it).  Default: 3 bands for frames of 64
+// rows or more (147^2 x 128: 1,101 -> 1,041 us; 74^2 x 256: 560 -> 548), one below (at 19^2 two
+// bands cost 119.5 -> 125 us: the extra halo rows outweigh the shorter tail; profiles/r04_dw_tn_ab.txt).
+// XCP_DW_BWD_BANDS=<b> forces b for every frame of >= 2 b rows.  (Read per call, so a test can
+// compare band counts in one process.)
 int dw_bwd_bands(int H) {
   const char* e = getenv("XCP_DW_BWD_BANDS");
-  int v = e ? atoi(e) : 1;
+  int v = e ? atoi(e) : (H >= 64 ? 3 : 1);
   v = v >= 1 && v <= 8 ? v : 1;
   return H >= 2 * v ? v : 1;
 }
 
-// XCP_DW_BWD_XCD=1: XCD-aware workgroup order for the backward walk (A/B; read per call)
+// XCD-aware workgroup order for the backward walk (default; 19^2 x 736: 119.5 -> 117.8 us, with the
+// residual 143.5 -> 137.8; the step +0.3 %, profiles/r04_dw_tn_ab.txt).  XCP_DW_BWD_XCD=0 turns it off
+// (read per call).
 int dw_bwd_xcd() {
   const char* e = getenv("XCP_DW_BWD_XCD");
-  return e && e[0] == '1' ? 1 : 0;
+  return e && e[0] == '0' ? 0 : 1;
 }
 
 template <typename T, int ACT>
@@ -1002,19 +850,6 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
     return launch_fwd<float, FWD_MAXPX128, 128>(act, a, stream);
   }
   DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype), tile_geo(H, W, FWD_MAXPX)};
-  if (dtype == XCP_BF16 && dw_fwd_persistent()) {
-    const int per = dw_fwd_persistent();
-    a.g = tile_geo(H, W, per == 2 ? 512 : 256, 5);
-    const int ntiles = a.N * a.g.nth * a.g.ntw * a.ngroups;
-    const int grid = min(ntiles, per * dw_gpu_cus());
-#define XCP_P(MP)                                                                                                     \
-    if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_p_kernel<ACT_NONE, MP, 5>), dim3(grid), dim3(256), 0, stream, a, ntiles); \
-    else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_p_kernel<ACT_RELU, MP, 5>), dim3(grid), dim3(256), 0, stream, a, ntiles); \
-    else hipLaunchKernelGGL((dw_fwd_p_kernel<ACT_BNRELU, MP, 5>), dim3(grid), dim3(256), 0, stream, a, ntiles);
-    if (per == 2) { XCP_P(512) } else { XCP_P(256) }
-#undef XCP_P
-    return (int)hipGetLastError();
-  }
   if (dtype == XCP_BF16 && dw_fwd_w2()) {
     const int sg = dw_fwd_w2();
     a.g = tile_geo(H, W, FWD_MAXPX, sg);

@@ -916,29 +916,3 @@ def test_permute_batch_plans(ops, gpu):
     torch.cuda.synchronize()
     for dst, ref, _ in want:
         assert torch.equal(dst, ref)
-
-
-@pytest.mark.parametrize("per", ["2", "4"])
-@pytest.mark.parametrize("N,C,H,act", [(64, 736, 19, 2), (64, 736, 19, 1), (16, 736, 37, 2), (8, 256, 74, 2),
-                                       (4, 128, 147, 2), (4, 64, 147, 0), (32, 1536, 10, 2), (3, 200, 9, 2),
-                                       (300, 736, 19, 2)])
-def test_dw_fwd_persistent_bitwise(ops, gpu, monkeypatch, per, N, C, H, act):
-    """The persistent double-buffered depthwise forward (XCP_DW_FWD_P=2 / 4 workgroups per CU; the
-    next tile's halo by LDS-DMA while this one is transformed in place, computed and stored):
-    bitwise equal to the default tile kernel (same bf16 rounding of the activation, same fma chain),
-    including the zero padding around the frame and many tiles per workgroup (N = 300)."""
-    W = H + 2
-    g = torch.Generator(device=gpu).manual_seed(N + C + H + act)
-    x = torch.randn(N * H * W, C, device=gpu, generator=g).bfloat16()
-    Wt = torch.randn(9, C, device=gpu, generator=g) / 3
-    sc = torch.rand(C, device=gpu, generator=g) + 0.5
-    sh = torch.randn(C, device=gpu, generator=g) * 0.2
-    outs = []
-    for v in ("0", per):
-        monkeypatch.setenv("XCP_DW_FWD_P", v)
-        Y = torch.full((N * H * W, C), float("nan"), device=gpu, dtype=torch.bfloat16)
-        ops.dw_fwd(act, x, Y, Wt, sc, sh, N, H, W, C)
-        torch.cuda.synchronize()
-        outs.append(Y)
-    assert not torch.isnan(outs[1].float()).any()
-    assert torch.equal(outs[0], outs[1])
