@@ -10,6 +10,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxcp.so")
+# XCP_LIB_PATH: load another build of the same ABI instead (A/B of a kernel change in the step;
+# tools/build_variant.py links one)
+LIB_PATH = os.environ.get("XCP_LIB_PATH") or LIB_PATH
 
 P = ctypes.c_void_p
 I = ctypes.c_int

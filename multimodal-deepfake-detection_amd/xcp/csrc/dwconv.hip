@@ -493,6 +493,29 @@ XCP_DEV void store_row(T* frame, int h, int W, int C, const RowLanes& rl, const 
   }
 }
 
+// LDS reads of the DMA ring by inline asm: a plain C++ read of LDS that an LDS-DMA may write makes
+// hipcc drain every outstanding vector-memory operation first (s_waitcnt vmcnt(0)) -- here right
+// after a step had issued the look-ahead rows, so every step waited for the rows it had just asked
+// for and the look-ahead never overlapped anything.  The counted vmwait at the top of a step is what
+// orders the ring; ring_fence() retires the asm reads before their values are used (pinned through
+// "+v" operands, so no use is scheduled ahead of the wait).
+XCP_DEV unsigned ring_u32(const char* p) {
+  unsigned v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((unsigned)(size_t)(const __attribute__((address_space(3))) char*)(p))
+               : "memory");
+  return v;
+}
+template <int N>
+XCP_DEV void ring_fence(unsigned (&v)[N]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+XCP_DEV void ring_fence1(unsigned& v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("" : "+v"(v));
+}
+
 // Without a residual input (ROLL = false) the three dY rows a step needs (h-1, h, h+1) are read
 // from the LDS ring one row at a time and consumed at once (dgrad and wgrad FMAs of that row), so
 // only one 7-column window is live instead of three rolling ones: 177 -> 140-152 VGPRs, three
@@ -500,7 +523,11 @@ XCP_DEV void store_row(T* frame, int h, int W, int C, const RowLanes& rl, const 
 // landed, h+3 staged).  With the residual (ROLL = true) the extra ring slots would cost a
 // workgroup per CU (LDS), so the rolling register windows stay: measured 125.2 vs 138.6 us
 // without, 148.1 vs 142.3 us with the residual at 19^2 x 736 (profiles/r03_dwb_ab.txt).
-template <typename T, int ACT, bool RES, bool ROLL, int BDV = 2, int MINW = (ROLL ? 2 : 3), bool SKIP = true>
+// BNRES: the BN partial sums are taken over the final dX against a.Yb (xcp_dw_bwd_resbn; a template
+// argument so the other forms carry no conditional loads -- a load behind a runtime branch made hipcc
+// drain vmcnt(0) at the branch's join on every row step)
+template <typename T, int ACT, bool RES, bool ROLL, int BDV = 2, int MINW = (ROLL ? 2 : 3), bool SKIP = true,
+          bool BNRES = false>
 __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   typedef RV<T> R;
   typedef typename R::V V;
@@ -531,7 +558,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const RowLanes rl_ld = row_lanes_load<T>(a.W, a.C, x0w, c0, lane);
   const RowLanes rl_st = row_lanes_store<T>(a.W, a.C, x0w, c0, lane);
   const bool bnsum = a.bnpart != nullptr;
-  const bool bnres = RES && bnsum && a.Yb != nullptr;   // sums over the final dX against Yb
+  constexpr bool bnres = RES && BNRES;                  // sums over the final dX against Yb (bnsum implied)
   const bool bnx = bnsum && !bnres;                     // sums over the masked dz against X
   V wt[9], dw[9], sc = V(1.f), sh = V(0.f), bs1 = V(0.f), bs2 = V(0.f), mu = V(0.f), is = V(0.f);
 #pragma unroll
@@ -560,10 +587,14 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
   T* dX = reinterpret_cast<T*>(a.dX) + fbase;
   const int lofs = sg * RS * SLICE + cl * 4;
-  auto rd = [&](const char* row, int k) { return *reinterpret_cast<const unsigned*>(row + lofs + k * SLICE); };
+  auto rd = [&](const char* row, int k) { return ring_u32(row + lofs + k * SLICE); };   // (retire with ring_fence)
   auto cvtg = [&](const char* row, V (&gy)[RS + 2]) {
+    unsigned u[RS + 2];
 #pragma unroll
-    for (int k = 0; k < RS + 2; ++k) gy[k] = R::unpack(rd(row, k));   // staged zero padding
+    for (int k = 0; k < RS + 2; ++k) u[k] = rd(row, k);
+    ring_fence(u);
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) gy[k] = R::unpack(u[k]);   // staged zero padding
   };
   auto sx = [&](int r) { return rx + (r % NS) * LROW; };
   auto sgs = [&](int r) { return rg + ((r + NSG) % NSG) * LROW; };   // (r >= -1)
@@ -585,19 +616,25 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     for (int j = 0; j < RS; ++j) pskp[j] = 0u;
     unsigned pyb[RES ? RS : 1];
     if constexpr (RES) {
-      if (bnres) {   // raw values of the BN input at this row's output pixels (clamped column, masked below)
+      if constexpr (bnres) {   // raw values of the BN input at this row's output pixels (clamped column, masked below)
         const T* yrow = reinterpret_cast<const T*>(a.Yb) + fbase + (long)h * a.W * a.C + cc;
 #pragma unroll
         for (int j = 0; j < RS; ++j) pyb[j] = *reinterpret_cast<const unsigned*>(yrow + (long)min(x0 + j, a.W - 1) * a.C);
       }
     }
-    if (skip_row) {
+    if constexpr (SKIP) {
+      // every step issues the same loads from clamped addresses (masked afterwards): a load behind
+      // a runtime branch makes hipcc drain vmcnt(0) where the branch joins, on every row step
+      const int srow = min(h / a.sS, max(a.sOH - 1, 0));
 #pragma unroll
       for (int j = 0; j < RS; ++j) {
         const int ow = x0 + j;
-        if (cok && ow % a.sS == 0 && ow / a.sS < a.sOW && ow < a.W)
-          pskp[j] = *reinterpret_cast<const unsigned*>(
-              dSkip + (((long)mp.n * a.sOH + h / a.sS) * a.sOW + ow / a.sS) * a.C + c);
+        const bool ok = skip_row && cok && ow % a.sS == 0 && ow / a.sS < a.sOW && ow < a.W;
+        const int scol = min(max(ow, 0) / a.sS, max(a.sOW - 1, 0));
+        const T* ptr = dSkip ? dSkip + (((long)mp.n * a.sOH + srow) * a.sOW + scol) * a.C + cc
+                             : reinterpret_cast<const T*>(g_dzero);
+        const unsigned v = *reinterpret_cast<const unsigned*>(ptr);
+        pskp[j] = ok ? v : 0u;
       }
     }
     // activated X row h (slot sxh; zero padded after the activation), raw centre values
@@ -605,9 +642,13 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     constexpr bool KEEP_XR = MINW < 4;
     V xa[RS + 2];
     unsigned xr[KEEP_XR ? RS : 1];
+    unsigned xu[RS + 2];
+#pragma unroll
+    for (int k = 0; k < RS + 2; ++k) xu[k] = rd(sxh, k);
+    ring_fence(xu);
 #pragma unroll
     for (int k = 0; k < RS + 2; ++k) {
-      const unsigned u = rd(sxh, k);
+      const unsigned u = xu[k];
       V v = R::unpack(u);
       if constexpr (ACT == ACT_BNRELU) {
         v = vmax0(vfma(v, sc, sh));
@@ -624,6 +665,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     if constexpr (RES) {
 #pragma unroll
       for (int j = 0; j < RS; ++j) pres[j] = rd(srh, j + 1);
+      ring_fence(pres);
     }
     stage_row<T>(X, h + BD, hx, a.W, a.C, rl_ld, sx(h + BD), lane);          // slot of X row h-1
     stage_row<T>(G, h + 1 + BD, hg, a.W, a.C, rl_ld, sgs(h + 1 + BD), lane);   // slot of dY row h
@@ -686,13 +728,19 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
         const bool valid = cok && x0 + j < a.W;
         const V dz = valid ? R::unpack(R::pack(s)) : V(0.f);   // the stored (rounded) dz
         bs1 += dz;
-        const unsigned xraw = KEEP_XR ? xr[KEEP_XR ? j : 0] : rd(sxh, j + 1);
+        unsigned xraw;
+        if constexpr (KEEP_XR) {
+          xraw = xr[j];
+        } else {
+          xraw = rd(sxh, j + 1);
+          ring_fence1(xraw);
+        }
         bs2 = vfma(dz, (R::unpack(xraw) - mu) * is, bs2);
       }
       if constexpr (RES) s += R::unpack(pres[j]);
       if (skip_row && !a.skip_pre) s += R::unpack(pskp[j]);
       if constexpr (RES) {
-        if (bnres) {
+        if constexpr (bnres) {
           const bool valid = cok && x0 + j < a.W;
           const V dz = valid ? R::unpack(R::pack(s)) : V(0.f);   // the stored (rounded) dX
           bs1 += dz;
@@ -810,7 +858,11 @@ int dw_bwd_xcd() {
 template <typename T, int ACT>
 void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
   if (a.dRes && dw_bwd_occ4() && !a.dSkip)
-    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, false, 1, 3, false>), dim3(blocks), dim3(256), 0, st, a);
+  {
+    if (a.Yb) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, false, 1, 3, false, true>), dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, false, 1, 3, false>), dim3(blocks), dim3(256), 0, st, a);
+  } else if (a.dRes && a.Yb)
+    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true, 2, 2, true, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (dw_bwd_roll_all()) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (dw_bwd_occ4() && !a.dSkip)
