@@ -527,7 +527,7 @@ XCP_DEV void ring_fence1(unsigned& v) {
 // argument so the other forms carry no conditional loads -- a load behind a runtime branch made hipcc
 // drain vmcnt(0) at the branch's join on every row step)
 template <typename T, int ACT, bool RES, bool ROLL, int BDV = 2, int MINW = (ROLL ? 2 : 3), bool SKIP = true,
-          bool BNRES = false>
+          bool BNRES = false, bool ASMRD = true>
 __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   typedef RV<T> R;
   typedef typename R::V V;
@@ -587,12 +587,20 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
   T* dX = reinterpret_cast<T*>(a.dX) + fbase;
   const int lofs = sg * RS * SLICE + cl * 4;
-  auto rd = [&](const char* row, int k) { return ring_u32(row + lofs + k * SLICE); };   // (retire with ring_fence)
+  // ring reads: inline asm retired by fence() (ASMRD), or plain C++ reads (hipcc's own waits; see
+  // ring_u32 above and launch_bwd_act for where each form is used)
+  auto rd = [&](const char* row, int k) {
+    if constexpr (ASMRD) return ring_u32(row + lofs + k * SLICE);
+    else return *reinterpret_cast<const unsigned*>(row + lofs + k * SLICE);
+  };
+  auto fence = [&](auto& v) {
+    if constexpr (ASMRD) ring_fence(v);
+  };
   auto cvtg = [&](const char* row, V (&gy)[RS + 2]) {
     unsigned u[RS + 2];
 #pragma unroll
     for (int k = 0; k < RS + 2; ++k) u[k] = rd(row, k);
-    ring_fence(u);
+    fence(u);
 #pragma unroll
     for (int k = 0; k < RS + 2; ++k) gy[k] = R::unpack(u[k]);   // staged zero padding
   };
@@ -645,7 +653,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     unsigned xu[RS + 2];
 #pragma unroll
     for (int k = 0; k < RS + 2; ++k) xu[k] = rd(sxh, k);
-    ring_fence(xu);
+    fence(xu);
 #pragma unroll
     for (int k = 0; k < RS + 2; ++k) {
       const unsigned u = xu[k];
@@ -665,7 +673,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     if constexpr (RES) {
 #pragma unroll
       for (int j = 0; j < RS; ++j) pres[j] = rd(srh, j + 1);
-      ring_fence(pres);
+      fence(pres);
     }
     stage_row<T>(X, h + BD, hx, a.W, a.C, rl_ld, sx(h + BD), lane);          // slot of X row h-1
     stage_row<T>(G, h + 1 + BD, hg, a.W, a.C, rl_ld, sgs(h + 1 + BD), lane);   // slot of dY row h
@@ -733,7 +741,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
           xraw = xr[j];
         } else {
           xraw = rd(sxh, j + 1);
-          ring_fence1(xraw);
+          if constexpr (ASMRD) ring_fence1(xraw);
         }
         bs2 = vfma(dz, (R::unpack(xraw) - mu) * is, bs2);
       }
@@ -855,6 +863,17 @@ int dw_bwd_xcd() {
   return e && e[0] == '0' ? 0 : 1;
 }
 
+// Ring reads by inline asm (no vmcnt(0) drain ahead of them) for frames below 32 rows, plain reads
+// above: at the step's shapes the asm form measured 118.4 -> 111.0 us at 19^2 x 736 but 398 -> 408 at
+// 37^2, 536 -> 544 at 74^2 and 1,034 -> 1,110 at 147^2 (tools/dw_ab.py, profiles/r04_dw_asm_ab.txt):
+// with long walks the drain costs less than the per-read lgkmcnt(0) fences that replace it.
+// XCP_DW_BWD_ASM=0 / 1 forces the plain / asm form for every frame (read per call).
+bool dw_bwd_asm_reads(int H) {
+  const char* e = getenv("XCP_DW_BWD_ASM");
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  return H < 32;
+}
+
 template <typename T, int ACT>
 void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
   if (a.dRes && dw_bwd_occ4() && !a.dSkip)
@@ -865,8 +884,13 @@ void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
     hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true, 2, 2, true, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (dw_bwd_roll_all()) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, true>), dim3(blocks), dim3(256), 0, st, a);
-  else if (dw_bwd_occ4() && !a.dSkip)
-    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 4, false>), dim3(blocks), dim3(256), 0, st, a);
+  else if (dw_bwd_occ4() && !a.dSkip) {
+    if (dw_bwd_asm_reads(a.H))
+      hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 4, false>), dim3(blocks), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 4, false, false, false>), dim3(blocks), dim3(256), 0,
+                         st, a);
+  }
   else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false>), dim3(blocks), dim3(256), 0, st, a);
 }
 

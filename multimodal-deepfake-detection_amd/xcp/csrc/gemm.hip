@@ -845,6 +845,7 @@ struct TNArgs {
   float* P;                // [S][N][K] fp32 partials
   int M, N, K, S, rows_per_split;
   Gather gx;               // gather of the X operand rows / columns
+  int xalign;              // 256x256 kernel: workgroup b = split (b / 8 / tiles) * 8 + b % 8, tile b / 8 % tiles
 };
 
 template <typename T, int GM>
@@ -1028,8 +1029,22 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[T_RING * T_STEP];
   const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
   const int tiles = gridN * gridK;
-  const int id = xcd_remap(blockIdx.x, gridDim.x);   // one split's tiles share an XCD (its rows stay in L2)
-  const int sp = id / tiles, t = id % tiles;
+  // one split's tiles on one XCD, where its row panels are shared through L2.  xalign: workgroups go
+  // to the XCDs round-robin (b % 8), so split (q / tiles) * 8 + b % 8 takes every tile q % tiles of
+  // XCD b % 8's slot row q / tiles -- whole splits per XCD (the grid is padded to 8 splits per slot
+  // row; the padding workgroups return at once).  Otherwise consecutive remapped ids share an XCD,
+  // and a split whose tiles straddle two ranges is read by both XCDs.
+  int sp, t;
+  if (a.xalign) {
+    const int q = blockIdx.x >> 3;
+    sp = (q / tiles) * 8 + (blockIdx.x & 7);
+    t = q % tiles;
+    if (sp >= a.S) return;
+  } else {
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    sp = id / tiles;
+    t = id % tiles;
+  }
   const int n0 = (t / gridK) * 256, k0 = (t % gridK) * 256;
   const int mbeg = sp * a.rows_per_split;
   const int mend = min(a.M, mbeg + a.rows_per_split);
@@ -1188,6 +1203,11 @@ bool tn_xcd_splits() {   // XCP_TN_XCD_SPLITS=1 (A/B; measured -0.3 % in the ste
     return e && e[0] == '1';
   }();
   return v;
+}
+// XCP_TN_XCD_ALIGN=1: whole splits per XCD for outputs of at most 32 tiles (read per call; A/B)
+bool tn_xcd_align() {
+  const char* e = getenv("XCP_TN_XCD_ALIGN");
+  return e && e[0] == '1';
 }
 int tn_target_wgs() {   // XCP_TN_TARGET_WGS=<n> overrides the default (A/B of the side-stream share)
   static const int v = [] {
@@ -1349,7 +1369,9 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
   TNArgs a{G, ldg, X, ldx, P, M, N, K, S, rows_per_split, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (tn_big(dtype, gmode, N, K, tile)) {
     if (rows_per_split % 32) return XCP_EINVAL;
-    const dim3 grid(xcp_cdiv(N, 256) * xcp_cdiv(K, 256) * S);
+    const int tiles = xcp_cdiv(N, 256) * xcp_cdiv(K, 256);
+    a.xalign = tiles <= 32 && S >= 2 && tn_xcd_align();
+    const dim3 grid(a.xalign ? 8 * xcp_cdiv(S, 8) * tiles : tiles * S);
     const bool buf = ((long)(M - 1) * ldg + N) * 2 <= BUF_LIMIT && ((long)(M - 1) * ldx + K) * 2 <= BUF_LIMIT;
     if (buf)
       hipLaunchKernelGGL(gemm_tn256_kernel<true>, grid, dim3(512), 0, stream, a);

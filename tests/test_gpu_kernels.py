@@ -193,6 +193,28 @@ def test_gemm_tn(ops, gpu, dt, M, N, K, tile):
     assert rel_err(acc.view(N, K), ref + base.view(N, K)) < (1e-5 if dt == torch.float32 else 1e-3)
 
 
+@pytest.mark.parametrize("M,N,K", [(92416, 728, 728), (20000, 1024, 736), (9000, 256, 512)])
+def test_gemm_tn_xcd_align_bitwise(ops, gpu, monkeypatch, M, N, K):
+    """Whole weight-gradient splits per XCD (XCP_TN_XCD_ALIGN=1: padded grid, another workgroup ->
+    (split, tile) map) computes every split's slab in the same order: slabs bitwise equal."""
+    g = torch.Generator(device=gpu).manual_seed(M + N)
+    G = torch.randn(M, N, device=gpu, generator=g).bfloat16()
+    X = torch.randn(M, K, device=gpu, generator=g).bfloat16()
+    rps = ops._lib.call("xcp_gemm_tn_rows_per_split", 1, 0, M, N, K, 0)
+    S = (M + rps - 1) // rps
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("XCP_TN_XCD_ALIGN", v)
+        P = torch.full((S * N * K,), float("nan"), device=gpu)
+        ops.gemm_tn(G, X, P, M, N, K, S, rps)
+        torch.cuda.synchronize()
+        outs.append(P)
+    assert not torch.isnan(outs[1]).any()
+    assert torch.equal(outs[0], outs[1])
+    ref = G.float().t() @ X.float()
+    assert rel_err(outs[1].view(S, N, K).sum(0), ref) < 1e-3
+
+
 @pytest.mark.parametrize("S,L", [(1, 5), (3, 1001), (28, 728 * 728), (768, 728 * 9), (2560, 128 * 9), (40, 2304),
                                  (17, 6), (300, 7)])
 @pytest.mark.parametrize("accumulate", [False, True])
@@ -367,6 +389,36 @@ def test_dw_bwd_row_bands(ops, gpu, monkeypatch, bands, N, C, H, act, res, skip)
     assert torch.equal(outs[2][0], outs[1][0]) and torch.equal(outs[2][1], outs[1][1])
     if act == 2:
         assert torch.equal(outs[2][2], outs[1][2])
+
+
+@pytest.mark.parametrize("N,C,H,act,res", [(64, 736, 19, 2, False), (16, 256, 37, 2, False), (4, 128, 74, 1, False),
+                                           (32, 1536, 10, 0, False), (64, 736, 19, 1, True)])
+def test_dw_bwd_ring_read_forms(ops, gpu, monkeypatch, N, C, H, act, res):
+    """Ring reads by inline asm (XCP_DW_BWD_ASM=1) or plain C++ reads (=0), whichever the frame
+    height selects by default: the same arithmetic on the same values, every output bitwise equal."""
+    W = H
+    g = torch.Generator(device=gpu).manual_seed(3 * N + C + H)
+    dt = torch.bfloat16
+    x = torch.randn(N * H * W, C, device=gpu, generator=g).to(dt)
+    dy = torch.randn(N * H * W, C, device=gpu, generator=g).to(dt)
+    Wt = torch.randn(9, C, device=gpu, generator=g) / 3
+    sc = torch.rand(C, device=gpu, generator=g) + 0.5
+    sh = torch.randn(C, device=gpu, generator=g) * 0.2
+    dR = torch.randn(N * H * W, C, device=gpu, generator=g).to(dt) if res else None
+    st = {"mean": torch.randn(C, device=gpu, generator=g) * 0.1,
+          "invstd": torch.rand(C, device=gpu, generator=g) + 0.5} if act == 2 else None
+    outs = []
+    for form in ("0", "1"):
+        monkeypatch.setenv("XCP_DW_BWD_ASM", form)
+        dX = torch.full((N * H * W, C), float("nan"), device=gpu, dtype=dt)
+        dW = torch.empty(C * 9, device=gpu)
+        bnpart, P = ops.dw_bwd(act, dy, x, Wt, sc, sh, dX, dW, N, H, W, C, dRes=dR, bn_stats=st)
+        torch.cuda.synchronize()
+        outs.append((dX, dW, bnpart.clone() if bnpart is not None else None))
+    assert not torch.isnan(outs[1][0].float()).any()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    if act == 2:
+        assert torch.equal(outs[0][2], outs[1][2])
 
 
 @pytest.mark.parametrize("dt", DTYPES)
