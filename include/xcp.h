@@ -162,6 +162,15 @@ int xcp_avgpool_bwd(int dtype, const float* dF, const void* Y, const float* s, c
 int xcp_conv1_fwd(int dtype, const float* X, const float* W, void* Y, int N, int IH, int IW, xcp_stream_t stream);
 int xcp_conv1_wgrad_parts(int N, int IH, int IW);
 int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int N, int IH, int IW, xcp_stream_t stream);
+/* 1 when xcp_conv1_wgrad_bn takes the shape (bf16, frames <= 320 wide), else 0 */
+int xcp_conv1_wgrad_fused(int dtype, int IH, int IW);
+/* conv1 weight-gradient partials (as xcp_conv1_wgrad) of dC1 = alpha*g + bcoef*Y + delta, formed on load
+ * and rounded to the storage type: BN1's backward apply (Xception.py:119,:169; coefficients from
+ * xcp_bn_bwd_finalize*), g = dZ masked to 0 where Y*mscale + mshift <= 0 (the ReLU of Xception.py:170)
+ * when mscale / mshift are given.  Replaces xcp_bn_bwd_apply + xcp_conv1_wgrad on the stored dC1. */
+int xcp_conv1_wgrad_bn(int dtype, const float* X, const void* dZ, const void* Y, const float* alpha, const float* bcoef,
+                       const float* delta, const float* mscale, const float* mshift, float* part, int N, int IH, int IW,
+                       xcp_stream_t stream);
 int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int d2, int p0, int p1, int p2,
                  xcp_stream_t stream);
 

@@ -400,6 +400,140 @@ __global__ __launch_bounds__(256) void conv1_wgrad_tile_kernel(const float* __re
   }
 }
 
+// Weight gradient over one output row per tile (bf16 output gradients, frames up to W1R_IW wide), with
+// the next tile's operands prefetched into registers while the current tile is computed from LDS, and
+// (MODE 1 / 2) BN1's backward apply fused into the load of the output gradient:
+//   dC1[p][c] = bf16(alpha[c] * g + bcoef[c] * y + delta[c]),  g = dZ[p][c], masked to 0 where
+//   y * ms[c] + mt[c] <= 0 (MODE 2: dZ is the gradient of relu(bn1(y)), Xception.py:170)
+// -- the value bn_bwd_apply_kernel stores (same fma order, same bf16 rounding), so the fused path equals
+// xcp_bn_bwd_apply + xcp_conv1_wgrad on the stored tensor up to the fp32 summation order of the sums.
+// MODE 0: dZ is dC1 itself.  Per tile: the three stride-2 input rows of each input channel (fp32, 4-B
+// loads) and the output row of dZ (and y) (16-B loads), ~31 KB; a thread owns one output-channel pair
+// x 27 taps (27 packed accumulators) for every 16th pixel of the row.  No LDS-DMA (a plain LDS read
+// after one makes hipcc drain every outstanding load), so the prefetch stays in flight through the
+// compute.
+constexpr int W1R_IW = 320;                          // widest frame: 9 input rows of pitch 320 floats
+constexpr int W1R_OW = (W1R_IW - 3) / 2 + 1;         // 159 output pixels -> 636 16-B chunks per row
+constexpr int W1R_XL = 18;                           // input dwords per thread and tile: 9 rows x 2 columns
+constexpr int W1R_DL = (W1R_OW * 4 + 255) / 256;     // 16-B output-gradient chunks per thread and tile (3)
+
+template <int MODE>
+__global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __restrict__ X, const bf16* __restrict__ dZ,
+                                                              const bf16* __restrict__ Yv, const float* alpha,
+                                                              const float* bcoef, const float* delta, const float* ms,
+                                                              const float* mt, float* __restrict__ part, int N, int IH,
+                                                              int IW, int OH, int OW) {
+  constexpr bool BN = MODE != 0;
+  __shared__ __attribute__((aligned(16))) char smem[9 * W1R_IW * 4 + 2 * W1R_OW * 64];
+  float* sx = reinterpret_cast<float*>(smem);                                    // [9 rows][P]
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 struct arrays end up in scratch)
+  u32x4* sd = reinterpret_cast<u32x4*>(smem + 9 * W1R_IW * 4);                   // [OW * 4] chunks of dZ
+  u32x4* sy = sd + W1R_OW * 4;                                                   // [OW * 4] chunks of y
+  const int tid = threadIdx.x, cp = tid & 15, pg = tid >> 4;
+  const int P = pitch1(IW), nch = OW * 4, T = N * OH;
+  const long fsz = (long)IH * IW;
+  // input rows (ci, ky) of a tile: this thread loads columns tid and tid + 256 of each (clamped)
+  const int xc0 = min(tid, IW - 1), xc1 = min(tid + 256, IW - 1);
+  float2 al = make_float2(1.f, 1.f), bc = make_float2(0.f, 0.f), de = bc, sm = al, tm = bc;
+  if constexpr (BN) {
+    al = *reinterpret_cast<const float2*>(alpha + 2 * cp);
+    bc = *reinterpret_cast<const float2*>(bcoef + 2 * cp);
+    de = *reinterpret_cast<const float2*>(delta + 2 * cp);
+  }
+  if constexpr (MODE == 2) {
+    sm = *reinterpret_cast<const float2*>(ms + 2 * cp);
+    tm = *reinterpret_cast<const float2*>(mt + 2 * cp);
+  }
+  float rx[W1R_XL];
+  u32x4 rd[W1R_DL], ry[BN ? W1R_DL : 1];
+  // operands of tile t (always a valid tile: loads are unconditional, from clamped addresses)
+  auto fetch = [&](int t) {
+    const int n = t / OH, oh = t - n * OH;
+    const float* xb = X + (long)n * 3 * fsz + (long)(2 * oh) * IW;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      const float* xr = xb + (r / 3) * fsz + (r % 3) * IW;
+      rx[2 * r] = xr[xc0];
+      rx[2 * r + 1] = xr[xc1];
+    }
+    const long db = ((long)n * OH + oh) * OW * C1;
+#pragma unroll
+    for (int i = 0; i < W1R_DL; ++i) {
+      const int j = min(tid + 256 * i, nch - 1);
+      rd[i] = *reinterpret_cast<const u32x4*>(dZ + db + j * 8);
+      if constexpr (BN) ry[i] = *reinterpret_cast<const u32x4*>(Yv + db + j * 8);
+    }
+  };
+  f2v acc[K1];   // channels (2cp, 2cp+1) x taps
+#pragma unroll
+  for (int k = 0; k < K1; ++k) acc[k] = f2v(0.f);
+  const float2* sx2 = reinterpret_cast<const float2*>(sx);
+  const unsigned* sdu = reinterpret_cast<const unsigned*>(sd);
+  const unsigned* syu = reinterpret_cast<const unsigned*>(sy);
+  auto bf2 = [](unsigned u) { return f2v{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; };
+  fetch(blockIdx.x);   // (the grid never exceeds the tile count)
+  for (int t = blockIdx.x; t < T; t += gridDim.x) {
+    __syncthreads();   // the previous tile's LDS reads are done
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {   // (columns past IW are never read)
+      if (tid < P) sx[r * P + tid] = rx[2 * r];
+      if (tid + 256 < P) sx[r * P + tid + 256] = rx[2 * r + 1];
+    }
+    static_assert(W1R_DL == 3, "the chunk stores below are written out for three chunks per thread");
+    auto put = [&](int i, const u32x4& v, const u32x4& w) {
+      if (tid + 256 * i < nch) {
+        sd[tid + 256 * i] = v;
+        if constexpr (BN) sy[tid + 256 * i] = w;
+      }
+    };
+    put(0, rd[0], ry[BN ? 0 : 0]);
+    put(1, rd[1], ry[BN ? 1 : 0]);
+    put(2, rd[2], ry[BN ? 2 : 0]);
+    __syncthreads();
+    fetch(min(t + (int)gridDim.x, T - 1));   // next tile (the last tile once more past the end)
+    for (int p = pg; p < OW; p += 16) {
+      f2v d = bf2(sdu[p * 16 + cp]);
+      if constexpr (BN) {
+        const f2v y = bf2(syu[p * 16 + cp]);
+        if constexpr (MODE == 2) {
+          d[0] = fmaf(y[0], sm.x, tm.x) > 0.f ? d[0] : 0.f;
+          d[1] = fmaf(y[1], sm.y, tm.y) > 0.f ? d[1] : 0.f;
+        }
+        d[0] = rnd<bf16>(fmaf(al.x, d[0], fmaf(bc.x, y[0], de.x)));
+        d[1] = rnd<bf16>(fmaf(al.y, d[1], fmaf(bc.y, y[1], de.y)));
+      }
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        const float2 x01 = sx2[(r * P >> 1) + p];
+        const float x2 = sx[r * P + 2 * p + 2];
+        acc[r * 3 + 0] = __builtin_elementwise_fma(f2v(x01.x), d, acc[r * 3 + 0]);
+        acc[r * 3 + 1] = __builtin_elementwise_fma(f2v(x01.y), d, acc[r * 3 + 1]);
+        acc[r * 3 + 2] = __builtin_elementwise_fma(f2v(x2), d, acc[r * 3 + 2]);
+      }
+    }
+  }
+  // reduce the 16 pixel groups: lanes xor 16 / 32 within the wave, then the 4 waves in LDS
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);   // [4 waves][C1][K1] (13.8 KB)
+  const int w = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < K1; ++k)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float v = acc[k][e];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if ((tid & 63) < 16) red[(w * C1 + 2 * cp + e) * K1 + k] = v;
+    }
+  __syncthreads();
+  for (int i = tid; i < C1 * K1; i += 256) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v += red[q * C1 * K1 + i];
+    part[(long)blockIdx.x * (C1 * K1) + i] = v;
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -459,10 +593,21 @@ int xcp_conv1_wgrad_parts(int N, int IH, int IW) {
   return (int)blocks;
 }
 
+// 1 when the row kernel (and so xcp_conv1_wgrad_bn) takes this shape: bf16, frames <= 320 wide
+int xcp_conv1_wgrad_fused(int dtype, int IH, int IW) {
+  return dtype == XCP_BF16 && IW >= 3 && IH >= 3 && IW <= W1R_IW && 3L * IH * IW < (1L << 30);
+}
+
 int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int N, int IH, int IW, hipStream_t st) {
   const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
   const long P = (long)N * OH * OW;
   const int blocks = xcp_conv1_wgrad_parts(N, IH, IW);
+  if (P <= 0) return XCP_OK;
+  if (xcp_conv1_wgrad_fused(dtype, IH, IW)) {
+    hipLaunchKernelGGL(conv1_wgrad_row_kernel<0>, dim3(blocks), dim3(256), 0, st, X, (const bf16*)dY, nullptr, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, part, N, IH, IW, OH, OW);
+    return (int)hipGetLastError();
+  }
   if (conv1_wgrad_lds(XCP_F32, IW, OW) <= 64 * 1024) {
     const size_t lds = conv1_wgrad_lds(dtype, IW, OW);
     if (dtype == XCP_BF16)
@@ -514,6 +659,26 @@ int xcp_permute3_blocks(int d0, int d1, int d2, int p0, int p1, int p2, long s0,
 int xcp_permute3_batch(const long long* jobs, int njobs, int nblocks, hipStream_t st) {
   if (njobs <= 0 || nblocks <= 0) return XCP_OK;
   hipLaunchKernelGGL(permute3_batch_kernel, dim3(nblocks), dim3(256), 0, st, jobs, njobs);
+  return (int)hipGetLastError();
+}
+
+// conv1 weight gradient with BN1's backward apply fused into the load of its output gradient (see
+// conv1_wgrad_row_kernel): part[blocks][32*27] as xcp_conv1_wgrad on dC1 = alpha*mask(dZ) + bcoef*Y + delta;
+// mscale / mshift (BN1's forward scale / shift) null: no ReLU mask.  Shapes: xcp_conv1_wgrad_fused.
+int xcp_conv1_wgrad_bn(int dtype, const float* X, const void* dZ, const void* Y, const float* alpha, const float* bcoef,
+                       const float* delta, const float* mscale, const float* mshift, float* part, int N, int IH, int IW,
+                       hipStream_t st) {
+  if (!xcp_conv1_wgrad_fused(dtype, IH, IW)) return XCP_EUNSUPPORTED;
+  if ((mscale == nullptr) != (mshift == nullptr)) return XCP_EINVAL;
+  const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
+  if ((long)N * OH * OW <= 0) return XCP_OK;
+  const int blocks = xcp_conv1_wgrad_parts(N, IH, IW);
+  if (mscale)
+    hipLaunchKernelGGL(conv1_wgrad_row_kernel<2>, dim3(blocks), dim3(256), 0, st, X, (const bf16*)dZ, (const bf16*)Y,
+                       alpha, bcoef, delta, mscale, mshift, part, N, IH, IW, OH, OW);
+  else
+    hipLaunchKernelGGL(conv1_wgrad_row_kernel<1>, dim3(blocks), dim3(256), 0, st, X, (const bf16*)dZ, (const bf16*)Y,
+                       alpha, bcoef, delta, nullptr, nullptr, part, N, IH, IW, OH, OW);
   return (int)hipGetLastError();
 }
 

@@ -121,6 +121,9 @@ SIDE_PRIO_LOW = os.environ.get("XCP_SIDE_PRIO", "") == "low"
 # BN1's backward coefficients before the side-stream conv2 weight gradient is launched
 # (XCP_STEM_BN1_FIRST=0: after it, the round-2 order; A/B)
 STEM_BN1_FIRST = os.environ.get("XCP_STEM_BN1_FIRST", "1") != "0"
+# conv1's weight gradient forms BN1's backward apply (+ ReLU mask) on load instead of reading a stored
+# dC1 (xcp_conv1_wgrad_bn; XCP_CONV1_BN_FUSED=0: bn_bwd_apply + conv1_wgrad, A/B)
+CONV1_BN_FUSED = os.environ.get("XCP_CONV1_BN_FUSED", "1") != "0"
 # depthwise weight-gradient slab reductions on the weight-gradient stream (XCP_DW_REDUCE_SIDE=0:
 # on the main stream right after each depthwise backward)
 DW_REDUCE_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_DW_REDUCE_SIDE", "1") != "0"
@@ -600,10 +603,14 @@ class XceptionEngine:
             keep.append(dC2)
         if not STEM_BN1_FIRST:
             coef1 = bn_coef(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], None, True)
-        dC1 = self._empty(rows1 * pc(32))
-        ops.bn_apply_coef(dA1, S["c1"], dC1, coef1, S["s1"], rows1, pc(32), relu=True)
         c1g, acc = g("conv1.weight", (32, 3, 3, 3))
-        ops.conv1_wgrad(S["x"], dC1, c1g, N, S["IH"], S["IW"], accumulate=acc)
+        if CONV1_BN_FUSED and pc(32) == 32 and ops.conv1_wgrad_fused(self.dtype, S["IH"], S["IW"]):
+            ops.conv1_wgrad_bn(S["x"], dA1, S["c1"], coef1, S["s1"], c1g, N, S["IH"], S["IW"], 32, relu=True,
+                               accumulate=acc)
+        else:
+            dC1 = self._empty(rows1 * pc(32))
+            ops.bn_apply_coef(dA1, S["c1"], dC1, coef1, S["s1"], rows1, pc(32), relu=True)
+            ops.conv1_wgrad(S["x"], dC1, c1g, N, S["IH"], S["IW"], accumulate=acc)
         if side is not None:
             main.wait_stream(side)
         keep.clear()   # after the wait: reuse of these blocks is ordered behind the side stream

@@ -395,6 +395,23 @@ def conv1_wgrad(X, dY, out, N, IH, IW, accumulate=False):
     reduce_slabs(part, R, 32 * 27, out, accumulate)
 
 
+def conv1_wgrad_fused(dtype, IH, IW):
+    """True when conv1_wgrad_bn takes the shape"""
+    return _lib.call("xcp_conv1_wgrad_fused", DT[dtype], IH, IW) == 1
+
+
+def conv1_wgrad_bn(X, dZ, Y, coef, st, out, N, IH, IW, C, relu=True, accumulate=False):
+    """conv1's weight gradient with BN1's backward apply fused: as bn_apply_coef(dZ, Y, dC1, coef, st, ...,
+    relu) followed by conv1_wgrad(X, dC1, out, ...), without storing dC1 (C: the channel pitch of coef)."""
+    R = _lib.call("xcp_conv1_wgrad_parts", N, IH, IW)
+    part = torch.empty(R * 32 * 27, device=X.device, dtype=torch.float32)
+    ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
+    with _timed("conv1_wgrad_bn", {"N": N, "IH": IH, "IW": IW}):
+        _lib.call("xcp_conv1_wgrad_bn", DT[dZ.dtype], _p(X), _p(dZ), _p(Y), _p(coef), _p(coef[C:]), _p(coef[2 * C:]),
+                  ms, mt, _p(part), N, IH, IW, stream())
+    reduce_slabs(part, R, 32 * 27, out, accumulate)
+
+
 def frames_u8_to_f32(frames, lengths, out):
     """frames: uint8 [B, Tmax, H, W, 3] (device), lengths: int32 [B] (device) -> out fp32
     [B, Tmax, 3, H, W] = frames / 255, zero past each clip's length (video_dataloader.py:35, :59-64)."""

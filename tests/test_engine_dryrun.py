@@ -55,6 +55,8 @@ def install_fake_lib(monkeypatch):
             return 5
         if name == "xcp_conv1_wgrad_parts":
             return 3
+        if name == "xcp_conv1_wgrad_fused":   # (dtype, IH, IW): the row kernel takes bf16 frames <= 320 wide
+            return 1 if args[0] == 1 and args[2] <= 320 else 0
         if name in ("xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows"):
             return 256
         if name in ("xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts"):
@@ -129,7 +131,10 @@ def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn):
     names = set(fake_lib)
     assert {"xcp_gemm_nt", "xcp_dw_fwd", "xcp_tail_fwd", "xcp_avgpool_fwd", "xcp_lstm_fwd", "xcp_lstm_bwd"} <= names
     if unfrozen:
-        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd_bnred", "xcp_conv1_wgrad"} <= names
+        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd_bnred"} <= names
+        # conv1's weight gradient: BN1's backward apply fused into it in bf16, apply + plain form in fp32
+        assert ("xcp_conv1_wgrad_bn" in names) == (prec == "bf16")
+        assert ("xcp_conv1_wgrad" in names) == (prec == "fp32")
         # stem conv2: direct MFMA conv in bf16, im2col GEMM (gather modes 2 / 3) in fp32
         assert ({"xcp_conv3x3", "xcp_conv3x3_wgrad"} <= names) == (prec == "bf16")
         # block1's and block2's units (64/128 -> 128, 128/256 -> 256): fused BN-apply + pointwise

@@ -688,6 +688,37 @@ def test_conv1_fwd_wgrad(ops, gpu, dt, IH, IW):
     assert rel_err(dW.view(32, 3, 3, 3), w.grad) < (1e-5 if dt == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("N,IH,IW", [(3, 299, 299), (2, 65, 64), (5, 17, 23), (1, 31, 320)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_conv1_wgrad_bn_fused(ops, gpu, N, IH, IW, relu):
+    """conv1's weight gradient with BN1's backward apply formed on load (xcp_conv1_wgrad_bn) equals the
+    apply kernel's stored dC1 fed to xcp_conv1_wgrad bit for bit (same bf16 rounding, same summation
+    order), and the fp32 conv2d weight gradient of that dC1."""
+    assert ops.conv1_wgrad_fused(torch.bfloat16, IH, IW)
+    OH, OW = (IH - 3) // 2 + 1, (IW - 3) // 2 + 1
+    rows, C = N * OH * OW, 32
+    g = torch.Generator(device=gpu).manual_seed(N * IH + IW)
+    x = torch.rand(N, 3, IH, IW, device=gpu, generator=g)
+    dZ = torch.randn(rows, C, device=gpu, generator=g).bfloat16()
+    Y = torch.randn(rows, C, device=gpu, generator=g).bfloat16()
+    coef = torch.randn(3 * C, device=gpu, generator=g)
+    st = {"scale": torch.randn(C, device=gpu, generator=g), "shift": torch.randn(C, device=gpu, generator=g) * 0.3}
+    dC1 = torch.empty(rows, C, device=gpu, dtype=torch.bfloat16)
+    ops.bn_apply_coef(dZ, Y, dC1, coef, st, rows, C, relu=relu)
+    ref = torch.empty(32 * 27, device=gpu)
+    ops.conv1_wgrad(x, dC1, ref, N, IH, IW)
+    out = torch.full((32 * 27,), float("nan"), device=gpu)
+    ops.conv1_wgrad_bn(x, dZ, Y, coef, st, out, N, IH, IW, C, relu=relu)
+    acc = torch.ones(32 * 27, device=gpu)
+    ops.conv1_wgrad_bn(x, dZ, Y, coef, st, acc, N, IH, IW, C, relu=relu, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    torch.testing.assert_close(acc, ref + 1, rtol=1e-6, atol=1e-5)
+    w = torch.zeros(32, 3, 3, 3, device=gpu, requires_grad=True)
+    F.conv2d(x, w, None, 2, 0).backward(nchw(dC1.view(N, OH, OW, C)).float())
+    assert rel_err(out.view(32, 3, 3, 3), w.grad) < 1e-5
+
+
 def test_permute3(ops, gpu):
     x = torch.randn(5, 7, 9, device=gpu)
     for perm in [(0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1), (2, 1, 0)]:

@@ -353,7 +353,23 @@ def main():
         rep("conv1 fwd 299^2 -> 149^2 x 32", timeit(lambda: ops.conv1_fwd(Xc, Wc, Yc, N, 299, 299), iters=10), byts)
         dWc = torch.empty(32 * 27, device=dev)
         rep("conv1 wgrad", timeit(lambda: ops.conv1_wgrad(Xc, Yc, dWc, N, 299, 299), iters=10), byts)
-        del Xc, Yc
+        # BN1's backward apply + ReLU mask, then the weight gradient, vs the fused form (reads dZ and y)
+        Zc = torch.randn(N * 149 * 149, 32, device=dev, generator=g).to(dt)
+        coef = torch.randn(96, device=dev, generator=g)
+        stc = {"scale": torch.randn(32, device=dev, generator=g), "shift": torch.randn(32, device=dev, generator=g)}
+        Dc = torch.empty_like(Yc)
+        rows1 = N * 149 * 149
+        rep("bn1 apply (dZ, y -> dC1)", timeit(lambda: ops.bn_apply_coef(Zc, Yc, Dc, coef, stc, rows1, 32, relu=True),
+                                               iters=10), 3 * Yc.numel() * 2)
+
+        def unfused():
+            ops.bn_apply_coef(Zc, Yc, Dc, coef, stc, rows1, 32, relu=True)
+            ops.conv1_wgrad(Xc, Dc, dWc, N, 299, 299)
+        rep("bn1 apply + conv1 wgrad", timeit(unfused, iters=10), byts + 3 * Yc.numel() * 2)
+        rep("conv1 wgrad with bn1 apply fused", timeit(lambda: ops.conv1_wgrad_bn(Xc, Zc, Yc, coef, stc, dWc, N, 299, 299,
+                                                                                  32), iters=10),
+            byts + Yc.numel() * 2)
+        del Xc, Yc, Zc, Dc
     if "unitbwd" in sel:   # block1 / block2 unit backward (256 frames): fused vs three kernels
         for (Hu, CO, CI) in ((147, 128, 128), (147, 128, 64), (74, 256, 256), (74, 256, 128)):
             Mu = N * Hu * Hu
