@@ -160,6 +160,12 @@ int xcp_avgpool_bwd(int dtype, const float* dF, const void* Y, const float* s, c
 
 /* ---- stem conv1 (Xception.py:118,:168) and weight packing ---- */
 int xcp_conv1_fwd(int dtype, const float* X, const float* W, void* Y, int N, int IH, int IW, xcp_stream_t stream);
+/* conv1 forward + BN1's batch-statistics partials (sum y, sum y^2 of the stored outputs) in
+ * part[xcp_conv1_fwd_parts(N, IH, IW)][2][32], for the shapes of xcp_conv1_wgrad_fused (Xception.py:168-169:
+ * the partial rows replace a per-channel reduce over the output) */
+int xcp_conv1_fwd_parts(int N, int IH, int IW);
+int xcp_conv1_fwd_stats(int dtype, const float* X, const float* W, void* Y, float* part, int N, int IH, int IW,
+                        xcp_stream_t stream);
 int xcp_conv1_wgrad_parts(int N, int IH, int IW);
 int xcp_conv1_wgrad(int dtype, const float* X, const void* dY, float* part, int N, int IH, int IW, xcp_stream_t stream);
 /* 1 when xcp_conv1_wgrad_bn takes the shape (bf16, frames <= 320 wide), else 0 */

@@ -52,6 +52,8 @@ SIGNATURES = {
     "xcp_avgpool_fwd": [I, P, P, P, P, I, I, I, P],
     "xcp_avgpool_bwd": [I, P, P, P, P, P, I, I, I, P],
     "xcp_conv1_fwd": [I, P, P, P, I, I, I, P],
+    "xcp_conv1_fwd_parts": [I, I, I],
+    "xcp_conv1_fwd_stats": [I, P, P, P, P, I, I, I, P],
     "xcp_conv1_wgrad_parts": [I, I, I],
     "xcp_conv1_wgrad": [I, P, P, P, I, I, I, P],
     "xcp_conv1_wgrad_fused": [I, I, I],
@@ -81,7 +83,7 @@ SIGNATURES = {
 # entry points that return a size, not a status
 SIZE_QUERIES = {"xcp_permute3_blocks", "xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
                 "xcp_colreduce_groups", "xcp_unit_bwd_rows_per_split",
-                "xcp_conv1_wgrad_parts", "xcp_conv1_wgrad_fused", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
+                "xcp_conv1_wgrad_parts", "xcp_conv1_wgrad_fused", "xcp_conv1_fwd_parts", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
                 "xcp_maxpool_bwd_bnred_parts"}
 
 _lib = None

@@ -400,6 +400,92 @@ __global__ __launch_bounds__(256) void conv1_wgrad_tile_kernel(const float* __re
   }
 }
 
+// Forward over one output row per tile (bf16 output, frames up to W1R_IW wide; see the weight-gradient
+// row kernel below for the tile and the register prefetch), with BN1's batch statistics (STATS): each
+// workgroup sums y and y^2 of the stored (bf16-rounded) outputs of its tiles per channel and writes one
+// partial row part[blockIdx][2][32] -- the per-channel reduce pass over the 364 MB output is gone.
+// A thread owns an output-channel pair (its 27 weight pairs in registers) for every 16th pixel of the row.
+template <bool STATS>
+__global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __restrict__ X, const float* __restrict__ Wt,
+                                                            bf16* __restrict__ Y, float* __restrict__ part, int N,
+                                                            int IH, int IW, int OH, int OW) {
+  constexpr int IWM = 320;
+  __shared__ __attribute__((aligned(16))) float sx[9 * IWM];   // [9 rows][P]
+  __shared__ float red[2][4][C1];
+  const int tid = threadIdx.x, cp = tid & 15, pg = tid >> 4;
+  const int P = pitch1(IW), T = N * OH;
+  const long fsz = (long)IH * IW;
+  const int xc0 = min(tid, IW - 1), xc1 = min(tid + 256, IW - 1);
+  f2v wk[K1];
+#pragma unroll
+  for (int k = 0; k < K1; ++k) wk[k] = f2v{Wt[(2 * cp) * K1 + k], Wt[(2 * cp + 1) * K1 + k]};
+  float rx[18];
+  auto fetch = [&](int t) {
+    const int n = t / OH, oh = t - n * OH;
+    const float* xb = X + (long)n * 3 * fsz + (long)(2 * oh) * IW;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      const float* xr = xb + (r / 3) * fsz + (r % 3) * IW;
+      rx[2 * r] = xr[xc0];
+      rx[2 * r + 1] = xr[xc1];
+    }
+  };
+  f2v s1 = f2v(0.f), s2 = f2v(0.f);
+  const float2* sx2 = reinterpret_cast<const float2*>(sx);
+  fetch(blockIdx.x);   // (the grid never exceeds the tile count)
+  for (int t = blockIdx.x; t < T; t += gridDim.x) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      if (tid < P) sx[r * P + tid] = rx[2 * r];
+      if (tid + 256 < P) sx[r * P + tid + 256] = rx[2 * r + 1];
+    }
+    __syncthreads();
+    fetch(min(t + (int)gridDim.x, T - 1));
+    bf16* yrow = Y + (long)t * OW * C1 + 2 * cp;
+    for (int p = pg; p < OW; p += 16) {
+      f2v a0 = f2v(0.f), a1 = f2v(0.f), a2 = f2v(0.f);   // three chains (kx), added in a fixed order
+#pragma unroll
+      for (int r = 0; r < 9; ++r) {
+        const float2 x01 = sx2[(r * P >> 1) + p];
+        const float x2 = sx[r * P + 2 * p + 2];
+        a0 = __builtin_elementwise_fma(f2v(x01.x), wk[r * 3 + 0], a0);
+        a1 = __builtin_elementwise_fma(f2v(x01.y), wk[r * 3 + 1], a1);
+        a2 = __builtin_elementwise_fma(f2v(x2), wk[r * 3 + 2], a2);
+      }
+      const f2v o = (a0 + a1) + a2;
+      typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
+      const bf16x2 ob{(bf16)o[0], (bf16)o[1]};
+      *reinterpret_cast<bf16x2*>(yrow + (long)p * C1) = ob;
+      if constexpr (STATS) {
+        const f2v q{(float)ob[0], (float)ob[1]};
+        s1 += q;
+        s2 = __builtin_elementwise_fma(q, q, s2);
+      }
+    }
+  }
+  if constexpr (STATS) {
+    const int w = tid >> 6;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float a = s1[e], b = s2[e];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      if ((tid & 63) < 16) {
+        red[0][w][2 * cp + e] = a;
+        red[1][w][2 * cp + e] = b;
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * C1) {
+      const int st = tid >> 5, c = tid & 31;
+      part[((long)blockIdx.x * 2 + st) * C1 + c] = (red[st][0][c] + red[st][1][c]) + (red[st][2][c] + red[st][3][c]);
+    }
+  }
+}
+
 // Weight gradient over one output row per tile (bf16 output gradients, frames up to W1R_IW wide), with
 // the next tile's operands prefetched into registers while the current tile is computed from LDS, and
 // (MODE 1 / 2) BN1's backward apply fused into the load of the output gradient:
@@ -544,10 +630,24 @@ constexpr int F1_TH = 4;
 
 extern "C" {
 
+int xcp_conv1_wgrad_fused(int dtype, int IH, int IW);
+
+// partial rows of xcp_conv1_fwd_stats ([parts][2][32]): one per workgroup of the row kernel
+int xcp_conv1_fwd_parts(int N, int IH, int IW) {
+  const int OH = (IH - 3) / 2 + 1;
+  const long tiles = (long)N * OH;
+  return (int)(tiles < 1024 ? (tiles > 0 ? tiles : 0) : 1024);
+}
+
 int xcp_conv1_fwd(int dtype, const float* X, const float* W, void* Y, int N, int IH, int IW, hipStream_t st) {
   const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
   const long total = (long)N * OH * OW * (C1 / 8);
   if (total <= 0) return XCP_OK;
+  if (xcp_conv1_wgrad_fused(dtype, IH, IW)) {
+    hipLaunchKernelGGL(conv1_fwd_row_kernel<false>, dim3(xcp_conv1_fwd_parts(N, IH, IW)), dim3(256), 0, st, X, W,
+                       (bf16*)Y, nullptr, N, IH, IW, OH, OW);
+    return (int)hipGetLastError();
+  }
   const size_t lds = ((size_t)3 * (2 * F1_TH + 1) * ((IW + 63) & ~63) + C1 * K1) * sizeof(float);
   if (lds <= 64 * 1024) {
     const unsigned blocks = (unsigned)(N * ((OH + F1_TH - 1) / F1_TH));
@@ -679,6 +779,18 @@ int xcp_conv1_wgrad_bn(int dtype, const float* X, const void* dZ, const void* Y,
   else
     hipLaunchKernelGGL(conv1_wgrad_row_kernel<1>, dim3(blocks), dim3(256), 0, st, X, (const bf16*)dZ, (const bf16*)Y,
                        alpha, bcoef, delta, nullptr, nullptr, part, N, IH, IW, OH, OW);
+  return (int)hipGetLastError();
+}
+
+// conv1 forward (bf16 output) with BN1's batch-statistics partials part[xcp_conv1_fwd_parts][2][32]
+// (sum y, sum y^2 over the stored outputs), shapes as xcp_conv1_wgrad_fused
+int xcp_conv1_fwd_stats(int dtype, const float* X, const float* W, void* Y, float* part, int N, int IH, int IW,
+                        hipStream_t st) {
+  if (!xcp_conv1_wgrad_fused(dtype, IH, IW)) return XCP_EUNSUPPORTED;
+  const int OH = (IH - 3) / 2 + 1, OW = (IW - 3) / 2 + 1;
+  if ((long)N * OH * OW <= 0) return XCP_OK;
+  hipLaunchKernelGGL(conv1_fwd_row_kernel<true>, dim3(xcp_conv1_fwd_parts(N, IH, IW)), dim3(256), 0, st, X, W, (bf16*)Y,
+                     part, N, IH, IW, OH, OW);
   return (int)hipGetLastError();
 }
 

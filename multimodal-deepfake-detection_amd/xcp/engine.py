@@ -124,6 +124,9 @@ STEM_BN1_FIRST = os.environ.get("XCP_STEM_BN1_FIRST", "1") != "0"
 # conv1's weight gradient forms BN1's backward apply (+ ReLU mask) on load instead of reading a stored
 # dC1 (xcp_conv1_wgrad_bn; XCP_CONV1_BN_FUSED=0: bn_bwd_apply + conv1_wgrad, A/B)
 CONV1_BN_FUSED = os.environ.get("XCP_CONV1_BN_FUSED", "1") != "0"
+# BN1's batch statistics from conv1's forward (xcp_conv1_fwd_stats; XCP_CONV1_STATS_FUSED=0: a per-channel
+# reduce over the stored output, A/B)
+CONV1_STATS_FUSED = os.environ.get("XCP_CONV1_STATS_FUSED", "1") != "0"
 # depthwise weight-gradient slab reductions on the weight-gradient stream (XCP_DW_REDUCE_SIDE=0:
 # on the main stream right after each depthwise backward)
 DW_REDUCE_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_DW_REDUCE_SIDE", "1") != "0"
@@ -328,11 +331,15 @@ class XceptionEngine:
         OH1, OW1 = (IH - 3) // 2 + 1, (IW - 3) // 2 + 1
         rows1 = N * OH1 * OW1
         c1 = self._empty(rows1 * 32)
-        ops.conv1_fwd(x, m.conv1.weight.detach(), c1, N, IH, IW)
-        if train:
+        if train and CONV1_STATS_FUSED and ops.conv1_wgrad_fused(self.dtype, IH, IW):
+            part, R = ops.conv1_fwd_stats(x, m.conv1.weight.detach(), c1, N, IH, IW)
+            s1 = self._bn_stats(part, R, 32, rows1, m.bn1, True)
+        elif train:
+            ops.conv1_fwd(x, m.conv1.weight.detach(), c1, N, IH, IW)
             part, R = ops.row_stats(c1, rows1, 32)
             s1 = self._bn_stats(part, R, 32, rows1, m.bn1, True)
         else:
+            ops.conv1_fwd(x, m.conv1.weight.detach(), c1, N, IH, IW)
             s1 = self._bn_stats(None, 0, 32, rows1, m.bn1, False)
         a1 = self._empty(rows1 * 32)
         ops.bn_act(c1, a1, s1.scale, s1.shift, True, rows1, 32)

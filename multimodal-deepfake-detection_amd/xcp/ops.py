@@ -388,6 +388,14 @@ def conv1_fwd(X, W, Y, N, IH, IW):
     _lib.call("xcp_conv1_fwd", DT[Y.dtype], _p(X), _p(W), _p(Y), N, IH, IW, stream())
 
 
+def conv1_fwd_stats(X, W, Y, N, IH, IW):
+    """conv1 forward + BN1 partial sums of the stored output: returns (part [R][2][32], R)"""
+    R = _lib.call("xcp_conv1_fwd_parts", N, IH, IW)
+    part = torch.empty(R * 2 * 32, device=X.device, dtype=torch.float32)
+    _lib.call("xcp_conv1_fwd_stats", DT[Y.dtype], _p(X), _p(W), _p(Y), _p(part), N, IH, IW, stream())
+    return part, R
+
+
 def conv1_wgrad(X, dY, out, N, IH, IW, accumulate=False):
     R = _lib.call("xcp_conv1_wgrad_parts", N, IH, IW)
     part = torch.empty(R * 32 * 27, device=X.device, dtype=torch.float32)

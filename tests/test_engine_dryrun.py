@@ -55,6 +55,8 @@ def install_fake_lib(monkeypatch):
             return 5
         if name == "xcp_conv1_wgrad_parts":
             return 3
+        if name == "xcp_conv1_fwd_parts":
+            return 3
         if name == "xcp_conv1_wgrad_fused":   # (dtype, IH, IW): the row kernel takes bf16 frames <= 320 wide
             return 1 if args[0] == 1 and args[2] <= 320 else 0
         if name in ("xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows"):

@@ -668,10 +668,11 @@ def test_avgpool(ops, gpu, dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("IH,IW", [(75, 75), (299, 299), (7, 1501)], ids=["75", "299", "wide-perpixel"])
+@pytest.mark.parametrize("IH,IW", [(75, 75), (299, 299), (7, 1501), (33, 320), (9, 331)],
+                         ids=["75", "299", "wide-perpixel", "row-widest", "tile-331"])
 def test_conv1_fwd_wgrad(ops, gpu, dt, IH, IW):
-    """Stem conv1 3x3 s2: tiled kernels, and the per-pixel kernels frames wider than the tiles'
-    64 KB LDS budget fall back to."""
+    """Stem conv1 3x3 s2: the row kernels (bf16, frames <= 320 wide), the tiled kernels (fp32 / wider
+    frames) and the per-pixel kernels frames wider than the tiles' 64 KB LDS budget fall back to."""
     N = 2
     x = torch.rand(N, 3, IH, IW, device=gpu)
     w = (torch.randn(32, 3, 3, 3, device=gpu) / 5).requires_grad_(True)
@@ -686,6 +687,28 @@ def test_conv1_fwd_wgrad(ops, gpu, dt, IH, IW):
     ops.conv1_wgrad(x, nhwc(dy), dW, N, IH, IW)
     torch.cuda.synchronize()
     assert rel_err(dW.view(32, 3, 3, 3), w.grad) < (1e-5 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("N,IH,IW", [(3, 299, 299), (2, 65, 64), (5, 17, 23), (1, 31, 320)])
+def test_conv1_fwd_stats(ops, gpu, N, IH, IW):
+    """conv1 forward with BN1's partial sums: the output equals the plain forward's bit for bit, and
+    the partial rows sum to the per-channel sum / sum of squares of the stored output."""
+    OH, OW = (IH - 3) // 2 + 1, (IW - 3) // 2 + 1
+    g = torch.Generator(device=gpu).manual_seed(7 * N + IW)
+    x = torch.rand(N, 3, IH, IW, device=gpu, generator=g)
+    w = torch.randn(32, 3, 3, 3, device=gpu, generator=g) / 5
+    Y0 = torch.empty(N * OH * OW, 32, device=gpu, dtype=torch.bfloat16)
+    Y1 = torch.full_like(Y0, float("nan"))
+    ops.conv1_fwd(x, w, Y0, N, IH, IW)
+    part, R = ops.conv1_fwd_stats(x, w, Y1, N, IH, IW)
+    torch.cuda.synchronize()
+    assert torch.equal(Y0, Y1)
+    sums = part.view(R, 2, 32).double().sum(0)
+    yd = Y1.double()
+    torch.testing.assert_close(sums[0], yd.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(sums[1], (yd * yd).sum(0), rtol=1e-5, atol=1e-3)
+    ref = F.conv2d(x, w, None, 2, 0)
+    assert rel_err(nchw(Y1.view(N, OH, OW, 32)).float(), ref) < 1e-2
 
 
 @pytest.mark.parametrize("N,IH,IW", [(3, 299, 299), (2, 65, 64), (5, 17, 23), (1, 31, 320)])

@@ -351,6 +351,12 @@ def main():
         Yc = torch.empty(N * 149 * 149, 32, device=dev, dtype=dt)
         byts = Xc.numel() * 4 + Yc.numel() * 2
         rep("conv1 fwd 299^2 -> 149^2 x 32", timeit(lambda: ops.conv1_fwd(Xc, Wc, Yc, N, 299, 299), iters=10), byts)
+
+        def fwd_then_stats():
+            ops.conv1_fwd(Xc, Wc, Yc, N, 299, 299)
+            ops.row_stats(Yc, N * 149 * 149, 32)
+        rep("conv1 fwd + bn1 row_stats pass", timeit(fwd_then_stats, iters=10), byts + Yc.numel() * 2)
+        rep("conv1 fwd with bn1 stats fused", timeit(lambda: ops.conv1_fwd_stats(Xc, Wc, Yc, N, 299, 299), iters=10), byts)
         dWc = torch.empty(32 * 27, device=dev)
         rep("conv1 wgrad", timeit(lambda: ops.conv1_wgrad(Xc, Yc, dWc, N, 299, 299), iters=10), byts)
         # BN1's backward apply + ReLU mask, then the weight gradient, vs the fused form (reads dZ and y)
@@ -370,6 +376,23 @@ def main():
                                                                                   32), iters=10),
             byts + Yc.numel() * 2)
         del Xc, Yc, Zc, Dc
+    if "conv2" in sel:   # stem conv2 3x3 32->64 at 256 frames of 149^2 -> 147^2 (bf16 NHWC): fwd (+stats), dgrad, wgrad
+        a1 = torch.randn(N * 149 * 149, 32, device=dev, generator=g).to(dt)
+        w2 = (torch.randn(64, 9, 32, device=dev, generator=g) / 17).to(dt)
+        w2t = w2.permute(2, 1, 0).contiguous()   # [32][9][64]
+        c2 = torch.empty(N * 147 * 147, 64, device=dev, dtype=dt)
+        R2 = ops.conv3x3_parts(0, N, 149, 149)
+        st2 = torch.empty(R2 * 2 * 64, device=dev)
+        byts = a1.numel() * 2 + c2.numel() * 2
+        rep("conv2 fwd +stats 149^2 x 32 -> 147^2 x 64", timeit(lambda: ops.conv3x3(0, a1, w2, c2, st2, N, 149, 149),
+                                                             iters=10), byts, 2.0 * c2.numel() * 288)
+        dA = torch.empty_like(a1)
+        rep("conv2 dgrad", timeit(lambda: ops.conv3x3(1, c2, w2t, dA, None, N, 147, 147), iters=10), byts,
+            2.0 * c2.numel() * 288)
+        w2g = torch.empty(64 * 288, device=dev)
+        rep("conv2 wgrad (+ slab reduce)", timeit(lambda: ops.conv3x3_wgrad(c2, a1, w2g, N, 149, 149), iters=10), byts,
+            2.0 * c2.numel() * 288)
+        del a1, c2, dA
     if "unitbwd" in sel:   # block1 / block2 unit backward (256 frames): fused vs three kernels
         for (Hu, CO, CI) in ((147, 128, 128), (147, 128, 64), (74, 256, 256), (74, 256, 128)):
             Mu = N * Hu * Hu
