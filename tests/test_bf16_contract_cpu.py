@@ -4,8 +4,9 @@
   (bf16_contract.scaled_input) leaves the loss and every gradient of the reference graph
   unchanged -- fp64 to 1e-12, fp32 to its own rounding noise -- so the autocast realizations at different c are
   draws of bf16 noise around ONE answer.
-* The bound arithmetic: TOL where PyTorch's bf16 is closer than TOL / K_AUTO, K_AUTO x its worst
-  realization above that, and the assertion fires on an error beyond the bound.
+* The bound arithmetic: TOL where PyTorch's bf16 is closer than TOL / K_RMS, K_RMS x the RMS of its
+  realizations above that, the engine's median realization against it, the pooled noise-scale ratio
+  RHO, and the assertions fire on an error beyond the bound or RHO beyond RHO_MAX.
 """
 import pytest
 import torch
@@ -48,15 +49,23 @@ def test_scaled_input_leaves_gradients_unchanged(dt, lim):
 
 def test_bound_and_check():
     auto = {"a": [0.001, 0.01, 0.004], "b": [0.05, 0.2, 0.1]}
-    assert C.bound("a", auto) == C.TOL
-    assert C.bound("b", auto) == pytest.approx(C.K_AUTO * 0.2)
+    rb = (sum(v * v for v in auto["b"]) / 3) ** 0.5
+    assert C.bound("a", auto) == C.TOL                      # K_RMS x rms below TOL
+    assert C.bound("b", auto) == pytest.approx(C.K_RMS * rb)
     assert C.bound("c", auto) == C.TOL
     assert C.bound("a", None) == C.TOL
+    assert C.med([0.3, 0.01, 0.02]) == 0.02 and C.med(0.3) == 0.3
+    r, n = C.rho({"a": [0.002, 0.004, 0.006], "b": [0.1, 0.1, 0.1], "c": 0.5}, auto)
+    assert n == 2 and r == pytest.approx(((0.004 / C.rms(auto["a"])) ** 2 / 2 + (0.1 / rb) ** 2 / 2) ** 0.5
+                                         / C.MED3_M2 ** 0.5)
     if C.RECORD:
         pytest.skip("XCP_BF16_RECORD=1 does not assert")
-    C.check("t", {"a": 0.049, "b": 0.49, "c": 0.01}, auto)
+    C.check("t", {"a": 0.049, "b": 0.99 * C.K_RMS * rb, "c": 0.01}, auto)
+    C.check("t", {"b": [10.0, 0.1, 0.12]}, auto)            # one wild realization: the median decides
     with pytest.raises(AssertionError):
         C.check("t", {"a": 0.051}, auto)
     with pytest.raises(AssertionError):
-        C.check("t", {"b": 0.51}, auto)
+        C.check("t", {"b": [1.01 * C.K_RMS * rb] * 3}, auto)
+    with pytest.raises(AssertionError, match="noise"):      # within every bound, but RHO > RHO_MAX
+        C.check("t", {"a": [0.04, 0.045, 0.05], "b": [0.05, 0.2, 0.1]}, auto)
     C.check("t", {"h": 0.9}, auto, skip=["h"])
