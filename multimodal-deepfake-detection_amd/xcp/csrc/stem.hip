@@ -400,6 +400,48 @@ __global__ __launch_bounds__(256) void conv1_wgrad_tile_kernel(const float* __re
   }
 }
 
+constexpr int W1R_IW = 320;                          // widest frame: 9 input rows of pitch 320 floats
+constexpr int W1R_OW = (W1R_IW - 3) / 2 + 1;         // 159 output pixels -> 636 16-B chunks per row
+constexpr int W1R_OWM = W1R_OW;
+constexpr int W1R_DL = (W1R_OW * 4 + 255) / 256;     // 16-B output(-gradient) chunks per thread and tile (3)
+
+// The nine stride-2 input rows (3 channels x 3 kernel rows) of one output row, fetched as 16-B
+// chunks: chunk e = tid + 256 k (k < 3) of the tile is row e / C4, columns 4 (e % C4) .. +3, the last
+// chunk of a row clamped to end at column IW - 1 (it rewrites three columns of its neighbour with the
+// same values).  Frame rows are 299 floats (no 16-B alignment): 4-B aligned dwordx4 loads.  One
+// 16-B load per lane instead of four 4-B ones (load issue, not bytes, bounds a 4-B-lane stream:
+// MI355X_MICROARCH "store tail ... 8x dwordx4 halves it").
+typedef float f4a4 __attribute__((ext_vector_type(4), aligned(4)));
+struct XRowChunks {
+  int off[3];   // element offset inside the frame's [3][IH][IW] block, relative to input row 2 oh
+  int lds[3];   // LDS float index (< 0: no chunk)
+};
+XCP_DEV XRowChunks xrow_chunks(int tid, int IH, int IW, int P) {
+  const int C4 = (IW + 3) / 4;
+  XRowChunks m;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int e = tid + 256 * k, r = e / C4, j = e - r * C4;
+    const int col = min(4 * j, IW - 4);
+    const bool ok = r < 9;
+    m.off[k] = ok ? (r / 3) * IH * IW + (r % 3) * IW + col : 0;
+    m.lds[k] = ok ? r * P + col : -1;
+  }
+  return m;
+}
+XCP_DEV void xrow_fetch(const float* xb, const XRowChunks& m, f4a4 (&rx)[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) rx[k] = *reinterpret_cast<const f4a4*>(xb + m.off[k]);
+}
+XCP_DEV void xrow_store(float* sx, const XRowChunks& m, const f4a4 (&rx)[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    if (m.lds[k] >= 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sx[m.lds[k] + i] = rx[k][i];   // (clamped chunks: not 16-B aligned)
+    }
+}
+
 // Forward over one output row per tile (bf16 output, frames up to W1R_IW wide; see the weight-gradient
 // row kernel below for the tile and the register prefetch), with BN1's batch statistics (STATS): each
 // workgroup sums y and y^2 of the stored (bf16-rounded) outputs of its tiles per channel and writes one
@@ -411,38 +453,29 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
                                                             int IH, int IW, int OH, int OW) {
   constexpr int IWM = 320;
   __shared__ __attribute__((aligned(16))) float sx[9 * IWM];   // [9 rows][P]
+  __shared__ __attribute__((aligned(16))) unsigned so[W1R_OWM * 16];   // the output row [OW][32] bf16
   __shared__ float red[2][4][C1];
   const int tid = threadIdx.x, cp = tid & 15, pg = tid >> 4;
   const int P = pitch1(IW), T = N * OH;
   const long fsz = (long)IH * IW;
-  const int xc0 = min(tid, IW - 1), xc1 = min(tid + 256, IW - 1);
+  const XRowChunks xm = xrow_chunks(tid, IH, IW, P);
   f2v wk[K1];
 #pragma unroll
   for (int k = 0; k < K1; ++k) wk[k] = f2v{Wt[(2 * cp) * K1 + k], Wt[(2 * cp + 1) * K1 + k]};
-  float rx[18];
+  f4a4 rx[3];
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
-    const float* xb = X + (long)n * 3 * fsz + (long)(2 * oh) * IW;
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      const float* xr = xb + (r / 3) * fsz + (r % 3) * IW;
-      rx[2 * r] = xr[xc0];
-      rx[2 * r + 1] = xr[xc1];
-    }
+    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, xm, rx);
   };
   f2v s1 = f2v(0.f), s2 = f2v(0.f);
   const float2* sx2 = reinterpret_cast<const float2*>(sx);
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   fetch(blockIdx.x);   // (the grid never exceeds the tile count)
   for (int t = blockIdx.x; t < T; t += gridDim.x) {
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      if (tid < P) sx[r * P + tid] = rx[2 * r];
-      if (tid + 256 < P) sx[r * P + tid + 256] = rx[2 * r + 1];
-    }
+    __syncthreads();   // the previous tile's LDS reads (input rows, output row) are done
+    xrow_store(sx, xm, rx);
     __syncthreads();
     fetch(min(t + (int)gridDim.x, T - 1));
-    bf16* yrow = Y + (long)t * OW * C1 + 2 * cp;
     for (int p = pg; p < OW; p += 16) {
       f2v a0 = f2v(0.f), a1 = f2v(0.f), a2 = f2v(0.f);   // three chains (kx), added in a fixed order
 #pragma unroll
@@ -456,13 +489,19 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
       const f2v o = (a0 + a1) + a2;
       typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
       const bf16x2 ob{(bf16)o[0], (bf16)o[1]};
-      *reinterpret_cast<bf16x2*>(yrow + (long)p * C1) = ob;
+      so[p * 16 + cp] = __builtin_bit_cast(unsigned, ob);
       if constexpr (STATS) {
         const f2v q{(float)ob[0], (float)ob[1]};
         s1 += q;
         s2 = __builtin_elementwise_fma(q, q, s2);
       }
     }
+    __syncthreads();   // the output row is staged: 16-B stores, 4 lanes per pixel
+    u32x4* yrow = reinterpret_cast<u32x4*>(Y + (long)t * OW * C1);
+    const u32x4* so4 = reinterpret_cast<const u32x4*>(so);
+#pragma unroll
+    for (int k = 0; k < W1R_DL; ++k)
+      if (tid + 256 * k < OW * 4) yrow[tid + 256 * k] = so4[tid + 256 * k];
   }
   if constexpr (STATS) {
     const int w = tid >> 6;
@@ -498,10 +537,6 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
 // x 27 taps (27 packed accumulators) for every 16th pixel of the row.  No LDS-DMA (a plain LDS read
 // after one makes hipcc drain every outstanding load), so the prefetch stays in flight through the
 // compute.
-constexpr int W1R_IW = 320;                          // widest frame: 9 input rows of pitch 320 floats
-constexpr int W1R_OW = (W1R_IW - 3) / 2 + 1;         // 159 output pixels -> 636 16-B chunks per row
-constexpr int W1R_XL = 18;                           // input dwords per thread and tile: 9 rows x 2 columns
-constexpr int W1R_DL = (W1R_OW * 4 + 255) / 256;     // 16-B output-gradient chunks per thread and tile (3)
 
 template <int MODE>
 __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __restrict__ X, const bf16* __restrict__ dZ,
@@ -518,8 +553,7 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
   const int tid = threadIdx.x, cp = tid & 15, pg = tid >> 4;
   const int P = pitch1(IW), nch = OW * 4, T = N * OH;
   const long fsz = (long)IH * IW;
-  // input rows (ci, ky) of a tile: this thread loads columns tid and tid + 256 of each (clamped)
-  const int xc0 = min(tid, IW - 1), xc1 = min(tid + 256, IW - 1);
+  const XRowChunks xm = xrow_chunks(tid, IH, IW, P);
   float2 al = make_float2(1.f, 1.f), bc = make_float2(0.f, 0.f), de = bc, sm = al, tm = bc;
   if constexpr (BN) {
     al = *reinterpret_cast<const float2*>(alpha + 2 * cp);
@@ -530,18 +564,12 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     sm = *reinterpret_cast<const float2*>(ms + 2 * cp);
     tm = *reinterpret_cast<const float2*>(mt + 2 * cp);
   }
-  float rx[W1R_XL];
+  f4a4 rx[3];
   u32x4 rd[W1R_DL], ry[BN ? W1R_DL : 1];
   // operands of tile t (always a valid tile: loads are unconditional, from clamped addresses)
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
-    const float* xb = X + (long)n * 3 * fsz + (long)(2 * oh) * IW;
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      const float* xr = xb + (r / 3) * fsz + (r % 3) * IW;
-      rx[2 * r] = xr[xc0];
-      rx[2 * r + 1] = xr[xc1];
-    }
+    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, xm, rx);
     const long db = ((long)n * OH + oh) * OW * C1;
 #pragma unroll
     for (int i = 0; i < W1R_DL; ++i) {
@@ -560,11 +588,7 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
   fetch(blockIdx.x);   // (the grid never exceeds the tile count)
   for (int t = blockIdx.x; t < T; t += gridDim.x) {
     __syncthreads();   // the previous tile's LDS reads are done
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {   // (columns past IW are never read)
-      if (tid < P) sx[r * P + tid] = rx[2 * r];
-      if (tid + 256 < P) sx[r * P + tid + 256] = rx[2 * r + 1];
-    }
+    xrow_store(sx, xm, rx);
     static_assert(W1R_DL == 3, "the chunk stores below are written out for three chunks per thread");
     auto put = [&](int i, const u32x4& v, const u32x4& w) {
       if (tid + 256 * i < nch) {
@@ -588,13 +612,33 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
         d[0] = rnd<bf16>(fmaf(al.x, d[0], fmaf(bc.x, y[0], de.x)));
         d[1] = rnd<bf16>(fmaf(al.y, d[1], fmaf(bc.y, y[1], de.y)));
       }
+      // the pixel's 27 inputs in two batches of reads (rows 0-4, 5-8), each batch read before its
+      // FMAs: two LDS round trips per pixel (left alone, hipcc reused one register triple and waited
+      // after every read: nine; one batch of all 27 spills at three waves per SIMD)
 #pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        const float2 x01 = sx2[(r * P >> 1) + p];
-        const float x2 = sx[r * P + 2 * p + 2];
-        acc[r * 3 + 0] = __builtin_elementwise_fma(f2v(x01.x), d, acc[r * 3 + 0]);
-        acc[r * 3 + 1] = __builtin_elementwise_fma(f2v(x01.y), d, acc[r * 3 + 1]);
-        acc[r * 3 + 2] = __builtin_elementwise_fma(f2v(x2), d, acc[r * 3 + 2]);
+      for (int h = 0; h < 2; ++h) {
+        constexpr int RB = 5;
+        float2 x01[RB];
+        float x2[RB];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int r = h * RB + i;
+          if (r < 9) {
+            x01[i] = sx2[(r * P >> 1) + p];
+            x2[i] = sx[r * P + 2 * p + 2];
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int r = h * RB + i;
+          if (r < 9) {
+            acc[r * 3 + 0] = __builtin_elementwise_fma(f2v(x01[i].x), d, acc[r * 3 + 0]);
+            acc[r * 3 + 1] = __builtin_elementwise_fma(f2v(x01[i].y), d, acc[r * 3 + 1]);
+            acc[r * 3 + 2] = __builtin_elementwise_fma(f2v(x2[i]), d, acc[r * 3 + 2]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
