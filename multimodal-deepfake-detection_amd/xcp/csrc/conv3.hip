@@ -33,6 +33,19 @@ namespace {
 
 __device__ __attribute__((aligned(64))) uint4 g_czero[4];
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate is 6 bits; n >= 16 waits for 15,
+// which is stricter)
+XCP_DEV void wait_vmcnt_dyn(int n) {
+  switch (n) {
+#define XCP_VMW(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    XCP_VMW(0) XCP_VMW(1) XCP_VMW(2) XCP_VMW(3) XCP_VMW(4) XCP_VMW(5) XCP_VMW(6) XCP_VMW(7)
+    XCP_VMW(8) XCP_VMW(9) XCP_VMW(10) XCP_VMW(11) XCP_VMW(12) XCP_VMW(13) XCP_VMW(14)
+#undef XCP_VMW
+    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+  }
+}
+
 // 16-B chunk swizzle of LDS column x (brute-force checked: conflict-free ds_read_b128 for
 // 16 consecutive columns at any row offset); depends on x mod 8 only
 template <int CIN>
@@ -114,10 +127,12 @@ __global__ __launch_bounds__(NW * 64, 1) void conv3x3_kernel(const bf16* __restr
   for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) loff[kx][ks] = PIPE ? ((ks * 4 + fg) ^ cswz<CIN>(fr + kx)) << 4 : 0;
+  int prev_st = 0;   // global stores this wave issued after the DMA of tile t (one per item)
   for (int k = 0; t < ntiles; ++k, t += G) {
-    // tile t landed (this wave's DMA and its previous stores) -> for every wave
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // tile t landed (this wave's DMA; the previous tile's stores, issued after it, may stay in
+    // flight) -> for every wave.  (__syncthreads would wait for those stores too: vmcnt(0).)
+    wait_vmcnt_dyn(prev_st);
+    lds_barrier();
     if (t + G < ntiles) stage(t + G, (k + 1) & 1);   // streams in under this tile's MFMAs
     const char* sb = smem + (k & 1) * BUF;
     const int n = t / tiles_h, oh0 = (t - n * tiles_h) * TH;
@@ -212,8 +227,10 @@ __global__ __launch_bounds__(NW * 64, 1) void conv3x3_kernel(const bf16* __restr
       bf16* ypix = Y + (((long)n * OH + oh) * OW + ow) * COUT + co0 + (odd ? 16 + 4 * (fg - 1) : 4 * fg);
       if (ok) *reinterpret_cast<uint4*>(ypix) = d;
     }
-    __syncthreads();   // every wave is done reading buffer k&1 before it is restaged
+    prev_st = nit;
+    lds_barrier();   // every wave is done reading buffer k&1 before it is restaged (LDS only)
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   if constexpr (STATS) {
     // reduce over the 16 pixel lanes (xor 1..8), then over the waves in LDS
