@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libxcp.so")
+LIB_PATH = DEFAULT_LIB_PATH = os.path.join(_HERE, "libxcp.so")
 # XCP_LIB_PATH: load another build of the same ABI instead (A/B of a kernel change in the step;
 # tools/build_variant.py links one)
 LIB_PATH = os.environ.get("XCP_LIB_PATH") or LIB_PATH
@@ -104,6 +104,8 @@ def load():
                        "There is no CPU fallback for the product path.")
     lib = ctypes.CDLL(LIB_PATH)
     for name, argtypes in SIGNATURES.items():
+        if LIB_PATH != DEFAULT_LIB_PATH and not hasattr(lib, name):
+            continue   # an A/B build of an older tree (XCP_LIB_PATH) may predate an entry point
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
