@@ -331,8 +331,9 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, in
   const int c = c0 + (lane & 31), stat = lane >> 5;
   // rows w, w + 16, ... in chunks of FIN_U: every load of a chunk is issued before the first is
   // added (clamped row, zero-selected past R), so a lane waits ceil(R / (16 FIN_U)) memory round
-  // trips, not one per 4 rows (722 partial rows of the middle flow: 3 instead of 12)
-  constexpr int FIN_U = 16;
+  // trips, not one per 4 rows (723 partial rows of the middle flow: one; the same summation order
+  // as smaller chunks, so the same bits)
+  constexpr int FIN_U = 48;
   double a = 0.0;
   if (c < C) {
     const float* col = part + (long)stat * CP + c;
