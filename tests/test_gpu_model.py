@@ -86,11 +86,14 @@ def engine_realizations(m, sd0, run, norm_ref, elem_ref=None, prefix=""):
         run(c)
         torch.cuda.synchronize()
         params = dict(m.named_parameters())
+        # the leaf is conv1.weight / c here (autocast_errors differentiates through the / c): its
+        # gradient is c x the reference's, so it is divided by c
+        grad = {n: (params[n].grad / c if n == key else params[n].grad) for n in set(out) | set(eout)}
         for n in out:
-            gn = params[n].grad.double().norm().item()
+            gn = grad[n].double().norm().item()
             out[n].append(abs(gn - float(norm_ref[n])) / max(float(norm_ref[n]), 1e-30))
         for n in eout:
-            eout[n].append(relerr(params[n].grad.cpu(), elem_ref[n]))
+            eout[n].append(relerr(grad[n].cpu(), elem_ref[n]))
     m.load_state_dict(sd0)
     return out, eout
 

@@ -43,7 +43,8 @@ def main():
         p = dict(m.named_parameters())
         for n in names:
             ref = float(g[f"gradnorm/{n}"])
-            out[n].append(abs(p[n].grad.double().norm().item() - ref) / ref)
+            gr = p[n].grad / c if n == "conv1.weight" else p[n].grad   # (the leaf is conv1.weight / c)
+            out[n].append(abs(gr.double().norm().item() - ref) / ref)
     tag = " ".join(f"{k}={os.environ[k]}" for k in sorted(os.environ) if k.startswith("XCP_"))
     print(f"[{tag or 'default'}] " + "  ".join(f"{n}: " + " ".join(f"{e:.4f}" for e in v) for n, v in out.items()),
           flush=True)
