@@ -56,7 +56,7 @@ XCP_DEV int cswz(int x) {
 
 
 template <int CIN, int COUT, int PAD, int TH, int MAXIW, bool STATS, int NW, bool PIPE>
-__global__ __launch_bounds__(NW * 64, 1) void conv3x3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wp,
+__global__ __launch_bounds__(NW * 64, 8 / NW) void conv3x3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wp,
                                                          bf16* __restrict__ Y, float* __restrict__ stats, int N,
                                                          int IH, int IW) {
   constexpr int CPP = CIN / 8;                // 16-B chunks per pixel
@@ -393,6 +393,13 @@ constexpr int TH_FWD = 4, TH_DGRAD = 2, MAXIW_FWD = 149, MAXIW_DGRAD = 147;
 // waves per workgroup (two per SIMD); the 64-deep dgrad keeps 144 VGPRs of kernel fragments
 // and has no room for the rotating read pipeline
 constexpr int NW_FWD = 8, NW_DGRAD = 8;
+// XCP_CONV3_FWD_2WG=1: the forward as two workgroups of 4 waves per CU on 2-row tiles (2 x 78 KB of LDS):
+// twice the tiles in flight per CU (A/B)
+constexpr int TH_FWD2 = 2, NW_FWD2 = 4;
+bool conv3_fwd_2wg() {   // (read per call: a test compares both forms in one process)
+  const char* e = getenv("XCP_CONV3_FWD_2WG");
+  return e && e[0] == '1';
+}
 
 
 int conv3_cus() {
@@ -425,9 +432,10 @@ extern "C" {
 int xcp_conv3x3_parts(int mode, int N, int IH, int IW) {
   if (IW > (mode == 0 ? MAXIW_FWD : MAXIW_DGRAD)) return 0;
   const int OH = mode == 0 ? IH - 2 : IH + 2;
-  const int th = mode == 0 ? TH_FWD : TH_DGRAD;
-  const int tiles = N * ((OH + th - 1) / th);
-  return tiles < conv3_cus() ? tiles : conv3_cus();
+  const bool two = mode == 0 && conv3_fwd_2wg();
+  const int th = mode == 0 ? (two ? TH_FWD2 : TH_FWD) : TH_DGRAD;
+  const int tiles = N * ((OH + th - 1) / th), cap = (two ? 2 : 1) * conv3_cus();
+  return tiles < cap ? tiles : cap;
 }
 
 // mode 0: Y[N][IH-2][IW-2][64] = conv3x3(X[N][IH][IW][32], W[64][9][32]) (+ BN partial sums)
@@ -439,7 +447,14 @@ int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, i
   if (IH < 3 || IW < 3 || (mode != 0 && mode != 1) || (mode == 1 && stats)) return XCP_EINVAL;
   if (IW > (mode == 0 ? MAXIW_FWD : MAXIW_DGRAD)) return XCP_EUNSUPPORTED;
   const dim3 grid((unsigned)xcp_conv3x3_parts(mode, N, IH, IW));
-  if (mode == 0) {
+  if (mode == 0 && conv3_fwd_2wg()) {
+    if (stats)
+      hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD2, MAXIW_FWD, true, NW_FWD2, true>), grid, dim3(64 * NW_FWD2), 0,
+                         st, (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+    else
+      hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD2, MAXIW_FWD, false, NW_FWD2, true>), grid, dim3(64 * NW_FWD2), 0,
+                         st, (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+  } else if (mode == 0) {
     if (stats)
       hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD, MAXIW_FWD, true, NW_FWD, true>), grid, dim3(64 * NW_FWD), 0, st, (const bf16*)X,
                          (const bf16*)W, (bf16*)Y, stats, N, IH, IW);

@@ -869,6 +869,28 @@ def test_conv3x3_stem_fwd_dgrad(ops, gpu, N, IH, IW):
     assert rel_err(got, ref_dw) < 1e-4
 
 
+@pytest.mark.parametrize("N,IH,IW", [(3, 149, 149), (2, 9, 40)])
+def test_conv3x3_fwd_two_workgroup_form(ops, gpu, monkeypatch, N, IH, IW):
+    """XCP_CONV3_FWD_2WG=1 (two 4-wave workgroups per CU on 2-row tiles): the same MFMAs per output
+    item, so the output is bitwise the one-workgroup form's; the BN partial rows (one per workgroup)
+    sum to the same statistics."""
+    g = torch.Generator(device=gpu).manual_seed(IH + N)
+    x = torch.randn(N * IH * IW, 32, device=gpu, generator=g).bfloat16()
+    Wp = (torch.randn(64, 288, device=gpu, generator=g) / 17).bfloat16()
+    OH, OW = IH - 2, IW - 2
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("XCP_CONV3_FWD_2WG", v)
+        R = ops.conv3x3_parts(0, N, IH, IW)
+        stats = torch.full((R, 2, 64), float("nan"), device=gpu)
+        Y = torch.full((N * OH * OW, 64), float("nan"), device=gpu, dtype=torch.bfloat16)
+        ops.conv3x3(0, x, Wp, Y, stats, N, IH, IW)
+        torch.cuda.synchronize()
+        outs.append((Y, stats.double().sum(0)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-6, atol=1e-3)
+
+
 @pytest.mark.parametrize("max_norm", [None, 1.0, 1e-3])
 def test_fused_adam_clip_vs_torch(ops, gpu, max_norm):
     """xcp.optim.FusedAdamClip (csrc/optim.hip) against clip_grad_norm_ + torch.optim.Adam (L2
