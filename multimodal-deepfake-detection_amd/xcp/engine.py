@@ -124,6 +124,9 @@ STEM_BN1_FIRST = os.environ.get("XCP_STEM_BN1_FIRST", "1") != "0"
 # conv1's weight gradient forms BN1's backward apply (+ ReLU mask) on load instead of reading a stored
 # dC1 (xcp_conv1_wgrad_bn; XCP_CONV1_BN_FUSED=0: bn_bwd_apply + conv1_wgrad, A/B)
 CONV1_BN_FUSED = os.environ.get("XCP_CONV1_BN_FUSED", "1") != "0"
+# conv2's weight gradient launched on the weight-gradient stream before conv2's input gradient instead of
+# after BN1's backward coefficients (XCP_STEM_WGRAD_EARLY=1, A/B)
+STEM_WGRAD_EARLY = os.environ.get("XCP_STEM_WGRAD_EARLY", "0") == "1"
 # BN1's batch statistics from conv1's forward (xcp_conv1_fwd_stats; XCP_CONV1_STATS_FUSED=0: a per-channel
 # reduce over the stored output, A/B)
 CONV1_STATS_FUSED = os.environ.get("XCP_CONV1_STATS_FUSED", "1") != "0"
@@ -578,6 +581,29 @@ class XceptionEngine:
             dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"], part=pre_part)
         else:
             dC2 = bn_bwd(m.bn2, "bn2", dX, S["c2"], rows2, 64, S["s2"], relu=True)   # relu (Xception.py:174) fused
+        def conv2_wgrad(st2):
+            """conv2's weight gradient (from dC2 and a1) on stream st2 (None: the current one)"""
+            if st2 is not None:
+                st2.wait_stream(main)
+            c2g, acc = g("conv2.weight", (64, 32, 3, 3))   # (allocated on the main stream)
+            with torch.cuda.stream(st2) if st2 is not None else contextlib.nullcontext():
+                w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
+                if self.dtype == torch.bfloat16 and ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0:
+                    ops.conv3x3_wgrad(dC2, S["a1"], w2g, N, OH1, OW1)
+                else:
+                    ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
+                if acc:
+                    tmp = torch.empty_like(c2g)
+                    ops.permute3(w2g, tmp, 64, 9, 32, (0, 2, 1))
+                    c2g.add_(tmp)
+                else:
+                    ops.permute3(w2g, c2g, 64, 9, 32, (0, 2, 1))
+            if st2 is not None:
+                keep.append(dC2)
+
+        st2 = side if STEM_WGRAD_SIDE else None
+        if STEM_WGRAD_EARLY and st2 is not None:   # beside conv2's input gradient (A/B)
+            conv2_wgrad(st2)
         dA1 = self._empty(rows1 * 32)
         if self.dtype == torch.bfloat16 and ops.conv3x3_parts(1, N, OH2, OW2) > 0:
             ops.conv3x3(1, dC2, pk["conv2T"], dA1, None, N, OH2, OW2)
@@ -590,24 +616,8 @@ class XceptionEngine:
         # 356 us per step on the main stream (profiles/r03_v3_kernels.txt)
         if STEM_BN1_FIRST:
             coef1 = bn_coef(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], None, True)   # relu (Xception.py:170)
-        st2 = side if STEM_WGRAD_SIDE else None
-        if st2 is not None:
-            st2.wait_stream(main)
-        c2g, acc = g("conv2.weight", (64, 32, 3, 3))   # (allocated on the main stream)
-        with torch.cuda.stream(st2) if st2 is not None else contextlib.nullcontext():
-            w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
-            if self.dtype == torch.bfloat16 and ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0:
-                ops.conv3x3_wgrad(dC2, S["a1"], w2g, N, OH1, OW1)
-            else:
-                ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)
-            if acc:
-                tmp = torch.empty_like(c2g)
-                ops.permute3(w2g, tmp, 64, 9, 32, (0, 2, 1))
-                c2g.add_(tmp)
-            else:
-                ops.permute3(w2g, c2g, 64, 9, 32, (0, 2, 1))
-        if st2 is not None:
-            keep.append(dC2)
+        if not (STEM_WGRAD_EARLY and st2 is not None):
+            conv2_wgrad(st2)
         if not STEM_BN1_FIRST:
             coef1 = bn_coef(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], None, True)
         c1g, acc = g("conv1.weight", (32, 3, 3, 3))
