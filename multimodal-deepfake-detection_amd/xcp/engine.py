@@ -124,9 +124,11 @@ STEM_BN1_FIRST = os.environ.get("XCP_STEM_BN1_FIRST", "1") != "0"
 # conv1's weight gradient forms BN1's backward apply (+ ReLU mask) on load instead of reading a stored
 # dC1 (xcp_conv1_wgrad_bn; XCP_CONV1_BN_FUSED=0: bn_bwd_apply + conv1_wgrad, A/B)
 CONV1_BN_FUSED = os.environ.get("XCP_CONV1_BN_FUSED", "1") != "0"
-# conv2's weight gradient launched on the weight-gradient stream before conv2's input gradient instead of
-# after BN1's backward coefficients (XCP_STEM_WGRAD_EARLY=1, A/B)
-STEM_WGRAD_EARLY = os.environ.get("XCP_STEM_WGRAD_EARLY", "0") == "1"
+# conv2's weight gradient launched on the weight-gradient stream before conv2's input gradient, so it runs
+# beside the dgrad, BN1's coefficients and conv1's weight gradient instead of after them and the backward
+# no longer ends waiting for it (+0.2-0.5 % in two interleaved rounds, profiles/r04_stem_order_ab.txt;
+# XCP_STEM_WGRAD_EARLY=0: after BN1's coefficients)
+STEM_WGRAD_EARLY = os.environ.get("XCP_STEM_WGRAD_EARLY", "1") != "0"
 # BN1's batch statistics from conv1's forward (xcp_conv1_fwd_stats; XCP_CONV1_STATS_FUSED=0: a per-channel
 # reduce over the stored output, A/B)
 CONV1_STATS_FUSED = os.environ.get("XCP_CONV1_STATS_FUSED", "1") != "0"

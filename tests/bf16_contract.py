@@ -84,10 +84,15 @@ def autocast_errors(sd, loss_fn, ref_norms, ref_elem=None, trainable=None, R=R_A
     trainable = set(ref_norms if trainable is None else trainable)
     norms = {n: [] for n in ref_norms}
     elem = {n: [] for n in (ref_elem or {})}
-    for c in SCALES[:R]:
+    import time
+    for i, c in enumerate(SCALES[:R]):
+        t0 = time.time()
         params = {k: (v.detach().clone().requires_grad_(True) if k in trainable else v.detach().clone())
                   for k, v in sd.items()}
         loss_fn(params, c).backward()
+        if i < 2 or i == R - 1:
+            torch.cuda.synchronize()
+            print(f"autocast realization {i}: {time.time() - t0:.2f} s", flush=True)
         for n in norms:
             gn = params[n].grad.double().norm().item()
             norms[n].append(abs(gn - float(ref_norms[n])) / max(float(ref_norms[n]), 1e-30))

@@ -13,6 +13,12 @@ for p in (PKG, REPO):
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# The autocast reference of the bf16 contract (tests/bf16_contract.py) runs the oracle graph through
+# MIOpen; its default find mode compiles and times every applicable solver for every new convolution
+# shape on a fresh box (most of the bench-size bf16 test's ~3 minutes).  FAST: immediate mode, one
+# kernel per shape.  (Test infrastructure only: the xcp path under test makes no MIOpen call.)
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP) device")
