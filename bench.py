@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="replay the whole train step as one HIP graph (auto: on at world size 1, off across ranks)")
     ap.add_argument("--small-batch", type=int, default=4,
                     help="lstmv: also time the unfrozen step at this many clips/GPU (train_visual.py:545 uses 4; "
                          "0: off)")
@@ -100,6 +102,14 @@ def launch_ranks(args):
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.call(cmd, env=env)
+
+
+def graph_mode(args, world):
+    """Replay the train step as one HIP graph: --graph on / off, auto = on at world size 1 (the
+    multi-rank step launches RCCL collectives from inside the backward; they stay eager)."""
+    if args.graph == "on":
+        return True
+    return args.graph == "auto" and world == 1 and args.model != "auface"
 
 
 def middle_hw(size):
@@ -334,11 +344,14 @@ class Run:
         self.params = list(self.model.parameters())
         self.buckets = ddp.GradBuckets(self.params, world=world, module=self.model)
         lr, wd = (1e-4, 0.0) if args.model == "lstma" else (1e-5, 1e-4)
+        self.use_graph = graph_mode(args, world)
+        self.graph = None
         if args.optim == "fused":
             from xcp.optim import FusedAdamClip
-            self.opt = FusedAdamClip(self.params, lr=lr, weight_decay=wd, max_norm=1.0)
+            self.opt = FusedAdamClip(self.params, lr=lr, weight_decay=wd, max_norm=1.0, capturable=self.use_graph)
         else:
-            self.opt = torch.optim.Adam([p for p in self.params if p.requires_grad], lr=lr, weight_decay=wd, fused=True)
+            self.opt = torch.optim.Adam([p for p in self.params if p.requires_grad], lr=lr, weight_decay=wd, fused=True,
+                                        capturable=self.use_graph)
         g = torch.Generator(device=dev).manual_seed(1234 + rank)
         if args.model == "lstma":
             self.x = torch.randn((B, T, 3, 13), generator=g, device=dev)
@@ -348,6 +361,32 @@ class Run:
             self.x = torch.rand((B, T, 3, S, S), generator=g, device=dev)
         gl = torch.Generator(device=dev).manual_seed(4321 + rank)
         self.y = torch.randint(0, 2, (B, 1), generator=gl, device=dev).float()
+
+    def capture(self):
+        """Record one train step (forward, backward with the side-stream weight gradients, clip + Adam
+        with device-side step counts) as a HIP graph.  Runs after the eager warm-up, which leaves every
+        persistent buffer, packed-weight table and optimiser table in place; one more eager step on a
+        side stream first, as torch.cuda.graph requires."""
+        import torch
+        cs = torch.cuda.Stream(self.dev)
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            self.step()
+        torch.cuda.current_stream().wait_stream(cs)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.gloss = self.step()
+        torch.cuda.synchronize()
+
+    def replay(self):
+        """One graph-replayed train step.  The replay updates the parameters without the Python that
+        bumps their autograd versions, so they are bumped here: an eager step after replays then repacks
+        its weights (engine.pack's cache is keyed on the versions)."""
+        from torch.autograd.graph import increment_version
+        self.graph.replay()
+        increment_version(self.params)
+        return self.gloss
 
     def step(self, ev=None):
         """One training step.  ev: 4 timing events recorded on the current stream at the step's
@@ -438,12 +477,18 @@ def timed(run, steps, warmup, world, timer=None, diag=None):
     import torch
     import torch.distributed as dist
     from xcp import ops
+    graph = getattr(run, "use_graph", False)
     for _ in range(warmup):
         run.step()
+    if graph and run.graph is None:
+        run.capture()
+        run.replay()   # (the first replay uploads the graph)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     if timer is not None:
+        if graph:
+            raise ValueError("per-kernel timing needs eager steps (timed(..., graph off))")
         ops.set_kernel_timer(timer)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)] if diag is not None else None
     m0 = mem_counters(run.dev)
@@ -452,7 +497,14 @@ def timed(run, steps, warmup, world, timer=None, diag=None):
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(steps):
-        loss = run.step(evs[i] if evs is not None else None)
+        if graph:
+            if evs is not None:
+                evs[i][0].record()
+            loss = run.replay()
+            if evs is not None:
+                evs[i][3].record()
+        else:
+            loss = run.step(evs[i] if evs is not None else None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -467,10 +519,14 @@ def timed(run, steps, warmup, world, timer=None, diag=None):
         st = torch.cuda.memory_stats(run.dev)
         step_ms = [evs[i][0].elapsed_time(evs[i + 1][0]) for i in range(steps - 1)] + \
                   [evs[-1][0].elapsed_time(evs[-1][3])]
-        ph = [[ev[k].elapsed_time(ev[k + 1]) for ev in evs] for k in range(3)]
         mean = lambda v: round(sum(v) / len(v), 3)   # noqa: E731
-        diag.update({"step_ms": [round(v, 2) for v in step_ms],
-                     "fwd_ms": mean(ph[0]), "bwd_ms": mean(ph[1]), "opt_ms": mean(ph[2]),
+        if graph:   # (one graph launch per step: no phase boundaries inside it)
+            ph = None
+        else:
+            ph = [[ev[k].elapsed_time(ev[k + 1]) for ev in evs] for k in range(3)]
+        diag.update({"step_ms": [round(v, 2) for v in step_ms], "graph": graph,
+                     "fwd_ms": mean(ph[0]) if ph else None, "bwd_ms": mean(ph[1]) if ph else None,
+                     "opt_ms": mean(ph[2]) if ph else None,
                      "alloc_in_timed_region": {k: m1[k] - m0[k] for k in MEM_KEYS},
                      "reserved_peak_gb": round(st.get("reserved_bytes.all.peak", 0) / 2 ** 30, 2),
                      "allocated_peak_gb": round(st.get("allocated_bytes.all.peak", 0) / 2 ** 30, 2)})
@@ -536,7 +592,16 @@ def main():
                 elapsed, loss = timed(run, steps, args.warmup, world, timer, dg)
             torch.cuda.current_stream().wait_stream(hs)
         else:
-            elapsed, loss = timed(run, steps, args.warmup, world, timer, dg)
+            elapsed, loss = timed(run, steps, args.warmup, world, None if run.use_graph else timer, dg)
+        if timer is not None and run.use_graph:
+            # per-kernel durations for the roofline lines: HIP events need the launches they bracket, so
+            # they come from eager steps of the same step (the graph replays exactly these launches)
+            run.use_graph = False
+            try:
+                timed(run, steps, 1, world, timer)
+            finally:
+                run.use_graph = True
+            timer.eager = True
         if dg is not None:
             if mode == modes[0]:
                 dg["clock_mhz_after"] = round(ops.clock_probe(dev), 1)
@@ -546,15 +611,16 @@ def main():
             log(f"{args.model} {mode}: {1e3 * elapsed / steps:.2f} ms/step")
         if diag is not None and mode == "unfrozen" and args.model == "lstmv" and not fusion:
             # the same step with the weight gradients on the main stream (no side-stream overlap)
-            prev_side = engine.WGRAD_SIDE_STREAM
+            prev_side, prev_graph = engine.WGRAD_SIDE_STREAM, run.use_graph
             engine.WGRAD_SIDE_STREAM = False
+            run.use_graph = False   # (eager: the captured graph holds the side-stream form)
             try:
                 s2 = max(3, args.steps // 2)
                 e2, _ = timed(run, s2, 2, world)
                 diag["unfrozen"]["wgrad_main_stream_ms"] = round(1e3 * e2 / s2, 3)
                 log(f"{args.model} {mode}, weight gradients on the main stream: {1e3 * e2 / s2:.2f} ms/step")
             finally:
-                engine.WGRAD_SIDE_STREAM = prev_side
+                engine.WGRAD_SIDE_STREAM, run.use_graph = prev_side, prev_graph
         del run
         torch.cuda.empty_cache()
     small = None
@@ -614,6 +680,12 @@ def main():
                     "kernel": f"gemm_tn256_kernel (split-K weight gradient dW = dY^T X of the 728->728 pointwise @{hm}x{hm}, "
                               f"side stream beside the backward's main stream; slab reduction not included)",
                     "flops_per_launch": flops, "avg_launch_ms": round(tn_ms, 4), "launches": timer.count("tn_728")}
+        if timer is not None and getattr(timer, "eager", False):
+            note = ("HIP events on the launch stream around every launch, on eager steps of the same train step "
+                    "run right after the timed region (the timed steps replay it as one HIP graph: the same launches)")
+            for r in [roof, extra.get("roofline_dw"), extra.get("roofline_wgrad")]:
+                if r:
+                    r["timing"] = note
         if not audio and not fusion and args.dtype == "bf16":
             ideal, fl, by = step_roofline(S, frames, head == "unfrozen")
             ms = 1e3 * elapsed / steps
@@ -658,7 +730,9 @@ def main():
                                         "accumulation 4, clip 1.0, AdamW, OneCycleLR, averaged model (train_au_face.py)"
                                         if fusion else "clip 1.0 + Adam, " + ("xcp FusedAdamClip" if args.optim == "fused"
                                                                               else "torch fused Adam")),
-                          "parallelism": f"dp{world}"},
+                          "parallelism": f"dp{world}",
+                          "execution": "one HIP graph per train step (captured after the eager warm-up, replayed)"
+                          if graph_mode(args, world) else "eager launches"},
                "roofline": roof, "loss": round(loss, 5)}
         out.update(extra)
         if small is not None:

@@ -222,6 +222,10 @@ int xcp_resize_bilinear(const float* in, float* out, int NC, int IH, int IW, int
 int xcp_opt_sumsq(const long long* tab, int nchunks, float* part, float max_norm, float* out, xcp_stream_t stream);
 int xcp_opt_adam(const long long* tab, int nchunks, const float* coef, float lr, float b1, float b2, float eps, float wd,
                  float bc1, float bc2sqrt, xcp_stream_t stream);
+/* xcp_opt_adam with the step count t read from device memory (tdev[0]; the bias corrections formed on
+ * the device in double from the double betas, as the host computes them): a graph-captured optimizer step */
+int xcp_opt_adam_dev(const long long* tab, int nchunks, const float* coef, float lr, double b1, double b2, float eps,
+                     float wd, const float* tdev, xcp_stream_t stream);
 
 /* njobs permute3 jobs in one launch: jobs = DEVICE array [njobs][12] int64
  * (in, out, d0, d1, d2, p0, p1, p2, out dtype, first workgroup, s0, s1), nblocks workgroups in

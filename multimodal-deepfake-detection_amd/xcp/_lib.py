@@ -66,6 +66,7 @@ SIGNATURES = {
     "xcp_frames_prep": [P, P, P, I, I, I, I, I, I, I, I, P],
     "xcp_opt_sumsq": [P, I, P, F, P, P],
     "xcp_opt_adam": [P, I, P, F, F, F, F, F, F, F, P],
+    "xcp_opt_adam_dev": [P, I, P, F, D, D, F, F, P, P],
     "xcp_conv3x3_parts": [I, I, I, I],
     "xcp_conv3x3": [I, P, P, P, P, I, I, I, P],
     "xcp_conv3x3_wgrad_parts": [I, I, I],

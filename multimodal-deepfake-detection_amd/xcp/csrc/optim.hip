@@ -65,7 +65,8 @@ __global__ __launch_bounds__(1024) void opt_clipcoef_kernel(const float* __restr
 
 __global__ __launch_bounds__(OPT_THREADS) void opt_adam_kernel(const long long* __restrict__ tab,
                                                                const float* __restrict__ coef, float lr, float b1,
-                                                               float b2, float eps, float wd, float bc1, float bc2sqrt) {
+                                                               float b2, float eps, float wd, float bc1, float bc2sqrt,
+                                                               const float* __restrict__ tdev, double b1d, double b2d) {
   const long long* e = tab + (long)blockIdx.x * 6;
   const long o = e[4];
   float* p = reinterpret_cast<float*>(e[0]) + o;
@@ -74,6 +75,11 @@ __global__ __launch_bounds__(OPT_THREADS) void opt_adam_kernel(const long long* 
   float* v = reinterpret_cast<float*>(e[3]) + o;
   const int n = (int)e[5];
   const float c = coef ? coef[0] : 1.f;
+  if (tdev) {   // step count on the device (graph-captured steps): the host formula, in double
+    const double t = (double)tdev[0];
+    bc1 = (float)(1.0 - pow(b1d, t));
+    bc2sqrt = (float)sqrt(1.0 - pow(b2d, t));
+  }
   const float step = lr / bc1;
   // 4 elements per thread per pass, every load issued before the math (memory-level parallelism)
   for (int i0 = threadIdx.x; i0 < n; i0 += 4 * OPT_THREADS) {
@@ -119,7 +125,19 @@ int xcp_opt_adam(const long long* tab, int nchunks, const float* coef, float lr,
                  float bc1, float bc2sqrt, hipStream_t st) {
   if (nchunks <= 0) return XCP_OK;
   hipLaunchKernelGGL(opt_adam_kernel, dim3(nchunks), dim3(OPT_THREADS), 0, st, tab, coef, lr, b1, b2, eps, wd, bc1,
-                     bc2sqrt);
+                     bc2sqrt, nullptr, 0.0, 0.0);
+  return (int)hipGetLastError();
+}
+
+// the same update with the step count read from device memory (tdev[0], the count after this step):
+// bc1 = 1 - b1^t, bc2sqrt = sqrt(1 - b2^t) formed on the device in double from the double betas, as
+// the host does for xcp_opt_adam -- so a captured (graph-replayed) step needs no host arithmetic
+int xcp_opt_adam_dev(const long long* tab, int nchunks, const float* coef, float lr, double b1, double b2, float eps,
+                     float wd, const float* tdev, hipStream_t st) {
+  if (nchunks <= 0) return XCP_OK;
+  if (!tdev) return XCP_EINVAL;
+  hipLaunchKernelGGL(opt_adam_kernel, dim3(nchunks), dim3(OPT_THREADS), 0, st, tab, coef, lr, (float)b1, (float)b2, eps,
+                     wd, 1.f, 1.f, tdev, b1, b2);
   return (int)hipGetLastError();
 }
 

@@ -18,6 +18,12 @@ total norm inside the update; ``param.grad`` keeps the unclipped gradient and ``
 returns the pre-clip total norm as a fresh 0-d device tensor (clip_grad_norm_'s return).
 Without ``max_norm`` the script's own clip_grad_norm_ call does the clipping (as the
 reference scripts do) and ``step()`` returns None.
+
+``capturable=True`` (torch Adam's flag of that name): the step count lives on the device (one
+0-d tensor per param group, shared by the group's parameters' ``state["step"]``), incremented and
+turned into the bias corrections on the device (xcp_opt_adam_dev), so the step can be captured in
+a HIP graph and replayed -- no host arithmetic, no host sync.  A group's parameters must then share
+one step count (they do unless states were loaded piecemeal).
 """
 import math
 
@@ -30,7 +36,8 @@ CHUNK = 16384
 
 
 class FusedAdamClip(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_norm=None):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_norm=None,
+                 capturable=False):
         if lr < 0.0 or eps < 0.0 or weight_decay < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
             raise ValueError("FusedAdamClip: invalid hyper-parameter")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -40,13 +47,15 @@ class FusedAdamClip(torch.optim.Optimizer):
                     raise ValueError("FusedAdamClip: fp32 contiguous parameters only")
                 ops.check_gpu(p)
         self.max_norm = max_norm
+        self.capturable = capturable
+        self._tdev = {}   # capturable: param-group index -> the group's device step count
         self._tables = {}
         self._out = None
 
-    def _state(self, p):
+    def _state(self, p, gi=None):
         st = self.state[p]
         if not st:
-            st["step"] = torch.tensor(0.0)
+            st["step"] = self._tdev[gi] if self.capturable else torch.tensor(0.0)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         return st
@@ -86,6 +95,8 @@ class FusedAdamClip(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self.capturable:
+            return self._step_capturable(loss)
         # parameters with a gradient, grouped by (param group, step count) for the bias corrections
         launches, every = [], []
         for gi, grp in enumerate(self.param_groups):
@@ -124,6 +135,58 @@ class FusedAdamClip(torch.optim.Optimizer):
         # the kernels wrote the parameters through raw pointers: bump their autograd version
         # counters as an in-place torch op would, so that consumers keyed on them (the xcp
         # engine's packed-weight cache, engine.pack) see the update
+        increment_version([row[0] for row in every])
+        if loss is not None:
+            return loss
+        return self._out[1].clone() if self.max_norm is not None else None
+
+    def _step_capturable(self, loss):
+        """step() with the step counts on the device: per group, t += 1 on the device, then one Adam
+        launch reading t (no .item(), no host-side bias corrections)"""
+        launches, every = [], []
+        for gi, grp in enumerate(self.param_groups):
+            rows = []
+            for p in grp["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("FusedAdamClip does not support sparse gradients")
+                if gi not in self._tdev:
+                    self._tdev[gi] = torch.zeros((), device=p.device, dtype=torch.float32)
+                st = self._state(p, gi)
+                if st["step"] is not self._tdev[gi]:
+                    # a loaded state: adopt its count into the group's device counter (all must agree)
+                    t = float(st["step"])
+                    if any(float(self.state[q]["step"]) != t for q in grp["params"] if q in self.state
+                           and self.state[q]["step"] is not self._tdev[gi]):
+                        raise ValueError("FusedAdamClip(capturable=True): a param group's step counts differ")
+                    self._tdev[gi].fill_(t)
+                    for q in grp["params"]:
+                        if q in self.state:
+                            self.state[q]["step"] = self._tdev[gi]
+                rows.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"]))
+            if rows:
+                launches.append((gi, grp, rows))
+                every.extend(rows)
+        if not every:
+            return loss
+        dev = every[0][0].device
+        with ops.device_guard(every[0][0]):
+            s = ops.stream()
+            coef = 0
+            if self.max_norm is not None:
+                tab = self._table(self._key("all", every), every, dev)
+                part = torch.empty(tab.shape[0], device=dev, dtype=torch.float32)
+                self._out = torch.empty(2, device=dev, dtype=torch.float32)
+                _lib.call("xcp_opt_sumsq", tab.data_ptr(), tab.shape[0], part.data_ptr(), float(self.max_norm),
+                          self._out.data_ptr(), s)
+                coef = self._out.data_ptr()
+            for gi, grp, rows in launches:
+                self._tdev[gi].add_(1.0)
+                tab = self._table(self._key("grp", rows), rows, dev)
+                b1, b2 = grp["betas"]
+                _lib.call("xcp_opt_adam_dev", tab.data_ptr(), tab.shape[0], coef, float(grp["lr"]), float(b1), float(b2),
+                          float(grp["eps"]), float(grp["weight_decay"]), self._tdev[gi].data_ptr(), s)
         increment_version([row[0] for row in every])
         if loss is not None:
             return loss

@@ -208,3 +208,79 @@ def test_second_step_forward_uses_updated_weights(gpu):
     torch.cuda.synchronize()
     assert not torch.equal(outs[0], outs[1])
     torch.testing.assert_close(got, want, rtol=0, atol=0)
+
+
+def test_fused_adam_capturable_matches_eager(gpu):
+    """FusedAdamClip(capturable=True) -- device step counts, bias corrections formed on the device --
+    captured in a HIP graph and replayed gives bit for bit the eager optimiser's parameters, moments
+    and step count (clip on)."""
+    from xcp.optim import FusedAdamClip
+    g = torch.Generator(device=gpu).manual_seed(5)
+    shapes = [(700, 33), (5,), (64, 3, 3, 3), (40000,)]
+    init = [torch.randn(s, device=gpu, generator=g) for s in shapes]
+    grads = [torch.randn(s, device=gpu, generator=g) for s in shapes]
+    pa = [t.clone().requires_grad_(True) for t in init]
+    pb = [t.clone().requires_grad_(True) for t in init]
+    for p, q, gr in zip(pa, pb, grads):
+        p.grad, q.grad = gr.clone(), gr.clone()
+    oa = FusedAdamClip(pa, lr=1e-2, weight_decay=1e-4, max_norm=1.0)
+    ob = FusedAdamClip(pb, lr=1e-2, weight_decay=1e-4, max_norm=1.0, capturable=True)
+    for _ in range(4):
+        oa.step()
+    ob.step()   # eager (creates the state and the tables), then one captured step replayed three times
+    s = torch.cuda.Stream(gpu)
+    s.wait_stream(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ob.step()
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    for p, q in zip(pa, pb):
+        assert torch.equal(p, q)
+        assert torch.equal(oa.state[p]["exp_avg"], ob.state[q]["exp_avg"])
+        assert torch.equal(oa.state[p]["exp_avg_sq"], ob.state[q]["exp_avg_sq"])
+        assert float(ob.state[q]["step"]) == 4.0
+
+
+def test_graph_captured_train_step_matches_eager(gpu):
+    """The bench's graph mode: a whole xception(num_classes=1) train step (bf16 engine forward and
+    backward with the side-stream weight gradients, BCE, clip + Adam with device step counts) captured
+    as one HIP graph and replayed gives bit for bit the parameters and BatchNorm buffers of the same
+    steps run eagerly."""
+    import xcp
+    from torch.autograd.graph import increment_version
+    from xcp.optim import FusedAdamClip
+    from Models.Xception import xception
+    x = seeded_uniform((4, 3, 96, 96), 31).to(gpu)
+    y = torch.tensor([[0.0], [1.0], [1.0], [0.0]], device=gpu)
+    models = []
+    for capt in (False, True):
+        torch.manual_seed(0)
+        m = xception(num_classes=1).to(gpu).train()
+        opt = FusedAdamClip(m.parameters(), lr=1e-3, weight_decay=1e-4, max_norm=1.0, capturable=capt)
+
+        def step():
+            opt.zero_grad(set_to_none=False)
+            nn.BCEWithLogitsLoss()(m(x), y).backward()
+            opt.step()
+
+        with xcp.precision("bf16"):
+            if not capt:
+                for _ in range(4):
+                    step()
+            else:
+                step()   # eager warm-up: persistent buffers, packs, optimiser tables
+                torch.cuda.synchronize()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    step()
+                for _ in range(3):
+                    graph.replay()
+                    increment_version(list(m.parameters()))
+        torch.cuda.synchronize()
+        models.append(m)
+    sa, sb = models[0].state_dict(), models[1].state_dict()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
