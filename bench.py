@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="replay the whole train step as one HIP graph (auto: on at world size 1, off across ranks)")
+                    help="replay the whole train step as one HIP graph (on: world size 1; auto = off, measured slower)")
     ap.add_argument("--small-batch", type=int, default=4,
                     help="lstmv: also time the unfrozen step at this many clips/GPU (train_visual.py:545 uses 4; "
                          "0: off)")
@@ -105,11 +105,11 @@ def launch_ranks(args):
 
 
 def graph_mode(args, world):
-    """Replay the train step as one HIP graph: --graph on / off, auto = on at world size 1 (the
-    multi-rank step launches RCCL collectives from inside the backward; they stay eager)."""
-    if args.graph == "on":
-        return True
-    return args.graph == "auto" and world == 1 and args.model != "auface"
+    """Replay the train step as one HIP graph (--graph on; world size 1 only: the multi-rank step
+    launches RCCL collectives from inside the backward).  auto = off: measured 1.1 % slower than eager
+    launches (profiles/r04_graph_ab.txt) -- the replay spreads the step's nodes over four hardware
+    queues with a barrier on every cross-queue edge, and the kernel-to-kernel dispatch gaps stay."""
+    return args.graph == "on" and world == 1 and args.model != "auface"
 
 
 def middle_hw(size):
