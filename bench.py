@@ -592,16 +592,19 @@ def main():
                 elapsed, loss = timed(run, steps, args.warmup, world, timer, dg)
             torch.cuda.current_stream().wait_stream(hs)
         else:
-            elapsed, loss = timed(run, steps, args.warmup, world, None if run.use_graph else timer, dg)
-        if timer is not None and run.use_graph:
-            # per-kernel durations for the roofline lines: HIP events need the launches they bracket, so
-            # they come from eager steps of the same step (the graph replays exactly these launches)
+            elapsed, loss = timed(run, steps, args.warmup, world, None, dg)
+        if timer is not None:
+            # per-kernel durations for the roofline lines, on a second timed region of the same steps right
+            # after the headline one: the bracketing HIP events cost the step 1.1-1.5 % (409.1 vs 414.5
+            # clips/s, profiles/r04_kernel_timer_ab.txt), so the headline region runs without them (and a
+            # graph-replayed step has no launches to bracket)
+            prev_graph = run.use_graph
             run.use_graph = False
             try:
                 timed(run, steps, 1, world, timer)
             finally:
-                run.use_graph = True
-            timer.eager = True
+                run.use_graph = prev_graph
+            timer.separate = True
         if dg is not None:
             if mode == modes[0]:
                 dg["clock_mhz_after"] = round(ops.clock_probe(dev), 1)
@@ -680,9 +683,10 @@ def main():
                     "kernel": f"gemm_tn256_kernel (split-K weight gradient dW = dY^T X of the 728->728 pointwise @{hm}x{hm}, "
                               f"side stream beside the backward's main stream; slab reduction not included)",
                     "flops_per_launch": flops, "avg_launch_ms": round(tn_ms, 4), "launches": timer.count("tn_728")}
-        if timer is not None and getattr(timer, "eager", False):
-            note = ("HIP events on the launch stream around every launch, on eager steps of the same train step "
-                    "run right after the timed region (the timed steps replay it as one HIP graph: the same launches)")
+        if timer is not None and getattr(timer, "separate", False):
+            note = ("HIP events on the launch stream around every launch of the op, over a second timed region of "
+                    f"{steps} eager steps of the same train step run right after the headline region (the events "
+                    "cost the step 1.1-1.5 %, so the headline region runs without them)")
             for r in [roof, extra.get("roofline_dw"), extra.get("roofline_wgrad")]:
                 if r:
                     r["timing"] = note
