@@ -446,7 +446,11 @@ XCP_DEV void xrow_store(float* sx, const XRowChunks& m, const f4a4 (&rx)[3]) {
 // row kernel below for the tile and the register prefetch), with BN1's batch statistics (STATS): each
 // workgroup sums y and y^2 of the stored (bf16-rounded) outputs of its tiles per channel and writes one
 // partial row part[blockIdx][2][32] -- the per-channel reduce pass over the 364 MB output is gone.
-// A thread owns an output-channel pair (its 27 weight pairs in registers) for every 16th pixel of the row.
+// The convolution is an im2col product on the matrix cores: per 16 output pixels, two
+// v_mfma_f32_16x16x32_bf16 (A = the pixels' 27 inputs padded to 32, gathered from the staged rows and
+// rounded to bf16 -- the input rounding of PyTorch's bf16 autocast conv; B = the 32 x 27 kernel, bf16, in
+// registers; fp32 accumulation).  The fp32 FMA form (27 packed FMAs and 18 LDS reads per pixel and
+// channel pair) was bound by LDS issue at ~2.4 TB/s.
 template <bool STATS>
 __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __restrict__ X, const float* __restrict__ Wt,
                                                             bf16* __restrict__ Y, float* __restrict__ part, int N,
@@ -455,45 +459,67 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
   __shared__ __attribute__((aligned(16))) float sx[9 * IWM];   // [9 rows][P]
   __shared__ __attribute__((aligned(16))) unsigned so[W1R_OWM * 16];   // the output row [OW][32] bf16
   __shared__ float red[2][4][C1];
-  const int tid = threadIdx.x, cp = tid & 15, pg = tid >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, kq = lane >> 4;
   const int P = pitch1(IW), T = N * OH;
   const long fsz = (long)IH * IW;
   const XRowChunks xm = xrow_chunks(tid, IH, IW, P);
-  f2v wk[K1];
+  // B fragments: kernel rows co = 16 cb + l16, taps k = 8 kq .. 8 kq + 7 (zero past 27); A gather offsets
+  // of this lane's taps inside the staged rows: tap k = 3 r + kx reads row r at column 2 p + kx
+  bf16x8 wb[2];
+  int toff[8];
+  unsigned kok = 0;
 #pragma unroll
-  for (int k = 0; k < K1; ++k) wk[k] = f2v{Wt[(2 * cp) * K1 + k], Wt[(2 * cp + 1) * K1 + k]};
+  for (int i = 0; i < 8; ++i) {
+    const int k = 8 * kq + i;
+    const bool ok = k < K1;
+    toff[i] = ok ? (k / 3) * P + k % 3 : 0;
+    kok |= ok ? 1u << i : 0u;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) wb[cb][i] = (bf16)(ok ? Wt[(16 * cb + l16) * K1 + k] : 0.f);
+  }
   f4a4 rx[3];
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
     xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, xm, rx);
   };
-  f2v s1 = f2v(0.f), s2 = f2v(0.f);
-  const float2* sx2 = reinterpret_cast<const float2*>(sx);
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+  bf16* sob = reinterpret_cast<bf16*>(so);
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int npg = (OW + 15) / 16;
   fetch(blockIdx.x);   // (the grid never exceeds the tile count)
   for (int t = blockIdx.x; t < T; t += gridDim.x) {
     __syncthreads();   // the previous tile's LDS reads (input rows, output row) are done
     xrow_store(sx, xm, rx);
     __syncthreads();
     fetch(min(t + (int)gridDim.x, T - 1));
-    for (int p = pg; p < OW; p += 16) {
-      f2v a0 = f2v(0.f), a1 = f2v(0.f), a2 = f2v(0.f);   // three chains (kx), added in a fixed order
+    for (int g = w; g < npg; g += 4) {
+      const int pa = min(g * 16 + l16, OW - 1);   // A row (clamped: rows past OW are not stored)
+      float xv[8];
 #pragma unroll
-      for (int r = 0; r < 9; ++r) {
-        const float2 x01 = sx2[(r * P >> 1) + p];
-        const float x2 = sx[r * P + 2 * p + 2];
-        a0 = __builtin_elementwise_fma(f2v(x01.x), wk[r * 3 + 0], a0);
-        a1 = __builtin_elementwise_fma(f2v(x01.y), wk[r * 3 + 1], a1);
-        a2 = __builtin_elementwise_fma(f2v(x2), wk[r * 3 + 2], a2);
-      }
-      const f2v o = (a0 + a1) + a2;
-      typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
-      const bf16x2 ob{(bf16)o[0], (bf16)o[1]};
-      so[p * 16 + cp] = __builtin_bit_cast(unsigned, ob);
-      if constexpr (STATS) {
-        const f2v q{(float)ob[0], (float)ob[1]};
-        s1 += q;
-        s2 = __builtin_elementwise_fma(q, q, s2);
+      for (int i = 0; i < 8; ++i) xv[i] = sx[toff[i] + 2 * pa];
+      bf16x8 a;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = (bf16)(((kok >> i) & 1) ? xv[i] : 0.f);
+      const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 acc[2];
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[0], z, 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[1], z, 0, 0, 0);
+      // acc[cb][r] = y[pixel 16 g + 4 kq + r][channel 16 cb + l16]
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = g * 16 + 4 * kq + r;
+        if (p < OW) {
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            const bf16 ob = (bf16)acc[cb][r];
+            sob[p * C1 + 16 * cb + l16] = ob;
+            if constexpr (STATS) {
+              const float q = (float)ob;
+              s1[cb] += q;
+              s2[cb] = fmaf(q, q, s2[cb]);
+            }
+          }
+        }
       }
     }
     __syncthreads();   // the output row is staged: 16-B stores, 4 lanes per pixel
@@ -504,17 +530,16 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
       if (tid + 256 * k < OW * 4) yrow[tid + 256 * k] = so4[tid + 256 * k];
   }
   if constexpr (STATS) {
-    const int w = tid >> 6;
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      float a = s1[e], b = s2[e];
+    for (int cb = 0; cb < 2; ++cb) {
+      float a = s1[cb], b = s2[cb];
       a += __shfl_xor(a, 16, 64);
       a += __shfl_xor(a, 32, 64);
       b += __shfl_xor(b, 16, 64);
       b += __shfl_xor(b, 32, 64);
-      if ((tid & 63) < 16) {
-        red[0][w][2 * cp + e] = a;
-        red[1][w][2 * cp + e] = b;
+      if (lane < 16) {
+        red[0][w][16 * cb + l16] = a;
+        red[1][w][16 * cb + l16] = b;
       }
     }
     __syncthreads();
@@ -531,13 +556,14 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
 //   dC1[p][c] = bf16(alpha[c] * g + bcoef[c] * y + delta[c]),  g = dZ[p][c], masked to 0 where
 //   y * ms[c] + mt[c] <= 0 (MODE 2: dZ is the gradient of relu(bn1(y)), Xception.py:170)
 // -- the value bn_bwd_apply_kernel stores (same fma order, same bf16 rounding), so the fused path equals
-// xcp_bn_bwd_apply + xcp_conv1_wgrad on the stored tensor up to the fp32 summation order of the sums.
-// MODE 0: dZ is dC1 itself.  Per tile: the three stride-2 input rows of each input channel (fp32, 4-B
-// loads) and the output row of dZ (and y) (16-B loads), ~31 KB; a thread owns one output-channel pair
-// x 27 taps (27 packed accumulators) for every 16th pixel of the row.  No LDS-DMA (a plain LDS read
-// after one makes hipcc drain every outstanding load), so the prefetch stays in flight through the
-// compute.
-
+// xcp_bn_bwd_apply + xcp_conv1_wgrad on the stored tensor bit for bit.  MODE 0: dZ is dC1 itself.
+// Per tile: the three stride-2 input rows of each input channel (fp32, 16-B loads) and the output row of
+// dZ (and y) (16-B loads), ~31 KB.  The sum over pixels runs on the matrix cores: per 32 pixels and
+// wave, dW[32 co][32 taps] += dC1^T[32 co][32 px] x Xcol[32 px][32 taps] as four
+// v_mfma_f32_16x16x32_bf16 (dC1 read by transposed LDS reads, ds_read_b64_tr_b16, and formed on the
+// spot; the inputs gathered and rounded to bf16, as PyTorch's bf16 autocast conv rounds them; fp32
+// accumulation).  No LDS-DMA (a plain LDS read after one makes hipcc drain every outstanding load), so
+// the prefetch stays in flight through the compute.
 template <int MODE>
 __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __restrict__ X, const bf16* __restrict__ dZ,
                                                               const bf16* __restrict__ Yv, const float* alpha,
@@ -545,24 +571,36 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
                                                               const float* mt, float* __restrict__ part, int N, int IH,
                                                               int IW, int OH, int OW) {
   constexpr bool BN = MODE != 0;
-  __shared__ __attribute__((aligned(16))) char smem[9 * W1R_IW * 4 + 2 * W1R_OW * 64];
+  constexpr int RPX = W1R_OW + 1;   // staged pixels per row (one spare: the transposed reads of the last
+                                    // 32-pixel group may address pixel OW)
+  __shared__ __attribute__((aligned(16))) char smem[9 * W1R_IW * 4 + 2 * RPX * 64];
   float* sx = reinterpret_cast<float*>(smem);                                    // [9 rows][P]
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 struct arrays end up in scratch)
   u32x4* sd = reinterpret_cast<u32x4*>(smem + 9 * W1R_IW * 4);                   // [OW * 4] chunks of dZ
-  u32x4* sy = sd + W1R_OW * 4;                                                   // [OW * 4] chunks of y
-  const int tid = threadIdx.x, cp = tid & 15, pg = tid >> 4;
+  u32x4* sy = sd + RPX * 4;                                                      // [OW * 4] chunks of y
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l16 = lane & 15, kq = lane >> 4;
   const int P = pitch1(IW), nch = OW * 4, T = N * OH;
   const long fsz = (long)IH * IW;
   const XRowChunks xm = xrow_chunks(tid, IH, IW, P);
-  float2 al = make_float2(1.f, 1.f), bc = make_float2(0.f, 0.f), de = bc, sm = al, tm = bc;
-  if constexpr (BN) {
-    al = *reinterpret_cast<const float2*>(alpha + 2 * cp);
-    bc = *reinterpret_cast<const float2*>(bcoef + 2 * cp);
-    de = *reinterpret_cast<const float2*>(delta + 2 * cp);
-  }
-  if constexpr (MODE == 2) {
-    sm = *reinterpret_cast<const float2*>(ms + 2 * cp);
-    tm = *reinterpret_cast<const float2*>(mt + 2 * cp);
+  // this lane's channels 16 cb + l16 (A rows) and their coefficients; its taps 16 kb + l16 (B columns)
+  float al[2] = {1.f, 1.f}, bc[2] = {0.f, 0.f}, de[2] = {0.f, 0.f}, sm[2] = {1.f, 1.f}, tm[2] = {0.f, 0.f};
+  int boff[2];
+  bool bok[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 16 * h + l16;
+    if constexpr (BN) {
+      al[h] = alpha[c];
+      bc[h] = bcoef[c];
+      de[h] = delta[c];
+    }
+    if constexpr (MODE == 2) {
+      sm[h] = ms[c];
+      tm[h] = mt[c];
+    }
+    const int k = 16 * h + l16;
+    bok[h] = k < K1;
+    boff[h] = bok[h] ? (k / 3) * P + k % 3 : 0;
   }
   f4a4 rx[3];
   u32x4 rd[W1R_DL], ry[BN ? W1R_DL : 1];
@@ -578,22 +616,24 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
       if constexpr (BN) ry[i] = *reinterpret_cast<const u32x4*>(Yv + db + j * 8);
     }
   };
-  f2v acc[K1];   // channels (2cp, 2cp+1) x taps
+  f32x4 acc[2][2];   // [co block][tap block]: lane holds dW[16 cb + 4 kq + r][16 kb + l16]
 #pragma unroll
-  for (int k = 0; k < K1; ++k) acc[k] = f2v(0.f);
-  const float2* sx2 = reinterpret_cast<const float2*>(sx);
-  const unsigned* sdu = reinterpret_cast<const unsigned*>(sd);
-  const unsigned* syu = reinterpret_cast<const unsigned*>(sy);
-  auto bf2 = [](unsigned u) { return f2v{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; };
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) acc[cb][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const char* sdc = reinterpret_cast<const char*>(sd);
+  const char* syc = reinterpret_cast<const char*>(sy);
+  const int q = l16 >> 2, pp = l16 & 3;   // transposed read: lane 4q + pp addresses pixel row q, channels 4pp..4pp+3
+  const int ngr = (OW + 31) / 32;
   fetch(blockIdx.x);   // (the grid never exceeds the tile count)
   for (int t = blockIdx.x; t < T; t += gridDim.x) {
     __syncthreads();   // the previous tile's LDS reads are done
     xrow_store(sx, xm, rx);
     static_assert(W1R_DL == 3, "the chunk stores below are written out for three chunks per thread");
-    auto put = [&](int i, const u32x4& v, const u32x4& w) {
+    auto put = [&](int i, const u32x4& v, const u32x4& wv) {
       if (tid + 256 * i < nch) {
         sd[tid + 256 * i] = v;
-        if constexpr (BN) sy[tid + 256 * i] = w;
+        if constexpr (BN) sy[tid + 256 * i] = wv;
       }
     };
     put(0, rd[0], ry[BN ? 0 : 0]);
@@ -601,65 +641,59 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     put(2, rd[2], ry[BN ? 2 : 0]);
     __syncthreads();
     fetch(min(t + (int)gridDim.x, T - 1));   // next tile (the last tile once more past the end)
-    for (int p = pg; p < OW; p += 16) {
-      f2v d = bf2(sdu[p * 16 + cp]);
-      if constexpr (BN) {
-        const f2v y = bf2(syu[p * 16 + cp]);
-        if constexpr (MODE == 2) {
-          d[0] = fmaf(y[0], sm.x, tm.x) > 0.f ? d[0] : 0.f;
-          d[1] = fmaf(y[1], sm.y, tm.y) > 0.f ? d[1] : 0.f;
+    for (int g = w; g < ngr; g += 4) {
+      const int p0 = 32 * g + 8 * kq;   // this lane's 8 pixels: A columns, B rows
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int o0 = ((p0 + q) * C1 + 16 * cb + 4 * pp) * 2, o1 = o0 + 4 * C1 * 2;
+        const bf16x4 d0 = ds_read_tr(sdc + o0), d1 = ds_read_tr(sdc + o1);
+        bf16x4 y0 = d0, y1 = d1;
+        if constexpr (BN) {
+          y0 = ds_read_tr(syc + o0);
+          y1 = ds_read_tr(syc + o1);
         }
-        d[0] = rnd<bf16>(fmaf(al.x, d[0], fmaf(bc.x, y[0], de.x)));
-        d[1] = rnd<bf16>(fmaf(al.y, d[1], fmaf(bc.y, y[1], de.y)));
-      }
-      // the pixel's 27 inputs in two batches of reads (rows 0-4, 5-8), each batch read before its
-      // FMAs: two LDS round trips per pixel (left alone, hipcc reused one register triple and waited
-      // after every read: nine; one batch of all 27 spills at three waves per SIMD)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        constexpr int RB = 5;
-        float2 x01[RB];
-        float x2[RB];
-#pragma unroll
-        for (int i = 0; i < RB; ++i) {
-          const int r = h * RB + i;
-          if (r < 9) {
-            x01[i] = sx2[(r * P >> 1) + p];
-            x2[i] = sx[r * P + 2 * p + 2];
+        for (int i = 0; i < 8; ++i) {
+          float d = (float)(i < 4 ? d0[i] : d1[i - 4]);
+          if constexpr (BN) {
+            const float y = (float)(i < 4 ? y0[i] : y1[i - 4]);
+            if constexpr (MODE == 2) d = fmaf(y, sm[cb], tm[cb]) > 0.f ? d : 0.f;
+            d = fmaf(al[cb], d, fmaf(bc[cb], y, de[cb]));
           }
+          a[cb][i] = (bf16)(p0 + i < OW ? d : 0.f);
         }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < RB; ++i) {
-          const int r = h * RB + i;
-          if (r < 9) {
-            acc[r * 3 + 0] = __builtin_elementwise_fma(f2v(x01[i].x), d, acc[r * 3 + 0]);
-            acc[r * 3 + 1] = __builtin_elementwise_fma(f2v(x01[i].y), d, acc[r * 3 + 1]);
-            acc[r * 3 + 2] = __builtin_elementwise_fma(f2v(x2[i]), d, acc[r * 3 + 2]);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
       }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int pc = min(p0 + i, OW - 1);
+          const float x = sx[boff[kb] + 2 * pc];
+          b[kb][i] = (bf16)(bok[kb] && p0 + i < OW ? x : 0.f);
+        }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) acc[cb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cb], b[kb], acc[cb][kb], 0, 0, 0);
     }
   }
-  // reduce the 16 pixel groups: lanes xor 16 / 32 within the wave, then the 4 waves in LDS
+  // reduce the 4 waves in LDS: red[wave][co][tap < 27]
   __syncthreads();
   float* red = reinterpret_cast<float*>(smem);   // [4 waves][C1][K1] (13.8 KB)
-  const int w = tid >> 6;
 #pragma unroll
-  for (int k = 0; k < K1; ++k)
+  for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      float v = acc[k][e];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      if ((tid & 63) < 16) red[(w * C1 + 2 * cp + e) * K1 + k] = v;
-    }
+    for (int kb = 0; kb < 2; ++kb)
+      if (bok[kb]) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(w * C1 + 16 * cb + 4 * kq + r) * K1 + 16 * kb + l16] = acc[cb][kb][r];
+      }
   __syncthreads();
   for (int i = tid; i < C1 * K1; i += 256) {
     float v = 0.f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v += red[q * C1 * K1 + i];
+    for (int qq = 0; qq < 4; ++qq) v += red[qq * C1 * K1 + i];
     part[(long)blockIdx.x * (C1 * K1) + i] = v;
   }
 }

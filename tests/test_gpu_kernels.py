@@ -737,8 +737,9 @@ def test_conv1_wgrad_bn_fused(ops, gpu, N, IH, IW, relu):
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
     torch.testing.assert_close(acc, ref + 1, rtol=1e-6, atol=1e-5)
+    # (the kernel rounds the inputs to bf16 for the matrix cores, as PyTorch's bf16 autocast conv does)
     w = torch.zeros(32, 3, 3, 3, device=gpu, requires_grad=True)
-    F.conv2d(x, w, None, 2, 0).backward(nchw(dC1.view(N, OH, OW, C)).float())
+    F.conv2d(x.bfloat16().float(), w, None, 2, 0).backward(nchw(dC1.view(N, OH, OW, C)).float())
     assert rel_err(out.view(32, 3, 3, 3), w.grad) < 1e-5
 
 
