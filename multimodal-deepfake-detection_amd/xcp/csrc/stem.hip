@@ -446,11 +446,13 @@ XCP_DEV void xrow_store(float* sx, const XRowChunks& m, const f4a4 (&rx)[3]) {
 // row kernel below for the tile and the register prefetch), with BN1's batch statistics (STATS): each
 // workgroup sums y and y^2 of the stored (bf16-rounded) outputs of its tiles per channel and writes one
 // partial row part[blockIdx][2][32] -- the per-channel reduce pass over the 364 MB output is gone.
-// The convolution is an im2col product on the matrix cores: per 16 output pixels, two
-// v_mfma_f32_16x16x32_bf16 (A = the pixels' 27 inputs padded to 32, gathered from the staged rows and
-// rounded to bf16 -- the input rounding of PyTorch's bf16 autocast conv; B = the 32 x 27 kernel, bf16, in
-// registers; fp32 accumulation).  The fp32 FMA form (27 packed FMAs and 18 LDS reads per pixel and
-// channel pair) was bound by LDS issue at ~2.4 TB/s.
+// The convolution is an im2col product on the matrix cores: per 16 output pixels and 16 channels,
+// v_mfma_f32_16x16x32_bf16 over A = the pixels' 27 inputs (padded to 32, gathered from the staged rows)
+// and B = the 32 x 27 kernel (in registers), each split into a bf16 head and a bf16 tail (x = hi + lo,
+// |lo| <= 2^-9 |x|): hi.hi + lo.hi + hi.lo in fp32, three MFMAs, products exact to ~2^-17 -- the fp32
+// conv's accuracy, not bf16's (a single bf16 x bf16 product moved the 64^2 features' cosine to the
+// fp32 reference from 0.9991 to 0.9988).  The fp32 FMA form (27 packed FMAs and 18 LDS reads per pixel
+// and channel pair) was bound by LDS issue at ~2.4 TB/s; the matrix cores leave the kernel memory-bound.
 template <bool STATS>
 __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __restrict__ X, const float* __restrict__ Wt,
                                                             bf16* __restrict__ Y, float* __restrict__ part, int N,
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
   const XRowChunks xm = xrow_chunks(tid, IH, IW, P);
   // B fragments: kernel rows co = 16 cb + l16, taps k = 8 kq .. 8 kq + 7 (zero past 27); A gather offsets
   // of this lane's taps inside the staged rows: tap k = 3 r + kx reads row r at column 2 p + kx
-  bf16x8 wb[2];
+  bf16x8 wb[2], wl[2];   // kernel head / tail
   int toff[8];
   unsigned kok = 0;
 #pragma unroll
@@ -475,7 +477,11 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
     toff[i] = ok ? (k / 3) * P + k % 3 : 0;
     kok |= ok ? 1u << i : 0u;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) wb[cb][i] = (bf16)(ok ? Wt[(16 * cb + l16) * K1 + k] : 0.f);
+    for (int cb = 0; cb < 2; ++cb) {
+      const float wv = ok ? Wt[(16 * cb + l16) * K1 + k] : 0.f;
+      wb[cb][i] = (bf16)wv;
+      wl[cb][i] = (bf16)(wv - (float)wb[cb][i]);
+    }
   }
   f4a4 rx[3];
   auto fetch = [&](int t) {
@@ -497,13 +503,21 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
       float xv[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) xv[i] = sx[toff[i] + 2 * pa];
-      bf16x8 a;
+      bf16x8 a, al;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = (bf16)(((kok >> i) & 1) ? xv[i] : 0.f);
+      for (int i = 0; i < 8; ++i) {
+        const float v = ((kok >> i) & 1) ? xv[i] : 0.f;
+        a[i] = (bf16)v;
+        al[i] = (bf16)(v - (float)a[i]);
+      }
       const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
       f32x4 acc[2];
-      acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[0], z, 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[1], z, 0, 0, 0);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wb[cb], z, 0, 0, 0);          // small terms first
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wl[cb], acc[cb], 0, 0, 0);
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[cb], acc[cb], 0, 0, 0);
+      }
       // acc[cb][r] = y[pixel 16 g + 4 kq + r][channel 16 cb + l16]
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -559,10 +573,10 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
 // xcp_bn_bwd_apply + xcp_conv1_wgrad on the stored tensor bit for bit.  MODE 0: dZ is dC1 itself.
 // Per tile: the three stride-2 input rows of each input channel (fp32, 16-B loads) and the output row of
 // dZ (and y) (16-B loads), ~31 KB.  The sum over pixels runs on the matrix cores: per 32 pixels and
-// wave, dW[32 co][32 taps] += dC1^T[32 co][32 px] x Xcol[32 px][32 taps] as four
-// v_mfma_f32_16x16x32_bf16 (dC1 read by transposed LDS reads, ds_read_b64_tr_b16, and formed on the
-// spot; the inputs gathered and rounded to bf16, as PyTorch's bf16 autocast conv rounds them; fp32
-// accumulation).  No LDS-DMA (a plain LDS read after one makes hipcc drain every outstanding load), so
+// wave, dW[32 co][32 taps] += dC1^T[32 co][32 px] x Xcol[32 px][32 taps] as v_mfma_f32_16x16x32_bf16
+// (dC1 -- bf16 already -- read by transposed LDS reads, ds_read_b64_tr_b16, and formed on the spot; the
+// gathered inputs split into a bf16 head and tail, two MFMAs per block, so the products are exact to
+// ~2^-17 as in the forward; fp32 accumulation).  No LDS-DMA (a plain LDS read after one makes hipcc drain every outstanding load), so
 // the prefetch stays in flight through the compute.
 template <int MODE>
 __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __restrict__ X, const bf16* __restrict__ dZ,
@@ -643,7 +657,7 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     fetch(min(t + (int)gridDim.x, T - 1));   // next tile (the last tile once more past the end)
     for (int g = w; g < ngr; g += 4) {
       const int p0 = 32 * g + 8 * kq;   // this lane's 8 pixels: A columns, B rows
-      bf16x8 a[2], b[2];
+      bf16x8 a[2], b[2], bl[2];
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int o0 = ((p0 + q) * C1 + 16 * cb + 4 * pp) * 2, o1 = o0 + 4 * C1 * 2;
@@ -669,13 +683,17 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int pc = min(p0 + i, OW - 1);
-          const float x = sx[boff[kb] + 2 * pc];
-          b[kb][i] = (bf16)(bok[kb] && p0 + i < OW ? x : 0.f);
+          const float x = bok[kb] && p0 + i < OW ? sx[boff[kb] + 2 * pc] : 0.f;
+          b[kb][i] = (bf16)x;
+          bl[kb][i] = (bf16)(x - (float)b[kb][i]);
         }
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) acc[cb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cb], b[kb], acc[cb][kb], 0, 0, 0);
+        for (int kb = 0; kb < 2; ++kb) {
+          acc[cb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cb], bl[kb], acc[cb][kb], 0, 0, 0);
+          acc[cb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cb], b[kb], acc[cb][kb], 0, 0, 0);
+        }
     }
   }
   // reduce the 4 waves in LDS: red[wave][co][tap < 27]

@@ -708,7 +708,7 @@ def test_conv1_fwd_stats(ops, gpu, N, IH, IW):
     torch.testing.assert_close(sums[0], yd.sum(0), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(sums[1], (yd * yd).sum(0), rtol=1e-5, atol=1e-3)
     ref = F.conv2d(x, w, None, 2, 0)
-    assert rel_err(nchw(Y1.view(N, OH, OW, 32)).float(), ref) < 1e-2
+    assert rel_err(nchw(Y1.view(N, OH, OW, 32)).float(), ref) < 4e-3   # the bf16 output rounding alone
 
 
 @pytest.mark.parametrize("N,IH,IW", [(3, 299, 299), (2, 65, 64), (5, 17, 23), (1, 31, 320)])
@@ -737,10 +737,10 @@ def test_conv1_wgrad_bn_fused(ops, gpu, N, IH, IW, relu):
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
     torch.testing.assert_close(acc, ref + 1, rtol=1e-6, atol=1e-5)
-    # (the kernel rounds the inputs to bf16 for the matrix cores, as PyTorch's bf16 autocast conv does)
+    # (the matrix-core products split each input into a bf16 head and tail: exact to ~2^-17)
     w = torch.zeros(32, 3, 3, 3, device=gpu, requires_grad=True)
-    F.conv2d(x.bfloat16().float(), w, None, 2, 0).backward(nchw(dC1.view(N, OH, OW, C)).float())
-    assert rel_err(out.view(32, 3, 3, 3), w.grad) < 1e-5
+    F.conv2d(x, w, None, 2, 0).backward(nchw(dC1.view(N, OH, OW, C)).float())
+    assert rel_err(out.view(32, 3, 3, 3), w.grad) < 2e-5
 
 
 def test_permute3(ops, gpu):
