@@ -122,6 +122,24 @@ def main():
             flops=2.0 * M * C * C)
         rep("roofline op: dw_fwd 736 pitch act=2", timeit(lambda: ops.dw_fwd(2, Xp, Yp, Wtp, scp, shp, N, H, W, CP)),
             2 * (2 * M * C) + 36 * C)
+    if "ntprobe" in sel:   # the 256x256 NT kernel at the step's shape and at whole rounds (probe variants)
+        CP = 736
+        Xp = torch.zeros(M, CP, device=dev, dtype=dt)
+        Xp[:, :C] = X
+        Yp = torch.empty_like(Xp)
+        Wpp = torch.zeros(CP, CP, device=dev, dtype=dt)
+        Wpp[:C, :C] = Wp
+        stp = torch.empty(ops.nt_stat_rows(M) * 2 * CP, device=dev)
+        rep("nt 736 pitch +stats", timeit(lambda: ops.gemm_nt(Xp, Wpp, Yp, M, CP, CP, stats=stp)), flops=2.0 * M * C * C)
+        del Xp, Yp
+        Nn = 1024
+        for K in (768, 3072):
+            m = 256 * 64 * 4
+            Xk = torch.randn(m, K, device=dev, generator=g).to(dt)
+            Wk = (torch.randn(Nn, K, device=dev, generator=g) / 27).to(dt)
+            Yk = torch.empty(m, Nn, device=dev, dtype=dt)
+            rep(f"nt R=4 K={K}", timeit(lambda: ops.gemm_nt(Xk, Wk, Yk, m, Nn, K, tile=3)), flops=2.0 * m * Nn * K)
+            del Xk, Wk, Yk
     if "dwf_only" in sel:     # one kernel for the PMC passes
         rep("dw_fwd act=2", timeit(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
     if "dwb_only" in sel:
