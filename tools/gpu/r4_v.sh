@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for v in base nofill noread nomfma; do
+for v in ${VARS:-base nofill noread nomfma}; do
   if [ $v = base ]; then E="XCP_NONE=1"; else E="XCP_LIB_PATH=$PWD/tools/exp/nt_$v/libxcp.so"; fi
   echo "== $v" >> gpurun_out/v_probe.log
   env $E timeout -k 10 120 python -u tools/kbench.py ntprobe >> gpurun_out/v_probe.log 2>&1 || exit $?
