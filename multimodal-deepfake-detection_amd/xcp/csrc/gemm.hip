@@ -427,8 +427,7 @@ constexpr int BUF_DWORD3 = 0x00020000;   // gfx9 raw buffer descriptor word 3
 constexpr int K_SLOT = 2 * K_OP;
 
 XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
-  if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (n >= 4) wait_vmcnt<4>();
+  if (n >= 4) wait_vmcnt<4>();
   else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else wait_vmcnt<0>();
 }
@@ -680,12 +679,7 @@ XCP_DEV void epilogue256_buf(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffe
   epilogue256_get<STATS>([&](int i, int j, int r) { return acc[i][j][r]; }, a, rC, rS, m0, n0, wr, wc, fr, fg);
 }
 
-// PH2: two MFMA phases per K-tile instead of four (A-top x both B halves, then A-bot x both), each
-// with 32 MFMAs per wave between its two barriers: half the barriers per K-tile, the same register
-// set (every phase already held A-top or A-bot plus both B halves), the same per-accumulator MFMA
-// order (bitwise-equal outputs).  Phase A issues three parts of the next K-tile's fill (A-top, both B
-// halves; retired at the end of phase B), phase B the fourth (A-bot; retired in the next phase A).
-template <bool STATS, bool PH2 = false>
+template <bool STATS>
 __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   constexpr int S_ST = 16 + (STATS ? 1 : 0);   // store instructions per wave per epilogue
   __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
@@ -817,61 +811,8 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
       }
       sync_mfma(1, bl, 0);
     };
-    // two-phase K-tile (PH2): phase A reads A-top and both B halves, phase B A-bot
-    auto ktile2 = [&](int kt, auto first) {
-      const char* sa = smem + (kt & 1) * K_SLOT;
-      const char* sb = sa + K_OP;
-      const bool nxt = kt + 1 < nk;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          bl[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + j * 16 + fr, ks * 4 + fg));
-          br[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + 32 + j * 16 + fr, ks * 4 + fg));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 16 + fr, ks * 4 + fg));
-      }
-      if (nxt) {   // A-top, B-left, B-right of kt+1: landed by the end of phase B
-        issue(0, kt + 1);
-        issue(1, kt + 1);
-        issue(2, kt + 1);
-      }
-      if constexpr (!decltype(first)::value) wait_cnt(nxt ? 6 : 0);   // A-bot(kt) for phase B
-      __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-      mfma_q(0, bl, 0);
-      mfma_q(0, br, 1);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_s_barrier();
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
-      if (nxt) {
-        issue(3, kt + 1);
-        wait_cnt(2);   // A-top / B-left / B-right(kt+1) for phase A(kt+1); also retires the previous epilogue's stores
-      }
-      __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-      mfma_q(1, br, 1);
-      mfma_q(1, bl, 0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_s_barrier();
-    };
-    if constexpr (PH2) {
-      ktile2(0, IC<1>{});
-      for (int kt = 1; kt < nk; ++kt) ktile2(kt, IC<0>{});
-    } else {
-      ktile(0, IC<1>{});
-      for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
-    }
+    ktile(0, IC<1>{});
+    for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
     if (wr == 0) __builtin_amdgcn_s_barrier();   // every wave is done reading both ring slots
     const int cm0 = m0, cn0 = n0;
     t += nwg;
@@ -1309,12 +1250,6 @@ bool nt_big_n256() {
   return v;
 }
 
-// XCP_NT_PH2=1: the persistent kernel's two-phase K-tile (read per call; A/B)
-bool nt_ph2() {
-  const char* e = getenv("XCP_NT_PH2");
-  return e && e[0] == '1';
-}
-
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
   if (tile == 2 || tile == 3) return true;
@@ -1358,13 +1293,8 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
     if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
       const int grid = min(mb * gridN, cus);
-      const bool ph2 = nt_ph2();
-      if (stats && ph2)
-        hipLaunchKernelGGL((gemm_nt256p_kernel<true, true>), dim3(grid), dim3(512), 0, stream, big);
-      else if (stats)
+      if (stats)
         hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
-      else if (ph2)
-        hipLaunchKernelGGL((gemm_nt256p_kernel<false, true>), dim3(grid), dim3(512), 0, stream, big);
       else
         hipLaunchKernelGGL(gemm_nt256p_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
     } else if (buf)
