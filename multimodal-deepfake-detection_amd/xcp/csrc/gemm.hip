@@ -427,7 +427,8 @@ constexpr int BUF_DWORD3 = 0x00020000;   // gfx9 raw buffer descriptor word 3
 constexpr int K_SLOT = 2 * K_OP;
 
 XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
-  if (n >= 4) wait_vmcnt<4>();
+  if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 4) wait_vmcnt<4>();
   else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else wait_vmcnt<0>();
 }
@@ -848,19 +849,26 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
     };
     auto sb0 = [&]() { __builtin_amdgcn_sched_barrier(0); };
     // pipelined K-tile: on entry A-top(kt) / B-left(kt) are read (issued by the previous K-tile's Q3,
-    // or here for the first K-tile of a tile)
+    // or here for the first K-tile of a tile).  The waves of wr = 1 run one barrier behind those of
+    // wr = 0, so a part read in phase p must be waited for before phase p-1's first barrier (two
+    // barriers ahead of the read for the lagging group); the four parts of K-tile kt+1 are therefore
+    // all issued at the start of K-tile kt (their slot's last reads were consumed in Q2(kt-1)).
     auto ktileP = [&](int kt, auto first) {
       const char* sa = smem + (kt & 1) * K_SLOT;
       const char* sb = sa + K_OP;
       const bool nxt = kt + 1 < nk;
+      const long dn = (kt + 1) & 1 ? K_SLOT : -K_SLOT;   // slot of kt+1 relative to kt's
       if constexpr (decltype(first)::value) {
         rd_b(sb, bl, 0, 0);
         rd_a(sa, 0, 0);
         rd_b(sb, bl, 0, 1);
         rd_a(sa, 0, 1);
       }
-      if (nxt) issue(0, kt + 1);
-      if constexpr (!decltype(first)::value) wait_cnt(2 + (nxt ? 2 : 0));   // B-right(kt), read in Q0
+      if (nxt) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) issue(h, kt + 1);
+      }
+      if constexpr (!decltype(first)::value) wait_cnt(nxt ? 8 : 0);   // A-bot(kt), read in Q1
       enter();   // Q0: A-top x B-left; B-right(kt) read beside it
       rd_b(sb, br, 1, 0);
       rd_b(sb, br, 1, 1);
@@ -868,8 +876,6 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
       mf(0, bl, 0, 0);
       mf(0, bl, 0, 1);
       leave();
-      if (nxt) issue(1, kt + 1);
-      if constexpr (!decltype(first)::value) wait_cnt(nxt ? 4 : 0);         // A-bot(kt), read in Q1
       enter();   // Q1: A-top x B-right; A-bot(kt) read into the A registers half by half
       mf(0, br, 1, 0);
       sb0();
@@ -879,28 +885,25 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
       sb0();
       rd_a(sa, 1, 1);
       leave();
-      if (nxt) issue(2, kt + 1);
+      if (nxt) wait_cnt(4);   // A-top / B-left(kt+1), read in Q3; also retires the previous epilogue's stores
       enter();   // Q2: A-bot x B-right
       mf(1, br, 1, 0);
       mf(1, br, 1, 1);
       leave();
-      if (nxt) {
-        issue(3, kt + 1);
-        wait_cnt(4);   // A-top / B-left(kt+1), read in Q3; also retires the previous epilogue's stores
-      }
+      if (nxt) wait_cnt(2);   // B-right(kt+1), read in Q0(kt+1)
       enter();   // Q3: A-bot x B-left; the next K-tile's A-top / B-left read half by half
       mf(1, bl, 0, 0);
       if (nxt) {
         sb0();
-        rd_a(sa + ((kt + 1) & 1 ? K_SLOT : -K_SLOT), 0, 0);
-        rd_b(sb + ((kt + 1) & 1 ? K_SLOT : -K_SLOT), bl, 0, 0);
+        rd_a(sa + dn, 0, 0);
+        rd_b(sb + dn, bl, 0, 0);
         sb0();
       }
       mf(1, bl, 0, 1);
       if (nxt) {
         sb0();
-        rd_a(sa + ((kt + 1) & 1 ? K_SLOT : -K_SLOT), 0, 1);
-        rd_b(sb + ((kt + 1) & 1 ? K_SLOT : -K_SLOT), bl, 0, 1);
+        rd_a(sa + dn, 0, 1);
+        rd_b(sb + dn, bl, 0, 1);
       }
       leave();
     };
