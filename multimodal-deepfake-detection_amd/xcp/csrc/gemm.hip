@@ -427,8 +427,7 @@ constexpr int BUF_DWORD3 = 0x00020000;   // gfx9 raw buffer descriptor word 3
 constexpr int K_SLOT = 2 * K_OP;
 
 XCP_DEV void wait_cnt(int n) {   // outstanding LDS-DMA loads allowed to remain
-  if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 4) wait_vmcnt<4>();
+  if (n >= 4) wait_vmcnt<4>();
   else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else wait_vmcnt<0>();
 }
@@ -680,14 +679,7 @@ XCP_DEV void epilogue256_buf(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffe
   epilogue256_get<STATS>([&](int i, int j, int r) { return acc[i][j][r]; }, a, rC, rS, m0, n0, wr, wc, fr, fg);
 }
 
-// PIPE: each phase's fragments are read during the previous phase's MFMAs instead of between the
-// barriers: B-right during Q0 (its registers are free), A-bot during Q1 and the next K-tile's A-top /
-// B-left during Q3 (the ks = 0 half of a register array once its 8 MFMAs are issued, the ks = 1 half
-// after the rest); the compiler's own lgkmcnt waits (no lgkmcnt(0) after the barrier) let a phase's
-// first MFMAs start while its ks = 1 halves land.  The same data-visibility waits as the four-phase
-// loop (each read stays behind the wait + barrier that made its part visible), the same registers,
-// the same per-accumulator MFMA order (bitwise-equal outputs).
-template <bool STATS, bool PIPE = false>
+template <bool STATS>
 __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   constexpr int S_ST = 16 + (STATS ? 1 : 0);   // store instructions per wave per epilogue
   __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
@@ -819,101 +811,8 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
       }
       sync_mfma(1, bl, 0);
     };
-    auto rd_a = [&](const char* sa, int half, int ks) {   // half 0: A-top, 1: A-bot
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + half * 64 + i * 16 + fr, ks * 4 + fg));
-    };
-    auto rd_b = [&](const char* sb, bf16x8 (&b)[2][2], int half, int ks) {   // half 0: B-left, 1: B-right
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        b[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + half * 32 + j * 16 + fr, ks * 4 + fg));
-    };
-    auto mf = [&](int ih, const bf16x8 (&b)[2][2], int jh, int ks) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[ih * 4 + i][jh * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][ks], af[i][ks], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
-    };
-    auto enter = [&]() {
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-    };
-    auto leave = [&]() {
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-    };
-    auto sb0 = [&]() { __builtin_amdgcn_sched_barrier(0); };
-    // pipelined K-tile: on entry A-top(kt) / B-left(kt) are read (issued by the previous K-tile's Q3,
-    // or here for the first K-tile of a tile).  The waves of wr = 1 run one barrier behind those of
-    // wr = 0, so a part read in phase p must be waited for before phase p-1's first barrier (two
-    // barriers ahead of the read for the lagging group); the four parts of K-tile kt+1 are therefore
-    // all issued at the start of K-tile kt (their slot's last reads were consumed in Q2(kt-1)).
-    auto ktileP = [&](int kt, auto first) {
-      const char* sa = smem + (kt & 1) * K_SLOT;
-      const char* sb = sa + K_OP;
-      const bool nxt = kt + 1 < nk;
-      const long dn = (kt + 1) & 1 ? K_SLOT : -K_SLOT;   // slot of kt+1 relative to kt's
-      if constexpr (decltype(first)::value) {
-        rd_b(sb, bl, 0, 0);
-        rd_a(sa, 0, 0);
-        rd_b(sb, bl, 0, 1);
-        rd_a(sa, 0, 1);
-      }
-      if (nxt) {
-#pragma unroll
-        for (int h = 0; h < 4; ++h) issue(h, kt + 1);
-      }
-      if constexpr (!decltype(first)::value) wait_cnt(nxt ? 8 : 0);   // A-bot(kt), read in Q1
-      enter();   // Q0: A-top x B-left; B-right(kt) read beside it
-      rd_b(sb, br, 1, 0);
-      rd_b(sb, br, 1, 1);
-      sb0();
-      mf(0, bl, 0, 0);
-      mf(0, bl, 0, 1);
-      leave();
-      enter();   // Q1: A-top x B-right; A-bot(kt) read into the A registers half by half
-      mf(0, br, 1, 0);
-      sb0();
-      rd_a(sa, 1, 0);
-      sb0();
-      mf(0, br, 1, 1);
-      sb0();
-      rd_a(sa, 1, 1);
-      leave();
-      if (nxt) wait_cnt(4);   // A-top / B-left(kt+1), read in Q3; also retires the previous epilogue's stores
-      enter();   // Q2: A-bot x B-right
-      mf(1, br, 1, 0);
-      mf(1, br, 1, 1);
-      leave();
-      if (nxt) wait_cnt(2);   // B-right(kt+1), read in Q0(kt+1)
-      enter();   // Q3: A-bot x B-left; the next K-tile's A-top / B-left read half by half
-      mf(1, bl, 0, 0);
-      if (nxt) {
-        sb0();
-        rd_a(sa + dn, 0, 0);
-        rd_b(sb + dn, bl, 0, 0);
-        sb0();
-      }
-      mf(1, bl, 0, 1);
-      if (nxt) {
-        sb0();
-        rd_a(sa + dn, 0, 1);
-        rd_b(sb + dn, bl, 0, 1);
-      }
-      leave();
-    };
-    if constexpr (PIPE) {
-      ktileP(0, IC<1>{});
-      for (int kt = 1; kt < nk; ++kt) ktileP(kt, IC<0>{});
-    } else {
-      ktile(0, IC<1>{});
-      for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
-    }
+    ktile(0, IC<1>{});
+    for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
     if (wr == 0) __builtin_amdgcn_s_barrier();   // every wave is done reading both ring slots
     const int cm0 = m0, cn0 = n0;
     t += nwg;
@@ -1351,12 +1250,6 @@ bool nt_big_n256() {
   return v;
 }
 
-// XCP_NT_PIPE=1: the persistent kernel's pipelined fragment reads (read per call; A/B)
-bool nt_pipe() {
-  const char* e = getenv("XCP_NT_PIPE");
-  return e && e[0] == '1';
-}
-
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
   if (tile == 2 || tile == 3) return true;
@@ -1400,13 +1293,8 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
     if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
       const int grid = min(mb * gridN, cus);
-      const bool pipe = nt_pipe();
-      if (stats && pipe)
-        hipLaunchKernelGGL((gemm_nt256p_kernel<true, true>), dim3(grid), dim3(512), 0, stream, big);
-      else if (stats)
+      if (stats)
         hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
-      else if (pipe)
-        hipLaunchKernelGGL((gemm_nt256p_kernel<false, true>), dim3(grid), dim3(512), 0, stream, big);
       else
         hipLaunchKernelGGL(gemm_nt256p_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
     } else if (buf)

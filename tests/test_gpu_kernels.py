@@ -989,30 +989,6 @@ def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("M,N,K", [(92416, 736, 736), (5120 * 9, 1024, 736), (2048 * 7 + 256, 512, 64),
-                                   (256 * 506 + 77, 256, 200), (256 * 600 + 77, 256, 448), (256 * 300, 512, 128)])
-def test_gemm_nt_pipelined_reads_bitwise(ops, gpu, M, N, K, monkeypatch):
-    """The persistent kernel with its fragment reads pipelined into the previous phase (XCP_NT_PIPE=1 /
-    0) keeps every accumulator's MFMA order: identical output and statistics bits, with and without
-    the statistics epilogue, for one to twelve K-tiles (a K-tile count of 1 takes no prefetch)."""
-    g = torch.Generator(device=gpu).manual_seed(M + N + K)
-    A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
-    B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
-    R = ops.nt_stat_rows(M)
-    for stats in (True, False):
-        outs = []
-        for pipe in ("0", "1"):
-            monkeypatch.setenv("XCP_NT_PIPE", pipe)
-            C = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
-            part = torch.full((R, 2, N), float("nan"), device=gpu) if stats else None
-            ops.gemm_nt(A, B, C, M, N, K, stats=part, tile=3)
-            torch.cuda.synchronize()
-            outs.append((C, part))
-        assert torch.equal(outs[0][0], outs[1][0])
-        if stats:
-            assert torch.equal(outs[0][1], outs[1][1])
-
-
 def test_reduce_batch_bitwise(ops, gpu):
     """ReduceBatch (xcp_colreduce_multi: up to 16 reductions per launch, two-level jobs split over
     two launches) gives bitwise reduce_slabs' outputs, for one-level and two-level shapes, a slab
