@@ -111,26 +111,64 @@ def main():
 ROOF = (("gemm_nt256p_kernel", 131072), ("dw_fwd_w2_kernel", 1507328))
 
 
+def phase_of(rows):
+    """'fwd' / 'bwd' per dispatch: a step runs from one optimizer launch (opt_adam_kernel) to the
+    next; its backward starts at the first kernel on a stream other than the main one (the
+    weight-gradient side stream) -- dispatches of the step before that are the forward."""
+    order = sorted(range(len(rows)), key=lambda i: rows[i][1])
+    main = rows[order[0]][3] if rows else None
+    ph, cur = [None] * len(rows), "fwd"
+    for i in order:
+        name = rows[i][0]
+        if rows[i][3] != main and cur == "fwd":
+            cur = "bwd"
+        ph[i] = cur
+        if "opt_adam_kernel" in name:
+            cur = "fwd"
+    return ph
+
+
 def contention(path):
-    """Launches of the roofline kernels split by whether another stream ran a kernel during them
-    (the side-stream weight gradients of the backward): bench.py times the op's forward launches,
-    which never overlap one, so its live average is the 'alone' column here (plus, for the
-    pointwise GEMM, the op's second launch: the sparse last round on the 128x128 kernel)."""
+    """Launches of the roofline kernels split by step phase (forward: the pointwise GEMM with its
+    BN-statistics epilogue, the op bench.py times; backward: the input-gradient GEMM) and by whether
+    another stream ran a kernel during them (the side-stream weight gradients of the backward).  The
+    op bench.py times live is the forward launch plus, for the pointwise GEMM, the op's second launch:
+    the sparse last round on the 128x128 kernel (grid 61440 at the step shape), listed per phase too."""
     with open(path) as f:
         rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Stream_Id"),
                  int(r.get("Grid_Size_X") or 0)) for r in csv.DictReader(f)]
-    print("\nroofline kernels: launches alone on the GPU vs overlapping another stream's kernels")
-    for name, grid in ROOF:
-        sel = [r for r in rows if base(r[0]) == name and r[4] == grid]
-        for role in sorted({decode(r[0]) or name for r in sel}):
+    ph = phase_of(rows)
+    print("\nroofline kernels per step phase: launches alone on the GPU vs overlapping another stream's kernels")
+    for name, grid in ROOF + (("gemm_nt_kernel", 61440),):
+        for phase in ("fwd", "bwd"):
             alone, shared = [], []
-            for r in sel:
-                if (decode(r[0]) or name) != role:
+            for i, r in enumerate(rows):
+                if base(r[0]) != name or r[4] != grid or ph[i] != phase:
                     continue
                 ov = any(o[3] != r[3] and o[1] < r[2] and o[2] > r[1] for o in rows if o is not r)
                 (shared if ov else alone).append((r[2] - r[1]) / 1e3)
+            if not alone and not shared:
+                continue
             f = lambda v: f"{len(v):5d} x {sum(v) / len(v):7.1f} us" if v else "    0"   # noqa: E731
-            print(f"{role[:34]:34s} grid {grid:>8d}  all {f(alone + shared)}  alone {f(alone)}  overlapped {f(shared)}")
+            print(f"{name[:22]:22s} {phase} grid {grid:>8d}  all {f(alone + shared)}  alone {f(alone)}  "
+                  f"overlapped {f(shared)}")
+    # the op bench.py's "roofline" times: the middle-flow 728 x 728 pointwise GEMM with its BN statistics,
+    # i.e. a forward persistent launch that follows the 19^2 x 736 depthwise forward and is followed by
+    # the sparse last round (grid 61440) -- the persistent kernel's grid is 256 workgroups for every
+    # shape with >= 256 tiles, so the grid alone does not identify the op
+    seq = sorted([r for r in rows if r[3] == rows[0][3]], key=lambda r: r[1]) if rows else []
+    ops_ = []
+    for i in range(1, len(seq) - 1):
+        if (base(seq[i][0]) == "gemm_nt256p_kernel" and base(seq[i - 1][0]) == "dw_fwd_w2_kernel"
+                and seq[i - 1][4] == 1507328 and base(seq[i + 1][0]) == "gemm_nt_kernel" and seq[i + 1][4] == 61440):
+            ops_.append(((seq[i][2] - seq[i][1]) / 1e3, (seq[i + 1][2] - seq[i + 1][1]) / 1e3,
+                         (seq[i + 1][2] - seq[i][1]) / 1e3))
+    if ops_:
+        n = len(ops_)
+        m = [sum(o[k] for o in ops_) / n for k in range(3)]
+        print(f"middle-flow forward op (728 x 728 @19^2 + BN statistics): {n} x persistent {m[0]:.1f} us + "
+              f"sparse round {m[1]:.1f} us = {m[0] + m[1]:.1f} us of kernel time, {m[2]:.1f} us first start to "
+              f"last end (bench.py's live figure: HIP events around the op)")
 
 
 if __name__ == "__main__":
