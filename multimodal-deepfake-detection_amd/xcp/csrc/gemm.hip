@@ -1250,13 +1250,6 @@ bool nt_big_n256() {
   return v;
 }
 
-// XCP_NT_STAGES=3: the 128x128 bf16 NT kernel with a 3-stage LDS ring (two K-stages in flight) instead
-// of 2 (read per call; A/B)
-int nt_stages() {
-  const char* e = getenv("XCP_NT_STAGES");
-  return e && e[0] == '3' ? 3 : 2;
-}
-
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
   if (tile == 2 || tile == 3) return true;
@@ -1314,29 +1307,23 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
       rest.A = reinterpret_cast<const bf16*>(A) + (long)big.M * lda;
       rest.C = reinterpret_cast<bf16*>(C) + (long)big.M * ldc;
       if (stats) rest.stats = stats + (long)(big.M / 128) * 2 * N;
-      if (nt_stages() == 3)
-        hipLaunchKernelGGL((gemm_nt_kernel<bf16, 0, 2, 3>), dim3(xcp_cdiv(rest.M, 128) * xcp_cdiv(N, NBN)), dim3(256), 0,
-                           stream, rest);
-      else
-        hipLaunchKernelGGL((gemm_nt_kernel<bf16, 0, 2, 2>), dim3(xcp_cdiv(rest.M, 128) * xcp_cdiv(N, NBN)), dim3(256), 0,
-                           stream, rest);
+      hipLaunchKernelGGL((gemm_nt_kernel<bf16, 0, 2, 2>), dim3(xcp_cdiv(rest.M, 128) * xcp_cdiv(N, NBN)), dim3(256), 0,
+                         stream, rest);
     }
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(M, 128) * xcp_cdiv(N, NBN);
-#define XCP_NT_LAUNCH(TT, ST)                                                                                   \
+#define XCP_NT_LAUNCH(TT)                                                                                       \
   switch (gmode) {                                                                                              \
-    case 0: hipLaunchKernelGGL((gemm_nt_kernel<TT, 0, 2, ST>), dim3(grid), dim3(256), 0, stream, a); break;    \
-    case 1: hipLaunchKernelGGL((gemm_nt_kernel<TT, 1, 2, ST>), dim3(grid), dim3(256), 0, stream, a); break;    \
-    case 2: hipLaunchKernelGGL((gemm_nt_kernel<TT, 2, 2, ST>), dim3(grid), dim3(256), 0, stream, a); break;    \
-    default: hipLaunchKernelGGL((gemm_nt_kernel<TT, 3, 2, ST>), dim3(grid), dim3(256), 0, stream, a); break;   \
+    case 0: hipLaunchKernelGGL((gemm_nt_kernel<TT, 0, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;     \
+    case 1: hipLaunchKernelGGL((gemm_nt_kernel<TT, 1, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;     \
+    case 2: hipLaunchKernelGGL((gemm_nt_kernel<TT, 2, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;     \
+    default: hipLaunchKernelGGL((gemm_nt_kernel<TT, 3, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;    \
   }
-  if (dtype == XCP_BF16 && nt_stages() == 3) {
-    XCP_NT_LAUNCH(bf16, 3)
-  } else if (dtype == XCP_BF16) {
-    XCP_NT_LAUNCH(bf16, 2)
+  if (dtype == XCP_BF16) {
+    XCP_NT_LAUNCH(bf16)
   } else if (dtype == XCP_F32) {
-    XCP_NT_LAUNCH(float, 2)
+    XCP_NT_LAUNCH(float)
   } else {
     return XCP_EUNSUPPORTED;
   }

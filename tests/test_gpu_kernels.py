@@ -989,28 +989,6 @@ def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("M,N,K,tile", [(92416, 736, 736, 0), (5120, 736, 736, 1), (20000 + 77, 256, 200, 1),
-                                        (4096, 128, 64, 1)])
-def test_gemm_nt_three_stage_ring_bitwise(ops, gpu, M, N, K, tile, monkeypatch):
-    """The 128x128 NT kernel with a 3-stage LDS ring (XCP_NT_STAGES=3: two K-stages in flight; tile 0 at
-    the middle-flow shape runs it as the sparse last round of the persistent kernel) keeps the MFMA
-    order: identical output and statistics bits against the 2-stage ring."""
-    g = torch.Generator(device=gpu).manual_seed(M + N + K)
-    A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
-    B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
-    R = ops.nt_stat_rows(M)
-    outs = []
-    for st in ("2", "3"):
-        monkeypatch.setenv("XCP_NT_STAGES", st)
-        C = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
-        part = torch.full((R, 2, N), float("nan"), device=gpu)
-        ops.gemm_nt(A, B, C, M, N, K, stats=part, tile=tile)
-        torch.cuda.synchronize()
-        outs.append((C, part))
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
-
-
 def test_reduce_batch_bitwise(ops, gpu):
     """ReduceBatch (xcp_colreduce_multi: up to 16 reductions per launch, two-level jobs split over
     two launches) gives bitwise reduce_slabs' outputs, for one-level and two-level shapes, a slab
