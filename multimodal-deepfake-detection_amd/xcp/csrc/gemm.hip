@@ -1250,6 +1250,12 @@ bool nt_big_n256() {
   return v;
 }
 
+// XCP_NT_SPARSE=0: no sparse last round (every row on the persistent kernel; read per call; A/B)
+bool nt_sparse() {
+  const char* e = getenv("XCP_NT_SPARSE");
+  return !(e && e[0] == '0');
+}
+
 bool nt_big(int dtype, int gmode, int M, int N, int K, int tile) {
   if (dtype != XCP_BF16 || gmode != 0 || tile == 1) return false;
   if (tile == 2 || tile == 3) return true;
@@ -1285,7 +1291,7 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     const int gridN = xcp_cdiv(N, 256), gridM = xcp_cdiv(M, 256), tiles = gridM * gridN;
     const int cus = gpu_cus();
     int mb = gridM;
-    if ((tile == 0 || tile == 4) && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3)
+    if ((tile == 0 || tile == 4) && nt_sparse() && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3)
       mb = (tiles / cus) * cus / gridN;
     NTArgs big = a;
     big.M = min(M, mb * 256);

@@ -140,6 +140,21 @@ def main():
             Yk = torch.empty(m, Nn, device=dev, dtype=dt)
             rep(f"nt R=4 K={K}", timeit(lambda: ops.gemm_nt(Xk, Wk, Yk, m, Nn, K, tile=3)), flops=2.0 * m * Nn * K)
             del Xk, Wk, Yk
+    if "sparse" in sel:   # the step's persistent-kernel shapes: auto (tile 0: sparse last round on the 128x128
+        # kernel when the last round is < 3/4 full) against every row on the persistent kernel (tile 3)
+        for (m, n, k, stats) in ((1401856, 256, 128, True), (1401856, 256, 256, True), (350464, 736, 256, True),
+                                 (350464, 736, 736, True), (92416, 736, 736, True), (92416, 1024, 736, True),
+                                 (25600, 1536, 1024, True), (25600, 2048, 1536, True), (25600, 1024, 1536, False),
+                                 (25600, 1536, 2048, False), (92416, 736, 1024, False), (92416, 736, 736, False),
+                                 (350464, 736, 736, False), (350464, 256, 736, False)):
+            Xs = torch.randn(m, k, device=dev, generator=g).to(dt)
+            Ws = (torch.randn(n, k, device=dev, generator=g) / 27).to(dt)
+            Ys = torch.empty(m, n, device=dev, dtype=dt)
+            sts = torch.empty(ops.nt_stat_rows(m) * 2 * n, device=dev) if stats else None
+            for tile in (0, 3, 0, 3):
+                rep(f"nt {m}x{n}x{k} stats={int(stats)} tile {tile}",
+                    timeit(lambda: ops.gemm_nt(Xs, Ws, Ys, m, n, k, stats=sts, tile=tile)), flops=2.0 * m * n * k)
+            del Xs, Ws, Ys, sts
     if "dwf_only" in sel:     # one kernel for the PMC passes
         rep("dw_fwd act=2", timeit(lambda: ops.dw_fwd(2, X, Y, Wt, sc, sh, N, H, W, C)), 2 * tensor_bytes)
     if "dwb_only" in sel:
