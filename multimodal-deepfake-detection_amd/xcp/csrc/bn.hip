@@ -331,9 +331,12 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, in
   const int c = c0 + (lane & 31), stat = lane >> 5;
   // rows w, w + 16, ... in chunks of FIN_U: every load of a chunk is issued before the first is
   // added (clamped row, zero-selected past R), so a lane waits ceil(R / (16 FIN_U)) memory round
-  // trips, not one per 4 rows (723 partial rows of the middle flow: one; the same summation order
-  // as smaller chunks, so the same bits)
-  constexpr int FIN_U = 48;
+  // trips, not one per 4 rows (723 partial rows of the middle flow: two; the same summation order
+  // as any other chunk size, so the same bits).  32, not 48: the finalize kernels are held to 72
+  // VGPRs (launch bounds below) so that their 16-wave workgroup fits on a CU beside the side
+  // stream's stem conv2 weight gradient (8 waves x 104 VGPRs, 123 KB of LDS on every CU); at 108
+  // VGPRs BN1's backward finalize waited ~230 us for that kernel to leave the CUs
+  constexpr int FIN_U = 32;
   double a = 0.0;
   if (c < C) {
     const float* col = part + (long)stat * CP + c;
@@ -357,7 +360,7 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, in
   }
 }
 
-__global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C, int CP,
+__global__ __launch_bounds__(1024, 7) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C, int CP,
                                                                 double count, const float* gamma, const float* beta,
                                                                 float* rmean, float* rvar, float momentum, float eps,
                                                                 float* mean_o, float* invstd_o, float* scale_o,
@@ -388,7 +391,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __r
   shift_o[c] = beta[c] - (float)mean * sc;
 }
 
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_part_kernel(const float* __restrict__ part, int R, int C,
+__global__ __launch_bounds__(1024, 7) void bn_bwd_finalize_part_kernel(const float* __restrict__ part, int R, int C,
                                                                     int CP, double count, const float* gamma,
                                                                     const float* mean, const float* invstd,
                                                                     float* alpha, float* bcoef, float* delta,
