@@ -325,7 +325,6 @@ __global__ void bn_finalize_kernel(const double* __restrict__ part2, int G, int 
 // many loads stay in flight), the 16 waves fold in LDS, and 32 threads finalize.
 constexpr int FIN_CH = 32, FIN_WAVES = 16;
 
-template <int FIN_WAVES>
 XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, int c0, double (*red)[64], double& s0,
                         double& s1) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -358,8 +357,7 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, in
   }
 }
 
-template <int FIN_WAVES>
-__global__ __launch_bounds__(64 * FIN_WAVES) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C, int CP,
+__global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C, int CP,
                                                                 double count, const float* gamma, const float* beta,
                                                                 float* rmean, float* rvar, float momentum, float eps,
                                                                 float* mean_o, float* invstd_o, float* scale_o,
@@ -367,7 +365,7 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void bn_finalize_part_kernel(const 
   __shared__ double red[FIN_WAVES][64];
   const int c0 = blockIdx.x * FIN_CH;
   double s, q;
-  fin_reduce<FIN_WAVES>(part, R, C, CP, c0, red, s, q);
+  fin_reduce(part, R, C, CP, c0, red, s, q);
   const int c = c0 + threadIdx.x;
   if (threadIdx.x >= FIN_CH || c >= CP) return;
   if (c >= C) {   // padding channel
@@ -390,8 +388,7 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void bn_finalize_part_kernel(const 
   shift_o[c] = beta[c] - (float)mean * sc;
 }
 
-template <int FIN_WAVES>
-__global__ __launch_bounds__(64 * FIN_WAVES) void bn_bwd_finalize_part_kernel(const float* __restrict__ part, int R, int C,
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_part_kernel(const float* __restrict__ part, int R, int C,
                                                                     int CP, double count, const float* gamma,
                                                                     const float* mean, const float* invstd,
                                                                     float* alpha, float* bcoef, float* delta,
@@ -399,7 +396,7 @@ __global__ __launch_bounds__(64 * FIN_WAVES) void bn_bwd_finalize_part_kernel(co
   __shared__ double red[FIN_WAVES][64];
   const int c0 = blockIdx.x * FIN_CH;
   double sdz, sdzy;
-  fin_reduce<FIN_WAVES>(part, R, C, CP, c0, red, sdz, sdzy);
+  fin_reduce(part, R, C, CP, c0, red, sdz, sdzy);
   const int c = c0 + threadIdx.x;
   if (threadIdx.x >= FIN_CH || c >= CP) return;
   if (c >= C) {   // padding channel: its gradient stays zero
@@ -1004,22 +1001,13 @@ int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mea
   return XCP_EUNSUPPORTED;
 }
 
-// XCP_FIN4_SMALL=0: the stem BNs' backward finalize on 16-wave workgroups too (A/B)
-static bool fin4_small() {
-  static const bool v = [] {
-    const char* e = getenv("XCP_FIN4_SMALL");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 // BatchNorm finalize straight from fp32 partial rows part[R][2][C] (train mode)
 int xcp_bn_finalize_part(const float* part, int R, int C, int CP, double count, const float* gamma, const float* beta,
                          float* rmean, float* rvar, float momentum, float eps, float* mean_o, float* invstd_o,
                          float* scale_o, float* shift_o, hipStream_t st) {
   if (C <= 0) return XCP_OK;
   if (R <= 0 || CP < C) return XCP_EINVAL;
-  hipLaunchKernelGGL(bn_finalize_part_kernel<FIN_WAVES>, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part, R,
+  hipLaunchKernelGGL(bn_finalize_part_kernel, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part, R,
                      C, CP, count, gamma, beta, rmean, rvar, momentum, eps, mean_o, invstd_o, scale_o, shift_o);
   return (int)hipGetLastError();
 }
@@ -1029,16 +1017,8 @@ int xcp_bn_bwd_finalize_part(const float* part, int R, int C, int CP, double cou
                              float* dgamma, float* dbeta, int accumulate, hipStream_t st) {
   if (C <= 0) return XCP_OK;
   if (R <= 0 || CP < C) return XCP_EINVAL;
-  // The stem's BNs (CP <= 64: one or two workgroups) finalize with 4-wave workgroups: their backward runs
-  // while the side stream's stem conv2 weight gradient holds every CU (123 KB of LDS, 8 waves at 176
-  // allocated VGPRs), beside which a 16-wave workgroup does not fit and BN1's finalize waited ~210 us
-  // for that kernel to leave the CUs (profiles/r04_fin4_ab.txt)
-  if (CP <= 64 && fin4_small())
-    hipLaunchKernelGGL(bn_bwd_finalize_part_kernel<4>, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(256), 0, st, part, R, C,
-                       CP, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
-  else
-    hipLaunchKernelGGL(bn_bwd_finalize_part_kernel<FIN_WAVES>, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0,
-                       st, part, R, C, CP, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
+  hipLaunchKernelGGL(bn_bwd_finalize_part_kernel, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part,
+                     R, C, CP, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
   return (int)hipGetLastError();
 }
 
