@@ -161,6 +161,21 @@ XCP_DEV inline void store_as(int dtype, void* out, long o, float v) {
   else reinterpret_cast<float*>(out)[o] = v;
 }
 
+// four consecutive elements (o a multiple of 4): one 8-B (bf16) or 16-B (fp32) store, the same
+// per-element conversion as store_as
+XCP_DEV inline void store4_as(int dtype, void* out, long o, float4 v) {
+  if (dtype == XCP_BF16) {
+    bf16x4 q;
+    q[0] = (bf16)v.x;
+    q[1] = (bf16)v.y;
+    q[2] = (bf16)v.z;
+    q[3] = (bf16)v.w;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(out) + o) = q;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void permute3_batch_kernel(const long long* __restrict__ jobs, int njobs) {
   __shared__ float tile[32][33];
   const int b = blockIdx.x;
@@ -198,6 +213,29 @@ __global__ __launch_bounds__(256) void permute3_batch_kernel(const long long* __
   const int bb = lb / (ntr * ntc), rem = lb - bb * (ntr * ntc), tr = rem / ntc, tc = rem - tr * ntc;
   const float* src = in + bb * q.ib;
   const long obase = bb * q.ob;
+  // rows of 4-element groups (16-B loads, 8-B bf16 / 16-B fp32 stores) whenever the input row length,
+  // the output pitch and the tile's edge allow; per element otherwise
+  const bool vec = (q.Cc & 3) == 0 && (q.ors & 3) == 0 && (q.R & 3) == 0;
+  if (vec) {
+    const int t8 = threadIdx.x & 7, tr32 = threadIdx.x >> 3;   // 32 rows x 8 four-element groups
+    const int r = tr * 32 + tr32, c4 = tc * 32 + t8 * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < q.R && c4 < q.Cc) v = *reinterpret_cast<const float4*>(src + (long)r * q.Cc + c4);
+    if (q.mode == 0) {
+      if (r < q.R && c4 < q.Cc) store4_as(dtype, out, obase + r * q.ors + c4, v);
+      return;
+    }
+    tile[tr32][t8 * 4] = v.x;
+    tile[tr32][t8 * 4 + 1] = v.y;
+    tile[tr32][t8 * 4 + 2] = v.z;
+    tile[tr32][t8 * 4 + 3] = v.w;
+    __syncthreads();
+    const int oc = tc * 32 + tr32, orow4 = tr * 32 + t8 * 4;   // output row = input column
+    if (oc < q.Cc && orow4 < q.R)
+      store4_as(dtype, out, obase + oc * q.ors + orow4,
+                make_float4(tile[t8 * 4][tr32], tile[t8 * 4 + 1][tr32], tile[t8 * 4 + 2][tr32], tile[t8 * 4 + 3][tr32]));
+    return;
+  }
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int c = tc * 32 + tx;
   if (q.mode == 0) {

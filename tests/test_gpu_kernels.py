@@ -1026,7 +1026,9 @@ def test_permute_batch_plans(ops, gpu):
     specs = [((728, 728, 1), (0, 1, 2), 736, torch.bfloat16), ((728, 728, 1), (1, 0, 2), 736, torch.bfloat16),
              ((1024, 728, 1), (1, 0, 2), 1024, torch.bfloat16), ((736, 9, 1), (1, 0, 2), 736, torch.float32),
              ((64, 32, 9), (0, 2, 1), None, torch.bfloat16), ((64, 32, 9), (1, 2, 0), None, torch.bfloat16),
-             ((5, 7, 3), (2, 0, 1), None, torch.float32), ((33, 65, 1), (0, 1, 2), 72, torch.float32)]
+             ((5, 7, 3), (2, 0, 1), None, torch.float32), ((33, 65, 1), (0, 1, 2), 72, torch.float32),
+             ((100, 200, 1), (1, 0, 2), 104, torch.bfloat16), ((36, 44, 1), (0, 1, 2), 48, torch.float32),
+             ((36, 44, 1), (1, 0, 2), 40, torch.float32)]   # partial 32 x 32 tiles on the 4-element path
     jobs, want = [], []
     for (d0, d1, d2), pm, pitch, dt in specs:
         src = torch.randn(d0, d1, d2, device=gpu, generator=g)
