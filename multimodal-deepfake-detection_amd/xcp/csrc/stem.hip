@@ -467,6 +467,22 @@ XCP_DEV XRowChunks xrow_chunks(int tid, int IH, int IW, int P) {
   }
   return m;
 }
+// the two input rows 2 oh + 1, 2 oh + 2 of every channel (the third, 2 oh, is the previous output row's
+// 2 (oh - 1) + 2, kept in LDS): 6 x C4 chunks, at most 2 per thread (k = 2 unused)
+XCP_DEV XRowChunks xrow_chunks6(int tid, int IH, int IW, int P) {
+  const int C4 = (IW + 3) / 4;
+  XRowChunks m;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int e = tid + 256 * k, r6 = e / C4, j = e - r6 * C4;
+    const int col = min(4 * j, IW - 4);
+    const bool ok = k < 2 && r6 < 6;
+    const int c = r6 >> 1, dr = 1 + (r6 & 1);
+    m.off[k] = ok ? c * IH * IW + dr * IW + col : 0;
+    m.lds[k] = ok ? (c * 3 + dr) * P + col : -1;
+  }
+  return m;
+}
 XCP_DEV void xrow_fetch(const float* xb, const XRowChunks& m, f4a4 (&rx)[3]) {
 #pragma unroll
   for (int k = 0; k < 3; ++k) rx[k] = *reinterpret_cast<const f4a4*>(xb + m.off[k]);
@@ -521,21 +537,37 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
       wl[cb][i] = (bf16)(wv - (float)wb[cb][i]);
     }
   }
+  // Each workgroup walks a contiguous range of output rows: a row that continues the previous one in the
+  // same frame shares its first input row (2 oh = 2 (oh - 1) + 2) with it, so only the other two input
+  // rows of each channel are fetched (the input is read once instead of 1.5 times)
+  const XRowChunks xm6 = xrow_chunks6(tid, IH, IW, P);
+  const int chunk = (T + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t0 = blockIdx.x * chunk, t1 = min(T, t0 + chunk);
   f4a4 rx[3];
+  auto cont = [&](int t) { return t > t0 && t % OH != 0; };   // rows t - 1 and t of one frame in this range
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
-    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, xm, rx);
+    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, cont(t) ? xm6 : xm, rx);
   };
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
   bf16* sob = reinterpret_cast<bf16*>(so);
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const int npg = (OW + 15) / 16;
-  fetch(blockIdx.x);   // (the grid never exceeds the tile count)
-  for (int t = blockIdx.x; t < T; t += gridDim.x) {
+  if (t0 < t1) fetch(t0);
+  for (int t = t0; t < t1; ++t) {
     __syncthreads();   // the previous tile's LDS reads (input rows, output row) are done
-    xrow_store(sx, xm, rx);
+    if (cont(t)) {     // input row 2 oh: the previous tile's third row of each channel, slot 2 -> slot 0
+      for (int i = tid; i < 3 * IW; i += 256) {
+        const int c = i / IW, col = i - c * IW;
+        sx[(c * 3) * P + col] = sx[(c * 3 + 2) * P + col];
+      }
+      __syncthreads();
+      xrow_store(sx, xm6, rx);
+    } else {
+      xrow_store(sx, xm, rx);
+    }
     __syncthreads();
-    fetch(min(t + (int)gridDim.x, T - 1));
+    if (t + 1 < t1) fetch(t + 1);
     for (int g = w; g < npg; g += 4) {
       const int pa = min(g * 16 + l16, OW - 1);   // A row (clamped: rows past OW are not stored)
       float xv[8];
