@@ -686,12 +686,17 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     bok[h] = k < K1;
     boff[h] = bok[h] ? (k / 3) * P + k % 3 : 0;
   }
+  // contiguous output-row ranges, the shared input row kept in LDS (as conv1_fwd_row_kernel)
+  const XRowChunks xm6 = xrow_chunks6(tid, IH, IW, P);
+  const int chunk = (T + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t0 = blockIdx.x * chunk, t1 = min(T, t0 + chunk);
+  auto cont = [&](int t) { return t > t0 && t % OH != 0; };
   f4a4 rx[3];
   u32x4 rd[W1R_DL], ry[BN ? W1R_DL : 1];
   // operands of tile t (always a valid tile: loads are unconditional, from clamped addresses)
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
-    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, xm, rx);
+    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, cont(t) ? xm6 : xm, rx);
     const long db = ((long)n * OH + oh) * OW * C1;
 #pragma unroll
     for (int i = 0; i < W1R_DL; ++i) {
@@ -709,10 +714,19 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
   const char* syc = reinterpret_cast<const char*>(sy);
   const int q = l16 >> 2, pp = l16 & 3;   // transposed read: lane 4q + pp addresses pixel row q, channels 4pp..4pp+3
   const int ngr = (OW + 31) / 32;
-  fetch(blockIdx.x);   // (the grid never exceeds the tile count)
-  for (int t = blockIdx.x; t < T; t += gridDim.x) {
+  if (t0 < t1) fetch(t0);
+  for (int t = t0; t < t1; ++t) {
     __syncthreads();   // the previous tile's LDS reads are done
-    xrow_store(sx, xm, rx);
+    if (cont(t)) {     // input row 2 oh: the previous tile's third row of each channel, slot 2 -> slot 0
+      for (int i = tid; i < 3 * IW; i += 256) {
+        const int c = i / IW, col = i - c * IW;
+        sx[(c * 3) * P + col] = sx[(c * 3 + 2) * P + col];
+      }
+      __syncthreads();
+      xrow_store(sx, xm6, rx);
+    } else {
+      xrow_store(sx, xm, rx);
+    }
     static_assert(W1R_DL == 3, "the chunk stores below are written out for three chunks per thread");
     auto put = [&](int i, const u32x4& v, const u32x4& wv) {
       if (tid + 256 * i < nch) {
@@ -724,7 +738,7 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     put(1, rd[1], ry[BN ? 1 : 0]);
     put(2, rd[2], ry[BN ? 2 : 0]);
     __syncthreads();
-    fetch(min(t + (int)gridDim.x, T - 1));   // next tile (the last tile once more past the end)
+    if (t + 1 < t1) fetch(t + 1);   // next tile
     for (int g = w; g < ngr; g += 4) {
       const int p0 = 32 * g + 8 * kq;   // this lane's 8 pixels: A columns, B rows
       bf16x8 a[2], b[2], bl[2];
