@@ -441,6 +441,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_tile_kernel(const float* __re
 constexpr int W1R_IW = 320;                          // widest frame: 9 input rows of pitch 320 floats
 constexpr int W1R_OW = (W1R_IW - 3) / 2 + 1;         // 159 output pixels -> 636 16-B chunks per row
 constexpr int W1R_OWM = W1R_OW;
+constexpr int W1R_G = 4;   // consecutive output rows per group of the conv1 row kernels' walk
 constexpr int W1R_DL = (W1R_OW * 4 + 255) / 256;     // 16-B output(-gradient) chunks per thread and tile (3)
 
 // The nine stride-2 input rows (3 channels x 3 kernel rows) of one output row, fetched as 16-B
@@ -537,14 +538,17 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
       wl[cb][i] = (bf16)(wv - (float)wb[cb][i]);
     }
   }
-  // Each workgroup walks a contiguous range of output rows: a row that continues the previous one in the
-  // same frame shares its first input row (2 oh = 2 (oh - 1) + 2) with it, so only the other two input
-  // rows of each channel are fetched (the input is read once instead of 1.5 times)
+  // Each workgroup walks groups of W1R_G consecutive output rows (group g = blockIdx.x + k gridDim.x, so the
+  // groups in flight are consecutive: a contiguous range per workgroup put all workgroups' streams a fixed
+  // stride apart and ran 3.6x slower); a row that continues the previous one of its group in the same frame
+  // shares its first input row (2 oh = 2 (oh - 1) + 2) with it, so only the other two input rows of each
+  // channel are fetched
   const XRowChunks xm6 = xrow_chunks6(tid, IH, IW, P);
-  const int chunk = (T + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int t0 = blockIdx.x * chunk, t1 = min(T, t0 + chunk);
   f4a4 rx[3];
-  auto cont = [&](int t) { return t > t0 && t % OH != 0; };   // rows t - 1 and t of one frame in this range
+  auto cont = [&](int t) { return t % W1R_G != 0 && t % OH != 0; };   // rows t - 1 and t of one group and frame
+  auto next_tile = [&](int t) {   // the tile after t in this workgroup's walk (>= T: none)
+    return (t + 1) % W1R_G != 0 && t + 1 < T ? t + 1 : (t / W1R_G + (int)gridDim.x) * W1R_G;
+  };
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
     xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, cont(t) ? xm6 : xm, rx);
@@ -553,8 +557,8 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
   bf16* sob = reinterpret_cast<bf16*>(so);
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const int npg = (OW + 15) / 16;
-  if (t0 < t1) fetch(t0);
-  for (int t = t0; t < t1; ++t) {
+  if ((int)blockIdx.x * W1R_G < T) fetch(blockIdx.x * W1R_G);
+  for (int t = blockIdx.x * W1R_G; t < T; t = next_tile(t)) {
     __syncthreads();   // the previous tile's LDS reads (input rows, output row) are done
     if (cont(t)) {     // input row 2 oh: the previous tile's third row of each channel, slot 2 -> slot 0
       for (int i = tid; i < 3 * IW; i += 256) {
@@ -567,7 +571,7 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
       xrow_store(sx, xm, rx);
     }
     __syncthreads();
-    if (t + 1 < t1) fetch(t + 1);
+    if (next_tile(t) < T) fetch(next_tile(t));
     for (int g = w; g < npg; g += 4) {
       const int pa = min(g * 16 + l16, OW - 1);   // A row (clamped: rows past OW are not stored)
       float xv[8];
@@ -686,11 +690,12 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     bok[h] = k < K1;
     boff[h] = bok[h] ? (k / 3) * P + k % 3 : 0;
   }
-  // contiguous output-row ranges, the shared input row kept in LDS (as conv1_fwd_row_kernel)
+  // groups of W1R_G consecutive output rows, the shared input row kept in LDS (as conv1_fwd_row_kernel)
   const XRowChunks xm6 = xrow_chunks6(tid, IH, IW, P);
-  const int chunk = (T + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int t0 = blockIdx.x * chunk, t1 = min(T, t0 + chunk);
-  auto cont = [&](int t) { return t > t0 && t % OH != 0; };
+  auto cont = [&](int t) { return t % W1R_G != 0 && t % OH != 0; };
+  auto next_tile = [&](int t) {
+    return (t + 1) % W1R_G != 0 && t + 1 < T ? t + 1 : (t / W1R_G + (int)gridDim.x) * W1R_G;
+  };
   f4a4 rx[3];
   u32x4 rd[W1R_DL], ry[BN ? W1R_DL : 1];
   // operands of tile t (always a valid tile: loads are unconditional, from clamped addresses)
@@ -714,8 +719,8 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
   const char* syc = reinterpret_cast<const char*>(sy);
   const int q = l16 >> 2, pp = l16 & 3;   // transposed read: lane 4q + pp addresses pixel row q, channels 4pp..4pp+3
   const int ngr = (OW + 31) / 32;
-  if (t0 < t1) fetch(t0);
-  for (int t = t0; t < t1; ++t) {
+  if ((int)blockIdx.x * W1R_G < T) fetch(blockIdx.x * W1R_G);
+  for (int t = blockIdx.x * W1R_G; t < T; t = next_tile(t)) {
     __syncthreads();   // the previous tile's LDS reads are done
     if (cont(t)) {     // input row 2 oh: the previous tile's third row of each channel, slot 2 -> slot 0
       for (int i = tid; i < 3 * IW; i += 256) {
@@ -738,7 +743,7 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     put(1, rd[1], ry[BN ? 1 : 0]);
     put(2, rd[2], ry[BN ? 2 : 0]);
     __syncthreads();
-    if (t + 1 < t1) fetch(t + 1);   // next tile
+    if (next_tile(t) < T) fetch(next_tile(t));   // next tile
     for (int g = w; g < ngr; g += 4) {
       const int p0 = 32 * g + 8 * kq;   // this lane's 8 pixels: A columns, B rows
       bf16x8 a[2], b[2], bl[2];
