@@ -544,6 +544,8 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
   // shares its first input row (2 oh = 2 (oh - 1) + 2) with it, so only the other two input rows of each
   // channel are fetched
   const XRowChunks xm6 = xrow_chunks6(tid, IH, IW, P);
+  const int xo0 = xm.off[0], xo1 = xm.off[1], xo2 = xm.off[2], xl0 = xm.lds[0], xl1 = xm.lds[1], xl2 = xm.lds[2];
+  const int yo0 = xm6.off[0], yo1 = xm6.off[1], yl0 = xm6.lds[0], yl1 = xm6.lds[1];
   f4a4 rx[3];
   auto cont = [&](int t) { return t % W1R_G != 0 && t % OH != 0; };   // rows t - 1 and t of one group and frame
   auto next_tile = [&](int t) {   // the tile after t in this workgroup's walk (>= T: none)
@@ -551,7 +553,11 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
   };
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
-    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, cont(t) ? xm6 : xm, rx);
+    const float* xb = X + (long)n * 3 * fsz + (long)(2 * oh) * IW;
+    const bool c6 = cont(t);   // (scalar selects: selecting between the two maps put them in scratch)
+    rx[0] = *reinterpret_cast<const f4a4*>(xb + (c6 ? yo0 : xo0));
+    rx[1] = *reinterpret_cast<const f4a4*>(xb + (c6 ? yo1 : xo1));
+    rx[2] = *reinterpret_cast<const f4a4*>(xb + xo2);
   };
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
   bf16* sob = reinterpret_cast<bf16*>(so);
@@ -566,9 +572,22 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
         sx[(c * 3) * P + col] = sx[(c * 3 + 2) * P + col];
       }
       __syncthreads();
-      xrow_store(sx, xm6, rx);
-    } else {
-      xrow_store(sx, xm, rx);
+    }
+    {
+      const bool c6 = cont(t);
+      const int l0 = c6 ? yl0 : xl0, l1 = c6 ? yl1 : xl1, l2 = c6 ? -1 : xl2;
+      if (l0 >= 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sx[l0 + i] = rx[0][i];
+      }
+      if (l1 >= 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sx[l1 + i] = rx[1][i];
+      }
+      if (l2 >= 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sx[l2 + i] = rx[2][i];
+      }
     }
     __syncthreads();
     if (next_tile(t) < T) fetch(next_tile(t));
@@ -692,6 +711,8 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
   }
   // groups of W1R_G consecutive output rows, the shared input row kept in LDS (as conv1_fwd_row_kernel)
   const XRowChunks xm6 = xrow_chunks6(tid, IH, IW, P);
+  const int xo0 = xm.off[0], xo1 = xm.off[1], xo2 = xm.off[2], xl0 = xm.lds[0], xl1 = xm.lds[1], xl2 = xm.lds[2];
+  const int yo0 = xm6.off[0], yo1 = xm6.off[1], yl0 = xm6.lds[0], yl1 = xm6.lds[1];
   auto cont = [&](int t) { return t % W1R_G != 0 && t % OH != 0; };
   auto next_tile = [&](int t) {
     return (t + 1) % W1R_G != 0 && t + 1 < T ? t + 1 : (t / W1R_G + (int)gridDim.x) * W1R_G;
@@ -701,7 +722,11 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
   // operands of tile t (always a valid tile: loads are unconditional, from clamped addresses)
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
-    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, cont(t) ? xm6 : xm, rx);
+    const float* xb = X + (long)n * 3 * fsz + (long)(2 * oh) * IW;
+    const bool c6 = cont(t);   // (scalar selects: selecting between the two maps put them in scratch)
+    rx[0] = *reinterpret_cast<const f4a4*>(xb + (c6 ? yo0 : xo0));
+    rx[1] = *reinterpret_cast<const f4a4*>(xb + (c6 ? yo1 : xo1));
+    rx[2] = *reinterpret_cast<const f4a4*>(xb + xo2);
     const long db = ((long)n * OH + oh) * OW * C1;
 #pragma unroll
     for (int i = 0; i < W1R_DL; ++i) {
@@ -728,9 +753,22 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
         sx[(c * 3) * P + col] = sx[(c * 3 + 2) * P + col];
       }
       __syncthreads();
-      xrow_store(sx, xm6, rx);
-    } else {
-      xrow_store(sx, xm, rx);
+    }
+    {
+      const bool c6 = cont(t);
+      const int l0 = c6 ? yl0 : xl0, l1 = c6 ? yl1 : xl1, l2 = c6 ? -1 : xl2;
+      if (l0 >= 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sx[l0 + i] = rx[0][i];
+      }
+      if (l1 >= 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sx[l1 + i] = rx[1][i];
+      }
+      if (l2 >= 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sx[l2 + i] = rx[2][i];
+      }
     }
     static_assert(W1R_DL == 3, "the chunk stores below are written out for three chunks per thread");
     auto put = [&](int i, const u32x4& v, const u32x4& wv) {
