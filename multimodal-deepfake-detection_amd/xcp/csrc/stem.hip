@@ -441,7 +441,6 @@ __global__ __launch_bounds__(256) void conv1_wgrad_tile_kernel(const float* __re
 constexpr int W1R_IW = 320;                          // widest frame: 9 input rows of pitch 320 floats
 constexpr int W1R_OW = (W1R_IW - 3) / 2 + 1;         // 159 output pixels -> 636 16-B chunks per row
 constexpr int W1R_OWM = W1R_OW;
-constexpr int W1R_G = 4;   // consecutive output rows per group of the conv1 row kernels' walk
 constexpr int W1R_DL = (W1R_OW * 4 + 255) / 256;     // 16-B output(-gradient) chunks per thread and tile (3)
 
 // The nine stride-2 input rows (3 channels x 3 kernel rows) of one output row, fetched as 16-B
@@ -465,22 +464,6 @@ XCP_DEV XRowChunks xrow_chunks(int tid, int IH, int IW, int P) {
     const bool ok = r < 9;
     m.off[k] = ok ? (r / 3) * IH * IW + (r % 3) * IW + col : 0;
     m.lds[k] = ok ? r * P + col : -1;
-  }
-  return m;
-}
-// the two input rows 2 oh + 1, 2 oh + 2 of every channel (the third, 2 oh, is the previous output row's
-// 2 (oh - 1) + 2, kept in LDS): 6 x C4 chunks, at most 2 per thread (k = 2 unused)
-XCP_DEV XRowChunks xrow_chunks6(int tid, int IH, int IW, int P) {
-  const int C4 = (IW + 3) / 4;
-  XRowChunks m;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    const int e = tid + 256 * k, r6 = e / C4, j = e - r6 * C4;
-    const int col = min(4 * j, IW - 4);
-    const bool ok = k < 2 && r6 < 6;
-    const int c = r6 >> 1, dr = 1 + (r6 & 1);
-    m.off[k] = ok ? c * IH * IW + dr * IW + col : 0;
-    m.lds[k] = ok ? (c * 3 + dr) * P + col : -1;
   }
   return m;
 }
@@ -538,59 +521,21 @@ __global__ __launch_bounds__(256, 4) void conv1_fwd_row_kernel(const float* __re
       wl[cb][i] = (bf16)(wv - (float)wb[cb][i]);
     }
   }
-  // Each workgroup walks groups of W1R_G consecutive output rows (group g = blockIdx.x + k gridDim.x, so the
-  // groups in flight are consecutive: a contiguous range per workgroup put all workgroups' streams a fixed
-  // stride apart and ran 3.6x slower); a row that continues the previous one of its group in the same frame
-  // shares its first input row (2 oh = 2 (oh - 1) + 2) with it, so only the other two input rows of each
-  // channel are fetched
-  const XRowChunks xm6 = xrow_chunks6(tid, IH, IW, P);
-  const int xo0 = xm.off[0], xo1 = xm.off[1], xo2 = xm.off[2], xl0 = xm.lds[0], xl1 = xm.lds[1], xl2 = xm.lds[2];
-  const int yo0 = xm6.off[0], yo1 = xm6.off[1], yl0 = xm6.lds[0], yl1 = xm6.lds[1];
   f4a4 rx[3];
-  auto cont = [&](int t) { return t % W1R_G != 0 && t % OH != 0; };   // rows t - 1 and t of one group and frame
-  auto next_tile = [&](int t) {   // the tile after t in this workgroup's walk (>= T: none)
-    return (t + 1) % W1R_G != 0 && t + 1 < T ? t + 1 : (t / W1R_G + (int)gridDim.x) * W1R_G;
-  };
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
-    const float* xb = X + (long)n * 3 * fsz + (long)(2 * oh) * IW;
-    const bool c6 = cont(t);   // (scalar selects: selecting between the two maps put them in scratch)
-    rx[0] = *reinterpret_cast<const f4a4*>(xb + (c6 ? yo0 : xo0));
-    rx[1] = *reinterpret_cast<const f4a4*>(xb + (c6 ? yo1 : xo1));
-    rx[2] = *reinterpret_cast<const f4a4*>(xb + xo2);
+    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, xm, rx);
   };
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
   bf16* sob = reinterpret_cast<bf16*>(so);
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const int npg = (OW + 15) / 16;
-  if ((int)blockIdx.x * W1R_G < T) fetch(blockIdx.x * W1R_G);
-  for (int t = blockIdx.x * W1R_G; t < T; t = next_tile(t)) {
+  fetch(blockIdx.x);   // (the grid never exceeds the tile count)
+  for (int t = blockIdx.x; t < T; t += gridDim.x) {
     __syncthreads();   // the previous tile's LDS reads (input rows, output row) are done
-    if (cont(t)) {     // input row 2 oh: the previous tile's third row of each channel, slot 2 -> slot 0
-      for (int i = tid; i < 3 * IW; i += 256) {
-        const int c = i / IW, col = i - c * IW;
-        sx[(c * 3) * P + col] = sx[(c * 3 + 2) * P + col];
-      }
-      __syncthreads();
-    }
-    {
-      const bool c6 = cont(t);
-      const int l0 = c6 ? yl0 : xl0, l1 = c6 ? yl1 : xl1, l2 = c6 ? -1 : xl2;
-      if (l0 >= 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sx[l0 + i] = rx[0][i];
-      }
-      if (l1 >= 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sx[l1 + i] = rx[1][i];
-      }
-      if (l2 >= 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sx[l2 + i] = rx[2][i];
-      }
-    }
+    xrow_store(sx, xm, rx);
     __syncthreads();
-    if (next_tile(t) < T) fetch(next_tile(t));
+    fetch(min(t + (int)gridDim.x, T - 1));
     for (int g = w; g < npg; g += 4) {
       const int pa = min(g * 16 + l16, OW - 1);   // A row (clamped: rows past OW are not stored)
       float xv[8];
@@ -709,24 +654,12 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     bok[h] = k < K1;
     boff[h] = bok[h] ? (k / 3) * P + k % 3 : 0;
   }
-  // groups of W1R_G consecutive output rows, the shared input row kept in LDS (as conv1_fwd_row_kernel)
-  const XRowChunks xm6 = xrow_chunks6(tid, IH, IW, P);
-  const int xo0 = xm.off[0], xo1 = xm.off[1], xo2 = xm.off[2], xl0 = xm.lds[0], xl1 = xm.lds[1], xl2 = xm.lds[2];
-  const int yo0 = xm6.off[0], yo1 = xm6.off[1], yl0 = xm6.lds[0], yl1 = xm6.lds[1];
-  auto cont = [&](int t) { return t % W1R_G != 0 && t % OH != 0; };
-  auto next_tile = [&](int t) {
-    return (t + 1) % W1R_G != 0 && t + 1 < T ? t + 1 : (t / W1R_G + (int)gridDim.x) * W1R_G;
-  };
   f4a4 rx[3];
   u32x4 rd[W1R_DL], ry[BN ? W1R_DL : 1];
   // operands of tile t (always a valid tile: loads are unconditional, from clamped addresses)
   auto fetch = [&](int t) {
     const int n = t / OH, oh = t - n * OH;
-    const float* xb = X + (long)n * 3 * fsz + (long)(2 * oh) * IW;
-    const bool c6 = cont(t);   // (scalar selects: selecting between the two maps put them in scratch)
-    rx[0] = *reinterpret_cast<const f4a4*>(xb + (c6 ? yo0 : xo0));
-    rx[1] = *reinterpret_cast<const f4a4*>(xb + (c6 ? yo1 : xo1));
-    rx[2] = *reinterpret_cast<const f4a4*>(xb + xo2);
+    xrow_fetch(X + (long)n * 3 * fsz + (long)(2 * oh) * IW, xm, rx);
     const long db = ((long)n * OH + oh) * OW * C1;
 #pragma unroll
     for (int i = 0; i < W1R_DL; ++i) {
@@ -744,32 +677,10 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
   const char* syc = reinterpret_cast<const char*>(sy);
   const int q = l16 >> 2, pp = l16 & 3;   // transposed read: lane 4q + pp addresses pixel row q, channels 4pp..4pp+3
   const int ngr = (OW + 31) / 32;
-  if ((int)blockIdx.x * W1R_G < T) fetch(blockIdx.x * W1R_G);
-  for (int t = blockIdx.x * W1R_G; t < T; t = next_tile(t)) {
+  fetch(blockIdx.x);   // (the grid never exceeds the tile count)
+  for (int t = blockIdx.x; t < T; t += gridDim.x) {
     __syncthreads();   // the previous tile's LDS reads are done
-    if (cont(t)) {     // input row 2 oh: the previous tile's third row of each channel, slot 2 -> slot 0
-      for (int i = tid; i < 3 * IW; i += 256) {
-        const int c = i / IW, col = i - c * IW;
-        sx[(c * 3) * P + col] = sx[(c * 3 + 2) * P + col];
-      }
-      __syncthreads();
-    }
-    {
-      const bool c6 = cont(t);
-      const int l0 = c6 ? yl0 : xl0, l1 = c6 ? yl1 : xl1, l2 = c6 ? -1 : xl2;
-      if (l0 >= 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sx[l0 + i] = rx[0][i];
-      }
-      if (l1 >= 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sx[l1 + i] = rx[1][i];
-      }
-      if (l2 >= 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sx[l2 + i] = rx[2][i];
-      }
-    }
+    xrow_store(sx, xm, rx);
     static_assert(W1R_DL == 3, "the chunk stores below are written out for three chunks per thread");
     auto put = [&](int i, const u32x4& v, const u32x4& wv) {
       if (tid + 256 * i < nch) {
@@ -781,7 +692,7 @@ __global__ __launch_bounds__(256, 3) void conv1_wgrad_row_kernel(const float* __
     put(1, rd[1], ry[BN ? 1 : 0]);
     put(2, rd[2], ry[BN ? 2 : 0]);
     __syncthreads();
-    if (next_tile(t) < T) fetch(next_tile(t));   // next tile
+    fetch(min(t + (int)gridDim.x, T - 1));   // next tile (the last tile once more past the end)
     for (int g = w; g < ngr; g += 4) {
       const int p0 = 32 * g + 8 * kq;   // this lane's 8 pixels: A columns, B rows
       bf16x8 a[2], b[2], bl[2];
