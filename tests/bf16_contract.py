@@ -24,12 +24,12 @@ summation-order change of the stem, block4.rep.8.weight 0.0551 against 0.0534). 
 the autocast scale to +-15 %, the median of 3 engine draws has a tail P(> t) ~ 3 P(|Z| > t)^2, and at
 K_RMS = 6 a parameter fails by chance with probability < 1e-6 at RHO = 1, 7.5e-6 at 1.5, 3.5e-4 at 2
 (R = 24), and 2.5e-6 / 1.4e-4 / 1.5e-3 with the bench size's R_AUTO_LARGE = 12; the measured RHO is
-0.95-1.44 (profiles/r04_bf16_rho.txt), i.e. family-wise well under 1 %, while an error many times the
+0.69-1.44 over the round-4 runs (profiles/r04_bf16_rho.txt, r04_stem_conv1_split.txt), i.e. family-wise well under 1 %, while an error many times the
 noise -- a defect -- still fails.
 
 How much noisier the engine is, is measured, not assumed: RHO = sqrt(mean_p median_j(err_xcp)^2 /
 rms_r(err_autocast)^2 / MED3_M2) pools every parameter above a floor (a tight estimate: ~150
-ratios), and is asserted <= RHO_MAX.  (Measured 0.95-1.44: the engine is about as noisy as autocast although it keeps
+ratios), and is asserted <= RHO_MAX.  (Measured 0.69-1.44: the engine is about as noisy as autocast although it keeps
 the residual stream -- block outputs and their gradients -- in bf16, where autocast's stays in fp32.)
 
 The realizations are decorrelated without changing the answer: the input clip is scaled by c and
