@@ -294,13 +294,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __res
   char* gs = smem;
   char* as = smem + 3 * WG_GSLOT;
   const int OH = IH - 2, OW = IW - 2;
+  const int n = blockIdx.x / nb, band = blockIdx.x - n * nb;
+  const int r0 = band * RB, r1 = min(OH, r0 + RB);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
   const int wsc = __builtin_amdgcn_readfirstlane(w);
-  // jobs (frame, band) = blockIdx.x, + gridDim.x, ...: one per workgroup at the default grid; a smaller
-  // grid (XCP_CONV3_WGRAD_WGS) sums several into one slab and leaves CUs to the other stream
-  const bf16* Gn = dY;
-  const bf16* Xn = X;
-  int r0 = 0, r1 = 0;
+  const bf16* Gn = dY + (long)n * OH * OW * 64;
+  const bf16* Xn = X + (long)n * IH * IW * 32;
   auto dma = [](const void* src, char* dst) {
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                      (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
@@ -325,6 +324,16 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __res
       else a_instr(oh + 2, j - WG_GI);
     }
   };
+  if (r0 >= r1) return;   // uniform
+  // prologue: dY row r0 and X rows r0, r0 + 1, r0 + 2 (56 instructions, 7 per wave), then step r0 + 1
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int j = wsc * 7 + i;
+    if (j < WG_GI) g_instr(r0, j);
+    else a_instr(r0 + (j - WG_GI) / WG_AI, (j - WG_GI) % WG_AI);
+  }
+  if (r0 + 1 < r1) issue_step(r0 + 1);
+
   const int cb = wsc >> 1, bb = wsc & 1;   // co block (16), ci block (16)
   const int q4 = fr >> 2, p4 = fr & 3;
   // per-lane byte offsets inside a slot: dY fragment rows 4fg + q4 (+16), columns 16cb + 4p4;
@@ -334,22 +343,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __res
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nch = (OW + 31) / 32;
-  for (int job = blockIdx.x; job < N * nb; job += gridDim.x) {
-  const int n = job / nb, band = job - n * nb;
-  r0 = band * RB;
-  r1 = min(OH, r0 + RB);
-  Gn = dY + (long)n * OH * OW * 64;
-  Xn = X + (long)n * IH * IW * 32;
-  if (r0 >= r1) continue;   // uniform
-  lds_barrier();   // every wave is done reading the previous job's ring slots
-  // prologue: dY row r0 and X rows r0, r0 + 1, r0 + 2 (56 instructions, 7 per wave), then step r0 + 1
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const int j = wsc * 7 + i;
-    if (j < WG_GI) g_instr(r0, j);
-    else a_instr(r0 + (j - WG_GI) / WG_AI, (j - WG_GI) % WG_AI);
-  }
-  if (r0 + 1 < r1) issue_step(r0 + 1);
   for (int oh = r0; oh < r1; ++oh) {
     if (oh + 1 < r1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -383,7 +376,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __res
       for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[t], acc[t], 0, 0, 0);
     }
   }
-  }   // job
   // acc[t][r] = dW[co = 16cb + 4fg + r][tap t][ci = 16bb + fr]
   float* Pb = P + (long)blockIdx.x * 64 * 288;
 #pragma unroll
@@ -418,14 +410,6 @@ int conv3_cus() {
     return n > 0 ? n : 256;
   }();
   return cus;
-}
-
-// workgroups of the weight gradient for `jobs` (frame, band) jobs: all of them (one job each) unless
-// XCP_CONV3_WGRAD_WGS=<n> caps the grid (read per call; A/B: fewer CUs held beside the main stream)
-int conv3_wgrad_grid(int jobs) {
-  const char* e = getenv("XCP_CONV3_WGRAD_WGS");
-  const int v = e ? atoi(e) : 0;
-  return v > 0 && v < jobs ? v : jobs;
 }
 
 // weight-gradient grid: bands of output rows per frame, about one workgroup per CU and
@@ -489,7 +473,7 @@ int xcp_conv3x3_wgrad_parts(int N, int IH, int IW) {
   if (N <= 0 || IH < 3 || IW < 3 || IW - 2 > WG_GPX) return 0;
   int nb, rb;
   wgrad_bands(N, IH - 2, nb, rb);
-  return conv3_wgrad_grid(N * nb);
+  return N * nb;
 }
 
 // P[parts][64][9 * 32] (fp32 slabs, sum them for dW[co][tap][ci]) = weight gradient of
@@ -500,7 +484,7 @@ int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, in
   if (IW - 2 > WG_GPX) return XCP_EUNSUPPORTED;
   int nb, rb;
   wgrad_bands(N, IH - 2, nb, rb);
-  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(conv3_wgrad_grid(N * nb)), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N, IH, IW,
+  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N, IH, IW,
                      nb, rb);
   return (int)hipGetLastError();
 }
