@@ -131,6 +131,15 @@ class Xception(nn.Module):
                 m.bias.data.zero_()
         self._xcp_engines = {}
         self._xcp_grad_sink = None   # xcp.ddp.GradBuckets(module=...) registers itself here
+        self._xcp_buffer_wait = None   # xcp.ddp.broadcast_buffers' completion event (async form)
+
+    def _xcp_wait_buffers(self):
+        """Make the current stream wait for a pending buffer broadcast (xcp.ddp.broadcast_buffers),
+        once: called where the forward first touches a BatchNorm running statistic."""
+        ev = getattr(self, "_xcp_buffer_wait", None)
+        if ev is not None:
+            self._xcp_buffer_wait = None
+            torch.cuda.current_stream(self.conv1.weight.device).wait_event(ev)
 
     def _engine(self):
         from xcp import compute_dtype
@@ -152,6 +161,7 @@ class Xception(nn.Module):
         r = super()._replicate_for_data_parallel()
         r._xcp_engines = {}
         r._xcp_grad_sink = None
+        r._xcp_buffer_wait = None
         return r
 
     def features(self, x):
@@ -177,6 +187,7 @@ class Xception(nn.Module):
     def forward_modules(self, x):
         """Xception.forward as the reference composes it (Xception.py:167-201), each sub-module on
         the xcp custom ops.  Returns fp32 features through ``fc``."""
+        self._xcp_wait_buffers()
         x = self.conv1(x)
         x = self.bn1(x)
         x = self.relu(x)
@@ -204,6 +215,7 @@ class Xception(nn.Module):
         d = self.__dict__.copy()
         d["_xcp_engines"] = {}
         d["_xcp_grad_sink"] = None
+        d["_xcp_buffer_wait"] = None
         return d
 
 

@@ -11,8 +11,17 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = DEFAULT_LIB_PATH = os.path.join(_HERE, "libxcp.so")
 # XCP_LIB_PATH: load another build of the same ABI instead (A/B of a kernel change in the step;
-# tools/build_variant.py links one)
-LIB_PATH = os.environ.get("XCP_LIB_PATH") or LIB_PATH
+# tools/build_variant.py links one).  A development switch: honoured only for a file inside this
+# repository's tree, announced on stderr at load with every entry point the build lacks.
+_REPO = os.path.dirname(os.path.dirname(_HERE))
+_OVERRIDE = os.environ.get("XCP_LIB_PATH")
+if _OVERRIDE:
+    _real = os.path.realpath(_OVERRIDE)
+    if os.path.commonpath([_real, os.path.realpath(_REPO)]) != os.path.realpath(_REPO):
+        raise ImportError(f"XCP_LIB_PATH={_OVERRIDE} is outside the repository ({_REPO}); "
+                          "only in-tree A/B builds may replace libxcp.so")
+    LIB_PATH = _real
+MISSING = []   # entry points an XCP_LIB_PATH build lacks (calling one raises XcpError)
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -106,17 +115,25 @@ def load():
     lib = ctypes.CDLL(LIB_PATH)
     for name, argtypes in SIGNATURES.items():
         if LIB_PATH != DEFAULT_LIB_PATH and not hasattr(lib, name):
-            continue   # an A/B build of an older tree (XCP_LIB_PATH) may predate an entry point
+            MISSING.append(name)   # an A/B build of an older tree (XCP_LIB_PATH) may predate an entry point
+            continue
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
+    if LIB_PATH != DEFAULT_LIB_PATH:
+        import sys
+        print(f"xcp: XCP_LIB_PATH override {LIB_PATH}; entry points it lacks: {MISSING or 'none'}",
+              file=sys.stderr)
     _lib = lib
     return lib
 
 
 def call(name, *args):
     """Call an entry point; raise XcpError on a non-zero status."""
-    fn = getattr(load(), name)
+    lib = load()
+    if MISSING and name in MISSING:
+        raise XcpError(f"{name} is not in the XCP_LIB_PATH build {LIB_PATH}")
+    fn = getattr(lib, name)
     rc = fn(*args)
     if name in SIZE_QUERIES:
         return rc

@@ -214,8 +214,11 @@ __global__ __launch_bounds__(256) void permute3_batch_kernel(const long long* __
   const float* src = in + bb * q.ib;
   const long obase = bb * q.ob;
   // rows of 4-element groups (16-B loads, 8-B bf16 / 16-B fp32 stores) whenever the input row length,
-  // the output pitch and the tile's edge allow; per element otherwise
-  const bool vec = (q.Cc & 3) == 0 && (q.ors & 3) == 0 && (q.R & 3) == 0;
+  // the output pitch, the per-batch strides, the tile's edge and both base addresses keep every
+  // group aligned; per element otherwise (offset views, odd pitches)
+  const unsigned long oal = dtype == XCP_BF16 ? 7ul : 15ul;
+  const bool vec = (q.Cc & 3) == 0 && (q.ors & 3) == 0 && (q.R & 3) == 0 && (q.ib & 3) == 0 && (q.ob & 3) == 0 &&
+                   (reinterpret_cast<unsigned long>(in) & 15ul) == 0 && (reinterpret_cast<unsigned long>(out) & oal) == 0;
   if (vec) {
     const int t8 = threadIdx.x & 7, tr32 = threadIdx.x >> 3;   // 32 rows x 8 four-element groups
     const int r = tr * 32 + tr32, c4 = tc * 32 + t8 * 4;

@@ -32,12 +32,23 @@ its backward).  Making the main stream wait on the side stream at every complete
 25 MB bucket, and give back the overlap the side stream exists for.  A third, dedicated
 communication stream waiting on both was measured and dropped (XCP_DDP_LAUNCH above).
 
+The mean is formed inside the collective: ``ReduceOp.AVG`` on RCCL (``"nccl"``), so no extra pass
+over the 100.8 MB buffer follows the reduction; gloo (the CPU tests) has no AVG and keeps SUM plus
+one scaling pass per bucket.
+
+Buffers.  ``broadcast_buffers`` launches rank 0's BatchNorm running statistics from a stream of its
+own (one persistent flat buffer: gather, broadcast, scatter back) and hands the completion event to
+every xcp Xception backbone in the module; the main stream waits on it only where the forward first
+reads or writes a running statistic (the stem's BN1 statistics, after conv1 has been enqueued), not
+before the step starts.
+
 Which parameters take part is re-read at every ``zero()``: the reference trains with
 the backbone frozen for three epochs and then unfreezes it (train_visual.py:547-556);
 frozen parameters keep ``grad = None`` (so an optimiser skips them, as in the reference)
 and buckets only span parameters that require grad.
 """
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -78,6 +89,8 @@ class GradBuckets:
         self._hooked = set()
         self._comm = None
         self.use_streams = dev.type == "cuda"
+        # average inside the collective where the backend has it (RCCL); gloo: SUM, then scale
+        self.avg = dist.is_initialized() and dist.get_backend() == "nccl"
         if module is not None:
             self.attach(module)
         self.zero()
@@ -169,7 +182,8 @@ class GradBuckets:
         for p in ps:   # a gradient autograd created after zero_grad(set_to_none) joins the flat buffer
             if not self._is_view(p):
                 self._adopt(p)
-        self._pending.append(dist.all_reduce(self.flat[a:b], op=dist.ReduceOp.SUM, async_op=True))
+        op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        self._pending.append(dist.all_reduce(self.flat[a:b], op=op, async_op=True))
 
     def comm_stream(self):
         """The stream the bucket all-reduces are launched from (created on first use)."""
@@ -240,17 +254,64 @@ class GradBuckets:
         for w in self._pending:   # the current (main) stream waits for the collectives
             w.wait()
         self._pending = []
-        for a, b, _ in self.buckets:
-            self.flat[a:b].mul_(1.0 / self.world)
+        if not self.avg:
+            for a, b, _ in self.buckets:
+                self.flat[a:b].mul_(1.0 / self.world)
 
 
-def broadcast_buffers(module, src=0):
+def _backbones(module):
+    """the xcp Xception backbones inside ``module`` (modules carrying the buffer-wait slot)"""
+    return [m for m in module.modules() if hasattr(m, "_xcp_wait_buffers")]
+
+
+_BCAST = weakref.WeakKeyDictionary()   # module -> its persistent broadcast buffer and stream
+
+
+def broadcast_buffers(module, src=0, use_streams=None):
+    """DDP ``broadcast_buffers``: every floating-point buffer of ``module`` takes rank 0's value.
+
+    On the GPU, when every such buffer belongs to an xcp Xception backbone, the gather, broadcast
+    and scatter run on a stream of their own and the backbones' forward makes the main stream wait
+    for them only at its first running-statistic access (``Xception._xcp_wait_buffers``); the
+    step's first kernels are not held up.  Otherwise (CPU / gloo, or buffers outside a backbone)
+    it completes on the current stream as before."""
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return
     bufs = [b for b in module.buffers() if b.is_floating_point()]
     if not bufs:
         return
-    flat = torch.cat([b.reshape(-1) for b in bufs])
-    dist.broadcast(flat, src)
-    # one multi-tensor launch instead of a copy kernel per BN buffer (~80 per step)
-    torch._foreach_copy_(bufs, [v.view_as(b) for v, b in zip(flat.split([b.numel() for b in bufs]), bufs)])
+    if use_streams is None:
+        use_streams = bufs[0].is_cuda
+    st = _BCAST.get(module)
+    n = sum(b.numel() for b in bufs)
+    if st is None or st["flat"].numel() != n or st["flat"].device != bufs[0].device:
+        st = {"flat": torch.empty(n, device=bufs[0].device, dtype=bufs[0].dtype), "stream": None}
+        _BCAST[module] = st
+    flat = st["flat"]
+    views = [v.view_as(b) for v, b in zip(flat.split([b.numel() for b in bufs]), bufs)]
+    bbs = _backbones(module)
+    owned = {id(b) for m in bbs for b in m.buffers() if b.is_floating_point()}
+    if not (use_streams and bbs and all(id(b) in owned for b in bufs)):
+        for m in bbs:
+            m._xcp_wait_buffers()
+        torch.cat([b.reshape(-1) for b in bufs], out=flat)
+        dist.broadcast(flat, src)
+        # one multi-tensor launch instead of a copy kernel per BN buffer (~80 per step)
+        torch._foreach_copy_(bufs, views)
+        return
+    for m in bbs:   # a previous broadcast nobody waited for is complete before this one reuses flat
+        m._xcp_wait_buffers()
+    if st["stream"] is None:
+        st["stream"] = torch.cuda.Stream(flat.device)
+    side, cur = st["stream"], torch.cuda.current_stream(flat.device)
+    torch.cat([b.reshape(-1) for b in bufs], out=flat)   # on the current stream: the buffers as of now
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        w = dist.broadcast(flat, src, async_op=True)
+        if w is not None:
+            w.wait()
+        torch._foreach_copy_(bufs, views)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    for m in bbs:
+        m._xcp_buffer_wait = ev

@@ -293,6 +293,7 @@ class XceptionEngine:
         CP = pc(C)
         s = Stats(CP, self.device)
         ref = _bn_ref(bnmod)
+        self.model._xcp_wait_buffers()   # a buffer broadcast still in flight (xcp.ddp.broadcast_buffers)
         if train:
             if ref["momentum"] is None:
                 ref["momentum"] = 1.0 / float(bnmod.num_batches_tracked.item() + 1)

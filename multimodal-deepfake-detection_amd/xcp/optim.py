@@ -19,11 +19,15 @@ returns the pre-clip total norm as a fresh 0-d device tensor (clip_grad_norm_'s 
 Without ``max_norm`` the script's own clip_grad_norm_ call does the clipping (as the
 reference scripts do) and ``step()`` returns None.
 
-``capturable=True`` (torch Adam's flag of that name): the step count lives on the device (one
-0-d tensor per param group, shared by the group's parameters' ``state["step"]``), incremented and
-turned into the bias corrections on the device (xcp_opt_adam_dev), so the step can be captured in
-a HIP graph and replayed -- no host arithmetic, no host sync.  A group's parameters must then share
-one step count (they do unless states were loaded piecemeal).
+``capturable=True`` (torch Adam's flag of that name): the step counts live on the device,
+incremented and turned into the bias corrections there (xcp_opt_adam_dev), so the step can be
+captured in a HIP graph and replayed -- no host arithmetic, no host sync.  Parameters whose counts
+are equal share one 0-d device counter (``state["step"]`` is that tensor), so a group normally costs
+one Adam launch.  Which parameters share a counter is decided on the host, without a device read,
+so that torch Adam's per-parameter semantics hold: a parameter whose state is created after its group has stepped (a backbone
+unfrozen after epoch 3, train_visual.py:547-556), a parameter whose grad is None on a step while its
+counter-mates step, and a loaded state whose count differs from the others each get a counter of
+their own (one more launch), never the group's count.
 """
 import math
 
@@ -48,14 +52,14 @@ class FusedAdamClip(torch.optim.Optimizer):
                 ops.check_gpu(p)
         self.max_norm = max_norm
         self.capturable = capturable
-        self._tdev = {}   # capturable: param-group index -> the group's device step count
+        self._counters = {}   # capturable: id(device step counter) -> the counter
         self._tables = {}
         self._out = None
 
-    def _state(self, p, gi=None):
+    def _state(self, p, counter=None):
         st = self.state[p]
         if not st:
-            st["step"] = self._tdev[gi] if self.capturable else torch.tensor(0.0)
+            st["step"] = counter if self.capturable else torch.tensor(0.0)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         return st
@@ -140,34 +144,72 @@ class FusedAdamClip(torch.optim.Optimizer):
             return loss
         return self._out[1].clone() if self.max_norm is not None else None
 
+    def _counter(self, value, device=None):
+        """a new device step counter: a fresh one holding the host number `value`, or a copy of the
+        device counter `value`.  Never inside a graph capture: the replay would re-run the fill /
+        copy, so the count would restart on every replay"""
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("FusedAdamClip(capturable=True): the set of parameters with gradients changed "
+                               "inside a graph capture; run one eager step with the captured structure first")
+        if torch.is_tensor(value):
+            t = value.clone()
+        else:
+            t = torch.full((), float(value), device=device, dtype=torch.float32)
+        self._counters[id(t)] = t
+        return t
+
     def _step_capturable(self, loss):
-        """step() with the step counts on the device: per group, t += 1 on the device, then one Adam
-        launch reading t (no .item(), no host-side bias corrections)"""
+        """step() with the step counts on the device: per distinct counter, t += 1 on the device,
+        then one Adam launch reading t (no .item(), no host-side bias corrections).  Counters are
+        regrouped on the host by which parameters hold them (never by reading a count), so that every
+        parameter's count is its own number of steps, as in torch Adam: a fresh state starts a fresh
+        counter at 0, a loaded state joins a counter of its own count, and a counter whose parameters
+        do not all step this time is split (a device copy) before the stepping ones advance it."""
         launches, every = [], []
         for gi, grp in enumerate(self.param_groups):
-            rows = []
+            stepping = []
+            fresh = None
             for p in grp["params"]:
                 if p.grad is None:
                     continue
                 if p.grad.is_sparse:
                     raise RuntimeError("FusedAdamClip does not support sparse gradients")
-                if gi not in self._tdev:
-                    self._tdev[gi] = torch.zeros((), device=p.device, dtype=torch.float32)
-                st = self._state(p, gi)
-                if st["step"] is not self._tdev[gi]:
-                    # a loaded state: adopt its count into the group's device counter (all must agree)
-                    t = float(st["step"])
-                    if any(float(self.state[q]["step"]) != t for q in grp["params"] if q in self.state
-                           and self.state[q]["step"] is not self._tdev[gi]):
-                        raise ValueError("FusedAdamClip(capturable=True): a param group's step counts differ")
-                    self._tdev[gi].fill_(t)
-                    for q in grp["params"]:
-                        if q in self.state:
-                            self.state[q]["step"] = self._tdev[gi]
-                rows.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"]))
-            if rows:
-                launches.append((gi, grp, rows))
+                if not self.state[p]:
+                    if fresh is None:
+                        fresh = self._counter(0, p.device)
+                    self._state(p, fresh)
+                stepping.append(p)
+            # adopt loaded (host / foreign) step tensors: one shared counter per distinct count
+            adopted = {}
+            for p in grp["params"]:
+                st = self.state.get(p)
+                if not st or id(st["step"]) in self._counters:
+                    continue
+                v = int(float(st["step"]))
+                if v not in adopted:
+                    adopted[v] = self._counter(v, p.device)
+                st["step"] = adopted[v]
+            # group the stepping parameters by counter; split counters whose other members skip
+            members = {}
+            for p in grp["params"]:
+                if p in self.state and self.state[p]:
+                    members.setdefault(id(self.state[p]["step"]), set()).add(p)
+            by_counter = {}
+            for p in stepping:
+                by_counter.setdefault(id(self.state[p]["step"]), []).append(p)
+            for cid, ps in by_counter.items():
+                t = self._counters[cid]
+                if len(ps) != len(members[cid]):
+                    t = self._counter(t)
+                    for p in ps:
+                        self.state[p]["step"] = t
+                rows = [(p, p.grad, self.state[p]["exp_avg"], self.state[p]["exp_avg_sq"]) for p in ps]
+                launches.append((grp, t, rows))
                 every.extend(rows)
+        # forget counters no parameter holds any more
+        live = {id(st["step"]) for st in self.state.values() if st and "step" in st}
+        for cid in [c for c in self._counters if c not in live]:
+            del self._counters[cid]
         if not every:
             return loss
         dev = every[0][0].device
@@ -181,12 +223,12 @@ class FusedAdamClip(torch.optim.Optimizer):
                 _lib.call("xcp_opt_sumsq", tab.data_ptr(), tab.shape[0], part.data_ptr(), float(self.max_norm),
                           self._out.data_ptr(), s)
                 coef = self._out.data_ptr()
-            for gi, grp, rows in launches:
-                self._tdev[gi].add_(1.0)
+            for grp, t, rows in launches:
+                t.add_(1.0)
                 tab = self._table(self._key("grp", rows), rows, dev)
                 b1, b2 = grp["betas"]
                 _lib.call("xcp_opt_adam_dev", tab.data_ptr(), tab.shape[0], coef, float(grp["lr"]), float(b1), float(b2),
-                          float(grp["eps"]), float(grp["weight_decay"]), self._tdev[gi].data_ptr(), s)
+                          float(grp["eps"]), float(grp["weight_decay"]), t.data_ptr(), s)
         increment_version([row[0] for row in every])
         if loss is not None:
             return loss

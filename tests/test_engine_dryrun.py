@@ -302,6 +302,17 @@ class _FakeStream:
     def wait_stream(self, other):
         _FakeStream.log.append((self.name, other.name, len(_FakeStream.calls)))
 
+    def wait_event(self, ev):
+        _FakeStream.log.append((self.name, ev.stream.name, len(_FakeStream.calls)))
+
+
+class _FakeEvent:
+    def __init__(self, *a, **k):
+        self.stream = None
+
+    def record(self, stream=None):
+        self.stream = stream or _FakeStream.current
+
 
 def _install_fake_streams(calls):
     _FakeStream.log, _FakeStream.calls = [], calls
@@ -316,6 +327,7 @@ def _install_fake_streams(calls):
             _FakeStream.current = prev
 
     torch.cuda.Stream = _FakeStream
+    torch.cuda.Event = _FakeEvent
     torch.cuda.stream = stream
     torch.cuda.current_stream = lambda *a, **k: _FakeStream.current
 
@@ -351,12 +363,23 @@ def _streams_worker(rank, world, port, out):
     gb = ddp.GradBuckets(params, bucket_bytes=1 << 20, world=world, module=m)
     gb.use_streams = True
     gb.zero()
+    with torch.no_grad():   # rank-dependent buffers: the broadcast must leave rank 0's everywhere
+        for b in m.buffers():
+            if b.is_floating_point():
+                b.fill_(rank + 1.0)
+    n_bc = len(calls)
+    ddp.broadcast_buffers(m, use_streams=True)
+    bstream = ddp._BCAST[m]["stream"].name
     m(torch.rand(2, 3, 71, 71)).sum().backward()
     last_dw = max(i for i, c in enumerate(calls) if c == "xcp_dw_bwd")
+    first_fin = min(i for i, c in enumerate(calls) if c.startswith("xcp_bn_finalize"))
     gb.allreduce()
     side = m._engine()._side.name
     out[rank] = {"log": list(_FakeStream.log), "launched": launched, "last_dw": last_dw, "side": side,
-                 "buckets": len(gb.buckets), "grads_ok": all(torch.all(p.grad == 1.5).item() for p in params)}
+                 "buckets": len(gb.buckets), "grads_ok": all(torch.all(p.grad == 1.5).item() for p in params),
+                 "bstream": bstream, "n_bc": n_bc, "first_fin": first_fin, "bufs_ok": all(
+                     torch.all(b == 1.0).item() for b in m.buffers() if b.is_floating_point()),
+                 "avg": gb.avg}
     dist.destroy_process_group()
 
 
@@ -381,6 +404,14 @@ def test_bucket_allreduce_does_not_stall_main_stream():
         # before each launch from the side stream, the side stream waited on the main stream
         side_waits_main = [n for w, o, n in r["log"] if w == r["side"] and o == "main"]
         assert all(any(m <= n for m in side_waits_main) for n, _ in during)
+        # broadcast_buffers: launched from a stream of its own after it waits on
+        # the main stream; the main stream waits for it once, after the forward's first kernel
+        # (conv1) and at the first running-statistic access (BN1's finalize), not at step start
+        assert r["bufs_ok"] and r["bstream"] not in ("main", r["side"])
+        assert (r["bstream"], "main", r["n_bc"]) in r["log"]
+        main_waits_b = [n for w, o, n in r["log"] if w == "main" and o == r["bstream"]]
+        assert len(main_waits_b) == 1 and r["n_bc"] < main_waits_b[0] <= r["first_fin"], (main_waits_b, r)
+        assert not r["avg"]   # gloo has no ReduceOp.AVG: SUM and one scaling pass
 
 
 def _cpu_replicate(net):
@@ -462,3 +493,34 @@ def test_sink_reattaches_after_zero_grad_set_to_none(fake_lib):
         for p in params:
             assert gb._is_view(p)
             assert torch.all(p.grad == FILL["v"])    # zeroed before accumulation, not stale
+
+
+def test_rccl_allreduce_averages_inside_the_collective(fake_lib, monkeypatch):
+    """On RCCL ("nccl" backend) the bucket all-reduces use ReduceOp.AVG and no scaling pass over the
+    flat buffer follows; the flat buffer is left exactly as the collective wrote
+    it."""
+    from xcp import ddp
+    ops_seen = []
+
+    class _W:
+        def wait(self):
+            pass
+
+    def fake_all_reduce(t, op=None, async_op=False):
+        ops_seen.append(op)
+        t.fill_(0.25)   # what the collective wrote: must not be rescaled afterwards
+        return _W()
+
+    monkeypatch.setattr(ddp.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(ddp.dist, "get_backend", lambda *a: "nccl")
+    monkeypatch.setattr(ddp.dist, "all_reduce", fake_all_reduce)
+    ps = [torch.zeros(1000, requires_grad=True), torch.zeros(37, requires_grad=True)]
+    gb = ddp.GradBuckets(ps, bucket_bytes=2048, world=4)
+    assert gb.avg
+    gb.zero()
+    for p in ps:
+        p.grad.fill_(1.0)
+    gb.allreduce()
+    assert ops_seen and all(o == ddp.dist.ReduceOp.AVG for o in ops_seen)
+    for p in ps:
+        assert torch.all(p.grad == 0.25)

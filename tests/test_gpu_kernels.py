@@ -784,6 +784,43 @@ def test_lstm_module_vs_oracle(ops, gpu, golden, H, T, kernel):
 
 
 @pytest.mark.parametrize("kernel", ["register", "generic"])
+def test_lstm_t120_vs_reference(ops, gpu, golden, kernel):
+    """XceptionLSTMA's own recurrence -- nn.LSTM(2048, 512) over T = 120 MFCC frames
+    (XceptionLSTMA.py:14-19, audio_dataloader.py:20,39) -- through both kernel families (0: the
+    per-step kernels H >= 256 use, 120 launches each way carrying h and c; 1: generic) against the
+    reference's own values (lstm_t120.npz): out / h_n / c_n at 1e-4, every time step's output norm
+    at 1e-4 (the error must not grow over the 120 steps), dx and the parameter gradients at 1e-3."""
+    import numpy as np
+    from xcp.lstm import LSTM
+    g = golden("lstm_t120.npz")
+    B, T, H = int(g["B"]), int(g["T"]), int(g["H"])
+    torch.manual_seed(0)
+    lstm = LSTM(2048, H, 1, batch_first=True).to(gpu)
+    lstm.xcp_kernel = 0 if kernel == "register" else 1
+    x = torch.randn((B, T, 2048), generator=torch.Generator().manual_seed(555)).to(gpu).requires_grad_(True)
+    o, (h, c) = lstm(x)
+    oc = o.detach().double().cpu()
+    np.testing.assert_allclose(oc.reshape(-1).numpy()[g["out/idx"]], g["out/val"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(oc.norm(dim=2).numpy(), g["out_step_norm"], rtol=1e-4)
+    np.testing.assert_allclose(o.detach()[:, -1].cpu().numpy(), g["out_last"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(h.detach().cpu().numpy(), g["h_n"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(c.detach().cpu().numpy(), g["c_n"], rtol=1e-4, atol=1e-5)
+    r = torch.randn(o.shape, generator=torch.Generator().manual_seed(556)).to(gpu)
+    rc = torch.randn(c.shape, generator=torch.Generator().manual_seed(557)).to(gpu)
+    ((o * r).sum() + (c * rc).sum()).backward()
+    dx = x.grad.double().cpu()
+    np.testing.assert_allclose(dx.reshape(-1).numpy()[g["dx/idx"]], g["dx/val"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(dx.norm(dim=2).numpy(), g["dx_step_norm"], rtol=1e-3)
+    for n, prm in lstm.named_parameters():
+        gr = prm.grad.double().cpu()
+        np.testing.assert_allclose(gr.norm().item(), g[f"gradnorm/{n}"], rtol=1e-3, err_msg=n)
+        np.testing.assert_allclose(gr.reshape(-1).numpy()[g[f"grad/{n}/idx"]], g[f"grad/{n}/val"], rtol=1e-3,
+                                   atol=1e-5, err_msg=n)
+        if f"gradfull/{n}" in g:
+            np.testing.assert_allclose(gr.numpy(), g[f"gradfull/{n}"], rtol=1e-3, atol=1e-5, err_msg=n)
+
+
+@pytest.mark.parametrize("kernel", ["register", "generic"])
 def test_lstm_h64_vs_oracle(ops, gpu, kernel):
     """H = 64 (the second register-resident instantiation) against the oracle's nn.LSTM
     restatement (oracle/xception_oracle.py lstm_forward, autograd for the gradients)."""

@@ -404,6 +404,65 @@ def test_xceptionlstma_step_vs_reference(gpu, golden, prec):
         check_head_on_features(m, feats, y, {n: p.grad for n, p in m.named_parameters() if is_head(n)})
 
 
+@pytest.mark.parametrize("prec,mode", [("fp32", "frozen"), ("fp32", "unfrozen"), ("bf16", "frozen")])
+def test_xceptionlstma_t120_step_vs_reference(gpu, golden, prec, mode):
+    """XceptionLSTMA(512) at its own clip length (audio_dataloader.py:20,39: T = 120 MFCC frames,
+    train_audio.py:33-44): 240 frames of 64^2 through the backbone, H = 512 over 120 steps, BCE,
+    Adam(1e-4) -- against the reference's step (audio_b2t120.npz).  fp32: features 1e-4, LSTM output
+    at the last step 1e-4, logits 1e-4, loss 1e-5, gradient norms 1e-3 (BN affine 5e-3), parameter
+    sums after Adam, BN buffers; bf16 (frozen, as shipped): features cosine, head on its own features."""
+    import xcp
+    from xcp.optim import FusedAdamClip
+    from Models.XceptionLSTMA import XceptionLSTMA
+    g = golden("audio_b2t120.npz")
+    B, T = int(g["B"]), int(g["T"])
+    x = seeded_normal((B, T, 3, 13), 778).to(gpu)
+    torch.manual_seed(0)
+    m = XceptionLSTMA(512, pretrained=False).to(gpu).train()
+    m.fc_layers.eval()
+    if mode == "unfrozen":
+        for p in m.feature_extractor.parameters():
+            p.requires_grad = True
+    logits = {}
+    m.fc_out.register_forward_hook(lambda mod, i, o: logits.__setitem__("v", o.detach()))
+    y = torch.tensor([[1.0], [0.0]], device=gpu)[:B]
+    opt = FusedAdamClip([p for p in m.parameters() if p.requires_grad], lr=1e-4)
+    with xcp.precision(prec):
+        feats = m.extract_features(x, gpu)
+        prob = m(feats)
+        loss = nn.BCELoss()(prob, y)
+        loss.backward()
+    torch.cuda.synchronize()
+    f32 = prec == "fp32"
+    fs = feats.detach().double().reshape(-1).cpu().numpy()[g[f"{mode}/features/idx"]]
+    if f32:
+        assert relerr(fs, g[f"{mode}/features/val"]) < 1e-4
+        lo, _ = m.lstm(feats.detach())
+        np.testing.assert_allclose(lo[:, -1].detach().cpu().numpy(), g[f"{mode}/lstm_last"], rtol=1e-4, atol=1e-5)
+    else:
+        assert cos(fs, g[f"{mode}/features/val"]) > 0.999
+    np.testing.assert_allclose(logits["v"].cpu().numpy(), g[f"{mode}/logits"], atol=1e-4 if f32 else 3e-2, rtol=0)
+    np.testing.assert_allclose(loss.item(), g[f"{mode}/loss"], rtol=1e-5 if f32 else 2e-2)
+    errs = {}
+    for n, p in m.named_parameters():
+        key = f"{mode}/gradnorm/{n}"
+        if p.grad is None:
+            assert key not in g, n
+            continue
+        errs[n] = abs(p.grad.double().norm().item() - g[key]) / max(g[key], 1e-30)
+    check_gradnorms(errs, bn_param_names(m), f32, skip_head=not f32, tag=f"audio_b2t120_{mode}")
+    if not f32:
+        check_head_on_features(m, feats, y, {n: p.grad for n, p in m.named_parameters() if is_head(n)})
+        return
+    opt.step()
+    torch.cuda.synchronize()
+    check_after_step(m, g, f"{mode}/after_adam", 1e-4, 0.005, names=lambda n: n.startswith(("lstm.", "fc_out")))
+    for name, t in m.state_dict().items():
+        k = f"{mode}/buf/{name}/sum"
+        if k in g:
+            np.testing.assert_allclose(t.double().sum().item(), g[k], rtol=1e-4, atol=1e-4, err_msg=name)
+
+
 def test_after_adam_and_buffers_b2t4(gpu, golden):
     """The captured `after_adam/*` and `buf/*` entries of the B2T4 299^2 step (fp32): one
     FusedAdamClip(lr 1e-4, no clipping) step after the BCE backward (capture_goldens.py

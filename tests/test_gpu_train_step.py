@@ -284,3 +284,29 @@ def test_graph_captured_train_step_matches_eager(gpu):
     sa, sb = models[0].state_dict(), models[1].state_dict()
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k
+
+
+def test_fused_adam_capturable_late_parameter_vs_torch(gpu):
+    """A parameter whose first gradient arrives at step 3 (the reference's unfreeze after epoch 3,
+    train_visual.py:547-556) and one that skips a step keep their own step counts under
+    capturable=True, as in torch.optim.Adam(capturable=True) (advisor round 4)."""
+    from xcp.optim import FusedAdamClip
+    g = torch.Generator(device=gpu).manual_seed(9)
+    shapes = [(300, 7), (64,), (32, 3, 3, 3)]
+    init = [torch.randn(s, device=gpu, generator=g) for s in shapes]
+    pa = [t.clone().requires_grad_(True) for t in init]
+    pb = [t.clone().requires_grad_(True) for t in init]
+    ref = torch.optim.Adam(pa, lr=1e-2, weight_decay=1e-4, capturable=True)
+    opt = FusedAdamClip(pb, lr=1e-2, weight_decay=1e-4, capturable=True)
+    for k in range(6):
+        for i, (p, q) in enumerate(zip(pa, pb)):
+            skip = (i == 1 and k < 2) or (i == 2 and k == 3)
+            gr = None if skip else torch.randn(shapes[i], device=gpu, generator=g)
+            p.grad = None if gr is None else gr.clone()
+            q.grad = None if gr is None else gr.clone()
+        ref.step()
+        opt.step()
+    torch.cuda.synchronize()
+    for p, q in zip(pa, pb):
+        torch.testing.assert_close(q, p, rtol=1e-5, atol=1e-6)
+        assert float(opt.state[q]["step"]) == float(ref.state[p]["step"])

@@ -206,3 +206,39 @@ def test_frame_step_c1(golden):
         if f"after_step/{n}/sum" in g:
             np.testing.assert_allclose(p.detach().double().sum().item(), g[f"after_step/{n}/sum"], rtol=1e-6,
                                        atol=1e-6, err_msg=n)
+
+
+def test_oracle_lstm_t120(golden):
+    """oracle.lstm_forward over XceptionLSTMA's own recurrence (H = 512, T = 120,
+    audio_dataloader.py:20,39) against the reference nn.LSTM (lstm_t120.npz), including the
+    per-time-step output norms and the backward through all 120 steps."""
+    g = golden("lstm_t120.npz")
+    B, T, H = int(g["B"]), int(g["T"]), int(g["H"])
+    torch.manual_seed(0)
+    ref = nn.LSTM(2048, H, 1, batch_first=True)
+    cp = {n: p.detach().clone().requires_grad_(True) for n, p in ref.named_parameters()}
+    x = seeded_normal((B, T, 2048), 555).requires_grad_(True)
+    o, h, c = O.lstm_forward(x, cp["weight_ih_l0"], cp["weight_hh_l0"], cp["bias_ih_l0"], cp["bias_hh_l0"])
+    check_fp(g, "out", o, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(o.detach().double().norm(dim=2).numpy(), g["out_step_norm"], rtol=1e-5)
+    np.testing.assert_allclose(h.detach().numpy(), g["h_n"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(c.detach().numpy(), g["c_n"], rtol=1e-5, atol=1e-6)
+    ((o * seeded_normal(o.shape, 556)).sum() + (c * seeded_normal(c.shape, 557)).sum()).backward()
+    check_fp(g, "dx", x.grad, rtol=1e-4, atol=1e-6)
+    for n, p in cp.items():
+        np.testing.assert_allclose(p.grad.double().norm().item(), g[f"gradnorm/{n}"], rtol=1e-5, err_msg=n)
+
+
+def test_audio_clip_t120(golden):
+    """oracle.clip_step on the XceptionLSTMA step at T = 120 (audio_b2t120.npz, frozen backbone as
+    shipped): 240 frames of 64^2, then H = 512 over 120 steps."""
+    g = golden("audio_b2t120.npz")
+    B, T = int(g["B"]), int(g["T"])
+    x = seeded_normal((B, T, 3, 13), 778)
+    y = torch.tensor([[1.0], [0.0]])[:B]
+    r = O.clip_step(_clip_sd(XceptionLSTMA, 512), x, y, unfrozen=False, audio=True)
+    check_fp(g, "frozen/features", r["features"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(r["logits"].numpy(), g["frozen/logits"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(r["loss"].item(), g["frozen/loss"], rtol=1e-6)
+    for k, gr in r["grads"].items():
+        np.testing.assert_allclose(gr.double().norm().item(), g[f"frozen/gradnorm/{k}"], rtol=1e-3, err_msg=k)

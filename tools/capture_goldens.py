@@ -220,6 +220,77 @@ def g_lstm(out_dir):
     np.savez_compressed(os.path.join(out_dir, "lstm.npz"), **out)
 
 
+def g_lstm_t120(out_dir, B=2, T=120, H=512):
+    """nn.LSTM(2048, 512) over XceptionLSTMA's own recurrence length (audio_dataloader.py:20,39: 120
+    MFCC frames per clip; XceptionLSTMA.py:14-19, train_audio.py:15).  Large tensors as fingerprints;
+    the per-time-step norms of out pin the error growth over the 120 steps."""
+    out = {"torch_version": torch.__version__, "B": B, "T": T, "H": H, "seed_w": 0, "seed_x": 555,
+           "seed_r": 556, "seed_rc": 557}
+    torch.manual_seed(0)
+    lstm = nn.LSTM(2048, H, 1, batch_first=True)
+    x = seeded_normal((B, T, 2048), 555).requires_grad_(True)
+    o, (h, c) = lstm(x)
+    r = seeded_normal(o.shape, 556)
+    rc = seeded_normal(c.shape, 557)
+    ((o * r).sum() + (c * rc).sum()).backward()
+    put_fp(out, "out", o)
+    out["out_step_norm"] = o.detach().double().norm(dim=2).numpy()   # [B, T]
+    out["out_last"] = o.detach()[:, -1].numpy()
+    out["h_n"] = h.detach().numpy()
+    out["c_n"] = c.detach().numpy()
+    put_fp(out, "dx", x.grad)
+    out["dx_step_norm"] = x.grad.double().norm(dim=2).numpy()
+    for name, prm in lstm.named_parameters():
+        out[f"gradnorm/{name}"] = prm.grad.double().norm().item()
+        put_fp(out, f"grad/{name}", prm.grad)
+        if prm.dim() == 1:
+            out[f"gradfull/{name}"] = prm.grad.numpy()
+    np.savez_compressed(os.path.join(out_dir, "lstm_t120.npz"), **out)
+
+
+def g_audio_t120(A, out_dir, B=2, T=120):
+    """XceptionLSTMA(512) train step (train_audio.py:33-44: BCELoss on the sigmoid output, Adam 1e-4)
+    at the reference's own clip length, T = 120 MFCC frames (audio_dataloader.py:20,39): 240 frames
+    of 64^2 through the backbone, then H = 512 over 120 steps.  Frozen backbone (as shipped,
+    XceptionLSTMA.py:11-12) and unfrozen; head dropout off."""
+    out = {"torch_version": torch.__version__, "B": B, "T": T, "seed_w": 0, "seed_x": 778}
+    x = seeded_normal((B, T, 3, 13), 778)
+    y = torch.tensor([[1.0], [0.0]])[:B]
+    for mode in ("frozen", "unfrozen"):
+        torch.manual_seed(0)
+        m = A.XceptionLSTMA(512)
+        if mode == "unfrozen":
+            for p in m.feature_extractor.parameters():
+                p.requires_grad = True
+        m.train()
+        m.fc_layers.eval()
+        store = {}
+        m.fc_out.register_forward_hook(_logit_hook(store))
+        feats = m.extract_features(x, "cpu")
+        prob = m(feats)
+        loss = nn.BCELoss()(prob, y)
+        opt = torch.optim.Adam([p for p in m.parameters() if p.requires_grad], lr=1e-4)
+        opt.zero_grad()
+        loss.backward()
+        put_fp(out, f"{mode}/features", feats)
+        lo, _ = m.lstm(feats.detach())
+        out[f"{mode}/lstm_last"] = lo[:, -1].detach().numpy()
+        out[f"{mode}/prob"] = prob.detach().numpy()
+        out[f"{mode}/logits"] = store["logits"].numpy()
+        out[f"{mode}/loss"] = loss.item()
+        grad_norms(out, f"{mode}/gradnorm", m)
+        opt.step()
+        for name, p in m.named_parameters():
+            if name.startswith("lstm.") or name.startswith("fc_out"):
+                a = p.detach().double()
+                out[f"{mode}/after_adam/{name}/sum"] = a.sum().item()
+                out[f"{mode}/after_adam/{name}/sumsq"] = (a * a).sum().item()
+        for name, t in m.state_dict().items():
+            if "running_mean" in name or "running_var" in name:
+                out[f"{mode}/buf/{name}/sum"] = t.double().sum().item()
+    np.savez_compressed(os.path.join(out_dir, "audio_b2t120.npz"), **out)
+
+
 def g_blocks(X, out_dir):
     """Block fwd/bwd at N=2 in train mode: block1 (s2, no leading relu), block4 (identity skip),
     block12 (grow_first=False, s2)."""
@@ -555,7 +626,8 @@ def main():
                                                 name="lstmv_b16t16.npz", ckpt=True),
             "c1": lambda: g_xception_frames(X, args.out, 4, "xception_c1_b4.npz"),
             "c2": lambda: g_xception_frames(X, args.out, 64, "xception_c2_b64.npz", ckpt=True),
-            "heads": lambda: g_heads(args.out), "arcface_step": lambda: g_arcface_step(V, args.out)}
+            "heads": lambda: g_heads(args.out), "arcface_step": lambda: g_arcface_step(V, args.out),
+            "lstm_t120": lambda: g_lstm_t120(args.out), "audio_t120": lambda: g_audio_t120(A, args.out)}
     for k, fn in jobs.items():
         if args.only and k not in args.only.split(","):
             continue
