@@ -272,6 +272,14 @@ int xcp_clock_probe(long long* out, int blocks, int iters, xcp_stream_t stream);
  * quotes the depthwise kernels against (the guide's float4 copy) */
 int xcp_stream_copy(const void* in, void* out, long n16, xcp_stream_t stream);
 
+/* ---- CU-partitioned streams (the backbone backward's two streams, engine XCP_SIDE_CUS) ----
+ * not a reference interface: the reference's backward runs on one stream.  Creates a stream
+ * restricted to quarters/4 of every XCD's CUs (complement = 1: the other CUs); *out receives the
+ * hipStream_t.  xcp_stream_cu_count: CUs a stream may use (negative on error). */
+int xcp_stream_create_cumask(int quarters, int complement, void** out);
+int xcp_stream_cu_count(xcp_stream_t stream);
+int xcp_stream_destroy(xcp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -88,13 +88,16 @@ SIGNATURES = {
     "xcp_lstm_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_clock_probe": [P, I, I, P],
     "xcp_stream_copy": [P, P, L, P],
+    "xcp_stream_create_cumask": [I, I, P],
+    "xcp_stream_cu_count": [P],
+    "xcp_stream_destroy": [P],
 }
 
 # entry points that return a size, not a status
 SIZE_QUERIES = {"xcp_permute3_blocks", "xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
                 "xcp_colreduce_groups", "xcp_unit_bwd_rows_per_split",
                 "xcp_conv1_wgrad_parts", "xcp_conv1_wgrad_fused", "xcp_conv1_fwd_parts", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
-                "xcp_maxpool_bwd_bnred_parts"}
+                "xcp_maxpool_bwd_bnred_parts", "xcp_stream_cu_count"}
 
 _lib = None
 

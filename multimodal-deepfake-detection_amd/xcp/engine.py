@@ -118,6 +118,13 @@ STEM_FUSED = os.environ.get("XCP_STEM_FUSED", "1") != "0"
 RESBN = os.environ.get("XCP_RESBN", "0") == "1"
 STEM_WGRAD_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_STEM_WGRAD_SIDE", "1") != "0"
 SIDE_PRIO_LOW = os.environ.get("XCP_SIDE_PRIO", "") == "low"
+# XCP_SIDE_CUS=q (1..3): the backbone backward runs on two CU-partitioned streams -- the weight
+# gradients on q/4 of every XCD's CUs, the main chain (BN backward, dgrad GEMMs, depthwise backward)
+# on the rest -- instead of two streams competing for every CU (a 160 KB-LDS weight-gradient
+# workgroup can only start on a CU that has drained, and then holds it whole).  0: off.
+SIDE_CUS = int(os.environ.get("XCP_SIDE_CUS", "0"))
+if not 0 <= SIDE_CUS <= 3:
+    raise ValueError("XCP_SIDE_CUS must be 0..3")
 # BN1's backward coefficients before the side-stream conv2 weight gradient is launched
 # (XCP_STEM_BN1_FIRST=0: after it, the round-2 order; A/B)
 STEM_BN1_FIRST = os.environ.get("XCP_STEM_BN1_FIRST", "1") != "0"
@@ -184,7 +191,10 @@ class XceptionEngine:
 
     def _side_stream(self, dev):
         st = getattr(self, "_side", None)
-        if st is None or st.device != dev:
+        if SIDE_CUS and (st is None or st.device != dev):
+            st = self._side = ops.cu_stream(SIDE_CUS, False, dev)
+            self._main_bwd = ops.cu_stream(SIDE_CUS, True, dev)
+        elif st is None or st.device != dev:
             # XCP_SIDE_PRIO=low: the weight-gradient stream at the least priority the device offers
             # (below the default stream's when the range has one), so the dispatcher prefers the
             # main stream's workgroups (A/B; the default creates it at the default priority)
@@ -450,7 +460,18 @@ class XceptionEngine:
         if not S["train"]:
             raise RuntimeError("xcp engine backward needs a train-mode forward (batch-stat BatchNorm)")
         with ops.device_guard(dfeat):
-            return self._backward(S, dfeat, out, notify)
+            if not (SIDE_CUS and WGRAD_SIDE_STREAM):
+                return self._backward(S, dfeat, out, notify)
+            # the CU-partitioned pair: the main chain on the complement stream, ordered after the
+            # caller's work and before the caller's next (the tensors it allocates go back to the
+            # caller ordered by those two waits)
+            self._side_stream(dfeat.device)
+            caller, mb = torch.cuda.current_stream(dfeat.device), self._main_bwd
+            mb.wait_stream(caller)
+            with torch.cuda.stream(mb):
+                r = self._backward(S, dfeat, out, notify)
+            caller.wait_stream(mb)
+            return r
 
     def _backward(self, S, dfeat, out, notify):
         pk = self.pack_bwd()

@@ -5,6 +5,8 @@ below launches a hand-written gfx950 kernel from ``libxcp.so`` on the current
 HIP stream.  There is no CPU or eager-PyTorch fallback: a missing library or a
 non-GPU tensor raises.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -565,3 +567,14 @@ def lstm_bwd(dout, dhn, dcn, whh, cst, gates, dgates, B, T, H, kernel=0):
     work = torch.empty(B * H + 4 * H * H, device=whh.device, dtype=torch.float32)
     _lib.call("xcp_lstm_bwd", _p(dout), _p(dhn), _p(dcn), _p(whh), _p(cst), _p(gates), _p(dgates), _p(work), B, T, H,
               kernel, stream())
+
+
+def cu_stream(quarters, complement, device):
+    """A torch stream over a HIP stream restricted to quarters/4 of every XCD's CUs (complement:
+    the other CUs), xcp_stream_create_cumask.  The HIP stream lives as long as the process."""
+    h = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        _lib.call("xcp_stream_create_cumask", int(quarters), int(bool(complement)), ctypes.byref(h))
+    s = torch.cuda.ExternalStream(h.value, device=device)
+    s._xcp_cus = _lib.call("xcp_stream_cu_count", h.value)
+    return s
