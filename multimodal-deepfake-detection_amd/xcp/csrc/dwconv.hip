@@ -292,6 +292,372 @@ int dw_fwd_w2() {
 }
 
 // ---------------------------------------------------------------------------------
+// Pipelined forward (dw_fwd_pipe_kernel): the tile of dw_fwd_w2_kernel, but persistent
+// workgroups (two per CU, 64 KB of LDS each) that stream their tiles through a two-slot LDS ring
+// by LDS-DMA, so a tile's loads are in flight while the previous tile computes and stores.  The
+// one-tile-per-workgroup kernel has loads in flight only during its staging phase (~1/3 of a
+// workgroup's life: ~16 GB/s per CU moved at 19^2 x 736, 0.42 of HBM); here every workgroup keeps
+// the next tile's ~23 KB in flight throughout.
+//   * The DMA lands raw bytes (out-of-frame halo pixels and channels past C read as zeros through
+//     the buffer resource's out-of-range offset).  The producer's BN + ReLU is then applied in
+//     place by one LDS pass over the tile's in-frame chunks (ACT_RELU needs no pass where the halo
+//     is zero: relu(0) = 0, but applies max(., 0) in the same pass), so the register window, the
+//     fma chain and the stored values are exactly those of dw_fwd_w2_kernel.
+//   * Every thread issues the same number of DMA instructions (nd per tile) and of output stores
+//     (ns per tile, masked ones as out-of-range buffer stores), so counted vmcnt waits retire a
+//     tile's DMA without waiting for the previous tile's stores.
+//   * Raw s_barrier / lgkmcnt only (no __syncthreads, whose fence would drain vmcnt).
+constexpr unsigned DBUF_OOB = 0x80000000u;
+constexpr long DBUF_LIMIT = 0x7fffffffL;
+constexpr int DBUF_RECORDS = 0x7fffffff;
+constexpr int DBUF_DWORD3 = 0x00020000;
+constexpr int PIPE_MAXPX = 512;
+constexpr int DW_PIPE_PX = PIPE_MAXPX * SLICE;        // 32 KB of pixel slices per ring slot
+constexpr int DW_PIPE_SLOT = DW_PIPE_PX + 4096;       // + the tile's parameters: scale @0, shift @1 KB, taps (9 x 128 B) @2 KB
+
+XCP_DEV void dvm_wait(int n) {   // s_waitcnt vmcnt(n), n clamped to [0, 63]
+  switch (n < 0 ? 0 : n > 63 ? 63 : n) {
+#define XCP_DVMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    XCP_DVMW(0) XCP_DVMW(1) XCP_DVMW(2) XCP_DVMW(3) XCP_DVMW(4) XCP_DVMW(5) XCP_DVMW(6) XCP_DVMW(7)
+    XCP_DVMW(8) XCP_DVMW(9) XCP_DVMW(10) XCP_DVMW(11) XCP_DVMW(12) XCP_DVMW(13) XCP_DVMW(14) XCP_DVMW(15)
+    XCP_DVMW(16) XCP_DVMW(17) XCP_DVMW(18) XCP_DVMW(19) XCP_DVMW(20) XCP_DVMW(21) XCP_DVMW(22) XCP_DVMW(23)
+    XCP_DVMW(24) XCP_DVMW(25) XCP_DVMW(26) XCP_DVMW(27) XCP_DVMW(28) XCP_DVMW(29) XCP_DVMW(30) XCP_DVMW(31)
+    XCP_DVMW(32) XCP_DVMW(33) XCP_DVMW(34) XCP_DVMW(35) XCP_DVMW(36) XCP_DVMW(37) XCP_DVMW(38) XCP_DVMW(39)
+    XCP_DVMW(40) XCP_DVMW(41) XCP_DVMW(42) XCP_DVMW(43) XCP_DVMW(44) XCP_DVMW(45) XCP_DVMW(46) XCP_DVMW(47)
+    XCP_DVMW(48) XCP_DVMW(49) XCP_DVMW(50) XCP_DVMW(51) XCP_DVMW(52) XCP_DVMW(53) XCP_DVMW(54) XCP_DVMW(55)
+    XCP_DVMW(56) XCP_DVMW(57) XCP_DVMW(58) XCP_DVMW(59) XCP_DVMW(60) XCP_DVMW(61) XCP_DVMW(62) XCP_DVMW(63)
+#undef XCP_DVMW
+  }
+}
+
+typedef int di32x2 __attribute__((ext_vector_type(2)));
+
+// LDS accesses of the pipelined kernel by inline asm, each block carrying its own lgkmcnt wait:
+// hipcc puts an s_waitcnt vmcnt(0) before any compiler-visible LDS access that may alias an LDS-DMA
+// destination, which would retire the next tile's DMA (the ring) at every read.  A load and the wait
+// for it sit in ONE asm statement, so no use or copy of the result can be scheduled between them.
+typedef unsigned du32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned du32x2 __attribute__((ext_vector_type(2)));
+XCP_DEV unsigned dlds(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)(p); }
+XCP_DEV void lds_ld4x128(const char* p0, const char* p1, const char* p2, const char* p3, du32x4& a, du32x4& b, du32x4& c,
+                         du32x4& d) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %5\n\t"
+      "ds_read_b128 %2, %6\n\t"
+      "ds_read_b128 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+      : "v"(dlds(p0)), "v"(dlds(p1)), "v"(dlds(p2)), "v"(dlds(p3))
+      : "memory");
+}
+XCP_DEV void lds_st128(char* p, const du32x4& v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(dlds(p)), "v"(v) : "memory");
+}
+XCP_DEV void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// the 3 x 7 window of a 5-pixel segment: rows r0, r1, r2 (byte addresses), pixels k * 64 B apart
+XCP_DEV void lds_win7(const char* r0, const char* r1, const char* r2, du32x2 (&v)[3][7]) {
+  asm volatile(
+      "ds_read_b64 %0, %21\n\t"
+      "ds_read_b64 %1, %21 offset:64\n\t"
+      "ds_read_b64 %2, %21 offset:128\n\t"
+      "ds_read_b64 %3, %21 offset:192\n\t"
+      "ds_read_b64 %4, %21 offset:256\n\t"
+      "ds_read_b64 %5, %21 offset:320\n\t"
+      "ds_read_b64 %6, %21 offset:384\n\t"
+      "ds_read_b64 %7, %22\n\t"
+      "ds_read_b64 %8, %22 offset:64\n\t"
+      "ds_read_b64 %9, %22 offset:128\n\t"
+      "ds_read_b64 %10, %22 offset:192\n\t"
+      "ds_read_b64 %11, %22 offset:256\n\t"
+      "ds_read_b64 %12, %22 offset:320\n\t"
+      "ds_read_b64 %13, %22 offset:384\n\t"
+      "ds_read_b64 %14, %23\n\t"
+      "ds_read_b64 %15, %23 offset:64\n\t"
+      "ds_read_b64 %16, %23 offset:128\n\t"
+      "ds_read_b64 %17, %23 offset:192\n\t"
+      "ds_read_b64 %18, %23 offset:256\n\t"
+      "ds_read_b64 %19, %23 offset:320\n\t"
+      "ds_read_b64 %20, %23 offset:384\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[0][2]), "=&v"(v[0][3]), "=&v"(v[0][4]), "=&v"(v[0][5]), "=&v"(v[0][6]),
+        "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[1][2]), "=&v"(v[1][3]), "=&v"(v[1][4]), "=&v"(v[1][5]), "=&v"(v[1][6]),
+        "=&v"(v[2][0]), "=&v"(v[2][1]), "=&v"(v[2][2]), "=&v"(v[2][3]), "=&v"(v[2][4]), "=&v"(v[2][5]), "=&v"(v[2][6])
+      : "v"(dlds(r0)), "v"(dlds(r1)), "v"(dlds(r2))
+      : "memory");
+}
+// the 3 x 6 window of a 4-pixel segment
+XCP_DEV void lds_win6(const char* r0, const char* r1, const char* r2, du32x2 (&v)[3][6]) {
+  asm volatile(
+      "ds_read_b64 %0, %18\n\t"
+      "ds_read_b64 %1, %18 offset:64\n\t"
+      "ds_read_b64 %2, %18 offset:128\n\t"
+      "ds_read_b64 %3, %18 offset:192\n\t"
+      "ds_read_b64 %4, %18 offset:256\n\t"
+      "ds_read_b64 %5, %18 offset:320\n\t"
+      "ds_read_b64 %6, %19\n\t"
+      "ds_read_b64 %7, %19 offset:64\n\t"
+      "ds_read_b64 %8, %19 offset:128\n\t"
+      "ds_read_b64 %9, %19 offset:192\n\t"
+      "ds_read_b64 %10, %19 offset:256\n\t"
+      "ds_read_b64 %11, %19 offset:320\n\t"
+      "ds_read_b64 %12, %20\n\t"
+      "ds_read_b64 %13, %20 offset:64\n\t"
+      "ds_read_b64 %14, %20 offset:128\n\t"
+      "ds_read_b64 %15, %20 offset:192\n\t"
+      "ds_read_b64 %16, %20 offset:256\n\t"
+      "ds_read_b64 %17, %20 offset:320\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[0][2]), "=&v"(v[0][3]), "=&v"(v[0][4]), "=&v"(v[0][5]),
+        "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[1][2]), "=&v"(v[1][3]), "=&v"(v[1][4]), "=&v"(v[1][5]),
+        "=&v"(v[2][0]), "=&v"(v[2][1]), "=&v"(v[2][2]), "=&v"(v[2][3]), "=&v"(v[2][4]), "=&v"(v[2][5])
+      : "v"(dlds(r0)), "v"(dlds(r1)), "v"(dlds(r2))
+      : "memory");
+}
+
+struct DwPipeArgs {
+  DwArgs a;
+  int ntiles;   // N * nth * ntw * ngroups
+  int nd;       // DMA instructions per wave per tile: ceil(HP * WP * 4 / 256)
+  int nit;      // row items per worker per tile: ceil(TH * nseg / 32)
+};
+
+template <int ACT, int SG>
+__global__ __launch_bounds__(256) void dw_fwd_pipe_kernel(DwPipeArgs pa) {
+  constexpr int FS = SLICE, LANES = FS / 8, NWK = 256 / LANES, CPL = 4;
+  __shared__ __attribute__((aligned(16))) char ring0[DW_PIPE_SLOT];
+  __shared__ __attribute__((aligned(16))) char ring1[DW_PIPE_SLOT];
+  // every field in a local scalar: the lambdas below take them by reference, and a reference to the
+  // kernel-argument struct itself put it in scratch (private memory), with a vmcnt(0) at each use
+  const int H = pa.a.H, W = pa.a.W, C = pa.a.C, ngroups = pa.a.ngroups;
+  const int TH = pa.a.g.TH, TW = pa.a.g.TW, HP = pa.a.g.HP, WP = pa.a.g.WP, ntw = pa.a.g.ntw, nseg = pa.a.g.nseg;
+  const int ntiles = pa.ntiles, ndp = pa.nd, nit = pa.nit;
+  const void* Xp = pa.a.X;
+  void* Yp = pa.a.Y;
+  const float *Wtp = pa.a.Wt, *scp = pa.a.scale, *shp = pa.a.shift;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cl = tid % LANES, wk = tid / LANES;
+  const int nwg = gridDim.x;
+  const int ntl = pa.a.g.nth * ntw;
+  const int total = HP * WP * 4;   // 16-B chunks of a staged tile
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(Xp), (short)0, DBUF_RECORDS,
+                                                                       DBUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(Yp, (short)0, DBUF_RECORDS, DBUF_DWORD3);
+  // tile id -> (channel slice, frame, spatial tile), as block_coords with the logical id
+  auto coords = [&](int id, int& grp, int& n, int& th0, int& tw0) {
+    grp = id % ngroups;
+    const int sp = id / ngroups;
+    const int tile = sp % ntl;
+    n = sp / ntl;
+    th0 = (tile / ntw) * TH;
+    tw0 = (tile % ntw) * TW;
+  };
+  const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Wtp), (short)0, DBUF_RECORDS,
+                                                                       DBUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(ACT == ACT_BNRELU ? scp : Wtp), (short)0, DBUF_RECORDS, DBUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(ACT == ACT_BNRELU ? shp : Wtp), (short)0, DBUF_RECORDS, DBUF_DWORD3);
+  // the DMA of tile `id` into ring slot `dst`: nd pixel pieces per wave (wave w's pieces j = w*nd + k),
+  // and by wave 0 two more pieces with the tile's parameters -- scale / shift of its 32 channels
+  // (chunks 0-15) and its 9 x 32 taps (chunks 16-87) -- so that nothing a tile reads is a register
+  // load younger than the DMA in flight (a vmcnt wait for one would drain the ring)
+  auto issue = [&](int id, char* dst) {
+    int grp, n, th0, tw0;
+    coords(id, grp, n, th0, tw0);
+    const int c0 = grp * 32;
+    const long nbase = (long)n * H * W;
+    if (w == 0) {   // (one buffer resource per instruction: a per-lane resource select is a waterfall loop)
+      char* pd = dst + DW_PIPE_PX;
+      if constexpr (ACT == ACT_BNRELU) {
+        const unsigned o = lane < 8 && c0 + lane * 4 < C ? (unsigned)((c0 + lane * 4) * 4) : DBUF_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, (__attribute__((address_space(3))) void*)pd, 16, o, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rT, (__attribute__((address_space(3))) void*)(pd + 1024), 16, o, 0, 0, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = k * 64 + lane, row = c >> 3, ch = c0 + (c & 7) * 4;
+        const unsigned o = c < 72 && ch < C ? (unsigned)(((long)row * C + ch) * 4) : DBUF_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (__attribute__((address_space(3))) void*)(pd + 2048 + k * 1024), 16, o,
+                                                 0, 0, 0);
+      }
+    }
+    for (int k = 0; k < ndp; ++k) {
+      const int j = w * ndp + k;
+      const int c = j * 64 + lane;
+      const int p = c >> 2, q = c & 3;
+      const int hy = p / WP, hx = p - hy * WP;
+      const int h = th0 - 1 + hy, x = tw0 - 1 + hx;
+      const int ch = c0 + q * 8;
+      const bool ok = c < total && h >= 0 && h < H && x >= 0 && x < W && ch < C;
+      const unsigned o = ok ? (unsigned)(((nbase + (long)h * W + x) * C + ch) * 2) : DBUF_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, o, 0,
+                                               0, 0);
+    }
+  };
+  // one tile: (BN +) ReLU in place, then the 3 x (SG+2) register windows and nit * SG output stores
+  auto work = [&](int id, char* sA) {
+    int grp, n, th0, tw0;
+    coords(id, grp, n, th0, tw0);
+    const int c0 = grp * 32;
+    const long nbase = (long)n * H * W;
+    const float* prm = reinterpret_cast<const float*>(sA + DW_PIPE_PX);   // scale[32] @0, shift[32] @256, taps[9][32] @512
+    if constexpr (ACT != ACT_NONE) {
+      // this thread's chunks are tid + 256 k: always channel chunk q = tid & 3
+      const int q = tid & 3;
+      float sc[8], sh[8];
+      if constexpr (ACT == ACT_BNRELU) {
+        du32x4 r[4];
+        lds_ld4x128(reinterpret_cast<const char*>(prm + q * 8), reinterpret_cast<const char*>(prm + q * 8 + 4),
+                    reinterpret_cast<const char*>(prm + 256 + q * 8), reinterpret_cast<const char*>(prm + 256 + q * 8 + 4),
+                    r[0], r[1], r[2], r[3]);
+        VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[0]), sc);
+        VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[1]), sc + 4);
+        VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[2]), sh);
+        VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[3]), sh + 4);
+      }
+      // four chunks per asm read block (out-of-tile chunks read chunk 0 and are not written back)
+      for (int c4 = tid; c4 < total; c4 += 1024) {
+        du32x4 u[4];
+        const int cs[4] = {c4, c4 + 256, c4 + 512, c4 + 768};
+        lds_ld4x128(sA + (cs[0] < total ? cs[0] : 0) * 16, sA + (cs[1] < total ? cs[1] : 0) * 16,
+                    sA + (cs[2] < total ? cs[2] : 0) * 16, sA + (cs[3] < total ? cs[3] : 0) * 16, u[0], u[1], u[2], u[3]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cs[r];
+          const int p = c >> 2;
+          const int hy = p / WP, hx = p - hy * WP;
+          const int h = th0 - 1 + hy, x = tw0 - 1 + hx;
+          // halo / padding chunks stay 0 (relu(bn(0)) need not be)
+          if (c >= total || h < 0 || h >= H || x < 0 || x >= W || c0 + q * 8 >= C) continue;
+          float f[8];
+          VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&u[r]), f);
+          typedef float p2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            p2 v = p2{f[e], f[e + 1]};
+            if constexpr (ACT == ACT_BNRELU) v = __builtin_elementwise_fma(v, p2{sc[e], sc[e + 1]}, p2{sh[e], sh[e + 1]});
+            v = __builtin_elementwise_max(v, p2(0.f));
+            f[e] = v[0];
+            f[e + 1] = v[1];
+          }
+          VecIO<bf16, 8>::store(reinterpret_cast<bf16*>(&u[r]), f);
+          lds_st128(sA + c * 16, u[r]);
+        }
+      }
+      lds_wait();
+      __builtin_amdgcn_s_barrier();
+    }
+    const int c = c0 + cl * CPL;
+    float wt[9][CPL];
+    {
+      du32x4 r[12];
+      const char* wb = reinterpret_cast<const char*>(prm + 512 + cl * CPL);
+      lds_ld4x128(wb, wb + 128, wb + 256, wb + 384, r[0], r[1], r[2], r[3]);
+      lds_ld4x128(wb + 512, wb + 640, wb + 768, wb + 896, r[4], r[5], r[6], r[7]);
+      lds_ld4x128(wb + 1024, wb + 1024, wb + 1024, wb + 1024, r[8], r[9], r[10], r[11]);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) VecIO<float, CPL>::load(reinterpret_cast<const float*>(&r[t]), wt[t]);
+    }
+    const int items = TH * nseg;
+    const char* lbase = sA + cl * 8;
+    for (int s = 0; s < nit; ++s) {
+      const int it = wk + s * NWK;
+      const bool real = it < items;
+      const int r = real ? it / nseg : 0, sg = real ? it - r * nseg : 0;
+      const int oh = th0 + r;
+      const int x0 = sg * SG;
+      const char* base = lbase + (r * WP + x0) * FS;
+      float win[3][SG + 2][CPL];
+      du32x2 raw[3][SG + 2];
+      if constexpr (SG == 5) lds_win7(base, base + WP * FS, base + 2 * WP * FS, raw);
+      else lds_win6(base, base + WP * FS, base + 2 * WP * FS, raw);
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int k = 0; k < SG + 2; ++k) {
+          unpack(raw[ky][k][0], win[ky][k], (bf16*)nullptr);
+          unpack(raw[ky][k][1], win[ky][k] + 2, (bf16*)nullptr);
+        }
+      const long rowe = (nbase + (long)oh * W + tw0) * C + c;
+#pragma unroll
+      for (int j = 0; j < SG; ++j) {
+        float o[CPL];
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
+          float sum = 0.f;
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) sum = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], sum);
+          o[e] = sum;
+        }
+        const int x = x0 + j;
+        const bool ok = real && c < C && oh < H && x < TW && tw0 + x < W;
+        const unsigned off = ok ? (unsigned)((rowe + (long)x * C) * 2) : DBUF_OOB;
+        const uint2 v = make_uint2(pack(o, (bf16*)nullptr), pack(o + 2, (bf16*)nullptr));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(di32x2, v), rY, (int)off, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_barrier();   // every wave is done with this slot before the next DMA into it
+  };
+  const int ns = nit * SG;                    // stores per thread per tile
+  const int nd = ndp + (w == 0 ? (ACT == ACT_BNRELU ? 4 : 2) : 0);   // DMA pieces per wave per tile
+  int t = xcd_remap(blockIdx.x, nwg);
+  if (t >= ntiles) return;
+  issue(t, ring0);
+  bool first = true;
+  // two ring slots as two LDS objects, the loop unrolled by two so each half names its slot
+  while (true) {
+    {
+      const int tn = t + nwg;
+      const bool more = tn < ntiles;
+      if (more) issue(tn, ring1);
+      dvm_wait((more ? nd : 0) + (first ? 0 : ns));   // tile t's DMA landed (this wave's pieces)
+      __builtin_amdgcn_s_barrier();                         // ... and every thread's
+      work(t, ring0);
+      first = false;
+      if (!more) break;
+      t = tn;
+    }
+    {
+      const int tn = t + nwg;
+      const bool more = tn < ntiles;
+      if (more) issue(tn, ring0);
+      dvm_wait((more ? nd : 0) + ns);
+      __builtin_amdgcn_s_barrier();
+      work(t, ring1);
+      if (!more) break;
+      t = tn;
+    }
+  }
+}
+
+// XCP_DW_FWD_PIPE=0: the one-tile-per-workgroup kernel (A/B); default: the pipelined one for bf16
+// 64-B slices.  XCP_DW_FWD_PIPE_WGS=<n>: workgroups per CU (default 2).
+int dw_fwd_pipe() {   // (read per call: the bitwise test compares both kernels in one process)
+  const char* e = getenv("XCP_DW_FWD_PIPE");
+  return e ? atoi(e) : 1;
+}
+int dw_fwd_pipe_wgs() {
+  static const int v = [] {
+    const char* e = getenv("XCP_DW_FWD_PIPE_WGS");
+    const int n = e ? atoi(e) : 2;
+    return n >= 1 && n <= 2 ? n : 2;
+  }();
+  return v;
+}
+int dw_gpu_cus() {
+  static const int cus = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      n = 0;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+// ---------------------------------------------------------------------------------
 // Fused backward.  Per pixel p:
 //   dA[p]   = sum_tap dY[p - off(tap)] * w[tap]          (transposed 3x3)
 //   dX[p]   = act'(p) * dA[p] + dRes[p] + (p at stride-multiple (h,w) ? dSkip[p/s] : 0)
@@ -929,6 +1295,19 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
   if (dtype == XCP_BF16 && dw_fwd_w2()) {
     const int sg = dw_fwd_w2();
     a.g = tile_geo(H, W, FWD_MAXPX, sg);
+    const long span = (long)N * H * W * C * 2;
+    if (dw_fwd_pipe() && span <= DBUF_LIMIT && a.g.HP * a.g.WP <= PIPE_MAXPX) {
+      DwPipeArgs pa{a, a.N * a.g.nth * a.g.ntw * a.ngroups, (a.g.HP * a.g.WP * 4 + 255) / 256,
+                    (a.g.TH * a.g.nseg + 31) / 32};
+      const int grid = min(pa.ntiles, dw_gpu_cus() * dw_fwd_pipe_wgs());
+#define XCP_PIPE(SGV)                                                                                                \
+      if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_NONE, SGV>), dim3(grid), dim3(256), 0, stream, pa); \
+      else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_RELU, SGV>), dim3(grid), dim3(256), 0, stream, pa); \
+      else hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_BNRELU, SGV>), dim3(grid), dim3(256), 0, stream, pa);
+      if (sg == 4) { XCP_PIPE(4) } else { XCP_PIPE(5) }
+#undef XCP_PIPE
+      return (int)hipGetLastError();
+    }
     const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
 #define XCP_W2(SGV)                                                                                                  \
     if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_w2_kernel<ACT_NONE, FWD_MAXPX, SGV>), dim3(blocks), dim3(256), 0, stream, a); \
