@@ -422,11 +422,10 @@ struct DwPipeArgs {
   int nit;      // row items per worker per tile: ceil(TH * nseg / 32)
 };
 
-template <int ACT, int SG>
-__global__ __launch_bounds__(256) void dw_fwd_pipe_kernel(DwPipeArgs pa) {
-  constexpr int FS = SLICE, LANES = FS / 8, NWK = 256 / LANES, CPL = 4;
-  __shared__ __attribute__((aligned(16))) char ring0[DW_PIPE_SLOT];
-  __shared__ __attribute__((aligned(16))) char ring1[DW_PIPE_SLOT];
+template <int ACT, int SG, int NWV, int NSLOT>
+__global__ __launch_bounds__(NWV * 64) void dw_fwd_pipe_kernel(DwPipeArgs pa) {
+  constexpr int NT = NWV * 64, FS = SLICE, LANES = FS / 8, NWK = NT / LANES, CPL = 4;
+  __shared__ __attribute__((aligned(16))) char ring[NSLOT * DW_PIPE_SLOT];
   // every field in a local scalar: the lambdas below take them by reference, and a reference to the
   // kernel-argument struct itself put it in scratch (private memory), with a vmcnt(0) at each use
   const int H = pa.a.H, W = pa.a.W, C = pa.a.C, ngroups = pa.a.ngroups;
@@ -503,7 +502,7 @@ __global__ __launch_bounds__(256) void dw_fwd_pipe_kernel(DwPipeArgs pa) {
     const long nbase = (long)n * H * W;
     const float* prm = reinterpret_cast<const float*>(sA + DW_PIPE_PX);   // scale[32] @0, shift[32] @256, taps[9][32] @512
     if constexpr (ACT != ACT_NONE) {
-      // this thread's chunks are tid + 256 k: always channel chunk q = tid & 3
+      // this thread's chunks are tid + NT k: always channel chunk q = tid & 3
       const int q = tid & 3;
       float sc[8], sh[8];
       if constexpr (ACT == ACT_BNRELU) {
@@ -517,9 +516,9 @@ __global__ __launch_bounds__(256) void dw_fwd_pipe_kernel(DwPipeArgs pa) {
         VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[3]), sh + 4);
       }
       // four chunks per asm read block (out-of-tile chunks read chunk 0 and are not written back)
-      for (int c4 = tid; c4 < total; c4 += 1024) {
+      for (int c4 = tid; c4 < total; c4 += 4 * NT) {
         du32x4 u[4];
-        const int cs[4] = {c4, c4 + 256, c4 + 512, c4 + 768};
+        const int cs[4] = {c4, c4 + NT, c4 + 2 * NT, c4 + 3 * NT};
         lds_ld4x128(sA + (cs[0] < total ? cs[0] : 0) * 16, sA + (cs[1] < total ? cs[1] : 0) * 16,
                     sA + (cs[2] < total ? cs[2] : 0) * 16, sA + (cs[3] < total ? cs[3] : 0) * 16, u[0], u[1], u[2], u[3]);
 #pragma unroll
@@ -603,49 +602,32 @@ __global__ __launch_bounds__(256) void dw_fwd_pipe_kernel(DwPipeArgs pa) {
   };
   const int ns = nit * SG;                    // stores per thread per tile
   const int nd = ndp + (w == 0 ? (ACT == ACT_BNRELU ? 4 : 2) : 0);   // DMA pieces per wave per tile
-  int t = xcd_remap(blockIdx.x, nwg);
-  if (t >= ntiles) return;
-  issue(t, ring0);
-  bool first = true;
-  // two ring slots as two LDS objects, the loop unrolled by two so each half names its slot
-  while (true) {
-    {
-      const int tn = t + nwg;
-      const bool more = tn < ntiles;
-      if (more) issue(tn, ring1);
-      dvm_wait((more ? nd : 0) + (first ? 0 : ns));   // tile t's DMA landed (this wave's pieces)
-      __builtin_amdgcn_s_barrier();                         // ... and every thread's
-      work(t, ring0);
-      first = false;
-      if (!more) break;
-      t = tn;
-    }
-    {
-      const int tn = t + nwg;
-      const bool more = tn < ntiles;
-      if (more) issue(tn, ring0);
-      dvm_wait((more ? nd : 0) + ns);
-      __builtin_amdgcn_s_barrier();
-      work(t, ring1);
-      if (!more) break;
-      t = tn;
-    }
+  const int t0 = xcd_remap(blockIdx.x, nwg);
+  if (t0 >= ntiles) return;
+  const int mine = (ntiles - 1 - t0) / nwg + 1;   // tiles of this workgroup: t0 + k nwg, k < mine
+  // prologue: the first NSLOT - 1 tiles in flight
+#pragma unroll
+  for (int k = 0; k < NSLOT - 1; ++k)
+    if (k < mine) issue(t0 + k * nwg, ring + k * DW_PIPE_SLOT);
+  for (int k = 0; k < mine; ++k) {
+    const int kn = k + NSLOT - 1;   // into the slot tile k - 1 has just left (its readers passed a barrier)
+    if (kn < mine) issue(t0 + kn * nwg, ring + (kn % NSLOT) * DW_PIPE_SLOT);
+    // tile k's DMA landed: younger are the stores of tiles k-NSLOT+1 .. k-1 and the DMA of tiles
+    // k+1 .. min(k+NSLOT-1, mine-1) (vmcnt retires in issue order)
+    const int younger = ns * min(NSLOT - 1, k) + nd * (min(kn, mine - 1) - k);
+    dvm_wait(younger);
+    __builtin_amdgcn_s_barrier();   // ... every wave's pieces of it
+    work(t0 + k * nwg, ring + (k % NSLOT) * DW_PIPE_SLOT);
   }
 }
 
-// XCP_DW_FWD_PIPE=0: the one-tile-per-workgroup kernel (A/B); default: the pipelined one for bf16
-// 64-B slices.  XCP_DW_FWD_PIPE_WGS=<n>: workgroups per CU (default 2).
+// XCP_DW_FWD_PIPE=0: the one-tile-per-workgroup kernel; m = 1..4 the pipelined form
+//   1: 4 waves, 2 slots, 2 workgroups per CU     2: 8 waves, 4 slots, 1 per CU
+//   3: 8 waves, 2 slots, 2 per CU                4: 4 waves, 4 slots, 1 per CU
 int dw_fwd_pipe() {   // (read per call: the bitwise test compares both kernels in one process)
   const char* e = getenv("XCP_DW_FWD_PIPE");
-  return e ? atoi(e) : 1;
-}
-int dw_fwd_pipe_wgs() {
-  static const int v = [] {
-    const char* e = getenv("XCP_DW_FWD_PIPE_WGS");
-    const int n = e ? atoi(e) : 2;
-    return n >= 1 && n <= 2 ? n : 2;
-  }();
-  return v;
+  const int m = e ? atoi(e) : 0;
+  return m >= 0 && m <= 4 ? m : 0;
 }
 int dw_gpu_cus() {
   static const int cus = [] {
@@ -1299,12 +1281,26 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
     if (dw_fwd_pipe() && span <= DBUF_LIMIT && a.g.HP * a.g.WP <= PIPE_MAXPX) {
       DwPipeArgs pa{a, a.N * a.g.nth * a.g.ntw * a.ngroups, (a.g.HP * a.g.WP * 4 + 255) / 256,
                     (a.g.TH * a.g.nseg + 31) / 32};
-      const int grid = min(pa.ntiles, dw_gpu_cus() * dw_fwd_pipe_wgs());
-#define XCP_PIPE(SGV)                                                                                                \
-      if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_NONE, SGV>), dim3(grid), dim3(256), 0, stream, pa); \
-      else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_RELU, SGV>), dim3(grid), dim3(256), 0, stream, pa); \
-      else hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_BNRELU, SGV>), dim3(grid), dim3(256), 0, stream, pa);
-      if (sg == 4) { XCP_PIPE(4) } else { XCP_PIPE(5) }
+      const int mode = dw_fwd_pipe();
+      const int nwv = mode == 2 || mode == 3 ? 8 : 4, wgs = mode == 1 || mode == 3 ? 2 : 1;
+      pa.nd = (a.g.HP * a.g.WP * 4 + 64 * nwv - 1) / (64 * nwv);
+      pa.nit = (a.g.TH * a.g.nseg + nwv * 8 - 1) / (nwv * 8);
+      const int grid = min(pa.ntiles, dw_gpu_cus() * wgs);
+#define XCP_PIPE(SGV, NWV, NSL)                                                                                         \
+      if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_NONE, SGV, NWV, NSL>), dim3(grid), dim3(NWV * 64), 0, stream, pa); \
+      else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_RELU, SGV, NWV, NSL>), dim3(grid), dim3(NWV * 64), 0, stream, pa); \
+      else hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_BNRELU, SGV, NWV, NSL>), dim3(grid), dim3(NWV * 64), 0, stream, pa);
+      if (sg == 4) {
+        XCP_PIPE(4, 4, 2)
+      } else if (mode == 2) {
+        XCP_PIPE(5, 8, 4)
+      } else if (mode == 3) {
+        XCP_PIPE(5, 8, 2)
+      } else if (mode == 4) {
+        XCP_PIPE(5, 4, 4)
+      } else {
+        XCP_PIPE(5, 4, 2)
+      }
 #undef XCP_PIPE
       return (int)hipGetLastError();
     }

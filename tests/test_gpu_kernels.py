@@ -295,8 +295,8 @@ def test_gemm_operands_over_2gb_global_address_path(ops, gpu):
                                      (4, 736, 37, 37), (1, 40, 13, 30), (600, 24, 9, 11), (2, 200, 1, 9)])
 def test_dw_fwd_pipelined_bitwise(ops, gpu, monkeypatch, act, N, C, H, W):
     """The pipelined depthwise forward (persistent workgroups, LDS-DMA ring, BN + ReLU applied in
-    LDS; XCP_DW_FWD_PIPE=1, the default) gives bit for bit the outputs of the one-tile-per-workgroup
-    kernel (XCP_DW_FWD_PIPE=0): the same register window and fma chain.  Shapes: the bench's 256-frame
+    LDS; XCP_DW_FWD_PIPE=1..4: 4 / 8 waves, 2 / 4 ring slots) gives bit for bit the outputs of the
+    one-tile-per-workgroup kernel (XCP_DW_FWD_PIPE=0, the default): the same register window and fma chain.  Shapes: the bench's 256-frame
     middle flow, ragged channel slices (C = 40, 24, 200), multi-tile frames (147^2, 74^2), more tiles
     than resident workgroups, non-square frames."""
     g = torch.Generator(device=gpu).manual_seed(N + C + H + act)
@@ -305,14 +305,15 @@ def test_dw_fwd_pipelined_bitwise(ops, gpu, monkeypatch, act, N, C, H, W):
     sc = torch.rand(C, device=gpu, generator=g) + 0.5
     sh = torch.randn(C, device=gpu, generator=g) * 0.2
     outs = []
-    for pipe in ("1", "0"):
+    for pipe in ("0", "1", "2", "3", "4"):   # one-tile kernel, then the four ring shapes
         monkeypatch.setenv("XCP_DW_FWD_PIPE", pipe)
         Y = torch.full((N * H * W, C), float("nan"), device=gpu, dtype=torch.bfloat16)
         ops.dw_fwd(act, x, Y, Wt, sc, sh, N, H, W, C)
         outs.append(Y)
     torch.cuda.synchronize()
     assert not torch.isnan(outs[0].float()).any()
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
 
 
 @pytest.mark.parametrize("dt", DTYPES)
