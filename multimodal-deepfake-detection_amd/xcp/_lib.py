@@ -33,6 +33,7 @@ D = ctypes.c_double
 SIGNATURES = {
     "xcp_gemm_nt": [I, P, L, P, L, P, L, I, I, I, P, I, I, I, I, I, I, I, I, P],
     "xcp_gemm_nt_stat_rows": [I],
+    "xcp_gemm_nt_bnfin": [I, P, L, P, L, P, L, I, I, I, I, I, I, I, I, I, I, I, P, P, I, D, P, P, P, P, F, F, P, P, P, P, P],
     "xcp_gemm_tn_rows_per_split": [I, I, I, I, I, I],
     "xcp_gemm_tn": [I, P, L, P, L, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "xcp_unit_bwd_rows_per_split": [I, I, I, I],
@@ -40,6 +41,7 @@ SIGNATURES = {
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
     "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, I, I, P],
+    "xcp_dw_bwd_fin": [I, I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P],
     "xcp_dw_bwd_resbn": [I, I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_colreduce_f32": [P, I, L, L, P, I, I, P],
     "xcp_colreduce_groups": [I, L],
@@ -47,6 +49,7 @@ SIGNATURES = {
     "xcp_chanred_parts": [L, I],
     "xcp_row_stats": [I, P, L, I, P, P],
     "xcp_bn_bwd_reduce": [I, P, P, P, P, P, P, L, I, P, P],
+    "xcp_bn_bwd_reduce_fin": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, P, P, I, P],
     "xcp_bn_finalize_part": [P, I, I, I, D, P, P, P, P, F, F, P, P, P, P, P],
     "xcp_bn_bwd_finalize_part": [P, I, I, I, D, P, P, P, P, P, P, P, P, I, P],
     "xcp_bn_finalize": [P, I, I, I, D, P, P, P, P, F, F, I, P, P, P, P, P],
@@ -58,6 +61,7 @@ SIGNATURES = {
     "xcp_maxpool_bwd": [I, P, P, P, I, I, I, I, P],
     "xcp_maxpool_bwd_bnred_parts": [I, I, I, I],
     "xcp_maxpool_bwd_bnred": [I, P, P, P, P, P, P, I, I, I, I, P, P],
+    "xcp_maxpool_bwd_bnred_fin": [I, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P],
     "xcp_avgpool_fwd": [I, P, P, P, P, I, I, I, P],
     "xcp_avgpool_bwd": [I, P, P, P, P, P, I, I, I, P],
     "xcp_conv1_fwd": [I, P, P, P, I, I, I, P],

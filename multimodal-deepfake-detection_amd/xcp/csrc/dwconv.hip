@@ -669,6 +669,7 @@ struct DwBwdArgs {
   int N, H, W, C, ngroups;
   int nbands, bandH;      // row bands per frame (one wave walks rows [band*bandH, +bandH))
   int xcd;                // 1: consecutive workgroups of the walk on one XCD (xcd_remap)
+  BnFin fin;              // fin.acc: the BN partial sums folded into that BN's backward finalize (common.h)
 };
 
 template <typename T, int P, int FS>
@@ -887,7 +888,11 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];   // output staging (separate object)
   const int ncg = (a.W + RCOLS - 1) / RCOLS;
   const RowMap mp = row_map(a.N, ncg, a.ngroups, a.nbands, a.xcd != 0);
-  if (!mp.live) return;
+  __shared__ int fin_last;
+  if (!mp.live) {   // (a folded finalize: every wave of the workgroup takes part in its arrival)
+    if (a.fin.acc && fin_arrive(a.fin, &fin_last)) fin_finalize(a.fin, threadIdx.x, 256);
+    return;
+  }
   // this wave's rows [r0, r1); it reads X rows r0 .. r1-1 and dY rows r0-1 .. r1 (rows past
   // those are staged from the zero line: never read)
   const int r0 = mp.band * a.bandH, r1 = min(a.H, r0 + a.bandH);
@@ -905,7 +910,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const int x0w = mp.cg * RCOLS, x0 = x0w + sg * RS;
   const RowLanes rl_ld = row_lanes_load<T>(a.W, a.C, x0w, c0, lane);
   const RowLanes rl_st = row_lanes_store<T>(a.W, a.C, x0w, c0, lane);
-  const bool bnsum = a.bnpart != nullptr;
+  const bool bnsum = a.bnpart != nullptr || a.fin.acc != nullptr;
   constexpr bool bnres = RES && BNRES;                  // sums over the final dX against Yb (bnsum implied)
   const bool bnx = bnsum && !bnres;                     // sums over the masked dz against X
   V wt[9], dw[9], sc = V(1.f), sh = V(0.f), bs1 = V(0.f), bs2 = V(0.f), mu = V(0.f), is = V(0.f);
@@ -1160,12 +1165,16 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     for (int e = 0; e < EPT; ++e) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) a.dWpart[((long)mp.unit * a.C + c + e) * 9 + t] = red[e][t];
-      if (bnsum) {
+      if (a.fin.acc) {
+        fin_add(a.fin.acc + c + e, red[e][9]);
+        fin_add(a.fin.acc + a.fin.CP + c + e, red[e][10]);
+      } else if (bnsum) {
         a.bnpart[((long)mp.unit * 2 + 0) * a.C + c + e] = red[e][9];
         a.bnpart[((long)mp.unit * 2 + 1) * a.C + c + e] = red[e][10];
       }
     }
   }
+  if (a.fin.acc && fin_arrive(a.fin, &fin_last)) fin_finalize(a.fin, threadIdx.x, 256);
 }
 
 // XCP_DW_BWD_ROLL=1: the rolling-window form for every variant (the round-2 kernel; A/B)
@@ -1326,12 +1335,13 @@ int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
 static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
                        const float* shift, const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre,
                        void* dX, float* dWpart, float* bnpart, const float* bmean, const float* binvstd, const void* Yb,
-                       int N, int H, int W, int C, hipStream_t stream) {
+                       int N, int H, int W, int C, hipStream_t stream, BnFin fin = BnFin{}) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
+  const bool sums = bnpart || fin.acc;
   if (Yb) {   // sums over the final dX: needs the residual input, no skip input, and the BN's statistics
-    if (!dRes || dSkip || !bnpart || !bmean || !binvstd) return XCP_EINVAL;
-  } else if (bnpart && (act != ACT_BNRELU || !bmean || !binvstd)) {
+    if (!dRes || dSkip || !sums || !bmean || !binvstd) return XCP_EINVAL;
+  } else if (sums && (act != ACT_BNRELU || !bmean || !binvstd)) {
     return XCP_EINVAL;
   }
   DwBwdArgs a{};
@@ -1343,6 +1353,11 @@ static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const 
   a.nbands = dw_bwd_bands(H);
   a.xcd = dw_bwd_xcd();
   a.bandH = (H + a.nbands - 1) / a.nbands;
+  a.fin = fin;
+  if (fin.acc) {   // every workgroup of the launch arrives (launch_bwd_lds: 4 waves per workgroup)
+    const long waves = (long)N * ((W + RCOLS - 1) / RCOLS) * a.nbands * a.ngroups;
+    a.fin.expected = (unsigned)((waves + 3) / 4);
+  }
   if (dtype == XCP_BF16) return launch_bwd_lds<bf16>(act, a, stream);
   if (dtype == XCP_F32) return launch_bwd_lds<float>(act, a, stream);
   return XCP_EUNSUPPORTED;
@@ -1353,6 +1368,35 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
                float* bnpart, const float* bmean, const float* binvstd, int N, int H, int W, int C, hipStream_t stream) {
   return dw_bwd_impl(dtype, act, dY, X, Wt, scale, shift, dRes, dSkip, sOH, sOW, sS, skip_pre, dX, dWpart, bnpart, bmean,
                      binvstd, nullptr, N, H, W, C, stream);
+}
+
+// xcp_dw_bwd with the preceding BN's backward finalize folded in (see include/xcp.h)
+int xcp_dw_bwd_fin(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
+                   const float* shift, const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre,
+                   void* dX, float* dWpart, const float* bmean, const float* binvstd, int N, int H, int W, int C, int Cbn,
+                   double* acc, unsigned* ticket, const float* gamma, float* alpha, float* bcoef, float* delta,
+                   float* dgamma, float* dbeta, int accumulate, hipStream_t stream) {
+  if (Cbn <= 0 || Cbn > C || !acc || !ticket || !gamma || !alpha || !bcoef || !delta ||
+      (dgamma == nullptr) != (dbeta == nullptr))
+    return XCP_EINVAL;
+  BnFin f{};
+  f.acc = acc;
+  f.ticket = ticket;
+  f.C = Cbn;
+  f.CP = C;
+  f.bwd = 1;
+  f.count = (double)N * H * W;
+  f.gamma = gamma;
+  f.o0 = alpha;
+  f.o1 = bcoef;
+  f.o2 = delta;
+  f.mean = bmean;
+  f.invstd = binvstd;
+  f.dgamma = dgamma;
+  f.dbeta = dbeta;
+  f.accumulate = accumulate;
+  return dw_bwd_impl(dtype, act, dY, X, Wt, scale, shift, dRes, dSkip, sOH, sOW, sS, skip_pre, dX, dWpart, nullptr, bmean,
+                     binvstd, nullptr, N, H, W, C, stream, f);
 }
 
 int xcp_dw_bwd_resbn(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
