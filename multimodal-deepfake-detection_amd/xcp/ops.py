@@ -252,7 +252,9 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
 # ---------------------------------------------------------------- batchnorm
 
 
-FIN_MAX_ROWS = 2048   # above this many partial rows, pre-reduce to FIN_GROUPS rows (fp64 sums, fp32 out)
+import os as _os
+# above this many partial rows, pre-reduce to FIN_GROUPS rows (fp64 sums, fp32 out); XCP_FIN_MAX_ROWS (A/B)
+FIN_MAX_ROWS = int(_os.environ.get("XCP_FIN_MAX_ROWS", "2048"))
 FIN_GROUPS = 256
 
 

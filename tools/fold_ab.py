@@ -34,9 +34,29 @@ def run(fold, prec, B, S):
     return r
 
 
+def compare(a, b, tag):
+    rows = []
+    for k in a:
+        nd = int((a[k] != b[k]).sum())
+        d = (a[k].double() - b[k].double()).abs()
+        rows.append((float(d.max() / b[k].double().abs().max().clamp_min(1e-30)), nd, k))
+    first = [r for r in rows if r[2].startswith("buf/") and r[1]]
+    print(f"  {tag}: {sum(r[1] for r in rows)} differing elements; buffers in module order, first differing:",
+          [(k, n, f"{x:.2e}") for x, n, k in first[:6]])
+    rows.sort(reverse=True)
+    for rel, nd, k in rows[:6]:
+        print(f"     {rel:.3e}  ({nd} elements)  {k}")
+
+
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     S = int(sys.argv[2]) if len(sys.argv) > 2 else 299
+    for prec in ("fp32",):
+        a, b, b2 = run(True, prec, B, S), run(False, prec, B, S), run(False, prec, B, S)
+        print(f"[{prec}] B={B} S={S} XCP_FIN_MAX_ROWS={os.environ.get('XCP_FIN_MAX_ROWS', '2048')}")
+        compare(b, b2, "partial rows vs partial rows (determinism)")
+        compare(a, b, "fold vs partial rows")
+    return
     for prec in ("fp32", "bf16"):
         a, b = run(True, prec, B, S), run(False, prec, B, S)
         worst, ndiff, ntot = [], 0, 0
