@@ -51,14 +51,6 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
                 float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, xcp_stream_t stream);
 /* number of partial rows in gemm_nt's stats array for M rows */
 int xcp_gemm_nt_stat_rows(int M);
-/* gemm_nt with the BatchNorm batch statistics of C's N columns (Cbn real channels, the rest padding)
- * finalised inside the op (see the folded-finalize note at xcp_bn_bwd_reduce_fin): mean / invstd /
- * scale / shift [N] (zero for padding), running statistics updated (rmean / rvar may both be null) */
-int xcp_gemm_nt_bnfin(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                      int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, double* acc,
-                      unsigned* ticket, int Cbn, double count, const float* gamma, const float* beta, float* rmean,
-                      float* rvar, float momentum, float eps, float* mean_o, float* invstd_o, float* scale_o,
-                      float* shift_o, xcp_stream_t stream);
 
 /* weight gradient of the above: P[s][N][K] = sum_{m in split s} G[m][N] X[m][K],
  * rows split in S chunks of rows_per_split; X rows gathered as in gemm_nt
@@ -97,13 +89,6 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
                const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre, void* dX, float* dWpart,
                float* bnpart, const float* bmean, const float* binvstd, int N, int H, int W, int C,
                xcp_stream_t stream);
-/* xcp_dw_bwd with that BatchNorm's backward finalize folded in instead of bnpart (see
- * xcp_bn_bwd_reduce_fin): alpha / bcoef / delta [C] (zero past Cbn), dgamma / dbeta [Cbn] */
-int xcp_dw_bwd_fin(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
-                   const float* shift, const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre,
-                   void* dX, float* dWpart, const float* bmean, const float* binvstd, int N, int H, int W, int C, int Cbn,
-                   double* acc, unsigned* ticket, const float* gamma, float* alpha, float* bcoef, float* delta,
-                   float* dgamma, float* dbeta, int accumulate, xcp_stream_t stream);
 /* The same backward with a residual input dRes (no skip input) whose BatchNorm partial sums are
  * those of the BN whose OUTPUT gradient is the final dX = act'(X) * dA + dRes (an identity-skip block
  * boundary, Xception.py:89-99 (skip = inp, x += skip at :96-98): the previous block's last BN feeds both this block's first ReLU and its
@@ -145,19 +130,6 @@ int xcp_bn_bwd_finalize_part(const float* part, int R, int C, int CP, double cou
 int xcp_bn_finalize(const double* part2, int G, int C, int CP, double count, const float* gamma, const float* beta,
                     float* rmean, float* rvar, float momentum, float eps, int train, float* mean, float* invstd,
                     float* scale, float* shift, xcp_stream_t stream);
-/* ---- BatchNorm finalize folded into the producing op (no partial rows, no finalize launch) ----
- * Every workgroup adds its fp32 partial sums into acc (fp64 [2][CP] + 1 sink double) with
- * device-scope atomics and takes a ticket; the last workgroup writes the finalize outputs (as
- * xcp_bn_finalize_part / xcp_bn_bwd_finalize_part) and leaves acc and *ticket zero.  acc and ticket
- * are caller-owned, zero before the first call, one pair per BN and direction, and must not be used
- * by two ops in flight at once.  fp64 sums in arrival order: exact unless a partial is 2^-19 below
- * the largest, the finalize outputs (fp32) then equal up to fp64 rounding of the sum.
- * Backward (xcp_bn_bwd_reduce_fin, xcp_maxpool_bwd_bnred_fin): xcp_bn_bwd_reduce /
- * xcp_maxpool_bwd_bnred + xcp_bn_bwd_finalize_part; C the channel pitch, Cbn the BN's channels. */
-int xcp_bn_bwd_reduce_fin(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd,
-                          const float* ms, const float* mt, long rows, int C, int Cbn, double* acc, unsigned* ticket,
-                          const float* gamma, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
-                          int accumulate, xcp_stream_t stream);
 int xcp_bn_act(int dtype, const void* X, void* Y, const float* scale, const float* shift, int relu, long rows, int C,
                xcp_stream_t stream);
 /* Y[n][oh][ow][c] = act(X[n][oh*S][ow*S][c] * scale[c] + shift[c]) (relu: max(., 0)): the activated
@@ -180,10 +152,6 @@ int xcp_maxpool_bwd_bnred_parts(int N, int H, int W, int C);
 int xcp_maxpool_bwd_bnred(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
                           const float* mean, const float* invstd, int N, int H, int W, int C, float* part,
                           xcp_stream_t stream);
-int xcp_maxpool_bwd_bnred_fin(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
-                              const float* mean, const float* invstd, int N, int H, int W, int C, int Cbn, double* acc,
-                              unsigned* ticket, const float* gamma, float* alpha, float* bcoef, float* delta,
-                              float* dgamma, float* dbeta, int accumulate, xcp_stream_t stream);
 /* bn4 + ReLU + adaptive_avg_pool2d (Xception.py:193-198) -> F[N][C] fp32 */
 int xcp_avgpool_fwd(int dtype, const void* Y, const float* s, const float* t, float* F, int N, int HW, int C,
                     xcp_stream_t stream);
@@ -304,13 +272,6 @@ int xcp_clock_probe(long long* out, int blocks, int iters, xcp_stream_t stream);
  * quotes the depthwise kernels against (the guide's float4 copy) */
 int xcp_stream_copy(const void* in, void* out, long n16, xcp_stream_t stream);
 
-/* ---- CU-partitioned streams (the backbone backward's two streams, engine XCP_SIDE_CUS) ----
- * not a reference interface: the reference's backward runs on one stream.  Creates a stream
- * restricted to quarters/4 of every XCD's CUs (complement = 1: the other CUs); *out receives the
- * hipStream_t.  xcp_stream_cu_count: CUs a stream may use (negative on error). */
-int xcp_stream_create_cumask(int quarters, int complement, void** out);
-int xcp_stream_cu_count(xcp_stream_t stream);
-int xcp_stream_destroy(xcp_stream_t stream);
 
 #ifdef __cplusplus
 }

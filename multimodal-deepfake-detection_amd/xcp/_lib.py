@@ -33,7 +33,6 @@ D = ctypes.c_double
 SIGNATURES = {
     "xcp_gemm_nt": [I, P, L, P, L, P, L, I, I, I, P, I, I, I, I, I, I, I, I, P],
     "xcp_gemm_nt_stat_rows": [I],
-    "xcp_gemm_nt_bnfin": [I, P, L, P, L, P, L, I, I, I, I, I, I, I, I, I, I, I, P, P, I, D, P, P, P, P, F, F, P, P, P, P, P],
     "xcp_gemm_tn_rows_per_split": [I, I, I, I, I, I],
     "xcp_gemm_tn": [I, P, L, P, L, P, I, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "xcp_unit_bwd_rows_per_split": [I, I, I, I],
@@ -41,7 +40,6 @@ SIGNATURES = {
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
     "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, I, I, P],
-    "xcp_dw_bwd_fin": [I, I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P],
     "xcp_dw_bwd_resbn": [I, I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_colreduce_f32": [P, I, L, L, P, I, I, P],
     "xcp_colreduce_groups": [I, L],
@@ -49,7 +47,6 @@ SIGNATURES = {
     "xcp_chanred_parts": [L, I],
     "xcp_row_stats": [I, P, L, I, P, P],
     "xcp_bn_bwd_reduce": [I, P, P, P, P, P, P, L, I, P, P],
-    "xcp_bn_bwd_reduce_fin": [I, P, P, P, P, P, P, L, I, I, P, P, P, P, P, P, P, P, I, P],
     "xcp_bn_finalize_part": [P, I, I, I, D, P, P, P, P, F, F, P, P, P, P, P],
     "xcp_bn_bwd_finalize_part": [P, I, I, I, D, P, P, P, P, P, P, P, P, I, P],
     "xcp_bn_finalize": [P, I, I, I, D, P, P, P, P, F, F, I, P, P, P, P, P],
@@ -61,7 +58,6 @@ SIGNATURES = {
     "xcp_maxpool_bwd": [I, P, P, P, I, I, I, I, P],
     "xcp_maxpool_bwd_bnred_parts": [I, I, I, I],
     "xcp_maxpool_bwd_bnred": [I, P, P, P, P, P, P, I, I, I, I, P, P],
-    "xcp_maxpool_bwd_bnred_fin": [I, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P, I, P],
     "xcp_avgpool_fwd": [I, P, P, P, P, I, I, I, P],
     "xcp_avgpool_bwd": [I, P, P, P, P, P, I, I, I, P],
     "xcp_conv1_fwd": [I, P, P, P, I, I, I, P],
@@ -92,16 +88,13 @@ SIGNATURES = {
     "xcp_lstm_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_clock_probe": [P, I, I, P],
     "xcp_stream_copy": [P, P, L, P],
-    "xcp_stream_create_cumask": [I, I, P],
-    "xcp_stream_cu_count": [P],
-    "xcp_stream_destroy": [P],
 }
 
 # entry points that return a size, not a status
 SIZE_QUERIES = {"xcp_permute3_blocks", "xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
                 "xcp_colreduce_groups", "xcp_unit_bwd_rows_per_split",
                 "xcp_conv1_wgrad_parts", "xcp_conv1_wgrad_fused", "xcp_conv1_fwd_parts", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
-                "xcp_maxpool_bwd_bnred_parts", "xcp_stream_cu_count"}
+                "xcp_maxpool_bwd_bnred_parts"}
 
 _lib = None
 

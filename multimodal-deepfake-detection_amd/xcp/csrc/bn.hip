@@ -164,10 +164,8 @@ ChanRed make_chanred(long rows, int C, int CPT, int target_blocks) {
 }
 long chanred_P(const ChanRed& r) { return (r.rows + r.rows_per_chunk - 1) / r.rows_per_chunk; }
 
-// fin.acc set: the partial sums go into the folded BN finalize (common.h BnFin) instead of part
 template <int CPT>
-XCP_DEV void chanred_finish(const ChanRed& r, float (*acc)[CPT], float* part, int cchunk, int pchunk, int lcv, int slot,
-                            const BnFin& fin = BnFin{}) {
+XCP_DEV void chanred_finish(const ChanRed& r, float (*acc)[CPT], float* part, int cchunk, int pchunk, int lcv, int slot) {
   extern __shared__ __attribute__((aligned(16))) float red[];   // [SPB][2][CVB*CPT]
   const int L = r.CVB * CPT;
   if (slot < r.SPB) {
@@ -183,14 +181,7 @@ XCP_DEV void chanred_finish(const ChanRed& r, float (*acc)[CPT], float* part, in
     float s = 0.f;
     for (int q = 0; q < r.SPB; ++q) s += red[(q * 2 + k) * L + cl];
     const int c = cchunk * L + cl;
-    if (c < r.C) {
-      if (fin.acc) fin_add(fin.acc + k * fin.CP + c, s);
-      else part[((long)pchunk * 2 + k) * r.C + c] = s;
-    }
-  }
-  if (fin.acc) {
-    __shared__ int last;
-    if (fin_arrive(fin, &last)) fin_finalize(fin, threadIdx.x, 256);
+    if (c < r.C) part[((long)pchunk * 2 + k) * r.C + c] = s;
   }
 }
 
@@ -219,7 +210,7 @@ template <> struct RawVec<float, 1> { typedef unsigned type; };
 template <typename T, int MODE, int CPT>
 __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av, const void* Bv, const float* mean,
                                                       const float* invstd, const float* ms, const float* mt,
-                                                      float* part, BnFin fin) {
+                                                      float* part) {
   const int cchunk = blockIdx.x % r.nch, pchunk = blockIdx.x / r.nch;
   const int lcv = threadIdx.x % r.CVB, slot = threadIdx.x / r.CVB;
   const int cv = cchunk * r.CVB + lcv;
@@ -284,7 +275,7 @@ __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av,
       }
     }
   }
-  chanred_finish<CPT>(r, acc, part, cchunk, pchunk, lcv, slot, fin);
+  chanred_finish<CPT>(r, acc, part, cchunk, pchunk, lcv, slot);
 }
 
 // ---------------------------------------------------------------- finalize
@@ -786,7 +777,7 @@ struct QuadRaw {
 template <typename T, int CPT>
 __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc ps, T* __restrict__ dZ,
                                                               const T* __restrict__ Y, const float* mean,
-                                                              const float* invstd, float* part, BnFin fin) {
+                                                              const float* invstd, float* part) {
   using Q = QuadRaw<T, CPT>;
   const int cchunk = blockIdx.x % r.nch, pchunk = blockIdx.x / r.nch;
   const int lcv = threadIdx.x % r.CVB, slot = threadIdx.x / r.CVB;
@@ -860,7 +851,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc
       cur = nxt;
     }
   }
-  chanred_finish<CPT>(r, acc, part, cchunk, pchunk, lcv, slot, fin);
+  chanred_finish<CPT>(r, acc, part, cchunk, pchunk, lcv, slot);
 }
 
 // final: feats[n][c] = mean_{hw} relu(y*s+t)   (fp32 out)
@@ -903,14 +894,13 @@ inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
 template <typename T, int MODE>
 int chanred_launch(long rows, int C, const void* A, const void* B, const float* mean, const float* invstd, float* part,
-                   hipStream_t st, const float* ms = nullptr, const float* mt = nullptr, BnFin fin = BnFin{}) {
+                   hipStream_t st, const float* ms = nullptr, const float* mt = nullptr) {
   constexpr int CPT = 8;
   ChanRed r = make_chanred(rows, C, CPT, 1024);
   const long P = chanred_P(r);
   const size_t smem = (size_t)r.SPB * 2 * r.CVB * CPT * sizeof(float);
-  fin.expected = (unsigned)(P * r.nch);
   hipLaunchKernelGGL((chanred_kernel<T, MODE, CPT>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, A, B, mean,
-                     invstd, ms, mt, part, fin);
+                     invstd, ms, mt, part);
   return (int)hipGetLastError();
 }
 
@@ -1008,42 +998,6 @@ int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mea
   }
   if (dtype == XCP_BF16) return chanred_launch<bf16, 1>(rows, C, dZ, Y, mean, invstd, part, st);
   if (dtype == XCP_F32) return chanred_launch<float, 1>(rows, C, dZ, Y, mean, invstd, part, st);
-  return XCP_EUNSUPPORTED;
-}
-
-// xcp_bn_bwd_reduce with the BN backward finalize folded in: the last workgroup writes the
-// coefficients (alpha, bcoef, delta at the pitch C) and dgamma / dbeta (see include/xcp.h)
-int xcp_bn_bwd_reduce_fin(int dtype, const void* dZ, const void* Y, const float* mean, const float* invstd,
-                          const float* ms, const float* mt, long rows, int C, int Cbn, double* acc, unsigned* ticket,
-                          const float* gamma, float* alpha, float* bcoef, float* delta, float* dgamma, float* dbeta,
-                          int accumulate, hipStream_t st) {
-  if (C % 8 || Cbn <= 0 || Cbn > C || !acc || !ticket || !gamma || !mean || !invstd || !alpha || !bcoef || !delta ||
-      (dgamma == nullptr) != (dbeta == nullptr))
-    return XCP_EINVAL;
-  if ((ms == nullptr) != (mt == nullptr)) return XCP_EINVAL;
-  BnFin f{};
-  f.acc = acc;
-  f.ticket = ticket;
-  f.C = Cbn;
-  f.CP = C;
-  f.bwd = 1;
-  f.count = (double)rows;
-  f.gamma = gamma;
-  f.o0 = alpha;
-  f.o1 = bcoef;
-  f.o2 = delta;
-  f.mean = mean;
-  f.invstd = invstd;
-  f.dgamma = dgamma;
-  f.dbeta = dbeta;
-  f.accumulate = accumulate;
-  if (ms) {
-    if (dtype == XCP_BF16) return chanred_launch<bf16, 2>(rows, C, dZ, Y, mean, invstd, nullptr, st, ms, mt, f);
-    if (dtype == XCP_F32) return chanred_launch<float, 2>(rows, C, dZ, Y, mean, invstd, nullptr, st, ms, mt, f);
-    return XCP_EUNSUPPORTED;
-  }
-  if (dtype == XCP_BF16) return chanred_launch<bf16, 1>(rows, C, dZ, Y, mean, invstd, nullptr, st, nullptr, nullptr, f);
-  if (dtype == XCP_F32) return chanred_launch<float, 1>(rows, C, dZ, Y, mean, invstd, nullptr, st, nullptr, nullptr, f);
   return XCP_EUNSUPPORTED;
 }
 
@@ -1195,61 +1149,23 @@ int xcp_maxpool_bwd_bnred_parts(int N, int H, int W, int C) {
 
 // xcp_maxpool_bwd + the BN-backward reduce of its output against Y [N][H][W][C] in one pass:
 // part[P][2][C] = (sum dz, sum dz*(y-mean)*invstd) partials, as xcp_bn_bwd_reduce
-}  // extern "C"
-namespace {
-int maxpool_bwd_bnred_impl(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
-                           const float* mean, const float* invstd, int N, int H, int W, int C, float* part, BnFin fin,
-                           hipStream_t st) {
+int xcp_maxpool_bwd_bnred(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
+                          const float* mean, const float* invstd, int N, int H, int W, int C, float* part,
+                          hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
   const PoolSrc ps = pool_src(dOut, amax, H, W);
   const ChanRed r = make_chanred((long)N * ps.OH * ps.OW, C, 8, 1024);
   const long P = chanred_P(r);
   const size_t smem = (size_t)r.SPB * 2 * r.CVB * 8 * sizeof(float);
-  fin.expected = (unsigned)(P * r.nch);
   if (dtype == XCP_BF16)
     hipLaunchKernelGGL((maxpool_bwd_red_kernel<bf16, 8>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, ps,
-                       (bf16*)dZ, (const bf16*)Y, mean, invstd, part, fin);
+                       (bf16*)dZ, (const bf16*)Y, mean, invstd, part);
   else if (dtype == XCP_F32)
     hipLaunchKernelGGL((maxpool_bwd_red_kernel<float, 8>), dim3((unsigned)(P * r.nch)), dim3(256), smem, st, r, ps,
-                       (float*)dZ, (const float*)Y, mean, invstd, part, fin);
+                       (float*)dZ, (const float*)Y, mean, invstd, part);
   else
     return XCP_EUNSUPPORTED;
   return (int)hipGetLastError();
-}
-}  // namespace
-extern "C" {
-
-int xcp_maxpool_bwd_bnred(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
-                          const float* mean, const float* invstd, int N, int H, int W, int C, float* part,
-                          hipStream_t st) {
-  return maxpool_bwd_bnred_impl(dtype, dOut, amax, dZ, Y, mean, invstd, N, H, W, C, part, BnFin{}, st);
-}
-
-// xcp_maxpool_bwd_bnred with the BN backward finalize folded in (see include/xcp.h)
-int xcp_maxpool_bwd_bnred_fin(int dtype, const void* dOut, const unsigned char* amax, void* dZ, const void* Y,
-                              const float* mean, const float* invstd, int N, int H, int W, int C, int Cbn, double* acc,
-                              unsigned* ticket, const float* gamma, float* alpha, float* bcoef, float* delta,
-                              float* dgamma, float* dbeta, int accumulate, hipStream_t st) {
-  if (Cbn <= 0 || Cbn > C || !acc || !ticket || !gamma || !mean || !invstd || !alpha || !bcoef || !delta ||
-      (dgamma == nullptr) != (dbeta == nullptr))
-    return XCP_EINVAL;
-  BnFin f{};
-  f.acc = acc;
-  f.ticket = ticket;
-  f.C = Cbn;
-  f.CP = C;
-  f.bwd = 1;
-  f.count = (double)N * H * W;   // the BN's rows: the pooled block's full-resolution tensor
-  f.gamma = gamma;
-  f.o0 = alpha;
-  f.o1 = bcoef;
-  f.o2 = delta;
-  f.mean = mean;
-  f.invstd = invstd;
-  f.dgamma = dgamma;
-  f.dbeta = dbeta;
-  f.accumulate = accumulate;
-  return maxpool_bwd_bnred_impl(dtype, dOut, amax, dZ, Y, mean, invstd, N, H, W, C, nullptr, f, st);
 }
 
 int xcp_avgpool_fwd(int dtype, const void* Y, const float* s, const float* t, float* F, int N, int HW, int C,

@@ -143,96 +143,3 @@ XCP_DEV int xcd_remap(int orig, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
-
-// ---------------------------------------------------------------------------------
-// BatchNorm statistics folded into their producer (no separate finalize launch).
-// Every workgroup of the producing op adds its fp32 partial sums into an fp64 accumulator
-// (device-scope atomics: performed at the memory side, past the per-XCD L2s), waits for them
-// (vmcnt(0): a no-return atomic stays counted until it is performed), and takes a ticket; the
-// workgroup that takes the last ticket reads the sums back with atomic exchanges (which also zero
-// the accumulator for the op's next call), forms the BN outputs in fp64 as the finalize kernels do
-// (bn.hip bn_finalize_part_kernel / bn_bwd_finalize_part_kernel) and resets the ticket.  The
-// accumulator [2][CP] (+ one sink double) and the ticket are caller-owned, zero between ops.
-// Summation order: the fp64 sum of fp32 partials is exact unless a partial is 2^-19 below the
-// largest one; the order can then change its last bits (the fp32 outputs practically never).
-struct BnFin {
-  double* acc;            // [2][CP] + 1 sink (nullptr: fold off)
-  unsigned* ticket;
-  unsigned expected;      // workgroups that arrive over the op's launches
-  int C, CP;              // logical channels, channel pitch (padding channels get zero outputs)
-  int bwd;                // 0: forward statistics; 1: backward coefficients
-  double count;
-  const float* gamma;
-  const float* beta;      // (fwd)
-  float* rmean;           // (fwd; nullptr: no running statistics)
-  float* rvar;
-  float momentum, eps;
-  float* o0;              // fwd: mean   bwd: alpha
-  float* o1;              // fwd: invstd bwd: bcoef
-  float* o2;              // fwd: scale  bwd: delta
-  float* o3;              // fwd: shift
-  const float* mean;      // bwd: the forward statistics
-  const float* invstd;
-  float* dgamma;          // bwd: affine gradients (nullptr: none), accumulated when accumulate
-  float* dbeta;
-  int accumulate;
-};
-
-XCP_DEV void fin_add(double* p, float v) {
-  (void)__hip_atomic_fetch_add(p, (double)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// every thread of the workgroup calls this once, at the end; true in the last workgroup to arrive
-XCP_DEV bool fin_arrive(const BnFin& f, int* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    *flag = __hip_atomic_fetch_add(f.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.expected - 1;
-  __syncthreads();
-  return *flag != 0;
-}
-
-XCP_DEV double fin_take(double* p) {
-  return __hip_atomic_exchange(p, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// the last workgroup: outputs for channels tid, tid + nth, ...
-XCP_DEV void fin_finalize(const BnFin& f, int tid, int nth) {
-  for (int c = tid; c < f.CP; c += nth) {
-    const double s = fin_take(f.acc + c), q = fin_take(f.acc + f.CP + c);
-    if (c >= f.C) {   // padding channel
-      f.o0[c] = f.o1[c] = f.o2[c] = 0.f;
-      if (!f.bwd) f.o3[c] = 0.f;
-      continue;
-    }
-    if (!f.bwd) {
-      const double mean = s / f.count;
-      double var = q / f.count - mean * mean;
-      if (var < 0.0) var = 0.0;
-      if (f.rmean) {
-        const double unb = f.count > 1.0 ? var * f.count / (f.count - 1.0) : var;
-        f.rmean[c] = (float)((1.0 - f.momentum) * f.rmean[c] + f.momentum * mean);
-        f.rvar[c] = (float)((1.0 - f.momentum) * f.rvar[c] + f.momentum * unb);
-      }
-      const float is = (float)(1.0 / sqrt(var + (double)f.eps));
-      const float sc = f.gamma[c] * is;
-      f.o0[c] = (float)mean;
-      f.o1[c] = is;
-      f.o2[c] = sc;
-      f.o3[c] = f.beta[c] - (float)mean * sc;
-    } else {
-      const double is = f.invstd[c], gm = f.gamma[c], mu = f.mean[c];
-      const double a = gm * is;
-      const double mdz = s / f.count, mdzy = q / f.count;
-      f.o0[c] = (float)a;
-      f.o1[c] = (float)(-a * is * mdzy);
-      f.o2[c] = (float)(-a * mdz + a * is * mu * mdzy);
-      if (f.dgamma) {
-        f.dgamma[c] = f.accumulate ? f.dgamma[c] + (float)q : (float)q;
-        f.dbeta[c] = f.accumulate ? f.dbeta[c] + (float)s : (float)s;
-      }
-    }
-  }
-  (void)fin_take(f.acc + 2 * f.CP);   // the sink
-  if (tid == 0) __hip_atomic_exchange(f.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}

@@ -68,44 +68,4 @@ int xcp_clock_probe(long long* out, int blocks, int iters, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-// CU-partitioned streams: a HIP stream whose kernels may only use the CUs selected by a mask
-// (hipExtStreamCreateWithCUMask).  quarters q in 1..3 selects CU c of every XCD with (c mod 4) < q
-// when the mask's bits interleave over the XCDs (bit i: XCD i mod 8, CU i / 8), and CUs
-// [0, 8 q) of every XCD when they are laid out per XCD (bit i: XCD i / 32, CU i mod 32): bit i is
-// set iff ((i / 8) mod 4) < q, which puts q / 4 of every XCD's CUs in the set under either layout.
-// complement = 1 selects the other CUs.  The handle is written to *out (destroy with
-// xcp_stream_destroy).
-int xcp_stream_create_cumask(int quarters, int complement, void** out) {
-  if (quarters < 1 || quarters > 3 || !out) return XCP_EINVAL;
-  int dev = 0, ncu = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return (int)e;
-  e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  if (e != hipSuccess) return (int)e;
-  if (ncu <= 0 || ncu > 1024) return XCP_EUNSUPPORTED;
-  uint32_t mask[32] = {0};
-  const int words = (ncu + 31) / 32;
-  for (int i = 0; i < ncu; ++i) {
-    const bool side = ((i / 8) % 4) < quarters;
-    if (side != (complement != 0)) mask[i / 32] |= 1u << (i % 32);
-  }
-  hipStream_t s = nullptr;
-  e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
-  if (e != hipSuccess) return (int)e;
-  *out = (void*)s;
-  return XCP_OK;
-}
-
-// number of CUs a stream may use (hipExtStreamGetCUMask), or a negative error code
-int xcp_stream_cu_count(void* stream) {
-  uint32_t mask[32] = {0};
-  const hipError_t e = hipExtStreamGetCUMask((hipStream_t)stream, 32, mask);
-  if (e != hipSuccess) return -(int)e;
-  int n = 0;
-  for (int w = 0; w < 32; ++w) n += __builtin_popcount(mask[w]);
-  return n;
-}
-
-int xcp_stream_destroy(void* stream) { return (int)hipStreamDestroy((hipStream_t)stream); }
-
 }  // extern "C"

@@ -292,354 +292,6 @@ int dw_fwd_w2() {
 }
 
 // ---------------------------------------------------------------------------------
-// Pipelined forward (dw_fwd_pipe_kernel): the tile of dw_fwd_w2_kernel, but persistent
-// workgroups (two per CU, 64 KB of LDS each) that stream their tiles through a two-slot LDS ring
-// by LDS-DMA, so a tile's loads are in flight while the previous tile computes and stores.  The
-// one-tile-per-workgroup kernel has loads in flight only during its staging phase (~1/3 of a
-// workgroup's life: ~16 GB/s per CU moved at 19^2 x 736, 0.42 of HBM); here every workgroup keeps
-// the next tile's ~23 KB in flight throughout.
-//   * The DMA lands raw bytes (out-of-frame halo pixels and channels past C read as zeros through
-//     the buffer resource's out-of-range offset).  The producer's BN + ReLU is then applied in
-//     place by one LDS pass over the tile's in-frame chunks (ACT_RELU needs no pass where the halo
-//     is zero: relu(0) = 0, but applies max(., 0) in the same pass), so the register window, the
-//     fma chain and the stored values are exactly those of dw_fwd_w2_kernel.
-//   * Every thread issues the same number of DMA instructions (nd per tile) and of output stores
-//     (ns per tile, masked ones as out-of-range buffer stores), so counted vmcnt waits retire a
-//     tile's DMA without waiting for the previous tile's stores.
-//   * Raw s_barrier / lgkmcnt only (no __syncthreads, whose fence would drain vmcnt).
-constexpr unsigned DBUF_OOB = 0x80000000u;
-constexpr long DBUF_LIMIT = 0x7fffffffL;
-constexpr int DBUF_RECORDS = 0x7fffffff;
-constexpr int DBUF_DWORD3 = 0x00020000;
-constexpr int PIPE_MAXPX = 512;
-constexpr int DW_PIPE_PX = PIPE_MAXPX * SLICE;        // 32 KB of pixel slices per ring slot
-constexpr int DW_PIPE_SLOT = DW_PIPE_PX + 4096;       // + the tile's parameters: scale @0, shift @1 KB, taps (9 x 128 B) @2 KB
-
-XCP_DEV void dvm_wait(int n) {   // s_waitcnt vmcnt(n), n clamped to [0, 63]
-  switch (n < 0 ? 0 : n > 63 ? 63 : n) {
-#define XCP_DVMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    XCP_DVMW(0) XCP_DVMW(1) XCP_DVMW(2) XCP_DVMW(3) XCP_DVMW(4) XCP_DVMW(5) XCP_DVMW(6) XCP_DVMW(7)
-    XCP_DVMW(8) XCP_DVMW(9) XCP_DVMW(10) XCP_DVMW(11) XCP_DVMW(12) XCP_DVMW(13) XCP_DVMW(14) XCP_DVMW(15)
-    XCP_DVMW(16) XCP_DVMW(17) XCP_DVMW(18) XCP_DVMW(19) XCP_DVMW(20) XCP_DVMW(21) XCP_DVMW(22) XCP_DVMW(23)
-    XCP_DVMW(24) XCP_DVMW(25) XCP_DVMW(26) XCP_DVMW(27) XCP_DVMW(28) XCP_DVMW(29) XCP_DVMW(30) XCP_DVMW(31)
-    XCP_DVMW(32) XCP_DVMW(33) XCP_DVMW(34) XCP_DVMW(35) XCP_DVMW(36) XCP_DVMW(37) XCP_DVMW(38) XCP_DVMW(39)
-    XCP_DVMW(40) XCP_DVMW(41) XCP_DVMW(42) XCP_DVMW(43) XCP_DVMW(44) XCP_DVMW(45) XCP_DVMW(46) XCP_DVMW(47)
-    XCP_DVMW(48) XCP_DVMW(49) XCP_DVMW(50) XCP_DVMW(51) XCP_DVMW(52) XCP_DVMW(53) XCP_DVMW(54) XCP_DVMW(55)
-    XCP_DVMW(56) XCP_DVMW(57) XCP_DVMW(58) XCP_DVMW(59) XCP_DVMW(60) XCP_DVMW(61) XCP_DVMW(62) XCP_DVMW(63)
-#undef XCP_DVMW
-  }
-}
-
-typedef int di32x2 __attribute__((ext_vector_type(2)));
-
-// LDS accesses of the pipelined kernel by inline asm, each block carrying its own lgkmcnt wait:
-// hipcc puts an s_waitcnt vmcnt(0) before any compiler-visible LDS access that may alias an LDS-DMA
-// destination, which would retire the next tile's DMA (the ring) at every read.  A load and the wait
-// for it sit in ONE asm statement, so no use or copy of the result can be scheduled between them.
-typedef unsigned du32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned du32x2 __attribute__((ext_vector_type(2)));
-XCP_DEV unsigned dlds(const void* p) { return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)(p); }
-XCP_DEV void lds_ld4x128(const char* p0, const char* p1, const char* p2, const char* p3, du32x4& a, du32x4& b, du32x4& c,
-                         du32x4& d) {
-  asm volatile(
-      "ds_read_b128 %0, %4\n\t"
-      "ds_read_b128 %1, %5\n\t"
-      "ds_read_b128 %2, %6\n\t"
-      "ds_read_b128 %3, %7\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
-      : "v"(dlds(p0)), "v"(dlds(p1)), "v"(dlds(p2)), "v"(dlds(p3))
-      : "memory");
-}
-XCP_DEV void lds_st128(char* p, const du32x4& v) {
-  asm volatile("ds_write_b128 %0, %1" ::"v"(dlds(p)), "v"(v) : "memory");
-}
-XCP_DEV void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// the 3 x 7 window of a 5-pixel segment: rows r0, r1, r2 (byte addresses), pixels k * 64 B apart
-XCP_DEV void lds_win7(const char* r0, const char* r1, const char* r2, du32x2 (&v)[3][7]) {
-  asm volatile(
-      "ds_read_b64 %0, %21\n\t"
-      "ds_read_b64 %1, %21 offset:64\n\t"
-      "ds_read_b64 %2, %21 offset:128\n\t"
-      "ds_read_b64 %3, %21 offset:192\n\t"
-      "ds_read_b64 %4, %21 offset:256\n\t"
-      "ds_read_b64 %5, %21 offset:320\n\t"
-      "ds_read_b64 %6, %21 offset:384\n\t"
-      "ds_read_b64 %7, %22\n\t"
-      "ds_read_b64 %8, %22 offset:64\n\t"
-      "ds_read_b64 %9, %22 offset:128\n\t"
-      "ds_read_b64 %10, %22 offset:192\n\t"
-      "ds_read_b64 %11, %22 offset:256\n\t"
-      "ds_read_b64 %12, %22 offset:320\n\t"
-      "ds_read_b64 %13, %22 offset:384\n\t"
-      "ds_read_b64 %14, %23\n\t"
-      "ds_read_b64 %15, %23 offset:64\n\t"
-      "ds_read_b64 %16, %23 offset:128\n\t"
-      "ds_read_b64 %17, %23 offset:192\n\t"
-      "ds_read_b64 %18, %23 offset:256\n\t"
-      "ds_read_b64 %19, %23 offset:320\n\t"
-      "ds_read_b64 %20, %23 offset:384\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[0][2]), "=&v"(v[0][3]), "=&v"(v[0][4]), "=&v"(v[0][5]), "=&v"(v[0][6]),
-        "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[1][2]), "=&v"(v[1][3]), "=&v"(v[1][4]), "=&v"(v[1][5]), "=&v"(v[1][6]),
-        "=&v"(v[2][0]), "=&v"(v[2][1]), "=&v"(v[2][2]), "=&v"(v[2][3]), "=&v"(v[2][4]), "=&v"(v[2][5]), "=&v"(v[2][6])
-      : "v"(dlds(r0)), "v"(dlds(r1)), "v"(dlds(r2))
-      : "memory");
-}
-// the 3 x 6 window of a 4-pixel segment
-XCP_DEV void lds_win6(const char* r0, const char* r1, const char* r2, du32x2 (&v)[3][6]) {
-  asm volatile(
-      "ds_read_b64 %0, %18\n\t"
-      "ds_read_b64 %1, %18 offset:64\n\t"
-      "ds_read_b64 %2, %18 offset:128\n\t"
-      "ds_read_b64 %3, %18 offset:192\n\t"
-      "ds_read_b64 %4, %18 offset:256\n\t"
-      "ds_read_b64 %5, %18 offset:320\n\t"
-      "ds_read_b64 %6, %19\n\t"
-      "ds_read_b64 %7, %19 offset:64\n\t"
-      "ds_read_b64 %8, %19 offset:128\n\t"
-      "ds_read_b64 %9, %19 offset:192\n\t"
-      "ds_read_b64 %10, %19 offset:256\n\t"
-      "ds_read_b64 %11, %19 offset:320\n\t"
-      "ds_read_b64 %12, %20\n\t"
-      "ds_read_b64 %13, %20 offset:64\n\t"
-      "ds_read_b64 %14, %20 offset:128\n\t"
-      "ds_read_b64 %15, %20 offset:192\n\t"
-      "ds_read_b64 %16, %20 offset:256\n\t"
-      "ds_read_b64 %17, %20 offset:320\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(v[0][0]), "=&v"(v[0][1]), "=&v"(v[0][2]), "=&v"(v[0][3]), "=&v"(v[0][4]), "=&v"(v[0][5]),
-        "=&v"(v[1][0]), "=&v"(v[1][1]), "=&v"(v[1][2]), "=&v"(v[1][3]), "=&v"(v[1][4]), "=&v"(v[1][5]),
-        "=&v"(v[2][0]), "=&v"(v[2][1]), "=&v"(v[2][2]), "=&v"(v[2][3]), "=&v"(v[2][4]), "=&v"(v[2][5])
-      : "v"(dlds(r0)), "v"(dlds(r1)), "v"(dlds(r2))
-      : "memory");
-}
-
-struct DwPipeArgs {
-  DwArgs a;
-  int ntiles;   // N * nth * ntw * ngroups
-  int nd;       // DMA instructions per wave per tile: ceil(HP * WP * 4 / 256)
-  int nit;      // row items per worker per tile: ceil(TH * nseg / 32)
-};
-
-template <int ACT, int SG, int NWV, int NSLOT>
-__global__ __launch_bounds__(NWV * 64) void dw_fwd_pipe_kernel(DwPipeArgs pa) {
-  constexpr int NT = NWV * 64, FS = SLICE, LANES = FS / 8, NWK = NT / LANES, CPL = 4;
-  __shared__ __attribute__((aligned(16))) char ring[NSLOT * DW_PIPE_SLOT];
-  // every field in a local scalar: the lambdas below take them by reference, and a reference to the
-  // kernel-argument struct itself put it in scratch (private memory), with a vmcnt(0) at each use
-  const int H = pa.a.H, W = pa.a.W, C = pa.a.C, ngroups = pa.a.ngroups;
-  const int TH = pa.a.g.TH, TW = pa.a.g.TW, HP = pa.a.g.HP, WP = pa.a.g.WP, ntw = pa.a.g.ntw, nseg = pa.a.g.nseg;
-  const int ntiles = pa.ntiles, ndp = pa.nd, nit = pa.nit;
-  const void* Xp = pa.a.X;
-  void* Yp = pa.a.Y;
-  const float *Wtp = pa.a.Wt, *scp = pa.a.scale, *shp = pa.a.shift;
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cl = tid % LANES, wk = tid / LANES;
-  const int nwg = gridDim.x;
-  const int ntl = pa.a.g.nth * ntw;
-  const int total = HP * WP * 4;   // 16-B chunks of a staged tile
-  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(Xp), (short)0, DBUF_RECORDS,
-                                                                       DBUF_DWORD3);
-  const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(Yp, (short)0, DBUF_RECORDS, DBUF_DWORD3);
-  // tile id -> (channel slice, frame, spatial tile), as block_coords with the logical id
-  auto coords = [&](int id, int& grp, int& n, int& th0, int& tw0) {
-    grp = id % ngroups;
-    const int sp = id / ngroups;
-    const int tile = sp % ntl;
-    n = sp / ntl;
-    th0 = (tile / ntw) * TH;
-    tw0 = (tile % ntw) * TW;
-  };
-  const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Wtp), (short)0, DBUF_RECORDS,
-                                                                       DBUF_DWORD3);
-  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(ACT == ACT_BNRELU ? scp : Wtp), (short)0, DBUF_RECORDS, DBUF_DWORD3);
-  const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(ACT == ACT_BNRELU ? shp : Wtp), (short)0, DBUF_RECORDS, DBUF_DWORD3);
-  // the DMA of tile `id` into ring slot `dst`: nd pixel pieces per wave (wave w's pieces j = w*nd + k),
-  // and by wave 0 two more pieces with the tile's parameters -- scale / shift of its 32 channels
-  // (chunks 0-15) and its 9 x 32 taps (chunks 16-87) -- so that nothing a tile reads is a register
-  // load younger than the DMA in flight (a vmcnt wait for one would drain the ring)
-  auto issue = [&](int id, char* dst) {
-    int grp, n, th0, tw0;
-    coords(id, grp, n, th0, tw0);
-    const int c0 = grp * 32;
-    const long nbase = (long)n * H * W;
-    if (w == 0) {   // (one buffer resource per instruction: a per-lane resource select is a waterfall loop)
-      char* pd = dst + DW_PIPE_PX;
-      if constexpr (ACT == ACT_BNRELU) {
-        const unsigned o = lane < 8 && c0 + lane * 4 < C ? (unsigned)((c0 + lane * 4) * 4) : DBUF_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rS, (__attribute__((address_space(3))) void*)pd, 16, o, 0, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rT, (__attribute__((address_space(3))) void*)(pd + 1024), 16, o, 0, 0, 0);
-      }
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int c = k * 64 + lane, row = c >> 3, ch = c0 + (c & 7) * 4;
-        const unsigned o = c < 72 && ch < C ? (unsigned)(((long)row * C + ch) * 4) : DBUF_OOB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rP, (__attribute__((address_space(3))) void*)(pd + 2048 + k * 1024), 16, o,
-                                                 0, 0, 0);
-      }
-    }
-    for (int k = 0; k < ndp; ++k) {
-      const int j = w * ndp + k;
-      const int c = j * 64 + lane;
-      const int p = c >> 2, q = c & 3;
-      const int hy = p / WP, hx = p - hy * WP;
-      const int h = th0 - 1 + hy, x = tw0 - 1 + hx;
-      const int ch = c0 + q * 8;
-      const bool ok = c < total && h >= 0 && h < H && x >= 0 && x < W && ch < C;
-      const unsigned o = ok ? (unsigned)(((nbase + (long)h * W + x) * C + ch) * 2) : DBUF_OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, o, 0,
-                                               0, 0);
-    }
-  };
-  // one tile: (BN +) ReLU in place, then the 3 x (SG+2) register windows and nit * SG output stores
-  auto work = [&](int id, char* sA) {
-    int grp, n, th0, tw0;
-    coords(id, grp, n, th0, tw0);
-    const int c0 = grp * 32;
-    const long nbase = (long)n * H * W;
-    const float* prm = reinterpret_cast<const float*>(sA + DW_PIPE_PX);   // scale[32] @0, shift[32] @256, taps[9][32] @512
-    if constexpr (ACT != ACT_NONE) {
-      // this thread's chunks are tid + NT k: always channel chunk q = tid & 3
-      const int q = tid & 3;
-      float sc[8], sh[8];
-      if constexpr (ACT == ACT_BNRELU) {
-        du32x4 r[4];
-        lds_ld4x128(reinterpret_cast<const char*>(prm + q * 8), reinterpret_cast<const char*>(prm + q * 8 + 4),
-                    reinterpret_cast<const char*>(prm + 256 + q * 8), reinterpret_cast<const char*>(prm + 256 + q * 8 + 4),
-                    r[0], r[1], r[2], r[3]);
-        VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[0]), sc);
-        VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[1]), sc + 4);
-        VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[2]), sh);
-        VecIO<float, 4>::load(reinterpret_cast<const float*>(&r[3]), sh + 4);
-      }
-      // four chunks per asm read block (out-of-tile chunks read chunk 0 and are not written back)
-      for (int c4 = tid; c4 < total; c4 += 4 * NT) {
-        du32x4 u[4];
-        const int cs[4] = {c4, c4 + NT, c4 + 2 * NT, c4 + 3 * NT};
-        lds_ld4x128(sA + (cs[0] < total ? cs[0] : 0) * 16, sA + (cs[1] < total ? cs[1] : 0) * 16,
-                    sA + (cs[2] < total ? cs[2] : 0) * 16, sA + (cs[3] < total ? cs[3] : 0) * 16, u[0], u[1], u[2], u[3]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = cs[r];
-          const int p = c >> 2;
-          const int hy = p / WP, hx = p - hy * WP;
-          const int h = th0 - 1 + hy, x = tw0 - 1 + hx;
-          // halo / padding chunks stay 0 (relu(bn(0)) need not be)
-          if (c >= total || h < 0 || h >= H || x < 0 || x >= W || c0 + q * 8 >= C) continue;
-          float f[8];
-          VecIO<bf16, 8>::load(reinterpret_cast<const bf16*>(&u[r]), f);
-          typedef float p2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-          for (int e = 0; e < 8; e += 2) {
-            p2 v = p2{f[e], f[e + 1]};
-            if constexpr (ACT == ACT_BNRELU) v = __builtin_elementwise_fma(v, p2{sc[e], sc[e + 1]}, p2{sh[e], sh[e + 1]});
-            v = __builtin_elementwise_max(v, p2(0.f));
-            f[e] = v[0];
-            f[e + 1] = v[1];
-          }
-          VecIO<bf16, 8>::store(reinterpret_cast<bf16*>(&u[r]), f);
-          lds_st128(sA + c * 16, u[r]);
-        }
-      }
-      lds_wait();
-      __builtin_amdgcn_s_barrier();
-    }
-    const int c = c0 + cl * CPL;
-    float wt[9][CPL];
-    {
-      du32x4 r[12];
-      const char* wb = reinterpret_cast<const char*>(prm + 512 + cl * CPL);
-      lds_ld4x128(wb, wb + 128, wb + 256, wb + 384, r[0], r[1], r[2], r[3]);
-      lds_ld4x128(wb + 512, wb + 640, wb + 768, wb + 896, r[4], r[5], r[6], r[7]);
-      lds_ld4x128(wb + 1024, wb + 1024, wb + 1024, wb + 1024, r[8], r[9], r[10], r[11]);
-#pragma unroll
-      for (int t = 0; t < 9; ++t) VecIO<float, CPL>::load(reinterpret_cast<const float*>(&r[t]), wt[t]);
-    }
-    const int items = TH * nseg;
-    const char* lbase = sA + cl * 8;
-    for (int s = 0; s < nit; ++s) {
-      const int it = wk + s * NWK;
-      const bool real = it < items;
-      const int r = real ? it / nseg : 0, sg = real ? it - r * nseg : 0;
-      const int oh = th0 + r;
-      const int x0 = sg * SG;
-      const char* base = lbase + (r * WP + x0) * FS;
-      float win[3][SG + 2][CPL];
-      du32x2 raw[3][SG + 2];
-      if constexpr (SG == 5) lds_win7(base, base + WP * FS, base + 2 * WP * FS, raw);
-      else lds_win6(base, base + WP * FS, base + 2 * WP * FS, raw);
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int k = 0; k < SG + 2; ++k) {
-          unpack(raw[ky][k][0], win[ky][k], (bf16*)nullptr);
-          unpack(raw[ky][k][1], win[ky][k] + 2, (bf16*)nullptr);
-        }
-      const long rowe = (nbase + (long)oh * W + tw0) * C + c;
-#pragma unroll
-      for (int j = 0; j < SG; ++j) {
-        float o[CPL];
-#pragma unroll
-        for (int e = 0; e < CPL; ++e) {
-          float sum = 0.f;
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < 3; ++kx) sum = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], sum);
-          o[e] = sum;
-        }
-        const int x = x0 + j;
-        const bool ok = real && c < C && oh < H && x < TW && tw0 + x < W;
-        const unsigned off = ok ? (unsigned)((rowe + (long)x * C) * 2) : DBUF_OOB;
-        const uint2 v = make_uint2(pack(o, (bf16*)nullptr), pack(o + 2, (bf16*)nullptr));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(di32x2, v), rY, (int)off, 0, 0);
-      }
-    }
-    __builtin_amdgcn_s_barrier();   // every wave is done with this slot before the next DMA into it
-  };
-  const int ns = nit * SG;                    // stores per thread per tile
-  const int nd = ndp + (w == 0 ? (ACT == ACT_BNRELU ? 4 : 2) : 0);   // DMA pieces per wave per tile
-  const int t0 = xcd_remap(blockIdx.x, nwg);
-  if (t0 >= ntiles) return;
-  const int mine = (ntiles - 1 - t0) / nwg + 1;   // tiles of this workgroup: t0 + k nwg, k < mine
-  // prologue: the first NSLOT - 1 tiles in flight
-#pragma unroll
-  for (int k = 0; k < NSLOT - 1; ++k)
-    if (k < mine) issue(t0 + k * nwg, ring + k * DW_PIPE_SLOT);
-  for (int k = 0; k < mine; ++k) {
-    const int kn = k + NSLOT - 1;   // into the slot tile k - 1 has just left (its readers passed a barrier)
-    if (kn < mine) issue(t0 + kn * nwg, ring + (kn % NSLOT) * DW_PIPE_SLOT);
-    // tile k's DMA landed: younger are the stores of tiles k-NSLOT+1 .. k-1 and the DMA of tiles
-    // k+1 .. min(k+NSLOT-1, mine-1) (vmcnt retires in issue order)
-    const int younger = ns * min(NSLOT - 1, k) + nd * (min(kn, mine - 1) - k);
-    dvm_wait(younger);
-    __builtin_amdgcn_s_barrier();   // ... every wave's pieces of it
-    work(t0 + k * nwg, ring + (k % NSLOT) * DW_PIPE_SLOT);
-  }
-}
-
-// XCP_DW_FWD_PIPE=0: the one-tile-per-workgroup kernel; m = 1..4 the pipelined form
-//   1: 4 waves, 2 slots, 2 workgroups per CU     2: 8 waves, 4 slots, 1 per CU
-//   3: 8 waves, 2 slots, 2 per CU                4: 4 waves, 4 slots, 1 per CU
-int dw_fwd_pipe() {   // (read per call: the bitwise test compares both kernels in one process)
-  const char* e = getenv("XCP_DW_FWD_PIPE");
-  const int m = e ? atoi(e) : 0;
-  return m >= 0 && m <= 4 ? m : 0;
-}
-int dw_gpu_cus() {
-  static const int cus = [] {
-    int d = 0, n = 0;
-    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-      n = 0;
-    return n > 0 ? n : 256;
-  }();
-  return cus;
-}
-
-// ---------------------------------------------------------------------------------
 // Fused backward.  Per pixel p:
 //   dA[p]   = sum_tap dY[p - off(tap)] * w[tap]          (transposed 3x3)
 //   dX[p]   = act'(p) * dA[p] + dRes[p] + (p at stride-multiple (h,w) ? dSkip[p/s] : 0)
@@ -669,7 +321,6 @@ struct DwBwdArgs {
   int N, H, W, C, ngroups;
   int nbands, bandH;      // row bands per frame (one wave walks rows [band*bandH, +bandH))
   int xcd;                // 1: consecutive workgroups of the walk on one XCD (xcd_remap)
-  BnFin fin;              // fin.acc: the BN partial sums folded into that BN's backward finalize (common.h)
 };
 
 template <typename T, int P, int FS>
@@ -888,11 +539,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];   // output staging (separate object)
   const int ncg = (a.W + RCOLS - 1) / RCOLS;
   const RowMap mp = row_map(a.N, ncg, a.ngroups, a.nbands, a.xcd != 0);
-  __shared__ int fin_last;
-  if (!mp.live) {   // (a folded finalize: every wave of the workgroup takes part in its arrival)
-    if (a.fin.acc && fin_arrive(a.fin, &fin_last)) fin_finalize(a.fin, threadIdx.x, 256);
-    return;
-  }
+  if (!mp.live) return;
   // this wave's rows [r0, r1); it reads X rows r0 .. r1-1 and dY rows r0-1 .. r1 (rows past
   // those are staged from the zero line: never read)
   const int r0 = mp.band * a.bandH, r1 = min(a.H, r0 + a.bandH);
@@ -910,7 +557,7 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const int x0w = mp.cg * RCOLS, x0 = x0w + sg * RS;
   const RowLanes rl_ld = row_lanes_load<T>(a.W, a.C, x0w, c0, lane);
   const RowLanes rl_st = row_lanes_store<T>(a.W, a.C, x0w, c0, lane);
-  const bool bnsum = a.bnpart != nullptr || a.fin.acc != nullptr;
+  const bool bnsum = a.bnpart != nullptr;
   constexpr bool bnres = RES && BNRES;                  // sums over the final dX against Yb (bnsum implied)
   const bool bnx = bnsum && !bnres;                     // sums over the masked dz against X
   V wt[9], dw[9], sc = V(1.f), sh = V(0.f), bs1 = V(0.f), bs2 = V(0.f), mu = V(0.f), is = V(0.f);
@@ -1165,16 +812,12 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     for (int e = 0; e < EPT; ++e) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) a.dWpart[((long)mp.unit * a.C + c + e) * 9 + t] = red[e][t];
-      if (a.fin.acc) {
-        fin_add(a.fin.acc + c + e, red[e][9]);
-        fin_add(a.fin.acc + a.fin.CP + c + e, red[e][10]);
-      } else if (bnsum) {
+      if (bnsum) {
         a.bnpart[((long)mp.unit * 2 + 0) * a.C + c + e] = red[e][9];
         a.bnpart[((long)mp.unit * 2 + 1) * a.C + c + e] = red[e][10];
       }
     }
   }
-  if (a.fin.acc && fin_arrive(a.fin, &fin_last)) fin_finalize(a.fin, threadIdx.x, 256);
 }
 
 // XCP_DW_BWD_ROLL=1: the rolling-window form for every variant (the round-2 kernel; A/B)
@@ -1286,33 +929,6 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
   if (dtype == XCP_BF16 && dw_fwd_w2()) {
     const int sg = dw_fwd_w2();
     a.g = tile_geo(H, W, FWD_MAXPX, sg);
-    const long span = (long)N * H * W * C * 2;
-    if (dw_fwd_pipe() && span <= DBUF_LIMIT && a.g.HP * a.g.WP <= PIPE_MAXPX) {
-      DwPipeArgs pa{a, a.N * a.g.nth * a.g.ntw * a.ngroups, (a.g.HP * a.g.WP * 4 + 255) / 256,
-                    (a.g.TH * a.g.nseg + 31) / 32};
-      const int mode = dw_fwd_pipe();
-      const int nwv = mode == 2 || mode == 3 ? 8 : 4, wgs = mode == 1 || mode == 3 ? 2 : 1;
-      pa.nd = (a.g.HP * a.g.WP * 4 + 64 * nwv - 1) / (64 * nwv);
-      pa.nit = (a.g.TH * a.g.nseg + nwv * 8 - 1) / (nwv * 8);
-      const int grid = min(pa.ntiles, dw_gpu_cus() * wgs);
-#define XCP_PIPE(SGV, NWV, NSL)                                                                                         \
-      if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_NONE, SGV, NWV, NSL>), dim3(grid), dim3(NWV * 64), 0, stream, pa); \
-      else if (act == ACT_RELU) hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_RELU, SGV, NWV, NSL>), dim3(grid), dim3(NWV * 64), 0, stream, pa); \
-      else hipLaunchKernelGGL((dw_fwd_pipe_kernel<ACT_BNRELU, SGV, NWV, NSL>), dim3(grid), dim3(NWV * 64), 0, stream, pa);
-      if (sg == 4) {
-        XCP_PIPE(4, 4, 2)
-      } else if (mode == 2) {
-        XCP_PIPE(5, 8, 4)
-      } else if (mode == 3) {
-        XCP_PIPE(5, 8, 2)
-      } else if (mode == 4) {
-        XCP_PIPE(5, 4, 4)
-      } else {
-        XCP_PIPE(5, 4, 2)
-      }
-#undef XCP_PIPE
-      return (int)hipGetLastError();
-    }
     const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
 #define XCP_W2(SGV)                                                                                                  \
     if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_w2_kernel<ACT_NONE, FWD_MAXPX, SGV>), dim3(blocks), dim3(256), 0, stream, a); \
@@ -1335,13 +951,12 @@ int xcp_dw_bwd_chunks(int N, int H, int W, int C) {
 static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
                        const float* shift, const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre,
                        void* dX, float* dWpart, float* bnpart, const float* bmean, const float* binvstd, const void* Yb,
-                       int N, int H, int W, int C, hipStream_t stream, BnFin fin = BnFin{}) {
+                       int N, int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
-  const bool sums = bnpart || fin.acc;
   if (Yb) {   // sums over the final dX: needs the residual input, no skip input, and the BN's statistics
-    if (!dRes || dSkip || !sums || !bmean || !binvstd) return XCP_EINVAL;
-  } else if (sums && (act != ACT_BNRELU || !bmean || !binvstd)) {
+    if (!dRes || dSkip || !bnpart || !bmean || !binvstd) return XCP_EINVAL;
+  } else if (bnpart && (act != ACT_BNRELU || !bmean || !binvstd)) {
     return XCP_EINVAL;
   }
   DwBwdArgs a{};
@@ -1353,11 +968,6 @@ static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const 
   a.nbands = dw_bwd_bands(H);
   a.xcd = dw_bwd_xcd();
   a.bandH = (H + a.nbands - 1) / a.nbands;
-  a.fin = fin;
-  if (fin.acc) {   // every workgroup of the launch arrives (launch_bwd_lds: 4 waves per workgroup)
-    const long waves = (long)N * ((W + RCOLS - 1) / RCOLS) * a.nbands * a.ngroups;
-    a.fin.expected = (unsigned)((waves + 3) / 4);
-  }
   if (dtype == XCP_BF16) return launch_bwd_lds<bf16>(act, a, stream);
   if (dtype == XCP_F32) return launch_bwd_lds<float>(act, a, stream);
   return XCP_EUNSUPPORTED;
@@ -1368,35 +978,6 @@ int xcp_dw_bwd(int dtype, int act, const void* dY, const void* X, const float* W
                float* bnpart, const float* bmean, const float* binvstd, int N, int H, int W, int C, hipStream_t stream) {
   return dw_bwd_impl(dtype, act, dY, X, Wt, scale, shift, dRes, dSkip, sOH, sOW, sS, skip_pre, dX, dWpart, bnpart, bmean,
                      binvstd, nullptr, N, H, W, C, stream);
-}
-
-// xcp_dw_bwd with the preceding BN's backward finalize folded in (see include/xcp.h)
-int xcp_dw_bwd_fin(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,
-                   const float* shift, const void* dRes, const void* dSkip, int sOH, int sOW, int sS, int skip_pre,
-                   void* dX, float* dWpart, const float* bmean, const float* binvstd, int N, int H, int W, int C, int Cbn,
-                   double* acc, unsigned* ticket, const float* gamma, float* alpha, float* bcoef, float* delta,
-                   float* dgamma, float* dbeta, int accumulate, hipStream_t stream) {
-  if (Cbn <= 0 || Cbn > C || !acc || !ticket || !gamma || !alpha || !bcoef || !delta ||
-      (dgamma == nullptr) != (dbeta == nullptr))
-    return XCP_EINVAL;
-  BnFin f{};
-  f.acc = acc;
-  f.ticket = ticket;
-  f.C = Cbn;
-  f.CP = C;
-  f.bwd = 1;
-  f.count = (double)N * H * W;
-  f.gamma = gamma;
-  f.o0 = alpha;
-  f.o1 = bcoef;
-  f.o2 = delta;
-  f.mean = bmean;
-  f.invstd = binvstd;
-  f.dgamma = dgamma;
-  f.dbeta = dbeta;
-  f.accumulate = accumulate;
-  return dw_bwd_impl(dtype, act, dY, X, Wt, scale, shift, dRes, dSkip, sOH, sOW, sS, skip_pre, dX, dWpart, nullptr, bmean,
-                     binvstd, nullptr, N, H, W, C, stream, f);
 }
 
 int xcp_dw_bwd_resbn(int dtype, int act, const void* dY, const void* X, const float* Wt, const float* scale,

@@ -103,7 +103,6 @@ struct NTArgs {
   int M, N, K;
   float* stats;           // [gridM][2][N] partial (sum, sumsq) or nullptr
   Gather ga;
-  BnFin fin;              // fin.acc: the statistics folded into the BN finalize instead (common.h)
 };
 
 // ---------------------------------------------------------------------------------
@@ -297,7 +296,7 @@ __global__ __launch_bounds__(WMW * 128) void gemm_nt_kernel(NTArgs a) {
       }
     }
   }
-  if (a.stats || a.fin.acc) {
+  if (a.stats) {
     // threads sharing chunk c: tid = c + CPR*rq; fold rq within the wave, then across waves
 #pragma unroll
     for (int e = 0; e < EPC; ++e)
@@ -323,19 +322,10 @@ __global__ __launch_bounds__(WMW * 128) void gemm_nt_kernel(NTArgs a) {
           t1 += red[(0 * (NTH / 64) + q) * NBN + tid];
           t2 += red[(1 * (NTH / 64) + q) * NBN + tid];
         }
-        if (a.fin.acc) {
-          fin_add(a.fin.acc + nn, t1);
-          fin_add(a.fin.acc + a.fin.CP + nn, t2);
-        } else {
-          a.stats[((long)bm * 2 + 0) * a.N + nn] = t1;
-          a.stats[((long)bm * 2 + 1) * a.N + nn] = t2;
-        }
+        a.stats[((long)bm * 2 + 0) * a.N + nn] = t1;
+        a.stats[((long)bm * 2 + 1) * a.N + nn] = t2;
       }
     }
-  }
-  if (a.fin.acc) {
-    __shared__ int last;
-    if (fin_arrive(a.fin, &last)) fin_finalize(a.fin, tid, NTH);
   }
 }
 
@@ -387,7 +377,7 @@ XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n
     if (mok && c0 < a.N) *reinterpret_cast<uint4*>(crow + c0) = st0;
     if (mok && c0 + 32 < a.N) *reinterpret_cast<uint4*>(crow + c0 + 32) = st1;
   }
-  if (a.stats || a.fin.acc) {
+  if (a.stats) {
     // reduce-scatter of v[32] = (s1[16], s2[16]) over the 16 row lanes
     float u[16], v8[8], v4[4], v2[2];
     const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
@@ -402,14 +392,8 @@ XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n
     // lane fr holds index 2fr, 2fr+1 of v: statistic fr>>3, j = (fr&7)>>1, r = (fr&1)*2 + q
     const int col = ncol + ((fr & 7) >> 1) * 16 + fg * 4 + (fr & 1) * 2;
     const int srow = bm * 2 + wr;
-    if (srow < stat_rows && col < a.N) {
-      if (a.fin.acc) {
-        fin_add(a.fin.acc + (fr >> 3) * a.fin.CP + col, v2[0]);
-        fin_add(a.fin.acc + (fr >> 3) * a.fin.CP + col + 1, v2[1]);
-      } else {
-        *reinterpret_cast<float2*>(a.stats + ((long)srow * 2 + (fr >> 3)) * a.N + col) = make_float2(v2[0], v2[1]);
-      }
-    }
+    if (srow < stat_rows && col < a.N)
+      *reinterpret_cast<float2*>(a.stats + ((long)srow * 2 + (fr >> 3)) * a.N + col) = make_float2(v2[0], v2[1]);
   }
 }
 
@@ -593,10 +577,6 @@ __global__ __launch_bounds__(512) void gemm_nt256k64_kernel(NTArgs a) {
   }
   if (STAG && wr == 0) __builtin_amdgcn_s_barrier();
   epilogue256_regs(acc, a, m0, n0, wr, wc, fr, fg);
-  if (a.fin.acc) {
-    __shared__ int last;
-    if (fin_arrive(a.fin, &last)) fin_finalize(a.fin, tid, 512);
-  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -631,9 +611,8 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // epilogue256_regs with buffer stores (always issued; OOB offset for masked lanes):
-// 16 C stores per lane, + 1 statistics store when STATS == 1, + 2 fp64 atomics (folded BN
-// finalize; masked lanes add to the accumulator's sink) when STATS == 2
-template <int STATS, typename Get>
+// 16 C stores per lane, + 1 statistics store when STATS
+template <bool STATS, typename Get>
 XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC, __amdgpu_buffer_rsrc_t rS, int m0,
                              int n0, int wr, int wc, int fr, int fg) {
   const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
@@ -688,30 +667,21 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     for (int q = 0; q < 2; ++q) v2[q] = (b0 ? v4[2 + q] : v4[q]) + __shfl_xor(b0 ? v4[q] : v4[2 + q], 1, 64);
     const int col = ncol + ((fr & 7) >> 1) * 16 + fg * 4 + (fr & 1) * 2;
     const int srow = bm * 2 + wr;
-    if constexpr (STATS == 2) {
-      const bool ok = srow < stat_rows && col < a.N;
-      double* d = ok ? a.fin.acc + (fr >> 3) * a.fin.CP + col : a.fin.acc + 2 * a.fin.CP;
-      fin_add(d, v2[0]);
-      fin_add(ok ? d + 1 : d, v2[1]);
-    } else {
-      const unsigned so = (srow < stat_rows && col < a.N) ? (unsigned)((((long)srow * 2 + (fr >> 3)) * a.N + col) * 4)
-                                                          : BUF_OOB;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_float2(v2[0], v2[1])), rS, (int)so, 0, 0);
-    }
+    const unsigned so = (srow < stat_rows && col < a.N) ? (unsigned)((((long)srow * 2 + (fr >> 3)) * a.N + col) * 4)
+                                                        : BUF_OOB;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_float2(v2[0], v2[1])), rS, (int)so, 0, 0);
   }
 }
 
-template <int STATS>
+template <bool STATS>
 XCP_DEV void epilogue256_buf(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffer_rsrc_t rC,
                              __amdgpu_buffer_rsrc_t rS, int m0, int n0, int wr, int wc, int fr, int fg) {
   epilogue256_get<STATS>([&](int i, int j, int r) { return acc[i][j][r]; }, a, rC, rS, m0, n0, wr, wc, fr, fg);
 }
 
-template <int STATS>
+template <bool STATS>
 __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
-  // vector-memory instructions per wave per epilogue: 16 stores, + 1 statistics store (STATS 1) or
-  // + 2 fp64 atomics (STATS 2: BN finalize folded in)
-  constexpr int S_ST = 16 + (STATS == 1 ? 1 : STATS == 2 ? 2 : 0);
+  constexpr int S_ST = 16 + (STATS ? 1 : 0);   // store instructions per wave per epilogue
   __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
   const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
   const int tiles = gridM * gridN, nwg = gridDim.x;
@@ -735,7 +705,7 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
                                                                        BUF_DWORD3);
   const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, BUF_RECORDS, BUF_DWORD3);
-  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(STATS == 1 ? (void*)a.stats : a.C, (short)0,
+  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(STATS ? (void*)a.stats : a.C, (short)0,
                                                                        BUF_RECORDS, BUF_DWORD3);
   unsigned voff[4][2];
   auto set_tile = [&](int m0, int n0) {
@@ -787,13 +757,7 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   };
 
   int t = slot;
-  if (t >= tiles) {
-    if constexpr (STATS == 2) {
-      __shared__ int last0;
-      if (fin_arrive(a.fin, &last0)) fin_finalize(a.fin, tid, 512);
-    }
-    return;
-  }
+  if (t >= tiles) return;
   int m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
   set_tile(m0, n0);
 #pragma unroll
@@ -863,10 +827,6 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
     epilogue256_buf<STATS>(acc, a, rC, rS, cm0, cn0, wr, wc, fr, fg);
     if (!more) break;
     extra = S_ST;
-  }
-  if constexpr (STATS == 2) {
-    __shared__ int last;
-    if (fin_arrive(a.fin, &last)) fin_finalize(a.fin, tid, 512);
   }
 }
 
@@ -1312,19 +1272,14 @@ bool tn_big(int dtype, int gmode, int N, int K, int tile) {
 
 extern "C" {
 
-}  // extern "C"
-
-namespace {
-// the gemm_nt op; fin.acc set: the BN finalize folded in (stats must then be null)
-int gemm_nt_impl(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                 float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, BnFin fin,
-                 hipStream_t stream) {
+// C[M,N] = A[M,K] . B[N,K]^T ; see include/xcp.h
+int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
+                float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return XCP_OK;
   if ((K % 8) || (N % 8) || (lda % 8) || (ldb % 8) || (ldc % 8)) return XCP_EINVAL;
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   if (tile < 0 || tile > 4) return XCP_EINVAL;
-  NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}, fin};
-  const bool fold = fin.acc != nullptr;
+  NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
   if (nt_big(dtype, gmode, M, N, K, tile)) {
     // automatic choice (tile 0): the persistent kernel; tile 4: the automatic choice with the
     // one-shot kernel (A/B)
@@ -1342,33 +1297,28 @@ int gemm_nt_impl(int dtype, const void* A, long lda, const void* B, long ldb, vo
     big.M = min(M, mb * 256);
     const bool buf = ((long)(big.M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
     const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
-    const bool pers = persist && buf && cbuf;
-    const int grid1 = pers ? min(mb * gridN, cus) : mb * gridN;
-    const int grid2 = big.M < M ? xcp_cdiv(M - big.M, 128) * xcp_cdiv(N, NBN) : 0;
-    if (fold) big.fin.expected = a.fin.expected = (unsigned)(grid1 + grid2);   // every workgroup of both launches arrives
-    if (pers) {   // persistent: one workgroup per CU walks the tiles
-      if (fold)
-        hipLaunchKernelGGL(gemm_nt256p_kernel<2>, dim3(grid1), dim3(512), 0, stream, big);
-      else if (stats)
-        hipLaunchKernelGGL(gemm_nt256p_kernel<1>, dim3(grid1), dim3(512), 0, stream, big);
+    if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
+      const int grid = min(mb * gridN, cus);
+      if (stats)
+        hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
       else
-        hipLaunchKernelGGL(gemm_nt256p_kernel<0>, dim3(grid1), dim3(512), 0, stream, big);
+        hipLaunchKernelGGL(gemm_nt256p_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
     } else if (buf)
-      hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(grid1), dim3(512), 0, stream, big);
+      hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(mb * gridN), dim3(512), 0, stream, big);
     else
-      hipLaunchKernelGGL(gemm_nt256k64_kernel<false>, dim3(grid1), dim3(512), 0, stream, big);
+      hipLaunchKernelGGL(gemm_nt256k64_kernel<false>, dim3(mb * gridN), dim3(512), 0, stream, big);
     if (big.M < M) {
       NTArgs rest = a;
       rest.M = M - big.M;
       rest.A = reinterpret_cast<const bf16*>(A) + (long)big.M * lda;
       rest.C = reinterpret_cast<bf16*>(C) + (long)big.M * ldc;
       if (stats) rest.stats = stats + (long)(big.M / 128) * 2 * N;
-      hipLaunchKernelGGL((gemm_nt_kernel<bf16, 0, 2, 2>), dim3(grid2), dim3(256), 0, stream, rest);
+      hipLaunchKernelGGL((gemm_nt_kernel<bf16, 0, 2, 2>), dim3(xcp_cdiv(rest.M, 128) * xcp_cdiv(N, NBN)), dim3(256), 0,
+                         stream, rest);
     }
     return (int)hipGetLastError();
   }
   const int grid = xcp_cdiv(M, 128) * xcp_cdiv(N, NBN);
-  if (fold) a.fin.expected = (unsigned)grid;
 #define XCP_NT_LAUNCH(TT)                                                                                       \
   switch (gmode) {                                                                                              \
     case 0: hipLaunchKernelGGL((gemm_nt_kernel<TT, 0, 2, 2>), dim3(grid), dim3(256), 0, stream, a); break;     \
@@ -1385,45 +1335,6 @@ int gemm_nt_impl(int dtype, const void* A, long lda, const void* B, long ldb, vo
   }
 #undef XCP_NT_LAUNCH
   return (int)hipGetLastError();
-}
-}  // namespace
-
-extern "C" {
-
-// C[M,N] = A[M,K] . B[N,K]^T ; see include/xcp.h
-int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                float* stats, int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, hipStream_t stream) {
-  return gemm_nt_impl(dtype, A, lda, B, ldb, C, ldc, M, N, K, stats, gmode, gH, gW, gOH, gOW, gS, gC, tile, BnFin{},
-                      stream);
-}
-
-// gemm_nt with the BatchNorm batch statistics of C's columns finalised in the op (see include/xcp.h)
-int xcp_gemm_nt_bnfin(int dtype, const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K,
-                      int gmode, int gH, int gW, int gOH, int gOW, int gS, int gC, int tile, double* acc,
-                      unsigned* ticket, int Cbn, double count, const float* gamma, const float* beta, float* rmean,
-                      float* rvar, float momentum, float eps, float* mean_o, float* invstd_o, float* scale_o,
-                      float* shift_o, hipStream_t stream) {
-  if (!acc || !ticket || !gamma || !beta || !mean_o || !invstd_o || !scale_o || !shift_o || Cbn <= 0 || Cbn > N ||
-      (rmean == nullptr) != (rvar == nullptr))
-    return XCP_EINVAL;
-  BnFin f{};
-  f.acc = acc;
-  f.ticket = ticket;
-  f.C = Cbn;
-  f.CP = N;
-  f.bwd = 0;
-  f.count = count;
-  f.gamma = gamma;
-  f.beta = beta;
-  f.rmean = rmean;
-  f.rvar = rvar;
-  f.momentum = momentum;
-  f.eps = eps;
-  f.o0 = mean_o;
-  f.o1 = invstd_o;
-  f.o2 = scale_o;
-  f.o3 = shift_o;
-  return gemm_nt_impl(dtype, A, lda, B, ldb, C, ldc, M, N, K, nullptr, gmode, gH, gW, gOH, gOW, gS, gC, tile, f, stream);
 }
 
 // rows of the stats partial array gemm_nt writes ([rows][2][N]): one per 128 output rows for

@@ -118,18 +118,6 @@ STEM_FUSED = os.environ.get("XCP_STEM_FUSED", "1") != "0"
 RESBN = os.environ.get("XCP_RESBN", "0") == "1"
 STEM_WGRAD_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_STEM_WGRAD_SIDE", "1") != "0"
 SIDE_PRIO_LOW = os.environ.get("XCP_SIDE_PRIO", "") == "low"
-# BatchNorm finalizes folded into their producers (include/xcp.h xcp_gemm_nt_bnfin, xcp_bn_bwd_reduce_fin,
-# xcp_maxpool_bwd_bnred_fin): the pointwise / skip GEMMs' statistics, the per-channel BN-backward reduces
-# and the pooled tails' reduces end in their last workgroup's finalize instead of a finalize launch over
-# partial rows.  XCP_BN_FOLD=0: partial rows + finalize launches (A/B, the round-4 path).
-BN_FOLD = os.environ.get("XCP_BN_FOLD", "1") != "0"
-# XCP_SIDE_CUS=q (1..3): the backbone backward runs on two CU-partitioned streams -- the weight
-# gradients on q/4 of every XCD's CUs, the main chain (BN backward, dgrad GEMMs, depthwise backward)
-# on the rest -- instead of two streams competing for every CU (a 160 KB-LDS weight-gradient
-# workgroup can only start on a CU that has drained, and then holds it whole).  0: off.
-SIDE_CUS = int(os.environ.get("XCP_SIDE_CUS", "0"))
-if not 0 <= SIDE_CUS <= 3:
-    raise ValueError("XCP_SIDE_CUS must be 0..3")
 # BN1's backward coefficients before the side-stream conv2 weight gradient is launched
 # (XCP_STEM_BN1_FIRST=0: after it, the round-2 order; A/B)
 STEM_BN1_FIRST = os.environ.get("XCP_STEM_BN1_FIRST", "1") != "0"
@@ -168,14 +156,6 @@ def pc(c):
     return PAD_PITCH.get(c, c)
 
 
-class _Coef:
-    """A BN's backward coefficients already formed by the op that produced its partial sums (a
-    folded finalize), passed where the partial sums used to go"""
-
-    def __init__(self, coef):
-        self.coef = coef
-
-
 class XceptionEngine:
     def __init__(self, model, dtype=torch.bfloat16):
         if dtype not in (torch.float32, torch.bfloat16):
@@ -195,7 +175,6 @@ class XceptionEngine:
         self._packed = {}
         self._packed_bwd_key = None
         self._bufs = {}
-        self._fins = {}   # (BN module, "f" / "b") -> ops.FinBuf of its folded finalize
         self._pack_fwd, self._pack_bwd = ops.PermuteBatch(), ops.PermuteBatch()
 
     @property
@@ -205,10 +184,7 @@ class XceptionEngine:
 
     def _side_stream(self, dev):
         st = getattr(self, "_side", None)
-        if SIDE_CUS and (st is None or st.device != dev):
-            st = self._side = ops.cu_stream(SIDE_CUS, False, dev)
-            self._main_bwd = ops.cu_stream(SIDE_CUS, True, dev)
-        elif st is None or st.device != dev:
+        if st is None or st.device != dev:
             # XCP_SIDE_PRIO=low: the weight-gradient stream at the least priority the device offers
             # (below the default stream's when the range has one), so the dispatcher prefers the
             # main stream's workgroups (A/B; the default creates it at the default priority)
@@ -312,44 +288,25 @@ class XceptionEngine:
     def _empty(self, n, dtype=None):
         return torch.empty(n, device=self.device, dtype=dtype or self.dtype)
 
-    def _fin(self, bnmod, kind, CP):
-        """the FinBuf of BN module ``bnmod``'s folded finalize (kind "f": forward statistics, "b":
-        backward coefficients) at channel pitch CP"""
-        key = (bnmod, kind)
-        f = self._fins.get(key)
-        if f is None or f.CP != CP or f.acc.device != self.device:
-            f = self._fins[key] = ops.FinBuf(CP, self.device)
-        return f
-
-    def _bn_ref_train(self, bnmod):
-        """_bn_ref with the momentum of this call resolved (None: cumulative average), after a pending
-        buffer broadcast (xcp.ddp.broadcast_buffers) has landed"""
-        ref = _bn_ref(bnmod)
-        self.model._xcp_wait_buffers()
-        if ref["momentum"] is None:
-            ref["momentum"] = 1.0 / float(bnmod.num_batches_tracked.item() + 1)
-        return ref
-
     def _bn_stats(self, part, R, C, count, bnmod, train):
         """BN statistics of a C-channel tensor (partials and Stats at its channel pitch)"""
         CP = pc(C)
         s = Stats(CP, self.device)
+        ref = _bn_ref(bnmod)
+        self.model._xcp_wait_buffers()   # a buffer broadcast still in flight (xcp.ddp.broadcast_buffers)
         if train:
-            ops.finalize_stats(part, R, C, count, self._bn_ref_train(bnmod), True, s, CP)
+            if ref["momentum"] is None:
+                ref["momentum"] = 1.0 / float(bnmod.num_batches_tracked.item() + 1)
+            ops.finalize_stats(part, R, C, count, ref, True, s, CP)
         else:
-            self.model._xcp_wait_buffers()   # a buffer broadcast still in flight (xcp.ddp.broadcast_buffers)
-            ops.eval_stats(C, _bn_ref(bnmod), s, self.device, CP)
+            ops.eval_stats(C, ref, s, self.device, CP)
         return s
 
     def _pw(self, A, Wp, M, cout, cin, train, bnmod, lda=None, gather=(0, 0, 0, 0, 0, 1, 0)):
         """pointwise conv at the channel pitches (padded output channels come out zero)"""
         cop, cip = pc(cout), pc(cin)
         Y = self._empty(M * cop)
-        if train and BN_FOLD:   # statistics + finalize inside the GEMM's last workgroup
-            st = Stats(cop, self.device)
-            ops.gemm_nt_bnfin(A, Wp, Y, M, cop, cip, self._bn_ref_train(bnmod), M, cout, st,
-                              self._fin(bnmod, "f", cop), lda=lda, gather=gather, tile=NT_TILE)
-        elif train:
+        if train:
             R = ops.nt_stat_rows(M)
             part = self._empty(R * 2 * cop, torch.float32)
             ops.gemm_nt(A, Wp, Y, M, cop, cip, lda=lda, stats=part, gather=gather, tile=NT_TILE)
@@ -493,18 +450,7 @@ class XceptionEngine:
         if not S["train"]:
             raise RuntimeError("xcp engine backward needs a train-mode forward (batch-stat BatchNorm)")
         with ops.device_guard(dfeat):
-            if not (SIDE_CUS and WGRAD_SIDE_STREAM):
-                return self._backward(S, dfeat, out, notify)
-            # the CU-partitioned pair: the main chain on the complement stream, ordered after the
-            # caller's work and before the caller's next (the tensors it allocates go back to the
-            # caller ordered by those two waits)
-            self._side_stream(dfeat.device)
-            caller, mb = torch.cuda.current_stream(dfeat.device), self._main_bwd
-            mb.wait_stream(caller)
-            with torch.cuda.stream(mb):
-                r = self._backward(S, dfeat, out, notify)
-            caller.wait_stream(mb)
-            return r
+            return self._backward(S, dfeat, out, notify)
 
     def _backward(self, S, dfeat, out, notify):
         pk = self.pack_bwd()
@@ -573,16 +519,13 @@ class XceptionEngine:
         def bn_coef(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
             """BN backward up to its coefficients (alpha, bcoef, delta; at the channel pitch);
             writes the affine grads"""
-            if isinstance(part, _Coef):   # finalised by the producer of the sums (it wrote the affine grads)
-                return part.coef
             P = part[1] if part is not None else 0
             (gw, acc), (gb, acc_b) = g(name + ".weight", (C,)), g(name + ".bias", (C,))
             if acc != acc_b:
                 raise NotImplementedError(f"xcp engine: {name}.weight and .bias must both (or neither) require grad")
-            fin = self._fin(bnmod, "b", pc(C)) if BN_FOLD and part is None else None
             return ops.bn_backward_coef(dZ, Y, rows, C, _bn_ref(bnmod), st, gw, gb,
                                         part=part[0] if part is not None else None, R=P, relu=relu, accumulate=acc,
-                                        CP=pc(C), fin=fin)
+                                        CP=pc(C))
 
         def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
             coef = bn_coef(bnmod, name, dZ, Y, rows, C, st, part, relu)
@@ -590,59 +533,31 @@ class XceptionEngine:
             ops.bn_apply_coef(dZ, Y, dY, coef, st, rows, pc(C), relu)
             return dY
 
-        def pool_coef(u, rec, dOut, amax, dZ, H, W):
-            """the pooled tail's max-pool backward into dZ with the BN backward of unit u (the BN before
-            the pool) reduced and finalised in the same op: returns that BN's coefficients"""
-            (gw, acc), (gb, acc_b) = g(u.bn_name + ".weight", (u.cout,)), g(u.bn_name + ".bias", (u.cout,))
-            if acc != acc_b:
-                raise NotImplementedError(f"xcp engine: {u.bn_name}.weight and .bias must both (or neither) require grad")
-            return ops.maxpool_bwd_bnred_fin(dOut, amax, dZ, rec["y"], rec["st"], N, H, W, pc(u.cout), u.cout,
-                                             _bn_ref(u.bn), gw, gb, self._fin(u.bn, "b", pc(u.cout)), accumulate=acc)
-
         def unit_bwd(u, rec, dZ, H, W, dRes=None, dSkip=None, skip_geom=(0, 0, 1), part=None, prev_st=None,
-                     skip_pre=False, res_bn=None, coef=None, prev_bn=None):
+                     skip_pre=False, res_bn=None):
             """dZ: gradient w.r.t. this unit's BN output (``part``: its fused BN-backward
             partial sums, if the producer emitted them).  Returns (gradient w.r.t. the
             depthwise input after the activation mask (+ residual / skip terms), and -- when
             ``prev_st`` is the Stats of the BN feeding this unit -- that BN's backward partial
-            sums; ``coef``: this unit's BN coefficients, already formed by the producer of dZ).
-            prev_bn = (module, name, channels) of that BN: with BN_FOLD its backward finalize runs in the
-            depthwise backward, which then returns its coefficients (_Coef) instead of the sums."""
-            if isinstance(part, _Coef):
-                coef, part = part.coef, None
+            sums)."""
             M = N * H * W
             dD = self._empty(M * pc(u.cin))
             if FUSED_UNIT_BWD and ops.unit_bwd_rows_per_split(dZ.dtype, M, u.cout, u.cin) > 0:
                 # narrow units: BN apply + pointwise dgrad + wgrad in one pass (dY stays on chip)
-                if coef is None:
-                    coef = bn_coef(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
+                coef = bn_coef(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
                 dst, acc = g(u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
                 ops.unit_bwd(dZ, rec["y"], coef, pk[u.name + ".pwT"], rec["d"], dD, M, u.cout, u.cin, dst, acc)
             else:
-                if coef is not None:
-                    dY = self._empty(M * pc(u.cout))
-                    ops.bn_apply_coef(dZ, rec["y"], dY, coef, rec["st"], M, pc(u.cout))
-                else:
-                    dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
+                dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
                 ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, pc(u.cin), pc(u.cout), tile=NT_TILE)
                 wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
             dX = self._empty(M * pc(u.cin))
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
-            bn_fin = None
-            if BN_FOLD and prev_bn is not None and prev_st is not None and res_bn is None:
-                pbn, pname, pC = prev_bn
-                (gw, pacc), (gb, pacc_b) = g(pname + ".weight", (pC,)), g(pname + ".bias", (pC,))
-                if pacc != pacc_b:
-                    raise NotImplementedError(f"xcp engine: {pname}.weight and .bias must both (or neither) require grad")
-                bn_fin = (self._fin(pbn, "b", pc(pC)), _bn_ref(pbn), pC, gw, gb, pacc)
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
                              pc(u.cin), dRes=dRes, dSkip=dSkip, skip_geom=skip_geom,
                              bn_stats=res_bn[1] if res_bn is not None else prev_st, accumulate=acc,
                              Cw=u.cin, skip_pre=skip_pre, reduce_stream=side if DW_REDUCE_SIDE else None,
-                             keep=keep, batch=rbatch, res_bn_input=res_bn[0] if res_bn is not None else None,
-                             bn_fin=bn_fin)
-            if bn_fin is not None:
-                return dX, _Coef(bnp[0])
+                             keep=keep, batch=rbatch, res_bn_input=res_bn[0] if res_bn is not None else None)
             return dX, (bnp if prev_st is not None or res_bn is not None else None)
 
         # ---- exit flow
@@ -652,7 +567,7 @@ class XceptionEngine:
         u3, u4 = self.exit_units
         dZ4 = self._empty(M * 2048)
         ops.avgpool_bwd(dfeat, e4["y"], e4["st"].scale, e4["st"].shift, dZ4, N, H * W, 2048)
-        dZ3, p3 = unit_bwd(u4, e4, dZ4, H, W, prev_st=e3["st"], prev_bn=(u3.bn, u3.bn_name, u3.cout))
+        dZ3, p3 = unit_bwd(u4, e4, dZ4, H, W, prev_st=e3["st"])
         dX, _ = unit_bwd(u3, e3, dZ3, H, W, part=p3)
         done()
         # ---- blocks, last to first
@@ -660,7 +575,7 @@ class XceptionEngine:
         for k in range(len(self.blocks) - 1, -1, -1):
             prev = (self.blocks[k - 1], S["blocks"][k - 1]) if k > 0 else None
             dX, pre_part, part_in = self._block_bwd(self.blocks[k], S["blocks"][k], dX, N, pk, bn_bwd, unit_bwd,
-                                                    wgrad, part_in, prev, pool_coef=pool_coef if BN_FOLD else None)
+                                                    wgrad, part_in, prev)
             done()
         # ---- stem
         OH1, OW1, OH2, OW2 = S["OH1"], S["OW1"], S["OH2"], S["OW2"]
@@ -722,7 +637,7 @@ class XceptionEngine:
         done()
         return grads
 
-    def _block_bwd(self, b, bs, dOut, N, pk, bn_bwd, unit_bwd, wgrad, part_in=None, prev=None, pool_coef=None):
+    def _block_bwd(self, b, bs, dOut, N, pk, bn_bwd, unit_bwd, wgrad, part_in=None, prev=None):
         """part_in: partial sums of this block's last BN (whose output gradient is dOut), produced by
         the next block's first depthwise backward; prev: (block, forward state) of the block before.
         Returns (gradient w.r.t. the block input, the stem BN2 partials (block1 only), the partial sums
@@ -734,14 +649,9 @@ class XceptionEngine:
         # reduces it for the last unit's BN backward (1.50 vs 1.58 ms with a separate reduce
         # at 147^2 x 128; gathering it inside the BN-backward kernels measured 1.83 / 1.88 ms)
         part = None if b.pool else part_in   # (a pooled tail's backward reduces its last BN itself)
-        last_coef = None                     # (... or, folded, also finalises it: pool_coef)
         if b.pool:
             dZ = self._empty(N * H * W * pc(b.cout))
-            if pool_coef is not None:
-                last_coef = pool_coef(b.units[-1], units[-1], dOut, bs["amax"], dZ, H, W)
-            else:
-                part = ops.maxpool_bwd_bnred(dOut, bs["amax"], dZ, units[-1]["y"], units[-1]["st"], N, H, W,
-                                             pc(b.cout))
+            part = ops.maxpool_bwd_bnred(dOut, bs["amax"], dZ, units[-1]["y"], units[-1]["st"], N, H, W, pc(b.cout))
         else:
             dZ = dOut
         dRes = dSkip = None
@@ -763,11 +673,8 @@ class XceptionEngine:
             dRes = dOut
         for i in range(len(b.units) - 1, -1, -1):
             u, rec = b.units[i], units[i]
-            coef_i = last_coef if i == len(b.units) - 1 else None
             if i > 0:
-                pu = b.units[i - 1]
-                dZ, part = unit_bwd(u, rec, dZ, H, W, part=part, prev_st=units[i - 1]["st"], coef=coef_i,
-                                    prev_bn=(pu.bn, pu.bn_name, pu.cout))
+                dZ, part = unit_bwd(u, rec, dZ, H, W, part=part, prev_st=units[i - 1]["st"])
             else:
                 pre = bs["pre_bn"]
                 # identity-skip boundary: prev's output is BN(y) + its input (no pool after the BN), so
@@ -778,8 +685,7 @@ class XceptionEngine:
                     last = prev[1]["units"][-1]
                     res_bn = (last["y"], last["st"])
                 dZ, out_part = unit_bwd(u, rec, dZ, H, W, dRes=dRes, dSkip=dSkip, skip_geom=skip_geom, part=part,
-                                        prev_st=pre, skip_pre=pre is not None, res_bn=res_bn, coef=coef_i,
-                                        prev_bn=(self.model.bn2, "bn2", 64) if pre is not None else None)
+                                        prev_st=pre, skip_pre=pre is not None, res_bn=res_bn)
                 pre_part = out_part if pre is not None else None
                 prev_part = out_part if res_bn is not None else None
         return dZ, pre_part, prev_part

@@ -5,8 +5,6 @@ below launches a hand-written gfx950 kernel from ``libxcp.so`` on the current
 HIP stream.  There is no CPU or eager-PyTorch fallback: a missing library or a
 non-GPU tensor raises.
 """
-import ctypes
-
 import torch
 
 from . import _lib
@@ -187,7 +185,7 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
 
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
            bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None, keep=None, batch=None,
-           res_bn_input=None, bn_fin=None):
+           res_bn_input=None):
     """Returns (bnpart, P) -- the preceding BN's backward partial sums -- when bn_stats
     (that BN's Stats) is given, else (None, 0).  dW_out receives the weight gradient in the
     nn.Conv2d [C][1][3][3] order (accumulate: added to it); Cw (default C): channels of the
@@ -200,25 +198,13 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
     ordering its stream behind this launch, and keeps the scratch alive through ``keep``).
     res_bn_input (with dRes, no dSkip; bn_stats then the Stats of that BN): the partial sums are
     those of the BN whose output gradient is the final dX (after the residual add) and whose input
-    is res_bn_input -- an identity-skip block boundary (xcp_dw_bwd_resbn).
-    bn_fin = (FinBuf, bn ref, Cbn, dgamma, dbeta, accumulate) with bn_stats: that BN's backward finalize
-    folded in (xcp_dw_bwd_fin); returns (coef [3][C], None) instead of the partial sums."""
+    is res_bn_input -- an identity-skip block boundary (xcp_dw_bwd_resbn)."""
     P = _lib.call("xcp_dw_bwd_chunks", N, H, W, C)
     part = torch.empty(P * C * 9, device=dY.device, dtype=torch.float32)
     bnpart = None
-    coef = None
-    if bn_stats is not None and bn_fin is None:
+    if bn_stats is not None:
         bnpart = torch.empty(P * 2 * C, device=dY.device, dtype=torch.float32)
-    if bn_fin is not None:
-        if bn_stats is None or res_bn_input is not None:
-            raise ValueError("xcp.dw_bwd: bn_fin needs bn_stats and no res_bn_input")
-        fin, bref, Cbn, dgamma, dbeta, bacc = bn_fin
-        coef = torch.empty(3 * C, device=dY.device, dtype=torch.float32)
-        _lib.call("xcp_dw_bwd_fin", DT[dY.dtype], act, _p(dY), _p(X), _p(Wt), _p(scale), _p(shift), _p(dRes), _p(dSkip),
-                  skip_geom[0], skip_geom[1], skip_geom[2], int(skip_pre), _p(dX), _p(part), _p(bn_stats["mean"]),
-                  _p(bn_stats["invstd"]), N, H, W, C, Cbn, _p(fin.acc), _p(fin.ticket), _p(bref["weight"]), _p(coef),
-                  _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta), 1 if bacc else 0, stream())
-    elif res_bn_input is not None:
+    if res_bn_input is not None:
         if dRes is None or dSkip is not None or bn_stats is None:
             raise ValueError("xcp.dw_bwd: res_bn_input needs dRes, no dSkip and the BN's bn_stats")
         _lib.call("xcp_dw_bwd_resbn", DT[dY.dtype], act, _p(dY), _p(X), _p(Wt), _p(scale), _p(shift), _p(dRes),
@@ -244,17 +230,13 @@ def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSki
         else:
             part.record_stream(reduce_stream)
             dW_out.record_stream(reduce_stream)
-    if coef is not None:
-        return coef, None
     return bnpart, (P if bnpart is not None else 0)
 
 
 # ---------------------------------------------------------------- batchnorm
 
 
-import os as _os
-# above this many partial rows, pre-reduce to FIN_GROUPS rows (fp64 sums, fp32 out); XCP_FIN_MAX_ROWS (A/B)
-FIN_MAX_ROWS = int(_os.environ.get("XCP_FIN_MAX_ROWS", "2048"))
+FIN_MAX_ROWS = 2048   # above this many partial rows, pre-reduce to FIN_GROUPS rows (fp64 sums, fp32 out)
 FIN_GROUPS = 256
 
 
@@ -280,30 +262,6 @@ def finalize_stats(part, R, C, count, bn, train, out, CP=None):
               float(bn["eps"]), _p(out["mean"]), _p(out["invstd"]), _p(out["scale"]), _p(out["shift"]), stream())
 
 
-class FinBuf:
-    """The caller-owned state of a folded BN finalize (include/xcp.h *_bnfin / *_fin entry points):
-    an fp64 accumulator [2][CP] + 1 sink and an arrival ticket, zero between ops (the op's last
-    workgroup leaves them zero).  One per BN and direction; ops on one FinBuf must not overlap."""
-
-    def __init__(self, CP, device):
-        self.CP = CP
-        self.acc = torch.zeros(2 * CP + 1, device=device, dtype=torch.float64)
-        self.ticket = torch.zeros(1, device=device, dtype=torch.int32)
-
-
-def gemm_nt_bnfin(A, B, C, M, N, K, bn, count, Cbn, out, fin, lda=None, gather=(0, 0, 0, 0, 0, 1, 0), tile=0):
-    """gemm_nt whose BatchNorm batch statistics of C's columns (Cbn real channels of the N-column
-    pitch) are finalised inside the op: out (Stats) gets mean / invstd / scale / shift, the running
-    statistics are updated (train mode) -- no partial rows, no finalize launch."""
-    dt = DT[A.dtype]
-    track = bn["track"]
-    with _timed("gemm_nt", {"M": M, "N": N, "K": K, "stats": True}):
-        _lib.call("xcp_gemm_nt_bnfin", dt, _p(A), lda or K, _p(B), K, _p(C), N, M, N, K, *gather, tile,
-                  _p(fin.acc), _p(fin.ticket), Cbn, float(count), _p(bn["weight"]), _p(bn["bias"]),
-                  _p(bn["running_mean"]) if track else 0, _p(bn["running_var"]) if track else 0, float(bn["momentum"]),
-                  float(bn["eps"]), _p(out["mean"]), _p(out["invstd"]), _p(out["scale"]), _p(out["shift"]), stream())
-
-
 def _bn_finalize(p2, G, C, count, bn, train, out, CP=None):
     mom = bn["momentum"]
     _lib.call("xcp_bn_finalize", _p(p2), G, C, CP or C, float(count), _p(bn["weight"]), _p(bn["bias"]),
@@ -324,25 +282,17 @@ def row_stats(X, rows, C):
     return part, R
 
 
-def bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False, CP=None,
-                     fin=None):
+def bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False, CP=None):
     """BatchNorm2d backward (train-mode batch stats) up to the per-channel coefficients:
     returns coef fp32 [3][C] (alpha, bcoef, delta: dY = alpha*dZ' + bcoef*Y + delta, dZ' the
     ReLU-masked dZ when relu) and writes (accumulate: adds to) dgamma/dbeta.
     ``part`` ([R][2][CP] partial (sum dz, sum dz*zhat)) may come fused from the
     producer of dZ; otherwise it is reduced here.  relu=True: dZ is the gradient of
     relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift).  CP (default C):
-    channel pitch of dZ / Y; coef then has CP entries per coefficient, zero for the padding.
-    fin (FinBuf, part None): the reduce and the finalize in one op (xcp_bn_bwd_reduce_fin)."""
+    channel pitch of dZ / Y; coef then has CP entries per coefficient, zero for the padding."""
     CP = CP or C
     ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
     dev, dt = Y.device, Y.dtype
-    if part is None and fin is not None:   # reduce + finalize in one op (the last workgroup finalises)
-        coef = torch.empty(3 * CP, device=dev, dtype=torch.float32)
-        _lib.call("xcp_bn_bwd_reduce_fin", DT[dt], _p(dZ), _p(Y), _p(st["mean"]), _p(st["invstd"]), ms, mt, rows, CP, C,
-                  _p(fin.acc), _p(fin.ticket), _p(bn["weight"]), _p(coef), _p(coef[CP:]), _p(coef[2 * CP:]),
-                  _p(dgamma), _p(dbeta), 1 if accumulate else 0, stream())
-        return coef
     if part is None:
         R = _lib.call("xcp_chanred_parts", rows, CP)
         part = torch.empty(R * 2 * CP, device=dev, dtype=torch.float32)
@@ -423,16 +373,6 @@ def maxpool_bwd_bnred(dOut, amax, dZ, Y, st, N, H, W, C):
     _lib.call("xcp_maxpool_bwd_bnred", DT[dOut.dtype], _p(dOut), _p(amax), _p(dZ), _p(Y), _p(st["mean"]),
               _p(st["invstd"]), N, H, W, C, _p(part), stream())
     return part, R
-
-
-def maxpool_bwd_bnred_fin(dOut, amax, dZ, Y, st, N, H, W, C, Cbn, bn, dgamma, dbeta, fin, accumulate=False):
-    """maxpool_bwd_bnred with the BN backward finalize folded in: returns coef [3][C] (alpha,
-    bcoef, delta at the pitch C) and writes (accumulate: adds to) dgamma / dbeta."""
-    coef = torch.empty(3 * C, device=Y.device, dtype=torch.float32)
-    _lib.call("xcp_maxpool_bwd_bnred_fin", DT[dOut.dtype], _p(dOut), _p(amax), _p(dZ), _p(Y), _p(st["mean"]),
-              _p(st["invstd"]), N, H, W, C, Cbn, _p(fin.acc), _p(fin.ticket), _p(bn["weight"]), _p(coef),
-              _p(coef[C:]), _p(coef[2 * C:]), _p(dgamma), _p(dbeta), 1 if accumulate else 0, stream())
-    return coef
 
 
 def avgpool_fwd(Y, s, t, F, N, HW, C):
@@ -626,13 +566,3 @@ def lstm_bwd(dout, dhn, dcn, whh, cst, gates, dgates, B, T, H, kernel=0):
     _lib.call("xcp_lstm_bwd", _p(dout), _p(dhn), _p(dcn), _p(whh), _p(cst), _p(gates), _p(dgates), _p(work), B, T, H,
               kernel, stream())
 
-
-def cu_stream(quarters, complement, device):
-    """A torch stream over a HIP stream restricted to quarters/4 of every XCD's CUs (complement:
-    the other CUs), xcp_stream_create_cumask.  The HIP stream lives as long as the process."""
-    h = ctypes.c_void_p()
-    with torch.cuda.device(device):
-        _lib.call("xcp_stream_create_cumask", int(quarters), int(bool(complement)), ctypes.byref(h))
-    s = torch.cuda.ExternalStream(h.value, device=device)
-    s._xcp_cus = _lib.call("xcp_stream_cu_count", h.value)
-    return s

@@ -18,9 +18,6 @@ import torch.nn as nn
 
 # value the fake kernels write into every gradient they produce (rank-dependent under gloo)
 FILL = {"v": 1.0}
-# folded BN finalizes: entry point -> (index of Cbn, index of dgamma (dbeta follows), index of accumulate)
-FIN_AFFINE = {"xcp_bn_bwd_reduce_fin": (9, 16, 18), "xcp_maxpool_bwd_bnred_fin": (11, 18, 20),
-              "xcp_dw_bwd_fin": (21, 28, 30)}
 
 
 def _fill(ptr, n, acc):
@@ -50,10 +47,6 @@ def install_fake_lib(monkeypatch):
         elif name == "xcp_bn_bwd_finalize_part" and args[11]:   # dgamma, dbeta (C each)
             _fill(args[11], args[2], args[13])
             _fill(args[12], args[2], args[13])
-        elif name in FIN_AFFINE and args[FIN_AFFINE[name][1]]:   # folded finalizes: dgamma, dbeta (Cbn each)
-            c, dg, acc = FIN_AFFINE[name]
-            _fill(args[dg], args[c], args[acc])
-            _fill(args[dg + 1], args[c], args[acc])
         elif name == "xcp_permute3" and args[0] == 0:          # fp32 permute (stem conv2 gradient)
             _fill(args[2], args[3] * args[4] * args[5], False)
         if name == "xcp_dw_bwd_chunks":
@@ -119,13 +112,12 @@ def fake_lib(monkeypatch):
 
 @pytest.mark.parametrize("prec", ["bf16", "fp32"])
 @pytest.mark.parametrize("unfrozen", [False, True])
-@pytest.mark.parametrize("resbn,fold", [(False, True), (True, True), (False, False)])
-def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn, fold):
+@pytest.mark.parametrize("resbn", [False, True])
+def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn):
     import xcp
     from xcp import engine as engine_mod
     from Models.XceptionLSTMV import XceptionLSTMV
     monkeypatch.setattr(engine_mod, "RESBN", resbn)
-    monkeypatch.setattr(engine_mod, "BN_FOLD", fold)
     torch.manual_seed(0)
     m = XceptionLSTMV(128, pretrained=False)
     if unfrozen:
@@ -140,23 +132,8 @@ def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn, 
         loss.backward()
     names = set(fake_lib)
     assert {"xcp_gemm_nt", "xcp_dw_fwd", "xcp_tail_fwd", "xcp_avgpool_fwd", "xcp_lstm_fwd", "xcp_lstm_bwd"} <= names
-    # BN finalizes folded into their producers: the 38 pointwise / skip GEMMs finalise
-    # their BNs' statistics; only the stem's bn1 / bn2 keep a finalize launch in the forward (fp32: conv2
-    # is an im2col GEMM, folded too)
-    fwd_fin = fake_lib.count("xcp_bn_finalize_part")
-    assert fwd_fin == ((2 if prec == "bf16" else 1) if fold else 40), fwd_fin
-    assert fake_lib.count("xcp_gemm_nt_bnfin") == ((38 if prec == "bf16" else 39) if fold else 0)
     if unfrozen:
-        bwd = "_fin" if fold else ""
-        assert {"xcp_gemm_tn", "xcp_bn_bwd_reduce" + bwd, "xcp_maxpool_bwd_bnred" + bwd} <= names
-        assert "xcp_dw_bwd" in names or "xcp_dw_bwd_fin" in names
-        # backward: every BN's coefficients come from its reduce / pooled tail / depthwise backward
-        # (fewer than 20 finalize + reduce launches per step), except at RESBN boundaries
-        nfin = fake_lib.count("xcp_bn_bwd_finalize_part")
-        if fold and not resbn:
-            assert nfin == 0 and nfin + fake_lib.count("xcp_bn_bwd_reduce_fin") < 20, nfin
-        elif not fold:
-            assert nfin == 40, nfin
+        assert {"xcp_dw_bwd", "xcp_gemm_tn", "xcp_bn_bwd_reduce", "xcp_maxpool_bwd_bnred"} <= names
         # conv1's weight gradient: BN1's backward apply fused into it in bf16, apply + plain form in fp32
         assert ("xcp_conv1_wgrad_bn" in names) == (prec == "bf16")
         assert ("xcp_conv1_wgrad" in names) == (prec == "fp32")

@@ -290,32 +290,6 @@ def test_gemm_operands_over_2gb_global_address_path(ops, gpu):
     assert rel_err(out.view(C, C), ref) < 1e-3
 
 
-@pytest.mark.parametrize("act", [0, 1, 2])
-@pytest.mark.parametrize("N,C,H,W", [(256, 736, 19, 19), (3, 728, 19, 20), (2, 64, 147, 147), (2, 128, 74, 74),
-                                     (4, 736, 37, 37), (1, 40, 13, 30), (600, 24, 9, 11), (2, 200, 1, 9)])
-def test_dw_fwd_pipelined_bitwise(ops, gpu, monkeypatch, act, N, C, H, W):
-    """The pipelined depthwise forward (persistent workgroups, LDS-DMA ring, BN + ReLU applied in
-    LDS; XCP_DW_FWD_PIPE=1..4: 4 / 8 waves, 2 / 4 ring slots) gives bit for bit the outputs of the
-    one-tile-per-workgroup kernel (XCP_DW_FWD_PIPE=0, the default): the same register window and fma chain.  Shapes: the bench's 256-frame
-    middle flow, ragged channel slices (C = 40, 24, 200), multi-tile frames (147^2, 74^2), more tiles
-    than resident workgroups, non-square frames."""
-    g = torch.Generator(device=gpu).manual_seed(N + C + H + act)
-    x = torch.randn(N * H * W, C, device=gpu, generator=g).to(torch.bfloat16)
-    Wt = torch.randn(9, C, device=gpu, generator=g) / 3
-    sc = torch.rand(C, device=gpu, generator=g) + 0.5
-    sh = torch.randn(C, device=gpu, generator=g) * 0.2
-    outs = []
-    for pipe in ("0", "1", "2", "3", "4"):   # one-tile kernel, then the four ring shapes
-        monkeypatch.setenv("XCP_DW_FWD_PIPE", pipe)
-        Y = torch.full((N * H * W, C), float("nan"), device=gpu, dtype=torch.bfloat16)
-        ops.dw_fwd(act, x, Y, Wt, sc, sh, N, H, W, C)
-        outs.append(Y)
-    torch.cuda.synchronize()
-    assert not torch.isnan(outs[0].float()).any()
-    for o in outs[1:]:
-        assert torch.equal(o, outs[0])
-
-
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("act", [0, 1, 2])
 @pytest.mark.parametrize("N,C,H", [(2, 64, 37), (3, 728, 19), (2, 1536, 10), (1, 128, 9), (1, 64, 147), (2, 256, 74),
@@ -1110,157 +1084,3 @@ def test_permute_batch_plans(ops, gpu):
     torch.cuda.synchronize()
     for dst, ref, _ in want:
         assert torch.equal(dst, ref)
-
-
-def _bnref(C, gpu, g, track=True):
-    gamma, beta = torch.rand(C, device=gpu, generator=g) + 0.5, torch.randn(C, device=gpu, generator=g) * 0.1
-    rm, rv = torch.randn(C, device=gpu, generator=g) * 0.1, torch.rand(C, device=gpu, generator=g) + 0.5
-    return {"weight": gamma, "bias": beta, "running_mean": rm if track else None, "running_var": rv if track else None,
-            "eps": 1e-5, "momentum": 0.1, "track": track}
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("M,N,K,C,tile", [(92416, 736, 736, 728, 0), (3 * 361, 736, 736, 728, 0), (5000, 256, 128, 256, 0),
-                                          (70000, 1024, 736, 1024, 3), (4100, 128, 64, 128, 1), (20000, 512, 512, 512, 2)])
-def test_gemm_nt_bnfin_vs_partial_rows(ops, gpu, dt, M, N, K, C, tile):
-    """The BN finalize folded into the pointwise GEMM (xcp_gemm_nt_bnfin: fp64 atomics, the last
-    workgroup finalises) against the partial-row path (gemm_nt stats + the finalize
-    launch) on the same product: same C bit for bit, mean / invstd / scale / shift and running statistics
-    to fp64 summation-order noise, padding channels zero; three calls in a row (the accumulator and
-    the ticket are left zero) -- every kernel form: persistent (+ sparse round), one-shot, 128x128."""
-    from xcp.engine import Stats
-    if dt == torch.float32 and tile != 1:
-        tile = 1
-    g = torch.Generator(device=gpu).manual_seed(M + N)
-    A = torch.randn(M, K, device=gpu, generator=g).to(dt)
-    B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).to(dt)
-    if C < N:
-        B[C:] = 0
-    bn0 = _bnref(C, gpu, g)
-    bn1 = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in bn0.items()}
-    C0 = torch.empty(M, N, device=gpu, dtype=dt)
-    part = torch.empty(ops.nt_stat_rows(M) * 2 * N, device=gpu)
-    ops.gemm_nt(A, B, C0, M, N, K, stats=part, tile=tile)
-    s0 = Stats(N, gpu)
-    ops.finalize_stats(part, ops.nt_stat_rows(M), C, M, bn0, True, s0, N)
-    fin = ops.FinBuf(N, gpu)
-    for rep in range(3):
-        C1 = torch.full((M, N), float("nan"), device=gpu, dtype=dt)
-        s1 = Stats(N, gpu)
-        ops.gemm_nt_bnfin(A, B, C1, M, N, K, bn1, M, C, s1, fin, tile=tile)
-        torch.cuda.synchronize()
-        assert torch.equal(C1, C0)
-        for k in ("mean", "invstd", "scale", "shift"):
-            torch.testing.assert_close(s1[k][:C], s0[k][:C], rtol=2e-6, atol=1e-6)
-            assert torch.all(s1[k][C:] == 0), k
-        assert torch.all(fin.acc == 0) and int(fin.ticket.item()) == 0
-        if rep == 0:
-            torch.testing.assert_close(bn1["running_mean"], bn0["running_mean"], rtol=1e-6, atol=1e-7)
-            torch.testing.assert_close(bn1["running_var"], bn0["running_var"], rtol=1e-6, atol=1e-7)
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("relu", [False, True])
-@pytest.mark.parametrize("rows,C,CP", [(92416, 728, 736), (100000, 128, 128), (50, 2048, 2048)])
-def test_bn_bwd_reduce_fin_vs_partial_rows(ops, gpu, dt, relu, rows, C, CP):
-    """The BN backward reduce with its finalize folded in (xcp_bn_bwd_reduce_fin) against reduce +
-    finalize launch: coefficients and affine gradients (plain and accumulate) to fp64 summation noise."""
-    from xcp.engine import Stats
-    g = torch.Generator(device=gpu).manual_seed(rows + C)
-    y = torch.zeros(rows, CP, device=gpu, dtype=dt)
-    dz = torch.zeros(rows, CP, device=gpu, dtype=dt)
-    y[:, :C] = (torch.randn(rows, C, device=gpu, generator=g) * 2 + 0.7).to(dt)
-    dz[:, :C] = torch.randn(rows, C, device=gpu, generator=g).to(dt)
-    bn = _bnref(C, gpu, g)
-    st = Stats(CP, gpu)
-    part, R = ops.row_stats(y, rows, CP)
-    ops.finalize_stats(part, R, C, rows, bn, True, st, CP)
-    fin = ops.FinBuf(CP, gpu)
-    for acc in (False, True):
-        dg0, db0 = torch.randn(C, device=gpu, generator=g), torch.randn(C, device=gpu, generator=g)
-        dg1, db1 = dg0.clone(), db0.clone()
-        c0 = ops.bn_backward_coef(dz, y, rows, C, bn, st, dg0, db0, relu=relu, accumulate=acc, CP=CP)
-        c1 = ops.bn_backward_coef(dz, y, rows, C, bn, st, dg1, db1, relu=relu, accumulate=acc, CP=CP, fin=fin)
-        torch.cuda.synchronize()
-        torch.testing.assert_close(c1, c0, rtol=2e-6, atol=1e-7)
-        torch.testing.assert_close(dg1, dg0, rtol=1e-6, atol=1e-5)
-        torch.testing.assert_close(db1, db0, rtol=1e-6, atol=1e-5)
-        assert torch.all(c1.view(3, CP)[:, C:] == 0)
-        assert torch.all(fin.acc == 0) and int(fin.ticket.item()) == 0
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("N,C,H,CP", [(256, 728, 19, 736), (3, 128, 37, 128), (2, 1024, 10, 1024)])
-def test_dw_bwd_fin_vs_partial_rows(ops, gpu, dt, N, C, H, CP):
-    """The depthwise backward with the preceding BN's backward finalize folded in (xcp_dw_bwd_fin)
-    against its partial sums + finalize launch: same dX and weight gradient bit for bit, coefficients and
-    affine gradients to fp64 summation noise."""
-    from xcp.engine import Stats
-    W = H
-    g = torch.Generator(device=gpu).manual_seed(N + C + H)
-    M = N * H * W
-    x = torch.zeros(M, CP, device=gpu, dtype=dt)
-    dy = torch.zeros(M, CP, device=gpu, dtype=dt)
-    x[:, :C] = torch.randn(M, C, device=gpu, generator=g).to(dt)
-    dy[:, :C] = torch.randn(M, C, device=gpu, generator=g).to(dt)
-    Wt = torch.zeros(9, CP, device=gpu)
-    Wt[:, :C] = torch.randn(9, C, device=gpu, generator=g) / 3
-    bn = _bnref(C, gpu, g)
-    st = Stats(CP, gpu)
-    part, R = ops.row_stats(x, M, CP)
-    ops.finalize_stats(part, R, C, M, bn, True, st, CP)
-    outs = []
-    fin = ops.FinBuf(CP, gpu)
-    for fold in (False, True):
-        dX = torch.full((M, CP), float("nan"), device=gpu, dtype=dt)
-        dW = torch.empty(C, 1, 3, 3, device=gpu)
-        dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
-        if fold:
-            coef, _ = ops.dw_bwd(2, dy, x, Wt, st.scale, st.shift, dX, dW, N, H, W, CP, bn_stats=st, Cw=C,
-                                 bn_fin=(fin, bn, C, dg, db, False))
-        else:
-            bnp, P = ops.dw_bwd(2, dy, x, Wt, st.scale, st.shift, dX, dW, N, H, W, CP, bn_stats=st, Cw=C)
-            coef = ops.bn_backward_coef(dX, x, M, C, bn, st, dg, db, part=bnp, R=P, CP=CP)
-        outs.append((dX, dW, coef, dg, db))
-    torch.cuda.synchronize()
-    (dX0, dW0, c0, g0, b0), (dX1, dW1, c1, g1, b1) = outs
-    assert torch.equal(dX1, dX0) and torch.equal(dW1, dW0)
-    torch.testing.assert_close(c1, c0, rtol=2e-6, atol=1e-7)
-    torch.testing.assert_close(g1, g0, rtol=1e-6, atol=1e-5)
-    torch.testing.assert_close(b1, b0, rtol=1e-6, atol=1e-5)
-    assert torch.all(fin.acc == 0) and int(fin.ticket.item()) == 0
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("N,C,H", [(256, 128, 147), (4, 736, 37), (3, 1024, 19)])
-def test_maxpool_bwd_bnred_fin_vs_partial_rows(ops, gpu, dt, N, C, H):
-    """The pooled tail's backward with its BN's backward finalize folded in (xcp_maxpool_bwd_bnred_fin)
-    against the fused reduce's partial sums + finalize launch."""
-    from xcp.engine import Stats
-    g = torch.Generator(device=gpu).manual_seed(N + C + H)
-    OH = (H - 1) // 2 + 1
-    y = torch.randn(N * H * H, C, device=gpu, generator=g).to(dt)
-    d = torch.randn(N * OH * OH, C, device=gpu, generator=g).to(dt)
-    s1, t1 = torch.rand(C, device=gpu, generator=g) + 0.5, torch.randn(C, device=gpu, generator=g)
-    ys = torch.randn(N * OH * OH, C, device=gpu, generator=g).to(dt)
-    out = torch.empty(N * OH * OH, C, device=gpu, dtype=dt)
-    amax = torch.empty(N * OH * OH * C, device=gpu, dtype=torch.uint8)
-    ops.tail_fwd(y, s1, t1, True, ys, None, None, out, amax, N, H, H, C)
-    bn = _bnref(C, gpu, g)
-    st = Stats(C, gpu)
-    part, R = ops.row_stats(y, N * H * H, C)
-    ops.finalize_stats(part, R, C, N * H * H, bn, True, st, C)
-    rows = N * H * H
-    dz0, dz1 = torch.empty(rows, C, device=gpu, dtype=dt), torch.full((rows, C), float("nan"), device=gpu, dtype=dt)
-    p0, R0 = ops.maxpool_bwd_bnred(d, amax, dz0, y, st, N, H, H, C)
-    dg0, db0 = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
-    c0 = ops.bn_backward_coef(dz0, y, rows, C, bn, st, dg0, db0, part=p0, R=R0)
-    fin = ops.FinBuf(C, gpu)
-    dg1, db1 = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
-    c1 = ops.maxpool_bwd_bnred_fin(d, amax, dz1, y, st, N, H, H, C, C, bn, dg1, db1, fin)
-    torch.cuda.synchronize()
-    assert torch.equal(dz1, dz0)
-    torch.testing.assert_close(c1, c0, rtol=2e-6, atol=1e-7)
-    torch.testing.assert_close(dg1, dg0, rtol=1e-6, atol=1e-5)
-    torch.testing.assert_close(db1, db0, rtol=1e-6, atol=1e-5)
-    assert torch.all(fin.acc == 0) and int(fin.ticket.item()) == 0

@@ -647,12 +647,8 @@ def test_xception_frame_step_vs_reference(gpu, golden, fname, prec):
     np.testing.assert_allclose(tot, g["total_gradnorm"], rtol=1e-3 if f32 else 5e-2)
     assert opt.step() is None
     torch.cuda.synchronize()
-    # (B = 4 frames: more near-zero gradient elements whose sign fp32 rounding decides.  fp32: up to 1 % of a
-    # parameter's elements; the engine's BN sums are exact fp64 since the folded finalizes of round 5, and
-    # 1-ulp differences in the BN statistics alone move C2's count from 3 to 4 of 728 elements on
-    # block4.rep.5.bias -- profiles/r05_fold_ab.txt: ulp-level forward differences reach 1-3 % of the largest
-    # element of some weight gradients at B = 64 in fp32)
-    check_after_step(m, g, "after_step", 1e-5, 1e-2 if f32 else 0.2)
+    # (B = 4 frames: more near-zero gradient elements whose sign fp32 rounding decides)
+    check_after_step(m, g, "after_step", 1e-5, 5e-3 if f32 else 0.2)
     for n, t in m.state_dict().items():
         if "running_var" in n:
             np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"], rtol=1e-4 if f32 else 2e-2,

@@ -1,4 +1,6 @@
-"""Folded BN finalizes (XCP_BN_FOLD) against the partial-row path on one model step: the same
+"""(Record tool: needs the round-5 commit 57007cf, whose folded finalizes were measured and reverted --
+profiles/r05_fold_ab.txt, r05_fold_step_ab.txt.)
+Folded BN finalizes (XCP_BN_FOLD) against the partial-row path on one model step: the same
 xception(num_classes=1) fp32 / bf16 forward + backward run with engine.BN_FOLD on and off in one
 process; prints, per tensor class, how many elements differ and the largest relative difference.
   python tools/fold_ab.py [B] [S]      (GPU box)"""
