@@ -584,6 +584,23 @@ def main():
                                      "tn_728": lambda name, a: name == "gemm_tn" and a["M"] == frames * hm * hm
                                      and a["N"] == 728 and a["K"] == 728})
         steps = args.steps if mode == modes[0] else max(3, args.steps // 2)
+        order_path = os.environ.get("XCP_BENCH_OP_ORDER")
+        if order_path and mode == modes[0]:
+            # one extra eager step (an additional warm-up step) whose ops are logged in call order with their
+            # launch stream, for tools/prof_summary.py --op-order (shapes of a rocprofv3 trace's launches)
+            oplog = []
+            prev_graph, run.use_graph = run.use_graph, False
+            ops.set_op_log(oplog)
+            try:
+                run.step()
+            finally:
+                ops.set_op_log(None)
+                run.use_graph = prev_graph
+            torch.cuda.synchronize()
+            if rank == 0:
+                main_stream = torch.cuda.current_stream().cuda_stream
+                with open(order_path, "w") as f:
+                    json.dump([dict(d, stream="main" if d["stream"] == main_stream else "side") for d in oplog], f)
         dg = {} if diag is not None else None
         if os.environ.get("XCP_BENCH_STREAM") == "high":   # A/B: the step on a high-priority stream
             hs = torch.cuda.Stream(dev, priority=torch.cuda.Stream.priority_range()[1])

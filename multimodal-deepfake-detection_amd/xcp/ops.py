@@ -65,9 +65,24 @@ def set_kernel_timer(t):
     _timer = t
 
 
+_op_log = None
+
+
+def set_op_log(log):
+    """Record every timed op's integer arguments and launch stream, in call order, into ``log``
+    (a list; None turns it off): bench.py's XCP_BENCH_OP_ORDER dumps one step of it so that
+    tools/prof_summary.py can put shapes on the launches of a rocprofv3 trace."""
+    global _op_log
+    _op_log = log
+
+
 class _timed:
     def __init__(self, op, a):
         self.key = _timer.match(op, a) if _timer is not None else None
+        if _op_log is not None:
+            d = {k: v for k, v in a.items() if isinstance(v, int)}
+            d["op"], d["stream"] = op, torch.cuda.current_stream().cuda_stream
+            _op_log.append(d)
 
     def __enter__(self):
         if self.key is not None:

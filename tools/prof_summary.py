@@ -7,8 +7,14 @@ under a lossy demangled one ("gemm_nt_kernel<bool _Accum, int, E, 2, 2>"); dispa
 therefore grouped on (base name, grid, workgroup, LDS, VGPRs) and labelled with the decoded
 mangled name seen in that group.
 
-usage: python tools/prof_summary.py <kernel_trace.csv | .db | dir> [top]
+With --op-order (the JSON bench.py writes under XCP_BENCH_OP_ORDER=<file>: one step's ops in call
+order with their shapes and launch stream) the weight-gradient GEMM launches of every complete step
+are matched to their op calls, stream by stream, and listed per shape (the middle-flow 728 x 728 one
+is bench.py's roofline_wgrad op).
+
+usage: python tools/prof_summary.py <kernel_trace.csv | .db | dir> [top] [--op-order order.json]
 """
+import json
 import csv
 import glob
 import os
@@ -69,8 +75,14 @@ def load(path):
 
 
 def main():
-    path = sys.argv[1]
-    top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    argv = list(sys.argv[1:])
+    order = None
+    if "--op-order" in argv:
+        i = argv.index("--op-order")
+        order = argv[i + 1]
+        del argv[i:i + 2]
+    path = argv[0]
+    top = int(argv[1]) if len(argv) > 1 else 40
     if os.path.isdir(path):
         cands = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True) + \
             glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
@@ -105,6 +117,9 @@ def main():
               f"{100 * t / total:6.2f}")
     if path.endswith(".csv"):
         contention(path)
+        if order:
+            with open(order) as f:
+                tn_by_shape(path, json.load(f))
 
 
 # the roofline kernels of bench.py, (kernel base name, grid) at the bench's middle-flow shape
@@ -169,6 +184,55 @@ def contention(path):
         print(f"middle-flow forward op (728 x 728 @19^2 + BN statistics): {n} x persistent {m[0]:.1f} us + "
               f"sparse round {m[1]:.1f} us = {m[0] + m[1]:.1f} us of kernel time, {m[2]:.1f} us first start to "
               f"last end (bench.py's live figure: HIP events around the op)")
+
+
+TN_KERNELS = ("gemm_tn256_kernel", "gemm_tn_kernel")
+PEAK_BF16_TF = 2500.0
+
+
+def tn_by_shape(path, order):
+    """Weight-gradient GEMM launches per shape: in each step (opt_adam_kernel to opt_adam_kernel) the
+    gemm_tn launches of the main stream and of the other stream(s) are matched, in start order, to the
+    step's gemm_tn op calls on that stream (one launch per call); steps whose launch count differs from
+    the op log's (the partial first / last step of the trace) are skipped."""
+    with open(path) as f:
+        rows = sorted([(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Stream_Id"))
+                       for r in csv.DictReader(f)], key=lambda r: r[1])
+    if not rows:
+        return
+    main = rows[0][3]
+    want = {k: [d for d in order if d["op"] == "gemm_tn" and d["stream"] == k] for k in ("main", "side")}
+    steps, cur = [], {"main": [], "side": []}
+    for r in rows:
+        if base(r[0]) in TN_KERNELS:
+            cur["main" if r[3] == main else "side"].append(r)
+        if "opt_adam_kernel" in r[0]:
+            steps.append(cur)
+            cur = {"main": [], "side": []}
+    per = defaultdict(list)
+    used = 0
+    for st in steps:
+        if any(len(st[k]) != len(want[k]) for k in want):
+            continue
+        used += 1
+        for k in want:
+            for d, r in zip(want[k], st[k]):
+                ov = any(o[3] != r[3] and o[1] < r[2] and o[2] > r[1] for o in rows if o is not r)
+                per[(k, d["M"], d["N"], d["K"], base(r[0]))].append(((r[2] - r[1]) / 1e3, ov))
+    print(f"\nweight-gradient GEMM per shape ({used} complete steps; flops 2 M N K over the launch; "
+          f"'shared': another stream's kernel overlapped it)")
+    print(f"{'stream':6s} {'M':>9s} {'N':>5s} {'K':>5s} {'kernel':18s} {'n':>4s} {'avg us':>8s} {'alone us':>9s} "
+          f"{'shared us':>9s} {'TF/s':>7s} {'frac':>6s}")
+    for key, v in sorted(per.items(), key=lambda kv: -sum(x for x, _ in kv[1])):
+        k, M, N, K, kern = key
+        d = [x for x, _ in v]
+        al = [x for x, o in v if not o]
+        sh = [x for x, o in v if o]
+        avg = sum(d) / len(d)
+        tf = 2.0 * M * N * K / (avg * 1e-6) / 1e12
+        f = lambda u: f"{sum(u) / len(u):9.1f}" if u else f"{'-':>9s}"   # noqa: E731
+        print(f"{k:6s} {M:9d} {N:5d} {K:5d} {kern[:18]:18s} {len(d):4d} {avg:8.1f} {f(al)} {f(sh)} {tf:7.1f} "
+              f"{tf / PEAK_BF16_TF:6.3f}")
 
 
 if __name__ == "__main__":
