@@ -40,7 +40,8 @@ Buffers.  ``broadcast_buffers`` launches rank 0's BatchNorm running statistics f
 own (one persistent flat buffer: gather, broadcast, scatter back) and hands the completion event to
 every xcp Xception backbone in the module; the main stream waits on it only where the forward first
 reads or writes a running statistic (the stem's BN1 statistics, after conv1 has been enqueued), not
-before the step starts.
+before the step starts.  That is the RCCL form; under gloo (whose wait() blocks the host until the
+side stream has drained) the broadcast completes on the current stream.
 
 Which parameters take part is re-read at every ``zero()``: the reference trains with
 the backbone frozen for three epochs and then unfreezes it (train_visual.py:547-556);
@@ -281,7 +282,11 @@ def broadcast_buffers(module, src=0, use_streams=None):
     if not bufs:
         return
     if use_streams is None:
-        use_streams = bufs[0].is_cuda
+        # RCCL enqueues the broadcast on the side stream; gloo blocks the host in wait() until the side
+        # stream (which waits on the main stream) has drained, so the stream buys nothing there
+        # (XCP_BCAST_STREAMS=0/1 overrides, A/B)
+        env = os.environ.get("XCP_BCAST_STREAMS")
+        use_streams = bufs[0].is_cuda and (env == "1" if env in ("0", "1") else dist.get_backend() == "nccl")
     st = _BCAST.get(module)
     n = sum(b.numel() for b in bufs)
     if st is None or st["flat"].numel() != n or st["flat"].device != bufs[0].device:

@@ -66,7 +66,7 @@ def _worker(rank, world, port, out):
 
     ddp.GradBuckets._launch = logged
     gb.zero()
-    ddp.broadcast_buffers(m)
+    ddp.broadcast_buffers(m, use_streams=True)   # the stream form RCCL takes by default (gloo: the sync form)
     with xcp.precision("fp32"):
         loss = nn.BCELoss()(m(m.extract_features(x, dev)), y)
         loss.backward()
@@ -75,7 +75,7 @@ def _worker(rank, world, port, out):
     torch.cuda.synchronize()
     grads = {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()}
     own_bufs = {n: b.detach().cpu().clone() for n, b in m.named_buffers() if b.is_floating_point()}
-    ddp.broadcast_buffers(m)   # the next step's forward starts from rank 0's buffers
+    ddp.broadcast_buffers(m, use_streams=True)   # the next step's forward starts from rank 0's buffers
     torch.cuda.synchronize()
     bufs = {n: b.detach().cpu().clone() for n, b in m.named_buffers() if b.is_floating_point()}
     out[rank] = {"grads": grads, "bufs": bufs, "own_bufs": own_bufs, "loss": loss.item(),
