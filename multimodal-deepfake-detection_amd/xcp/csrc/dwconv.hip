@@ -133,16 +133,13 @@ XCP_DEV void stage(const T* __restrict__ src, char* dst, const TileGeo& g, long 
   }
 }
 
-// rev: frames walked from the last one down (the producer of the input wrote the last frames last, so
-// they are the ones still in the Infinity Cache)
-XCP_DEV int block_coords(int ngroups, const TileGeo& g, int& grp, int& n, int& th0, int& tw0, int N = 0, int rev = 0) {
+XCP_DEV int block_coords(int ngroups, const TileGeo& g, int& grp, int& n, int& th0, int& tw0) {
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   grp = id % ngroups;
   const int sp = id / ngroups;
   const int ntiles = g.nth * g.ntw;
   const int tile = sp % ntiles;
   n = sp / ntiles;
-  if (rev) n = N - 1 - n;
   th0 = (tile / g.ntw) * g.TH;
   tw0 = (tile % g.ntw) * g.TW;
   return sp;
@@ -156,7 +153,6 @@ struct DwArgs {
   const float* shift;   // [C]
   int N, H, W, C, ngroups;
   TileGeo g;
-  int rev;              // 1: frames in reverse order (block_coords)
 };
 
 // FS: bytes of channels per pixel per workgroup (64, or 128 when the channel pitch is a
@@ -231,7 +227,7 @@ __global__ __launch_bounds__(256) void dw_fwd_w2_kernel(DwArgs a) {
   __shared__ __attribute__((aligned(16))) char sA[MAXPX * FS];
   const TileGeo& g = a.g;
   int grp, n, th0, tw0;
-  block_coords(a.ngroups, g, grp, n, th0, tw0, a.N, a.rev);
+  block_coords(a.ngroups, g, grp, n, th0, tw0);
   const int c0 = grp * (FS / 2);
   const long nbase = (long)n * a.H * a.W;
   const int cl = threadIdx.x % LANES, wk = threadIdx.x / LANES;
@@ -286,12 +282,6 @@ __global__ __launch_bounds__(256) void dw_fwd_w2_kernel(DwArgs a) {
 // at 19^2 x 736, 262 -> 246 at 37^2, 766 -> 733 at 147^2 x 128, bitwise-equal outputs
 // (tools/kbench.py dwshapes fingerprints, profiles/r03_dw_fwd_w2_ab.txt).  XCP_DW_FWD_W2=0 selects
 // dw_fwd_kernel, =4 4-pixel segments (A/B).
-// XCP_DW_FWD_REV=1: the bf16 forward walks frames last to first (A/B; read per call)
-int dw_fwd_rev() {
-  const char* e = getenv("XCP_DW_FWD_REV");
-  return e && e[0] == '1' ? 1 : 0;
-}
-
 int dw_fwd_w2() {
   static const int v = [] {
     const char* e = getenv("XCP_DW_FWD_W2");
@@ -939,7 +929,6 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
   if (dtype == XCP_BF16 && dw_fwd_w2()) {
     const int sg = dw_fwd_w2();
     a.g = tile_geo(H, W, FWD_MAXPX, sg);
-    a.rev = dw_fwd_rev();
     const int blocks = a.N * a.g.nth * a.g.ntw * a.ngroups;
 #define XCP_W2(SGV)                                                                                                  \
     if (act == ACT_NONE) hipLaunchKernelGGL((dw_fwd_w2_kernel<ACT_NONE, FWD_MAXPX, SGV>), dim3(blocks), dim3(256), 0, stream, a); \
