@@ -38,6 +38,8 @@ SIGNATURES = {
     "xcp_unit_bwd_rows_per_split": [I, I, I, I],
     "xcp_unit_bwd": [I, P, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "xcp_dw_fwd": [I, I, P, P, P, P, P, I, I, I, I, P],
+    "xcp_sep_fwd_parts": [I, I, I, I, I, I],
+    "xcp_sep_fwd": [I, I, P, P, P, P, P, P, P, P, I, I, I, I, I, P],
     "xcp_dw_bwd_chunks": [I, I, I, I],
     "xcp_dw_bwd": [I, I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, I, I, I, I, P],
     "xcp_dw_bwd_resbn": [I, I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
@@ -91,7 +93,7 @@ SIGNATURES = {
 }
 
 # entry points that return a size, not a status
-SIZE_QUERIES = {"xcp_permute3_blocks", "xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
+SIZE_QUERIES = {"xcp_permute3_blocks", "xcp_sep_fwd_parts", "xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
                 "xcp_colreduce_groups", "xcp_unit_bwd_rows_per_split",
                 "xcp_conv1_wgrad_parts", "xcp_conv1_wgrad_fused", "xcp_conv1_fwd_parts", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
                 "xcp_maxpool_bwd_bnred_parts"}

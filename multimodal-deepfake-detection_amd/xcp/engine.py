@@ -140,6 +140,10 @@ DW_REDUCE_SIDE = WGRAD_SIDE_STREAM and os.environ.get("XCP_DW_REDUCE_SIDE", "1")
 REDUCE_BATCH = os.environ.get("XCP_REDUCE_BATCH", "1") != "0"
 # XCP_NT_ONESHOT=1: the big pointwise GEMMs on the one-shot 256x256 kernel instead of its
 # persistent form (gemm.hip tile 4 vs 0; A/B); XCP_NT_TILE=<t> pins any gemm.hip tile choice for them
+# block1's units (147^2, 64 -> 128 and 128 -> 128) run depthwise + pointwise + BN sums as one kernel
+# (csrc/sepfwd.hip): the depthwise output goes to the MFMAs through LDS instead of back through HBM
+# (XCP_SEP_FUSED=0: the two kernels; A/B)
+SEP_FUSED = os.environ.get("XCP_SEP_FUSED", "1") != "0"
 NT_TILE = int(os.environ.get("XCP_NT_TILE", "4" if os.environ.get("XCP_NT_ONESHOT", "0") == "1" else "0"))
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
@@ -413,8 +417,16 @@ class XceptionEngine:
             act, sc, sh = ACT_BNRELU, pre_bn.scale, pre_bn.shift
         for u in b.units:
             d = self._empty(M * pc(u.cin))
-            ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, pc(u.cin))
-            y, st = self._pw(d, pk[u.name + ".pw"], M, u.cout, u.cin, train, u.bn)
+            R = (ops.sep_fwd_parts(self.dtype, N, H, W, u.cin, u.cout)
+                 if SEP_FUSED and train and pc(u.cin) == u.cin and pc(u.cout) == u.cout else 0)
+            if R > 0:
+                y = self._empty(M * u.cout)
+                part = self._empty(R * 2 * u.cout, torch.float32)
+                ops.sep_fwd(act, src, sc, sh, pk[u.name + ".dw"], pk[u.name + ".pw"], d, y, part, N, H, W, u.cin, u.cout)
+                st = self._bn_stats(part, R, u.cout, M, u.bn, True)
+            else:
+                ops.dw_fwd(act, src, d, pk[u.name + ".dw"], sc, sh, N, H, W, pc(u.cin))
+                y, st = self._pw(d, pk[u.name + ".pw"], M, u.cout, u.cin, train, u.bn)
             units.append({"src": src, "act": act, "sc": sc, "sh": sh, "d": d, "y": y, "st": st})
             src, act, sc, sh = y, ACT_BNRELU, st.scale, st.shift
         if b.pool or b.stride != 1:

@@ -198,6 +198,20 @@ def dw_fwd(act, X, Y, Wt, scale, shift, N, H, W, C):
         _lib.call("xcp_dw_fwd", DT[X.dtype], act, _p(X), _p(Y), _p(Wt), _p(scale), _p(shift), N, H, W, C, stream())
 
 
+def sep_fwd_parts(dtype, N, H, W, cin, cout):
+    """BN partial-sum rows of xcp_sep_fwd for this shape (0: not supported by the fused kernel)."""
+    return _lib.call("xcp_sep_fwd_parts", DT[dtype], N, H, W, cin, cout)
+
+
+def sep_fwd(act, X, scale, shift, dwt, pw, D, Y, part, N, H, W, cin, cout):
+    """Fused depthwise 3x3 + pointwise 1x1 (+ BN partial sums of Y) of one entry-flow unit
+    (csrc/sepfwd.hip): D = dw3x3(act(X)), Y = D pw^T, part [R][2][cout]."""
+    check_gpu(X, D, Y)
+    with _timed("sep_fwd", {"N": N, "H": H, "W": W, "C": cin, "CO": cout}):
+        _lib.call("xcp_sep_fwd", DT[X.dtype], act, _p(X), _p(scale), _p(shift), _p(dwt), _p(pw), _p(D), _p(Y), _p(part),
+                  N, H, W, cin, cout, stream())
+
+
 def dw_bwd(act, dY, X, Wt, scale, shift, dX, dW_out, N, H, W, C, dRes=None, dSkip=None, skip_geom=(0, 0, 1),
            bn_stats=None, accumulate=False, Cw=None, skip_pre=False, reduce_stream=None, keep=None, batch=None,
            res_bn_input=None):

@@ -1084,3 +1084,49 @@ def test_permute_batch_plans(ops, gpu):
     torch.cuda.synchronize()
     for dst, ref, _ in want:
         assert torch.equal(dst, ref)
+
+
+@pytest.mark.parametrize("CIN", [64, 128])
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("N,H,W", [(2, 147, 147), (3, 9, 150), (5, 1, 152), (2, 6, 3), (1, 300, 37)])
+def test_sep_fwd_vs_dw_and_gemm(ops, gpu, N, H, W, CIN, act):
+    """Fused depthwise + pointwise forward of block1's units (csrc/sepfwd.hip) against the two kernels it
+    replaces: D bitwise xcp_dw_fwd's, Y bitwise the 128x128 NT kernel's (same MFMA operands and K order),
+    the BN partial sums to fp32 summation order against the NT epilogue's; frames as wide as the kernel
+    takes, one row, three columns (W <= 8 powers of two take dwframe.hip, fp32 windows), more tiles than workgroups and fewer."""
+    g = torch.Generator(device=gpu).manual_seed(N * 1000 + H + W + CIN + act)
+    M = N * H * W
+    X = torch.randn(M, CIN, device=gpu, generator=g).bfloat16()
+    sc = torch.rand(CIN, device=gpu, generator=g) + 0.5
+    sh = torch.randn(CIN, device=gpu, generator=g) * 0.5
+    dwt = torch.randn(9, CIN, device=gpu, generator=g) * 0.3
+    pw = (torch.randn(128, CIN, device=gpu, generator=g) / CIN ** 0.5).bfloat16()
+    D_ref = torch.empty(M, CIN, device=gpu, dtype=torch.bfloat16)
+    ops.dw_fwd(act, X, D_ref, dwt, sc, sh, N, H, W, CIN)
+    Y_ref = torch.empty(M, 128, device=gpu, dtype=torch.bfloat16)
+    R_ref = ops.nt_stat_rows(M)
+    part_ref = torch.zeros(R_ref * 2 * 128, device=gpu)
+    ops.gemm_nt(D_ref, pw, Y_ref, M, 128, CIN, stats=part_ref, tile=1)
+    R = ops.sep_fwd_parts(torch.bfloat16, N, H, W, CIN, 128)
+    assert R == min(N * H, torch.cuda.get_device_properties(gpu).multi_processor_count)
+    D = torch.full((M, CIN), float("nan"), device=gpu, dtype=torch.bfloat16)
+    Y = torch.full((M, 128), float("nan"), device=gpu, dtype=torch.bfloat16)
+    part = torch.full((R * 2 * 128,), float("nan"), device=gpu)
+    ops.sep_fwd(act, X, sc, sh, dwt, pw, D, Y, part, N, H, W, CIN, 128)
+    torch.cuda.synchronize()
+    assert torch.equal(D, D_ref)
+    assert torch.equal(Y, Y_ref)
+    sums = part.view(R, 2, 128).double().sum(0)
+    sums_ref = part_ref.view(R_ref, 2, 128).double().sum(0)
+    yd = Y_ref.double()
+    exact = torch.stack([yd.sum(0), (yd * yd).sum(0)])
+    scale = torch.stack([yd.abs().sum(0), (yd * yd).sum(0)]) + 1e-30
+    assert ((sums - exact).abs() / scale).max().item() < 2e-6
+    assert ((sums_ref - exact).abs() / scale).max().item() < 2e-6
+
+
+def test_sep_fwd_rejects_unsupported(ops, gpu):
+    assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 153, 64, 128) == 0   # wider than 152
+    assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 8, 256, 128) == 0
+    assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 8, 64, 256) == 0
+    assert ops.sep_fwd_parts(torch.float32, 2, 8, 8, 64, 128) == 0
