@@ -5,48 +5,41 @@
 //
 // Unfused, the depthwise output D is written by dw_fwd and read back by the GEMM; here it goes from
 // the depthwise FMAs through LDS straight into the MFMAs (D is still written once: the unit's
-// backward reads it).  Bytes per output pixel: CIN*2 (input) + CIN*2 (D) + 256 (Y), against
+// backward reads it).  HBM bytes per output pixel: CIN*2 (input) + CIN*2 (D) + 256 (Y), against
 // 2*CIN*2 + CIN*2 + 256 for the two kernels.
 //
-// Persistent: one 512-thread workgroup per CU walks output rows (tiles = one row of one frame,
-// consecutive rows of a round on one XCD, so the three staged input rows are shared in L2).  A tile
-// is CIN / 32 jobs of one 32-channel slice each:
-//   * the slice's 3 input rows (W + 2 pixels x 64 B, zero padding by out-of-range buffer offsets)
-//     arrive by LDS-DMA into a 3-slot ring, two jobs ahead (no registers held for the prefetch);
-//   * the input BatchNorm + ReLU of the previous unit is applied in place (padding kept zero) and
-//     rounded to bf16, as dw_fwd's staging does;
-//   * each lane computes 5 pixels x 2 channels of the depthwise conv from a 3 x 7 window, the same
-//     fma chain per channel as dw_fwd_w2_kernel (so D is bitwise dw_fwd's), into an LDS tile
-//     [160 pixels][32 channels];
-//   * wave w accumulates Y[px][16w .. 16w+15] += D[px][slice] W[16w..][slice]^T over the 10 pixel
-//     blocks with v_mfma_f32_16x16x32_bf16 (operands and K order as gemm_nt_kernel: Y bitwise);
-//   * the D slice is stored with 16-B buffer stores; after the last slice Y is stored and its
-//     bf16 values enter per-lane BN sums, which the workgroup writes as one partial row at the end.
-// The ring is read and written by inline asm (a compiler-visible LDS access that may alias an
-// LDS-DMA destination makes hipcc wait for every outstanding vector-memory operation), and every
-// VMEM instruction is issued by every wave whatever its lanes' validity, so the counted waits are
-// exact: at job j the wave waits for the LDS-DMA of job j with the stores of jobs j-2, j-1 and the
-// LDS-DMA of jobs j+1, j+2 still allowed in flight.
+// One 512-thread workgroup per CU walks the rows of a band of one frame (a whole frame when there
+// are at least as many frames as CUs), so every input row is fetched once:
+//   * LDS holds a sliding window of three activated input rows (all CIN channels, W + 2 pixels with
+//     the zero padding); the next row is loaded into registers one output row ahead, activated
+//     (the previous unit's BatchNorm + ReLU, rounded to bf16 as dw_fwd's staging does) and written
+//     over the row that left the window;
+//   * an output row is done in two halves of 80 pixels: each lane computes 5 pixels x 2 channels of
+//     the depthwise conv from a 3 x 7 window (the fma chain per channel of dw_fwd_w2_kernel, so D is
+//     bitwise dw_fwd's) into an LDS tile [80 px][CIN]; wave w then accumulates
+//     Y[px][16w .. 16w+15] += D[px][:] W[16w..][:]^T with v_mfma_f32_16x16x32_bf16 (the weights of
+//     its 16 output channels live in registers; operands and K order as gemm_nt_kernel, so Y is
+//     bitwise the NT GEMM's) and the D tile is stored with 16-B buffer stores;
+//   * the row's Y is stored from the accumulators (8 B per lane) and its bf16 values enter per-lane
+//     BN sums, written as one partial row per workgroup at the end.
+// Every VMEM instruction is a buffer load / store issued by every lane (out-of-range lanes get an
+// offset past the buffer: loads return zero, stores are dropped), so the one counted wait per row --
+// for the prefetched input row, with that row's D and Y stores still in flight -- is exact.
 #include "common.h"
 
 namespace {
 
-constexpr int SP_WMAX = 152;                              // widest frame
-constexpr int SP_ROWPX = SP_WMAX + 2;                     // staged pixels per input row (with padding)
-constexpr int SP_NIN_MAX = (12 * SP_ROWPX + 63) / 64;     // LDS-DMA instructions per slice (29)
-constexpr int SP_SLOT = SP_NIN_MAX * 1024;                // ring slot bytes
-constexpr int SP_PXB = 160;                               // pixel rows of the D tile (10 MFMA blocks)
-constexpr int SP_XP = 80;                                 // D tile pitch (64 B + 16: conflict-free b128 reads)
-constexpr int SP_WP = 272;                                // weight pitch (256 B + 16)
+constexpr int SP_WMAX = 152;                // widest frame
+constexpr int SP_RPX = SP_WMAX + 2;         // staged pixels per input row (with the padding)
+constexpr int SP_HALF = 80;                 // pixels per half row (5 MFMA blocks)
 constexpr int SP_CO = 128;
-constexpr int SP_SEG = 5;                                 // depthwise outputs per lane
+constexpr int SP_SEG = 5;                   // depthwise outputs per lane
 constexpr unsigned SP_OOB = 0x80000000u;
 constexpr int SP_REC = 0x7fffffff;
 constexpr int SP_DW3 = 0x00020000;
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 struct SepArgs {
   const bf16* X;        // [N][H][W][CIN] unit input (before the input transform)
@@ -58,6 +51,7 @@ struct SepArgs {
   bf16* Y;              // [N][H][W][128] pointwise output
   float* part;          // [gridDim.x][2][128] BN partial sums of Y (nullptr: none)
   int N, H, W;
+  int nbands, bandH;    // row bands per frame (tiles = N * nbands)
 };
 
 XCP_DEV void sp_vm_wait(int n) {   // s_waitcnt vmcnt(n), n in [0, 63]
@@ -68,31 +62,11 @@ XCP_DEV void sp_vm_wait(int n) {   // s_waitcnt vmcnt(n), n in [0, 63]
     SP_VMW(16) SP_VMW(17) SP_VMW(18) SP_VMW(19) SP_VMW(20) SP_VMW(21) SP_VMW(22) SP_VMW(23)
     SP_VMW(24) SP_VMW(25) SP_VMW(26) SP_VMW(27) SP_VMW(28) SP_VMW(29) SP_VMW(30) SP_VMW(31)
     SP_VMW(32) SP_VMW(33) SP_VMW(34) SP_VMW(35) SP_VMW(36) SP_VMW(37) SP_VMW(38) SP_VMW(39)
-    SP_VMW(40) SP_VMW(41) SP_VMW(42) SP_VMW(43) SP_VMW(44) SP_VMW(45) SP_VMW(46) SP_VMW(47)
-    SP_VMW(48) SP_VMW(49) SP_VMW(50) SP_VMW(51) SP_VMW(52) SP_VMW(53) SP_VMW(54) SP_VMW(55)
-    SP_VMW(56) SP_VMW(57) SP_VMW(58) SP_VMW(59) SP_VMW(60) SP_VMW(61) SP_VMW(62) SP_VMW(63)
 #undef SP_VMW
+    default: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
   }
 }
 
-// ring accesses (inline asm: see the header)
-XCP_DEV unsigned sp_rd32(const char* p) {
-  unsigned v;
-  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"((unsigned)(size_t)(const __attribute__((address_space(3))) char*)(p))
-               : "memory");
-  return v;
-}
-XCP_DEV u32x4 sp_rd128(const char* p) {
-  u32x4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((unsigned)(size_t)(const __attribute__((address_space(3))) char*)(p))
-               : "memory");
-  return v;
-}
-XCP_DEV void sp_wr128(char* p, u32x4 v) {
-  asm volatile("ds_write_b128 %0, %1" :: "v"((unsigned)(size_t)(__attribute__((address_space(3))) char*)(p)), "v"(v)
-               : "memory");
-}
-XCP_DEV void sp_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 XCP_DEV void sp_barrier() {   // LDS-only workgroup barrier (no vmcnt wait)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -111,210 +85,189 @@ XCP_DEV unsigned sp_pack(float a, float b) {
 
 template <int ACT, int CIN>
 __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
-  constexpr int S = CIN / 32;   // slices (jobs) per tile
-  __shared__ __attribute__((aligned(16))) char ring[3 * SP_SLOT];
-  __shared__ __attribute__((aligned(16))) char sx[2][SP_PXB * SP_XP];
-  __shared__ __attribute__((aligned(16))) char sw[SP_CO * SP_WP];
-  __shared__ float sprm[2][CIN];
-  __shared__ float stap[9][CIN];
+  constexpr int S = CIN / 32;                     // K steps of 32
+  constexpr int CH = CIN / 8;                     // 16-B chunks per pixel
+  constexpr int PB = CIN * 2;                     // bytes per staged pixel
+  constexpr int RB = SP_RPX * PB;                 // bytes per staged row slot
+  constexpr int DP = PB + 16;                     // D tile pitch (conflict-free b128 fragment reads)
+  constexpr int KL = (SP_RPX * CH + 511) / 512;   // input loads per thread per row
+  constexpr int KD = (SP_HALF * CH + 511) / 512;  // D stores per thread per half row
+  constexpr int LPS = CIN / 2;                    // lanes per depthwise segment (2 channels each)
+  constexpr int SPW = 64 / LPS;                   // segments per wave per pass
+  constexpr int NPASS = (SP_HALF / SP_SEG) / (8 * SPW);   // passes per half row (16 segments)
+  constexpr int NST = 2 * KD + 10;                // stores per output row
+  __shared__ __attribute__((aligned(16))) char rows[3 * RB];
+  __shared__ __attribute__((aligned(16))) char dt[SP_HALF * DP];
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
   const int H = a.H, W = a.W;
-  const int T = a.N * H;                      // tiles (frame rows)
-  const int G = gridDim.x;
-  const int slot_id = xcd_remap(blockIdx.x, G);
-  const int ntiles = (T - slot_id + G - 1) / G;
-  const int njobs = ntiles * S;
-  const int rowb = (W + 2) * 64;              // staged row bytes
-  const int nch = 12 * (W + 2);               // 16-B chunks per staged slice
-  const int nin = (nch + 63) >> 6;            // LDS-DMA instructions per slice
-  const int cnt = w < nin ? (nin - w + 7) >> 3 : 0;   // this wave's share
-
+  const int nch = (W + 2) * CH;                   // staged chunks per row
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.X), (short)0, SP_REC, SP_DW3);
   const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(a.D, (short)0, SP_REC, SP_DW3);
   const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, SP_REC, SP_DW3);
 
-  // ---- resident operands: the pointwise weight, the input BN affine, the taps
-  for (int c = tid; c < SP_CO * (CIN / 8); c += 512) {
-    const int r = c / (CIN / 8), k = c % (CIN / 8);
-    *reinterpret_cast<uint4*>(sw + r * SP_WP + k * 16) = *reinterpret_cast<const uint4*>(a.pw + (long)r * CIN + k * 8);
-  }
-  for (int c = tid; c < CIN; c += 512) {
-    sprm[0][c] = ACT == ACT_BNRELU ? a.scale[c] : 1.f;
-    sprm[1][c] = ACT == ACT_BNRELU ? a.shift[c] : 0.f;
-  }
-  for (int c = tid; c < 9 * CIN; c += 512) stap[c / CIN][c % CIN] = a.dwt[c];
-  __syncthreads();
-
-  auto tile_of = [&](int j, int& n, int& h, int& s) {
-    const int r = j / S;
-    s = j - r * S;
-    const int t = r * G + slot_id;
-    n = t / H;
-    h = t - n * H;
-  };
-  // LDS-DMA of job j's slice into ring slot j % 3 (every wave issues its cnt instructions; a job
-  // past the end stages zeros)
-  auto issue = [&](int j) {
-    char* slot = ring + (j % 3) * SP_SLOT;
-    int n = 0, h = 0, s = 0;
-    const bool live = j < njobs;
-    if (live) tile_of(j, n, h, s);
-    for (int m = 0; m < cnt; ++m) {
-      const int k = w + 8 * m;
-      const int i = k * 64 + lane;
-      const int row = i / (4 * (W + 2));
-      const int rem = i - row * 4 * (W + 2);
-      const int px = rem >> 2, q = rem & 3;
-      const int hh = h - 1 + row, ww = px - 1;
-      const bool ok = live && i < nch && hh >= 0 && hh < H && ww >= 0 && ww < W;
-      const unsigned off = ok ? (unsigned)(((((long)n * H + hh) * W + ww) * CIN + s * 32 + q * 8) * 2) : SP_OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rX, (__attribute__((address_space(3))) void*)(slot + k * 1024), 16, off, 0,
-                                               0, 0);
-    }
-  };
-
-  // depthwise lane map: channels 2*cl, 2*cl+1 of the slice; pixels x0 .. x0+4
-  const int cl = tid & 15, x0 = (tid >> 4) * SP_SEG;
-  int wcol[SP_SEG + 2];
+  // ---- per-thread constants: this wave's weights, this lane's taps, this thread's staging channels
+  bf16x8 wf[S];
 #pragma unroll
-  for (int k = 0; k < SP_SEG + 2; ++k) wcol[k] = min(x0 + k, W + 1) * 64 + cl * 4;
-
-  f32x4 acc[10];
+  for (int s = 0; s < S; ++s) wf[s] = *reinterpret_cast<const bf16x8*>(a.pw + (long)(w * 16 + fr) * CIN + s * 32 + fg * 8);
+  const int ch = 2 * (lane % LPS);                // depthwise channels ch, ch + 1
+  float tp[9][2];
 #pragma unroll
-  for (int b = 0; b < 10; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < 9; ++t) {
+    tp[t][0] = a.dwt[t * CIN + ch];
+    tp[t][1] = a.dwt[t * CIN + ch + 1];
+  }
+  const int q = tid % CH;                         // staging chunk of every load of this thread
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = ACT == ACT_BNRELU ? a.scale[q * 8 + e] : 1.f;
+    sh[e] = ACT == ACT_BNRELU ? a.shift[q * 8 + e] : 0.f;
+  }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 
-  issue(0);
-  issue(1);
-  int st_prev1 = 0, st_prev2 = 0;   // store instructions of jobs j-1, j-2
-  for (int j = 0; j < njobs; ++j) {
-    issue(j + 2);
-    sp_vm_wait(2 * cnt + st_prev1 + st_prev2);
-    sp_barrier();   // job j's slice is in LDS for every wave
-    int n, h, s;
-    tile_of(j, n, h, s);
-    char* slot = ring + (j % 3) * SP_SLOT;
-
-    if constexpr (ACT != ACT_NONE) {   // input transform in place, padding stays zero
-      const int q = tid & 3;
-      float sc[8], sh[8];
+  // input row hh of frame n -> registers (zeros outside the frame and in the padding columns)
+  uint4 rg[KL];
+  auto load_row = [&](int n, int hh) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sc[e] = sprm[0][s * 32 + q * 8 + e];
-        sh[e] = sprm[1][s * 32 + q * 8 + e];
-      }
-      u32x4 v[4];
+    for (int k = 0; k < KL; ++k) {
+      const int c = tid + 512 * k;
+      const int px = c / CH;
+      const bool ok = c < nch && hh >= 0 && hh < H && px >= 1 && px <= W;
+      const unsigned off = ok ? (unsigned)(((((long)n * H + hh) * W + px - 1) * CIN + q * 8) * 2) : SP_OOB;
+      rg[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rX, (int)off, 0, 0));
+    }
+  };
+  // registers -> LDS slot of row hh, activated (the padding stays zero)
+  auto store_row = [&](int hh) {
+    char* slot = rows + ((hh + 3) % 3) * RB;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int c = tid + 512 * m;
-        v[m] = sp_rd128(slot + min(c, nch - 1) * 16);
-      }
-      sp_lgkm0();
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int c = tid + 512 * m;
-        const int row = c / (4 * (W + 2));
-        const int px = (c - row * 4 * (W + 2)) >> 2;
-        const int hh = h - 1 + row, ww = px - 1;
-        if (c < nch && hh >= 0 && hh < H && ww >= 0 && ww < W) {
-          u32x4 o;
+    for (int k = 0; k < KL; ++k) {
+      const int c = tid + 512 * k;
+      if (c >= nch) continue;
+      const int px = c / CH;
+      uint4 u = rg[k];
+      if constexpr (ACT != ACT_NONE) {
+        if (hh >= 0 && hh < H && px >= 1 && px <= W) {
+          unsigned v[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float lo = sp_lo(v[m][e]), hi = sp_hi(v[m][e]);
+            float lo = sp_lo(v[e]), hi = sp_hi(v[e]);
             if constexpr (ACT == ACT_BNRELU) {
               lo = fmaf(lo, sc[2 * e], sh[2 * e]);
               hi = fmaf(hi, sc[2 * e + 1], sh[2 * e + 1]);
             }
-            o[e] = sp_pack(fmaxf(lo, 0.f), fmaxf(hi, 0.f));
+            v[e] = sp_pack(fmaxf(lo, 0.f), fmaxf(hi, 0.f));
           }
-          sp_wr128(slot + c * 16, o);
+          u = make_uint4(v[0], v[1], v[2], v[3]);
         }
       }
-      sp_barrier();
+      *reinterpret_cast<uint4*>(slot + px * PB + q * 16) = u;
     }
+  };
 
-    // depthwise 3x3: 5 pixels x 2 channels per lane -> D tile
-    char* dx = sx[j & 1];
-    {
-      float tp[9][2];
+  const int tiles = a.N * a.nbands;
+  for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < tiles; tile += gridDim.x) {
+    const int n = tile / a.nbands, band = tile % a.nbands;
+    const int r0 = band * a.bandH, r1 = min(H, r0 + a.bandH);
+    // prologue: rows r0-1 .. r0+1 into the window, row r0+2 in flight
+    sp_barrier();   // (a previous tile's readers of the window are done)
+    for (int hh = r0 - 1; hh <= r0 + 1; ++hh) {
+      load_row(n, hh);
+      sp_vm_wait(0);
+      store_row(hh);
+    }
+    load_row(n, r0 + 2);
+    sp_barrier();
+    for (int h = r0; h < r1; ++h) {
+      const long prow = ((long)n * H + h) * W;
+      const char* rw0 = rows + ((h + 2) % 3) * RB;   // row h-1
+      const char* rw1 = rows + ((h + 3) % 3) * RB;   // row h
+      const char* rw2 = rows + ((h + 4) % 3) * RB;   // row h+1
+      f32x4 acc[10];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        tp[t][0] = stap[t][s * 32 + 2 * cl];
-        tp[t][1] = stap[t][s * 32 + 2 * cl + 1];
-      }
-      unsigned u[3][SP_SEG + 2];
+      for (int b = 0; b < 10; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
+      for (int hf = 0; hf < 2; ++hf) {
+        // depthwise: segments of 5 pixels, 2 channels per lane, all CIN channels per segment
 #pragma unroll
-        for (int k = 0; k < SP_SEG + 2; ++k) u[ky][k] = sp_rd32(slot + ky * rowb + wcol[k]);
-      sp_lgkm0();
+        for (int p = 0; p < NPASS; ++p) {
+          const int seg = p * 8 * SPW + w * SPW + lane / LPS;
+          const int xl = seg * SP_SEG;               // first pixel in the half
+          const int x0 = hf * SP_HALF + xl;          // first output pixel (= its window's first staged pixel)
+          unsigned u[3][SP_SEG + 2];
 #pragma unroll
-      for (int jj = 0; jj < SP_SEG; ++jj) {
-        float o[2];
+          for (int k = 0; k < SP_SEG + 2; ++k) {
+            const int off = min(x0 + k, W + 1) * PB + ch * 2;
+            u[0][k] = *reinterpret_cast<const unsigned*>(rw0 + off);
+            u[1][k] = *reinterpret_cast<const unsigned*>(rw1 + off);
+            u[2][k] = *reinterpret_cast<const unsigned*>(rw2 + off);
+          }
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          float acc_d = 0.f;
+          for (int jj = 0; jj < SP_SEG; ++jj) {
+            float o[2];
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
+            for (int e = 0; e < 2; ++e) {
+              float d = 0.f;
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) {
-              const unsigned uu = u[ky][jj + kx];
-              acc_d = fmaf(e ? sp_hi(uu) : sp_lo(uu), tp[ky * 3 + kx][e], acc_d);
+              for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                  const unsigned uu = u[ky][jj + kx];
+                  d = fmaf(e ? sp_hi(uu) : sp_lo(uu), tp[ky * 3 + kx][e], d);
+                }
+              o[e] = d;
             }
-          o[e] = acc_d;
+            *reinterpret_cast<unsigned*>(dt + (xl + jj) * DP + ch * 2) = x0 + jj < W ? sp_pack(o[0], o[1]) : 0u;
+          }
         }
-        const int px = x0 + jj;
-        if (px < SP_PXB)
-          *reinterpret_cast<unsigned*>(dx + px * SP_XP + cl * 4) = px < W ? sp_pack(o[0], o[1]) : 0u;
-      }
-    }
-    sp_barrier();   // D tile complete
-
-    // pointwise: acc[b] += W[16w + .][slice] x D[16b + .][slice]
-    {
-      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(sw + (w * 16 + fr) * SP_WP + (s * 32 + fg * 8) * 2);
+        sp_barrier();   // D tile complete
+        // pointwise: acc[b] += W[16w + .][:] x D[16b + .][:], K in steps of 32 (gemm_nt_kernel's order)
 #pragma unroll
-      for (int b = 0; b < 10; ++b) {
-        const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dx + (b * 16 + fr) * SP_XP + fg * 16);
-        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw, ad, acc[b], 0, 0, 0);
-      }
-    }
-    // the D slice -> HBM (2 buffer stores per lane, out-of-range lanes dropped)
-    const long prow = ((long)n * H + h) * W;
+        for (int b = 0; b < 5; ++b)
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const int c = tid + 512 * m;
-      const int px = c >> 2, q = c & 3;
-      const bool ok = px < W;
-      const uint4 v = *reinterpret_cast<const uint4*>(dx + min(px, SP_PXB - 1) * SP_XP + q * 16);
-      const unsigned off = ok ? (unsigned)(((prow + px) * CIN + s * 32 + q * 8) * 2) : SP_OOB;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rD, (int)off, 0, 0);
-    }
-    int st = 2;
-    if (s == S - 1) {   // the tile's Y row: 10 stores of 4 channels per lane, then the BN sums
+          for (int s = 0; s < S; ++s) {
+            const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dt + (b * 16 + fr) * DP + (s * 32 + fg * 8) * 2);
+            acc[hf * 5 + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], ad, acc[hf * 5 + b], 0, 0, 0);
+          }
+        // the D half row -> HBM
+#pragma unroll
+        for (int k = 0; k < KD; ++k) {
+          const int c = tid + 512 * k;
+          const int pl = min(c / CH, SP_HALF - 1), qq = c % CH;
+          const int px = hf * SP_HALF + pl;
+          const bool ok = c < SP_HALF * CH && px < W;
+          const uint4 v = *reinterpret_cast<const uint4*>(dt + pl * DP + qq * 16);
+          const unsigned off = ok ? (unsigned)(((prow + px) * CIN + qq * 8) * 2) : SP_OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rD, (int)off, 0, 0);
+        }
+        sp_barrier();   // the D tile is free again (and, after the second half, the window row h-1)
+      }
+      // the row's Y: 10 stores of 4 channels per lane, then the BN sums
 #pragma unroll
       for (int b = 0; b < 10; ++b) {
         const int px = b * 16 + fr;
         float f[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) f[r] = (float)(bf16)acc[b][r];
-        const unsigned lo = sp_pack(f[0], f[1]), hi = sp_pack(f[2], f[3]);
         const unsigned off = px < W ? (unsigned)(((prow + px) * SP_CO + w * 16 + 4 * fg) * 2) : SP_OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_uint2(lo, hi)), rY, (int)off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_uint2(sp_pack(f[0], f[1]), sp_pack(f[2], f[3]))),
+                                              rY, (int)off, 0, 0);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {   // (pixels past W hold zero: D rows past W are zero)
+        for (int r = 0; r < 4; ++r) {   // (pixels past W hold zero: their D rows are zero)
           s1[r] += f[r];
           s2[r] = fmaf(f[r], f[r], s2[r]);
         }
-        acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      st += 10;
+      // slide the window: row h+2 (loaded one row ago) replaces row h-1, row h+3 goes in flight
+      sp_vm_wait(NST);
+      store_row(h + 2);
+      load_row(n, h + 3);
+      sp_barrier();
     }
-    st_prev2 = st_prev1;
-    st_prev1 = st;
   }
+  sp_vm_wait(0);
   // BN partial row of this workgroup: reduce the 16 pixel lanes of each channel group
   if (a.part) {
 #pragma unroll
@@ -345,6 +298,17 @@ int sp_cus() {
   return v;
 }
 
+// bands per frame: enough (frame, band) tiles for every CU, bands of at least 8 rows
+void sp_bands(int N, int H, int& nb, int& bandH) {
+  const int cus = sp_cus();
+  nb = N >= cus ? 1 : (cus + N - 1) / N;
+  const int maxb = H >= 16 ? H / 8 : 1;
+  if (nb > maxb) nb = maxb;
+  if (nb < 1) nb = 1;
+  bandH = (H + nb - 1) / nb;
+  nb = (H + bandH - 1) / bandH;
+}
+
 }  // namespace
 
 extern "C" {
@@ -355,7 +319,9 @@ int xcp_sep_fwd_parts(int dtype, int N, int H, int W, int CIN, int COUT) {
     return 0;
   const long pix = (long)N * H * W;
   if (pix * CIN * 2 > 0x7fffffffL || pix * SP_CO * 2 > 0x7fffffffL) return 0;   // 32-bit buffer offsets
-  const long tiles = (long)N * H;
+  int nb, bh;
+  sp_bands(N, H, nb, bh);
+  const long tiles = (long)N * nb;
   return (int)(tiles < sp_cus() ? tiles : sp_cus());
 }
 
@@ -364,7 +330,8 @@ int xcp_sep_fwd(int dtype, int act, const void* X, const float* scale, const flo
   const int grid = xcp_sep_fwd_parts(dtype, N, H, W, CIN, COUT);
   if (grid <= 0) return XCP_EUNSUPPORTED;
   if (act < ACT_NONE || act > ACT_BNRELU || (act == ACT_BNRELU && (!scale || !shift))) return XCP_EINVAL;
-  SepArgs a{(const bf16*)X, scale, shift, dwt, (const bf16*)pw, (bf16*)D, (bf16*)Y, part, N, H, W};
+  SepArgs a{(const bf16*)X, scale, shift, dwt, (const bf16*)pw, (bf16*)D, (bf16*)Y, part, N, H, W, 1, H};
+  sp_bands(N, H, a.nbands, a.bandH);
 #define SP_LAUNCH(A, C) hipLaunchKernelGGL((sep_fwd_kernel<A, C>), dim3(grid), dim3(512), 0, stream, a)
   if (CIN == 64) {
     if (act == ACT_NONE) SP_LAUNCH(ACT_NONE, 64);
