@@ -67,7 +67,7 @@ def install_fake_lib(monkeypatch):
             return 4
         if name == "xcp_sep_fwd_parts":   # (dtype, N, H, W, CIN, COUT): block1's fused forward
             ok = args[0] == 1 and args[4] in (64, 128) and args[5] == 128 and args[3] <= 152
-            return min(args[1] * args[2], 256) if ok else 0
+            return min(args[1], 256) if ok else 0
         if name == "xcp_unit_bwd_rows_per_split":   # (dtype, M, CO, CI): the fused narrow unit
             ok = args[0] == 1 and (args[2], args[3]) in ((128, 64), (128, 128), (256, 128), (256, 256))
             return 64 if ok else 0

@@ -1108,7 +1108,7 @@ def test_sep_fwd_vs_dw_and_gemm(ops, gpu, N, H, W, CIN, act):
     part_ref = torch.zeros(R_ref * 2 * 128, device=gpu)
     ops.gemm_nt(D_ref, pw, Y_ref, M, 128, CIN, stats=part_ref, tile=1)
     R = ops.sep_fwd_parts(torch.bfloat16, N, H, W, CIN, 128)
-    assert R == min(N * H, torch.cuda.get_device_properties(gpu).multi_processor_count)
+    assert 0 < R <= min(N * H, torch.cuda.get_device_properties(gpu).multi_processor_count)
     D = torch.full((M, CIN), float("nan"), device=gpu, dtype=torch.bfloat16)
     Y = torch.full((M, 128), float("nan"), device=gpu, dtype=torch.bfloat16)
     part = torch.full((R * 2 * 128,), float("nan"), device=gpu)
