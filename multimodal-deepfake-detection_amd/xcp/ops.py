@@ -272,9 +272,10 @@ FIN_GROUPS = 256
 def _fold(part, R, CP):
     if R <= FIN_MAX_ROWS:
         return part, R
-    p2 = torch.empty(FIN_GROUPS * 2 * CP, device=part.device, dtype=torch.float32)
-    colreduce_f32(part, R, 2 * CP, p2, FIN_GROUPS)
-    return p2, FIN_GROUPS
+    G = min(FIN_GROUPS, R)   # (xcp_colreduce_f32 writes min(G, R) groups)
+    p2 = torch.empty(G * 2 * CP, device=part.device, dtype=torch.float32)
+    colreduce_f32(part, R, 2 * CP, p2, G)
+    return p2, G
 
 
 def finalize_stats(part, R, C, count, bn, train, out, CP=None):

@@ -183,7 +183,9 @@ def test_backbone64_vs_reference(gpu, golden, prec):
         if prec == "fp32":
             assert relerr(fe, g["features"]) < 1e-4
         else:
-            assert cos(fe, g["features"]) > 0.999
+            # (equally valid summation orders of the BN statistics alone move this cosine over
+            # 0.998973-0.999040, profiles/r05_bn_order_cos.txt; a bf16-rounded stem product gave 0.9988)
+            assert cos(fe, g["features"]) > 0.99893
         errs = {}
         for n, p in m.named_parameters():
             key = f"gradnorm/{n}"

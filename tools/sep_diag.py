@@ -45,6 +45,32 @@ def main():
     for n in bufs[False][0]:
         a, b = bufs[False][0][n], bufs[True][0][n]
         print(f"{n:40s} max rel diff {np.abs(a - b).max() / max(np.abs(a).max(), 1e-30):.3e}")
+    # the same bf16 model under other summation orders of the BN statistics, each as valid as the
+    # shipped one: the cosine to the fp32 reference's features moves by about this much
+    from xcp import ops
+    variants = {
+        "two kernels (shipped before)": dict(SEP_FUSED=False),
+        "fused": dict(SEP_FUSED=True),
+        "two kernels, NT 128-tile everywhere": dict(SEP_FUSED=False, NT_TILE=1),
+        "two kernels, NT one-shot 256": dict(SEP_FUSED=False, NT_TILE=2),
+        "two kernels, stats pre-reduced to 3 groups": dict(SEP_FUSED=False, FIN=(1, 3)),
+        "fused, stats pre-reduced to 3 groups": dict(SEP_FUSED=True, FIN=(1, 3)),
+        "two kernels, stats pre-reduced to 7 groups": dict(SEP_FUSED=False, FIN=(1, 7)),
+    }
+    base = (engine.SEP_FUSED, engine.NT_TILE, ops.FIN_MAX_ROWS, ops.FIN_GROUPS)
+    for name, v in variants.items():
+        engine.SEP_FUSED = v.get("SEP_FUSED", base[0])
+        engine.NT_TILE = v.get("NT_TILE", base[1])
+        ops.FIN_MAX_ROWS, ops.FIN_GROUPS = v.get("FIN", (base[2], base[3]))
+        torch.manual_seed(0)
+        m = xception(num_classes=1000)
+        m.fc = nn.Identity()
+        m = m.to(dev).train()
+        x = seeded_uniform((4, 3, 64, 64), 1234).to(dev)
+        with xcp.precision("bf16"):
+            f = m(x).detach().cpu().numpy()
+        print(f"{name:45s} cos to golden {cos(f, g['features']):.6f}")
+    engine.SEP_FUSED, engine.NT_TILE, ops.FIN_MAX_ROWS, ops.FIN_GROUPS = base
 
 
 if __name__ == "__main__":
