@@ -42,6 +42,7 @@ constexpr int SP_DW3 = 0x00020000;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __attribute__((aligned(64))) unsigned g_sp_zero[16];   // the source of out-of-frame loads
 
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   __syncthreads();
   const int ch = 2 * (lane % LPS);                // depthwise channels ch, ch + 1
   const int q = tid % CH;                         // staging chunk of every load of this thread
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  f2 s1[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, s2[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};   // channels 4fg + 0..3
 
   // input row hh of frame n -> registers (zeros outside the frame and in the padding columns); two
   // register sets, rows two ahead of the one being consumed
@@ -169,14 +170,12 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
           unsigned v[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float lo = sp_lo(v[e]), hi = sp_hi(v[e]);
-            if constexpr (ACT == ACT_BNRELU) {
-              const float2 scv = *reinterpret_cast<const float2*>(&sprm[0][q * 8 + 2 * e]);
-              const float2 shv = *reinterpret_cast<const float2*>(&sprm[1][q * 8 + 2 * e]);
-              lo = fmaf(lo, scv.x, shv.x);
-              hi = fmaf(hi, scv.y, shv.y);
-            }
-            v[e] = sp_pack(fmaxf(lo, 0.f), fmaxf(hi, 0.f));
+            f2 x = f2{sp_lo(v[e]), sp_hi(v[e])};
+            if constexpr (ACT == ACT_BNRELU)
+              x = __builtin_elementwise_fma(x, *reinterpret_cast<const f2*>(&sprm[0][q * 8 + 2 * e]),
+                                            *reinterpret_cast<const f2*>(&sprm[1][q * 8 + 2 * e]));
+            x = __builtin_elementwise_max(x, f2{0.f, 0.f});
+            v[e] = sp_pack(x[0], x[1]);
           }
           u = make_uint4(v[0], v[1], v[2], v[3]);
         }
@@ -215,37 +214,29 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
           const int seg = p * 8 * SPW + w * SPW + lane / LPS;
           const int xl = seg * SP_SEG;               // first pixel in the half
           const int x0 = hf * SP_HALF + xl;          // first output pixel (= its window's first staged pixel)
-          float tp[9][2];
+          // (packed pairs: each channel keeps dw_fwd's fma chain in (ky, kx) order)
+          f2 tp[9];
 #pragma unroll
-          for (int t = 0; t < 9; ++t) {
-            const float2 v = *reinterpret_cast<const float2*>(&stap[t][ch]);
-            tp[t][0] = v.x;
-            tp[t][1] = v.y;
-          }
-          unsigned u[3][SP_SEG + 2];
+          for (int t = 0; t < 9; ++t) tp[t] = *reinterpret_cast<const f2*>(&stap[t][ch]);
+          f2 win[3][SP_SEG + 2];
 #pragma unroll
           for (int k = 0; k < SP_SEG + 2; ++k) {
             const int off = min(x0 + k, W + 1) * PB + ch * 2;
-            u[0][k] = *reinterpret_cast<const unsigned*>(rw0 + off);
-            u[1][k] = *reinterpret_cast<const unsigned*>(rw1 + off);
-            u[2][k] = *reinterpret_cast<const unsigned*>(rw2 + off);
+            const unsigned u0 = *reinterpret_cast<const unsigned*>(rw0 + off);
+            const unsigned u1 = *reinterpret_cast<const unsigned*>(rw1 + off);
+            const unsigned u2 = *reinterpret_cast<const unsigned*>(rw2 + off);
+            win[0][k] = f2{sp_lo(u0), sp_hi(u0)};
+            win[1][k] = f2{sp_lo(u1), sp_hi(u1)};
+            win[2][k] = f2{sp_lo(u2), sp_hi(u2)};
           }
 #pragma unroll
           for (int jj = 0; jj < SP_SEG; ++jj) {
-            float o[2];
+            f2 d = f2{0.f, 0.f};
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              float d = 0.f;
+            for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-              for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) {
-                  const unsigned uu = u[ky][jj + kx];
-                  d = fmaf(e ? sp_hi(uu) : sp_lo(uu), tp[ky * 3 + kx][e], d);
-                }
-              o[e] = d;
-            }
-            *reinterpret_cast<unsigned*>(dt + (xl + jj) * DP + ch * 2) = x0 + jj < W ? sp_pack(o[0], o[1]) : 0u;
+              for (int kx = 0; kx < 3; ++kx) d = __builtin_elementwise_fma(win[ky][jj + kx], tp[ky * 3 + kx], d);
+            *reinterpret_cast<unsigned*>(dt + (xl + jj) * DP + ch * 2) = x0 + jj < W ? sp_pack(d[0], d[1]) : 0u;
           }
         }
         sp_barrier();   // D tile complete
@@ -279,9 +270,10 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_uint2(sp_pack(f[0], f[1]), sp_pack(f[2], f[3]))),
                                                 rY, (int)off, 0, 0);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {   // (pixels past W hold zero: their D rows are zero)
-            s1[r] += f[r];
-            s2[r] = fmaf(f[r], f[r], s2[r]);
+          for (int r = 0; r < 2; ++r) {   // (pixels past W hold zero: their D rows are zero)
+            const f2 v = f2{f[2 * r], f[2 * r + 1]};
+            s1[r] += v;
+            s2[r] = __builtin_elementwise_fma(v, v, s2[r]);
           }
         }
         sp_barrier();   // the D tile is free again (and, after the second half, the window row h-1)
@@ -301,19 +293,23 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   sp_vm_wait(0);
   // BN partial row of this workgroup: reduce the 16 pixel lanes of each channel group
   if (a.part) {
+    float t1[4], t2[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < 4; ++r) {
+      t1[r] = s1[r >> 1][r & 1];
+      t2[r] = s2[r >> 1][r & 1];
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
-        s1[r] += __shfl_xor(s1[r], o, 64);
-        s2[r] += __shfl_xor(s2[r], o, 64);
+        t1[r] += __shfl_xor(t1[r], o, 64);
+        t2[r] += __shfl_xor(t2[r], o, 64);
       }
+    }
     if (fr == 0) {
       float* p = a.part + (long)blockIdx.x * 2 * SP_CO + w * 16 + 4 * fg;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        p[r] = s1[r];
-        p[SP_CO + r] = s2[r];
+        p[r] = t1[r];
+        p[SP_CO + r] = t2[r];
       }
     }
   }
