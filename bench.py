@@ -127,6 +127,8 @@ BLOCKS = [(64, 128, 2, 2, False, True), (128, 256, 2, 2, True, True), (256, 728,
 
 # (cout, cin) of the units whose BN apply + pointwise dgrad + wgrad run fused in bf16
 FUSED_UNITS = {(128, 64), (128, 128), (256, 128), (256, 256)}
+# (cout, cin) of the units whose depthwise + pointwise forward run as one kernel in bf16 (sepfwd.hip)
+SEP_FUSED_UNITS = {(128, 64), (128, 128)}
 
 
 def step_roofline(size, frames, unfrozen, s=2):
@@ -154,8 +156,11 @@ def step_roofline(size, frames, unfrozen, s=2):
 
     def unit(cin, cout, hw, reduce=False):
         P = n * hw * hw
-        op(0, 2 * s * P * cin + 36 * cin)                       # depthwise fwd (BN+ReLU on load)
-        op(2 * P * cin * cout, s * P * (cin + cout))            # pointwise (+BN stats epilogue)
+        if s == 2 and (cout, cin) in SEP_FUSED_UNITS:           # depthwise + pointwise in one pass
+            op(2 * P * cin * cout, s * P * (2 * cin + cout) + 36 * cin)
+        else:
+            op(0, 2 * s * P * cin + 36 * cin)                   # depthwise fwd (BN+ReLU on load)
+            op(2 * P * cin * cout, s * P * (cin + cout))        # pointwise (+BN stats epilogue)
         # BN backward: apply (read dz, y; write dy); its reduce comes fused from the consumer's
         # depthwise backward / the max-pool backward, except after a residual / the avg-pool
         if s == 2 and (cout, cin) in FUSED_UNITS:   # apply + dgrad + wgrad in one pass (unitbwd.hip)
