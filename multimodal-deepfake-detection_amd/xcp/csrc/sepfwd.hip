@@ -20,8 +20,9 @@
 //     Y[px][16w .. 16w+15] += D[px][:] W[16w..][:]^T with v_mfma_f32_16x16x32_bf16 (the weights of
 //     its 16 output channels live in registers; operands and K order as gemm_nt_kernel, so Y is
 //     bitwise the NT GEMM's) and the D tile is stored with 16-B buffer stores;
-//   * the row's Y is stored from the accumulators (8 B per lane) and its bf16 values enter per-lane
-//     BN sums, written as one partial row per workgroup at the end.
+//   * the half row's Y goes through LDS (the D tile's space at CIN = 128) so that it leaves as 16-B
+//     stores of whole pixel rows (8-B stores of 32-B pieces from the accumulators measured 3-5 %
+//     slower); its bf16 values enter per-thread BN sums, written as one partial row per workgroup.
 // Every VMEM instruction is issued by every lane (out-of-range loads read a zero line, out-of-range
 // buffer stores get an offset past the buffer and are dropped), so the one counted wait per row --
 // for the input row loaded two rows ago, with the D and Y stores of the last two rows and the next
@@ -115,9 +116,13 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   constexpr int LPS = CIN / 2;                    // lanes per depthwise segment (2 channels each)
   constexpr int SPW = 64 / LPS;                   // segments per wave per pass
   constexpr int NPASS = (SP_HALF / SP_SEG) / (8 * SPW);   // passes per half row (16 segments)
-  constexpr int NST = 2 * KD + 10;                // stores per output row
+  constexpr int YP = SP_CO * 2 + 16;              // Y staging pitch (the D tile's at CIN = 128)
+  constexpr int KY = (SP_HALF * 16 + 511) / 512;  // Y stores per thread per half row
+  constexpr int NST = 2 * (KD + KY);              // stores per output row
   __shared__ __attribute__((aligned(16))) char rows[3 * RB];
   __shared__ __attribute__((aligned(16))) char dt[SP_HALF * DP];
+  __shared__ __attribute__((aligned(16))) char yown[CIN == 128 ? 16 : SP_HALF * YP];
+  char* const yt = CIN == 128 ? dt : yown;        // Y half-row staging (after the D tile is stored)
   __shared__ __attribute__((aligned(16))) float stap[9][CIN];   // depthwise taps
   __shared__ __attribute__((aligned(16))) float sprm[2][CIN];   // input BN scale / shift
 
@@ -140,7 +145,9 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   __syncthreads();
   const int ch = 2 * (lane % LPS);                // depthwise channels ch, ch + 1
   const int q = tid % CH;                         // staging chunk of every load of this thread
-  f2 s1[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, s2[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};   // channels 4fg + 0..3
+  f2 s1[4], s2[4];   // BN sums of channels 8 * (tid % 16) + 0..7
+#pragma unroll
+  for (int r = 0; r < 4; ++r) s1[r] = s2[r] = f2{0.f, 0.f};
 
   // input row hh of frame n -> registers (zeros outside the frame and in the padding columns); two
   // register sets, rows two ahead of the one being consumed
@@ -259,21 +266,34 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
           const unsigned off = ok ? (unsigned)(((prow + px) * CIN + qq * 8) * 2) : SP_OOB;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rD, (int)off, 0, 0);
         }
-        // the half row's Y: 5 stores of 4 channels per lane, then the BN sums
+        // the half row's Y through LDS: 16-B stores of whole pixel rows, then the BN sums
+        sp_barrier();   // (CIN = 128: every wave is done with the D tile)
 #pragma unroll
         for (int b = 0; b < 5; ++b) {
-          const int px = hf * SP_HALF + b * 16 + fr;
           float f[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) f[r] = (float)(bf16)acc[b][r];
-          const unsigned off = px < W ? (unsigned)(((prow + px) * SP_CO + w * 16 + 4 * fg) * 2) : SP_OOB;
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_uint2(sp_pack(f[0], f[1]), sp_pack(f[2], f[3]))),
-                                                rY, (int)off, 0, 0);
+          for (int r = 0; r < 4; ++r) f[r] = acc[b][r];
+          *reinterpret_cast<uint2*>(yt + (b * 16 + fr) * YP + (w * 16 + 4 * fg) * 2) =
+              make_uint2(sp_pack(f[0], f[1]), sp_pack(f[2], f[3]));
+        }
+        sp_barrier();
 #pragma unroll
-          for (int r = 0; r < 2; ++r) {   // (pixels past W hold zero: their D rows are zero)
-            const f2 v = f2{f[2 * r], f[2 * r + 1]};
-            s1[r] += v;
-            s2[r] = __builtin_elementwise_fma(v, v, s2[r]);
+        for (int k = 0; k < KY; ++k) {
+          const int c = tid + 512 * k;
+          const int pl = min(c >> 4, SP_HALF - 1), qq = c & 15;
+          const int px = hf * SP_HALF + pl;
+          const bool ok = c < SP_HALF * 16 && px < W;
+          const uint4 v = *reinterpret_cast<const uint4*>(yt + pl * YP + qq * 16);
+          const unsigned off = ok ? (unsigned)(((prow + px) * SP_CO + qq * 8) * 2) : SP_OOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rY, (int)off, 0, 0);
+          if (ok) {
+            const unsigned u4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const f2 y = f2{sp_lo(u4[r]), sp_hi(u4[r])};
+              s1[r] += y;
+              s2[r] = __builtin_elementwise_fma(y, y, s2[r]);
+            }
           }
         }
         sp_barrier();   // the D tile is free again (and, after the second half, the window row h-1)
@@ -291,26 +311,37 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
     }
   }
   sp_vm_wait(0);
-  // BN partial row of this workgroup: reduce the 16 pixel lanes of each channel group
+  // BN partial row of this workgroup: lanes of one channel group (tid % 16) across the wave, then the
+  // 8 waves through LDS
   if (a.part) {
-    float t1[4], t2[4];
+    float t[2][8];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      t1[r] = s1[r >> 1][r & 1];
-      t2[r] = s2[r >> 1][r & 1];
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        t1[r] += __shfl_xor(t1[r], o, 64);
-        t2[r] += __shfl_xor(t2[r], o, 64);
+      for (int e = 0; e < 2; ++e) {
+        t[0][2 * r + e] = s1[r][e];
+        t[1][2 * r + e] = s2[r][e];
       }
-    }
-    if (fr == 0) {
-      float* p = a.part + (long)blockIdx.x * 2 * SP_CO + w * 16 + 4 * fg;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        p[r] = t1[r];
-        p[SP_CO + r] = t2[r];
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        t[m][e] += __shfl_xor(t[m][e], 16, 64);
+        t[m][e] += __shfl_xor(t[m][e], 32, 64);
       }
+    sp_barrier();
+    float* red = reinterpret_cast<float*>(rows);   // [8 waves][2][128]
+    if (lane < 16)
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[(w * 2 + m) * SP_CO + lane * 8 + e] = t[m][e];
+    sp_barrier();
+    if (tid < 2 * SP_CO) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) v += red[ww * 2 * SP_CO + tid];
+      a.part[(long)blockIdx.x * 2 * SP_CO + tid] = v;
     }
   }
 }
