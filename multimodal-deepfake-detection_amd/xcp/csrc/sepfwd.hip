@@ -299,8 +299,10 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
         sp_barrier();   // the D tile is free again (and, after the second half, the window row h-1)
       }
       // slide the window: row h+2 (loaded two rows ago into rg) replaces row h-1 and row h+4 goes into
-      // rg; issued after row h+2's loads: the stores of rows h-1 and h and the loads of row h+3
-      sp_vm_wait((h > r0 ? 2 * NST : NST) + KL);
+      // rg; issued after row h+2's loads: the stores of rows h-1 and h and the loads of row h+3.  One
+      // constant wait leaves this row's stores and row h+3's loads in flight (the previous row's stores,
+      // a row old, are retired with it): a single s_waitcnt on every path
+      sp_vm_wait(NST + KL);
       store_row(rg, h + 2);
       load_row(rg, n, h + 4);
       sp_barrier();
@@ -309,6 +311,7 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
       row(h, rga);
       if (h + 1 < r1) row(h + 1, rgb);
     }
+    sp_vm_wait(0);   // the look-ahead loads past the band land before the next tile reuses their registers
   }
   sp_vm_wait(0);
   // BN partial row of this workgroup: lanes of one channel group (tid % 16) across the wave, then the

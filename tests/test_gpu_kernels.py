@@ -1088,12 +1088,13 @@ def test_permute_batch_plans(ops, gpu):
 
 @pytest.mark.parametrize("CIN", [64, 128])
 @pytest.mark.parametrize("act", [0, 1, 2])
-@pytest.mark.parametrize("N,H,W", [(2, 147, 147), (3, 9, 150), (5, 1, 152), (2, 6, 3), (1, 300, 37)])
+@pytest.mark.parametrize("N,H,W", [(2, 147, 147), (3, 9, 150), (5, 1, 152), (2, 6, 3), (1, 300, 37), (600, 3, 20)])
 def test_sep_fwd_vs_dw_and_gemm(ops, gpu, N, H, W, CIN, act):
     """Fused depthwise + pointwise forward of block1's units (csrc/sepfwd.hip) against the two kernels it
     replaces: D bitwise xcp_dw_fwd's, Y bitwise the 128x128 NT kernel's (same MFMA operands and K order),
     the BN partial sums to fp32 summation order against the NT epilogue's; frames as wide as the kernel
-    takes, one row, three columns (W <= 8 powers of two take dwframe.hip, fp32 windows), more tiles than workgroups and fewer."""
+    takes, one row, three columns (W <= 8 powers of two take dwframe.hip, fp32 windows), fewer tiles than workgroups and
+    more (600 frames: a workgroup walks several frames, its look-ahead loads crossing tile boundaries)."""
     g = torch.Generator(device=gpu).manual_seed(N * 1000 + H + W + CIN + act)
     M = N * H * W
     X = torch.randn(M, CIN, device=gpu, generator=g).bfloat16()
