@@ -1,4 +1,5 @@
-"""Interleaved A/B of the persistent NT GEMM with and without PRE2 (two K-tiles of the next tile issued
+"""(Record tool: needs the round-5 PRE2 build of gemm.hip, measured and reverted -- profiles/r05_nt_pre2_ab.txt.)
+Interleaved A/B of the persistent NT GEMM with and without PRE2 (two K-tiles of the next tile issued
 before the epilogue so the stores drain under two K-tiles instead of one), bf16, with / without the
 BN-statistics epilogue, at the middle-flow shape and two K depths; checks PRE2 is bitwise equal.
 
