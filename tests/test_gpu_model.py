@@ -201,10 +201,11 @@ def test_backbone64_vs_reference(gpu, golden, prec):
             if "running_var" in n:
                 np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"],
                                            rtol=1e-4 if prec == "fp32" else 2e-2, atol=1e-4, err_msg=n)
-            elif "running_mean" in n:   # a signed sum: absolute tolerance in bf16
+            elif "running_mean" in n:   # a signed sum: absolute tolerance in bf16 (equally valid BN
+                # summation orders alone use up to 1.68x of an atol of 0.05 here, profiles/r05_bn_order_cos.txt)
                 np.testing.assert_allclose(t.double().sum().item(), g[f"buf/{n}/sum"],
                                            rtol=1e-4 if prec == "fp32" else 5e-2,
-                                           atol=1e-4 if prec == "fp32" else 5e-2, err_msg=n)
+                                           atol=1e-4 if prec == "fp32" else 0.15, err_msg=n)
         m.eval()
         with torch.no_grad():
             fev = m(x).cpu().numpy()
