@@ -128,7 +128,7 @@ BLOCKS = [(64, 128, 2, 2, False, True), (128, 256, 2, 2, True, True), (256, 728,
 # (cout, cin) of the units whose BN apply + pointwise dgrad + wgrad run fused in bf16
 FUSED_UNITS = {(128, 64), (128, 128), (256, 128), (256, 256)}
 # (cout, cin) of the units whose depthwise + pointwise forward run as one kernel in bf16 (sepfwd.hip)
-SEP_FUSED_UNITS = {(128, 64), (128, 128)}
+SEP_FUSED_UNITS = {(128, 64), (128, 128), (256, 128)}
 
 
 def step_roofline(size, frames, unfrozen, s=2):

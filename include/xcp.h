@@ -78,10 +78,11 @@ int xcp_unit_bwd(int dtype, const void* G, const void* Y, const float* alpha, co
  * Wt is the [9][C] fp32 tap-major packing of the [C,1,3,3] weight. */
 int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, const float* scale, const float* shift, int N,
                int H, int W, int C, xcp_stream_t stream);
-/* fused depthwise + pointwise forward of an entry-flow unit (Xception.py:37-47 for block1's units):
- * D = dw3x3(act(X)) (bitwise xcp_dw_fwd's), Y = D . pw^T (bitwise xcp_gemm_nt's 128x128 kernel),
+/* fused depthwise + pointwise forward of an entry-flow unit (Xception.py:37-47; block1's units, block2's first):
+ * D = dw3x3(act(X)) (bitwise xcp_dw_fwd's), Y = D . pw^T (bitwise xcp_gemm_nt's),
  * part[R][2][COUT] BN partial sums (sum, sum of squares) of the stored bf16 Y, R = xcp_sep_fwd_parts().
- * dwt: [9][CIN] fp32 taps; pw: [COUT][CIN] bf16.  bf16, CIN 64 or 128, COUT 128, W <= 152. */
+ * dwt: [9][CIN] fp32 taps; pw: [COUT][CIN] bf16.  bf16; (CIN, COUT) = (64 | 128, 128) with W <= 152 or
+ * (128, 256) with W <= 78. */
 int xcp_sep_fwd_parts(int dtype, int N, int H, int W, int CIN, int COUT);   /* 0: shape not supported */
 int xcp_sep_fwd(int dtype, int act, const void* X, const float* scale, const float* shift, const float* dwt, const void* pw,
                 void* D, void* Y, float* part, int N, int H, int W, int CIN, int COUT, xcp_stream_t stream);

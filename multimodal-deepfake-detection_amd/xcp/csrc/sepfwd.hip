@@ -1,7 +1,8 @@
 // Fused forward of one entry-flow SeparableConv2d: depthwise 3x3 (stride 1, pad 1) followed by the
 // 1x1 pointwise conv to 128 channels, with the BatchNorm batch statistics of the pointwise output --
 // Xception.py:37-47 (SeparableConv2d.forward = pointwise(conv1(x))) for block1's two units
-// (147^2: 64 -> 128, 128 -> 128), whose pointwise GEMMs (K = 64 / 128) are HBM-bound.
+// (147^2: 64 -> 128, 128 -> 128) and block2's first (74^2: 128 -> 256), whose pointwise GEMMs
+// (K = 64 / 128) are HBM-bound.
 //
 // Unfused, the depthwise output D is written by dw_fwd and read back by the GEMM; here it goes from
 // the depthwise FMAs through LDS straight into the MFMAs (D is still written once: the unit's
@@ -17,9 +18,9 @@
 //   * an output row is done in two halves of 80 pixels: each lane computes 5 pixels x 2 channels of
 //     the depthwise conv from a 3 x 7 window (the fma chain per channel of dw_fwd_w2_kernel, so D is
 //     bitwise dw_fwd's) into an LDS tile [80 px][CIN]; wave w then accumulates
-//     Y[px][16w .. 16w+15] += D[px][:] W[16w..][:]^T with v_mfma_f32_16x16x32_bf16 (the weights of
-//     its 16 output channels live in registers; operands and K order as gemm_nt_kernel, so Y is
-//     bitwise the NT GEMM's) and the D tile is stored with 16-B buffer stores;
+//     Y[px][16w .. 16w+15] (and 16(w+8) .. for 256 outputs) += D[px][:] W[..][:]^T with
+//     v_mfma_f32_16x16x32_bf16 (the weights of its output channels live in registers; operands and
+//     K order as the NT GEMMs, so Y is bitwise theirs) and the D tile is stored with 16-B buffer stores;
 //   * the half row's Y goes through LDS (the D tile's space at CIN = 128) so that it leaves as 16-B
 //     stores of whole pixel rows (8-B stores of 32-B pieces from the accumulators measured 3-5 %
 //     slower); its bf16 values enter per-thread BN sums, written as one partial row per workgroup.
@@ -31,10 +32,9 @@
 
 namespace {
 
-constexpr int SP_WMAX = 152;                // widest frame
-constexpr int SP_RPX = SP_WMAX + 2;         // staged pixels per input row (with the padding)
+constexpr int SP_WMAX = 152;                // widest frame (two 80-pixel halves per row)
+constexpr int SP_WMAX1 = 78;                // widest frame of the one-half form (COUT = 256)
 constexpr int SP_HALF = 80;                 // pixels per half row (5 MFMA blocks)
-constexpr int SP_CO = 128;
 constexpr int SP_SEG = 5;                   // depthwise outputs per lane
 constexpr unsigned SP_OOB = 0x80000000u;
 constexpr int SP_REC = 0x7fffffff;
@@ -104,8 +104,12 @@ XCP_DEV unsigned sp_pack(float a, float b) {
   return (unsigned)r[0] | ((unsigned)r[1] << 16);
 }
 
-template <int ACT, int CIN>
+// COUT: 128 (block1) or 256 (block2's first unit, whose 74-pixel rows are one half: NHALF = 1)
+template <int ACT, int CIN, int COUT, int NHALF>
 __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
+  constexpr int SP_RPX = (NHALF == 2 ? SP_WMAX : SP_WMAX1) + 2;   // staged pixels per input row (with the padding)
+  constexpr int NB = COUT / 128;                  // 16-channel output blocks per wave (w, w + 8)
+  constexpr int YC = COUT / 8;                    // 16-B chunks per Y pixel row
   constexpr int S = CIN / 32;                     // K steps of 32
   constexpr int CH = CIN / 8;                     // 16-B chunks per pixel
   constexpr int PB = CIN * 2;                     // bytes per staged pixel
@@ -116,13 +120,14 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   constexpr int LPS = CIN / 2;                    // lanes per depthwise segment (2 channels each)
   constexpr int SPW = 64 / LPS;                   // segments per wave per pass
   constexpr int NPASS = (SP_HALF / SP_SEG) / (8 * SPW);   // passes per half row (16 segments)
-  constexpr int YP = SP_CO * 2 + 16;              // Y staging pitch (the D tile's at CIN = 128)
-  constexpr int KY = (SP_HALF * 16 + 511) / 512;  // Y stores per thread per half row
+  constexpr int YP = COUT * 2 + 16;               // Y staging pitch (the D tile's at CIN = COUT = 128)
+  constexpr int KY = (SP_HALF * YC + 511) / 512;  // Y stores per thread per half row
+  constexpr bool YSHARE = YP == DP;               // Y staged in the D tile's space
   constexpr int NST = 2 * (KD + KY);              // stores per output row
   __shared__ __attribute__((aligned(16))) char rows[3 * RB];
   __shared__ __attribute__((aligned(16))) char dt[SP_HALF * DP];
-  __shared__ __attribute__((aligned(16))) char yown[CIN == 128 ? 16 : SP_HALF * YP];
-  char* const yt = CIN == 128 ? dt : yown;        // Y half-row staging (after the D tile is stored)
+  __shared__ __attribute__((aligned(16))) char yown[YSHARE ? 16 : SP_HALF * YP];
+  char* const yt = YSHARE ? dt : yown;            // Y half-row staging (after the D tile is stored)
   __shared__ __attribute__((aligned(16))) float stap[9][CIN];   // depthwise taps
   __shared__ __attribute__((aligned(16))) float sprm[2][CIN];   // input BN scale / shift
 
@@ -134,9 +139,12 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(a.Y, (short)0, SP_REC, SP_DW3);
 
   // ---- this wave's weights in registers; taps and the input BN affine in LDS
-  bf16x8 wf[S];
+  bf16x8 wf[NB][S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) wf[s] = *reinterpret_cast<const bf16x8*>(a.pw + (long)(w * 16 + fr) * CIN + s * 32 + fg * 8);
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      wf[j][s] = *reinterpret_cast<const bf16x8*>(a.pw + (long)((w + 8 * j) * 16 + fr) * CIN + s * 32 + fg * 8);
   for (int c = tid; c < 9 * CIN; c += 512) stap[c / CIN][c % CIN] = a.dwt[c];
   for (int c = tid; c < CIN; c += 512) {
     sprm[0][c] = ACT == ACT_BNRELU ? a.scale[c] : 1.f;
@@ -145,7 +153,7 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   __syncthreads();
   const int ch = 2 * (lane % LPS);                // depthwise channels ch, ch + 1
   const int q = tid % CH;                         // staging chunk of every load of this thread
-  f2 s1[4], s2[4];   // BN sums of channels 8 * (tid % 16) + 0..7
+  f2 s1[4], s2[4];   // BN sums of channels 8 * (tid % YC) + 0..7
 #pragma unroll
   for (int r = 0; r < 4; ++r) s1[r] = s2[r] = f2{0.f, 0.f};
 
@@ -211,10 +219,12 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
       const char* rw1 = rows + ((h + 3) % 3) * RB;   // row h
       const char* rw2 = rows + ((h + 4) % 3) * RB;   // row h+1
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        f32x4 acc[5];
+      for (int hf = 0; hf < NHALF; ++hf) {
+        f32x4 acc[5][NB];
 #pragma unroll
-        for (int b = 0; b < 5; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < 5; ++b)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) acc[b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         // depthwise: segments of 5 pixels, 2 channels per lane, all CIN channels per segment
 #pragma unroll 1
         for (int p = 0; p < NPASS; ++p) {
@@ -247,13 +257,14 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
           }
         }
         sp_barrier();   // D tile complete
-        // pointwise: acc[b] += W[16w + .][:] x D[16b + .][:], K in steps of 32 (gemm_nt_kernel's order)
+        // pointwise: acc[b][j] += W[16(w + 8j) + .][:] x D[16b + .][:], K in steps of 32 (the NT GEMMs' order)
 #pragma unroll
         for (int b = 0; b < 5; ++b)
 #pragma unroll
           for (int s = 0; s < S; ++s) {
             const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dt + (b * 16 + fr) * DP + (s * 32 + fg * 8) * 2);
-            acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], ad, acc[b], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < NB; ++j) acc[b][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][s], ad, acc[b][j], 0, 0, 0);
           }
         // the D half row -> HBM
 #pragma unroll
@@ -267,24 +278,22 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rD, (int)off, 0, 0);
         }
         // the half row's Y through LDS: 16-B stores of whole pixel rows, then the BN sums
-        sp_barrier();   // (CIN = 128: every wave is done with the D tile)
+        if constexpr (YSHARE) sp_barrier();   // every wave is done with the D tile
 #pragma unroll
-        for (int b = 0; b < 5; ++b) {
-          float f[4];
+        for (int b = 0; b < 5; ++b)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) f[r] = acc[b][r];
-          *reinterpret_cast<uint2*>(yt + (b * 16 + fr) * YP + (w * 16 + 4 * fg) * 2) =
-              make_uint2(sp_pack(f[0], f[1]), sp_pack(f[2], f[3]));
-        }
+          for (int j = 0; j < NB; ++j)
+            *reinterpret_cast<uint2*>(yt + (b * 16 + fr) * YP + ((w + 8 * j) * 16 + 4 * fg) * 2) =
+                make_uint2(sp_pack(acc[b][j][0], acc[b][j][1]), sp_pack(acc[b][j][2], acc[b][j][3]));
         sp_barrier();
 #pragma unroll
         for (int k = 0; k < KY; ++k) {
           const int c = tid + 512 * k;
-          const int pl = min(c >> 4, SP_HALF - 1), qq = c & 15;
+          const int pl = min(c / YC, SP_HALF - 1), qq = c % YC;
           const int px = hf * SP_HALF + pl;
-          const bool ok = c < SP_HALF * 16 && px < W;
+          const bool ok = c < SP_HALF * YC && px < W;
           const uint4 v = *reinterpret_cast<const uint4*>(yt + pl * YP + qq * 16);
-          const unsigned off = ok ? (unsigned)(((prow + px) * SP_CO + qq * 8) * 2) : SP_OOB;
+          const unsigned off = ok ? (unsigned)(((prow + px) * COUT + qq * 8) * 2) : SP_OOB;
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), rY, (int)off, 0, 0);
           if (ok) {
             const unsigned u4[4] = {v.x, v.y, v.z, v.w};
@@ -314,7 +323,7 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
     sp_vm_wait(0);   // the look-ahead loads past the band land before the next tile reuses their registers
   }
   sp_vm_wait(0);
-  // BN partial row of this workgroup: lanes of one channel group (tid % 16) across the wave, then the
+  // BN partial row of this workgroup: lanes of one channel group (tid % YC) across the wave, then the
   // 8 waves through LDS
   if (a.part) {
     float t[2][8];
@@ -329,22 +338,22 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
     for (int m = 0; m < 2; ++m)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        t[m][e] += __shfl_xor(t[m][e], 16, 64);
+        if constexpr (YC == 16) t[m][e] += __shfl_xor(t[m][e], 16, 64);
         t[m][e] += __shfl_xor(t[m][e], 32, 64);
       }
     sp_barrier();
-    float* red = reinterpret_cast<float*>(rows);   // [8 waves][2][128]
-    if (lane < 16)
+    float* red = reinterpret_cast<float*>(rows);   // [8 waves][2][COUT]
+    if (lane < YC)
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) red[(w * 2 + m) * SP_CO + lane * 8 + e] = t[m][e];
+        for (int e = 0; e < 8; ++e) red[(w * 2 + m) * COUT + lane * 8 + e] = t[m][e];
     sp_barrier();
-    if (tid < 2 * SP_CO) {
+    for (int i = tid; i < 2 * COUT; i += 512) {
       float v = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < 8; ++ww) v += red[ww * 2 * SP_CO + tid];
-      a.part[(long)blockIdx.x * 2 * SP_CO + tid] = v;
+      for (int ww = 0; ww < 8; ++ww) v += red[ww * 2 * COUT + i];
+      a.part[(long)blockIdx.x * 2 * COUT + i] = v;
     }
   }
 }
@@ -376,10 +385,12 @@ extern "C" {
 
 // partial-sum rows xcp_sep_fwd writes (one per workgroup); 0: the shape is not supported
 int xcp_sep_fwd_parts(int dtype, int N, int H, int W, int CIN, int COUT) {
-  if (dtype != XCP_BF16 || COUT != SP_CO || (CIN != 64 && CIN != 128) || W < 1 || W > SP_WMAX || N <= 0 || H <= 0)
-    return 0;
+  // (CIN, COUT) = (64 | 128, 128) up to 152 pixels wide, (128, 256) up to 78
+  const bool shape = (COUT == 128 && (CIN == 64 || CIN == 128) && W <= SP_WMAX) ||
+                     (COUT == 256 && CIN == 128 && W <= SP_WMAX1);
+  if (dtype != XCP_BF16 || !shape || W < 1 || N <= 0 || H <= 0) return 0;
   const long pix = (long)N * H * W;
-  if (pix * CIN * 2 > 0x7fffffffL || pix * SP_CO * 2 > 0x7fffffffL) return 0;   // 32-bit buffer offsets
+  if (pix * CIN * 2 > 0x7fffffffL || pix * COUT * 2 > 0x7fffffffL) return 0;   // 32-bit buffer offsets
   int nb, bh;
   sp_bands(N, H, nb, bh);
   const long tiles = (long)N * nb;
@@ -393,16 +404,19 @@ int xcp_sep_fwd(int dtype, int act, const void* X, const float* scale, const flo
   if (act < ACT_NONE || act > ACT_BNRELU || (act == ACT_BNRELU && (!scale || !shift))) return XCP_EINVAL;
   SepArgs a{(const bf16*)X, scale, shift, dwt, (const bf16*)pw, (bf16*)D, (bf16*)Y, part, N, H, W, 1, H};
   sp_bands(N, H, a.nbands, a.bandH);
-#define SP_LAUNCH(A, C) hipLaunchKernelGGL((sep_fwd_kernel<A, C>), dim3(grid), dim3(512), 0, stream, a)
-  if (CIN == 64) {
-    if (act == ACT_NONE) SP_LAUNCH(ACT_NONE, 64);
-    else if (act == ACT_RELU) SP_LAUNCH(ACT_RELU, 64);
-    else SP_LAUNCH(ACT_BNRELU, 64);
+#define SP_LAUNCH(A, C, O, NH) hipLaunchKernelGGL((sep_fwd_kernel<A, C, O, NH>), dim3(grid), dim3(512), 0, stream, a)
+#define SP_ACTS(C, O, NH)                          \
+  if (act == ACT_NONE) SP_LAUNCH(ACT_NONE, C, O, NH); \
+  else if (act == ACT_RELU) SP_LAUNCH(ACT_RELU, C, O, NH); \
+  else SP_LAUNCH(ACT_BNRELU, C, O, NH);
+  if (COUT == 256) {
+    SP_ACTS(128, 256, 1)
+  } else if (CIN == 64) {
+    SP_ACTS(64, 128, 2)
   } else {
-    if (act == ACT_NONE) SP_LAUNCH(ACT_NONE, 128);
-    else if (act == ACT_RELU) SP_LAUNCH(ACT_RELU, 128);
-    else SP_LAUNCH(ACT_BNRELU, 128);
+    SP_ACTS(128, 128, 2)
   }
+#undef SP_ACTS
 #undef SP_LAUNCH
   return (int)hipGetLastError();
 }

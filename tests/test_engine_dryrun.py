@@ -66,7 +66,8 @@ def install_fake_lib(monkeypatch):
         if name == "xcp_maxpool_bwd_bnred_parts":
             return 4
         if name == "xcp_sep_fwd_parts":   # (dtype, N, H, W, CIN, COUT): block1's fused forward
-            ok = args[0] == 1 and args[4] in (64, 128) and args[5] == 128 and args[3] <= 152
+            ok = args[0] == 1 and ((args[4] in (64, 128) and args[5] == 128 and args[3] <= 152) or
+                                   (args[4] == 128 and args[5] == 256 and args[3] <= 78))
             return min(args[1], 256) if ok else 0
         if name == "xcp_unit_bwd_rows_per_split":   # (dtype, M, CO, CI): the fused narrow unit
             ok = args[0] == 1 and (args[2], args[3]) in ((128, 64), (128, 128), (256, 128), (256, 256))
@@ -153,9 +154,9 @@ def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn):
     else:
         assert "xcp_dw_bwd" not in names
         assert all(p.grad is None for p in m.feature_extractor.parameters())
-    # 34 depthwise + 34 pointwise convs per pass; in bf16 block1's two units run
-    # depthwise + pointwise as one fused launch
-    assert fake_lib.count("xcp_sep_fwd") == (2 if prec == "bf16" else 0)
+    # 34 depthwise + 34 pointwise convs per pass; in bf16 block1's two units and block2's
+    # first run depthwise + pointwise as one fused launch
+    assert fake_lib.count("xcp_sep_fwd") == (3 if prec == "bf16" else 0)
     assert fake_lib.count("xcp_dw_fwd") == 34 - fake_lib.count("xcp_sep_fwd")
     assert fake_lib.count("xcp_tail_fwd") == 12
 

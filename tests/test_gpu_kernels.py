@@ -1086,39 +1086,43 @@ def test_permute_batch_plans(ops, gpu):
         assert torch.equal(dst, ref)
 
 
-@pytest.mark.parametrize("CIN", [64, 128])
+@pytest.mark.parametrize("CIN,COUT", [(64, 128), (128, 128), (128, 256)])
 @pytest.mark.parametrize("act", [0, 1, 2])
-@pytest.mark.parametrize("N,H,W", [(2, 147, 147), (3, 9, 150), (5, 1, 152), (2, 6, 3), (1, 300, 37), (600, 3, 20)])
-def test_sep_fwd_vs_dw_and_gemm(ops, gpu, N, H, W, CIN, act):
-    """Fused depthwise + pointwise forward of block1's units (csrc/sepfwd.hip) against the two kernels it
-    replaces: D bitwise xcp_dw_fwd's, Y bitwise the 128x128 NT kernel's (same MFMA operands and K order),
-    the BN partial sums to fp32 summation order against the NT epilogue's; frames as wide as the kernel
-    takes, one row, three columns (W <= 8 powers of two take dwframe.hip, fp32 windows), fewer tiles than workgroups and
-    more (600 frames: a workgroup walks several frames, its look-ahead loads crossing tile boundaries)."""
-    g = torch.Generator(device=gpu).manual_seed(N * 1000 + H + W + CIN + act)
+@pytest.mark.parametrize("N,H,W", [(2, 147, 147), (3, 9, 150), (5, 1, 152), (2, 6, 3), (1, 300, 37), (600, 3, 20),
+                                   (2, 74, 74), (3, 5, 78)])
+def test_sep_fwd_vs_dw_and_gemm(ops, gpu, N, H, W, CIN, COUT, act):
+    """Fused depthwise + pointwise forward of block1's units and block2's first (csrc/sepfwd.hip) against
+    the two kernels it replaces: D bitwise xcp_dw_fwd's, Y bitwise the NT GEMM's (same MFMA operands and K
+    order; the 128x128 kernel for 128 outputs, the persistent 256x256 one for 256), the BN partial sums to
+    fp32 summation order against the NT epilogue's; frames as wide as each form takes, one row, three
+    columns (W <= 8 powers of two take dwframe.hip, fp32 windows), fewer tiles than workgroups and more
+    (600 frames: a workgroup walks several frames, its look-ahead loads crossing tile boundaries)."""
+    if COUT == 256 and W > 78:
+        pytest.skip("the 256-output form takes frames up to 78 wide")
+    g = torch.Generator(device=gpu).manual_seed(N * 1000 + H + W + CIN + COUT + act)
     M = N * H * W
     X = torch.randn(M, CIN, device=gpu, generator=g).bfloat16()
     sc = torch.rand(CIN, device=gpu, generator=g) + 0.5
     sh = torch.randn(CIN, device=gpu, generator=g) * 0.5
     dwt = torch.randn(9, CIN, device=gpu, generator=g) * 0.3
-    pw = (torch.randn(128, CIN, device=gpu, generator=g) / CIN ** 0.5).bfloat16()
+    pw = (torch.randn(COUT, CIN, device=gpu, generator=g) / CIN ** 0.5).bfloat16()
     D_ref = torch.empty(M, CIN, device=gpu, dtype=torch.bfloat16)
     ops.dw_fwd(act, X, D_ref, dwt, sc, sh, N, H, W, CIN)
-    Y_ref = torch.empty(M, 128, device=gpu, dtype=torch.bfloat16)
+    Y_ref = torch.empty(M, COUT, device=gpu, dtype=torch.bfloat16)
     R_ref = ops.nt_stat_rows(M)
-    part_ref = torch.zeros(R_ref * 2 * 128, device=gpu)
-    ops.gemm_nt(D_ref, pw, Y_ref, M, 128, CIN, stats=part_ref, tile=1)
-    R = ops.sep_fwd_parts(torch.bfloat16, N, H, W, CIN, 128)
+    part_ref = torch.zeros(R_ref * 2 * COUT, device=gpu)
+    ops.gemm_nt(D_ref, pw, Y_ref, M, COUT, CIN, stats=part_ref)
+    R = ops.sep_fwd_parts(torch.bfloat16, N, H, W, CIN, COUT)
     assert 0 < R <= min(N * H, torch.cuda.get_device_properties(gpu).multi_processor_count)
     D = torch.full((M, CIN), float("nan"), device=gpu, dtype=torch.bfloat16)
-    Y = torch.full((M, 128), float("nan"), device=gpu, dtype=torch.bfloat16)
-    part = torch.full((R * 2 * 128,), float("nan"), device=gpu)
-    ops.sep_fwd(act, X, sc, sh, dwt, pw, D, Y, part, N, H, W, CIN, 128)
+    Y = torch.full((M, COUT), float("nan"), device=gpu, dtype=torch.bfloat16)
+    part = torch.full((R * 2 * COUT,), float("nan"), device=gpu)
+    ops.sep_fwd(act, X, sc, sh, dwt, pw, D, Y, part, N, H, W, CIN, COUT)
     torch.cuda.synchronize()
     assert torch.equal(D, D_ref)
     assert torch.equal(Y, Y_ref)
-    sums = part.view(R, 2, 128).double().sum(0)
-    sums_ref = part_ref.view(R_ref, 2, 128).double().sum(0)
+    sums = part.view(R, 2, COUT).double().sum(0)
+    sums_ref = part_ref.view(R_ref, 2, COUT).double().sum(0)
     yd = Y_ref.double()
     exact = torch.stack([yd.sum(0), (yd * yd).sum(0)])
     scale = torch.stack([yd.abs().sum(0), (yd * yd).sum(0)]) + 1e-30
@@ -1130,4 +1134,6 @@ def test_sep_fwd_rejects_unsupported(ops, gpu):
     assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 153, 64, 128) == 0   # wider than 152
     assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 8, 256, 128) == 0
     assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 8, 64, 256) == 0
+    assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 79, 128, 256) == 0   # the 256-output form: one half row
+    assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 8, 256, 256) == 0
     assert ops.sep_fwd_parts(torch.float32, 2, 8, 8, 64, 128) == 0
