@@ -192,15 +192,18 @@ int xcp_permute3(int out_dtype, const float* in, void* out, int d0, int d1, int 
  * mode 0: Y[N][IH-2][IW-2][64] = conv3x3(X[N][IH][IW][32], W[64][9][32]); stats (may be null):
  *         BatchNorm partial sums [parts][2][64] of the stored values
  * mode 1: input gradient: Y[N][IH+2][IW+2][32] from X = dY[N][IH][IW][64], W = [32][9][64]
+ * in_scale / in_shift (mode 0, may be null): X is the raw input of a BatchNorm + ReLU, applied on load
+ * (relu(x * in_scale[c] + in_shift[c]) rounded to bf16: bitwise the xcp_bn_act of X fed in)
  * xcp_conv3x3_parts returns the workgroup count (stats rows), 0 if the width is unsupported */
 int xcp_conv3x3_parts(int mode, int N, int IH, int IW);
 int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, int N, int IH, int IW,
-                xcp_stream_t stream);
+                const float* in_scale, const float* in_shift, xcp_stream_t stream);
 /* weight gradient of mode 0 (replaces the autograd wgrad of Xception.conv2, Xception.py:122):
  * P[parts][64][9*32] fp32 slabs whose sum is dW[co][kh*3+kw][ci], from dY[N][IH-2][IW-2][64]
  * and X[N][IH][IW][32]; xcp_conv3x3_wgrad_parts returns the slab count, 0 if unsupported */
 int xcp_conv3x3_wgrad_parts(int N, int IH, int IW);
-int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, int IW, xcp_stream_t stream);
+int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, int IW, const float* in_scale,
+                      const float* in_shift, xcp_stream_t stream);   /* in_scale / in_shift: as xcp_conv3x3 */
 
 /* ---- clip input (video_dataloader.py:22-68): uint8 frames -> fp32 model input ----
  * in [B][Tmax][H][W][3] uint8 (device), len [B] int32 (device): frames t >= len[b] are padding;

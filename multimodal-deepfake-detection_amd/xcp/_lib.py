@@ -79,9 +79,9 @@ SIGNATURES = {
     "xcp_opt_adam": [P, I, P, F, F, F, F, F, F, F, P],
     "xcp_opt_adam_dev": [P, I, P, F, D, D, F, F, P, P],
     "xcp_conv3x3_parts": [I, I, I, I],
-    "xcp_conv3x3": [I, P, P, P, P, I, I, I, P],
+    "xcp_conv3x3": [I, P, P, P, P, I, I, I, P, P, P],
     "xcp_conv3x3_wgrad_parts": [I, I, I],
-    "xcp_conv3x3_wgrad": [P, P, P, I, I, I, P],
+    "xcp_conv3x3_wgrad": [P, P, P, I, I, I, P, P, P],
     "xcp_arcface_fwd": [P, P, P, P, I, I, I, F, F, P],
     "xcp_arcface_bwd": [P, P, P, P, P, P, I, I, I, F, F, P],
     "xcp_focal_ce": [P, P, P, F, P, P, P, I, I, P],

@@ -46,6 +46,78 @@ XCP_DEV void wait_vmcnt_dyn(int n) {
   }
 }
 
+// In-place BN + ReLU of staged input chunks (ACTIN): LDS accesses by inline asm, since a compiler-visible
+// access to LDS an LDS-DMA may still be writing makes hipcc wait for every outstanding vector-memory
+// operation (here: the next tile's / row's DMA, issued just before)
+typedef unsigned c3u4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64;
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+XCP_DEV c3u4 c3_rd128(const char* p) {
+  c3u4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((unsigned)(size_t)(const __attribute__((address_space(3))) char*)(p))
+               : "memory");
+  return v;
+}
+XCP_DEV void c3_wr128(char* p, c3u4 v) {
+  asm volatile("ds_write_b128 %0, %1" :: "v"((unsigned)(size_t)(__attribute__((address_space(3))) char*)(p)), "v"(v)
+               : "memory");
+}
+XCP_DEV u64 ds_read_tr_u64(const char* p) {
+  u64 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1"
+               : "=v"(v)
+               : "v"((unsigned)(size_t)(const __attribute__((address_space(3))) char*)(p))
+               : "memory");
+  return v;
+}
+// s_waitcnt lgkmcnt(0) that a chunk's 20 fragment halves depend on (no use is scheduled ahead of it)
+XCP_DEV void c3_tr_fence(u64 (&g)[2], u64 (&b)[9][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(g[0]), "+v"(g[1]), "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]),
+                 "+v"(b[2][1]), "+v"(b[3][0]), "+v"(b[3][1]), "+v"(b[4][0]), "+v"(b[4][1]), "+v"(b[5][0]),
+                 "+v"(b[5][1]), "+v"(b[6][0]), "+v"(b[6][1]), "+v"(b[7][0]), "+v"(b[7][1]), "+v"(b[8][0]),
+                 "+v"(b[8][1])
+               :
+               : "memory");
+}
+// the BN parameters (n <= 64 floats each) into LDS by LDS-DMA from wave 0 (lane i -> word i): a
+// compiler-visible global load here makes hipcc drain every in-flight DMA before the main loop's LDS reads
+XCP_DEV void c3_load_prm(float* sc, float* sh, const float* isc, const float* ish, int n, int lane) {
+  if (lane < n) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(isc + lane),
+                                     (void __attribute__((address_space(3)))*)sc, 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(ish + lane),
+                                     (void __attribute__((address_space(3)))*)sh, 4, 0, 0);
+  }
+}
+// relu(x * sc + sh) of 8 bf16 (rounded to bf16, as bn_act does); c8: first channel
+XCP_DEV c3u4 c3_act(c3u4 v, const float* sc, const float* sh, int c8) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float lo = fmaxf(fmaf(__uint_as_float(v[e] << 16), sc[c8 + 2 * e], sh[c8 + 2 * e]), 0.f);
+    const float hi = fmaxf(fmaf(__uint_as_float(v[e] & 0xffff0000u), sc[c8 + 2 * e + 1], sh[c8 + 2 * e + 1]), 0.f);
+    bf16x4 b;
+    b[0] = (bf16)lo;
+    b[1] = (bf16)hi;
+    const u16x4 r = __builtin_bit_cast(u16x4, b);
+    v[e] = (unsigned)r[0] | ((unsigned)r[1] << 16);
+  }
+  return v;
+}
+// activate chunks q = q0, q0 + step, ... < total of an LDS buffer; chunk q holds channels c8(q) .. +7
+template <int MAXK, typename C8>
+XCP_DEV void c3_act_chunks(char* base, int q0, int step, int total, const float* sc, const float* sh, C8 c8) {
+  c3u4 v[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) v[k] = c3_rd128(base + min(q0 + k * step, total - 1) * 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    const int q = q0 + k * step;
+    if (q < total) c3_wr128(base + q * 16, c3_act(v[k], sc, sh, c8(q)));
+  }
+}
+
 // 16-B chunk swizzle of LDS column x (brute-force checked: conflict-free ds_read_b128 for
 // 16 consecutive columns at any row offset); depends on x mod 8 only
 template <int CIN>
@@ -55,10 +127,13 @@ XCP_DEV int cswz(int x) {
 }
 
 
-template <int CIN, int COUT, int PAD, int TH, int MAXIW, bool STATS, int NW, bool PIPE>
+// ACTIN: X is the raw input of a BatchNorm + ReLU (the stem's conv1 output): each staged tile is
+// activated in place, relu(x * isc[c] + ish[c]) rounded to bf16 as bn_act does, before its reads
+template <int CIN, int COUT, int PAD, int TH, int MAXIW, bool STATS, int NW, bool PIPE, bool ACTIN = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void conv3x3_kernel(const bf16* __restrict__ X, const bf16* __restrict__ Wp,
                                                          bf16* __restrict__ Y, float* __restrict__ stats, int N,
-                                                         int IH, int IW) {
+                                                         int IH, int IW, const float* __restrict__ isc,
+                                                         const float* __restrict__ ish) {
   constexpr int CPP = CIN / 8;                // 16-B chunks per pixel
   constexpr int PB = CPP * 16;                // LDS bytes per pixel
   constexpr int KS = CIN / 32;                // 32-deep MFMA steps per tap
@@ -67,7 +142,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void conv3x3_kernel(const bf16* __
   constexpr int BUF = ((TH + 2) * (MAXIW + 2 * PAD) + 16) * PB;   // + slack for junk columns past OW
   constexpr int F3 = 3 * KS;                  // B-fragments per pipeline third (9 x KS per item)
   static_assert(COUT % 32 == 0, "pieces are exchanged between channel-group pairs");
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  // (the BN parameters live in the same LDS object as the tiles: with a second object the LDS accesses
+  // carry alias scopes, and hipcc then waits for all in-flight DMA before the fragment reads)
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + (ACTIN ? 8 * CIN : 0)];
+  float* const sprm0 = reinterpret_cast<float*>(smem + 2 * BUF);
+  float* const sprm1 = sprm0 + CIN;
   const int OH = IH + 2 * PAD - 2, OW = IW + 2 * PAD - 2, LW = IW + 2 * PAD;
   const int tiles_h = (OH + TH - 1) / TH, ntiles = N * tiles_h, G = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
@@ -97,6 +176,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void conv3x3_kernel(const bf16* __
 
   int t = blockIdx.x;
   if (t >= ntiles) return;   // uniform, before any barrier
+  static_assert(!ACTIN || CIN <= 64, "one DMA lane per channel");
+  if constexpr (ACTIN)   // lands with tile t (first wait: vmcnt(0))
+    if (wsc == 0) c3_load_prm(sprm0, sprm1, isc, ish, CIN, lane);
   stage(t, 0);
 
   // ---- kernel fragments, loaded once: wf[cg][tap][ks] = W[co0+cg*16+fr][tap'][ks*32 + fg*8 .. +8]
@@ -133,6 +215,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void conv3x3_kernel(const bf16* __
     // flight) -> for every wave.  (__syncthreads would wait for those stores too: vmcnt(0).)
     wait_vmcnt_dyn(prev_st);
     lds_barrier();
+    if constexpr (ACTIN) {   // (rows past the image turn from zero into junk that only rows past OH read)
+      // before the next tile's DMA is issued: no LDS-DMA is in flight while the tile is rewritten
+      constexpr int MAXK = ((TH + 2) * MAXIW * CPP + NW * 64 - 1) / (NW * 64);
+      c3_act_chunks<MAXK>(smem + (k & 1) * BUF, tid, NW * 64, total, sprm0, sprm1, [&](int q) {
+        const int p = q / CPP, cpos = q - p * CPP;
+        return (cpos ^ cswz<CIN>(PIPE ? p % LW : p)) * 8;
+      });
+      lds_barrier();
+    }
     if (t + G < ntiles) stage(t + G, (k + 1) & 1);   // streams in under this tile's MFMAs
     const char* sb = smem + (k & 1) * BUF;
     const int n = t / tiles_h, oh0 = (t - n * tiles_h) * TH;
@@ -287,10 +378,16 @@ constexpr int WG_GI = WG_GSLOT / 1024, WG_AI = WG_ASLOT / 1024;   // 1-KB DMA in
 static_assert((WG_GI + WG_AI) % 8 == 0, "uniform DMA count per wave");
 constexpr int WG_PER_WAVE = (WG_GI + WG_AI) / 8;            // 4
 
+// ACTIN: X is the raw input of a BatchNorm + ReLU (isc / ish), activated in place as each row lands
+template <bool ACTIN>
 __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
                                                                float* __restrict__ P, int N, int IH, int IW, int nb,
-                                                               int RB) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * WG_GSLOT + 5 * WG_ASLOT];
+                                                               int RB, const float* __restrict__ isc,
+                                                               const float* __restrict__ ish) {
+  // (BN parameters inside the ring's LDS object: see conv3x3_kernel)
+  __shared__ __attribute__((aligned(16))) char smem[3 * WG_GSLOT + 5 * WG_ASLOT + (ACTIN ? 256 : 0)];
+  float* const sprm0 = reinterpret_cast<float*>(smem + 3 * WG_GSLOT + 5 * WG_ASLOT);
+  float* const sprm1 = sprm0 + 32;
   char* gs = smem;
   char* as = smem + 3 * WG_GSLOT;
   const int OH = IH - 2, OW = IW - 2;
@@ -325,6 +422,14 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __res
     }
   };
   if (r0 >= r1) return;   // uniform
+  if constexpr (ACTIN)   // issued before the rows: complete at the first step's wait
+    if (wsc == 0) c3_load_prm(sprm0, sprm1, isc, ish, 32, lane);
+  // X row of ring slot row % 5 activated in place (pixels past IW turn into junk that meets only the
+  // zero dY past OW)
+  auto act_row = [&](int row) {
+    c3_act_chunks<(WG_APX * 4 + 511) / 512>(as + (row % 5) * WG_ASLOT, tid, 512, WG_APX * 4, sprm0, sprm1,
+                                            [](int q) { return ((q & 3) ^ ((((q >> 2) >> 2) & 1) << 1)) * 8; });
+  };
   // prologue: dY row r0 and X rows r0, r0 + 1, r0 + 2 (56 instructions, 7 per wave), then step r0 + 1
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
@@ -348,32 +453,54 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __res
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();   // (not __syncthreads: that would also drain the next row's DMA)
     if (oh + 2 < r1) issue_step(oh + 2);
+    if constexpr (ACTIN) {   // the X row that landed for this step (at the first step all three)
+      if (oh == r0) {
+        act_row(r0);
+        act_row(r0 + 1);
+      }
+      act_row(oh + 2);
+      lds_barrier();
+    }
     const char* gslot = gs + (oh % 3) * WG_GSLOT;
     const char* a0 = as + (oh % 5) * WG_ASLOT;
     const char* a1 = as + ((oh + 1) % 5) * WG_ASLOT;
     const char* a2 = as + ((oh + 2) % 5) * WG_ASLOT;
     const char* arow[3] = {a0, a1, a2};
-    for (int ch = 0; ch < nch; ++ch) {
+    // fragments of chunk ch: the transposed dY fragment (g) and the nine shifted X fragments (b), each
+    // two 64-bit halves.  Transposed reads by inline asm: hipcc waits vmcnt(0) before every
+    // ds_read_tr builtin while any LDS-DMA is in flight (here: the next two rows, drained each row);
+    // the counted vmcnt + barrier above orders them, c3_tr_fence retires them before their use.
+    auto rd = [&](int ch, u64 (&g)[2], u64 (&b)[9][2]) {
       const int pb = ch * 32 + 4 * fg + q4;
-      bf16x8 A;
-      {
-        const int plo = pb, phi = pb + 16;
-        const bf16x4 lo = ds_read_tr(gslot + plo * 128 + ((gch ^ (plo & 7)) << 4) + sub);
-        const bf16x4 hi = ds_read_tr(gslot + phi * 128 + ((gch ^ (phi & 7)) << 4) + sub);
-        A = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      bf16x8 B[9];
+      g[0] = ds_read_tr_u64(gslot + pb * 128 + ((gch ^ (pb & 7)) << 4) + sub);
+      g[1] = ds_read_tr_u64(gslot + (pb + 16) * 128 + ((gch ^ ((pb + 16) & 7)) << 4) + sub);
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw) {
           const int plo = pb + kw, phi = pb + kw + 16;
-          const bf16x4 lo = ds_read_tr(arow[kh] + plo * 64 + ((ach ^ (((plo >> 2) & 1) << 1)) << 4) + sub);
-          const bf16x4 hi = ds_read_tr(arow[kh] + phi * 64 + ((ach ^ (((phi >> 2) & 1) << 1)) << 4) + sub);
-          B[kh * 3 + kw] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          b[kh * 3 + kw][0] = ds_read_tr_u64(arow[kh] + plo * 64 + ((ach ^ (((plo >> 2) & 1) << 1)) << 4) + sub);
+          b[kh * 3 + kw][1] = ds_read_tr_u64(arow[kh] + phi * 64 + ((ach ^ (((phi >> 2) & 1) << 1)) << 4) + sub);
         }
+    };
+    auto mma = [&](const u64 (&g)[2], const u64 (&b)[9][2]) {
+      const bf16x8 A = __builtin_bit_cast(bf16x8, u64x2{g[0], g[1]});
 #pragma unroll
-      for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[t], acc[t], 0, 0, 0);
+      for (int t = 0; t < 9; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, __builtin_bit_cast(bf16x8, u64x2{b[t][0], b[t][1]}), acc[t],
+                                                         0, 0, 0);
+    };
+    // two register sets: chunk ch + 1's reads fly under chunk ch's MFMAs
+    u64 gA[2], bA[9][2], gB[2], bB[9][2];
+    rd(0, gA, bA);
+    for (int ch = 0; ch < nch; ch += 2) {
+      c3_tr_fence(gA, bA);
+      if (ch + 1 < nch) rd(ch + 1, gB, bB);
+      mma(gA, bA);
+      if (ch + 1 >= nch) break;
+      c3_tr_fence(gB, bB);
+      if (ch + 2 < nch) rd(ch + 2, gA, bA);
+      mma(gB, bB);
     }
   }
   // acc[t][r] = dW[co = 16cb + 4fg + r][tap t][ci = 16bb + fr]
@@ -442,29 +569,32 @@ int xcp_conv3x3_parts(int mode, int N, int IH, int IW) {
 // mode 1: Y[N][IH+2][IW+2][32] = input gradient of that conv from X = dY[N][IH][IW][64],
 //         W = the forward kernel transposed to [32][9][64] (flipped inside).  bf16 only.
 int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, int N, int IH, int IW,
-                hipStream_t st) {
+                const float* in_scale, const float* in_shift, hipStream_t st) {
   if (N <= 0) return XCP_OK;
   if (IH < 3 || IW < 3 || (mode != 0 && mode != 1) || (mode == 1 && stats)) return XCP_EINVAL;
+  if ((in_scale != nullptr) != (in_shift != nullptr) || (mode == 1 && in_scale)) return XCP_EINVAL;
   if (IW > (mode == 0 ? MAXIW_FWD : MAXIW_DGRAD)) return XCP_EUNSUPPORTED;
   const dim3 grid((unsigned)xcp_conv3x3_parts(mode, N, IH, IW));
-  if (mode == 0 && conv3_fwd_2wg()) {
-    if (stats)
-      hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD2, MAXIW_FWD, true, NW_FWD2, true>), grid, dim3(64 * NW_FWD2), 0,
-                         st, (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
-    else
-      hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD2, MAXIW_FWD, false, NW_FWD2, true>), grid, dim3(64 * NW_FWD2), 0,
-                         st, (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
-  } else if (mode == 0) {
-    if (stats)
-      hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD, MAXIW_FWD, true, NW_FWD, true>), grid, dim3(64 * NW_FWD), 0, st, (const bf16*)X,
-                         (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
-    else
-      hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH_FWD, MAXIW_FWD, false, NW_FWD, true>), grid, dim3(64 * NW_FWD), 0, st,
-                         (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+  const bf16 *x = (const bf16*)X, *w = (const bf16*)W;
+  bf16* y = (bf16*)Y;
+#define XCP_C3F(TH, NW, STATS, ACT)                                                                                  \
+  hipLaunchKernelGGL((conv3x3_kernel<32, 64, 0, TH, MAXIW_FWD, STATS, NW, true, ACT>), grid, dim3(64 * NW), 0, st, x, w, y, \
+                     stats, N, IH, IW, in_scale, in_shift)
+  if (mode == 0) {
+    const bool two = conv3_fwd_2wg(), act = in_scale != nullptr;
+    if (two && stats && act) XCP_C3F(TH_FWD2, NW_FWD2, true, true);
+    else if (two && stats) XCP_C3F(TH_FWD2, NW_FWD2, true, false);
+    else if (two && act) XCP_C3F(TH_FWD2, NW_FWD2, false, true);
+    else if (two) XCP_C3F(TH_FWD2, NW_FWD2, false, false);
+    else if (stats && act) XCP_C3F(TH_FWD, NW_FWD, true, true);
+    else if (stats) XCP_C3F(TH_FWD, NW_FWD, true, false);
+    else if (act) XCP_C3F(TH_FWD, NW_FWD, false, true);
+    else XCP_C3F(TH_FWD, NW_FWD, false, false);
   } else {
     hipLaunchKernelGGL((conv3x3_kernel<64, 32, 2, TH_DGRAD, MAXIW_DGRAD, false, NW_DGRAD, false>), grid, dim3(64 * NW_DGRAD), 0, st,
-                       (const bf16*)X, (const bf16*)W, (bf16*)Y, stats, N, IH, IW);
+                       x, w, y, stats, N, IH, IW, nullptr, nullptr);
   }
+#undef XCP_C3F
   return (int)hipGetLastError();
 }
 
@@ -478,14 +608,19 @@ int xcp_conv3x3_wgrad_parts(int N, int IH, int IW) {
 
 // P[parts][64][9 * 32] (fp32 slabs, sum them for dW[co][tap][ci]) = weight gradient of
 // Y = conv3x3(X) from dY[N][IH-2][IW-2][64] and X[N][IH][IW][32].  bf16 only.
-int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, int IW, hipStream_t st) {
+int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, int IW, const float* in_scale,
+                      const float* in_shift, hipStream_t st) {
   if (N <= 0) return XCP_OK;
-  if (IH < 3 || IW < 3) return XCP_EINVAL;
+  if (IH < 3 || IW < 3 || (in_scale != nullptr) != (in_shift != nullptr)) return XCP_EINVAL;
   if (IW - 2 > WG_GPX) return XCP_EUNSUPPORTED;
   int nb, rb;
   wgrad_bands(N, IH - 2, nb, rb);
-  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N, IH, IW,
-                     nb, rb);
+  if (in_scale)
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<true>, dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N, IH,
+                       IW, nb, rb, in_scale, in_shift);
+  else
+    hipLaunchKernelGGL(conv3x3_wgrad_kernel<false>, dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N,
+                       IH, IW, nb, rb, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 

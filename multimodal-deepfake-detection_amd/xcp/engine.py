@@ -144,6 +144,9 @@ REDUCE_BATCH = os.environ.get("XCP_REDUCE_BATCH", "1") != "0"
 # (csrc/sepfwd.hip): the depthwise output goes to the MFMAs through LDS instead of back through HBM
 # (XCP_SEP_FUSED=0: the two kernels; A/B)
 SEP_FUSED = os.environ.get("XCP_SEP_FUSED", "1") != "0"
+# the stem conv2 (forward and weight gradient) applies BN1 + ReLU on load instead of reading a
+# materialised relu(bn1(conv1)) (XCP_CONV2_ACTIN=0: bn_act + the plain conv; A/B)
+CONV2_ACT_ON_LOAD = os.environ.get("XCP_CONV2_ACTIN", "1") != "0"
 NT_TILE = int(os.environ.get("XCP_NT_TILE", "4" if os.environ.get("XCP_NT_ONESHOT", "0") == "1" else "0"))
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
@@ -351,15 +354,24 @@ class XceptionEngine:
         else:
             ops.conv1_fwd(x, m.conv1.weight.detach(), c1, N, IH, IW)
             s1 = self._bn_stats(None, 0, 32, rows1, m.bn1, False)
-        a1 = self._empty(rows1 * 32)
-        ops.bn_act(c1, a1, s1.scale, s1.shift, True, rows1, 32)
         OH2, OW2 = OH1 - 2, OW1 - 2
         rows2 = N * OH2 * OW2
         R2 = ops.conv3x3_parts(0, N, OH1, OW1) if self.dtype == torch.bfloat16 else 0
+        # conv2 and its weight gradient apply BN1 + ReLU to conv1's output as they stage it: a1 =
+        # relu(bn1(c1)) is never written (CONV2_ACT_ON_LOAD)
+        act_on_load = CONV2_ACT_ON_LOAD and R2 > 0 and (not train or ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0)
+        if act_on_load:
+            a1 = None
+        else:
+            a1 = self._empty(rows1 * 32)
+            ops.bn_act(c1, a1, s1.scale, s1.shift, True, rows1, 32)
         if R2 > 0:   # direct MFMA conv (conv3.hip)
             c2 = self._empty(rows2 * 64)
             part = self._empty(R2 * 2 * 64, torch.float32) if train else None
-            ops.conv3x3(0, a1, pk["conv2"], c2, part, N, OH1, OW1)
+            if act_on_load:
+                ops.conv3x3(0, c1, pk["conv2"], c2, part, N, OH1, OW1, in_scale=s1.scale, in_shift=s1.shift)
+            else:
+                ops.conv3x3(0, a1, pk["conv2"], c2, part, N, OH1, OW1)
             s2 = self._bn_stats(part, R2, 64, rows2, m.bn2, train)
         else:        # implicit GEMM (im2col gather)
             c2, s2 = self._pw(a1, pk["conv2"], rows2, 64, 288, train, m.bn2, lda=32,
@@ -603,7 +615,9 @@ class XceptionEngine:
             c2g, acc = g("conv2.weight", (64, 32, 3, 3))   # (allocated on the main stream)
             with torch.cuda.stream(st2) if st2 is not None else contextlib.nullcontext():
                 w2g = torch.empty(64 * 288, device=dev, dtype=torch.float32)
-                if self.dtype == torch.bfloat16 and ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0:
+                if S["a1"] is None:   # (conv2 read conv1's output with BN1 + ReLU on load)
+                    ops.conv3x3_wgrad(dC2, S["c1"], w2g, N, OH1, OW1, in_scale=S["s1"].scale, in_shift=S["s1"].shift)
+                elif self.dtype == torch.bfloat16 and ops.conv3x3_wgrad_parts(N, OH1, OW1) > 0:
                     ops.conv3x3_wgrad(dC2, S["a1"], w2g, N, OH1, OW1)
                 else:
                     ops.weight_grad(dC2, S["a1"], rows2, 64, 288, w2g, gather=(2, OH1, OW1, OH2, OW2, 1, 32), ldx=32)

@@ -499,28 +499,30 @@ def conv3x3_parts(mode, N, IH, IW):
     return _lib.call("xcp_conv3x3_parts", mode, N, IH, IW)
 
 
-def conv3x3(mode, X, W, Y, stats, N, IH, IW):
+def conv3x3(mode, X, W, Y, stats, N, IH, IW, in_scale=None, in_shift=None):
     """Stem conv2 as a direct MFMA conv (bf16): mode 0 forward 32->64 (+ BN partial sums),
-    mode 1 its input gradient 64->32 (W = the [32][9][64] transposed kernel)."""
+    mode 1 its input gradient 64->32 (W = the [32][9][64] transposed kernel).  in_scale /
+    in_shift (mode 0): X is conv1's raw output, BN1 + ReLU applied on load."""
     if X.dtype != torch.bfloat16:
         raise ValueError("xcp_conv3x3 is bf16 only")
-    _lib.call("xcp_conv3x3", mode, _p(X), _p(W), _p(Y), _p(stats), N, IH, IW, stream())
+    _lib.call("xcp_conv3x3", mode, _p(X), _p(W), _p(Y), _p(stats), N, IH, IW, _p(in_scale), _p(in_shift), stream())
 
 
 def conv3x3_wgrad_parts(N, IH, IW):
     return _lib.call("xcp_conv3x3_wgrad_parts", N, IH, IW)
 
 
-def conv3x3_wgrad(dY, X, out, N, IH, IW):
+def conv3x3_wgrad(dY, X, out, N, IH, IW, in_scale=None, in_shift=None):
     """out[64][9*32] fp32 = weight gradient of the stem conv2 (tap-major, [co][kh*3+kw][ci])
-    from dY [N,IH-2,IW-2,64] and X [N,IH,IW,32] (bf16): per-workgroup slabs + colreduce."""
+    from dY [N,IH-2,IW-2,64] and X [N,IH,IW,32] (bf16): per-workgroup slabs + colreduce.
+    in_scale / in_shift: X is conv1's raw output, BN1 + ReLU applied on load."""
     if dY.dtype != torch.bfloat16 or X.dtype != torch.bfloat16:
         raise ValueError("xcp_conv3x3_wgrad is bf16 only")
     S = conv3x3_wgrad_parts(N, IH, IW)
     if S <= 0:
         raise ValueError("xcp_conv3x3_wgrad: unsupported width")
     P = torch.empty(S * 64 * 288, device=dY.device, dtype=torch.float32)
-    _lib.call("xcp_conv3x3_wgrad", _p(dY), _p(X), _p(P), N, IH, IW, stream())
+    _lib.call("xcp_conv3x3_wgrad", _p(dY), _p(X), _p(P), N, IH, IW, _p(in_scale), _p(in_shift), stream())
     reduce_slabs(P, S, 64 * 288, out)
 
 

@@ -907,6 +907,43 @@ def test_conv3x3_stem_fwd_dgrad(ops, gpu, N, IH, IW):
     assert rel_err(got, ref_dw) < 1e-4
 
 
+@pytest.mark.parametrize("N,IH,IW", [(2, 149, 149), (3, 21, 38), (1, 6, 147)])
+def test_conv3x3_bn_relu_on_load_bitwise(ops, gpu, N, IH, IW):
+    """in_scale / in_shift (the stem's BN1 + ReLU applied to each staged conv1-output tile, forward and
+    weight gradient) against bn_act into a separate activation followed by the plain kernels: the same
+    rounded activations meet the same MFMAs, so the outputs, the BN partial sums and the weight-gradient
+    slabs are bitwise equal (junk activated past the image only meets rows / columns never stored or a
+    zero dY)."""
+    g = torch.Generator(device=gpu).manual_seed(IH + 7 * IW)
+    rows = N * IH * IW
+    x = (torch.randn(rows, 32, device=gpu, generator=g) * 1.5 + 0.3).bfloat16()
+    sc = torch.rand(32, device=gpu, generator=g) + 0.4
+    sh = torch.randn(32, device=gpu, generator=g) * 0.5
+    Wp = (torch.randn(64, 288, device=gpu, generator=g) / 17).bfloat16()
+    a = torch.empty_like(x)
+    ops.bn_act(x, a, sc, sh, True, rows, 32)
+    OH, OW = IH - 2, IW - 2
+    R = ops.conv3x3_parts(0, N, IH, IW)
+    outs = []
+    for src, kw in ((a, {}), (x, {"in_scale": sc, "in_shift": sh})):
+        stats = torch.full((R, 2, 64), float("nan"), device=gpu)
+        Y = torch.full((N * OH * OW, 64), float("nan"), device=gpu, dtype=torch.bfloat16)
+        ops.conv3x3(0, src, Wp, Y, stats, N, IH, IW, **kw)
+        outs.append((Y, stats))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    dy = torch.randn(N * OH * OW, 64, device=gpu, generator=g).bfloat16()
+    dws = []
+    for src, kw in ((a, {}), (x, {"in_scale": sc, "in_shift": sh})):
+        dW = torch.full((64 * 288,), float("nan"), device=gpu)
+        ops.conv3x3_wgrad(dy, src, dW, N, IH, IW, **kw)
+        dws.append(dW)
+    assert torch.equal(dws[0], dws[1])
+    ref_dw = torch.nn.grad.conv2d_weight(nchw(a.view(N, IH, IW, 32)).float(), (64, 32, 3, 3),
+                                         nchw(dy.view(N, OH, OW, 64)).float())
+    assert rel_err(dws[1].view(64, 3, 3, 32).permute(0, 3, 1, 2), ref_dw) < 1e-4
+
+
 @pytest.mark.parametrize("N,IH,IW", [(3, 149, 149), (2, 9, 40)])
 def test_conv3x3_fwd_two_workgroup_form(ops, gpu, monkeypatch, N, IH, IW):
     """XCP_CONV3_FWD_2WG=1 (two 4-wave workgroups per CU on 2-row tiles): the same MFMAs per output

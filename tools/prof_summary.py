@@ -64,8 +64,9 @@ def load(path):
     rows = []
     if path.endswith(".db"):
         c = sqlite3.connect(path)
-        for name, dur, grid in c.execute("select name, duration, grid_x from kernels order by start"):
-            rows.append((name, dur, (grid,)))
+        for name, dur, grid, wg, lds, vgpr in c.execute(
+                "select name, duration, grid_x, workgroup_x, lds_size, vgpr_count from kernels order by start"):
+            rows.append((name, dur, (grid, wg, lds, vgpr)))
     else:
         with open(path) as f:
             for r in csv.DictReader(f):
