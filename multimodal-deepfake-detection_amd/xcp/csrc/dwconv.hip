@@ -480,23 +480,35 @@ XCP_DEV void stage_row(const T* frame, int h, int H, int W, int C, const RowLane
 }
 
 // Write the staged output row (20 pixels x 64 B in `stg`) to row h: two 16-B stores
-// per lane-slot; lanes without a valid pixel write the sink.
+// per lane-slot; lanes without a valid pixel write the sink.  The staging reads are inline asm:
+// the staging shares the ring's LDS object, and a compiler-visible read of it would make hipcc
+// wait for every LDS-DMA in flight (vmcnt(0): the look-ahead rows) before the stores.
+typedef unsigned dwu4 __attribute__((ext_vector_type(4)));
 template <typename T>
 XCP_DEV void store_row(T* frame, int h, int W, int C, const RowLanes& rl, const char* stg, int lane) {
   T* row = frame + (long)h * W * C;
+  dwu4 v[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int ch = i * 64 + lane;
-    const uint4 v = *reinterpret_cast<const uint4*>(stg + min(ch, 4 * RCOLS - 1) * 16);
+    asm volatile("ds_read_b128 %0, %1"
+                 : "=v"(v[i])
+                 : "v"((unsigned)(size_t)(const __attribute__((address_space(3))) char*)(stg + min(ch, 4 * RCOLS - 1) * 16))
+                 : "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]) : : "memory");
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
     uint4* dstp = rl.off[i] >= 0 ? reinterpret_cast<uint4*>(row + rl.off[i]) : g_dsink + lane;
-    *dstp = v;
+    *dstp = make_uint4(v[i][0], v[i][1], v[i][2], v[i][3]);
   }
 }
 
-// LDS reads of the DMA ring by inline asm: a plain C++ read of LDS that an LDS-DMA may write makes
-// hipcc drain every outstanding vector-memory operation first (s_waitcnt vmcnt(0)) -- here right
-// after a step had issued the look-ahead rows, so every step waited for the rows it had just asked
-// for and the look-ahead never overlapped anything.  The counted vmwait at the top of a step is what
+// LDS reads of the DMA ring by inline asm (XCP_DW_BWD_ASM=1): while the output staging was a second
+// __shared__ object, a plain C++ read of the ring made hipcc drain every outstanding vector-memory
+// operation first (s_waitcnt vmcnt(0)), right after a step had issued the look-ahead rows; the asm
+// reads avoided that.  With one LDS object the plain reads carry no such wait
+// (test_dma_pipelines_not_drained_by_compiler_waits).  The counted vmwait at the top of a step is what
 // orders the ring; ring_fence() retires the asm reads before their values are used (pinned through
 // "+v" operands, so no use is scheduled ahead of the wait).
 XCP_DEV unsigned ring_u32(const char* p) {
@@ -535,8 +547,11 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   constexpr int BD = BDV;                                // rows of look-ahead per staged tensor
   constexpr int NS = BD + 1;                             // X / dRes ring slots
   constexpr int NSG = ROLL ? NS : BD + 3;                // dY ring slots
-  __shared__ __attribute__((aligned(16))) char sm[4][(NS + NSG + (RES ? NS : 0)) * LROW];
-  __shared__ __attribute__((aligned(16))) char so[4][RCOLS * SLICE];   // output staging (separate object)
+  // one LDS object for the rings and the output staging: with a second object the LDS accesses carry
+  // alias scopes, and hipcc then drains every in-flight LDS-DMA (vmcnt(0)) ahead of the first plain
+  // ring read of a step, right after the look-ahead row was issued
+  constexpr int RING = (NS + NSG + (RES ? NS : 0)) * LROW;
+  __shared__ __attribute__((aligned(16))) char sm[4 * RING + 4 * RCOLS * SLICE];
   const int ncg = (a.W + RCOLS - 1) / RCOLS;
   const RowMap mp = row_map(a.N, ncg, a.ngroups, a.nbands, a.xcd != 0);
   if (!mp.live) return;
@@ -545,11 +560,11 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const int r0 = mp.band * a.bandH, r1 = min(a.H, r0 + a.bandH);
   const int hx = r1, hg = min(a.H, r1 + 1);
   const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
-  char* ring = sm[threadIdx.x >> 6];
+  char* ring = sm + (threadIdx.x >> 6) * RING;
   char* rx = ring;                  // X rows, slot r % NS
   char* rg = ring + NS * LROW;      // dY rows, slot r % NSG
   char* rres = rg + NSG * LROW;     // dRes rows (RES), slot r % NS
-  char* stg = so[threadIdx.x >> 6];
+  char* stg = sm + 4 * RING + (threadIdx.x >> 6) * (RCOLS * SLICE);
   const int c0 = mp.grp * CPG;
   const int c = c0 + cl * EPT;
   const bool cok = c < a.C;
@@ -863,15 +878,15 @@ int dw_bwd_xcd() {
   return e && e[0] == '0' ? 0 : 1;
 }
 
-// Ring reads by inline asm (no vmcnt(0) drain ahead of them) for frames below 32 rows, plain reads
-// above: at the step's shapes the asm form measured 118.4 -> 111.0 us at 19^2 x 736 but 398 -> 408 at
-// 37^2, 536 -> 544 at 74^2 and 1,034 -> 1,110 at 147^2 (tools/dw_ab.py, profiles/r04_dw_asm_ab.txt):
-// with long walks the drain costs less than the per-read lgkmcnt(0) fences that replace it.
-// XCP_DW_BWD_ASM=0 / 1 forces the plain / asm form for every frame (read per call).
-bool dw_bwd_asm_reads(int H) {
+// Ring reads: plain C++ reads by default.  Round 4 measured inline-asm reads faster below 32 rows
+// (118.4 -> 111.0 us at 19^2 x 736, profiles/r04_dw_asm_ab.txt) because hipcc drained vmcnt(0) ahead
+// of the first plain ring read of every step; with the rings and the staging in one LDS object (round
+// 5) that drain is gone and the plain form (offsets folded into the reads, no per-window fences) is as
+// fast or faster at every step shape (19^2: 103.6 / 102.6 us plain / asm, 10^2: 90.9 / 96.7;
+// profiles/r05_dw_bwd_onelds_ab.txt).  XCP_DW_BWD_ASM=1 forces the asm form (read per call).
+bool dw_bwd_asm_reads(int) {
   const char* e = getenv("XCP_DW_BWD_ASM");
-  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
-  return H < 32;
+  return e && e[0] == '1';
 }
 
 template <typename T, int ACT>

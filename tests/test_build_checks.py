@@ -78,3 +78,65 @@ def test_sep_fwd_asm_loads_untouched_until_their_wait(tmp_path):
                     todo.append(labels[t.split()[1]])
                 k += 1
     assert loads >= 6 * 2, loads
+
+
+def _compiler_vmcnt0_in_loops(lines, name_filter):
+    """{kernel: [(line, instruction after the wait)]}: compiler-inserted (not inline asm) s_waitcnt with
+    vmcnt(0) inside a loop (between a label and a backward branch to it) of each matching kernel."""
+    import re
+    out = {}
+    k = 0
+    while k < len(lines):
+        m = re.match(r"^(_Z\S+):", lines[k])
+        if not m:
+            k += 1
+            continue
+        j = k
+        while j < len(lines) and not lines[j].startswith(".Lfunc_end"):
+            j += 1
+        body = lines[k:j]
+        if name_filter(m.group(1)):
+            labels = {x.split(":")[0]: i for i, x in enumerate(body) if re.match(r"^\.LBB\S+:", x)}
+            loops = []
+            for i, x in enumerate(body):
+                b = re.match(r"\s*s_(?:c)?branch\w*\s+(\.LBB\S+)", x)
+                if b and b.group(1) in labels and labels[b.group(1)] < i:
+                    loops.append((labels[b.group(1)], i))
+            bad = [(i, body[i + 1].strip()) for i, x in enumerate(body)
+                   if "s_waitcnt" in x and "vmcnt(0)" in x and "ASMSTART" not in body[i - 1]
+                   and any(a <= i <= e for a, e in loops)]
+            out[m.group(1)] = bad
+        k = max(j, k + 1)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc") and not shutil.which("hipcc"), reason="hipcc absent")
+def test_dma_pipelines_not_drained_by_compiler_waits(tmp_path):
+    """The LDS-DMA pipelined kernels keep their look-ahead loads in flight: no compiler-inserted
+    vmcnt(0) inside their loops (hipcc adds one ahead of an LDS access it cannot prove disjoint from an
+    in-flight DMA -- a ds_read_tr builtin, an access after a second __shared__ object gave the accesses
+    alias scopes, a compiler-visible global load in the prologue -- and it drains the look-ahead every
+    iteration).  GEMMs (NT / TN 256x256), stem conv2 forward / dgrad / weight gradient, the depthwise
+    backward's occupancy-4 forms (plain and asm ring reads, with and without the residual)."""
+    import re
+    hipcc = "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else shutil.which("hipcc")
+    csrc = os.path.join(REPO, "multimodal-deepfake-detection_amd", "xcp", "csrc")
+    checks = {
+        "gemm.hip": lambda n: re.search(r"gemm_(nt256p|nt256k64|tn256)_kernel", n),
+        "conv3.hip": lambda n: "conv3x3" in n,
+        # dw_bwd_lds_kernel<T, ACT, RES, ROLL=false, BD=1, MINW, SKIP=false, BNRES=false, ASMRD>
+        "dwconv.hip": lambda n: re.search(r"dw_bwd_lds_kernelI(DF16b|f)Li\dELb[01]ELb0ELi1ELi[34]ELb0ELb0ELb[01]E", n),
+    }
+    procs = {}
+    for f in checks:
+        out = tmp_path / (f + ".s")
+        procs[f] = (out, subprocess.Popen([hipcc, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
+                                           "-S", os.path.join(csrc, f), "-o", str(out)],
+                                          stdout=subprocess.PIPE, stderr=subprocess.PIPE))
+    for f, (out, p) in procs.items():
+        _, err = p.communicate()
+        assert p.returncode == 0, err.decode()[-2000:]
+        found = _compiler_vmcnt0_in_loops(out.read_text().splitlines(), checks[f])
+        assert found, f"{f}: no kernel matched"
+        bad = {k: v for k, v in found.items() if v}
+        assert not bad, f"{f}: {bad}"

@@ -394,8 +394,8 @@ def test_dw_bwd_row_bands(ops, gpu, monkeypatch, bands, N, C, H, act, res, skip)
 @pytest.mark.parametrize("N,C,H,act,res", [(64, 736, 19, 2, False), (16, 256, 37, 2, False), (4, 128, 74, 1, False),
                                            (32, 1536, 10, 0, False), (64, 736, 19, 1, True)])
 def test_dw_bwd_ring_read_forms(ops, gpu, monkeypatch, N, C, H, act, res):
-    """Ring reads by inline asm (XCP_DW_BWD_ASM=1) or plain C++ reads (=0), whichever the frame
-    height selects by default: the same arithmetic on the same values, every output bitwise equal."""
+    """Ring reads by inline asm (XCP_DW_BWD_ASM=1) or plain C++ reads (the default): the same
+    arithmetic on the same values, every output bitwise equal."""
     W = H
     g = torch.Generator(device=gpu).manual_seed(3 * N + C + H)
     dt = torch.bfloat16

@@ -1,6 +1,8 @@
 """A/B of the depthwise backward against the committed version (git HEAD's csrc/dwconv.hip, built
-into tools/exp/libdw_base.so): both libraries' xcp_dw_bwd on identical inputs at the step's shapes,
-interleaved rounds, median launch time; outputs compared (max |diff| of dX, dW partials, BN sums).
+into probe/libdw_base.so, a path the GPU upload carries -- delete it afterwards): both libraries'
+xcp_dw_bwd on identical inputs at the step's shapes, interleaved rounds, median launch time; the new
+library also with the ring reads forced plain (XCP_DW_BWD_ASM=0) and asm (=1); outputs compared against
+the base (max |diff| of dX, dW partials, BN sums).
 
   python tools/dw_ab.py build [rev]   # here (rev: git revision of the baseline, default HEAD)
   python tools/dw_ab.py run           # GPU box
@@ -14,7 +16,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(REPO, "multimodal-deepfake-detection_amd", "xcp", "csrc")
-OUT = os.path.join(HERE, "exp")
+OUT = os.path.join(REPO, "probe")
 BASE = os.path.join(OUT, "libdw_base.so")
 
 
@@ -51,6 +53,8 @@ def run():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     st = torch.cuda.current_stream().cuda_stream
+    variants = {"base": (libs["base"], None), "new": (libs["new"], None), "plain": (libs["new"], "0"),
+                "asm": (libs["new"], "1")}
     shapes = [(256, 19, 19, 736, 2, False), (256, 19, 19, 736, 1, True), (256, 37, 37, 736, 2, False),
               (256, 74, 74, 256, 2, False), (256, 147, 147, 128, 2, False), (256, 10, 10, 1536, 2, False)]
     for N, H, W, C, act, res in shapes:
@@ -64,20 +68,25 @@ def run():
         mu, isd = torch.randn(C, device=dev, generator=g), torch.rand(C, device=dev, generator=g) + 0.5
         P = libs["new"].xcp_dw_bwd_chunks(N, H, W, C)
         outs = {}
-        for k in libs:
+        for k in variants:
             outs[k] = (torch.empty(M * C, device=dev, dtype=torch.bfloat16), torch.empty(P * C * 9, device=dev),
                        torch.empty(P * 2 * C, device=dev) if act == 2 else None)
         p = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else 0)   # noqa: E731
 
         def call(k):
             dX, dWp, bnp = outs[k]
-            rc = libs[k].xcp_dw_bwd(1, act, p(dY), p(X), p(Wt), p(sc), p(sh), p(dR), None, 0, 0, 1, 0, p(dX), p(dWp),
+            lib, env = variants[k]
+            if env is None:
+                os.environ.pop("XCP_DW_BWD_ASM", None)
+            else:
+                os.environ["XCP_DW_BWD_ASM"] = env
+            rc = lib.xcp_dw_bwd(1, act, p(dY), p(X), p(Wt), p(sc), p(sh), p(dR), None, 0, 0, 1, 0, p(dX), p(dWp),
                                     p(bnp), p(mu) if act == 2 else None, p(isd) if act == 2 else None, N, H, W, C, st)
             assert rc == 0, rc
 
-        times = {k: [] for k in libs}
+        times = {k: [] for k in variants}
         for _ in range(5):
-            for k in libs:
+            for k in variants:
                 for _w in range(2):
                     call(k)
                 torch.cuda.synchronize()
@@ -89,7 +98,8 @@ def run():
                 torch.cuda.synchronize()
                 times[k].append(s.elapsed_time(e) / 10 * 1e3)
         byts = 2 * M * C * (3 + (1 if res else 0))
-        d = [(outs["base"][i].float() - outs["new"][i].float()).abs().max().item() for i in range(3) if outs["base"][i] is not None]
+        d = [(outs["base"][i].float() - outs[k][i].float()).abs().max().item() for k in variants if k != "base"
+             for i in range(3) if outs["base"][i] is not None]
         line = "  ".join(f"{k} {statistics.median(v):7.1f} us ({byts / statistics.median(v) / 1e3:6.0f} GB/s)" for k, v in times.items())
         print(f"{N}x{H}x{W}x{C} act={act} res={int(res)}: {line}   max|diff| {['%.2e' % x for x in d]}", flush=True)
 
