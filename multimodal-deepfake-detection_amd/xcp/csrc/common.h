@@ -16,6 +16,8 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 enum XcpDtype { XCP_F32 = 0, XCP_BF16 = 1 };
 
@@ -132,6 +134,13 @@ XCP_DEV bf16x4 ds_read_tr(const char* p) {
   typedef short s4 __attribute__((ext_vector_type(4)));
   s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p));
   return __builtin_bit_cast(bf16x4, v);
+}
+
+// two floats -> packed bf16 pair (a in the low half), one v_cvt_pk_bf16_f32 (round to nearest even, the
+// same result as two scalar conversions; assigning the elements of a bf16 vector one at a time made
+// hipcc convert each against a zero and merge the halves: 2-3 extra VALU per pair)
+XCP_DEV unsigned pk_bf16(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
 
 static inline int xcp_cdiv(long a, long b) { return (int)((a + b - 1) / b); }

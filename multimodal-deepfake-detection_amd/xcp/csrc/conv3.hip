@@ -96,11 +96,7 @@ XCP_DEV c3u4 c3_act(c3u4 v, const float* sc, const float* sh, int c8) {
   for (int e = 0; e < 4; ++e) {
     const float lo = fmaxf(fmaf(__uint_as_float(v[e] << 16), sc[c8 + 2 * e], sh[c8 + 2 * e]), 0.f);
     const float hi = fmaxf(fmaf(__uint_as_float(v[e] & 0xffff0000u), sc[c8 + 2 * e + 1], sh[c8 + 2 * e + 1]), 0.f);
-    bf16x4 b;
-    b[0] = (bf16)lo;
-    b[1] = (bf16)hi;
-    const u16x4 r = __builtin_bit_cast(u16x4, b);
-    v[e] = (unsigned)r[0] | ((unsigned)r[1] << 16);
+    v[e] = pk_bf16(lo, hi);
   }
   return v;
 }
@@ -297,10 +293,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void conv3x3_kernel(const bf16* __
       uint2 pc[2];
 #pragma unroll
       for (int cg = 0; cg < CG; ++cg) {
-        bf16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = (bf16)acc[cg][i];
-        pc[cg] = __builtin_bit_cast(uint2, v);
+        pc[cg] = make_uint2(pk_bf16(acc[cg][0], acc[cg][1]), pk_bf16(acc[cg][2], acc[cg][3]));
+        const bf16x4 v = __builtin_bit_cast(bf16x4, pc[cg]);
         if (STATS && ok) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {

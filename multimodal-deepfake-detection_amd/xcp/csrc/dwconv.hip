@@ -59,13 +59,7 @@ XCP_DEV void unpack(unsigned u, float* v, bf16*) {
   v[1] = __uint_as_float(u & 0xffff0000u);
 }
 XCP_DEV void unpack(unsigned u, float* v, float*) { v[0] = __uint_as_float(u); }
-XCP_DEV unsigned pack(const float* v, bf16*) {
-  bf16x4 q;  // hardware RNE conversion (v_cvt_pk_bf16_f32)
-  q[0] = (bf16)v[0];
-  q[1] = (bf16)v[1];
-  const u16x4 r = __builtin_bit_cast(u16x4, q);
-  return (unsigned)r[0] | ((unsigned)r[1] << 16);
-}
+XCP_DEV unsigned pack(const float* v, bf16*) { return pk_bf16(v[0], v[1]); }   // hardware RNE conversion
 XCP_DEV unsigned pack(const float* v, float*) { return __float_as_uint(v[0]); }
 
 template <int ACT>
@@ -79,6 +73,11 @@ XCP_DEV float act1(float x, float s, float t) {
 // ([HP*WP][SLICE bytes]); with TRANSFORM the activation is applied.  All global
 // loads of a thread are issued before any is consumed (unconditional loads from a
 // clamped address, zero-selected afterwards).
+typedef int dwi2 __attribute__((ext_vector_type(2)));
+constexpr unsigned DW_BUF_OOB = 0x80000000u;     // >= num_records: the access is dropped, a load returns zeros
+constexpr int DW_BUF_RECORDS = 0x7fffffff;
+constexpr int DW_BUF_DWORD3 = 0x00020000;        // gfx9 raw buffer descriptor word 3
+
 template <typename T, int ACT, bool TRANSFORM, int MAXPX, int FS = SLICE>
 XCP_DEV void stage(const T* __restrict__ src, char* dst, const TileGeo& g, long nbase, int th0, int tw0, int H, int W,
                    int C, int c0, const float* scale, const float* shift) {
@@ -94,25 +93,43 @@ XCP_DEV void stage(const T* __restrict__ src, char* dst, const TileGeo& g, long 
     VecIO<float, EPC>::load(scale + cq, sc);
     VecIO<float, EPC>::load(shift + cq, sh);
   }
+  // Chunk k of this thread is tile pixel p = tid / CPP + k * (256 / CPP), channel chunk tid % CPP: its
+  // (row, column) in the padded tile and its byte offset in the frame advance incrementally (a runtime
+  // division and a 64-bit address product per chunk were most of this loop's VALU cycles), and the loads
+  // go through a buffer resource on the frame, 32-bit offsets (frames are far below 2 GB).
+  constexpr int PSTEP = 256 / CPP;
+  const int q = threadIdx.x % CPP, c = c0 + q * EPC;
+  const int p0 = threadIdx.x / CPP;
+  int hy = p0 / g.WP, hx = p0 - hy * g.WP;
+  const int dhy = PSTEP / g.WP, dhx = PSTEP - dhy * g.WP;
+  const int rowb = W * C * (int)sizeof(T), pixb = C * (int)sizeof(T);
+  int boff = (th0 - 1 + hy) * rowb + (tw0 - 1 + hx) * pixb + c * (int)sizeof(T);
+  const int stepb = dhy * rowb + dhx * pixb, wrapb = rowb - g.WP * pixb;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(src + nbase * C), (short)0, DW_BUF_RECORDS, DW_BUF_DWORD3);
   uint4 v[MAXIT];
   bool ok[MAXIT];
 #pragma unroll
   for (int k = 0; k < MAXIT; ++k) {
     const int i = threadIdx.x + 256 * k;
-    const int p = i / CPP, q = i - p * CPP;
-    const int hy = p / g.WP, hx = p - hy * g.WP;
     const int h = th0 - 1 + hy, w = tw0 - 1 + hx;
-    const int c = c0 + q * EPC;
     ok[k] = i < total && h >= 0 && h < H && w >= 0 && w < W && c < C;
-    const T* ptr = ok[k] ? src + (nbase + (long)h * W + w) * C + c : src;
-    v[k] = *reinterpret_cast<const uint4*>(ptr);
+    v[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok[k] ? boff : (int)DW_BUF_OOB, 0, 0));
+    hx += dhx;
+    hy += dhy;
+    boff += stepb;
+    if (hx >= g.WP) {
+      hx -= g.WP;
+      ++hy;
+      boff += wrapb;
+    }
   }
 #pragma unroll
   for (int k = 0; k < MAXIT; ++k) {
     const int i = threadIdx.x + 256 * k;
     if (i >= total) break;
-    const int p = i / CPP, q = i - p * CPP;
-    uint4 u = ok[k] ? v[k] : make_uint4(0, 0, 0, 0);
+    const int p = i / CPP;
+    uint4 u = v[k];   // (zero where !ok: the out-of-range load returns zeros)
     if constexpr (TRANSFORM && ACT != ACT_NONE) {
       if (ok[k]) {
         float f[EPC];
@@ -181,38 +198,50 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwArgs a) {
                              a.shift);
   __syncthreads();
   if (c >= a.C) return;
+  // stores and item walk as dw_fwd_w2_kernel (buffer resource on the frame, dropped out-of-range stores)
   T* Y = reinterpret_cast<T*>(a.Y);
+  const __amdgpu_buffer_rsrc_t rY =
+      __builtin_amdgcn_make_buffer_rsrc(Y + nbase * a.C, (short)0, DW_BUF_RECORDS, DW_BUF_DWORD3);
   const int items = g.TH * g.nseg;
   const char* lbase = sA + cl * 4;
+  const int xlim = min(g.TW, a.W - tw0);
+  const int nseg = g.nseg, dr = NWK / nseg, ds = NWK - dr * nseg;
+  int r = wk / nseg, sg = wk - r * nseg;
   for (int it = wk; it < items; it += NWK) {
-    const int r = it / g.nseg, sg = it - r * g.nseg;
     const int oh = th0 + r;
     const int x0 = sg * SEGL;
-    if (oh >= a.H) continue;
-    const char* base = lbase + (r * g.WP + x0) * FS;
-    float win[3][SEGL + 2][EPT];
+    if (oh < a.H) {
+      const char* base = lbase + (r * g.WP + x0) * FS;
+      float win[3][SEGL + 2][EPT];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+      for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int k = 0; k < SEGL + 2; ++k)
-        unpack(*reinterpret_cast<const unsigned*>(base + (ky * g.WP + k) * FS), win[ky][k], (T*)nullptr);
-    T* yrow = Y + (nbase + (long)oh * a.W + tw0) * a.C + c;
+        for (int k = 0; k < SEGL + 2; ++k)
+          unpack(*reinterpret_cast<const unsigned*>(base + (ky * g.WP + k) * FS), win[ky][k], (T*)nullptr);
+      const int off = ((oh * a.W + tw0 + x0) * a.C + c) * (int)sizeof(T);
 #pragma unroll
-    for (int j = 0; j < SEGL; ++j) {
-      float o[EPT];
-      // (one fma chain per channel in (ky, kx) order: the summation order the bf16 parity
-      // tests were pinned with; a per-row split into packed pairs measured only ~3 % faster)
+      for (int j = 0; j < SEGL; ++j) {
+        float o[EPT];
+        // (one fma chain per channel in (ky, kx) order: the summation order the bf16 parity
+        // tests were pinned with; a per-row split into packed pairs measured only ~3 % faster)
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        float s = 0.f;
+        for (int e = 0; e < EPT; ++e) {
+          float s = 0.f;
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+          for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
-        o[e] = s;
+            for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
+          o[e] = s;
+        }
+        __builtin_amdgcn_raw_buffer_store_b32((int)pack(o, (T*)nullptr), rY,
+                                              x0 + j < xlim ? off + j * a.C * (int)sizeof(T) : (int)DW_BUF_OOB, 0, 0);
       }
-      const int x = x0 + j;
-      if (x < g.TW && tw0 + x < a.W) *reinterpret_cast<unsigned*>(yrow + (long)x * a.C) = pack(o, (T*)nullptr);
+    }
+    sg += ds;
+    r += dr;
+    if (sg >= nseg) {
+      sg -= nseg;
+      ++r;
     }
   }
 }
@@ -240,40 +269,55 @@ __global__ __launch_bounds__(256) void dw_fwd_w2_kernel(DwArgs a) {
                                     a.shift);
   __syncthreads();
   if (c >= a.C) return;
+  // Y through a buffer resource on the frame: 32-bit byte offsets (a frame is far below 2 GB), and the
+  // pixels past the tile or the image get an out-of-range offset, so the store is dropped instead of
+  // branched around; the item walk advances (row, segment) incrementally.  (The 64-bit per-pixel
+  // address products and the per-item division were a fifth of the loop's VALU cycles.)
   bf16* Y = reinterpret_cast<bf16*>(a.Y);
+  const __amdgpu_buffer_rsrc_t rY =
+      __builtin_amdgcn_make_buffer_rsrc(Y + nbase * a.C, (short)0, DW_BUF_RECORDS, DW_BUF_DWORD3);
   const int items = g.TH * g.nseg;
   const char* lbase = sA + cl * 8;
+  const int xlim = min(g.TW, a.W - tw0);                 // tile columns inside the image
+  const int nseg = g.nseg, dr = NWK / nseg, ds = NWK - dr * nseg;
+  int r = wk / nseg, sg = wk - r * nseg;
   for (int it = wk; it < items; it += NWK) {
-    const int r = it / g.nseg, sg = it - r * g.nseg;
     const int oh = th0 + r;
     const int x0 = sg * SG;
-    if (oh >= a.H) continue;
-    const char* base = lbase + (r * g.WP + x0) * FS;
-    float win[3][SG + 2][CPL];
+    if (oh < a.H) {
+      const char* base = lbase + (r * g.WP + x0) * FS;
+      float win[3][SG + 2][CPL];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+      for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-      for (int k = 0; k < SG + 2; ++k) {
-        const uint2 u = *reinterpret_cast<const uint2*>(base + (ky * g.WP + k) * FS);
-        unpack(u.x, win[ky][k], (bf16*)nullptr);
-        unpack(u.y, win[ky][k] + 2, (bf16*)nullptr);
+        for (int k = 0; k < SG + 2; ++k) {
+          const uint2 u = *reinterpret_cast<const uint2*>(base + (ky * g.WP + k) * FS);
+          unpack(u.x, win[ky][k], (bf16*)nullptr);
+          unpack(u.y, win[ky][k] + 2, (bf16*)nullptr);
+        }
+      const int off = ((oh * a.W + tw0 + x0) * a.C + c) * 2;
+#pragma unroll
+      for (int j = 0; j < SG; ++j) {
+        float o[CPL];
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
+          float s = 0.f;
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
+          o[e] = s;
+        }
+        const uint2 v = make_uint2(pack(o, (bf16*)nullptr), pack(o + 2, (bf16*)nullptr));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(dwi2, v), rY,
+                                              x0 + j < xlim ? off + j * a.C * 2 : (int)DW_BUF_OOB, 0, 0);
       }
-    bf16* yrow = Y + (nbase + (long)oh * a.W + tw0) * a.C + c;
-#pragma unroll
-    for (int j = 0; j < SG; ++j) {
-      float o[CPL];
-#pragma unroll
-      for (int e = 0; e < CPL; ++e) {
-        float s = 0.f;
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) s = fmaf(win[ky][j + kx][e], wt[ky * 3 + kx][e], s);
-        o[e] = s;
-      }
-      const int x = x0 + j;
-      if (x < g.TW && tw0 + x < a.W)
-        *reinterpret_cast<uint2*>(yrow + (long)x * a.C) = make_uint2(pack(o, (bf16*)nullptr), pack(o + 2, (bf16*)nullptr));
+    }
+    sg += ds;
+    r += dr;
+    if (sg >= nseg) {
+      sg -= nseg;
+      ++r;
     }
   }
 }
@@ -363,13 +407,7 @@ template <> struct RV<bf16> {
   typedef rf2 V;
   static constexpr int EPT = 2;
   static XCP_DEV V unpack(unsigned u) { return V{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)}; }
-  static XCP_DEV unsigned pack(V v) {
-    bf16x4 q;
-    q[0] = (bf16)v[0];
-    q[1] = (bf16)v[1];
-    const u16x4 r = __builtin_bit_cast(u16x4, q);
-    return (unsigned)r[0] | ((unsigned)r[1] << 16);
-  }
+  static XCP_DEV unsigned pack(V v) { return pk_bf16(v[0], v[1]); }
   static XCP_DEV V load(const float* p) { return V{p[0], p[1]}; }
   static XCP_DEV float get(V v, int e) { return v[e]; }
 };
@@ -935,6 +973,8 @@ int xcp_dw_fwd(int dtype, int act, const void* X, void* Y, const float* Wt, cons
     if (rc != XCP_EUNSUPPORTED) return rc;
   }
   if (dtype != XCP_BF16 && dtype != XCP_F32) return XCP_EUNSUPPORTED;
+  // the staging and the stores address one frame by 32-bit byte offsets
+  if ((long)H * W * C * (dtype == XCP_BF16 ? 2 : 4) >= 0x7fffffffL) return XCP_EUNSUPPORTED;
   if (fwd_slice_bytes(C, dtype == XCP_BF16 ? 2 : 4, H, W) == 128) {
     DwArgs a{X, Y, Wt, scale, shift, N, H, W, C, ngroups_for(C, dtype, 128), tile_geo(H, W, FWD_MAXPX128)};
     if (dtype == XCP_BF16) return launch_fwd<bf16, FWD_MAXPX128, 128>(act, a, stream);

@@ -351,10 +351,8 @@ XCP_DEV void epilogue256_regs(f32x4 (&acc)[8][4], const NTArgs& a, int m0, int n
     uint2 pc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      bf16x4 q;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) q[r] = (bf16)acc[i][j][r];
-      pc[j] = __builtin_bit_cast(uint2, q);
+      pc[j] = make_uint2(pk_bf16(acc[i][j][0], acc[i][j][1]), pk_bf16(acc[i][j][2], acc[i][j][3]));
+      const bf16x4 q = __builtin_bit_cast(bf16x4, pc[j]);
       if (mok) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -628,9 +626,8 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     const bool mok = m < a.M;
     uint2 pc[4];
     static_for<0, 4>([&](auto j) {
-      bf16x4 q;
-      static_for<0, 4>([&](auto r) { q[(int)r] = (bf16)acc(i, j, r); });
-      pc[j] = __builtin_bit_cast(uint2, q);
+      pc[j] = make_uint2(pk_bf16(acc(i, j, 0), acc(i, j, 1)), pk_bf16(acc(i, j, 2), acc(i, j, 3)));
+      const bf16x4 q = __builtin_bit_cast(bf16x4, pc[j]);
       if constexpr (STATS) {   // (branch-free: rows past M add zero)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

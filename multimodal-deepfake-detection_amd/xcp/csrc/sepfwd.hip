@@ -96,13 +96,7 @@ XCP_DEV void sp_barrier() {   // LDS-only workgroup barrier (no vmcnt wait)
 
 XCP_DEV float sp_lo(unsigned u) { return __uint_as_float(u << 16); }
 XCP_DEV float sp_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
-XCP_DEV unsigned sp_pack(float a, float b) {
-  bf16x4 q;
-  q[0] = (bf16)a;
-  q[1] = (bf16)b;
-  const u16x4 r = __builtin_bit_cast(u16x4, q);
-  return (unsigned)r[0] | ((unsigned)r[1] << 16);
-}
+XCP_DEV unsigned sp_pack(float a, float b) { return pk_bf16(a, b); }
 
 // COUT: 128 (block1) or 256 (block2's first unit, whose 74-pixel rows are one half: NHALF = 1)
 template <int ACT, int CIN, int COUT, int NHALF>

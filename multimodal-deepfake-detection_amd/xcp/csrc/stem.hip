@@ -165,12 +165,7 @@ XCP_DEV inline void store_as(int dtype, void* out, long o, float v) {
 // per-element conversion as store_as
 XCP_DEV inline void store4_as(int dtype, void* out, long o, float4 v) {
   if (dtype == XCP_BF16) {
-    bf16x4 q;
-    q[0] = (bf16)v.x;
-    q[1] = (bf16)v.y;
-    q[2] = (bf16)v.z;
-    q[3] = (bf16)v.w;
-    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(out) + o) = q;
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + o) = make_uint2(pk_bf16(v.x, v.y), pk_bf16(v.z, v.w));
   } else {
     *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) = v;
   }
