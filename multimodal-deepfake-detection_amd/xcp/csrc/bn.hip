@@ -237,13 +237,17 @@ __global__ __launch_bounds__(256) void chanred_kernel(ChanRed r, const void* Av,
     constexpr int CR_U = 8;
     constexpr int NB = MODE == 0 ? 1 : 2;
     typedef typename RawVec<T, CPT>::type RV;
+    // (32-bit element offsets: the launcher checks rows * C < 2^31; a 64-bit product per load was three
+    // quarter-rate multiplies)
+    const unsigned last = (unsigned)(re - 1) * (unsigned)r.C + (unsigned)c0, ustep = (unsigned)r.SPB * (unsigned)r.C;
     for (long p0 = rb + slot; p0 < re; p0 += (long)CR_U * r.SPB) {
       RV raw[NB][CR_U];
+      const unsigned o0 = (unsigned)p0 * (unsigned)r.C + (unsigned)c0;
 #pragma unroll
       for (int u = 0; u < CR_U; ++u) {
-        const long p = min(p0 + (long)u * r.SPB, re - 1);
-        raw[0][u] = *reinterpret_cast<const RV*>(A + p * r.C + c0);
-        if constexpr (MODE >= 1) raw[NB - 1][u] = *reinterpret_cast<const RV*>(B + p * r.C + c0);
+        const unsigned o = min(o0 + (unsigned)u * ustep, last);
+        raw[0][u] = *reinterpret_cast<const RV*>(A + o);
+        if constexpr (MODE >= 1) raw[NB - 1][u] = *reinterpret_cast<const RV*>(B + o);
       }
       __builtin_amdgcn_sched_barrier(0);   // (the scheduler would sink each load to its use)
 #pragma unroll
@@ -333,14 +337,17 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, in
   // added (clamped row, zero-selected past R), so a lane waits ceil(R / (16 FIN_U)) memory round
   // trips, not one per 4 rows (723 partial rows of the middle flow: one; the same summation order
   // as smaller chunks, so the same bits)
+  // (the row offsets are wave-uniform, so they are formed on the scalar unit: the 64-bit product per
+  // load in vector registers was three quarter-rate multiplies, 144 in the loop)
   constexpr int FIN_U = 48;
   double a = 0.0;
   if (c < C) {
     const float* col = part + (long)stat * CP + c;
-    for (int r0 = w; r0 < R; r0 += FIN_U * FIN_WAVES) {
+    const int ws = __builtin_amdgcn_readfirstlane(w);
+    for (int r0 = ws; r0 < R; r0 += FIN_U * FIN_WAVES) {
       float v[FIN_U];
 #pragma unroll
-      for (int u = 0; u < FIN_U; ++u) v[u] = col[(long)min(r0 + u * FIN_WAVES, R - 1) * 2 * CP];
+      for (int u = 0; u < FIN_U; ++u) v[u] = col[min(r0 + u * FIN_WAVES, R - 1) * 2 * CP];
 #pragma unroll
       for (int u = 0; u < FIN_U; ++u) a += r0 + u * FIN_WAVES < R ? (double)v[u] : 0.0;
     }
@@ -471,18 +478,20 @@ template <typename T, int CPT, bool MASK, int RPT>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ dZ, const T* __restrict__ Yv, T* dY,
                                                            const float* alpha, const float* bcoef, const float* delta,
                                                            const float* ms, const float* mt, long rows, int C) {
-  const int CV = C / CPT;
-  const long rq = (rows + RPT - 1) / RPT;
-  const long g = (long)blockIdx.x * 256 + threadIdx.x;
+  // 32-bit index arithmetic (the launcher checks rows * C < 2^31): a 64-bit division and 64-bit
+  // address products per thread were most of its VALU
+  const unsigned CV = (unsigned)C / CPT;
+  const unsigned rq = (unsigned)((rows + RPT - 1) / RPT), nrows = (unsigned)rows;
+  const unsigned g = blockIdx.x * 256u + threadIdx.x;
   if (g >= rq * CV) return;
-  const int c0 = (int)(g % CV) * CPT;
-  const long p0 = g / CV;
+  const unsigned p0 = g / CV, c0 = (g - p0 * CV) * CPT;
+  const unsigned o0 = p0 * (unsigned)C + c0, ostep = rq * (unsigned)C, olast = (nrows - 1) * (unsigned)C + c0;
   float dz[RPT][CPT], y[RPT][CPT], al[CPT], bc[CPT], de[CPT];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
-    const long p = min(p0 + k * rq, rows - 1);
-    VecIO<T, CPT>::load(dZ + p * C + c0, dz[k]);
-    VecIO<T, CPT>::load(Yv + p * C + c0, y[k]);
+    const unsigned o = min(o0 + k * ostep, olast);
+    VecIO<T, CPT>::load(dZ + o, dz[k]);
+    VecIO<T, CPT>::load(Yv + o, y[k]);
   }
   VecIO<float, CPT>::load(alpha + c0, al);
   VecIO<float, CPT>::load(bcoef + c0, bc);
@@ -500,8 +509,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   for (int k = 0; k < RPT; ++k) {
 #pragma unroll
     for (int j = 0; j < CPT; ++j) dz[k][j] = fmaf(al[j], dz[k][j], fmaf(bc[j], y[k][j], de[j]));
-    const long p = p0 + k * rq;
-    if (p < rows) VecIO<T, CPT>::store(dY + p * C + c0, dz[k]);
+    if (p0 + k * rq < nrows) VecIO<T, CPT>::store(dY + o0 + k * ostep, dz[k]);
   }
 }
 
@@ -527,15 +535,13 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const T* __restrict__ Y, 
                                                        const T* __restrict__ S, const float* s2, const float* t2,
                                                        T* __restrict__ Out, unsigned char* __restrict__ amax, int N, int H,
                                                        int W, int C, int OH, int OW) {
-  const int CV = C / CPT;
-  const long g = (long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (long)N * OH * OW * CV) return;
-  const int c0 = (int)(g % CV) * CPT;
-  const long op = g / CV;   // output pixel
-  const int ow = (int)(op % OW);
-  const long t = op / OW;
-  const int oh = (int)(t % OH);
-  const int n = (int)(t / OH);
+  // 32-bit index arithmetic (the launcher checks N * H * W * C < 2^31)
+  const unsigned CV = (unsigned)C / CPT;
+  const unsigned g = blockIdx.x * 256u + threadIdx.x;
+  if (g >= (unsigned)N * OH * OW * CV) return;
+  const unsigned op = g / CV, c0 = (g - op * CV) * CPT;   // output pixel, first channel
+  const unsigned t = op / OW, ow = op - t * OW;
+  const unsigned n = t / OH, oh = t - n * OH;
   float sc[CPT], sh[CPT], o[CPT];
   VecIO<float, CPT>::load(s1 + c0, sc);
   VecIO<float, CPT>::load(t1 + c0, sh);
@@ -545,13 +551,13 @@ __global__ __launch_bounds__(256) void tail_fwd_kernel(const T* __restrict__ Y, 
 #pragma unroll
     for (int j = 0; j < CPT; ++j) { m[j] = -INFINITY; am[j] = 0; }
     for (int ky = 0; ky < 3; ++ky) {
-      const int ih = oh * 2 - 1 + ky;
+      const int ih = (int)oh * 2 - 1 + ky;
       if (ih < 0 || ih >= H) continue;
       for (int kx = 0; kx < 3; ++kx) {
-        const int iw = ow * 2 - 1 + kx;
+        const int iw = (int)ow * 2 - 1 + kx;
         if (iw < 0 || iw >= W) continue;
         float v[CPT];
-        VecIO<T, CPT>::load(Y + (((long)n * H + ih) * W + iw) * C + c0, v);
+        VecIO<T, CPT>::load(Y + ((n * H + ih) * W + iw) * C + c0, v);
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
           const float z = fmaf(v[j], sc[j], sh[j]);
@@ -598,16 +604,15 @@ __global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict
                                                              const T* __restrict__ S, const float* s2, const float* t2,
                                                              T* __restrict__ Out, unsigned char* __restrict__ amax,
                                                              int N, int H, int W, int C, int OH, int OW) {
-  const int CV = C / CPT;
-  const int QH = (OH + 1) / 2, QW = (OW + 1) / 2;
-  const long g = (long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (long)N * QH * QW * CV) return;
-  const int c0 = (int)(g % CV) * CPT;
-  const long q = g / CV;
-  const int qb = (int)(q % QW);
-  const long t = q / QW;
-  const int qa = (int)(t % QH);
-  const int n = (int)(t / QH);
+  // 32-bit index arithmetic (the launcher checks N * H * W * C < 2^31): row and column offsets formed
+  // once each (64-bit products per load were 75 of the thread's quarter-rate multiplies)
+  const unsigned CV = (unsigned)C / CPT;
+  const unsigned QH = (OH + 1) / 2, QW = (OW + 1) / 2;
+  const unsigned g = blockIdx.x * 256u + threadIdx.x;
+  if (g >= (unsigned)N * QH * QW * CV) return;
+  const unsigned q = g / CV, c0 = (g - q * CV) * CPT;
+  const unsigned t = q / QW, qb = q - t * QW;
+  const unsigned n = t / QH, qa = t - n * QH;
   float sc[CPT], sh[CPT];
   VecIO<float, CPT>::load(s1 + c0, sc);
   VecIO<float, CPT>::load(t1 + c0, sh);
@@ -616,11 +621,14 @@ __global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict
   // but without a branch per load all 25 loads (and the 4 skip loads) can be in flight at once
   // (with a branch each, every load was its own round trip).
   const int oh0 = 2 * qa, ow0 = 2 * qb;
+  unsigned colo[5];
+#pragma unroll
+  for (int cc = 0; cc < 5; ++cc) colo[cc] = (unsigned)min(max(4 * (int)qb - 1 + cc, 0), W - 1) * C + c0;
   float sv[4][CPT];
 #pragma unroll
   for (int o = 0; o < 4; ++o) {
     const int oh = min(oh0 + (o >> 1), OH - 1), ow = min(ow0 + (o & 1), OW - 1);
-    VecIO<T, CPT>::load(S + (((long)n * OH + oh) * OW + ow) * C + c0, sv[o]);
+    VecIO<T, CPT>::load(S + ((n * OH + oh) * OW + ow) * C + c0, sv[o]);
   }
   float m[4][CPT];
   unsigned char am[4][CPT];
@@ -633,16 +641,15 @@ __global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict
     }
 #pragma unroll
   for (int r = 0; r < 5; ++r) {
-    const int ihr = 4 * qa - 1 + r;
+    const int ihr = 4 * (int)qa - 1 + r;
     const bool rok = ihr >= 0 && ihr < H;
-    const int ih = min(max(ihr, 0), H - 1);
+    const unsigned rowo = (n * H + (unsigned)min(max(ihr, 0), H - 1)) * W * C;
 #pragma unroll
     for (int cc = 0; cc < 5; ++cc) {
-      const int iwr = 4 * qb - 1 + cc;
+      const int iwr = 4 * (int)qb - 1 + cc;
       const bool ok = rok && iwr >= 0 && iwr < W;
-      const int iw = min(max(iwr, 0), W - 1);
       float v[CPT];
-      VecIO<T, CPT>::load(Y + (((long)n * H + ih) * W + iw) * C + c0, v);
+      VecIO<T, CPT>::load(Y + rowo + colo[cc], v);
 #pragma unroll
       for (int j = 0; j < CPT; ++j) v[j] = ok ? fmaf(v[j], sc[j], sh[j]) : -INFINITY;
 #pragma unroll
@@ -673,7 +680,7 @@ __global__ __launch_bounds__(256) void tail_pool_quad_kernel(const T* __restrict
   for (int o = 0; o < 4; ++o) {
     const int oh = 2 * qa + (o >> 1), ow = 2 * qb + (o & 1);
     if (oh >= OH || ow >= OW) continue;
-    const long op = ((long)n * OH + oh) * OW + ow;
+    const unsigned op = (n * OH + oh) * OW + ow;
     float res[CPT];
 #pragma unroll
     for (int j = 0; j < CPT; ++j) res[j] = m[o][j] + (s2 ? fmaf(sv[o][j], a2[j], b2[j]) : sv[o][j]);
@@ -792,24 +799,44 @@ __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc
     VecIO<float, CPT>::load(invstd + c0, is);
     const T* dOut = reinterpret_cast<const T*>(ps.dOut);
     const long rb = (long)pchunk * r.rows_per_chunk, re = min(r.rows, rb + r.rows_per_chunk);
-    auto coords = [&](long p, unsigned& n, unsigned& a, unsigned& b) {
-      const unsigned q = (unsigned)p;
-      const unsigned t = q / (unsigned)ps.OW;
-      b = q - t * ps.OW;
-      n = t / (unsigned)ps.OH;
-      a = t - n * ps.OH;
+    // Quad coordinates (n, a, b) advance incrementally by SPB quads (one division at the start, not two per
+    // quad), and every offset is a 32-bit element offset formed once per quad: the four input pixels
+    // and the four pooled positions are the quad's base plus uniform strides (the launcher checks that
+    // both tensors have fewer than 2^31 elements).
+    const unsigned OH = ps.OH, OW = ps.OW, H = ps.H, W = ps.W, C = r.C;
+    auto coords = [&](unsigned q, unsigned& n, unsigned& a, unsigned& b) {
+      const unsigned t = q / OW;
+      b = q - t * OW;
+      n = t / OH;
+      a = t - n * OH;
     };
-    auto fetch = [&](long p, Q& in) {
-      unsigned n, a, b;
-      coords(p, n, a, b);
+    const unsigned db = (unsigned)r.SPB % OW, da = (unsigned)r.SPB / OW;
+    auto advance = [&](unsigned& n, unsigned& a, unsigned& b) {
+      b += db;
+      a += da;
+      if (b >= OW) {
+        b -= OW;
+        ++a;
+      }
+      while (a >= OH) {
+        a -= OH;
+        ++n;
+      }
+    };
+    // input pixel (2a + dy, 2b + dx) of the quad, clamped into the image as the forward's window reads
+    auto ybase = [&](unsigned n, unsigned a, unsigned b) { return ((n * H + 2 * a) * W + 2 * b) * C + (unsigned)c0; };
+    auto fetch = [&](unsigned q, unsigned n, unsigned a, unsigned b, Q& in) {
+      const unsigned y0 = ybase(n, a, b);
+      const unsigned sy = 2 * a + 1 < H ? W * C : 0u, sx = 2 * b + 1 < W ? C : 0u;
+      const unsigned d0 = q * C + (unsigned)c0;
+      const bool okx = b + 1 < OW, oky = a + 1 < OH;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const unsigned h = min(2 * a + (k >> 1), (unsigned)ps.H - 1), w = min(2 * b + (k & 1), (unsigned)ps.W - 1);
-        const uint4* src = reinterpret_cast<const uint4*>(Y + ((long)(n * ps.H + h) * ps.W + w) * r.C + c0);
+        const uint4* src = reinterpret_cast<const uint4*>(Y + y0 + (k & 2 ? sy : 0u) + (k & 1 ? sx : 0u));
 #pragma unroll
         for (int i = 0; i < Q::NQ; ++i) in.y[k][i] = src[i];
-        long op;
-        pool_win(ps, n, a, b, r.C, (unsigned)c0, k, op);
+        const bool ok = (k & 1 ? okx : true) && (k & 2 ? oky : true);   // as pool_win
+        const unsigned op = d0 + (ok ? (k & 1 ? C : 0u) + (k & 2 ? OW * C : 0u) : 0u);
         const uint4* dsrc = reinterpret_cast<const uint4*>(dOut + op);
 #pragma unroll
         for (int i = 0; i < Q::NQ; ++i) in.d[k][i] = dsrc[i];
@@ -818,18 +845,23 @@ __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc
     };
     Q cur;
     long p = rb + slot;
-    if (p < re) fetch(p, cur);
+    unsigned n = 0, a = 0, b = 0, nl, al, bl;
+    coords((unsigned)(re - 1), nl, al, bl);   // the clamped look-ahead past the chunk
+    if (p < re) {
+      coords((unsigned)p, n, a, b);
+      fetch((unsigned)p, n, a, b, cur);
+    }
     for (; p < re; p += r.SPB) {
+      unsigned n2 = n, a2 = a, b2 = b;
+      advance(n2, a2, b2);
       Q nxt;
-      fetch(min(p + r.SPB, re - 1), nxt);
-      unsigned n, a, b;
-      coords(p, n, a, b);
+      if (p + r.SPB < re) fetch((unsigned)(p + r.SPB), n2, a2, b2, nxt);
+      else fetch((unsigned)(re - 1), nl, al, bl, nxt);
       float d[4][CPT], y[4][CPT];
       unsigned am[4][2];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        long op;
-        const bool ok = pool_win(ps, n, a, b, r.C, (unsigned)c0, k, op);
+        const bool ok = (k & 1 ? b + 1 < OW : true) && (k & 2 ? a + 1 < OH : true);
         VecIO<T, CPT>::load(reinterpret_cast<const T*>(cur.d[k]), d[k]);
         VecIO<T, CPT>::load(reinterpret_cast<const T*>(cur.y[k]), y[k]);
         am[k][0] = ok ? cur.am[k].x : 0xffffffffu;   // 0xff never matches a tap
@@ -837,11 +869,12 @@ __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc
       }
       float g[4][CPT];
       pool_combine<T, CPT>(d, am, g);
+      const unsigned y0 = ybase(n, a, b);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const unsigned h = 2 * a + (k >> 1), w = 2 * b + (k & 1);
-        if (h >= (unsigned)ps.H || w >= (unsigned)ps.W) continue;
-        VecIO<T, CPT>::store(dZ + ((long)(n * ps.H + h) * ps.W + w) * r.C + c0, g[k]);
+        if (h >= H || w >= W) continue;
+        VecIO<T, CPT>::store(dZ + y0 + (k & 2 ? W * C : 0u) + (k & 1 ? C : 0u), g[k]);
 #pragma unroll
         for (int j = 0; j < CPT; ++j) {
           acc[0][j] += g[k][j];
@@ -849,6 +882,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_red_kernel(ChanRed r, PoolSrc
         }
       }
       cur = nxt;
+      n = n2;
+      a = a2;
+      b = b2;
     }
   }
   chanred_finish<CPT>(r, acc, part, cchunk, pchunk, lcv, slot);
@@ -896,6 +932,7 @@ template <typename T, int MODE>
 int chanred_launch(long rows, int C, const void* A, const void* B, const float* mean, const float* invstd, float* part,
                    hipStream_t st, const float* ms = nullptr, const float* mt = nullptr) {
   constexpr int CPT = 8;
+  if (rows * C >= 0x7fffffffL) return XCP_EUNSUPPORTED;   // 32-bit element offsets in the kernel
   ChanRed r = make_chanred(rows, C, CPT, 1024);
   const long P = chanred_P(r);
   const size_t smem = (size_t)r.SPB * 2 * r.CVB * CPT * sizeof(float);
@@ -1069,6 +1106,7 @@ int xcp_bn_bwd_apply(int dtype, const void* dZ, const void* Y, void* dY, const f
   if (C % 8) return XCP_EINVAL;
   if ((ms == nullptr) != (mt == nullptr)) return XCP_EINVAL;
   if (rows <= 0) return XCP_OK;
+  if (rows * C >= 0x7fffffffL) return XCP_EUNSUPPORTED;   // 32-bit element offsets in the kernel
   // rows per thread: 4 with the mask (5 coefficient vectors), 2 without (3); at 92,416 x 736 bf16
   // 91.5 -> 74 us and 71 -> 71 us against one row per thread (profiles/r02_bnapply_ab.txt)
   const long rq4 = (rows + 3) / 4, rq2 = (rows + 1) / 2;
@@ -1104,6 +1142,7 @@ int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int
   if (C % 8) return XCP_EINVAL;
   const int OH = pool ? (H - 1) / 2 + 1 : H, OW = pool ? (W - 1) / 2 + 1 : W;
   if (pool) {   // one thread per 2 x 2 output quad x 8 channels
+    if ((long)N * H * W * C >= 0x7fffffffL) return XCP_EUNSUPPORTED;   // 32-bit element offsets in the kernel
     const unsigned gq = nblk((long)N * ((OH + 1) / 2) * ((OW + 1) / 2) * (C / 8));
     if (dtype == XCP_BF16)
       hipLaunchKernelGGL((tail_pool_quad_kernel<bf16, 8>), dim3(gq), dim3(256), 0, st, (const bf16*)Y, s1, t1,
@@ -1115,6 +1154,7 @@ int xcp_tail_fwd(int dtype, const void* Y, const float* s1, const float* t1, int
       return XCP_EUNSUPPORTED;
     return (int)hipGetLastError();
   }
+  if ((long)N * H * W * C >= 0x7fffffffL) return XCP_EUNSUPPORTED;   // 32-bit element offsets in the kernel
   const unsigned g = nblk((long)N * OH * OW * (C / 8));
   if (dtype == XCP_BF16)
     hipLaunchKernelGGL((tail_fwd_kernel<bf16, 8>), dim3(g), dim3(256), 0, st, (const bf16*)Y, s1, t1, pool,
@@ -1153,6 +1193,7 @@ int xcp_maxpool_bwd_bnred(int dtype, const void* dOut, const unsigned char* amax
                           const float* mean, const float* invstd, int N, int H, int W, int C, float* part,
                           hipStream_t st) {
   if (C % 8) return XCP_EINVAL;
+  if ((long)N * H * W * C >= 0x7fffffffL) return XCP_EUNSUPPORTED;   // 32-bit element offsets in the kernel
   const PoolSrc ps = pool_src(dOut, amax, H, W);
   const ChanRed r = make_chanred((long)N * ps.OH * ps.OW, C, 8, 1024);
   const long P = chanred_P(r);
