@@ -505,15 +505,20 @@ XCP_DEV RowLanes row_lanes_store(int W, int C, int x0w, int c0, int lane) {
 
 // Stage pixels x0w-1 .. x0w+20 (64-B slice at channel c0) of row h of a frame into
 // dst (LDS, 1408 B) with two LDS-DMA instructions (88 lanes of 16 B).
+// The frame is a buffer resource (SGPRs): the row's offset is scalar, the lane's part fixed, and
+// rows past H / pixels outside the frame get an out-of-range offset (the DMA writes zeros) -- no
+// 64-bit address or select of a zero-line pointer per instruction.
 template <typename T>
-XCP_DEV void stage_row(const T* frame, int h, int H, int W, int C, const RowLanes& rl, char* dst, int lane) {
-  const T* row = frame + (long)h * W * C;
+XCP_DEV void stage_row(__amdgpu_buffer_rsrc_t frame, int h, int H, int W, int C, const RowLanes& rl, char* dst, int lane) {
+  // (rows past H: a base at the out-of-range bound, so every lane's offset is out of range without a
+  // branch on the row)
+  const unsigned rowb = h < H ? (unsigned)(h * W * C * (int)sizeof(T)) : DW_BUF_OOB;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const void* src = (h < H && rl.off[i] >= 0) ? (const void*)(row + rl.off[i]) : (const void*)g_dzero;
+    const int o = rl.off[i] >= 0 ? (int)(rowb + (unsigned)(rl.off[i] * (int)sizeof(T))) : (int)DW_BUF_OOB;
     if (i == 0 || lane < 24)
-      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
-                                       (void __attribute__((address_space(3)))*)(dst + i * 1024), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(frame, (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, o,
+                                               0, 0, 0);
   }
 }
 
@@ -598,11 +603,12 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   const int r0 = mp.band * a.bandH, r1 = min(a.H, r0 + a.bandH);
   const int hx = r1, hg = min(a.H, r1 + 1);
   const int lane = threadIdx.x & 63, cl = lane & 15, sg = lane >> 4;
-  char* ring = sm + (threadIdx.x >> 6) * RING;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // (wave-uniform: the DMA's LDS address is M0)
+  char* ring = sm + wv * RING;
   char* rx = ring;                  // X rows, slot r % NS
   char* rg = ring + NS * LROW;      // dY rows, slot r % NSG
   char* rres = rg + NSG * LROW;     // dRes rows (RES), slot r % NS
-  char* stg = sm + 4 * RING + (threadIdx.x >> 6) * (RCOLS * SLICE);
+  char* stg = sm + 4 * RING + wv * (RCOLS * SLICE);
   const int c0 = mp.grp * CPG;
   const int c = c0 + cl * EPT;
   const bool cok = c < a.C;
@@ -634,9 +640,12 @@ __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
     okm |= (col >= 0 && col < a.W) ? (1u << k) : 0u;
   }
   const long fbase = (long)mp.n * a.H * a.W * a.C;
-  const T* X = reinterpret_cast<const T*>(a.X) + fbase;
-  const T* G = reinterpret_cast<const T*>(a.dY) + fbase;
-  const T* dRes = RES ? reinterpret_cast<const T*>(a.dRes) + fbase : nullptr;
+  auto frame_rsrc = [&](const void* t) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(reinterpret_cast<const T*>(t) + fbase), (short)0,
+                                             DW_BUF_RECORDS, DW_BUF_DWORD3);
+  };
+  const __amdgpu_buffer_rsrc_t X = frame_rsrc(a.X), G = frame_rsrc(a.dY);
+  const __amdgpu_buffer_rsrc_t dRes = frame_rsrc(RES ? a.dRes : a.X);
   const T* dSkip = reinterpret_cast<const T*>(a.dSkip);
   T* dX = reinterpret_cast<T*>(a.dX) + fbase;
   const int lofs = sg * RS * SLICE + cl * 4;
@@ -1009,6 +1018,8 @@ static int dw_bwd_impl(int dtype, int act, const void* dY, const void* X, const 
                        int N, int H, int W, int C, hipStream_t stream) {
   if (C % 8) return XCP_EINVAL;
   if (N <= 0 || H <= 0 || W <= 0) return XCP_OK;
+  // the row walk stages a frame by 32-bit byte offsets
+  if ((long)H * W * C * (dtype == XCP_BF16 ? 2 : 4) >= 0x7fffffffL) return XCP_EUNSUPPORTED;
   if (Yb) {   // sums over the final dX: needs the residual input, no skip input, and the BN's statistics
     if (!dRes || dSkip || !bnpart || !bmean || !binvstd) return XCP_EINVAL;
   } else if (bnpart && (act != ACT_BNRELU || !bmean || !binvstd)) {

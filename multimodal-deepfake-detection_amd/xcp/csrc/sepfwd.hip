@@ -45,17 +45,20 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ __attribute__((aligned(64))) unsigned g_sp_zero[16];   // the source of out-of-frame loads
 
 // prefetch loads by inline asm: hipcc tracks the loads it emits itself and, merging the two register
 // sets' states at the row loop's back edge, waited for both sets at every row (one row of look-ahead
 // instead of two); these it does not see, so the one counted wait per row is the only one, and
 // sp_fence() pins every use of a loaded register after it
-XCP_DEV u32x4 sp_gload(const void* p) {
+// through a buffer resource on the input row (SGPRs) and a 32-bit lane offset: the row's base is
+// scalar work, the lane offsets are fixed per thread, and an out-of-range offset (padding columns,
+// rows outside the frame via num_records 0) loads zeros -- no 64-bit address arithmetic per load
+XCP_DEV u32x4 sp_bload(__amdgpu_buffer_rsrc_t r, int off) {
   u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
   return v;
 }
+
 template <int N>
 XCP_DEV void sp_fence(u32x4 (&v)[N]) {
 #pragma unroll
@@ -154,15 +157,19 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   // input row hh of frame n -> registers (zeros outside the frame and in the padding columns); two
   // register sets, rows two ahead of the one being consumed
   u32x4 rga[KL], rgb[KL];
-  auto load_row = [&](u32x4 (&rg)[KL], int n, int hh) {
+  int loff[KL];   // byte offset of this thread's chunk k within an input row (SP_OOB: padding / past the row)
 #pragma unroll
-    for (int k = 0; k < KL; ++k) {
-      const int c = tid + 512 * k;
-      const int px = c / CH;
-      const bool ok = c < nch && hh >= 0 && hh < H && px >= 1 && px <= W;
-      const void* src = ok ? (const void*)(a.X + ((((long)n * H + hh) * W + px - 1) * CIN + q * 8)) : (const void*)g_sp_zero;
-      rg[k] = sp_gload(src);
-    }
+  for (int k = 0; k < KL; ++k) {
+    const int c = tid + 512 * k;
+    const int px = c / CH;
+    loff[k] = c < nch && px >= 1 && px <= W ? ((px - 1) * CIN + q * 8) * 2 : (int)SP_OOB;
+  }
+  auto load_row = [&](u32x4 (&rg)[KL], int n, int hh) {
+    const bool rok = hh >= 0 && hh < H;   // (uniform)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(a.X + ((long)n * H + (rok ? hh : 0)) * W * CIN), (short)0, rok ? SP_REC : 0, SP_DW3);
+#pragma unroll
+    for (int k = 0; k < KL; ++k) rg[k] = sp_bload(rs, loff[k]);
   };
   // registers -> LDS slot of row hh, activated (the padding stays zero)
   auto store_row = [&](u32x4 (&rg)[KL], int hh) {

@@ -40,6 +40,11 @@ struct UnitBwdArgs {
 // CO: unit output channels; CIW: input channels per workgroup (grid = S splits x CI / CIW
 // channel blocks: the blocks of one split are adjacent ids, so they run together on one XCD
 // and the second reads G / Y from L2); NTH: threads.
+constexpr int UB_DWORD3 = 0x00020000;   // gfx9 raw buffer descriptor word 3
+constexpr int UB_RECORDS = 0x7fffffff;
+constexpr int UB_OOB = (int)0x80000000u;   // >= num_records: loads return zeros, stores are dropped
+typedef int ub_i32x4 __attribute__((ext_vector_type(4)));
+
 template <int CO, int CIW, int NTH>
 __global__ __launch_bounds__(NTH, 512 / NTH) void unit_bwd_kernel(UnitBwdArgs a) {
   constexpr int TM = UB_TM;
@@ -86,20 +91,35 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void unit_bwd_kernel(UnitBwdArgs a)
   VecIO<float, 8>::load(a.delta + gc * 8, de);
   const int xc = tid % XCH, xrow = tid / XCH;   // X rows xrow + (NTH / XCH) i
 
+  // G, Y, X and dD through buffer resources on this split's rows: 32-bit offsets from the split's first
+  // row, the per-thread part fixed, rows past the split out of range (loads return zeros -- stage_tile
+  // masks those rows anyway -- and stores are dropped).  (The 64-bit row products per load and store
+  // were a fifth of the kernel's VALU.)
+  // (num_records is the 2 GB maximum -- the GEMMs measured an exact span slower -- and rows past the
+  // split get the out-of-range offset explicitly)
+  const int nrows = (int)(mend - mbeg);
+  const __amdgpu_buffer_rsrc_t rsG = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.G + mbeg * CO), (short)0,
+                                                                       UB_RECORDS, UB_DWORD3);
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.Y + mbeg * CO), (short)0,
+                                                                       UB_RECORDS, UB_DWORD3);
+  const __amdgpu_buffer_rsrc_t rsX = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.X + mbeg * a.CI), (short)0,
+                                                                       UB_RECORDS, UB_DWORD3);
+  const int goff = (grow * CO + gc * 8) * 2, xoff = (xrow * a.CI + c0 + xc * 8) * 2;
   uint4 rG[GLD], rY[GLD], rX[XLD];
   auto load_tile = [&](long m0) {
+    const int tb = (int)(m0 - mbeg);   // tile's first row within the split
 #pragma unroll
     for (int i = 0; i < GLD; ++i) {
-      const long m = m0 + grow + (NTH / GCH) * i;
-      const long mm = m < mend ? m : mbeg;
-      rG[i] = *reinterpret_cast<const uint4*>(a.G + mm * CO + gc * 8);
-      rY[i] = *reinterpret_cast<const uint4*>(a.Y + mm * CO + gc * 8);
+      const int rw = tb + grow + (NTH / GCH) * i;
+      const int o = rw < nrows ? (tb + (NTH / GCH) * i) * CO * 2 + goff : UB_OOB;
+      rG[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsG, o, 0, 0));
+      rY[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsY, o, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < XLD; ++i) {
-      const long m = m0 + xrow + (NTH / XCH) * i;
-      const long mm = m < mend ? m : mbeg;
-      rX[i] = *reinterpret_cast<const uint4*>(a.X + mm * a.CI + c0 + xc * 8);
+      const int rw = tb + xrow + (NTH / XCH) * i;
+      rX[i] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(rsX, rw < nrows ? (tb + (NTH / XCH) * i) * a.CI * 2 + xoff : UB_OOB, 0, 0));
     }
   };
   auto stage_tile = [&](long m0) {
@@ -121,6 +141,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void unit_bwd_kernel(UnitBwdArgs a)
     }
   };
 
+  const __amdgpu_buffer_rsrc_t rsD = __builtin_amdgcn_make_buffer_rsrc(a.dD + mbeg * a.CI, (short)0, UB_RECORDS, UB_DWORD3);
   f32x4 accw[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -194,9 +215,9 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void unit_bwd_kernel(UnitBwdArgs a)
 #pragma unroll
     for (int i = 0; i < XLD; ++i) {
       const int r = xrow + (NTH / XCH) * i;
-      if (m0 + r < mend)
-        *reinterpret_cast<uint4*>(a.dD + (m0 + r) * a.CI + c0 + xc * 8) =
-            *reinterpret_cast<const uint4*>(sX + r * XP + xc * 16);
+      const int rw = (int)(m0 - mbeg) + r;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ub_i32x4, *reinterpret_cast<const uint4*>(sX + r * XP + xc * 16)),
+                                             rsD, rw < nrows ? ((int)(m0 - mbeg) + (NTH / XCH) * i) * a.CI * 2 + xoff : UB_OOB, 0, 0);
     }
   }
   // weight-gradient slab: accw[i][j][r] = P[co = wm*64 + i*16 + 4*fg + r][ci = c0 + wn*WN + j*16 + fr]

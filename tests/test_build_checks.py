@@ -31,7 +31,7 @@ def _vregs(operand):
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc") and not shutil.which("hipcc"), reason="hipcc absent")
 def test_sep_fwd_asm_loads_untouched_until_their_wait(tmp_path):
     """The fused block1 forward (csrc/sepfwd.hip) loads its look-ahead input rows with inline-asm
-    global loads the compiler does not track; correctness needs every instruction between such a load
+    buffer loads the compiler does not track; correctness needs every instruction between such a load
     and the next vmcnt wait to leave its destination registers alone (a copy or a spill of one would read
     the register before the data lands).  Checked on the gfx950 assembly of every instantiation, along
     every control-flow path from each load to the first vmcnt wait."""
@@ -50,7 +50,7 @@ def test_sep_fwd_asm_loads_untouched_until_their_wait(tmp_path):
 
     loads = 0
     for i, l in enumerate(lines):
-        m = re.match(r"\s*global_load_dwordx4 (v\[\d+:\d+\]),", l)
+        m = re.match(r"\s*(?:global|buffer)_load_dwordx4 (v\[\d+:\d+\]),", l)
         if not m:
             continue
         loads += 1
@@ -64,7 +64,7 @@ def test_sep_fwd_asm_loads_untouched_until_their_wait(tmp_path):
                 t = instr(k)
                 if t.startswith("s_waitcnt") and "vmcnt" in t or t.startswith("s_endpgm"):
                     break
-                if t.startswith("global_load_dwordx4"):
+                if t.startswith(("global_load_dwordx4", "buffer_load_dwordx4")):
                     k += 1
                     continue
                 if t:
