@@ -936,6 +936,13 @@ bool dw_bwd_asm_reads(int) {
   return e && e[0] == '1';
 }
 
+// XCP_DW_BWD_SKIP4=0: calls with a strided-skip gradient (the first unit of blocks 2, 3 and 12) keep the
+// two-rows-of-look-ahead form instead of the one-row form with plain ring reads (A/B; read per call)
+bool dw_bwd_skip4() {
+  const char* e = getenv("XCP_DW_BWD_SKIP4");
+  return !(e && e[0] == '0');
+}
+
 template <typename T, int ACT>
 void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
   if (a.dRes && dw_bwd_occ4() && !a.dSkip)
@@ -946,6 +953,9 @@ void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
     hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true, 2, 2, true, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true>), dim3(blocks), dim3(256), 0, st, a);
   else if (dw_bwd_roll_all()) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, true>), dim3(blocks), dim3(256), 0, st, a);
+  else if (dw_bwd_occ4() && a.dSkip && dw_bwd_skip4())
+    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 3, true, false, false>), dim3(blocks), dim3(256), 0,
+                       st, a);
   else if (dw_bwd_occ4() && !a.dSkip) {
     if (dw_bwd_asm_reads(a.H))
       hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 4, false>), dim3(blocks), dim3(256), 0, st, a);

@@ -1,8 +1,8 @@
 """A/B of the depthwise backward against the committed version (git HEAD's csrc/dwconv.hip, built
 into probe/libdw_base.so, a path the GPU upload carries -- delete it afterwards): both libraries'
-xcp_dw_bwd on identical inputs at the step's shapes, interleaved rounds, median launch time; the new
-library also with the ring reads forced plain (XCP_DW_BWD_ASM=0) and asm (=1); outputs compared against
-the base (max |diff| of dX, dW partials, BN sums).
+xcp_dw_bwd on identical inputs at the step's shapes (with and without a strided-skip gradient),
+interleaved rounds, median launch time; the new library also with XCP_DW_BWD_SKIP4=0; outputs compared
+against the base (max |diff| of dX, dW partials, BN sums).
 
   python tools/dw_ab.py build [rev]   # here (rev: git revision of the baseline, default HEAD)
   python tools/dw_ab.py run           # GPU box
@@ -53,15 +53,18 @@ def run():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     st = torch.cuda.current_stream().cuda_stream
-    variants = {"base": (libs["base"], None), "new": (libs["new"], None), "plain": (libs["new"], "0"),
-                "asm": (libs["new"], "1")}
-    shapes = [(256, 19, 19, 736, 2, False), (256, 19, 19, 736, 1, True), (256, 37, 37, 736, 2, False),
-              (256, 74, 74, 256, 2, False), (256, 147, 147, 128, 2, False), (256, 10, 10, 1536, 2, False)]
-    for N, H, W, C, act, res in shapes:
+    variants = {"base": (libs["base"], None), "new": (libs["new"], None), "skip4off": (libs["new"], "S0")}
+    # (N, H, W, C, act, residual, strided-skip gradient): the skip shapes are the first units of blocks 2, 3, 12
+    shapes = [(256, 19, 19, 736, 2, False, False), (256, 19, 19, 736, 1, True, False), (256, 37, 37, 736, 2, False, False),
+              (256, 74, 74, 256, 2, False, False), (256, 147, 147, 128, 2, False, False), (256, 10, 10, 1536, 2, False, False),
+              (256, 74, 74, 128, 1, False, True), (256, 37, 37, 256, 1, False, True), (256, 19, 19, 736, 1, False, True)]
+    for N, H, W, C, act, res, skip in shapes:
         M = N * H * W
         dY = torch.randn(M * C, device=dev, generator=g).bfloat16()
         X = torch.randn(M * C, device=dev, generator=g).bfloat16()
         dR = torch.randn(M * C, device=dev, generator=g).bfloat16() if res else None
+        sO = (H - 1) // 2 + 1
+        dS = torch.randn(N * sO * sO * C, device=dev, generator=g).bfloat16() if skip else None
         Wt = torch.randn(9 * C, device=dev, generator=g)
         sc = torch.rand(C, device=dev, generator=g) + 0.5
         sh = torch.randn(C, device=dev, generator=g)
@@ -76,11 +79,14 @@ def run():
         def call(k):
             dX, dWp, bnp = outs[k]
             lib, env = variants[k]
-            if env is None:
-                os.environ.pop("XCP_DW_BWD_ASM", None)
-            else:
+            os.environ.pop("XCP_DW_BWD_ASM", None)
+            os.environ.pop("XCP_DW_BWD_SKIP4", None)
+            if env == "S0":
+                os.environ["XCP_DW_BWD_SKIP4"] = "0"
+            elif env is not None:
                 os.environ["XCP_DW_BWD_ASM"] = env
-            rc = lib.xcp_dw_bwd(1, act, p(dY), p(X), p(Wt), p(sc), p(sh), p(dR), None, 0, 0, 1, 0, p(dX), p(dWp),
+            rc = lib.xcp_dw_bwd(1, act, p(dY), p(X), p(Wt), p(sc), p(sh), p(dR), p(dS), sO if skip else 0,
+                                sO if skip else 0, 2 if skip else 1, 0, p(dX), p(dWp),
                                     p(bnp), p(mu) if act == 2 else None, p(isd) if act == 2 else None, N, H, W, C, st)
             assert rc == 0, rc
 
@@ -97,11 +103,12 @@ def run():
                 e.record()
                 torch.cuda.synchronize()
                 times[k].append(s.elapsed_time(e) / 10 * 1e3)
-        byts = 2 * M * C * (3 + (1 if res else 0))
+        byts = 2 * M * C * (3 + (1 if res else 0)) + (2 * N * sO * sO * C if skip else 0)
         d = [(outs["base"][i].float() - outs[k][i].float()).abs().max().item() for k in variants if k != "base"
              for i in range(3) if outs["base"][i] is not None]
         line = "  ".join(f"{k} {statistics.median(v):7.1f} us ({byts / statistics.median(v) / 1e3:6.0f} GB/s)" for k, v in times.items())
-        print(f"{N}x{H}x{W}x{C} act={act} res={int(res)}: {line}   max|diff| {['%.2e' % x for x in d]}", flush=True)
+        print(f"{N}x{H}x{W}x{C} act={act} res={int(res)} skip={int(skip)}: {line}   max|diff| {['%.2e' % x for x in d]}",
+              flush=True)
 
 
 if __name__ == "__main__":
