@@ -1,0 +1,29 @@
+# Round 5 (final): record of HEAD (v5) on one box: full -m gpu suite, smoke, default bench line, kernel trace +
+# per-stream timeline + per-role summary of the headline step, HBM traffic per launch (step and op PMC passes)
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+( while true; do date >> gpurun_out/f_heartbeat.txt; sleep 50; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+timeout -k 10 1100 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 500 --timeout-method thread -rf --durations=15 > gpurun_out/f_suite.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/f_suite.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/f_smoke.log 2>&1 || exit $?
+timeout -k 10 600 python bench.py > gpurun_out/f_bench.json 2> gpurun_out/f_bench.err || exit $?
+B="python bench.py --cpu-baseline off --mode unfrozen --steps 5 --warmup 2 --small-batch 0 --measured-peaks off --diag off"
+XCP_BENCH_OP_ORDER=gpurun_out/f_oporder.json timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r5f -o kt -- $B > gpurun_out/f_prof.log 2>&1 || exit $?
+python tools/stream_timeline.py "$(find gpurun_out/prof_r5f -name "*kernel_trace.csv" | head -1)" 40 > gpurun_out/f_timeline.txt 2>&1
+python tools/prof_summary.py gpurun_out/prof_r5f 60 --op-order gpurun_out/f_oporder.json > gpurun_out/f_kernels.txt 2>&1
+P="python bench.py --cpu-baseline off --mode unfrozen --steps 3 --warmup 1 --small-batch 0 --measured-peaks off --diag off --no-kernel-timing"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/f_pmct_fetch -o p -- $P > gpurun_out/f_pmct_f.log 2>&1 || exit $?
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/f_pmct_write -o p -- $P > gpurun_out/f_pmct_w.log 2>&1 || exit $?
+python tools/pmc_traffic.py $(find gpurun_out/f_pmct_fetch -name "*counter_collection.csv" | head -1) $(find gpurun_out/f_pmct_write -name "*counter_collection.csv" | head -1) gpurun_out/f_step_traffic.json > gpurun_out/f_pmct.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/f_pmco_fetch -o p -- python tools/kbench.py roof_ops > gpurun_out/f_pmco_f.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/f_pmco_write -o p -- python tools/kbench.py roof_ops > gpurun_out/f_pmco_w.log 2>&1 || exit $?
+python tools/pmc_traffic.py $(find gpurun_out/f_pmco_fetch -name "*counter_collection.csv" | head -1) $(find gpurun_out/f_pmco_write -name "*counter_collection.csv" | head -1) gpurun_out/f_optraffic.json > gpurun_out/f_pmco.log 2>&1
+G="python bench.py --gpus 2 --cpu-baseline off --mode unfrozen --steps 3 --warmup 1 --small-batch 0 --measured-peaks off --diag off --no-kernel-timing"
+XCP_BENCH_BACKEND=gloo timeout -k 10 400 $G > gpurun_out/f_2rank_gloo.json 2> gpurun_out/f_2rank_gloo.err || exit $?
+# keep the merged-back output small: the summaries above are what is kept
+find gpurun_out/prof_r5f gpurun_out/f_pmct_fetch gpurun_out/f_pmct_write gpurun_out/f_pmco_fetch gpurun_out/f_pmco_write -name "*.csv" -size +2M -delete 2>/dev/null || true
