@@ -22,6 +22,9 @@
 // XOR-swizzled with (row>>1)&7 so a 16-lane ds_read_b128 group is conflict-free.
 #include "common.h"
 #include <stdlib.h>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 namespace {
 
@@ -103,6 +106,7 @@ struct NTArgs {
   int M, N, K;
   float* stats;           // [gridM][2][N] partial (sum, sumsq) or nullptr
   Gather ga;
+  int tqs;                // gemm_nt256p_kernel: tile-queue slot + 1 (0: static tile walk)
 };
 
 // ---------------------------------------------------------------------------------
@@ -676,10 +680,22 @@ XCP_DEV void epilogue256_buf(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffe
   epilogue256_get<STATS>([&](int i, int j, int r) { return acc[i][j][r]; }, a, rC, rS, m0, n0, wr, wc, fr, fg);
 }
 
+// Tile counters of the persistent NT kernel, one per (device, stream) slot: a workgroup takes its first
+// tile by its slot and every further one from the counter (fetched by one thread at a tile's start,
+// consumed after the K loop), so the workgroups that run absorb the tiles of those that start late
+// (CUs held by the side stream's weight-gradient GEMM).  Each launch fetches exactly `tiles` times
+// (one failing fetch per active workgroup ends its walk), so the fetch that returns tiles - 1 is the
+// last and resets the counter for the next launch (graph replays included).
+__device__ int g_nt_tq[64];
+
 template <bool STATS>
 __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   constexpr int S_ST = 16 + (STATS ? 1 : 0);   // store instructions per wave per epilogue
-  __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT];
+  // (+ 16 B for the tile-queue broadcast: in the ring's LDS object, since a second object would give the
+  // LDS accesses alias scopes and hipcc would drain the DMA ahead of the fragment reads)
+  __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT + 16];
+  int* const s_next = reinterpret_cast<int*>(smem + 2 * K_SLOT);
+  int* const tq = a.tqs > 0 ? g_nt_tq + (a.tqs - 1) : nullptr;
   const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
   const int tiles = gridM * gridN, nwg = gridDim.x;
   const int slot = xcd_remap(blockIdx.x, nwg);
@@ -767,6 +783,12 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (extra) vm_wait(S_ST);   // K-tile 0 landed (the previous epilogue's stores may still drain)
     else wait_vmcnt<0>();
+    // (thread 0) the queue position of the next tile, by inline asm: the compiler would wait for the
+    // returned value at once (vmcnt(0), draining the prefetch).  Issued after the wait above and before
+    // K-tile 1's loads, it has retired by the time the K loop waits for those (VMEM returns in order).
+    unsigned nxt = 0;
+    if (tq && tid == 0)
+      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(nxt) : "v"(tq), "v"(1u) : "memory");
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();
     // one 64-deep K-tile; FIRST (kt == 0): its data was retired by the wait above, so the two
@@ -812,7 +834,17 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
     for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
     if (wr == 0) __builtin_amdgcn_s_barrier();   // every wave is done reading both ring slots
     const int cm0 = m0, cn0 = n0;
-    t += nwg;
+    if (tq) {
+      if (tid == 0) {
+        asm volatile("" : "+v"(nxt));   // (used only here, after the K loop's waits)
+        *s_next = (int)nxt;
+        if ((int)nxt == tiles - 1) __hip_atomic_store(tq, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      lds_barrier();
+      t = nwg + __builtin_amdgcn_readfirstlane(*s_next);
+    } else {
+      t += nwg;
+    }
     const bool more = t < tiles;
     if (more) {   // the next tile's first K-tile, ahead of this tile's stores
       m0 = (t / gridN) * 256;
@@ -1267,6 +1299,26 @@ bool tn_big(int dtype, int gmode, int N, int K, int tile) {
 }
 }  // namespace
 
+// XCP_NT_DYNQ=0: the persistent NT kernel walks its static tile list (A/B; read per call)
+bool nt_dynq() {
+  const char* e = getenv("XCP_NT_DYNQ");
+  return !(e && e[0] == '0');
+}
+// tile-queue slot + 1 of (device, stream) for gemm_nt256p_kernel (0: static walk, past 64 streams)
+int nt_tq_slot(hipStream_t st) {
+  if (!nt_dynq()) return 0;
+  static std::mutex mu;
+  static std::vector<std::pair<int, hipStream_t>> slots;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  for (size_t i = 0; i < slots.size(); ++i)
+    if (slots[i].first == dev && slots[i].second == st) return (int)i + 1;
+  if (slots.size() >= 64) return 0;
+  slots.emplace_back(dev, st);
+  return (int)slots.size();
+}
+
 extern "C" {
 
 // C[M,N] = A[M,K] . B[N,K]^T ; see include/xcp.h
@@ -1296,6 +1348,11 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
     if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
       const int grid = min(mb * gridN, cus);
+      // the tile queue for the calls without BN statistics: the backward's input gradients, which run beside
+      // the side stream's weight gradients (the forward's launches have the GPU to themselves and keep
+      // the static XCD-ordered walk: with the queue they measured 1 % slower); K >= 128: the counter's
+      // fetch retires within two K-tiles
+      big.tqs = K >= 128 && !stats ? nt_tq_slot(stream) : 0;
       if (stats)
         hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
       else
