@@ -1,4 +1,4 @@
-# Round 5 (final): record of HEAD (v5) on one box: full -m gpu suite, smoke, default bench line, kernel trace +
+# Round 5 (final): record of HEAD on one box: full -m gpu suite, smoke, default bench line, kernel trace +
 # per-stream timeline + per-role summary of the headline step, HBM traffic per launch (step and op PMC passes)
 set -o pipefail
 mkdir -p gpurun_out
