@@ -1063,6 +1063,35 @@ def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("M,N,K", [(92416, 736, 736), (256 * 600 + 77, 256, 448), (5120 * 9, 1024, 736)])
+def test_gemm_nt_persistent_tile_queue_bitwise(ops, gpu, M, N, K):
+    """Calls without BN statistics (the backward's input gradients) take the persistent kernel's tiles
+    from a per-stream queue (XCP_NT_DYNQ): identical bits against the one-shot kernel, over repeated
+    launches (each launch's last fetch resets the counter) and on two streams at once (one counter
+    each)."""
+    g = torch.Generator(device=gpu).manual_seed(M + 3 * N)
+    A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
+    B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
+    ref = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+    ops.gemm_nt(A, B, ref, M, N, K, tile=2)
+    for _ in range(3):
+        C = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        ops.gemm_nt(A, B, C, M, N, K, tile=3)
+        torch.cuda.synchronize()
+        assert torch.equal(C, ref)
+    s1, s2 = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    outs = []
+    for st in (s1, s2, s1, s2):
+        st.wait_stream(torch.cuda.current_stream(gpu))
+        with torch.cuda.stream(st):
+            C = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+            ops.gemm_nt(A, B, C, M, N, K, tile=3)
+        outs.append(C)
+    torch.cuda.synchronize()
+    for C in outs:
+        assert torch.equal(C, ref)
+
+
 def test_reduce_batch_bitwise(ops, gpu):
     """ReduceBatch (xcp_colreduce_multi: up to 16 reductions per launch, two-level jobs split over
     two launches) gives bitwise reduce_slabs' outputs, for one-level and two-level shapes, a slab
