@@ -147,6 +147,11 @@ SEP_FUSED = os.environ.get("XCP_SEP_FUSED", "1") != "0"
 # the stem conv2 (forward and weight gradient) applies BN1 + ReLU on load instead of reading a
 # materialised relu(bn1(conv1)) (XCP_CONV2_ACTIN=0: bn_act + the plain conv; A/B)
 CONV2_ACT_ON_LOAD = os.environ.get("XCP_CONV2_ACTIN", "1") != "0"
+# A unit's pointwise weight gradient is launched on the side stream before its input gradient, so the two
+# overlap (the input gradient's persistent GEMM takes its tiles from a queue and absorbs the CUs the weight
+# gradient holds): +0.4 % in the step against launching it after (profiles/r05_wgrad_first_ab.txt);
+# XCP_WGRAD_FIRST=0 restores the old order (A/B)
+WGRAD_FIRST = os.environ.get("XCP_WGRAD_FIRST", "1") != "0"
 NT_TILE = int(os.environ.get("XCP_NT_TILE", "4" if os.environ.get("XCP_NT_ONESHOT", "0") == "1" else "0"))
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
@@ -573,8 +578,11 @@ class XceptionEngine:
                 ops.unit_bwd(dZ, rec["y"], coef, pk[u.name + ".pwT"], rec["d"], dD, M, u.cout, u.cin, dst, acc)
             else:
                 dY = bn_bwd(u.bn, u.bn_name, dZ, rec["y"], M, u.cout, rec["st"], part)
+                if WGRAD_FIRST:   # the side stream starts on dY before this unit's input gradient (A/B)
+                    wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
                 ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, pc(u.cin), pc(u.cout), tile=NT_TILE)
-                wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
+                if not WGRAD_FIRST:
+                    wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
             dX = self._empty(M * pc(u.cin))
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,
