@@ -147,11 +147,10 @@ SEP_FUSED = os.environ.get("XCP_SEP_FUSED", "1") != "0"
 # the stem conv2 (forward and weight gradient) applies BN1 + ReLU on load instead of reading a
 # materialised relu(bn1(conv1)) (XCP_CONV2_ACTIN=0: bn_act + the plain conv; A/B)
 CONV2_ACT_ON_LOAD = os.environ.get("XCP_CONV2_ACTIN", "1") != "0"
-# A unit's pointwise weight gradient is launched on the side stream before its input gradient, so the two
-# overlap (the input gradient's persistent GEMM takes its tiles from a queue and absorbs the CUs the weight
-# gradient holds): +0.4 % in the step against launching it after (profiles/r05_wgrad_first_ab.txt);
-# XCP_WGRAD_FIRST=0 restores the old order (A/B)
-WGRAD_FIRST = os.environ.get("XCP_WGRAD_FIRST", "1") != "0"
+# XCP_WGRAD_FIRST=1: a unit's pointwise weight gradient launched on the side stream before its input
+# gradient, so the two overlap (A/B; +0.40 % on one box, -0.17 % on another: profiles/r05_wgrad_first_ab.txt;
+# off: the side stream waits for the input gradient)
+WGRAD_FIRST = os.environ.get("XCP_WGRAD_FIRST", "0") == "1"
 NT_TILE = int(os.environ.get("XCP_NT_TILE", "4" if os.environ.get("XCP_NT_ONESHOT", "0") == "1" else "0"))
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
