@@ -1304,6 +1304,10 @@ bool nt_dynq() {
   const char* e = getenv("XCP_NT_DYNQ");
   return !(e && e[0] == '0');
 }
+bool nt_sparse_dgrad() {   // XCP_NT_SPARSE_DGRAD=1 (A/B; read per call)
+  const char* e = getenv("XCP_NT_SPARSE_DGRAD");
+  return e && e[0] == '1';
+}
 // tile-queue slot + 1 of (device, stream) for gemm_nt256p_kernel (0: static walk, past 64 streams)
 int nt_tq_slot(hipStream_t st) {
   if (!nt_dynq()) return 0;
@@ -1340,7 +1344,12 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     const int gridN = xcp_cdiv(N, 256), gridM = xcp_cdiv(M, 256), tiles = gridM * gridN;
     const int cus = gpu_cus();
     int mb = gridM;
-    if ((tile == 0 || tile == 4) && nt_sparse() && tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3)
+    // (calls that take the tile queue keep every row on the persistent kernel: the queue spreads the last
+    // round's tiles over whichever workgroups finish first; +0.2 % in the step, profiles/r05_nt_dynq_ab.txt;
+    // XCP_NT_SPARSE_DGRAD=1 moves their sparse last round to the 128x128 kernel as before)
+    const bool queued = tile == 0 && K >= 128 && !stats && nt_dynq();
+    if ((tile == 0 || tile == 4) && nt_sparse() && (!queued || nt_sparse_dgrad()) && tiles > cus && tiles % cus != 0 &&
+        (tiles % cus) * 4 < cus * 3)
       mb = (tiles / cus) * cus / gridN;
     NTArgs big = a;
     big.M = min(M, mb * 256);
