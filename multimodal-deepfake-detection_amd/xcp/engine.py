@@ -151,6 +151,9 @@ CONV2_ACT_ON_LOAD = os.environ.get("XCP_CONV2_ACTIN", "1") != "0"
 # gradient, so the two overlap (A/B; +0.40 % on one box, -0.17 % on another: profiles/r05_wgrad_first_ab.txt;
 # off: the side stream waits for the input gradient)
 WGRAD_FIRST = os.environ.get("XCP_WGRAD_FIRST", "0") == "1"
+# XCP_SKIP_WGRAD_LATE=1: a block's skip-conv weight gradient launched on the side stream after the block's
+# units instead of before them (A/B: off keeps it beside the block's own depthwise backward)
+SKIP_WGRAD_LATE = os.environ.get("XCP_SKIP_WGRAD_LATE", "0") == "1"
 NT_TILE = int(os.environ.get("XCP_NT_TILE", "4" if os.environ.get("XCP_NT_ONESHOT", "0") == "1" else "0"))
 # Channel pitch of the 728-channel flow (block3 .. block12): 736, so every pixel row starts on a
 # 64-B (bf16) / 128-B (fp32) boundary.  The 8 padding channels are zero throughout: zero rows /
@@ -691,11 +694,15 @@ class XceptionEngine:
         skip_geom = (0, 0, 1)
         if b.skip is not None:
             dYs = bn_bwd(b.skipbn, b.name + ".skipbn", dOut, bs["ys"], Ms, b.cout, bs["sks"])
-            if bs["skip_x"] is not None:
-                wgrad(dYs, bs["skip_x"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1))
-            else:
-                wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1),
-                      gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
+
+            def skip_wgrad():
+                if bs["skip_x"] is not None:
+                    wgrad(dYs, bs["skip_x"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1))
+                else:
+                    wgrad(dYs, bs["x_in"], Ms, b.cout, b.cin, b.name + ".skip.weight", (b.cout, b.cin, 1, 1),
+                          gather=(1, H, W, OH, OW, b.stride, 0) if b.stride != 1 else (0, 0, 0, 0, 0, 1, 0))
+            if not SKIP_WGRAD_LATE:
+                skip_wgrad()
             dXs = self._empty(Ms * pc(b.cin))
             ops.gemm_nt(dYs, pk[b.name + ".skipT"], dXs, Ms, pc(b.cin), pc(b.cout), tile=NT_TILE)
             if b.stride != 1:
@@ -721,6 +728,8 @@ class XceptionEngine:
                                         prev_st=pre, skip_pre=pre is not None, res_bn=res_bn)
                 pre_part = out_part if pre is not None else None
                 prev_part = out_part if res_bn is not None else None
+        if b.skip is not None and SKIP_WGRAD_LATE:
+            skip_wgrad()
         return dZ, pre_part, prev_part
 
 
