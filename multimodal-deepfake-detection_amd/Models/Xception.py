@@ -132,6 +132,7 @@ class Xception(nn.Module):
         self._xcp_engines = {}
         self._xcp_grad_sink = None   # xcp.ddp.GradBuckets(module=...) registers itself here
         self._xcp_buffer_wait = None   # xcp.ddp.broadcast_buffers' completion event (async form)
+        self.register_state_dict_pre_hook(_wait_buffers_hook)   # a checkpoint reads broadcast values
 
     def _xcp_wait_buffers(self):
         """Make the current stream wait for a pending buffer broadcast (xcp.ddp.broadcast_buffers),
@@ -158,6 +159,7 @@ class Xception(nn.Module):
         """nn.DataParallel replica (train_audio.py:16-18): its own engine cache (an engine holds
         the module it packs weights from) and no gradient sink -- a replica's gradients reach
         the original parameters through DataParallel's autograd broadcast."""
+        self._xcp_wait_buffers()   # replicas copy the buffers as broadcast
         r = super()._replicate_for_data_parallel()
         r._xcp_engines = {}
         r._xcp_grad_sink = None
@@ -187,8 +189,8 @@ class Xception(nn.Module):
     def forward_modules(self, x):
         """Xception.forward as the reference composes it (Xception.py:167-201), each sub-module on
         the xcp custom ops.  Returns fp32 features through ``fc``."""
-        self._xcp_wait_buffers()
         x = self.conv1(x)
+        self._xcp_wait_buffers()   # (xcp.ddp.broadcast_buffers) first running-statistic access
         x = self.bn1(x)
         x = self.relu(x)
         x = self.conv2(x)
@@ -212,11 +214,16 @@ class Xception(nn.Module):
         return self.fc(self.features(x))
 
     def __getstate__(self):   # copies (torch.save, deepcopy for AveragedModel) share no engine / sink
+        self._xcp_wait_buffers()
         d = self.__dict__.copy()
         d["_xcp_engines"] = {}
         d["_xcp_grad_sink"] = None
         d["_xcp_buffer_wait"] = None
         return d
+
+
+def _wait_buffers_hook(module, prefix, keep_vars):
+    module._xcp_wait_buffers()
 
 
 def _local_weights(pretrained):

@@ -582,7 +582,7 @@ XCP_DEV void ring_fence1(unsigned& v) {
 // argument so the other forms carry no conditional loads -- a load behind a runtime branch made hipcc
 // drain vmcnt(0) at the branch's join on every row step)
 template <typename T, int ACT, bool RES, bool ROLL, int BDV = 2, int MINW = (ROLL ? 2 : 3), bool SKIP = true,
-          bool BNRES = false, bool ASMRD = true>
+          bool BNRES = false, bool ASMRD = false>
 __global__ __launch_bounds__(256, MINW) void dw_bwd_lds_kernel(DwBwdArgs a) {
   typedef RV<T> R;
   typedef typename R::V V;
@@ -945,25 +945,27 @@ bool dw_bwd_skip4() {
 
 template <typename T, int ACT>
 void launch_bwd_act(const DwBwdArgs& a, int blocks, hipStream_t st) {
-  if (a.dRes && dw_bwd_occ4() && !a.dSkip)
-  {
-    if (a.Yb) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, false, 1, 3, false, true>), dim3(blocks), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, false, 1, 3, false>), dim3(blocks), dim3(256), 0, st, a);
+  // every form reads the ring with plain C++ reads unless XCP_DW_BWD_ASM=1 (the inline-asm form, kept
+  // for the bitwise A/B test_dw_bwd_ring_read_forms)
+  const bool asmrd = dw_bwd_asm_reads(a.H);
+#define DWB(...)                                                                                  \
+  do {                                                                                            \
+    if (asmrd) hipLaunchKernelGGL((dw_bwd_lds_kernel<__VA_ARGS__, true>), dim3(blocks), dim3(256), 0, st, a); \
+    else hipLaunchKernelGGL((dw_bwd_lds_kernel<__VA_ARGS__, false>), dim3(blocks), dim3(256), 0, st, a);     \
+  } while (0)
+  if (a.dRes && dw_bwd_occ4() && !a.dSkip) {
+    if (a.Yb) DWB(T, ACT, true, false, 1, 3, false, true);
+    else DWB(T, ACT, true, false, 1, 3, false, false);
   } else if (a.dRes && a.Yb)
-    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true, 2, 2, true, true>), dim3(blocks), dim3(256), 0, st, a);
-  else if (a.dRes) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, true, true>), dim3(blocks), dim3(256), 0, st, a);
-  else if (dw_bwd_roll_all()) hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, true>), dim3(blocks), dim3(256), 0, st, a);
+    DWB(T, ACT, true, true, 2, 2, true, true);
+  else if (a.dRes) DWB(T, ACT, true, true, 2, 2, true, false);
+  else if (dw_bwd_roll_all()) DWB(T, ACT, false, true, 2, 2, true, false);
   else if (dw_bwd_occ4() && a.dSkip && dw_bwd_skip4())
-    hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 3, true, false, false>), dim3(blocks), dim3(256), 0,
-                       st, a);
-  else if (dw_bwd_occ4() && !a.dSkip) {
-    if (dw_bwd_asm_reads(a.H))
-      hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 4, false>), dim3(blocks), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false, 1, 4, false, false, false>), dim3(blocks), dim3(256), 0,
-                         st, a);
-  }
-  else hipLaunchKernelGGL((dw_bwd_lds_kernel<T, ACT, false, false>), dim3(blocks), dim3(256), 0, st, a);
+    DWB(T, ACT, false, false, 1, 3, true, false);
+  else if (dw_bwd_occ4() && !a.dSkip)
+    DWB(T, ACT, false, false, 1, 4, false, false);
+  else DWB(T, ACT, false, false, 2, 3, true, false);
+#undef DWB
 }
 
 template <typename T>

@@ -860,6 +860,301 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+// Persistent 256x256 NT kernel, two MFMA phases per 64-deep K-tile and the fill issued ~1.5
+// K-tiles ahead (gemm_nt256q_kernel, the default; XCP_NT_LOOP=4 keeps gemm_nt256p_kernel).
+//
+// The four-phase loop above pays 8 s_barrier per K-tile around 16-MFMA phases and issues the
+// next K-tile's fill during the current one (its probe, profiles/r04_nt_probe.txt: MFMAs plus
+// that barrier skeleton 1.31 us per K-tile against 0.86 us of MFMA issue at 2.4 GHz, the fill
+// another 0.47 us exposed).  Here each wave's K-tile is
+//   R0  reads B (its 64 columns) and A-top (its group's first 64 rows): 16 ds_read_b128
+//   M0  32 MFMAs into acc[0..3][0..3]
+//   R1  reads A-bot: 8 ds_read_b128
+//   M1  32 MFMAs into acc[4..7][0..3]
+// with one barrier between consecutive intervals (4 per K-tile) and wave group 1 (waves 4-7)
+// one interval behind group 0, so every interval pairs one group's MFMAs with the other group's
+// LDS reads and DMA issue on each SIMD.  A read interval ends with lgkmcnt(0), so the MFMA
+// interval after it starts on registers that have landed.
+// Ring: the two 64 KB slots of gemm_nt256p_kernel, refilled by region as soon as both groups have
+// read it: a slot's A-top + B region (6 LDS-DMA instructions per wave) is free after both groups'
+// R0, its A-bot region (2 per wave) after both groups' R1.  So during K-tile k a wave issues
+//   R0(k): A-bot of K-tile k+1        R1(k): A-top + B of K-tile k+2
+// which leaves every region 6 intervals (1.5 K-tiles) between its issue and its first reader.
+// K-tiles run on across tiles (the next tile's first two K-tiles are issued during this tile's
+// last two) and a finished tile's epilogue is split over the next tile's read intervals: rows
+// 0-63 of each group (acc[0..3]) are stored and zeroed in R0, rows 64-127 (acc[4..7]) and the BN
+// statistics row in R1 -- beside the other group's MFMAs.
+// Every wave waits for its own fill with one counted vmcnt per region: the count is the number of
+// VMEM instructions the wave issued after the awaited region (epilogue stores are always issued,
+// masked lanes by an out-of-range offset), so each wait retires exactly that region; wave 0's
+// tile-queue fetch can only add a younger instruction (a stricter wait).  Needs K > 64.
+template <bool STATS, int H>
+XCP_DEV void epilogue256_half(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffer_rsrc_t rC,
+                              __amdgpu_buffer_rsrc_t rS, int m0, int n0, int wr, int wc, int fr, int fg,
+                              float (&red)[2]) {
+  const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
+  const int mrow = m0 + wr * 128 + fr;
+  const int ncol = n0 + wc * 64;
+  const bool odd = fg & 1;
+  float s1[16], s2[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) s1[q] = s2[q] = 0.f;
+  const int c0 = ncol + (odd ? 16 + (fg - 1) * 4 : fg * 4);
+  static_for<4 * H, 4 * H + 4>([&](auto i) {
+    const int m = mrow + i * 16;
+    const bool mok = m < a.M;
+    uint2 pc[4];
+    static_for<0, 4>([&](auto j) {
+      pc[j] = make_uint2(pk_bf16(acc[i][j][0], acc[i][j][1]), pk_bf16(acc[i][j][2], acc[i][j][3]));
+      const bf16x4 q = __builtin_bit_cast(bf16x4, pc[j]);
+      if constexpr (STATS) {   // (branch-free: rows past M add zero)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float f = mok ? (float)q[r] : 0.f;
+          s1[j * 4 + r] += f;
+          s2[j * 4 + r] = fmaf(f, f, s2[j * 4 + r]);
+        }
+      }
+      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    });
+    const uint2 snd0 = odd ? pc[0] : pc[1], snd1 = odd ? pc[2] : pc[3];
+    uint2 rc0, rc1;
+    rc0.x = __shfl_xor(snd0.x, 16, 64);
+    rc0.y = __shfl_xor(snd0.y, 16, 64);
+    rc1.x = __shfl_xor(snd1.x, 16, 64);
+    rc1.y = __shfl_xor(snd1.y, 16, 64);
+    const uint4 st0 = odd ? make_uint4(rc0.x, rc0.y, pc[1].x, pc[1].y) : make_uint4(pc[0].x, pc[0].y, rc0.x, rc0.y);
+    const uint4 st1 = odd ? make_uint4(rc1.x, rc1.y, pc[3].x, pc[3].y) : make_uint4(pc[2].x, pc[2].y, rc1.x, rc1.y);
+    const unsigned rowb = (unsigned)((long)m * a.ldc * 2);
+    const unsigned o0 = (mok && c0 < a.N) ? rowb + (unsigned)c0 * 2 : BUF_OOB;
+    const unsigned o1 = (mok && c0 + 32 < a.N) ? rowb + (unsigned)(c0 + 32) * 2 : BUF_OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 0);
+  });
+  if constexpr (STATS) {   // this half's column sums, reduced over the wave as epilogue256_get does
+    float u[16], v8[8], v4[4];
+    const bool b3 = fr & 8, b2 = fr & 4, b1 = fr & 2, b0 = fr & 1;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) u[q] = (b3 ? s2[q] : s1[q]) + __shfl_xor(b3 ? s1[q] : s2[q], 8, 64);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v8[q] = (b2 ? u[8 + q] : u[q]) + __shfl_xor(b2 ? u[q] : u[8 + q], 4, 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v4[q] = (b1 ? v8[4 + q] : v8[q]) + __shfl_xor(b1 ? v8[q] : v8[4 + q], 2, 64);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) red[q] += (b0 ? v4[2 + q] : v4[q]) + __shfl_xor(b0 ? v4[q] : v4[2 + q], 1, 64);
+    if constexpr (H == 1) {
+      const int col = ncol + ((fr & 7) >> 1) * 16 + fg * 4 + (fr & 1) * 2;
+      const int srow = bm * 2 + wr;
+      const unsigned so = (srow < stat_rows && col < a.N)
+                              ? (unsigned)((((long)srow * 2 + (fr >> 3)) * a.N + col) * 4) : BUF_OOB;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_float2(red[0], red[1])), rS, (int)so, 0, 0);
+      red[0] = red[1] = 0.f;
+    }
+  }
+}
+
+// s_waitcnt vmcnt(n) for the counts gemm_nt256q_kernel forms (steady state 8 first; any other
+// value waits for everything, which is only ever stricter)
+XCP_DEV void vm_wait_q(int n) {
+#define XCP_VMQ(k) if (n == k) { asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); return; }
+  XCP_VMQ(8) XCP_VMQ(16) XCP_VMQ(17) XCP_VMQ(18) XCP_VMQ(19) XCP_VMQ(24) XCP_VMQ(25) XCP_VMQ(2)
+#undef XCP_VMQ
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+XCP_DEV void nt_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(512) void gemm_nt256q_kernel(NTArgs a) {
+  constexpr int EA = 8, EB = 8 + (STATS ? 1 : 0);   // epilogue stores per wave in R0 / in R1
+  __shared__ __attribute__((aligned(16))) char smem[2 * K_SLOT + 16];
+  int* const s_next = reinterpret_cast<int*>(smem + 2 * K_SLOT);
+  int* const tq = a.tqs > 0 ? g_nt_tq + (a.tqs - 1) : nullptr;
+  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
+  const int tiles = gridM * gridN, nwg = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int arow = (w < 4 ? 16 * w : 128 + 16 * (w - 4));
+  const int brow = 64 * (w >> 1) + 16 * (w & 1);
+  const int lr = lane >> 3;
+  // per lane: the rows it fills of each half-tile (wave base + i * 8 + lr) and the 16-B chunk of the
+  // 128-B row (XOR-swizzled by (row >> 1) & 7 = (i * 4 + lr / 2) & 7: every base is a multiple of 16);
+  // the tile only adds a scalar row offset, so the per-lane part of each offset is tile-independent
+  const int kc8[2] = {((lane & 7) ^ ((lr >> 1) & 7)) * 8, ((lane & 7) ^ ((4 + (lr >> 1)) & 7)) * 8};
+  auto hbase = [&](int h) {   // wave-uniform first row of half-tile h this wave fills
+    return (h == 0 || h == 3) ? arow + (h == 3 ? 64 : 0) : brow + (h == 2 ? 32 : 0);
+  };
+  unsigned lpart[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool isA = (h == 0 || h == 3);
+      lpart[h][i] = (unsigned)(((long)(hbase(h) + i * 8 + lr) * (isA ? a.lda : a.ldb) + kc8[i]) * 2);
+    }
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, BUF_RECORDS, BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(STATS ? (void*)a.stats : a.C, (short)0,
+                                                                       BUF_RECORDS, BUF_DWORD3);
+  // half-tile h of K-tile kt of tile tt into ring slot sl: 2 instructions
+  auto issue = [&](int tt, int h, int kt, int sl) {
+    const bool isA = (h == 0 || h == 3);
+    const int row0 = hbase(h);
+    const int tb = isA ? (tt / gridN) * 256 : (tt % gridN) * 256;   // (uniform)
+    const unsigned tofs = (unsigned)((long)tb * (isA ? a.lda : a.ldb) * 2);
+    char* d = smem + sl * K_SLOT + (isA ? 0 : K_OP) + row0 * 128;
+    const int kb = kt * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = tb + row0 + i * 8 + lr < (isA ? a.M : a.N) && kb + kc8[i] < a.K;
+      const unsigned o = ok ? lpart[h][i] + tofs + kb * 2 : BUF_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? rA : rB, (__attribute__((address_space(3))) void*)(d + i * 1024),
+                                               16, o, 0, 0, 0);
+    }
+  };
+  auto issue_atb = [&](int tt, int kt, int sl) {   // 6 instructions
+    issue(tt, 0, kt, sl);
+    issue(tt, 1, kt, sl);
+    issue(tt, 2, kt, sl);
+  };
+
+  int t = xcd_remap(blockIdx.x, nwg);
+  if (t >= tiles) return;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float red[2] = {0.f, 0.f};
+  const int nk = (a.K + 63) / 64;
+  const int fr = lane & 15, fg = lane >> 4;
+  bf16x8 af[4][2], bf[4][2];
+  // the next tile: known now on the static walk; with the tile queue fetched at each tile's start
+  // and published at K-tile nk-2
+  int tn = t + nwg;
+  bool more = !tq && tn < tiles;
+  // prologue: A-top + B of K-tiles 0 and 1, A-bot of 0; wait for K-tile 0's A-top + B
+  issue_atb(t, 0, 0);
+  issue(t, 3, 0, 0);
+  issue_atb(t, 1, 1);
+  vm_wait_q(8);
+  nt_barrier();
+  if (wr == 1) nt_barrier();
+
+  int sb = 0;              // ring slot of this tile's K-tile 0
+  int pt = 0;              // the finished tile whose epilogue runs during K-tile 0 (when follow)
+  bool follow = false;     // this tile follows another one of this workgroup
+  unsigned nxt = 0;
+  int kt = 0;
+  while (true) {
+    const int sl = (sb + kt) & 1;
+    const char* sa = smem + sl * K_SLOT;
+    const char* sbp = sa + K_OP;
+    const bool last = kt + 1 == nk;
+    const bool e0 = follow && kt == 0;           // epilogue halves in this K-tile's R0 / R1
+    const bool e_prev = follow && kt == 1;       // ... in the previous K-tile's
+    const bool ex1 = !last || more;              // K-tile k+1 exists (this tile's or the next one's)
+    // ---- R0: epilogue rows 0-63, B + A-top fragments, A-bot fill of K-tile k+1
+    if (e0) epilogue256_half<STATS, 0>(acc, a, rC, rS, (pt / gridN) * 256, (pt % gridN) * 256, wr, wc, fr, fg, red);
+    if (kt == 0 && tq && tid == 0)
+      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(nxt) : "v"(tq), "v"(1u) : "memory");
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[j][ks] = *reinterpret_cast<const bf16x8*>(sbp + swz(wc * 64 + j * 16 + fr, ks * 4 + fg));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 16 + fr, ks * 4 + fg));
+    }
+    if (!last) issue(t, 3, kt + 1, sl ^ 1);
+    else if (more) issue(tn, 3, 0, sl ^ 1);
+    // A-bot of K-tile k (issued in R0(k-1)) is followed by: R1(k-1)'s epilogue half and A-top + B of
+    // k+1, this R0's epilogue half and A-bot of k+1
+    const int c_ab = (e_prev ? EB : 0) + (ex1 ? 8 : 0) + (e0 ? EA : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (wr == 1) vm_wait_q(c_ab);
+    nt_barrier();
+    // ---- M0
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 0) vm_wait_q(c_ab);
+    if (tq && kt == nk - 2 && tid == 0) {   // publish the next tile (the fetch has retired)
+      if (nk == 2) vm_wait_q(2);              // (K-tile 0: only A-bot of K-tile 1 follows the fetch)
+      asm volatile("" : "+v"(nxt));
+      *s_next = (int)nxt;
+      if ((int)nxt == tiles - 1) __hip_atomic_store(tq, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    nt_barrier();
+    // ---- R1: epilogue rows 64-127 + statistics, A-bot fragments, A-top + B fill of K-tile k+2
+    if (tq && kt == nk - 2) {
+      tn = nwg + __builtin_amdgcn_readfirstlane(*s_next);
+      more = tn < tiles;
+    }
+    if (e0) epilogue256_half<STATS, 1>(acc, a, rC, rS, (pt / gridN) * 256, (pt % gridN) * 256, wr, wc, fr, fg, red);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
+    const bool ex2 = kt + 2 < nk || more;        // K-tile k+2 exists
+    if (kt + 2 < nk) issue_atb(t, kt + 2, sl);
+    else if (more) issue_atb(tn, kt + 2 - nk, sl);
+    // A-top + B of K-tile k+1 (issued in R1(k-1)) is followed by: this K-tile's two epilogue halves,
+    // A-bot of k+1 and A-top + B of k+2
+    const int c_atb = (e0 ? EA + EB : 0) + (ex1 ? 2 : 0) + (ex2 ? 6 : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (wr == 1 && ex1) vm_wait_q(c_atb);
+    nt_barrier();
+    // ---- M1
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][ks], af[i][ks], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 0 && ex1) vm_wait_q(c_atb);
+    nt_barrier();
+    if (!last) {
+      ++kt;
+      continue;
+    }
+    if (!more) break;
+    // next tile: its K-tiles 0 and 1 are in flight, this one's epilogue runs in its K-tile 0
+    pt = t;
+    t = tn;
+    sb = (sb + nk) & 1;
+    kt = 0;
+    follow = true;
+    tn = t + nwg;
+    more = !tq && tn < tiles;
+  }
+  if (wr == 0) nt_barrier();   // (group 1 ran one barrier behind)
+  const int m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
+  epilogue256_half<STATS, 0>(acc, a, rC, rS, m0, n0, wr, wc, fr, fg, red);
+  epilogue256_half<STATS, 1>(acc, a, rC, rS, m0, n0, wr, wc, fr, fg, red);
+}
+
+// ---------------------------------------------------------------------------------
 // Weight gradient: P[s][n][k] = sum_{m in split s} G[m][n] * X[m][k]
 // G: [M][ldg] (output-gradient pixel rows), X: [M][ldx] (layer-input pixel rows).
 // Both operands are pixel-major, so the reduction index m is the slow memory
@@ -1299,6 +1594,13 @@ bool tn_big(int dtype, int gmode, int N, int K, int tile) {
 }
 }  // namespace
 
+// XCP_NT_LOOP=4: the persistent NT kernel with four MFMA phases per K-tile (gemm_nt256p_kernel) instead of
+// two (gemm_nt256q_kernel; A/B, read per call)
+bool nt_loop2() {
+  const char* e = getenv("XCP_NT_LOOP");
+  return e && e[0] == '2';
+}
+
 // XCP_NT_DYNQ=0: the persistent NT kernel walks its static tile list (A/B; read per call)
 bool nt_dynq() {
   const char* e = getenv("XCP_NT_DYNQ");
@@ -1307,6 +1609,15 @@ bool nt_dynq() {
 bool nt_sparse_dgrad() {   // XCP_NT_SPARSE_DGRAD=1 (A/B; read per call)
   const char* e = getenv("XCP_NT_SPARSE_DGRAD");
   return e && e[0] == '1';
+}
+// A tile-queue counter is keyed by the (device, stream) of the launch, and each launch relies on being
+// its counter's only user between its first fetch and its last (which resets it).  Launches on one
+// stream are ordered, so eager use is safe.  A graph node would keep the capture stream's counter
+// whatever stream the graph is replayed on (and two replays could overlap), so calls under stream
+// capture take the static tile walk instead.
+bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 // tile-queue slot + 1 of (device, stream) for gemm_nt256p_kernel (0: static walk, past 64 streams)
 int nt_tq_slot(hipStream_t st) {
@@ -1361,8 +1672,13 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
       // the side stream's weight gradients (the forward's launches have the GPU to themselves and keep
       // the static XCD-ordered walk: with the queue they measured 1 % slower); K >= 128: the counter's
       // fetch retires within two K-tiles
-      big.tqs = K >= 128 && !stats ? nt_tq_slot(stream) : 0;
-      if (stats)
+      big.tqs = K >= 128 && !stats && !stream_capturing(stream) ? nt_tq_slot(stream) : 0;
+      if (K > 64 && nt_loop2()) {   // two MFMA phases per K-tile, fill 1.5 K-tiles ahead
+        if (stats)
+          hipLaunchKernelGGL(gemm_nt256q_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
+        else
+          hipLaunchKernelGGL(gemm_nt256q_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
+      } else if (stats)
         hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
       else
         hipLaunchKernelGGL(gemm_nt256p_kernel<false>, dim3(grid), dim3(512), 0, stream, big);

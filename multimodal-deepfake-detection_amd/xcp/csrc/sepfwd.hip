@@ -120,7 +120,11 @@ __global__ __launch_bounds__(512) void sep_fwd_kernel(SepArgs a) {
   constexpr int YP = COUT * 2 + 16;               // Y staging pitch (the D tile's at CIN = COUT = 128)
   constexpr int KY = (SP_HALF * YC + 511) / 512;  // Y stores per thread per half row
   constexpr bool YSHARE = YP == DP;               // Y staged in the D tile's space
-  constexpr int NST = 2 * (KD + KY);              // stores per output row
+  constexpr int NST = NHALF * (KD + KY);          // stores per output row
+  // the per-row wait vmcnt(NST + KL) must retire the oldest register set on every row: on a band's
+  // first row only that set's KL-load successor (the other set) and this row's NST stores follow it;
+  // on later rows the previous row's NST stores come first and are retired with it
+  static_assert(NST + KL <= 39, "counted wait exceeds sp_vm_wait's range");
   __shared__ __attribute__((aligned(16))) char rows[3 * RB];
   __shared__ __attribute__((aligned(16))) char dt[SP_HALF * DP];
   __shared__ __attribute__((aligned(16))) char yown[YSHARE ? 16 : SP_HALF * YP];

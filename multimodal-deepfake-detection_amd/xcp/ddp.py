@@ -39,8 +39,9 @@ one scaling pass per bucket.
 Buffers.  ``broadcast_buffers`` launches rank 0's BatchNorm running statistics from a stream of its
 own (one persistent flat buffer: gather, broadcast, scatter back) and hands the completion event to
 every xcp Xception backbone in the module; the main stream waits on it only where the forward first
-reads or writes a running statistic (the stem's BN1 statistics, after conv1 has been enqueued), not
-before the step starts.  That is the RCCL form; under gloo (whose wait() blocks the host until the
+reads or writes a running statistic (the stem's BN1 statistics, after conv1 has been enqueued -- on
+the fused engine and on the module path alike), not before the step starts.  ``state_dict()``,
+pickling and DataParallel replication wait too; other readers call ``wait_buffers(module)``.  That is the RCCL form; under gloo (whose wait() blocks the host until the
 side stream has drained) the broadcast completes on the current stream.
 
 Which parameters take part is re-read at every ``zero()``: the reference trains with
@@ -287,14 +288,28 @@ def broadcast_buffers(module, src=0, use_streams=None):
         # (XCP_BCAST_STREAMS=0/1 overrides, A/B)
         env = os.environ.get("XCP_BCAST_STREAMS")
         use_streams = bufs[0].is_cuda and (env == "1" if env in ("0", "1") else dist.get_backend() == "nccl")
+    bbs = _backbones(module)
+    if len({(b.dtype, b.device) for b in bufs}) > 1:
+        # mixed dtypes / devices (e.g. a float64 running stat): one flat buffer per group, on the
+        # current stream
+        for m in bbs:
+            m._xcp_wait_buffers()
+        groups = {}
+        for b in bufs:
+            groups.setdefault((b.dtype, b.device), []).append(b)
+        for g in groups.values():
+            flat = torch.cat([b.reshape(-1) for b in g])
+            dist.broadcast(flat, src)
+            torch._foreach_copy_(g, [v.view_as(b) for v, b in zip(flat.split([b.numel() for b in g]), g)])
+        return
     st = _BCAST.get(module)
     n = sum(b.numel() for b in bufs)
-    if st is None or st["flat"].numel() != n or st["flat"].device != bufs[0].device:
-        st = {"flat": torch.empty(n, device=bufs[0].device, dtype=bufs[0].dtype), "stream": None}
+    key = (n, bufs[0].device, bufs[0].dtype)
+    if st is None or st["key"] != key:
+        st = {"flat": torch.empty(n, device=bufs[0].device, dtype=bufs[0].dtype), "stream": None, "key": key}
         _BCAST[module] = st
     flat = st["flat"]
     views = [v.view_as(b) for v, b in zip(flat.split([b.numel() for b in bufs]), bufs)]
-    bbs = _backbones(module)
     owned = {id(b) for m in bbs for b in m.buffers() if b.is_floating_point()}
     if not (use_streams and bbs and all(id(b) in owned for b in bufs)):
         for m in bbs:
@@ -320,3 +335,12 @@ def broadcast_buffers(module, src=0, use_streams=None):
         ev.record(side)
     for m in bbs:
         m._xcp_buffer_wait = ev
+
+
+def wait_buffers(module):
+    """Make the current stream wait for a ``broadcast_buffers`` still in flight on ``module``'s
+    backbones.  The forward, ``state_dict()``, pickling / deepcopy and nn.DataParallel replication
+    of an xcp Xception do this themselves; call it before touching the BN buffers any other way
+    (e.g. an in-place EMA of the running statistics outside forward)."""
+    for m in _backbones(module):
+        m._xcp_wait_buffers()

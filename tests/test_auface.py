@@ -85,11 +85,13 @@ def test_trainer_construction_and_checkpoint_cpu(tmp_path):
 
 
 @pytest.mark.gpu
-def test_auface_forward_backward_vs_oracle(gpu):
+@pytest.mark.parametrize("T,A,S", [(3, 4, 64), (75, 17, 128)], ids=["small", "reference_shape"])
+def test_auface_forward_backward_vs_oracle(gpu, T, A, S):
     """HIP path vs oracle.auface_forward in fp32: logits, both token streams, the harness loss
     (CB-focal on ArcFace(m=0.30) of the embed head, + 0.2 align + 0.1 temporal; embed head in
     eval so its dropout is off), and every parameter's gradient norm (test_gpu_model contract:
-    1e-3, BatchNorm affine 5e-3)."""
+    1e-3, BatchNorm affine 5e-3).  ``reference_shape`` is train_au_face.py:563-570's own
+    per-step shape: batch 2, 75 frames, 17 AUs, 128 x 128."""
     import xcp
     from xcp.auface import auface_losses
     from xcp.heads import ArcFaceHead, CBFocalLoss
@@ -104,10 +106,15 @@ def test_auface_forward_backward_vs_oracle(gpu):
     w_cpu = arc.weight.detach().clone().requires_grad_(True)
     m, embed, arc = m.to(gpu), embed.to(gpu), arc.to(gpu)
     cb = CBFocalLoss([300, 1700]).to(gpu)
-    videos = seeded((2, 3, 3, 64, 64), 11)
-    aus = seeded((2, 4, 3, 64, 64), 12)
-    mask = torch.tensor([[1., 1., 0., 1.], [1., 0., 1., 1.]])
-    weight = torch.tensor([[1., .5, 1., .25], [1., 1., .75, 1.]])
+    videos = seeded((2, 3, T, S, S), 11)
+    aus = seeded((2, A, 3, S, S), 12)
+    if A == 4:
+        mask = torch.tensor([[1., 1., 0., 1.], [1., 0., 1., 1.]])
+        weight = torch.tensor([[1., .5, 1., .25], [1., 1., .75, 1.]])
+    else:   # some AUs absent (mask 0) and uneven weights, as the dataset's per-AU detection gives
+        g = torch.Generator().manual_seed(13)
+        mask = (torch.rand(2, A, generator=g) > 0.25).float()
+        weight = 0.25 + 0.75 * torch.rand(2, A, generator=g)
     labels = torch.tensor([0, 1])
     with xcp.precision("fp32"):
         logits, v_tok, au_tok = m(videos.to(gpu), aus.to(gpu), au_mask=mask.to(gpu), au_weight=weight.to(gpu))
