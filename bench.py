@@ -60,6 +60,12 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay the whole train step as one HIP graph (on: world size 1; auto = off, measured slower)")
+    ap.add_argument("--ddp-proxy", type=int, default=0, metavar="G",
+                    help="world size 1 only: at every bucket-ready point launch a stand-in of a G-rank RCCL all-reduce "
+                         "(xcp_comm_proxy) from the stream the real one would use, and report its timings "
+                         "(xcp.ddp proxy mode, profiles/r06_ddp_proxy.txt); 0 = off")
+    ap.add_argument("--ddp-proxy-busbw", type=float, default=300.0, help="stand-in all-reduce bus bandwidth, GB/s")
+    ap.add_argument("--ddp-proxy-blocks", type=int, default=32, help="stand-in workgroups (RCCL channel blocks)")
     ap.add_argument("--small-batch", type=int, default=4,
                     help="lstmv: also time the unfrozen step at this many clips/GPU (train_visual.py:545 uses 4; "
                          "0: off)")
@@ -347,7 +353,9 @@ class Run:
             model.fc.weight.requires_grad = model.fc.bias.requires_grad = True
         self.model = model.to(dev).train()
         self.params = list(self.model.parameters())
-        self.buckets = ddp.GradBuckets(self.params, world=world, module=self.model)
+        proxy = ({"world": args.ddp_proxy, "busbw": args.ddp_proxy_busbw, "blocks": args.ddp_proxy_blocks}
+                 if args.ddp_proxy and world == 1 else None)
+        self.buckets = ddp.GradBuckets(self.params, world=world, module=self.model, proxy=proxy)
         lr, wd = (1e-4, 0.0) if args.model == "lstma" else (1e-5, 1e-4)
         self.use_graph = graph_mode(args, world)
         self.graph = None
@@ -575,6 +583,7 @@ def main():
     if diag is not None:
         diag["clock_mhz_idle"] = round(ops.clock_probe(dev), 1)
         diag["stream_priority_range"] = list(torch.cuda.Stream.priority_range())
+    proxy_rep = None
     for mode in modes:
         if rank == 0:
             log(f"{args.model} {mode}: building model")
@@ -615,6 +624,9 @@ def main():
             torch.cuda.current_stream().wait_stream(hs)
         else:
             elapsed, loss = timed(run, steps, args.warmup, world, None, dg)
+        if mode == modes[0] and getattr(getattr(run, "buckets", None), "proxy", None) is not None:
+            from xcp import ddp as _ddp
+            proxy_rep = _ddp.proxy_report(run.buckets, steps)
         if timer is not None:
             # per-kernel durations for the roofline lines, on a second timed region of the same steps right
             # after the headline one: the bracketing HIP events cost the step 1.1-1.5 % (409.1 vs 414.5
@@ -761,6 +773,8 @@ def main():
                           if graph_mode(args, world) else "eager launches"},
                "roofline": roof, "loss": round(loss, 5)}
         out.update(extra)
+        if proxy_rep is not None:
+            out["ddp_proxy"] = proxy_rep
         if small is not None:
             out["small_batch"] = small
         if diag is not None:

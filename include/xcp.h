@@ -264,10 +264,17 @@ int xcp_focal_ce(const float* Z, const long long* labels, const float* weights, 
 /* ---- LSTM recurrence (nn.LSTM, XceptionLSTMV.py:18-23, :67) ----
  * whh is W_hh [4H][H] as nn.LSTM stores it (weight_hh_l0); whhT ([H][4H]) is read only by the
  * generic kernel, i.e. when xcp_lstm_needs_whhT(B, H, kernel) returns 1 (H = 64 / 128 run
- * register-resident, H = 256 / 512 / 1024 on per-step kernels while B fits their LDS budget).
+ * register-resident, H = 256 / 512 with B <= 32 on one persistent launch per direction -- W_hh
+ * slices held in VGPRs by H / 4 workgroups that hand h_t / dgates_t over through L2 with sharded
+ * step counters; H = 1024 (and 256 / 512 when the persistent grid cannot be resident, or with
+ * XCP_LSTM_PERSIST=0) on per-step kernels while B fits their LDS budget).
  * kernel: 0 = automatic, 1 = the generic kernels.  xcp_lstm_bwd's work: B*H + 4*H*H floats (the
  * per-step kernels' cell-gradient carry and a transposed W_hh). */
 int xcp_lstm_needs_whhT(int B, int H, int kernel);
+/* 1 if a persistent LSTM launch gave up waiting for its workgroups since the last call (its
+ * outputs are then invalid; no wave spins forever), 0 if not, -1 on a HIP error.  Synchronises the
+ * device and clears the flags. */
+int xcp_lstm_sync_error(void);
 int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
                  float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, int kernel,
                  xcp_stream_t stream);
@@ -282,6 +289,14 @@ int xcp_clock_probe(long long* out, int blocks, int iters, xcp_stream_t stream);
 /* out[i] = in[i] for n16 16-byte units (a multiple of 1024): the streaming-copy rate bench.py
  * quotes the depthwise kernels against (the guide's float4 copy) */
 int xcp_stream_copy(const void* in, void* out, long n16, xcp_stream_t stream);
+/* One-GPU stand-in for a bucket all-reduce (xcp.ddp proxy mode; no reference counterpart): `blocks`
+ * workgroups copy n16 16-byte units in -> out and hold their CUs until `ticks` of the 100 MHz real-time
+ * clock passed since each started.  rec: DEVICE uint64 [3], set to {UINT64_MAX, 0, 0} by the caller:
+ * first workgroup start, last workgroup start, last workgroup end.  xcp_stamp: *out = max(*out, now) on
+ * the same clock, as a stream marker. */
+int xcp_comm_proxy(const void* in, void* out, long n16, int blocks, long long ticks, unsigned long long* rec,
+                   xcp_stream_t stream);
+int xcp_stamp(unsigned long long* out, xcp_stream_t stream);
 
 
 #ifdef __cplusplus

@@ -88,15 +88,18 @@ SIGNATURES = {
     "xcp_lstm_needs_whhT": [I, I, I],
     "xcp_lstm_fwd": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "xcp_lstm_bwd": [P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "xcp_lstm_sync_error": [],
     "xcp_clock_probe": [P, I, I, P],
     "xcp_stream_copy": [P, P, L, P],
+    "xcp_comm_proxy": [P, P, L, I, ctypes.c_longlong, P, P],
+    "xcp_stamp": [P, P],
 }
 
 # entry points that return a size, not a status
 SIZE_QUERIES = {"xcp_permute3_blocks", "xcp_sep_fwd_parts", "xcp_gemm_tn_rows_per_split", "xcp_gemm_nt_stat_rows", "xcp_dw_bwd_chunks", "xcp_chanred_parts",
                 "xcp_colreduce_groups", "xcp_unit_bwd_rows_per_split",
                 "xcp_conv1_wgrad_parts", "xcp_conv1_wgrad_fused", "xcp_conv1_fwd_parts", "xcp_lstm_needs_whhT", "xcp_conv3x3_parts", "xcp_conv3x3_wgrad_parts",
-                "xcp_maxpool_bwd_bnred_parts"}
+                "xcp_maxpool_bwd_bnred_parts", "xcp_lstm_sync_error"}
 
 _lib = None
 

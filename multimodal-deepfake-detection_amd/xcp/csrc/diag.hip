@@ -50,9 +50,47 @@ __global__ __launch_bounds__(256) void stream_copy_kernel(const uint4* __restric
   for (int k = 0; k < 4; ++k) out[base + k * 256] = v[k];
 }
 
+// One-GPU stand-in for a bucket all-reduce (xcp.ddp proxy mode, profiles/r06_ddp_proxy.txt): `gridDim.x`
+// workgroups (RCCL's channel blocks) stream the bucket's bytes through the chip once (read + write) and
+// then hold their CUs until `ticks` of the 100 MHz real-time clock have passed since each started -- the
+// time the ring all-reduce would take on the links.  rec (uint64 [3], pre-set to {~0, 0, 0}): the first
+// workgroup start, the last workgroup start and the last workgroup end, on the same clock as
+// stamp_kernel (so a stand-in that waits for CUs the weight-gradient stream holds shows it).
+__global__ __launch_bounds__(256) void comm_proxy_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, long n16,
+                                                         long long ticks, unsigned long long* rec) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    atomicMin(rec, t0);
+    atomicMax(rec + 1, t0);
+  }
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) out[i] = in[i];
+  while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(rec + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+// one 100 MHz real-time stamp into *out (a marker on a stream, on comm_proxy_kernel's clock)
+__global__ __launch_bounds__(64) void stamp_kernel(unsigned long long* out) {
+  if (threadIdx.x == 0) atomicMax(out, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
 }  // namespace
 
 extern "C" {
+
+int xcp_comm_proxy(const void* in, void* out, long n16, int blocks, long long ticks, unsigned long long* rec,
+                   hipStream_t stream) {
+  if (n16 < 0 || blocks <= 0 || blocks > 1024 || ticks < 0 || !rec) return XCP_EINVAL;
+  hipLaunchKernelGGL(comm_proxy_kernel, dim3(blocks), dim3(256), 0, stream, reinterpret_cast<const uint4*>(in),
+                     reinterpret_cast<uint4*>(out), n16, ticks, rec);
+  return (int)hipGetLastError();
+}
+
+int xcp_stamp(unsigned long long* out, hipStream_t stream) {
+  if (!out) return XCP_EINVAL;
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, stream, out);
+  return (int)hipGetLastError();
+}
 
 int xcp_stream_copy(const void* in, void* out, long n16, hipStream_t stream) {
   if (n16 <= 0 || n16 % 1024) return XCP_EINVAL;

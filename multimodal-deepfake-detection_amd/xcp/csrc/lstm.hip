@@ -10,6 +10,10 @@
 // these kernels run the serial part: one workgroup per clip walks the T steps,
 // keeping h in LDS and reading W_hh^T (coalesced across gate lanes) from L2.
 #include "common.h"
+#include <stdlib.h>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 namespace {
 
@@ -517,6 +521,301 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Persistent recurrence for H = 256 / 512 (XceptionLSTMA: H = 512, T = 120): ONE launch per
+// direction walks all T steps, instead of the T launches of the per-step kernels above (each of
+// which re-read its W_hh slice from L2 and paid a kernel boundary per step).
+//
+// G = H / 4 workgroups of 256 threads, each owning 4 hidden units for the whole launch, with
+// their W_hh slice in VGPRs (one wave per SIMD, 128 fp32 weights per lane):
+//   forward : lane l holds W_hh[16 gate rows of its units][k = l*KL .. +KL)  (KL = H / 64)
+//   backward: lane l holds W_hh[j = l*JL .. +JL)[its 4 units]              (JL = 4H / 64)
+// Wave v handles clips 16p + 4v .. +3 (pass p = 0, 1 for B <= 32).  A step's dot products are
+// per-lane FMA chains over the lane's k (j) range; the 64 lanes' partial sums (16 rows x 4 clips
+// forward, 4 units x 4 clips backward) are combined by a reduce-scatter butterfly (each xor level
+// halves what a lane keeps), so after 6 levels lane l holds one complete (clip, row) sum
+// (forward: clip l >> 4, row l & 15 = gate * 4 + unit; backward: clip l >> 4, unit (l >> 2) & 3).
+// The cell runs on 16 lanes per wave with c (forward) / the cell-gradient carry (backward) kept
+// in a register across steps.
+// Step hand-off (guide: MI355X_MICROARCH.md "Valid forms", first table row): every store of
+// h_t (forward) / dgates_t (backward) is a 4-B sc1 store; each storing wave waits vmcnt(0),
+// the workgroup barriers, and one lane adds 1 to its shard counter (blockIdx % 8, one 128-B line
+// each, agent-scope atomic).  Before a step, wave 0 polls the 8 shards with sc1 loads until each
+// counted every one of its workgroups for the previous step, the workgroup barriers, and every
+// load of the handed-off values is a 16-B sc1 buffer load.  Counters are zeroed by the host per
+// launch; a poll that runs past ~LP_SPIN sleeps sets the error word and the workgroup leaves
+// (the results are then invalid, but no wave spins forever: e.g. if fewer than G workgroups
+// could ever be resident, which the host rules out with the occupancy query).
+constexpr int LP_U = 4;                   // hidden units per workgroup
+constexpr int LP_SHARD = 32;              // uints per shard counter (one 128-B line)
+constexpr unsigned LP_SPIN = 1u << 22;    // polls (each after s_sleep 2) before giving up
+constexpr int LP_CSP = 0x00020000;        // raw buffer descriptor word 3
+constexpr int LP_SC1 = 16;                // cache policy: sc1
+
+struct LstmSync {
+  unsigned* cnt;   // [8][LP_SHARD]
+  unsigned* err;   // set to 1 on a poll timeout
+};
+
+// wave 0 waits until every shard has `steps` arrivals from each of its workgroups; then the
+// workgroup barrier.  false (every thread) on a timeout.
+XCP_DEV bool lp_wait(const LstmSync& sy, unsigned steps) {
+  __shared__ int s_ok;
+  const int tid = threadIdx.x, lane = tid & 63, G = gridDim.x;
+  if (tid < 64) {
+    const unsigned want = steps * (unsigned)(G / 8 + ((lane & 7) < G % 8 ? 1 : 0));
+    unsigned it = 0;
+    bool ok = false;
+    while (true) {
+      const unsigned v = lane < 8 ? __hip_atomic_load(sy.cnt + lane * LP_SHARD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : want;
+      ok = __all(v >= want);
+      if (ok || ++it > LP_SPIN) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (tid == 0) {
+      s_ok = ok;
+      if (!ok) __hip_atomic_store(sy.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// every wave's sc1 stores have completed; then one arrival on this workgroup's shard
+XCP_DEV void lp_publish(const LstmSync& sy) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(sy.cnt + (blockIdx.x % 8) * LP_SHARD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+XCP_DEV void lp_st(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// reduce-scatter of v[N] over the 64 lanes: level d keeps the upper half where lane & d; after
+// log2(N) levels lane l holds index (l >> (6 - log2 N)) complete over those lanes, the remaining
+// levels sum plainly (every lane of a group ends with the same value)
+template <int N>
+XCP_DEV float lp_rscatter(float (&v)[N], int lane) {
+  int n = N;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    if (n >= 2) {
+      const bool up = lane & d;
+#pragma unroll
+      for (int c = 0; c < N / 2; ++c) {
+        if (c < n / 2) {
+          const float keep = up ? v[n / 2 + c] : v[c];
+          const float send = up ? v[c] : v[n / 2 + c];
+          v[c] = keep + __shfl_xor(send, d, 64);
+        }
+      }
+      n /= 2;
+    } else {
+      v[0] += __shfl_xor(v[0], d, 64);
+    }
+  }
+  return v[0];
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ xproj,
+                                                               const float* __restrict__ whh,
+                                                               const float* __restrict__ bih,
+                                                               const float* __restrict__ bhh, float* out,
+                                                               float* __restrict__ hprev, float* __restrict__ cst,
+                                                               float* __restrict__ gates, float* __restrict__ hn,
+                                                               float* __restrict__ cn, int B, int T, LstmSync sy) {
+  constexpr int KL = H / 64, R = 4 * LP_U, G4 = 4 * H;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int u0 = blockIdx.x * LP_U, k0 = lane * KL;
+  float w[R][KL];
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+    for (int i = 0; i < KL; i += 4) {
+      const float4 v4 = *reinterpret_cast<const float4*>(whh + (long)((rr / LP_U) * H + u0 + rr % LP_U) * H + k0 + i);
+      w[rr][i] = v4.x; w[rr][i + 1] = v4.y; w[rr][i + 2] = v4.z; w[rr][i + 3] = v4.w;
+    }
+  // cell lanes: lane = c * 16 + u (gate 0 of unit u of clip c); the other gates at lane + 4q
+  const bool cell = (lane & 12) == 0;
+  const int cu = lane & 3, k = u0 + cu;
+  const int npass = (B + 15) / 16;
+  float cstate[2] = {0.f, 0.f}, hst[2] = {0.f, 0.f}, xq[2][4];
+  const __amdgpu_buffer_rsrc_t rO = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7fffffff, LP_CSP);
+  auto clip = [&](int p, int c) { return p * 16 + wv * 4 + c; };
+  auto load_xp = [&](int t) {   // x W_ih^T of step t for this lane's cell (prefetched a step ahead)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int b = clip(p, lane >> 4);
+      const bool ok = cell && p < npass && b < B && t < T;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xq[p][q] = ok ? xproj[((long)b * T + t) * G4 + q * H + k] : 0.f;
+    }
+  };
+  load_xp(0);
+  for (int t = 0; t < T; ++t) {
+    float xc[2][4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xc[p][q] = xq[p][q];
+    load_xp(t + 1);
+    if (t > 0 && !lp_wait(sy, (unsigned)t)) return;
+    for (int p = 0; p < npass; ++p) {
+      float part[4 * R];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int b = clip(p, c);
+        float hv[KL];
+        if (t > 0 && b < B) {   // (wave-uniform) h_{t-1}[b][k0 .. k0+KL): 16-B sc1 loads
+#pragma unroll
+          for (int i = 0; i < KL; i += 4) {
+            const float4 v4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                rO, (int)((((long)b * T + t - 1) * H + k0 + i) * 4), 0, LP_SC1));
+            hv[i] = v4.x; hv[i + 1] = v4.y; hv[i + 2] = v4.z; hv[i + 3] = v4.w;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < KL; ++i) hv[i] = 0.f;
+        }
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+          float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+          for (int i = 0; i < KL; i += 2) {
+            a0 = fmaf(w[rr][i], hv[i], a0);
+            a1 = fmaf(w[rr][i + 1], hv[i + 1], a1);
+          }
+          part[c * R + rr] = a0 + a1;
+        }
+      }
+      const float rec = lp_rscatter(part, lane);   // clip lane >> 4, row lane & 15
+      float pre[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pre[q] = __shfl(rec, (lane & ~15) | (q * 4 + cu), 64);
+      const int b = clip(p, lane >> 4);
+      if (cell && b < B) {
+        float g[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[q] = ((pre[q] + xc[p][q]) + bih[q * H + k]) + bhh[q * H + k];
+        const float ig = sigm(g[0]), fg = sigm(g[1]), gg = tanhf(g[2]), og = sigm(g[3]);
+        const float c = fmaf(fg, cstate[p], ig * gg);
+        const float h = og * tanhf(c);
+        const long ob = ((long)b * T + t) * H;
+        float* gt = gates + ((long)b * T + t) * G4;
+        gt[k] = ig; gt[H + k] = fg; gt[2 * H + k] = gg; gt[3 * H + k] = og;
+        hprev[ob + k] = hst[p];
+        cst[ob + k] = c;
+        lp_st(out + ob + k, h);
+        if (t == T - 1) {
+          hn[(long)b * H + k] = h;
+          cn[(long)b * H + k] = c;
+        }
+        cstate[p] = c;
+        hst[p] = h;
+      }
+    }
+    if (t + 1 < T) lp_publish(sy);
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const float* __restrict__ dout,
+                                                               const float* __restrict__ dhn,
+                                                               const float* __restrict__ dcn,
+                                                               const float* __restrict__ whh,
+                                                               const float* __restrict__ cst,
+                                                               const float* __restrict__ gates, float* dgates, int B,
+                                                               int T, LstmSync sy) {
+  constexpr int JL = 4 * H / 64, G4 = 4 * H;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int u0 = blockIdx.x * LP_U, j0 = lane * JL;
+  float w[JL][LP_U];
+#pragma unroll
+  for (int i = 0; i < JL; ++i) {
+    const float4 v4 = *reinterpret_cast<const float4*>(whh + (long)(j0 + i) * H + u0);
+    w[i][0] = v4.x; w[i][1] = v4.y; w[i][2] = v4.z; w[i][3] = v4.w;
+  }
+  // cell lanes: lane = c * 16 + u * 4 (clip c, unit u)
+  const bool cell = (lane & 3) == 0;
+  const int cu = (lane >> 2) & 3, k = u0 + cu;
+  const int npass = (B + 15) / 16;
+  float carry[2] = {0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(dgates, (short)0, 0x7fffffff, LP_CSP);
+  auto clip = [&](int p, int c) { return p * 16 + wv * 4 + c; };
+  for (int t = T - 1; t >= 0; --t) {
+    const bool last = t == T - 1;
+    // this step's cell operands (independent of the recurrence: loaded before the wait)
+    float vc[2], vcp[2], vg[2][4], vdo[2], vhn[2], vcn[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int b = clip(p, lane >> 4);
+      const bool ok = cell && p < npass && b < B;
+      const long ob = ((long)b * T + t) * H + k;
+      vc[p] = ok ? cst[ob] : 0.f;
+      vcp[p] = ok && t > 0 ? cst[ob - H] : 0.f;
+      vdo[p] = ok && dout ? dout[ob] : 0.f;
+      vhn[p] = ok && last && dhn ? dhn[(long)b * H + k] : 0.f;
+      vcn[p] = ok && last && dcn ? dcn[(long)b * H + k] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vg[p][q] = ok ? gates[((long)b * T + t) * G4 + q * H + k] : 0.f;
+    }
+    if (!last && !lp_wait(sy, (unsigned)(T - 1 - t))) return;
+    for (int p = 0; p < npass; ++p) {
+      float part[4 * LP_U];
+#pragma unroll
+      for (int q = 0; q < 4 * LP_U; ++q) part[q] = 0.f;
+      if (!last) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int b = clip(p, c);
+          if (b < B) {   // (wave-uniform) dgates_{t+1}[b][j0 .. j0+JL): 16-B sc1 loads
+            float dg[JL];
+#pragma unroll
+            for (int i = 0; i < JL; i += 4) {
+              const float4 v4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                  rG, (int)((((long)b * T + t + 1) * G4 + j0 + i) * 4), 0, LP_SC1));
+              dg[i] = v4.x; dg[i + 1] = v4.y; dg[i + 2] = v4.z; dg[i + 3] = v4.w;
+            }
+#pragma unroll
+            for (int u = 0; u < LP_U; ++u) {
+              float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+              for (int i = 0; i < JL; i += 2) {
+                a0 = fmaf(dg[i], w[i][u], a0);
+                a1 = fmaf(dg[i + 1], w[i + 1][u], a1);
+              }
+              part[c * LP_U + u] = a0 + a1;
+            }
+          }
+        }
+      }
+      const float rec = lp_rscatter(part, lane);   // clip lane >> 4, unit (lane >> 2) & 3
+      const int b = clip(p, lane >> 4);
+      if (cell && b < B) {
+        const float ig = vg[p][0], fg = vg[p][1], gg = vg[p][2], og = vg[p][3];
+        const float dhr = !last ? rec : vhn[p];
+        const float dcr = !last ? carry[p] : vcn[p];
+        const float dh = dhr + vdo[p];
+        const float tc = tanhf(vc[p]);
+        const float dO = dh * tc;
+        const float dc = dcr + dh * og * (1.f - tc * tc);
+        const float dI = dc * gg, dG = dc * ig, dF = dc * vcp[p];
+        carry[p] = dc * fg;
+        float* dgo = dgates + ((long)b * T + t) * G4;
+        lp_st(dgo + k, dI * ig * (1.f - ig));
+        lp_st(dgo + H + k, dF * fg * (1.f - fg));
+        lp_st(dgo + 2 * H + k, dG * (1.f - gg * gg));
+        lp_st(dgo + 3 * H + k, dO * og * (1.f - og));
+      }
+    }
+    if (t > 0) lp_publish(sy);
+  }
+}
+
+__device__ unsigned g_lstm_sync[64][8 * LP_SHARD + 32];   // per (device, stream) slot: shards, error word
+
 // Kernel choice (`kernel` argument: 0 = auto, 1 = the generic kernels, used by tests to pin
 // them at shapes the specialised kernels also cover).
 // register-resident: one 1024-thread workgroup per clip, W_hh slice in VGPRs
@@ -529,13 +828,85 @@ bool lstm_step(int B, int H, int kernel) {
          fwd_lds <= 65536 && bwd_lds <= 65536;
 }
 
+// persistent kernels (XCP_LSTM_PERSIST=0: the per-step kernels; read per call): H = 256 / 512, B <= 32,
+// and all G = H / 4 workgroups resident at once by the occupancy query
+bool lstm_persist_env() {
+  const char* e = getenv("XCP_LSTM_PERSIST");
+  return e && e[0] == '1';
+}
+template <typename K>
+bool lp_resident(K kern, int G) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, 0) != hipSuccess) return false;
+  return (long)per * cus >= G;
+}
+bool lstm_persist(int B, int H, int kernel, bool fwd) {
+  if (kernel != 0 || B > 32 || !(H == 256 || H == 512) || !lstm_persist_env()) return false;
+  static int ok[2][2] = {{-1, -1}, {-1, -1}};   // [fwd][H == 512]
+  int& v = ok[fwd][H == 512];
+  if (v < 0) {
+    if (fwd) v = H == 512 ? lp_resident(lstm_fwd_persist_kernel<512>, H / LP_U) : lp_resident(lstm_fwd_persist_kernel<256>, H / LP_U);
+    else v = H == 512 ? lp_resident(lstm_bwd_persist_kernel<512>, H / LP_U) : lp_resident(lstm_bwd_persist_kernel<256>, H / LP_U);
+  }
+  return v == 1;
+}
+
+// the sync words of (device, stream), zeroed on the stream before each persistent launch
+int lp_sync(hipStream_t st, LstmSync& sy) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, hipStream_t>> slots;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return XCP_EINVAL;
+  int slot = -1;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (size_t i = 0; i < slots.size(); ++i)
+      if (slots[i].first == dev && slots[i].second == st) slot = (int)i;
+    if (slot < 0) {
+      if (slots.size() >= 64) return XCP_EUNSUPPORTED;
+      slots.emplace_back(dev, st);
+      slot = (int)slots.size() - 1;
+    }
+  }
+  void* base = nullptr;
+  if (hipGetSymbolAddress(&base, HIP_SYMBOL(g_lstm_sync)) != hipSuccess) return XCP_EINVAL;
+  unsigned* words = reinterpret_cast<unsigned*>(base) + (long)slot * (8 * LP_SHARD + 32);
+  if (hipMemsetAsync(words, 0, 8 * LP_SHARD * sizeof(unsigned), st) != hipSuccess) return XCP_EINVAL;
+  sy.cnt = words;
+  sy.err = words + 8 * LP_SHARD;
+  return XCP_OK;
+}
+
 }  // namespace
 
 
 extern "C" {
 
+// 1 when a persistent LSTM launch on any stream gave up waiting for its workgroups (its results are
+// invalid); clears the flags.  Synchronises the device.
+int xcp_lstm_sync_error() {
+  void* base = nullptr;
+  if (hipDeviceSynchronize() != hipSuccess || hipGetSymbolAddress(&base, HIP_SYMBOL(g_lstm_sync)) != hipSuccess)
+    return -1;
+  static unsigned host[64][8 * LP_SHARD + 32];
+  if (hipMemcpy(host, base, sizeof(host), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  int any = 0;
+  for (int i = 0; i < 64; ++i)
+    if (host[i][8 * LP_SHARD]) {
+      any = 1;
+      unsigned* w = reinterpret_cast<unsigned*>(base) + (long)i * (8 * LP_SHARD + 32) + 8 * LP_SHARD;
+      if (hipMemset(w, 0, sizeof(unsigned)) != hipSuccess) return -1;
+    }
+  return any;
+}
+
 // 1 when xcp_lstm_fwd (same B, H, kernel) runs the generic kernel, which reads the transposed W_hh
-int xcp_lstm_needs_whhT(int B, int H, int kernel) { return lstm_reg(H, kernel) || lstm_step(B, H, kernel) ? 0 : 1; }
+int xcp_lstm_needs_whhT(int B, int H, int kernel) {
+  const bool persist = kernel == 0 && B <= 32 && (H == 256 || H == 512);   // (the persistent kernels read W_hh)
+  return lstm_reg(H, kernel) || lstm_step(B, H, kernel) || persist ? 0 : 1;
+}
 
 int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
                  float* hprev, float* cst, float* gates, float* hn, float* cn, int B, int T, int H, int kernel,
@@ -549,6 +920,18 @@ int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const 
     else
       hipLaunchKernelGGL(lstm_fwd_reg_kernel<64>, dim3(B), dim3(1024), 0, st, xproj, whh, bih, bhh, out, hprev, cst,
                          gates, hn, cn, T);
+    return (int)hipGetLastError();
+  }
+  if (lstm_persist(B, H, kernel, true)) {
+    LstmSync sy;
+    const int rc = lp_sync(st, sy);
+    if (rc != XCP_OK) return rc;
+    if (H == 512)
+      hipLaunchKernelGGL(lstm_fwd_persist_kernel<512>, dim3(H / LP_U), dim3(256), 0, st, xproj, whh, bih, bhh, out, hprev,
+                         cst, gates, hn, cn, B, T, sy);
+    else
+      hipLaunchKernelGGL(lstm_fwd_persist_kernel<256>, dim3(H / LP_U), dim3(256), 0, st, xproj, whh, bih, bhh, out, hprev,
+                         cst, gates, hn, cn, B, T, sy);
     return (int)hipGetLastError();
   }
   if (lstm_step(B, H, kernel)) {
@@ -577,6 +960,18 @@ int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const fl
                  const float* gates, float* dgates, float* work, int B, int T, int H, int kernel, hipStream_t st) {
   if (B <= 0 || T <= 0) return XCP_OK;
   if (kernel < 0 || kernel > 1) return XCP_EINVAL;
+  if (lstm_persist(B, H, kernel, false)) {
+    LstmSync sy;
+    const int rc = lp_sync(st, sy);
+    if (rc != XCP_OK) return rc;
+    if (H == 512)
+      hipLaunchKernelGGL(lstm_bwd_persist_kernel<512>, dim3(H / LP_U), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates,
+                         dgates, B, T, sy);
+    else
+      hipLaunchKernelGGL(lstm_bwd_persist_kernel<256>, dim3(H / LP_U), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates,
+                         dgates, B, T, sy);
+    return (int)hipGetLastError();
+  }
   if (lstm_step(B, H, kernel)) {
     if (!work) return XCP_EINVAL;
     float* whhT = work + (long)B * H;

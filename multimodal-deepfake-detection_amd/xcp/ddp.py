@@ -66,7 +66,14 @@ if DDP_LAUNCH not in ("side", "comm", "main"):
 
 
 class GradBuckets:
-    def __init__(self, params, bucket_bytes=25 << 20, world=None, module=None):
+    def __init__(self, params, bucket_bytes=25 << 20, world=None, module=None, proxy=None):
+        """proxy (one GPU, world size 1 only): {"world": G, "busbw": GB/s, "blocks": n} launches, at each
+        bucket-ready point and from the same stream a real all-reduce would start on, a stand-in of
+        RCCL's footprint (xcp_comm_proxy: n workgroups stream the bucket once and hold their CUs for
+        2 (G - 1) / G x bytes / busbw) and stamps the ready point, each stand-in's first / last
+        workgroup start and end and the backward's end on one clock (proxy_report()).  It measures
+        whether the collectives would start while the weight-gradient stream holds the CUs and how
+        much of them would be left after the backward (profiles/r06_ddp_proxy.txt)."""
         self.params = list(params)
         if not self.params:
             raise ValueError("GradBuckets: no parameters")
@@ -84,7 +91,8 @@ class GradBuckets:
             self.views[p] = (off, p.numel())
             self._slot[p] = slot(p.numel())
             off += self._slot[p]
-        self.overlap = self.world > 1
+        self.proxy = dict(proxy) if proxy and self.world == 1 and dev.type == "cuda" else None
+        self.overlap = self.world > 1 or self.proxy is not None
         self.sync = True   # False: gradient accumulation micro-batch, no all-reduce launched
         self._active_key = None
         self._pending = []
@@ -95,6 +103,9 @@ class GradBuckets:
         self.avg = dist.is_initialized() and dist.get_backend() == "nccl"
         if module is not None:
             self.attach(module)
+        if self.proxy is not None:
+            self._prx_step = -1
+            self._prx_scratch = torch.empty_like(self.flat)
         self.zero()
 
     # ------------------------------------------------------------ layout
@@ -150,6 +161,15 @@ class GradBuckets:
         self._left = [len(ps) for _, _, ps in self.buckets]
         self._done = set()
         self._pending = []
+        if self.proxy is not None:   # a ring of 64 steps x (buckets + 1) x {ready, first start, last start, end}
+            nb = len(self.buckets)
+            if getattr(self, "_prx_rec", None) is None or self._prx_rec.shape[1] != nb + 1:
+                self._prx_rec = torch.zeros(64, nb + 1, 4, dtype=torch.int64, device=self.flat.device)
+                self._prx_step = -1
+            self._prx_step += 1
+            r = self._prx_rec[self._prx_step % 64]
+            r.zero_()
+            r[:, 1] = -1   # (UINT64_MAX: atomicMin target)
 
     def _is_view(self, p):
         o, _ = self.views[p]
@@ -179,11 +199,27 @@ class GradBuckets:
             v.copy_(p.grad)
         p.grad = v
 
+    def _prx_rec_row(self, i):
+        return self._prx_rec[self._prx_step % 64, i]
+
     def _launch(self, bi):
         a, b, ps = self.buckets[bi]
         for p in ps:   # a gradient autograd created after zero_grad(set_to_none) joins the flat buffer
             if not self._is_view(p):
                 self._adopt(p)
+        if self.proxy is not None:
+            from xcp import _lib, ops
+            G = self.proxy.get("world", 8)
+            bus = 2.0 * (G - 1) / G * 4 * (b - a)
+            ticks = int(bus / (self.proxy.get("busbw", 300.0) * 1e9) * 1e8)
+            row = self._prx_rec_row(bi)
+            n16 = 4 * (b - a) // 16
+            _lib.call("xcp_comm_proxy", self.flat.data_ptr() + 4 * a, self._prx_scratch.data_ptr() + 4 * a, n16,
+                      int(self.proxy.get("blocks", 32)), ticks, row.data_ptr() + 8, ops.stream())
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending.append(ev)
+            return
         op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
         self._pending.append(dist.all_reduce(self.flat[a:b], op=op, async_op=True))
 
@@ -237,6 +273,10 @@ class GradBuckets:
             self._left[bi] -= 1
             if self._left[bi] == 0:
                 full.append(bi)
+        if self.proxy is not None and full:
+            from xcp import _lib, ops
+            for bi in full:   # the ready point, on the current (main) stream
+                _lib.call("xcp_stamp", self._prx_rec_row(bi).data_ptr(), ops.stream())
         self._launch_from_comm(full, side_stream)
 
     def _on_grad(self, p):
@@ -245,6 +285,18 @@ class GradBuckets:
     def allreduce(self):
         """Finish the gradient mean across ranks (no-op at world size 1).  Buckets that did not
         complete during backward (parameters without a gradient this step) are reduced here."""
+        if self.proxy is not None:
+            from xcp import _lib, ops
+            _lib.call("xcp_stamp", self._prx_rec_row(len(self.buckets)).data_ptr(), ops.stream())   # backward end
+            rest = [bi for bi in range(len(self.buckets)) if self._left[bi] != 0]
+            for bi in rest:
+                self._left[bi] = 0
+            self._launch_from_comm(rest)
+            cur = torch.cuda.current_stream(self.flat.device)
+            for ev in self._pending:   # (as w.wait() on a collective)
+                cur.wait_event(ev)
+            self._pending = []
+            return
         if self.world <= 1:
             return
         rest = []
@@ -259,6 +311,33 @@ class GradBuckets:
         if not self.avg:
             for a, b, _ in self.buckets:
                 self.flat[a:b].mul_(1.0 / self.world)
+
+
+def proxy_report(buckets, steps):
+    """Per-bucket timings of the last ``steps`` steps of a proxy-mode GradBuckets (synchronises), in
+    microseconds: ready -> first stand-in workgroup start ("start_delay"), first -> last workgroup
+    start ("cu_wait"), stand-in duration, and the backward end -> last stand-in end ("exposed")."""
+    import torch as _t
+    _t.cuda.synchronize()
+    n = min(steps, 64, buckets._prx_step + 1)
+    rows = [buckets._prx_rec[(buckets._prx_step - i) % 64].cpu() for i in range(n)]
+    nb = len(buckets.buckets)
+    us = lambda t: t / 100.0   # noqa: E731  (100 MHz ticks)
+    per = []
+    for bi in range(nb):
+        a, b, _ = buckets.buckets[bi]
+        rd = [float(us(r[bi, 1] - r[bi, 0])) for r in rows]
+        cw = [float(us(r[bi, 2] - r[bi, 1])) for r in rows]
+        du = [float(us(r[bi, 3] - r[bi, 1])) for r in rows]
+        per.append({"bucket_mb": round(4 * (b - a) / 1e6, 2), "start_delay_us": round(sum(rd) / n, 1),
+                    "start_delay_max_us": round(max(rd), 1), "cu_wait_us": round(sum(cw) / n, 1),
+                    "duration_us": round(sum(du) / n, 1)})
+    exp = [float(us(max(int(r[bi, 3]) for bi in range(nb)) - r[nb, 0])) for r in rows]
+    first = [float(us(min(int(r[bi, 1]) for bi in range(nb)) - r[nb, 0])) for r in rows]
+    return {"steps": n, "world": buckets.proxy.get("world", 8), "busbw_gbs": buckets.proxy.get("busbw", 300.0),
+            "blocks": buckets.proxy.get("blocks", 32), "buckets": per,
+            "first_start_vs_backward_end_us": round(sum(first) / n, 1),
+            "exposed_after_backward_us": round(sum(exp) / n, 1), "exposed_max_us": round(max(exp), 1)}
 
 
 def _backbones(module):

@@ -592,6 +592,12 @@ def lstm_fwd(xproj, whh, whhT, bih, bhh, out, hprev, cst, gates, hn, cn, B, T, H
               _p(cn), B, T, H, kernel, stream())
 
 
+def lstm_sync_error():
+    """1 if a persistent LSTM launch gave up waiting for its workgroups since the last call (its
+    outputs are invalid then), else 0; synchronises the device and clears the flags."""
+    return _lib.call("xcp_lstm_sync_error")
+
+
 def lstm_bwd(dout, dhn, dcn, whh, cst, gates, dgates, B, T, H, kernel=0):
     # per-step kernels: cell-gradient carry [B][H] + W_hh^T [H][4H]
     work = torch.empty(B * H + 4 * H * H, device=whh.device, dtype=torch.float32)

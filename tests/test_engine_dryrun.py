@@ -196,7 +196,7 @@ def test_header_matches_binding():
     decls = dict(re.findall(r"int\s+(xcp_\w+)\(([^;]*)\);", hdr, re.S))
     assert set(decls) == set(_lib.SIGNATURES)
     for name, args in decls.items():
-        n = len([a for a in args.split(",") if a.strip()])
+        n = len([a for a in args.split(",") if a.strip() and a.strip() != "void"])
         assert n == len(_lib.SIGNATURES[name]), name
 
 

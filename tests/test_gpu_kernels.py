@@ -783,20 +783,22 @@ def test_lstm_module_vs_oracle(ops, gpu, golden, H, T, kernel):
             np.testing.assert_allclose(prm.grad.cpu().numpy(), ref, rtol=1e-3, atol=1e-5)
 
 
-@pytest.mark.parametrize("kernel", ["register", "generic"])
-def test_lstm_t120_vs_reference(ops, gpu, golden, kernel):
+@pytest.mark.parametrize("kernel", ["persistent", "step", "generic"])
+def test_lstm_t120_vs_reference(ops, gpu, golden, monkeypatch, kernel):
     """XceptionLSTMA's own recurrence -- nn.LSTM(2048, 512) over T = 120 MFCC frames
-    (XceptionLSTMA.py:14-19, audio_dataloader.py:20,39) -- through both kernel families (0: the
-    per-step kernels H >= 256 use, 120 launches each way carrying h and c; 1: generic) against the
-    reference's own values (lstm_t120.npz): out / h_n / c_n at 1e-4, every time step's output norm
-    at 1e-4 (the error must not grow over the 120 steps), dx and the parameter gradients at 1e-3."""
+    (XceptionLSTMA.py:14-19, audio_dataloader.py:20,39) -- through the three kernel families H = 512
+    can take (persistent: one launch each way, the default; step: XCP_LSTM_PERSIST=0, 120 launches
+    each way carrying h and c; generic) against the reference's own values (lstm_t120.npz): out /
+    h_n / c_n at 1e-4, every time step's output norm at 1e-4 (the error must not grow over the 120
+    steps), dx and the parameter gradients at 1e-3."""
     import numpy as np
     from xcp.lstm import LSTM
     g = golden("lstm_t120.npz")
     B, T, H = int(g["B"]), int(g["T"]), int(g["H"])
+    monkeypatch.setenv("XCP_LSTM_PERSIST", "0" if kernel == "step" else "1")
     torch.manual_seed(0)
     lstm = LSTM(2048, H, 1, batch_first=True).to(gpu)
-    lstm.xcp_kernel = 0 if kernel == "register" else 1
+    lstm.xcp_kernel = 1 if kernel == "generic" else 0
     x = torch.randn((B, T, 2048), generator=torch.Generator().manual_seed(555)).to(gpu).requires_grad_(True)
     o, (h, c) = lstm(x)
     oc = o.detach().double().cpu()
@@ -818,6 +820,40 @@ def test_lstm_t120_vs_reference(ops, gpu, golden, kernel):
                                    atol=1e-5, err_msg=n)
         if f"gradfull/{n}" in g:
             np.testing.assert_allclose(gr.numpy(), g[f"gradfull/{n}"], rtol=1e-3, atol=1e-5, err_msg=n)
+    assert ops.lstm_sync_error() == 0
+
+
+@pytest.mark.parametrize("B,T,H", [(16, 120, 512), (20, 37, 512), (3, 5, 256), (32, 9, 256)])
+def test_lstm_persistent_vs_step_kernels(ops, gpu, monkeypatch, B, T, H):
+    """The persistent recurrence (one launch per direction, W_hh in VGPRs, step hand-off through
+    sharded counters) against the per-step kernels on the same inputs, with every optional operand
+    (dout, dh_n, dc_n): outputs, states, gates and the pre-activation gradients within 1e-5 relative
+    (only the summation order of the W_hh dot products differs).  B = 20 / 32 take the second
+    clip pass, B = 3 a partial clip group; no launch may report a poll timeout."""
+    G4 = 4 * H
+    gen = torch.Generator(device=gpu).manual_seed(B * 1000 + T + H)
+    xp = torch.randn(B, T, G4, device=gpu, generator=gen)
+    whh = torch.randn(G4, H, device=gpu, generator=gen) / H ** 0.5
+    bih, bhh = torch.randn(G4, device=gpu, generator=gen) * 0.1, torch.randn(G4, device=gpu, generator=gen) * 0.1
+    dout = torch.randn(B, T, H, device=gpu, generator=gen)
+    dhn, dcn = torch.randn(B, H, device=gpu, generator=gen), torch.randn(B, H, device=gpu, generator=gen)
+    res = {}
+    for form in ("0", "1"):
+        monkeypatch.setenv("XCP_LSTM_PERSIST", form)
+        f = {k: torch.full((B, T, n), float("nan"), device=gpu) for k, n in
+             (("out", H), ("hprev", H), ("cst", H), ("gates", G4))}
+        hn, cn = torch.empty(B, H, device=gpu), torch.empty(B, H, device=gpu)
+        ops.lstm_fwd(xp, whh, None, bih, bhh, f["out"], f["hprev"], f["cst"], f["gates"], hn, cn, B, T, H)
+        dg = torch.full((B, T, G4), float("nan"), device=gpu)
+        ops.lstm_bwd(dout, dhn, dcn, whh, f["cst"], f["gates"], dg, B, T, H)
+        torch.cuda.synchronize()
+        res[form] = dict(f, hn=hn, cn=cn, dg=dg)
+    assert ops.lstm_sync_error() == 0
+    for k, want in res["0"].items():
+        got = res["1"][k]
+        assert not torch.isnan(got).any(), k
+        err = ((got - want).norm() / want.norm()).item()
+        assert err < 1e-5, (k, err)
 
 
 @pytest.mark.parametrize("kernel", ["register", "generic"])
