@@ -268,8 +268,9 @@ int xcp_focal_ce(const float* Z, const long long* labels, const float* weights, 
  * slices held in VGPRs by H / 4 workgroups that hand h_t / dgates_t over through L2 with sharded
  * step counters; H = 1024 (and 256 / 512 when the persistent grid cannot be resident, or with
  * XCP_LSTM_PERSIST=0) on per-step kernels while B fits their LDS budget).
- * kernel: 0 = automatic, 1 = the generic kernels.  xcp_lstm_bwd's work: B*H + 4*H*H floats (the
- * per-step kernels' cell-gradient carry and a transposed W_hh). */
+ * kernel: 0 = automatic, 1 = the generic kernels.  xcp_lstm_bwd's work: max(B*H + 4*H*H, B*H*H/2)
+ * floats (the per-step kernels' cell-gradient carry and a transposed W_hh; the persistent kernel's
+ * double-buffered dh partials [2][H/4][B][H]). */
 int xcp_lstm_needs_whhT(int B, int H, int kernel);
 /* 1 if a persistent LSTM launch gave up waiting for its workgroups since the last call (its
  * outputs are then invalid; no wave spins forever), 0 if not, -1 on a HIP error.  Synchronises the

@@ -1508,6 +1508,159 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
   }
 }
 
+// Weight-gradient kernel with ONE MFMA phase of 32 per 32-row step and the fill four steps ahead
+// (gemm_tn256q_kernel; XCP_TN_LOOP=2, A/B against gemm_tn256_kernel's two 16-MFMA phases).  Per step
+// a wave reads all its fragments (X: 4 k-frags, G: 8 n-frags = 24 ds_read_b64_tr_b16) and issues
+// step s+4 into the slot step s-1 left (both wave groups finished reading it two intervals earlier),
+// waits lgkmcnt(0), and its 32 MFMAs run in the next interval beside the other group's reads: two
+// barriers per step instead of four, and 4 x 32 KB of the 5-slot ring in flight instead of 3.
+XCP_DEV void tn_vm_wait(int n) {
+  if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool BUF>
+__global__ __launch_bounds__(512) void gemm_tn256q_kernel(TNArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[T_RING * T_STEP];
+  const int gridN = (a.N + 255) / 256, gridK = (a.K + 255) / 256;
+  const int tiles = gridN * gridK;
+  int sp, t;
+  if (a.xalign) {
+    const int q = blockIdx.x >> 3;
+    sp = (q / tiles) * 8 + (blockIdx.x & 7);
+    t = q % tiles;
+    if (sp >= a.S) return;
+  } else {
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    sp = id / tiles;
+    t = id % tiles;
+  }
+  const int n0 = (t / gridK) * 256, k0 = (t % gridK) * 256;
+  const int mbeg = sp * a.rows_per_split;
+  const int mend = min(a.M, mbeg + a.rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const bf16* G = reinterpret_cast<const bf16*>(a.G);
+  const bf16* X = reinterpret_cast<const bf16*>(a.X);
+  const int pc = lane & 31;
+  int rr[2], lc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    rr[i] = 4 * w + 2 * i + (lane >> 5);
+    lc[i] = pc ^ ((rr[i] & 7) << 1);
+  }
+  const void* zero = g_zero16;
+  asm volatile("" : "+v"(zero));
+  auto glds = [](const void* p, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)p,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.G), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.X), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  auto issue = [&](bool isG, int st, int sl) {   // 2 instructions
+    char* d = smem + sl * T_STEP + (isG ? 0 : T_HALF);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = mbeg + st * 32 + rr[i];
+      const int col = (isG ? n0 : k0) + lc[i] * 8;
+      const bool ok = m < mend && col < (isG ? a.N : a.K);
+      char* dst = d + (4 * w + 2 * i) * 512;
+      if constexpr (BUF) {
+        const unsigned o = ok ? (unsigned)(((long)m * (isG ? a.ldg : a.ldx) + col) * 2) : BUF_OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(isG ? rG : rX, (__attribute__((address_space(3))) void*)dst, 16, o,
+                                                 0, 0, 0);
+      } else {
+        const void* src = ok ? (isG ? (const void*)(G + (long)m * a.ldg + col)
+                                    : (const void*)(X + (long)m * a.ldx + col))
+                             : zero;
+        glds(src, dst);
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ns = (mend - mbeg + 31) / 32;
+  // prologue: steps 0..3 in flight, step 0 retired
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+    if (st < ns) {
+      issue(true, st, st);
+      issue(false, st, st);
+    }
+  tn_vm_wait(4 * (min(ns, 4) - 1));
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int q4 = fr >> 2, p4 = fr & 3;
+  auto frag = [&](const char* slab, int cb, u64 (&r)[2]) {
+    const int m0r = 4 * fg + q4;
+    const int col = cb + 4 * p4;
+    r[0] = ds_read_tr_asm(slab + tswz(m0r, col));
+    r[1] = ds_read_tr_asm(slab + tswz(m0r + 16, col));
+  };
+  auto b8 = [](const u64 (&r)[2]) { return __builtin_bit_cast(bf16x8, u64x2{r[0], r[1]}); };
+  u64 gr[8][2], xr[4][2];
+  int slot = 0, pslot = 4;   // ring slots of step s and of step s + 4
+  for (int s = 0; s < ns; ++s) {
+    const char* sg = smem + slot * T_STEP;
+    const char* sx = sg + T_HALF;
+    // R: every fragment of the step, step s+4's fill
+#pragma unroll
+    for (int j = 0; j < 4; ++j) frag(sx, wc * 64 + j * 16, xr[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) frag(sg, wr * 128 + i * 16, gr[i]);
+    if (s + 4 < ns) {
+      issue(true, s + 4, pslot);
+      issue(false, s + 4, pslot);
+    }
+    lds_fence(xr[0], xr[1], xr[2], xr[3]);
+    lds_pin(gr[0], gr[1], gr[2], gr[3]);
+    lds_pin(gr[4], gr[5], gr[6], gr[7]);
+    // step s+1 landed (this wave's part): after it, steps s+2 .. s+4 (4 instructions each, if issued)
+    const int younger = 4 * (min(ns - 1, s + 4) - (s + 1));
+    if (wr == 1 && s + 1 < ns) tn_vm_wait(younger);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    // M: 32 MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b8(xr[j]), b8(gr[i]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 0 && s + 1 < ns) tn_vm_wait(younger);
+    __builtin_amdgcn_s_barrier();
+    slot = slot == T_RING - 1 ? 0 : slot + 1;
+    pslot = pslot == T_RING - 1 ? 0 : pslot + 1;
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();
+
+  float* P = a.P + (long)sp * a.N * a.K;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = n0 + wr * 128 + i * 16 + fr;
+    if (n >= a.N) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wc * 64 + j * 16 + 4 * fg;
+      if (k < a.K) *reinterpret_cast<f32x4*>(P + (long)n * a.K + k) = acc[i][j];
+    }
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -1527,6 +1680,12 @@ bool tn_xcd_splits() {   // XCP_TN_XCD_SPLITS=1 (A/B; measured -0.3 % in the ste
     return e && e[0] == '1';
   }();
   return v;
+}
+// XCP_TN_LOOP=2: the weight-gradient kernel with one 32-MFMA phase per step and the fill 4 steps ahead
+// (gemm_tn256q_kernel; read per call; A/B)
+bool tn_loop2() {
+  const char* e = getenv("XCP_TN_LOOP");
+  return e && e[0] == '2';
 }
 // XCP_TN_XCD_ALIGN=1: whole splits per XCD for outputs of at most 32 tiles (read per call; A/B)
 bool tn_xcd_align() {
@@ -1758,7 +1917,12 @@ int xcp_gemm_tn(int dtype, const void* G, long ldg, const void* X, long ldx, flo
     a.xalign = tiles <= 32 && S >= 2 && tn_xcd_align();
     const dim3 grid(a.xalign ? 8 * xcp_cdiv(S, 8) * tiles : tiles * S);
     const bool buf = ((long)(M - 1) * ldg + N) * 2 <= BUF_LIMIT && ((long)(M - 1) * ldx + K) * 2 <= BUF_LIMIT;
-    if (buf)
+    if (tn_loop2()) {
+      if (buf)
+        hipLaunchKernelGGL(gemm_tn256q_kernel<true>, grid, dim3(512), 0, stream, a);
+      else
+        hipLaunchKernelGGL(gemm_tn256q_kernel<false>, grid, dim3(512), 0, stream, a);
+    } else if (buf)
       hipLaunchKernelGGL(gemm_tn256_kernel<true>, grid, dim3(512), 0, stream, a);
     else
       hipLaunchKernelGGL(gemm_tn256_kernel<false>, grid, dim3(512), 0, stream, a);

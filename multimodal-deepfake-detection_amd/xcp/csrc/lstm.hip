@@ -552,6 +552,8 @@ constexpr unsigned LP_SPIN = 1u << 22;    // polls (each after s_sleep 2) before
 constexpr int LP_CSP = 0x00020000;        // raw buffer descriptor word 3
 constexpr int LP_SC1 = 16;                // cache policy: sc1
 
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+
 struct LstmSync {
   unsigned* cnt;   // [8][LP_SHARD]
   unsigned* err;   // set to 1 on a poll timeout
@@ -592,40 +594,49 @@ XCP_DEV void lp_publish(const LstmSync& sy) {
 
 XCP_DEV void lp_st(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
+template <int V> struct LpIC {
+  static constexpr int value = V;
+};
+template <int B, int E, typename F>
+XCP_DEV void lp_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(LpIC<B>{});
+    lp_static_for<B + 1, E>(f);
+  }
+}
+
 // reduce-scatter of v[N] over the 64 lanes: level d keeps the upper half where lane & d; after
 // log2(N) levels lane l holds index (l >> (6 - log2 N)) complete over those lanes, the remaining
-// levels sum plainly (every lane of a group ends with the same value)
+// levels sum plainly (every lane of a group ends with the same value).  Every index is a
+// compile-time constant (the array stays in VGPRs).
 template <int N>
 XCP_DEV float lp_rscatter(float (&v)[N], int lane) {
-  int n = N;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    if (n >= 2) {
+  lp_static_for<0, 6>([&](auto L) {
+    constexpr int d = 32 >> decltype(L)::value;
+    constexpr int n = N >> decltype(L)::value;
+    if constexpr (n >= 2) {
       const bool up = lane & d;
 #pragma unroll
-      for (int c = 0; c < N / 2; ++c) {
-        if (c < n / 2) {
-          const float keep = up ? v[n / 2 + c] : v[c];
-          const float send = up ? v[c] : v[n / 2 + c];
-          v[c] = keep + __shfl_xor(send, d, 64);
-        }
+      for (int c = 0; c < n / 2; ++c) {
+        const float keep = up ? v[n / 2 + c] : v[c];
+        const float send = up ? v[c] : v[n / 2 + c];
+        v[c] = keep + __shfl_xor(send, d, 64);
       }
-      n /= 2;
     } else {
       v[0] += __shfl_xor(v[0], d, 64);
     }
-  }
+  });
   return v[0];
 }
 
+// (one wave per SIMD: the whole 512-entry register file, so a step's loads all go out before the
+// first use -- at 256 registers hipcc issued them clip by clip, one L2 round trip each)
 template <int H>
-__global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __restrict__ xproj,
-                                                               const float* __restrict__ whh,
-                                                               const float* __restrict__ bih,
-                                                               const float* __restrict__ bhh, float* out,
-                                                               float* __restrict__ hprev, float* __restrict__ cst,
-                                                               float* __restrict__ gates, float* __restrict__ hn,
-                                                               float* __restrict__ cn, int B, int T, LstmSync sy) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void lstm_fwd_persist_kernel(const float* __restrict__ xproj, const float* __restrict__ whh,
+                             const float* __restrict__ bih, const float* __restrict__ bhh, float* out,
+                             float* __restrict__ hprev, float* __restrict__ cst, float* __restrict__ gates,
+                             float* __restrict__ hn, float* __restrict__ cn, int B, int T, LstmSync sy) {
   constexpr int KL = H / 64, R = 4 * LP_U, G4 = 4 * H;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int u0 = blockIdx.x * LP_U, k0 = lane * KL;
@@ -640,17 +651,23 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
   // cell lanes: lane = c * 16 + u (gate 0 of unit u of clip c); the other gates at lane + 4q
   const bool cell = (lane & 12) == 0;
   const int cu = lane & 3, k = u0 + cu;
+  float bi[4], bh[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    bi[q] = bih[q * H + k];
+    bh[q] = bhh[q * H + k];
+  }
   const int npass = (B + 15) / 16;
   float cstate[2] = {0.f, 0.f}, hst[2] = {0.f, 0.f}, xq[2][4];
   const __amdgpu_buffer_rsrc_t rO = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7fffffff, LP_CSP);
   auto clip = [&](int p, int c) { return p * 16 + wv * 4 + c; };
-  auto load_xp = [&](int t) {   // x W_ih^T of step t for this lane's cell (prefetched a step ahead)
+  auto load_xp = [&](int t) {   // x W_ih^T of step t for this lane's cell (prefetched a step ahead; clamped)
+    const int tt = min(t, T - 1);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      const int b = clip(p, lane >> 4);
-      const bool ok = cell && p < npass && b < B && t < T;
+      const int b = min(clip(p, lane >> 4), B - 1);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) xq[p][q] = ok ? xproj[((long)b * T + t) * G4 + q * H + k] : 0.f;
+      for (int q = 0; q < 4; ++q) xq[p][q] = xproj[((long)b * T + tt) * G4 + q * H + k];
     }
   };
   load_xp(0);
@@ -663,33 +680,37 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
     load_xp(t + 1);
     if (t > 0 && !lp_wait(sy, (unsigned)t)) return;
     for (int p = 0; p < npass; ++p) {
-      float part[4 * R];
+      float hv[4][KL];
+      if (t > 0) {   // h_{t-1} of the wave's 4 clips (clamped), every 16-B sc1 load issued before any use
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int b = clip(p, c);
-        float hv[KL];
-        if (t > 0 && b < B) {   // (wave-uniform) h_{t-1}[b][k0 .. k0+KL): 16-B sc1 loads
+        for (int c = 0; c < 4; ++c) {
+          const int b = min(clip(p, c), B - 1);
 #pragma unroll
           for (int i = 0; i < KL; i += 4) {
             const float4 v4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                 rO, (int)((((long)b * T + t - 1) * H + k0 + i) * 4), 0, LP_SC1));
-            hv[i] = v4.x; hv[i + 1] = v4.y; hv[i + 2] = v4.z; hv[i + 3] = v4.w;
+            hv[c][i] = v4.x; hv[c][i + 1] = v4.y; hv[c][i + 2] = v4.z; hv[c][i + 3] = v4.w;
           }
-        } else {
-#pragma unroll
-          for (int i = 0; i < KL; ++i) hv[i] = 0.f;
         }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int i = 0; i < KL; ++i) hv[c][i] = 0.f;
+      }
+      float part[4 * R];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int rr = 0; rr < R; ++rr) {
           float a0 = 0.f, a1 = 0.f;
 #pragma unroll
           for (int i = 0; i < KL; i += 2) {
-            a0 = fmaf(w[rr][i], hv[i], a0);
-            a1 = fmaf(w[rr][i + 1], hv[i + 1], a1);
+            a0 = fmaf(w[rr][i], hv[c][i], a0);
+            a1 = fmaf(w[rr][i + 1], hv[c][i + 1], a1);
           }
           part[c * R + rr] = a0 + a1;
         }
-      }
       const float rec = lp_rscatter(part, lane);   // clip lane >> 4, row lane & 15
       float pre[4];
 #pragma unroll
@@ -698,7 +719,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
       if (cell && b < B) {
         float g[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) g[q] = ((pre[q] + xc[p][q]) + bih[q * H + k]) + bhh[q * H + k];
+        for (int q = 0; q < 4; ++q) g[q] = ((pre[q] + xc[p][q]) + bi[q]) + bh[q];
         const float ig = sigm(g[0]), fg = sigm(g[1]), gg = tanhf(g[2]), og = sigm(g[3]);
         const float c = fmaf(fg, cstate[p], ig * gg);
         const float h = og * tanhf(c);
@@ -720,79 +741,94 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const float* __re
   }
 }
 
+// Backward: dh_t[b][k] = dout + sum_j dgates_{t+1}[b][j] W_hh[j][k] needs every gate row j, so instead of
+// gathering dgates_{t+1} (B x 4H floats) into every workgroup, each workgroup turns ITS 16 rows'
+// dgates into a partial of dh for all H units -- lane l: part[b][k = l*KL .. +KL) = sum over its rows
+// of dgates[b][row] W_hh[row][k] (the forward's W slice, the row values broadcast from the cell lanes
+// by readlane) -- and publishes it (4 KB per clip, sc1); the next step gathers its 4 units' columns
+// of the G partials (16 B per clip and producer) and reduces them over the wave.  Per step and
+// workgroup: B x H x 4 B out and B x 16 x G B in (at B = 16, 32 KB each way) instead of B x 4H x 4 B in.
+// part: [2 (step parity)][G][B][H] fp32 (the caller's work buffer).
 template <int H>
-__global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const float* __restrict__ dout,
-                                                               const float* __restrict__ dhn,
-                                                               const float* __restrict__ dcn,
-                                                               const float* __restrict__ whh,
-                                                               const float* __restrict__ cst,
-                                                               const float* __restrict__ gates, float* dgates, int B,
-                                                               int T, LstmSync sy) {
-  constexpr int JL = 4 * H / 64, G4 = 4 * H;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int u0 = blockIdx.x * LP_U, j0 = lane * JL;
-  float w[JL][LP_U];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void lstm_bwd_persist_kernel(const float* __restrict__ dout, const float* __restrict__ dhn,
+                             const float* __restrict__ dcn, const float* __restrict__ whh,
+                             const float* __restrict__ cst, const float* __restrict__ gates,
+                             float* __restrict__ dgates, float* part, int B, int T, LstmSync sy) {
+  constexpr int KL = H / 64, R = 4 * LP_U, G4 = 4 * H;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, G = gridDim.x;
+  const int u0 = blockIdx.x * LP_U, k0 = lane * KL;
+  float w[R][KL];   // W_hh[gate q, unit u0 + u][k0 .. k0+KL), row rr = q * 4 + u
 #pragma unroll
-  for (int i = 0; i < JL; ++i) {
-    const float4 v4 = *reinterpret_cast<const float4*>(whh + (long)(j0 + i) * H + u0);
-    w[i][0] = v4.x; w[i][1] = v4.y; w[i][2] = v4.z; w[i][3] = v4.w;
-  }
-  // cell lanes: lane = c * 16 + u * 4 (clip c, unit u)
+  for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+    for (int i = 0; i < KL; i += 4) {
+      const float4 v4 = *reinterpret_cast<const float4*>(whh + (long)((rr / LP_U) * H + u0 + rr % LP_U) * H + k0 + i);
+      w[rr][i] = v4.x; w[rr][i + 1] = v4.y; w[rr][i + 2] = v4.z; w[rr][i + 3] = v4.w;
+    }
+  // cell lanes: lane = c * 16 + u * 4 (clip c of the wave, unit u)
   const bool cell = (lane & 3) == 0;
   const int cu = (lane >> 2) & 3, k = u0 + cu;
   const int npass = (B + 15) / 16;
+  const long pstride = (long)G * B * H;   // one parity's partials
   float carry[2] = {0.f, 0.f};
-  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(dgates, (short)0, 0x7fffffff, LP_CSP);
+  const __amdgpu_buffer_rsrc_t rP = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0x7fffffff, LP_CSP);
   auto clip = [&](int p, int c) { return p * 16 + wv * 4 + c; };
   for (int t = T - 1; t >= 0; --t) {
     const bool last = t == T - 1;
-    // this step's cell operands (independent of the recurrence: loaded before the wait)
+    // this step's cell operands (independent of the recurrence: loaded before the wait; clamped
+    // addresses, absent operands selected away)
     float vc[2], vcp[2], vg[2][4], vdo[2], vhn[2], vcn[2];
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      const int b = clip(p, lane >> 4);
-      const bool ok = cell && p < npass && b < B;
-      const long ob = ((long)b * T + t) * H + k;
-      vc[p] = ok ? cst[ob] : 0.f;
-      vcp[p] = ok && t > 0 ? cst[ob - H] : 0.f;
-      vdo[p] = ok && dout ? dout[ob] : 0.f;
-      vhn[p] = ok && last && dhn ? dhn[(long)b * H + k] : 0.f;
-      vcn[p] = ok && last && dcn ? dcn[(long)b * H + k] : 0.f;
+      const int b = min(clip(p, lane >> 4), B - 1);
+      const long ob = ((long)b * T + t) * H + k, bk = (long)b * H + k;
+      vc[p] = cst[ob];
+      vcp[p] = cst[t > 0 ? ob - H : ob];
+      vdo[p] = *(dout ? dout + ob : cst + ob);
+      vhn[p] = *(dhn ? dhn + bk : cst + ob);
+      vcn[p] = *(dcn ? dcn + bk : cst + ob);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) vg[p][q] = ok ? gates[((long)b * T + t) * G4 + q * H + k] : 0.f;
+      for (int q = 0; q < 4; ++q) vg[p][q] = gates[((long)b * T + t) * G4 + q * H + k];
+      if (t == 0) vcp[p] = 0.f;
+      if (!dout) vdo[p] = 0.f;
+      if (!dhn) vhn[p] = 0.f;
+      if (!dcn) vcn[p] = 0.f;
     }
     if (!last && !lp_wait(sy, (unsigned)(T - 1 - t))) return;
     for (int p = 0; p < npass; ++p) {
-      float part[4 * LP_U];
-#pragma unroll
-      for (int q = 0; q < 4 * LP_U; ++q) part[q] = 0.f;
-      if (!last) {
+      if (clip(p, 0) >= B) continue;   // (wave-uniform: no clip of this wave in this pass)
+      float red[4 * LP_U];
+      if (!last) {   // this workgroup's 4 units of the G partials of step t+1: lanes l and l + 64
+        const float* pp = part + (long)((t + 1) & 1) * pstride;
+        float4 pv[4][2];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const int b = clip(p, c);
-          if (b < B) {   // (wave-uniform) dgates_{t+1}[b][j0 .. j0+JL): 16-B sc1 loads
-            float dg[JL];
+          const int b = min(clip(p, c), B - 1);
 #pragma unroll
-            for (int i = 0; i < JL; i += 4) {
-              const float4 v4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                  rG, (int)((((long)b * T + t + 1) * G4 + j0 + i) * 4), 0, LP_SC1));
-              dg[i] = v4.x; dg[i + 1] = v4.y; dg[i + 2] = v4.z; dg[i + 3] = v4.w;
-            }
-#pragma unroll
-            for (int u = 0; u < LP_U; ++u) {
-              float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-              for (int i = 0; i < JL; i += 2) {
-                a0 = fmaf(dg[i], w[i][u], a0);
-                a1 = fmaf(dg[i + 1], w[i + 1][u], a1);
-              }
-              part[c * LP_U + u] = a0 + a1;
-            }
+          for (int e = 0; e < 2; ++e) {
+            const int src = min(lane + 64 * e, G - 1);
+            pv[c][e] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                rP, (int)((((long)((t + 1) & 1) * pstride + ((long)src * B + b) * H + u0) * 4)), 0, LP_SC1));
           }
         }
+        (void)pp;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bool e1 = lane + 64 < G;
+          red[c * 4 + 0] = pv[c][0].x + (e1 ? pv[c][1].x : 0.f);
+          red[c * 4 + 1] = pv[c][0].y + (e1 ? pv[c][1].y : 0.f);
+          red[c * 4 + 2] = pv[c][0].z + (e1 ? pv[c][1].z : 0.f);
+          red[c * 4 + 3] = pv[c][0].w + (e1 ? pv[c][1].w : 0.f);
+          if (lane >= G) red[c * 4] = red[c * 4 + 1] = red[c * 4 + 2] = red[c * 4 + 3] = 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4 * LP_U; ++q) red[q] = 0.f;
       }
-      const float rec = lp_rscatter(part, lane);   // clip lane >> 4, unit (lane >> 2) & 3
+      const float rec = lp_rscatter(red, lane);   // clip lane >> 4, unit (lane >> 2) & 3
       const int b = clip(p, lane >> 4);
+      float dg[4] = {0.f, 0.f, 0.f, 0.f};
       if (cell && b < B) {
         const float ig = vg[p][0], fg = vg[p][1], gg = vg[p][2], og = vg[p][3];
         const float dhr = !last ? rec : vhn[p];
@@ -803,11 +839,38 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const float* __re
         const float dc = dcr + dh * og * (1.f - tc * tc);
         const float dI = dc * gg, dG = dc * ig, dF = dc * vcp[p];
         carry[p] = dc * fg;
+        dg[0] = dI * ig * (1.f - ig);
+        dg[1] = dF * fg * (1.f - fg);
+        dg[2] = dG * (1.f - gg * gg);
+        dg[3] = dO * og * (1.f - og);
         float* dgo = dgates + ((long)b * T + t) * G4;
-        lp_st(dgo + k, dI * ig * (1.f - ig));
-        lp_st(dgo + H + k, dF * fg * (1.f - fg));
-        lp_st(dgo + 2 * H + k, dG * (1.f - gg * gg));
-        lp_st(dgo + 3 * H + k, dO * og * (1.f - og));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dgo[q * H + k] = dg[q];
+      }
+      if (t > 0) {   // this workgroup's partial of dh_{t-1} for the wave's clips, every unit k0 .. k0+KL
+        float* pw = part + (long)(t & 1) * pstride + (long)blockIdx.x * B * H;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int bc = clip(p, c);
+          float acc[KL];
+#pragma unroll
+          for (int i = 0; i < KL; ++i) acc[i] = 0.f;
+#pragma unroll
+          for (int rr = 0; rr < R; ++rr) {   // dgates[bc][gate q, unit u] from cell lane c * 16 + u * 4
+            const float d = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                __builtin_bit_cast(int, dg[rr / LP_U]), c * 16 + (rr % LP_U) * 4));
+#pragma unroll
+            for (int i = 0; i < KL; ++i) acc[i] = fmaf(d, w[rr][i], acc[i]);
+          }
+          if (bc < B) {
+#pragma unroll
+            for (int i = 0; i < KL; i += 4)
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  __builtin_bit_cast(i32x4v, make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3])), rP,
+                  (int)(((long)(t & 1) * pstride + ((long)blockIdx.x * B + bc) * H + k0 + i) * 4), 0, LP_SC1);
+          }
+          (void)pw;
+        }
       }
     }
     if (t > 0) lp_publish(sy);
@@ -904,8 +967,8 @@ int xcp_lstm_sync_error() {
 
 // 1 when xcp_lstm_fwd (same B, H, kernel) runs the generic kernel, which reads the transposed W_hh
 int xcp_lstm_needs_whhT(int B, int H, int kernel) {
-  const bool persist = kernel == 0 && B <= 32 && (H == 256 || H == 512);   // (the persistent kernels read W_hh)
-  return lstm_reg(H, kernel) || lstm_step(B, H, kernel) || persist ? 0 : 1;
+  // (the register-resident, persistent and per-step forward kernels read W_hh as stored)
+  return lstm_reg(H, kernel) || lstm_persist(B, H, kernel, true) || lstm_step(B, H, kernel) ? 0 : 1;
 }
 
 int xcp_lstm_fwd(const float* xproj, const float* whh, const float* whhT, const float* bih, const float* bhh, float* out,
@@ -964,12 +1027,13 @@ int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const fl
     LstmSync sy;
     const int rc = lp_sync(st, sy);
     if (rc != XCP_OK) return rc;
+    if (!work) return XCP_EINVAL;
     if (H == 512)
       hipLaunchKernelGGL(lstm_bwd_persist_kernel<512>, dim3(H / LP_U), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates,
-                         dgates, B, T, sy);
+                         dgates, work, B, T, sy);
     else
       hipLaunchKernelGGL(lstm_bwd_persist_kernel<256>, dim3(H / LP_U), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates,
-                         dgates, B, T, sy);
+                         dgates, work, B, T, sy);
     return (int)hipGetLastError();
   }
   if (lstm_step(B, H, kernel)) {

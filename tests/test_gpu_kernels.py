@@ -1076,13 +1076,19 @@ def test_fused_adam_clip_load_state_dict_resume(ops, gpu):
         torch.testing.assert_close(opt_a.state[p]["exp_avg"], opt_b.state[q]["exp_avg"], rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("loop", ["4", "2"])
 @pytest.mark.parametrize("M,N,K,ref", [(92416, 736, 736, 2), (5120 * 9, 1024, 736, 2), (2048 * 7 + 256, 512, 64, 2),
-                                       (256 * 506 + 77, 256, 200, 2), (256 * 600 + 77, 256, 448, 2)])
-def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref):
-    """The persistent 256x256 kernel (tile 3, every row on it) computes every tile with the
-    one-shot kernel's MFMA order: identical output and statistics bits against tile 2 (the
-    one-shot kernel for every row), across several tiles per workgroup (the prefetch / epilogue
-    overlap must not change a value)."""
+                                       (256 * 506 + 77, 256, 200, 2), (256 * 600 + 77, 256, 448, 2),
+                                       (256 * 300 + 5, 512, 128, 2)])
+def test_gemm_nt_persistent_bitwise(ops, gpu, monkeypatch, M, N, K, ref, loop):
+    """The persistent 256x256 kernel (tile 3, every row on it; loop 4: gemm_nt256p_kernel, loop 2:
+    gemm_nt256q_kernel's two MFMA phases per K-tile) computes every tile with the one-shot kernel's
+    MFMA order: identical output bits against tile 2 (the one-shot kernel for every row), across
+    several tiles per workgroup (the prefetch / epilogue overlap must not change a value).  The BN
+    statistics are bitwise too for loop 4; loop 2 reduces each 64-row half of a wave's rows over the
+    wave and adds the two (its epilogue runs in two halves), so its sums differ by fp32 rounding only
+    (1e-6 relative here).  K = 128: two K-tiles per tile, the shortest the two-phase loop runs."""
+    monkeypatch.setenv("XCP_NT_LOOP", loop)
     tile = 3
     g = torch.Generator(device=gpu).manual_seed(M + N)
     A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
@@ -1096,7 +1102,11 @@ def test_gemm_nt_persistent_bitwise(ops, gpu, M, N, K, ref):
         outs.append((C, part))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
+    if loop == "4":
+        assert torch.equal(outs[0][1], outs[1][1])
+    else:
+        assert not torch.isnan(outs[1][1]).any()
+        torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-6, atol=1e-6 * outs[0][1].abs().max().item())
 
 
 @pytest.mark.parametrize("M,N,K", [(92416, 736, 736), (256 * 600 + 77, 256, 448), (5120 * 9, 1024, 736)])
@@ -1239,3 +1249,28 @@ def test_sep_fwd_rejects_unsupported(ops, gpu):
     assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 79, 128, 256) == 0   # the 256-output form: one half row
     assert ops.sep_fwd_parts(torch.bfloat16, 2, 8, 8, 256, 256) == 0
     assert ops.sep_fwd_parts(torch.float32, 2, 8, 8, 64, 128) == 0
+
+
+@pytest.mark.parametrize("M,N,K", [(92416, 728, 728), (3000, 296, 520), (32 * 7 + 5, 256, 264), (20000, 1024, 256)])
+def test_gemm_tn_loops_bitwise(ops, gpu, monkeypatch, M, N, K):
+    """The weight-gradient kernel with one 32-MFMA phase per step and the fill four steps ahead
+    (XCP_TN_LOOP=2, gemm_tn256q_kernel) against gemm_tn256_kernel: the same MFMA order per
+    accumulator, so the fp32 partial slabs are bitwise equal (ragged M / N / K, splits shorter than
+    the ring)."""
+    g = torch.Generator(device=gpu).manual_seed(M + N + K)
+    G = torch.randn(M, N, device=gpu, generator=g).bfloat16()
+    X = torch.randn(M, K, device=gpu, generator=g).bfloat16()
+    rps = ops._lib.call("xcp_gemm_tn_rows_per_split", 1, 0, M, N, K, 2)
+    S = (M + rps - 1) // rps
+    outs = []
+    for form in ("1", "2"):
+        monkeypatch.setenv("XCP_TN_LOOP", form)
+        P = torch.full((S * N * K,), float("nan"), device=gpu)
+        ops.gemm_tn(G, X, P, M, N, K, S, rps, tile=2)
+        torch.cuda.synchronize()
+        outs.append(P)
+    assert not torch.isnan(outs[1]).any()
+    assert torch.equal(outs[0], outs[1])
+    ref = (G.float().t() @ X.float())
+    got = outs[1].view(S, N, K).sum(0)
+    torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
