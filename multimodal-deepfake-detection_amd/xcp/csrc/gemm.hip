@@ -1509,7 +1509,7 @@ __global__ __launch_bounds__(512) void gemm_tn256_kernel(TNArgs a) {
 }
 
 // Weight-gradient kernel with ONE MFMA phase of 32 per 32-row step and the fill four steps ahead
-// (gemm_tn256q_kernel; XCP_TN_LOOP=2, A/B against gemm_tn256_kernel's two 16-MFMA phases).  Per step
+// (gemm_tn256q_kernel, the default; XCP_TN_LOOP=1 runs gemm_tn256_kernel's two 16-MFMA phases).  Per step
 // a wave reads all its fragments (X: 4 k-frags, G: 8 n-frags = 24 ds_read_b64_tr_b16) and issues
 // step s+4 into the slot step s-1 left (both wave groups finished reading it two intervals earlier),
 // waits lgkmcnt(0), and its 32 MFMAs run in the next interval beside the other group's reads: two
@@ -1681,11 +1681,12 @@ bool tn_xcd_splits() {   // XCP_TN_XCD_SPLITS=1 (A/B; measured -0.3 % in the ste
   }();
   return v;
 }
-// XCP_TN_LOOP=2: the weight-gradient kernel with one 32-MFMA phase per step and the fill 4 steps ahead
-// (gemm_tn256q_kernel; read per call; A/B)
+// The weight-gradient kernel with one 32-MFMA phase per step and the fill 4 steps ahead (gemm_tn256q_kernel):
+// 9-13 % faster alone at every step shape, the partial slabs bitwise equal (profiles/r06_tn_loop_ab.txt).
+// XCP_TN_LOOP=1: gemm_tn256_kernel's two 16-MFMA phases (read per call; A/B)
 bool tn_loop2() {
   const char* e = getenv("XCP_TN_LOOP");
-  return e && e[0] == '2';
+  return !(e && e[0] == '1');
 }
 // XCP_TN_XCD_ALIGN=1: whole splits per XCD for outputs of at most 32 tiles (read per call; A/B)
 bool tn_xcd_align() {

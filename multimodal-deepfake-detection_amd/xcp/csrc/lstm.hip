@@ -891,12 +891,16 @@ bool lstm_step(int B, int H, int kernel) {
          fwd_lds <= 65536 && bwd_lds <= 65536;
 }
 
-// persistent kernels (XCP_LSTM_PERSIST=0: the per-step kernels; read per call): H = 256 / 512, B <= 32,
-// and all G = H / 4 workgroups resident at once by the occupancy query
-bool lstm_persist_env() {
+// persistent kernels for H = 256 / 512, B <= 32, when all G = H / 4 workgroups can be resident at once (the
+// occupancy query).  Default: the forward only -- at XceptionLSTMA's shape (B 16, T 120, H 512) it runs 4.6 us
+// per step against the per-step kernels' 6.3; the persistent backward (published dh partials) is faster at
+// small B (3.9 vs 4.6 us per step at B 2) but slower at B 16 (9.5 vs 7.3: the partials' sc1 traffic), so the
+// per-step backward stays (profiles/r06_lstm_ab.txt).  XCP_LSTM_PERSIST=0: neither, 1: both (read per call).
+int lstm_persist_mode() {
   const char* e = getenv("XCP_LSTM_PERSIST");
-  return e && e[0] == '1';
+  return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 2 : 1;
 }
+bool lstm_persist_env(bool fwd) { return lstm_persist_mode() >= (fwd ? 1 : 2); }
 template <typename K>
 bool lp_resident(K kern, int G) {
   int dev = 0, cus = 0, per = 0;
@@ -906,7 +910,7 @@ bool lp_resident(K kern, int G) {
   return (long)per * cus >= G;
 }
 bool lstm_persist(int B, int H, int kernel, bool fwd) {
-  if (kernel != 0 || B > 32 || !(H == 256 || H == 512) || !lstm_persist_env()) return false;
+  if (kernel != 0 || B > 32 || !(H == 256 || H == 512) || !lstm_persist_env(fwd)) return false;
   static int ok[2][2] = {{-1, -1}, {-1, -1}};   // [fwd][H == 512]
   int& v = ok[fwd][H == 512];
   if (v < 0) {

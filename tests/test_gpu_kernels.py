@@ -787,8 +787,9 @@ def test_lstm_module_vs_oracle(ops, gpu, golden, H, T, kernel):
 def test_lstm_t120_vs_reference(ops, gpu, golden, monkeypatch, kernel):
     """XceptionLSTMA's own recurrence -- nn.LSTM(2048, 512) over T = 120 MFCC frames
     (XceptionLSTMA.py:14-19, audio_dataloader.py:20,39) -- through the three kernel families H = 512
-    can take (persistent: one launch each way, the default; step: XCP_LSTM_PERSIST=0, 120 launches
-    each way carrying h and c; generic) against the reference's own values (lstm_t120.npz): out /
+    can take (persistent: XCP_LSTM_PERSIST=1, one launch each way -- the default runs the forward
+    that way and the backward per step; step: XCP_LSTM_PERSIST=0, 120 launches each way carrying h
+    and c; generic) against the reference's own values (lstm_t120.npz): out /
     h_n / c_n at 1e-4, every time step's output norm at 1e-4 (the error must not grow over the 120
     steps), dx and the parameter gradients at 1e-3."""
     import numpy as np
@@ -1254,7 +1255,7 @@ def test_sep_fwd_rejects_unsupported(ops, gpu):
 @pytest.mark.parametrize("M,N,K", [(92416, 728, 728), (3000, 296, 520), (32 * 7 + 5, 256, 264), (20000, 1024, 256)])
 def test_gemm_tn_loops_bitwise(ops, gpu, monkeypatch, M, N, K):
     """The weight-gradient kernel with one 32-MFMA phase per step and the fill four steps ahead
-    (XCP_TN_LOOP=2, gemm_tn256q_kernel) against gemm_tn256_kernel: the same MFMA order per
+    (gemm_tn256q_kernel, the default) against gemm_tn256_kernel (XCP_TN_LOOP=1): the same MFMA order per
     accumulator, so the fp32 partial slabs are bitwise equal (ragged M / N / K, splits shorter than
     the ring)."""
     g = torch.Generator(device=gpu).manual_seed(M + N + K)

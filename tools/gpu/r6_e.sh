@@ -1,4 +1,4 @@
-# Round 6 (e): persistent LSTM with every load of a step issued before its first use (512-register waves,
+# Round 6 (e + f): persistent LSTM with every load of a step issued before its first use (512-register waves,
 # compile-time reduce-scatter): LSTM tests, fwd/bwd A/B, the lstma step A/B; the weight-gradient loop
 # (XCP_TN_LOOP=2) in the lstmv step with the default NT loop
 set -o pipefail
@@ -15,4 +15,10 @@ done
 for r in 1 2; do
   timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --cpu-baseline off > gpurun_out/e_base_$r.log 2> gpurun_out/e_base_$r.err || exit $?
   XCP_TN_LOOP=2 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --cpu-baseline off > gpurun_out/e_tn2_$r.log 2> gpurun_out/e_tn2_$r.err || exit $?
+done
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for r in 1 2; do
+  timeout -k 10 200 python -u tools/kbench.py ntprobe > gpurun_out/f_base_$r.log 2>&1 || exit $?
+  XCP_LIB_PATH=probe/oobstore/libxcp.so timeout -k 10 200 python -u tools/kbench.py ntprobe > gpurun_out/f_oob_$r.log 2>&1 || exit $?
+  XCP_LIB_PATH=probe/nostore/libxcp.so timeout -k 10 200 python -u tools/kbench.py ntprobe > gpurun_out/f_nost_$r.log 2>&1 || exit $?
 done
