@@ -107,6 +107,7 @@ struct NTArgs {
   float* stats;           // [gridM][2][N] partial (sum, sumsq) or nullptr
   Gather ga;
   int tqs;                // gemm_nt256p_kernel: tile-queue slot + 1 (0: static tile walk)
+  int nsplit;             // gemm_nt256p_kernel: the last nsplit tiles are walked as 2 half tiles each, first
 };
 
 // ---------------------------------------------------------------------------------
@@ -616,7 +617,7 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 // 16 C stores per lane, + 1 statistics store when STATS
 template <bool STATS, typename Get>
 XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC, __amdgpu_buffer_rsrc_t rS, int m0,
-                             int n0, int wr, int wc, int fr, int fg) {
+                             int n0, int wr, int wc, int fr, int fg, int side = 0) {
   const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
   const int mrow = m0 + wr * 128 + fr;
   const int ncol = n0 + wc * 64;
@@ -650,8 +651,9 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     const uint4 st0 = odd ? make_uint4(rc0.x, rc0.y, pc[1].x, pc[1].y) : make_uint4(pc[0].x, pc[0].y, rc0.x, rc0.y);
     const uint4 st1 = odd ? make_uint4(rc1.x, rc1.y, pc[3].x, pc[3].y) : make_uint4(pc[2].x, pc[2].y, rc1.x, rc1.y);
     const unsigned rowb = (unsigned)((long)m * a.ldc * 2);
-    const unsigned o0 = (mok && c0 < a.N) ? rowb + (unsigned)c0 * 2 : BUF_OOB;
-    const unsigned o1 = (mok && c0 + 32 < a.N) ? rowb + (unsigned)(c0 + 32) * 2 : BUF_OOB;
+    // (a half tile stores only its side: st0 holds the left 32 columns of the wave, st1 the right 32)
+    const unsigned o0 = (mok && c0 < a.N && side != 2) ? rowb + (unsigned)c0 * 2 : BUF_OOB;
+    const unsigned o1 = (mok && c0 + 32 < a.N && side != 1) ? rowb + (unsigned)(c0 + 32) * 2 : BUF_OOB;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 0);
   });
@@ -668,16 +670,17 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     for (int q = 0; q < 2; ++q) v2[q] = (b0 ? v4[2 + q] : v4[q]) + __shfl_xor(b0 ? v4[q] : v4[2 + q], 1, 64);
     const int col = ncol + ((fr & 7) >> 1) * 16 + fg * 4 + (fr & 1) * 2;
     const int srow = bm * 2 + wr;
-    const unsigned so = (srow < stat_rows && col < a.N) ? (unsigned)((((long)srow * 2 + (fr >> 3)) * a.N + col) * 4)
-                                                        : BUF_OOB;
+    const bool sok = side == 0 || (side == 1) == (((fr & 7) >> 1) < 2);   // (a half tile: its side's columns)
+    const unsigned so = (srow < stat_rows && col < a.N && sok)
+                            ? (unsigned)((((long)srow * 2 + (fr >> 3)) * a.N + col) * 4) : BUF_OOB;
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_float2(v2[0], v2[1])), rS, (int)so, 0, 0);
   }
 }
 
 template <bool STATS>
 XCP_DEV void epilogue256_buf(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffer_rsrc_t rC,
-                             __amdgpu_buffer_rsrc_t rS, int m0, int n0, int wr, int wc, int fr, int fg) {
-  epilogue256_get<STATS>([&](int i, int j, int r) { return acc[i][j][r]; }, a, rC, rS, m0, n0, wr, wc, fr, fg);
+                             __amdgpu_buffer_rsrc_t rS, int m0, int n0, int wr, int wc, int fr, int fg, int side = 0) {
+  epilogue256_get<STATS>([&](int i, int j, int r) { return acc[i][j][r]; }, a, rC, rS, m0, n0, wr, wc, fr, fg, side);
 }
 
 // Tile counters of the persistent NT kernel, one per (device, stream) slot: a workgroup takes its first
@@ -688,7 +691,7 @@ XCP_DEV void epilogue256_buf(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffe
 // last and resets the counter for the next launch (graph replays included).
 __device__ int g_nt_tq[64];
 
-template <bool STATS>
+template <bool STATS, bool HALF>
 __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   constexpr int S_ST = 16 + (STATS ? 1 : 0);   // store instructions per wave per epilogue
   // (+ 16 B for the tile-queue broadcast: in the ring's LDS object, since a second object would give the
@@ -698,6 +701,21 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   int* const tq = a.tqs > 0 ? g_nt_tq + (a.tqs - 1) : nullptr;
   const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
   const int tiles = gridM * gridN, nwg = gridDim.x;
+  // work items: the last nsplit tiles as 2 half tiles each (side 1: the B-left 32 columns of every wave's 64,
+  // side 2: the B-right 32), walked FIRST, then the other tiles whole (side 0).  A half tile runs only its
+  // side's two quadrant phases, so the workgroups that start with one reach their tile boundaries (and their
+  // epilogue stores) about half a tile out of step with the rest: the rounds' store bursts no longer coincide.
+  const int nsplit = HALF ? a.nsplit : 0, nhalf = 2 * nsplit, items = tiles + nsplit;
+  auto item_tile = [&](int it, int& side) {
+    if constexpr (HALF) {
+      if (it < nhalf) {
+        side = 1 + (it & 1);
+        return tiles - nsplit + (it >> 1);
+      }
+    }
+    side = 0;
+    return it - nhalf;
+  };
   const int slot = xcd_remap(blockIdx.x, nwg);
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: LDS-DMA destinations (M0) from SGPRs
   const int wr = w >> 2, wc = w & 3;
@@ -721,14 +739,15 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(STATS ? (void*)a.stats : a.C, (short)0,
                                                                        BUF_RECORDS, BUF_DWORD3);
   unsigned voff[4][2];
-  auto set_tile = [&](int m0, int n0) {
+  auto set_tile = [&](int m0, int n0, int side) {
 #pragma unroll
     for (int h = 0; h < 4; ++h)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const bool isA = (h == 0 || h == 3);
         const int r = (isA ? m0 : n0) + rowt[h][i];
-        const bool ok = isA ? r < a.M : r < a.N;
+        // (a half tile's other B half is not fetched: its DMA slots load the zero line)
+        const bool ok = (isA ? r < a.M : r < a.N) && !(HALF && ((h == 1 && side == 2) || (h == 2 && side == 1)));
         voff[h][i] = ok ? (unsigned)(((long)r * (isA ? a.lda : a.ldb) + kc8[h][i]) * 2) : BUF_OOB;
       }
   };
@@ -759,20 +778,25 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
           acc[ih * 4 + i][jh * 2 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][ks], af[i][ks], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
   };
+  int side = 0;   // of the current item (wave-uniform)
   auto sync_mfma = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    mfma_q(ih, b, jh);
-    __builtin_amdgcn_s_setprio(0);
+    if (!HALF || side != 2 - jh) {   // (a half tile skips the other side's quadrants)
+      __builtin_amdgcn_s_setprio(1);
+      mfma_q(ih, b, jh);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
   };
 
   int t = slot;
-  if (t >= tiles) return;
-  int m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
-  set_tile(m0, n0);
+  if (t >= items) return;
+  int tile = item_tile(t, side);
+  int m0 = (tile / gridN) * 256, n0 = (tile % gridN) * 256;
+  set_tile(m0, n0, side);
 #pragma unroll
   for (int h = 0; h < 4; ++h) issue(h, 0);
   int extra = 0;   // epilogue stores of the previous tile still allowed in flight during K-tile 0
@@ -833,27 +857,28 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
     ktile(0, IC<1>{});
     for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
     if (wr == 0) __builtin_amdgcn_s_barrier();   // every wave is done reading both ring slots
-    const int cm0 = m0, cn0 = n0;
+    const int cm0 = m0, cn0 = n0, cside = side;
     if (tq) {
       if (tid == 0) {
         asm volatile("" : "+v"(nxt));   // (used only here, after the K loop's waits)
         *s_next = (int)nxt;
-        if ((int)nxt == tiles - 1) __hip_atomic_store(tq, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int)nxt == items - 1) __hip_atomic_store(tq, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       lds_barrier();
       t = nwg + __builtin_amdgcn_readfirstlane(*s_next);
     } else {
       t += nwg;
     }
-    const bool more = t < tiles;
+    const bool more = t < items;
     if (more) {   // the next tile's first K-tile, ahead of this tile's stores
-      m0 = (t / gridN) * 256;
-      n0 = (t % gridN) * 256;
-      set_tile(m0, n0);
+      tile = item_tile(t, side);
+      m0 = (tile / gridN) * 256;
+      n0 = (tile % gridN) * 256;
+      set_tile(m0, n0, side);
 #pragma unroll
       for (int h = 0; h < 4; ++h) issue(h, 0);
     }
-    epilogue256_buf<STATS>(acc, a, rC, rS, cm0, cn0, wr, wc, fr, fg);
+    epilogue256_buf<STATS>(acc, a, rC, rS, cm0, cn0, wr, wc, fr, fg, HALF ? cside : 0);
     if (!more) break;
     extra = S_ST;
   }
@@ -1760,6 +1785,10 @@ bool nt_loop2() {
   const char* e = getenv("XCP_NT_LOOP");
   return e && e[0] == '2';
 }
+bool nt_half() {   // XCP_NT_HALF=1 (read per call; A/B)
+  const char* e = getenv("XCP_NT_HALF");
+  return e && e[0] == '1';
+}
 
 // XCP_NT_DYNQ=0: the persistent NT kernel walks its static tile list (A/B; read per call)
 bool nt_dynq() {
@@ -1819,11 +1848,16 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
     // round's tiles over whichever workgroups finish first; +0.2 % in the step, profiles/r05_nt_dynq_ab.txt;
     // XCP_NT_SPARSE_DGRAD=1 moves their sparse last round to the 128x128 kernel as before)
     const bool queued = tile == 0 && K >= 128 && !stats && nt_dynq();
-    if ((tile == 0 || tile == 4) && nt_sparse() && (!queued || nt_sparse_dgrad()) && tiles > cus && tiles % cus != 0 &&
-        (tiles % cus) * 4 < cus * 3)
+    const bool partial = tiles > cus && tiles % cus != 0 && (tiles % cus) * 4 < cus * 3;   // last round < 3/4 full
+    // XCP_NT_HALF=1: the last round's tiles as half tiles walked FIRST by the persistent kernel (every row on it;
+    // the half-tile workgroups run half a tile out of step with the rest, so the rounds' epilogue store bursts
+    // are split in two)
+    const bool halves = tile == 0 && persist && partial && K > 64 && nt_half() && !nt_loop2();
+    if ((tile == 0 || tile == 4) && !halves && nt_sparse() && (!queued || nt_sparse_dgrad()) && partial)
       mb = (tiles / cus) * cus / gridN;
     NTArgs big = a;
     big.M = min(M, mb * 256);
+    if (halves) big.nsplit = tiles % cus;
     const bool buf = ((long)(big.M - 1) * lda + K) * 2 <= BUF_LIMIT && ((long)(N - 1) * ldb + K) * 2 <= BUF_LIMIT;
     const bool cbuf = ((long)(big.M - 1) * ldc + N) * 2 <= BUF_LIMIT && (!stats || (long)xcp_cdiv(M, 128) * 2 * N * 4 <= BUF_LIMIT);
     if (persist && buf && cbuf) {   // persistent: one workgroup per CU walks the tiles
@@ -1838,10 +1872,15 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
           hipLaunchKernelGGL(gemm_nt256q_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
         else
           hipLaunchKernelGGL(gemm_nt256q_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
+      } else if (halves) {
+        if (stats)
+          hipLaunchKernelGGL((gemm_nt256p_kernel<true, true>), dim3(grid), dim3(512), 0, stream, big);
+        else
+          hipLaunchKernelGGL((gemm_nt256p_kernel<false, true>), dim3(grid), dim3(512), 0, stream, big);
       } else if (stats)
-        hipLaunchKernelGGL(gemm_nt256p_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
+        hipLaunchKernelGGL((gemm_nt256p_kernel<true, false>), dim3(grid), dim3(512), 0, stream, big);
       else
-        hipLaunchKernelGGL(gemm_nt256p_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
+        hipLaunchKernelGGL((gemm_nt256p_kernel<false, false>), dim3(grid), dim3(512), 0, stream, big);
     } else if (buf)
       hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(mb * gridN), dim3(512), 0, stream, big);
     else

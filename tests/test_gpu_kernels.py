@@ -1275,3 +1275,27 @@ def test_gemm_tn_loops_bitwise(ops, gpu, monkeypatch, M, N, K):
     ref = (G.float().t() @ X.float())
     got = outs[1].view(S, N, K).sum(0)
     torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("M,N,K,stats", [(92416, 736, 736, True), (92416, 736, 736, False), (256 * 100 + 7, 768, 200, True),
+                                         (256 * 100 + 7, 768, 392, False)])
+def test_gemm_nt_half_tiles_bitwise(ops, gpu, monkeypatch, M, N, K, stats):
+    """XCP_NT_HALF=1: the persistent kernel walks the last round's tiles as two half tiles each (only one
+    B half's quadrants and columns per half) before the whole tiles -- with the static walk (statistics) and
+    with the tile queue (none): output and statistics bits identical to the one-shot kernel for every row."""
+    monkeypatch.setenv("XCP_NT_HALF", "1")
+    g = torch.Generator(device=gpu).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
+    B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
+    R = ops.nt_stat_rows(M)
+    outs = []
+    for t in (2, 0, 0):   # (twice: the tile queue's counter must be reset by the first launch)
+        C = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
+        part = torch.full((R, 2, N), float("nan"), device=gpu) if stats else None
+        ops.gemm_nt(A, B, C, M, N, K, stats=part, tile=t)
+        outs.append((C, part))
+    torch.cuda.synchronize()
+    for C, part in outs[1:]:
+        assert torch.equal(outs[0][0], C)
+        if stats:
+            assert torch.equal(outs[0][1], part)

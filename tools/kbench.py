@@ -122,6 +122,33 @@ def main():
             flops=2.0 * M * C * C)
         rep("roofline op: dw_fwd 736 pitch act=2", timeit(lambda: ops.dw_fwd(2, Xp, Yp, Wtp, scp, shp, N, H, W, CP)),
             2 * (2 * M * C) + 36 * C)
+    if "dw_after" in sel:   # the 19^2 x 736 depthwise forward alone (its input re-read every launch) against
+        # right after the pointwise GEMM that writes its input (as in the step), timed by events around it only
+        CP = 736
+        Xp = torch.zeros(M, CP, device=dev, dtype=dt)
+        Xp[:, :C] = X
+        Yp, Zp = torch.empty_like(Xp), torch.empty_like(Xp)
+        Wpp = torch.zeros(CP, CP, device=dev, dtype=dt)
+        Wpp[:C, :C] = Wp
+        Wtp = torch.zeros(9, CP, device=dev)
+        Wtp[:, :C] = Wt
+        scp, shp = torch.zeros(CP, device=dev), torch.zeros(CP, device=dev)
+        scp[:C], shp[:C] = sc, sh
+        stp = torch.empty(ops.nt_stat_rows(M) * 2 * CP, device=dev)
+        ops.gemm_nt(Xp, Wpp, Yp, M, CP, CP, stats=stp)
+        rep("dw_fwd 736 pitch act=2 alone", timeit(lambda: ops.dw_fwd(2, Yp, Zp, Wtp, scp, shp, N, H, W, CP)), 2 * (2 * M * C))
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        for i in range(23):
+            ops.gemm_nt(Xp, Wpp, Yp, M, CP, CP, stats=stp)
+            if i >= 3:
+                evs[i - 3][0].record()
+            ops.dw_fwd(2, Yp, Zp, Wtp, scp, shp, N, H, W, CP)
+            if i >= 3:
+                evs[i - 3][1].record()
+        torch.cuda.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        rep("dw_fwd 736 pitch act=2 after its GEMM", ms, 2 * (2 * M * C))
+        del Xp, Yp, Zp
     if "ntprobe" in sel:   # the 256x256 NT kernel at the step's shape and at whole rounds (probe variants)
         CP = 736
         Xp = torch.zeros(M, CP, device=dev, dtype=dt)
