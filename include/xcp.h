@@ -270,7 +270,7 @@ int xcp_focal_ce(const float* Z, const long long* labels, const float* weights, 
  * XCP_LSTM_PERSIST=0) on per-step kernels while B fits their LDS budget).
  * kernel: 0 = automatic, 1 = the generic kernels.  xcp_lstm_bwd's work: max(B*H + 4*H*H, B*H*H/2)
  * floats (the per-step kernels' cell-gradient carry and a transposed W_hh; the persistent kernel's
- * double-buffered dh partials [2][H/4][B][H]). */
+ * double-buffered dh partials [2][B][H/4][H/4][4]). */
 int xcp_lstm_needs_whhT(int B, int H, int kernel);
 /* 1 if a persistent LSTM launch gave up waiting for its workgroups since the last call (its
  * outputs are then invalid; no wave spins forever), 0 if not, -1 on a HIP error.  Synchronises the

@@ -748,7 +748,9 @@ void lstm_fwd_persist_kernel(const float* __restrict__ xproj, const float* __res
 // by readlane) -- and publishes it (4 KB per clip, sc1); the next step gathers its 4 units' columns
 // of the G partials (16 B per clip and producer) and reduces them over the wave.  Per step and
 // workgroup: B x H x 4 B out and B x 16 x G B in (at B = 16, 32 KB each way) instead of B x 4H x 4 B in.
-// part: [2 (step parity)][G][B][H] fp32 (the caller's work buffer).
+// part: [2 (step parity)][B][H / 4 (unit group)][G (producer)][4] fp32 (the caller's work buffer): a reader's
+// gather (its unit group, every producer) is one contiguous 16 x G-byte run per clip, the writes are 16-B
+// pieces G x 16 B apart (fire-and-forget; only the publish waits for them).
 template <int H>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void lstm_bwd_persist_kernel(const float* __restrict__ dout, const float* __restrict__ dhn,
@@ -809,7 +811,8 @@ void lstm_bwd_persist_kernel(const float* __restrict__ dout, const float* __rest
           for (int e = 0; e < 2; ++e) {
             const int src = min(lane + 64 * e, G - 1);
             pv[c][e] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-                rP, (int)((((long)((t + 1) & 1) * pstride + ((long)src * B + b) * H + u0) * 4)), 0, LP_SC1));
+                rP, (int)((((long)((t + 1) & 1) * pstride + (((long)b * (H / 4) + blockIdx.x) * G + src) * 4) * 4)), 0,
+                LP_SC1));
           }
         }
         (void)pp;
@@ -862,12 +865,13 @@ void lstm_bwd_persist_kernel(const float* __restrict__ dout, const float* __rest
 #pragma unroll
             for (int i = 0; i < KL; ++i) acc[i] = fmaf(d, w[rr][i], acc[i]);
           }
-          if (bc < B) {
+          if (bc < B) {   // units k0 + i .. +3 = unit group (k0 + i) / 4 of this producer
 #pragma unroll
             for (int i = 0; i < KL; i += 4)
               __builtin_amdgcn_raw_buffer_store_b128(
                   __builtin_bit_cast(i32x4v, make_float4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3])), rP,
-                  (int)(((long)(t & 1) * pstride + ((long)blockIdx.x * B + bc) * H + k0 + i) * 4), 0, LP_SC1);
+                  (int)(((long)(t & 1) * pstride + (((long)bc * (H / 4) + (k0 + i) / 4) * G + blockIdx.x) * 4) * 4), 0,
+                  LP_SC1);
           }
           (void)pw;
         }

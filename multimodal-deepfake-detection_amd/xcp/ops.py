@@ -600,7 +600,7 @@ def lstm_sync_error():
 
 def lstm_bwd(dout, dhn, dcn, whh, cst, gates, dgates, B, T, H, kernel=0):
     # per-step kernels: cell-gradient carry [B][H] + W_hh^T [H][4H]; persistent kernels: the dh partials
-    # [2][H / 4][B][H] (include/xcp.h)
+    # [2][B][H / 4][H / 4][4] (include/xcp.h)
     work = torch.empty(max(B * H + 4 * H * H, B * H * H // 2), device=whh.device, dtype=torch.float32)
     _lib.call("xcp_lstm_bwd", _p(dout), _p(dhn), _p(dcn), _p(whh), _p(cst), _p(gates), _p(dgates), _p(work), B, T, H,
               kernel, stream())
