@@ -299,7 +299,7 @@ def pmc_traffic():
     steps = sorted(glob.glob(os.path.join(REPO, "profiles", "*_step_traffic.json")))
     if steps:
         data = json.load(open(steps[-1]))
-        cand = [v for v in data.values() if isinstance(v, dict) and v.get("base") == "gemm_tn256_kernel"]
+        cand = [v for v in data.values() if isinstance(v, dict) and v.get("base", "").startswith("gemm_tn256")]
         if cand:
             v = max(cand, key=lambda v: v["launches"])
             out["gemm_tn"] = (v["traffic_bytes"], f"{os.path.relpath(steps[-1], REPO)}: {v['kernel']} grid={v['grid']}, "
@@ -714,7 +714,8 @@ def main():
                     "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic.get("gemm_tn", (None,))[0],
                     "traffic_source": traffic.get("gemm_tn", (None, None))[1],
-                    "kernel": f"gemm_tn256_kernel (split-K weight gradient dW = dY^T X of the 728->728 pointwise @{hm}x{hm}, "
+                    "kernel": f"{'gemm_tn256_kernel' if os.environ.get('XCP_TN_LOOP') == '1' else 'gemm_tn256q_kernel'} "
+                              f"(split-K weight gradient dW = dY^T X of the 728->728 pointwise @{hm}x{hm}, "
                               f"side stream beside the backward's main stream; slab reduction not included)",
                     "flops_per_launch": flops, "avg_launch_ms": round(tn_ms, 4), "launches": timer.count("tn_728")}
         if timer is not None and getattr(timer, "separate", False):

@@ -654,8 +654,14 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     // (a half tile stores only its side: st0 holds the left 32 columns of the wave, st1 the right 32)
     const unsigned o0 = (mok && c0 < a.N && side != 2) ? rowb + (unsigned)c0 * 2 : BUF_OOB;
     const unsigned o1 = (mok && c0 + 32 < a.N && side != 1) ? rowb + (unsigned)(c0 + 32) * 2 : BUF_OOB;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 0);
+    // non-temporal (nt) C stores: the tile's 128 KB leave as streaming writes, so the round's 32 MB burst does
+    // not sit in the L2s as ordinary dirty lines ahead of the next kernel's reads (the depthwise forward that
+    // reads this output ran 0.433 -> 0.48 of HBM in the step, the op itself 130 -> 125 us, the step +0.9 %;
+    // sc1 write-through measured slower: profiles/r06_nt_cstore_ab.txt)
+    // (A/B: tools/exp/gemm_cnt.hip / gemm_csc1.hip were this file with the policy argument 2 / 16 instead of 0;
+    // a runtime-selected policy costs the persistent kernel 18 more spilled SGPRs, so it is fixed here)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 2);
   });
   if constexpr (STATS) {
     float u[16], v8[8], v4[4], v2[2];
