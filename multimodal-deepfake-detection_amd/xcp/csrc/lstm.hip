@@ -881,6 +881,105 @@ void lstm_bwd_persist_kernel(const float* __restrict__ dout, const float* __rest
   }
 }
 
+// Backward, gather form (XCP_LSTM_BWD=gather): each workgroup keeps its 4 units' COLUMNS of W_hh (lane l:
+// rows j = l*JL .. +JL, JL = 4H / 64) and gathers the whole dgates_{t+1} of its wave's 4 clips each step
+// (every 16-B sc1 load of the step issued before the first use: 512-register waves); per-lane FMA chains,
+// reduce-scatter over the wave; it publishes only its own dgates_t (16 floats per clip).
+template <int H>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void lstm_bwd_gather_kernel(const float* __restrict__ dout, const float* __restrict__ dhn,
+                            const float* __restrict__ dcn, const float* __restrict__ whh,
+                            const float* __restrict__ cst, const float* __restrict__ gates, float* dgates, int B,
+                            int T, LstmSync sy) {
+  constexpr int JL = 4 * H / 64, G4 = 4 * H;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int u0 = blockIdx.x * LP_U, j0 = lane * JL;
+  float w[JL][LP_U];
+#pragma unroll
+  for (int i = 0; i < JL; ++i) {
+    const float4 v4 = *reinterpret_cast<const float4*>(whh + (long)(j0 + i) * H + u0);
+    w[i][0] = v4.x; w[i][1] = v4.y; w[i][2] = v4.z; w[i][3] = v4.w;
+  }
+  const bool cell = (lane & 3) == 0;   // lane = c * 16 + u * 4 (clip c, unit u)
+  const int cu = (lane >> 2) & 3, k = u0 + cu;
+  const int npass = (B + 15) / 16;
+  float carry[2] = {0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(dgates, (short)0, 0x7fffffff, LP_CSP);
+  auto clip = [&](int p, int c) { return p * 16 + wv * 4 + c; };
+  for (int t = T - 1; t >= 0; --t) {
+    const bool last = t == T - 1;
+    float vc[2], vcp[2], vg[2][4], vdo[2], vhn[2], vcn[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int b = min(clip(p, lane >> 4), B - 1);
+      const long ob = ((long)b * T + t) * H + k, bk = (long)b * H + k;
+      vc[p] = cst[ob];
+      vcp[p] = cst[t > 0 ? ob - H : ob];
+      vdo[p] = *(dout ? dout + ob : cst + ob);
+      vhn[p] = *(dhn ? dhn + bk : cst + ob);
+      vcn[p] = *(dcn ? dcn + bk : cst + ob);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vg[p][q] = gates[((long)b * T + t) * G4 + q * H + k];
+      if (t == 0) vcp[p] = 0.f;
+      if (!dout) vdo[p] = 0.f;
+      if (!dhn) vhn[p] = 0.f;
+      if (!dcn) vcn[p] = 0.f;
+    }
+    if (!last && !lp_wait(sy, (unsigned)(T - 1 - t))) return;
+    for (int p = 0; p < npass; ++p) {
+      if (clip(p, 0) >= B) continue;   // (wave-uniform)
+      float part[4 * LP_U];
+      if (!last) {
+        float dg[4][JL];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int b = min(clip(p, c), B - 1);
+#pragma unroll
+          for (int i = 0; i < JL; i += 4) {
+            const float4 v4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                rG, (int)((((long)b * T + t + 1) * G4 + j0 + i) * 4), 0, LP_SC1));
+            dg[c][i] = v4.x; dg[c][i + 1] = v4.y; dg[c][i + 2] = v4.z; dg[c][i + 3] = v4.w;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int u = 0; u < LP_U; ++u) {
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < JL; i += 2) {
+              a0 = fmaf(dg[c][i], w[i][u], a0);
+              a1 = fmaf(dg[c][i + 1], w[i + 1][u], a1);
+            }
+            part[c * LP_U + u] = a0 + a1;
+          }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4 * LP_U; ++q) part[q] = 0.f;
+      }
+      const float rec = lp_rscatter(part, lane);   // clip lane >> 4, unit (lane >> 2) & 3
+      const int b = clip(p, lane >> 4);
+      if (cell && b < B) {
+        const float ig = vg[p][0], fg = vg[p][1], gg = vg[p][2], og = vg[p][3];
+        const float dhr = !last ? rec : vhn[p];
+        const float dcr = !last ? carry[p] : vcn[p];
+        const float dh = dhr + vdo[p];
+        const float tc = tanhf(vc[p]);
+        const float dO = dh * tc;
+        const float dc = dcr + dh * og * (1.f - tc * tc);
+        const float dI = dc * gg, dG = dc * ig, dF = dc * vcp[p];
+        carry[p] = dc * fg;
+        float* dgo = dgates + ((long)b * T + t) * G4;
+        lp_st(dgo + k, dI * ig * (1.f - ig));
+        lp_st(dgo + H + k, dF * fg * (1.f - fg));
+        lp_st(dgo + 2 * H + k, dG * (1.f - gg * gg));
+        lp_st(dgo + 3 * H + k, dO * og * (1.f - og));
+      }
+    }
+    if (t > 0) lp_publish(sy);
+  }
+}
+
 __device__ unsigned g_lstm_sync[64][8 * LP_SHARD + 32];   // per (device, stream) slot: shards, error word
 
 // Kernel choice (`kernel` argument: 0 = auto, 1 = the generic kernels, used by tests to pin
@@ -905,6 +1004,10 @@ int lstm_persist_mode() {
   return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 2 : 1;
 }
 bool lstm_persist_env(bool fwd) { return lstm_persist_mode() >= (fwd ? 1 : 2); }
+bool lstm_bwd_gather() {   // XCP_LSTM_BWD=gather: the persistent backward's gather form (A/B; read per call)
+  const char* e = getenv("XCP_LSTM_BWD");
+  return e && e[0] == 'g';
+}
 template <typename K>
 bool lp_resident(K kern, int G) {
   int dev = 0, cus = 0, per = 0;
@@ -1035,6 +1138,15 @@ int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const fl
     LstmSync sy;
     const int rc = lp_sync(st, sy);
     if (rc != XCP_OK) return rc;
+    if (lstm_bwd_gather()) {
+      if (H == 512)
+        hipLaunchKernelGGL(lstm_bwd_gather_kernel<512>, dim3(H / LP_U), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates,
+                           dgates, B, T, sy);
+      else
+        hipLaunchKernelGGL(lstm_bwd_gather_kernel<256>, dim3(H / LP_U), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates,
+                           dgates, B, T, sy);
+      return (int)hipGetLastError();
+    }
     if (!work) return XCP_EINVAL;
     if (H == 512)
       hipLaunchKernelGGL(lstm_bwd_persist_kernel<512>, dim3(H / LP_U), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates,

@@ -39,3 +39,6 @@ head -3 $(find gpurun_out/v2_gstep_a -name "*counter_collection.csv" | head -1) 
 python tools/pmc_compare.py "dw_fwd_w2|gemm_nt256p|dw_bwd_lds" step=$(find gpurun_out/v2_gstep_a -name "*counter_collection.csv" | head -1),$(find gpurun_out/v2_gstep_b -name "*counter_collection.csv" | head -1) alone=$(find gpurun_out/v2_giso_a -name "*counter_collection.csv" | head -1),$(find gpurun_out/v2_giso_b -name "*counter_collection.csv" | head -1) > gpurun_out/v2_dwpmc.txt 2>&1
 timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --cpu-baseline off --ddp-proxy 8 > gpurun_out/v2_proxy.json 2> gpurun_out/v2_proxy.err || exit $?
 find gpurun_out/v2_gstep_a gpurun_out/v2_gstep_b gpurun_out/v2_giso_a gpurun_out/v2_giso_b -name "*.csv" -size +3M -delete 2>/dev/null || true
+timeout -k 10 300 python -u tools/kbench.py vendor > gpurun_out/v2_vendor.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/lstm_ab.py 3 > gpurun_out/v2_lstmab.log 2>&1 || exit $?
+XCP_LSTM_BWD=gather XCP_LSTM_PERSIST=1 timeout -k 10 300 python -u -m pytest -p no:cacheprovider --timeout 200 --timeout-method thread -x -q tests/test_gpu_kernels.py -k "lstm" > gpurun_out/v2_lstmgather_tests.log 2>&1 || exit $?

@@ -122,6 +122,20 @@ def main():
             flops=2.0 * M * C * C)
         rep("roofline op: dw_fwd 736 pitch act=2", timeit(lambda: ops.dw_fwd(2, Xp, Yp, Wtp, scp, shp, N, H, W, CP)),
             2 * (2 * M * C) + 36 * C)
+    if "vendor" in sel:   # hipBLASLt (torch.matmul) on the middle-flow pointwise shape, against the xcp op
+        CP = 736
+        Xp = torch.zeros(M, CP, device=dev, dtype=dt)
+        Xp[:, :C] = X
+        Wpp = torch.zeros(CP, CP, device=dev, dtype=dt)
+        Wpp[:C, :C] = Wp
+        Yp = torch.empty_like(Xp)
+        stp = torch.empty(ops.nt_stat_rows(M) * 2 * CP, device=dev)
+        WT = Wpp.t().contiguous()
+        rep("hipBLASLt torch.matmul 92416x736x736", timeit(lambda: torch.matmul(Xp, WT, out=Yp)), flops=2.0 * M * C * C)
+        rep("xcp gemm_nt 92416x736x736 (no stats)", timeit(lambda: ops.gemm_nt(Xp, Wpp, Yp, M, CP, CP)), flops=2.0 * M * C * C)
+        rep("xcp gemm_nt 92416x736x736 +stats", timeit(lambda: ops.gemm_nt(Xp, Wpp, Yp, M, CP, CP, stats=stp)),
+            flops=2.0 * M * C * C)
+        del Xp, Yp
     if "dw_after" in sel:   # the 19^2 x 736 depthwise forward alone (its input re-read every launch) against
         # right after the pointwise GEMM that writes its input (as in the step), timed by events around it only
         CP = 736

@@ -45,18 +45,23 @@ def main():
         dg = torch.empty(B, T, G4, device=dev)
         fwd = lambda: ops.lstm_fwd(xp, whh, None, bih, bhh, out, hp, cs, gt, hn, cn, B, T, H)   # noqa: E731
         bwd = lambda: ops.lstm_bwd(dout, None, None, whh, cs, gt, dg, B, T, H)   # noqa: E731
-        t = {(f, d): [] for f in ("0", "1") for d in ("fwd", "bwd")}
+        forms = ("0", "1", "g")   # per-step kernels, persistent (backward: dh partials), persistent (backward: gather)
+        t = {(f, d): [] for f in forms for d in ("fwd", "bwd")}
         for _ in range(rounds):
-            for form in ("0", "1"):
-                os.environ["XCP_LSTM_PERSIST"] = form
+            for form in forms:
+                os.environ["XCP_LSTM_PERSIST"] = "0" if form == "0" else "1"
+                os.environ["XCP_LSTM_BWD"] = "gather" if form == "g" else "partials"
                 t[(form, "fwd")].append(timeit(fwd))
                 t[(form, "bwd")].append(timeit(bwd))
         err = ops.lstm_sync_error()
         for d in ("fwd", "bwd"):
-            a, b = statistics.median(t[("0", d)]), statistics.median(t[("1", d)])
+            a, b, c = (statistics.median(t[(f, d)]) for f in forms)
             print(f"B={B:2d} T={T} H={H} {d}: per-step {a:8.1f} us ({a / T:5.2f} us/step)  persistent {b:8.1f} us "
-                  f"({b / T:5.2f} us/step)  {(b / a - 1) * 100:+6.1f} %  sync_error={err}", flush=True)
+                  f"({b / T:5.2f} us/step, {(b / a - 1) * 100:+6.1f} %)" +
+                  (f"  gather {c:8.1f} us ({c / T:5.2f} us/step, {(c / a - 1) * 100:+6.1f} %)" if d == "bwd" else "") +
+                  f"  sync_error={err}", flush=True)
     os.environ.pop("XCP_LSTM_PERSIST", None)
+    os.environ.pop("XCP_LSTM_BWD", None)
 
 
 if __name__ == "__main__":
