@@ -144,6 +144,12 @@ REDUCE_BATCH = os.environ.get("XCP_REDUCE_BATCH", "1") != "0"
 # (csrc/sepfwd.hip): the depthwise output goes to the MFMAs through LDS instead of back through HBM
 # (XCP_SEP_FUSED=0: the two kernels; A/B)
 SEP_FUSED = os.environ.get("XCP_SEP_FUSED", "1") != "0"
+# ... from these frame widths on: the kernel computes whole 80-pixel half rows (two for 128 outputs, one
+# for 256) with four barriers each, so on narrow frames most of its work is padding and the per-row
+# barriers dominate (64^2 clips, block1 at 29^2: 848 us per launch against the two kernels' ~300, C4
+# line 1847 -> 2279 clips/s with the two kernels, profiles/r06_c4_ab.txt).  XCP_SEP_NARROW=1: every
+# width the kernel supports (A/B)
+SEP_MIN_W = {128: 0, 256: 0} if os.environ.get("XCP_SEP_NARROW", "0") == "1" else {128: 120, 256: 64}
 # the stem conv2 (forward and weight gradient) applies BN1 + ReLU on load instead of reading a
 # materialised relu(bn1(conv1)) (XCP_CONV2_ACTIN=0: bn_act + the plain conv; A/B)
 CONV2_ACT_ON_LOAD = os.environ.get("XCP_CONV2_ACTIN", "1") != "0"
@@ -437,7 +443,8 @@ class XceptionEngine:
         for u in b.units:
             d = self._empty(M * pc(u.cin))
             R = (ops.sep_fwd_parts(self.dtype, N, H, W, u.cin, u.cout)
-                 if SEP_FUSED and train and pc(u.cin) == u.cin and pc(u.cout) == u.cout else 0)
+                 if SEP_FUSED and train and pc(u.cin) == u.cin and pc(u.cout) == u.cout
+                 and W >= SEP_MIN_W.get(u.cout, 1 << 30) else 0)
             if R > 0:
                 y = self._empty(M * u.cout)
                 part = self._empty(R * 2 * u.cout, torch.float32)

@@ -122,6 +122,9 @@ def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn):
     from xcp import engine as engine_mod
     from Models.XceptionLSTMV import XceptionLSTMV
     monkeypatch.setattr(engine_mod, "RESBN", resbn)
+    # (71^2 frames: block1 at 33^2, narrower than the fused forward's default minimum; the call
+    # sequence is checked with it on, test_sep_fwd_width_gate checks the default)
+    monkeypatch.setattr(engine_mod, "SEP_MIN_W", {128: 0, 256: 0})
     torch.manual_seed(0)
     m = XceptionLSTMV(128, pretrained=False)
     if unfrozen:
@@ -159,6 +162,23 @@ def test_lstmv_step_call_sequence(fake_lib, monkeypatch, unfrozen, prec, resbn):
     assert fake_lib.count("xcp_sep_fwd") == (3 if prec == "bf16" else 0)
     assert fake_lib.count("xcp_dw_fwd") == 34 - fake_lib.count("xcp_sep_fwd")
     assert fake_lib.count("xcp_tail_fwd") == 12
+
+
+def test_sep_fwd_width_gate(fake_lib):
+    """block1's / block2's fused depthwise + pointwise forward only on frames wide enough for its
+    80-pixel half rows (engine.SEP_MIN_W): 71^2 clips (block1 at 33^2, block2 at 17^2) take the two
+    kernels, bitwise the same results (test_sep_fwd_vs_dw_and_gemm)"""
+    import xcp
+    from xcp import engine as engine_mod
+    from Models.XceptionLSTMV import XceptionLSTMV
+    assert engine_mod.SEP_MIN_W == {128: 120, 256: 64}
+    torch.manual_seed(0)
+    m = XceptionLSTMV(128, pretrained=False)
+    with xcp.precision("bf16"):
+        feats = m.extract_features(torch.rand(2, 3, 3, 71, 71), "cpu")
+        torch.nan_to_num(m(feats)).sum().backward()
+    assert fake_lib.count("xcp_sep_fwd") == 0
+    assert fake_lib.count("xcp_dw_fwd") == 34
 
 
 def test_weights_repacked_after_fused_optimizer_step(fake_lib):
