@@ -697,7 +697,15 @@ XCP_DEV void epilogue256_buf(f32x4 (&acc)[8][4], const NTArgs& a, __amdgpu_buffe
 // last and resets the counter for the next launch (graph replays included).
 __device__ int g_nt_tq[64];
 
-template <bool STATS, bool HALF>
+// PF2 (opt-in, XCP_NT_PF2=1; C bitwise equal, but the step measured 0.4-0.6 % slower and the in-step
+// middle-flow op 754 -> 738 TFLOP/s, the K = 128 entry shapes up to 11 % slower alone:
+// profiles/r06_nt_pf2_ab.txt): at a tile boundary the next tile's first TWO K-tiles (both ring slots) are issued ahead of this tile's
+// epilogue stores, so the stores stay in flight through the next tile's K-tile 0 and most of K-tile 1 (the
+// first wait that retires them is K-tile 1's phase Q3) instead of K-tile 0's Q3: the round's 32 MB store
+// burst gets two K-tiles to drain instead of one.  (The first tile has no stores ahead of it: its waits
+// count without them.  Dropped out-of-range stores in their place measured wrong C: their counts may retire
+// ahead of older loads.)
+template <bool STATS, bool HALF, bool PF2>
 __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   constexpr int S_ST = 16 + (STATS ? 1 : 0);   // store instructions per wave per epilogue
   // (+ 16 B for the tile-queue broadcast: in the ring's LDS object, since a second object would give the
@@ -805,13 +813,24 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
   set_tile(m0, n0, side);
 #pragma unroll
   for (int h = 0; h < 4; ++h) issue(h, 0);
+  if constexpr (PF2) {
+    if (nk > 1)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) issue(h, 1);
+  }
   int extra = 0;   // epilogue stores of the previous tile still allowed in flight during K-tile 0
   while (true) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (extra) vm_wait(S_ST);   // K-tile 0 landed (the previous epilogue's stores may still drain)
+    if constexpr (PF2) {   // K-tile 0 landed (K-tile 1's loads and the previous epilogue's stores may remain)
+      if (nk > 1) {
+        if (extra) vm_wait(8 + S_ST);
+        else vm_wait(8);
+      } else if (extra) vm_wait(S_ST);
+      else wait_vmcnt<0>();
+    } else if (extra) vm_wait(S_ST);   // K-tile 0 landed (the previous epilogue's stores may still drain)
     else wait_vmcnt<0>();
     // (thread 0) the queue position of the next tile, by inline asm: the compiler would wait for the
     // returned value at once (vmcnt(0), draining the prefetch).  Issued after the wait above and before
@@ -821,9 +840,14 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
       asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(nxt) : "v"(tq), "v"(1u) : "memory");
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();
-    // one 64-deep K-tile; FIRST (kt == 0): its data was retired by the wait above, so the two
-    // in-tile waits are skipped (they would otherwise also wait for the previous epilogue's stores)
-    auto ktile = [&](int kt, auto first) {
+    // one 64-deep K-tile.  MODE 1 (kt == 0): its data was retired by the wait above, so the two
+    // in-tile waits are skipped (they would otherwise also wait for the previous epilogue's stores);
+    // with PF2 it issues nothing (K-tile 1 is in flight) and its Q3 wait leaves the stores in flight.
+    // MODE 2 (PF2, kt == 1): the previous epilogue's S_ST stores sit between K-tile 1's loads and K-tile
+    // 2's, so its Q0 / Q1 waits allow S_ST more; its Q3 wait retires them.
+    auto ktile = [&](int kt, auto mode) {
+      constexpr int MODE = decltype(mode)::value;
+      constexpr bool ISSUE = !(PF2 && MODE == 1);
       const char* sa = smem + (kt & 1) * K_SLOT;
       const char* sb = sa + K_OP;
       const bool nxt = kt + 1 < nk;
@@ -836,32 +860,55 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
         for (int i = 0; i < 4; ++i)
           af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + i * 16 + fr, ks * 4 + fg));
       }
-      if (nxt) issue(0, kt + 1);
-      if constexpr (!decltype(first)::value) wait_cnt(2 + (nxt ? 2 : 0));   // B-right(kt) for Q1
+      if (ISSUE && nxt) issue(0, kt + 1);
+      if constexpr (MODE == 0) wait_cnt(2 + (nxt ? 2 : 0));   // B-right(kt) for Q1
+      if constexpr (MODE == 2) {
+        if (nxt) {
+          if (extra) vm_wait(4 + S_ST);
+          else vm_wait(4);
+        } else if (extra) vm_wait(2 + S_ST);
+        else vm_wait(2);
+      }
       sync_mfma(0, bl, 0);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           br[j][ks] = *reinterpret_cast<const bf16x8*>(sb + swz(wc * 64 + 32 + j * 16 + fr, ks * 4 + fg));
-      if (nxt) issue(1, kt + 1);
-      if constexpr (!decltype(first)::value) wait_cnt(nxt ? 4 : 0);         // A-bot(kt) for Q2
+      if (ISSUE && nxt) issue(1, kt + 1);
+      if constexpr (MODE == 0) wait_cnt(nxt ? 4 : 0);         // A-bot(kt) for Q2
+      if constexpr (MODE == 2) {   // (nk == 2: everything, the tile-queue fetch included, is retired here)
+        if (!nxt) wait_vmcnt<0>();
+        else if (extra) vm_wait(4 + S_ST);
+        else vm_wait(4);
+      }
       sync_mfma(0, br, 1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
-      if (nxt) issue(2, kt + 1);
+      if (ISSUE && nxt) issue(2, kt + 1);
       sync_mfma(1, br, 1);
       if (nxt) {
-        issue(3, kt + 1);
-        wait_cnt(4);   // A-top / B-left(kt+1) for Q0(kt+1); also retires the previous epilogue's stores
+        if constexpr (ISSUE) {
+          issue(3, kt + 1);
+          wait_cnt(4);   // A-top / B-left(kt+1) for Q0(kt+1); also retires the previous epilogue's stores
+        } else if (extra) {
+          vm_wait(4 + S_ST);   // A-top / B-left(1): B-right / A-bot(1) and the stores may remain
+        } else {
+          vm_wait(4);
+        }
       }
       sync_mfma(1, bl, 0);
     };
     ktile(0, IC<1>{});
-    for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
+    if constexpr (PF2) {
+      if (nk > 1) ktile(1, IC<2>{});
+      for (int kt = 2; kt < nk; ++kt) ktile(kt, IC<0>{});
+    } else {
+      for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
+    }
     if (wr == 0) __builtin_amdgcn_s_barrier();   // every wave is done reading both ring slots
     const int cm0 = m0, cn0 = n0, cside = side;
     if (tq) {
@@ -883,6 +930,11 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
       set_tile(m0, n0, side);
 #pragma unroll
       for (int h = 0; h < 4; ++h) issue(h, 0);
+      if constexpr (PF2) {
+        if (nk > 1)
+#pragma unroll
+          for (int h = 0; h < 4; ++h) issue(h, 1);
+      }
     }
     epilogue256_buf<STATS>(acc, a, rC, rS, cm0, cn0, wr, wc, fr, fg, HALF ? cside : 0);
     if (!more) break;
@@ -1791,6 +1843,10 @@ bool nt_loop2() {
   const char* e = getenv("XCP_NT_LOOP");
   return e && e[0] == '2';
 }
+bool nt_pf2() {   // XCP_NT_PF2=1: gemm_nt256p_kernel's two-K-tile prefetch at tile boundaries (read per call; A/B)
+  const char* e = getenv("XCP_NT_PF2");
+  return e && e[0] == '1';
+}
 bool nt_half() {   // XCP_NT_HALF=1 (read per call; A/B)
   const char* e = getenv("XCP_NT_HALF");
   return e && e[0] == '1';
@@ -1880,13 +1936,18 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
           hipLaunchKernelGGL(gemm_nt256q_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
       } else if (halves) {
         if (stats)
-          hipLaunchKernelGGL((gemm_nt256p_kernel<true, true>), dim3(grid), dim3(512), 0, stream, big);
+          hipLaunchKernelGGL((gemm_nt256p_kernel<true, true, false>), dim3(grid), dim3(512), 0, stream, big);
         else
-          hipLaunchKernelGGL((gemm_nt256p_kernel<false, true>), dim3(grid), dim3(512), 0, stream, big);
+          hipLaunchKernelGGL((gemm_nt256p_kernel<false, true, false>), dim3(grid), dim3(512), 0, stream, big);
+      } else if (nt_pf2()) {
+        if (stats)
+          hipLaunchKernelGGL((gemm_nt256p_kernel<true, false, true>), dim3(grid), dim3(512), 0, stream, big);
+        else
+          hipLaunchKernelGGL((gemm_nt256p_kernel<false, false, true>), dim3(grid), dim3(512), 0, stream, big);
       } else if (stats)
-        hipLaunchKernelGGL((gemm_nt256p_kernel<true, false>), dim3(grid), dim3(512), 0, stream, big);
+        hipLaunchKernelGGL((gemm_nt256p_kernel<true, false, false>), dim3(grid), dim3(512), 0, stream, big);
       else
-        hipLaunchKernelGGL((gemm_nt256p_kernel<false, false>), dim3(grid), dim3(512), 0, stream, big);
+        hipLaunchKernelGGL((gemm_nt256p_kernel<false, false, false>), dim3(grid), dim3(512), 0, stream, big);
     } else if (buf)
       hipLaunchKernelGGL(gemm_nt256k64_kernel<true>, dim3(mb * gridN), dim3(512), 0, stream, big);
     else

@@ -1277,13 +1277,16 @@ def test_gemm_tn_loops_bitwise(ops, gpu, monkeypatch, M, N, K):
     torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
 
 
+@pytest.mark.parametrize("form", ["XCP_NT_HALF", "XCP_NT_PF2"])
 @pytest.mark.parametrize("M,N,K,stats", [(92416, 736, 736, True), (92416, 736, 736, False), (256 * 100 + 7, 768, 200, True),
-                                         (256 * 100 + 7, 768, 392, False)])
-def test_gemm_nt_half_tiles_bitwise(ops, gpu, monkeypatch, M, N, K, stats):
+                                         (256 * 100 + 7, 768, 392, False), (256 * 300 + 5, 512, 128, False)])
+def test_gemm_nt_half_tiles_bitwise(ops, gpu, monkeypatch, M, N, K, stats, form):
     """XCP_NT_HALF=1: the persistent kernel walks the last round's tiles as two half tiles each (only one
-    B half's quadrants and columns per half) before the whole tiles -- with the static walk (statistics) and
-    with the tile queue (none): output and statistics bits identical to the one-shot kernel for every row."""
-    monkeypatch.setenv("XCP_NT_HALF", "1")
+    B half's quadrants and columns per half) before the whole tiles; XCP_NT_PF2=1: it issues the next tile's
+    first two K-tiles ahead of each epilogue (K = 128: two K-tiles, every wait of the second one's form) --
+    with the static walk (statistics) and with the tile queue (none): output and statistics bits identical
+    to the one-shot kernel for every row."""
+    monkeypatch.setenv(form, "1")
     g = torch.Generator(device=gpu).manual_seed(M + N + K)
     A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
     B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
