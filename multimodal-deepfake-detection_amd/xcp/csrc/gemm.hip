@@ -615,9 +615,14 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // epilogue256_regs with buffer stores (always issued; OOB offset for masked lanes):
 // 16 C stores per lane, + 1 statistics store when STATS
-template <bool STATS, typename Get>
-XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC, __amdgpu_buffer_rsrc_t rS, int m0,
-                             int n0, int wr, int wc, int fr, int fg, int side = 0) {
+// (FENCE: no instruction moves across a row block's end -- for accumulators in AGPRs, whose reads the
+// scheduler otherwise hoists all at once into VGPRs.  SKIP: a store whose every lane is out of range is not
+// issued (wave-uniform test), and the count of store instructions issued is returned: a store dropped whole by
+// the range check was seen to retire its vmcnt ahead of older loads, which a counted wait cannot allow for)
+template <bool STATS, typename Get, bool FENCE = false, bool SKIP = false>
+XCP_DEV int epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC, __amdgpu_buffer_rsrc_t rS, int m0,
+                            int n0, int wr, int wc, int fr, int fg, int side = 0) {
+  int issued = 0;
   const int bm = m0 / 256, stat_rows = (a.M + 127) / 128;
   const int mrow = m0 + wr * 128 + fr;
   const int ncol = n0 + wc * 64;
@@ -660,8 +665,21 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     // sc1 write-through measured slower: profiles/r06_nt_cstore_ab.txt)
     // (A/B: tools/exp/gemm_cnt.hip / gemm_csc1.hip were this file with the policy argument 2 / 16 instead of 0;
     // a runtime-selected policy costs the persistent kernel 18 more spilled SGPRs, so it is fixed here)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 2);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 2);
+    if constexpr (SKIP) {
+      const bool rows = m0 + wr * 128 + i * 16 < a.M;   // (wave-uniform: some row of the block in range)
+      if (rows && ncol < a.N) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 2);
+        ++issued;
+      }
+      if (rows && ncol + 32 < a.N) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 2);
+        ++issued;
+      }
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st0), rC, (int)o0, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, st1), rC, (int)o1, 0, 2);
+    }
+    if constexpr (FENCE) __builtin_amdgcn_sched_barrier(0);
   });
   if constexpr (STATS) {
     float u[16], v8[8], v4[4], v2[2];
@@ -679,8 +697,12 @@ XCP_DEV void epilogue256_get(Get acc, const NTArgs& a, __amdgpu_buffer_rsrc_t rC
     const bool sok = side == 0 || (side == 1) == (((fr & 7) >> 1) < 2);   // (a half tile: its side's columns)
     const unsigned so = (srow < stat_rows && col < a.N && sok)
                             ? (unsigned)((((long)srow * 2 + (fr >> 3)) * a.N + col) * 4) : BUF_OOB;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_float2(v2[0], v2[1])), rS, (int)so, 0, 0);
+    if (!SKIP || (bm * 2 + wr < stat_rows && ncol < a.N)) {
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(i32x2, make_float2(v2[0], v2[1])), rS, (int)so, 0, 0);
+      ++issued;
+    }
   }
+  return issued;
 }
 
 template <bool STATS>
@@ -940,6 +962,198 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
     if (!more) break;
     extra = S_ST;
   }
+}
+
+// ---------------------------------------------------------------------------------
+// Persistent 256x256 NT kernel at ONE wave per SIMD (gemm_nt4w_kernel; opt-in XCP_NT_4W=1 while measured).
+//
+// The 8-wave kernels above split a 256x256 tile into 128x64 wave tiles (two waves per SIMD) and pay
+// 8 s_barrier per 64-deep K-tile around 16-MFMA phases (profiles/r04_nt_probe.txt: that skeleton is
+// 0.45 us per K-tile over 0.86 us of MFMA issue).  Here 4 waves each own a 128x128 quarter (64
+// accumulators, 256 registers; 512 per wave at one wave per SIMD):
+//   * K advances in 32-deep steps through a 4-slot LDS ring (32 KB per step: A and B 256 rows x 64 B);
+//     steps g+1 .. g+3 are in flight while step g computes, and step g+4 is issued into g's slot;
+//   * ONE barrier per step: after it every wave's pieces of step g+1 have landed (each wave waits for
+//     its own by a counted vmcnt) and every wave has its step-g fragments in registers (lgkmcnt(0)
+//     before the barrier), so g's slot is refilled and g+1's fragments are read while g's 64 MFMAs
+//     run (fragments double-buffered in registers);
+//   * the fill is one continuous stream over the workgroup's tiles: a tile's last steps issue the next
+//     tile's first ones, so there is no per-tile prologue; the epilogue's stores (32 + 1 per wave) then
+//     stay in flight through the next tile's first three steps.  Past the walk's end the stream
+//     re-issues its last tile's first step (real loads), so every step counts the same instructions.
+// Operand images: rows of 64 B, 16-B chunk c of row r at chunk c ^ f((r >> 2) & 3), f = (0, 2, 3, 1):
+// every lane group of a ds_read_b128 fragment read (rows fr, chunks fg) then covers 16 distinct bank
+// quads.  LDS-DMA writes 16 B per lane at consecutive addresses, so the swizzle is applied to the
+// source: lane l of a piece fetches row (l >> 2), logical chunk (l & 3) ^ f(l >> 4).
+// C and the BN statistics: the 256p kernel's operand order, K order, epilogue packing and statistics
+// reduction tree, so both are bitwise equal to it.
+constexpr int W4_OP = 256 * 64;     // one operand of one 32-deep K-step (16 KB)
+constexpr int W4_SLOT = 2 * W4_OP;  // A + B
+constexpr int W4_NS = 4;
+
+XCP_DEV int w4_f(int q) { return (0x1320 >> (q * 4)) & 3; }
+// the MFMA by inline asm with the accumulator pinned to AGPRs and the operands to VGPRs: with 256 accumulator
+// registers and 128 fragment registers the builtin's register-class choice shuttled accumulators between the
+// two files (v_accvgpr_write / read around every MFMA, and spills).  hipcc pads no hazard for an asm MFMA:
+// the accumulators are zeroed >= 4 wait states before the first one reads them and read back only after an
+// s_nop pad (w4_pad), and the fragments come from ds_read (no VALU-write -> MFMA-read hazard)
+XCP_DEV void w4_mfma(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+XCP_DEV void w4_pad() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+XCP_DEV int w4_swz(int r, int c) { return r * 64 + ((c ^ w4_f((r >> 2) & 3)) << 4); }
+
+template <bool STATS, bool W4_ILV>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt4w_kernel(NTArgs a) {
+  constexpr bool w4_ilv = W4_ILV;
+  // the ring, then 16 KB of zeros: the fragments of a padding step are read from there
+  __shared__ __attribute__((aligned(16))) char smem[W4_NS * W4_SLOT + W4_OP];
+  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
+  const int tiles = gridM * gridN, nwg = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, nwg);
+  if (slot >= tiles) return;
+  for (int i = threadIdx.x; i < W4_OP / 16; i += 256)
+    reinterpret_cast<uint4*>(smem + W4_NS * W4_SLOT)[i] = make_uint4(0u, 0u, 0u, 0u);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  // 32-deep steps: nkr of them, walked as an even number nk (an odd count gets one more step that loads step 0's
+  // data again -- no load past K is ever issued whole -- and multiplies fragments read from the zero block:
+  // the accumulators start at +0, so adding the +-0 products leaves every bit as it was)
+  const int nkr = (a.K + 31) / 32, nk = (nkr + 1) & ~1;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, BUF_RECORDS, BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(STATS ? (void*)a.stats : a.C, (short)0,
+                                                                       BUF_RECORDS, BUF_DWORD3);
+  // ---- the fill stream: wave w loads rows w*64 .. w*64+63 of both operands, 4 pieces of 16 rows each
+  const int lrow = w * 64 + (lane >> 2);           // + 16 i
+  const int lc = (lane & 3) ^ w4_f(lane >> 4);    // logical chunk of this lane ((row >> 2) & 3 == lane >> 4)
+  unsigned va[4], vb[4];                          // this lane's chunk offsets in the fill tile (BUF_OOB: past M / N)
+  int dt = slot, dks = 0, nfill = 0;              // fill pointer: tile, step; steps issued
+  auto set_fill = [&](int t) __attribute__((always_inline)) {
+    const int m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ra = m0 + lrow + 16 * i, rb = n0 + lrow + 16 * i;
+      va[i] = ra < a.M ? (unsigned)(((long)ra * a.lda + lc * 8) * 2) : BUF_OOB;
+      vb[i] = rb < a.N ? (unsigned)(((long)rb * a.ldb + lc * 8) * 2) : BUF_OOB;
+    }
+  };
+  auto piece = [&](int q, int ks) __attribute__((always_inline)) {   // piece q (A 0..3, B 4..7) of step ks into slot nfill % 4
+    ks = ks < nkr ? ks : 0;
+    char* d = smem + (nfill & 3) * W4_SLOT + (q < 4 ? 0 : W4_OP) + (w * 64 + 16 * (q & 3)) * 64;
+    const unsigned v = q < 4 ? va[q & 3] : vb[q & 3];
+    const unsigned o = (ks * 32 + lc * 8 < a.K && v != BUF_OOB) ? v + ks * 64 : BUF_OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 4 ? rA : rB, (__attribute__((address_space(3))) void*)d, 16, o, 0, 0, 0);
+  };
+  auto fill_next = [&]() __attribute__((always_inline)) {   // (past the walk: the last tile's step 0 again)
+    ++nfill;
+    if (dt < tiles && ++dks == nk) {
+      dks = 0;
+      if (dt + nwg < tiles) {
+        dt += nwg;
+        set_fill(dt);
+      } else {
+        dt = tiles;
+      }
+    }
+  };
+  set_fill(dt);
+#pragma unroll 1
+  for (int s = 0; s < W4_NS; ++s) {
+    const int ks = dks;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) piece(q, ks);
+    fill_next();
+  }
+
+  f32x4 acc[8][8];
+  bf16x8 fa[2][8], fb[2][8];
+  auto read_frag_at = [&](auto P, int q, int sl) __attribute__((always_inline)) {   // fragments q of the step in slot sl % 4
+    const char* sa = smem + (sl & 3) * W4_SLOT;
+    fa[P][q] = *reinterpret_cast<const bf16x8*>(sa + w4_swz(wr * 128 + q * 16 + fr, fg));
+    fb[P][q] = *reinterpret_cast<const bf16x8*>(sa + W4_OP + w4_swz(wc * 128 + q * 16 + fr, fg));
+  };
+  auto read_frag = [&](auto P, int q, bool zero) __attribute__((always_inline)) {   // fragments q of the step in slot (nfill + 1) % 4
+    const char* sa = zero ? smem + W4_NS * W4_SLOT : smem + ((nfill + 1) & 3) * W4_SLOT;
+    const char* sb = zero ? smem + W4_NS * W4_SLOT : sa + W4_OP;
+    fa[P][q] = *reinterpret_cast<const bf16x8*>(sa + w4_swz(wr * 128 + q * 16 + fr, fg));
+    fb[P][q] = *reinterpret_cast<const bf16x8*>(sb + w4_swz(wc * 128 + q * 16 + fr, fg));
+  };
+  // step 0's fragments
+  vm_wait(24);
+  __builtin_amdgcn_s_barrier();
+  {
+    const char* sa = smem;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      fa[0][q] = *reinterpret_cast<const bf16x8*>(sa + w4_swz(wr * 128 + q * 16 + fr, fg));
+      fb[0][q] = *reinterpret_cast<const bf16x8*>(sa + W4_OP + w4_swz(wc * 128 + q * 16 + fr, fg));
+    }
+  }
+  // one step: fill step g+4 into g's slot, read g+1's fragments, g's 64 MFMAs (C: g's register set)
+  auto step = [&](auto C, bool zn) __attribute__((always_inline)) {   // (zn: the next step is a padding step)
+    constexpr int X = 1 - decltype(C)::value;
+    const int ks = dks;
+    static_for<0, 8>([&](auto q) __attribute__((always_inline)) {
+      piece(q, ks);
+      read_frag(IC<X>{}, q, zn);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w4_mfma(acc[q][j], fb[C][j], fa[C][q]);
+      if (w4_ilv) __builtin_amdgcn_sched_barrier(0);   // (W4_ILV: each group's piece and reads beside its MFMAs)
+    });
+    fill_next();
+  };
+  int st = 0;   // store instructions of the last epilogue (younger than the fills of a tile's first three steps)
+  // step ks of a tile: step g+1 landed (younger: steps g+2, g+3 and, for a tile's first three steps, the last
+  // epilogue's stores); this wave's step-g fragments are in registers (every wave's, after the barrier)
+  auto sync = [&](int ks) __attribute__((always_inline)) {
+    if (ks < 3) vm_wait(16 + st);
+    else vm_wait(16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // one tile: an even number of steps (K padded with zero chunks to a multiple of 64: the accumulators start at
+  // +0 and a zero product adds exactly nothing, so C is unchanged) alternating fragment sets 0 and 1; its last
+  // step reads the next tile's first fragments (already landed: the stream is continuous) into set 0
+  auto tile_body = [&](int t) __attribute__((always_inline)) {
+    const int m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    w4_pad();
+#pragma unroll 1
+    for (int ks = 0; ks < nk; ks += 2) {
+      sync(ks);
+      step(IC<0>{}, ks + 1 >= nkr);
+      __builtin_amdgcn_sched_barrier(0);
+      sync(ks + 1);
+      step(IC<1>{}, false);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    w4_pad();   // (the last MFMAs' results, before the epilogue reads the accumulators)
+    // ---- epilogue: the 256p kernel's, once per 64-column half of the wave's quarter (16-B nt stores of 8
+    // columns; BN partial sums per 128 rows, the same reduction tree, so C and the sums are bitwise its)
+    int ns = 0;
+    static_for<0, 2>([&](auto h) __attribute__((always_inline)) {
+      auto get = [&](int i, int j, int r) __attribute__((always_inline)) {   // one accumulator, AGPR -> VGPR
+        float v;
+        asm("v_accvgpr_read_b32 %0, %1" : "=v"(v) : "a"(acc[i][4 * h + j][r]));
+        return v;
+      };
+      ns += epilogue256_get<STATS, decltype(get), true, true>(get, a, rC, rS, m0, n0, wr, 2 * wc + h, fr, fg);
+    });
+    st = ns;
+  };
+#pragma unroll 1
+  for (int t = slot; t < tiles; t += nwg) tile_body(t);
+  vm_wait(0);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1843,6 +2057,14 @@ bool nt_loop2() {
   const char* e = getenv("XCP_NT_LOOP");
   return e && e[0] == '2';
 }
+bool nt_4w() {   // XCP_NT_4W=1 / 2: gemm_nt4w_kernel (one wave per SIMD) for the persistent calls from K = 128 (read per call; A/B)
+  const char* e = getenv("XCP_NT_4W");
+  return e && (e[0] == '1' || e[0] == '2');
+}
+bool nt_4w_ilv() {   // XCP_NT_4W=2: its steps fenced per 8-MFMA group
+  const char* e = getenv("XCP_NT_4W");
+  return e && e[0] == '2';
+}
 bool nt_pf2() {   // XCP_NT_PF2=1: gemm_nt256p_kernel's two-K-tile prefetch at tile boundaries (read per call; A/B)
   const char* e = getenv("XCP_NT_PF2");
   return e && e[0] == '1';
@@ -1939,6 +2161,16 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
           hipLaunchKernelGGL((gemm_nt256p_kernel<true, true, false>), dim3(grid), dim3(512), 0, stream, big);
         else
           hipLaunchKernelGGL((gemm_nt256p_kernel<false, true, false>), dim3(grid), dim3(512), 0, stream, big);
+      } else if (nt_4w() && K >= 128) {
+        const bool ilv = nt_4w_ilv();
+        if (stats && ilv)
+          hipLaunchKernelGGL((gemm_nt4w_kernel<true, true>), dim3(grid), dim3(256), 0, stream, big);
+        else if (stats)
+          hipLaunchKernelGGL((gemm_nt4w_kernel<true, false>), dim3(grid), dim3(256), 0, stream, big);
+        else if (ilv)
+          hipLaunchKernelGGL((gemm_nt4w_kernel<false, true>), dim3(grid), dim3(256), 0, stream, big);
+        else
+          hipLaunchKernelGGL((gemm_nt4w_kernel<false, false>), dim3(grid), dim3(256), 0, stream, big);
       } else if (nt_pf2()) {
         if (stats)
           hipLaunchKernelGGL((gemm_nt256p_kernel<true, false, true>), dim3(grid), dim3(512), 0, stream, big);

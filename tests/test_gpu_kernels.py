@@ -1277,25 +1277,29 @@ def test_gemm_tn_loops_bitwise(ops, gpu, monkeypatch, M, N, K):
     torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
 
 
-@pytest.mark.parametrize("form", ["XCP_NT_HALF", "XCP_NT_PF2"])
+@pytest.mark.parametrize("form", ["XCP_NT_HALF", "XCP_NT_PF2", "XCP_NT_4W"])
 @pytest.mark.parametrize("M,N,K,stats", [(92416, 736, 736, True), (92416, 736, 736, False), (256 * 100 + 7, 768, 200, True),
                                          (256 * 100 + 7, 768, 392, False), (256 * 300 + 5, 512, 128, False)])
 def test_gemm_nt_half_tiles_bitwise(ops, gpu, monkeypatch, M, N, K, stats, form):
     """XCP_NT_HALF=1: the persistent kernel walks the last round's tiles as two half tiles each (only one
     B half's quadrants and columns per half) before the whole tiles; XCP_NT_PF2=1: it issues the next tile's
-    first two K-tiles ahead of each epilogue (K = 128: two K-tiles, every wait of the second one's form) --
+    first two K-tiles ahead of each epilogue (K = 128: two K-tiles, every wait of the second one's form);
+    XCP_NT_4W=1: the one-wave-per-SIMD kernel (gemm_nt4w_kernel; K = 200 / 392 / 736: an odd number of
+    32-deep steps, padded by a step of zero fragments) --
     with the static walk (statistics) and with the tile queue (none): output and statistics bits identical
-    to the one-shot kernel for every row."""
-    monkeypatch.setenv(form, "1")
+    to the reference run for every row: the one-shot kernel for the half tiles (every row on the persistent
+    kernel), the default persistent kernel (same sparse last round on the 128x128 kernel) for the others."""
     g = torch.Generator(device=gpu).manual_seed(M + N + K)
     A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
     B = (torch.randn(N, K, device=gpu, generator=g) / K ** 0.5).bfloat16()
     R = ops.nt_stat_rows(M)
     outs = []
-    for t in (2, 0, 0):   # (twice: the tile queue's counter must be reset by the first launch)
+    for i, t in enumerate((2 if form == "XCP_NT_HALF" else 0, 0, 0)):   # (twice: the tile queue's counter must be reset)
+        monkeypatch.setenv(form, "1" if i else "0")
         C = torch.full((M, N), float("nan"), device=gpu, dtype=torch.bfloat16)
         part = torch.full((R, 2, N), float("nan"), device=gpu) if stats else None
         ops.gemm_nt(A, B, C, M, N, K, stats=part, tile=t)
+        torch.cuda.synchronize()
         outs.append((C, part))
     torch.cuda.synchronize()
     for C, part in outs[1:]:
