@@ -59,7 +59,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="replay the whole train step as one HIP graph (on: world size 1; auto = off, measured slower)")
+                    help="replay the whole train step as one HIP graph (on: world size 1; auto = on for lstma only, "
+                         "measured slower on the others)")
     ap.add_argument("--ddp-proxy", type=int, default=0, metavar="G",
                     help="world size 1 only: at every bucket-ready point launch a stand-in of a G-rank RCCL all-reduce "
                          "(xcp_comm_proxy) from the stream the real one would use, and report its timings "
@@ -112,10 +113,14 @@ def launch_ranks(args):
 
 def graph_mode(args, world):
     """Replay the train step as one HIP graph (--graph on; world size 1 only: the multi-rank step
-    launches RCCL collectives from inside the backward).  auto = off: measured 1.1 % slower than eager
-    launches (profiles/r04_graph_ab.txt) -- the replay spreads the step's nodes over four hardware
-    queues with a barrier on every cross-queue edge, and the kernel-to-kernel dispatch gaps stay."""
-    return args.graph == "on" and world == 1 and args.model != "auface"
+    launches RCCL collectives from inside the backward).  auto: on for the C4 line only.  The headline
+    step measured 1.1 % (round 4) and 4.6 % (round 6) slower replayed than launched eagerly
+    (profiles/r04_graph_ab.txt, r06_graph_ab.txt) -- the replay spreads the step's nodes over four
+    hardware queues with a barrier on every cross-queue edge; the C4 step (120 per-step LSTM backward
+    launches of ~8 us) +1.2 % replayed."""
+    if world != 1 or args.model == "auface":
+        return False
+    return args.graph == "on" or (args.graph == "auto" and args.model == "lstma")
 
 
 def middle_hw(size):
