@@ -1157,6 +1157,131 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 }
 
 // ---------------------------------------------------------------------------------
+// Persistent 256x256 NT kernel, 8 waves (two per SIMD, 128x64 each as the 256p kernel) on the 4W kernel's ring
+// (gemm_nt8w_kernel; opt-in XCP_NT_8W=1 while measured): 32-deep steps through 4 LDS slots, ONE barrier per
+// step, the fill one stream over the workgroup's tiles (each wave 4 LDS-DMA pieces per step).  No phase
+// structure: the two waves of a SIMD interleave by themselves, one's fill issue and fragment reads beside the
+// other's MFMAs.  A fragments roll (row block q's next-step fragment is read right after its last MFMA), B
+// fragments are double-buffered; padding step, store counting and epilogue as gemm_nt4w_kernel.
+template <bool STATS>
+__global__ __launch_bounds__(512) void gemm_nt8w_kernel(NTArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[W4_NS * W4_SLOT + W4_OP];
+  const int gridN = (a.N + 255) / 256, gridM = (a.M + 255) / 256;
+  const int tiles = gridM * gridN, nwg = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, nwg);
+  if (slot >= tiles) return;
+  for (int i = threadIdx.x; i < W4_OP / 16; i += 512)
+    reinterpret_cast<uint4*>(smem + W4_NS * W4_SLOT)[i] = make_uint4(0u, 0u, 0u, 0u);
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nkr = (a.K + 31) / 32, nk = (nkr + 1) & ~1;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.A), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.B), (short)0, BUF_RECORDS,
+                                                                       BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rC = __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, BUF_RECORDS, BUF_DWORD3);
+  const __amdgpu_buffer_rsrc_t rS = __builtin_amdgcn_make_buffer_rsrc(STATS ? (void*)a.stats : a.C, (short)0,
+                                                                       BUF_RECORDS, BUF_DWORD3);
+  // ---- the fill stream: wave w loads rows w*32 .. w*32+31 of both operands, 2 pieces of 16 rows each
+  const int lrow = w * 32 + (lane >> 2);
+  const int lc = (lane & 3) ^ w4_f(lane >> 4);
+  unsigned va[2], vb[2];
+  int dt = slot, dks = 0, nfill = 0;
+  auto set_fill = [&](int t) __attribute__((always_inline)) {
+    const int m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ra = m0 + lrow + 16 * i, rb = n0 + lrow + 16 * i;
+      va[i] = ra < a.M ? (unsigned)(((long)ra * a.lda + lc * 8) * 2) : BUF_OOB;
+      vb[i] = rb < a.N ? (unsigned)(((long)rb * a.ldb + lc * 8) * 2) : BUF_OOB;
+    }
+  };
+  auto piece = [&](int q, int ks) __attribute__((always_inline)) {   // piece q (A 0..1, B 2..3) into slot nfill % 4
+    ks = ks < nkr ? ks : 0;
+    char* d = smem + (nfill & 3) * W4_SLOT + (q < 2 ? 0 : W4_OP) + (w * 32 + 16 * (q & 1)) * 64;
+    const unsigned v = q < 2 ? va[q & 1] : vb[q & 1];
+    const unsigned o = (ks * 32 + lc * 8 < a.K && v != BUF_OOB) ? v + ks * 64 : BUF_OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(q < 2 ? rA : rB, (__attribute__((address_space(3))) void*)d, 16, o, 0, 0, 0);
+  };
+  auto fill_next = [&]() __attribute__((always_inline)) {
+    ++nfill;
+    if (dt < tiles && ++dks == nk) {
+      dks = 0;
+      if (dt + nwg < tiles) {
+        dt += nwg;
+        set_fill(dt);
+      } else {
+        dt = tiles;
+      }
+    }
+  };
+  set_fill(dt);
+#pragma unroll 1
+  for (int s = 0; s < W4_NS; ++s) {
+    const int ks = dks;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) piece(q, ks);
+    fill_next();
+  }
+  f32x4 acc[8][4];
+  bf16x8 fa[8], fb[2][4];
+  auto abase = [&](bool zero) __attribute__((always_inline)) {   // the step in slot (nfill + 1) % 4, or the zero block
+    return zero ? smem + W4_NS * W4_SLOT : smem + ((nfill + 1) & 3) * W4_SLOT;
+  };
+  vm_wait(12);
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) fa[q] = *reinterpret_cast<const bf16x8*>(smem + w4_swz(wr * 128 + q * 16 + fr, fg));
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    fb[0][j] = *reinterpret_cast<const bf16x8*>(smem + W4_OP + w4_swz(wc * 64 + j * 16 + fr, fg));
+  auto step = [&](auto C, bool zn) __attribute__((always_inline)) {   // (zn: the next step is a padding step)
+    constexpr int X = 1 - decltype(C)::value;
+    const int ks = dks;
+    const char* sa = abase(zn);
+    const char* sb = zn ? sa : sa + W4_OP;
+    static_for<0, 8>([&](auto q) __attribute__((always_inline)) {
+      if constexpr (q < 4) piece(q, ks);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[q][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[C][j], fa[q], acc[q][j], 0, 0, 0);
+      fa[q] = *reinterpret_cast<const bf16x8*>(sa + w4_swz(wr * 128 + q * 16 + fr, fg));
+      if constexpr (q < 4) fb[X][q] = *reinterpret_cast<const bf16x8*>(sb + w4_swz(wc * 64 + q * 16 + fr, fg));
+    });
+    fill_next();
+  };
+  int st = 0;   // store instructions of the last epilogue (younger than the fills of a tile's first three steps)
+  auto sync = [&](int ks) __attribute__((always_inline)) {
+    if (ks < 3) vm_wait(8 + st);
+    else vm_wait(8);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#pragma unroll 1
+  for (int t = slot; t < tiles; t += nwg) {
+    const int m0 = (t / gridN) * 256, n0 = (t % gridN) * 256;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int ks = 0; ks < nk; ks += 2) {
+      sync(ks);
+      step(IC<0>{}, ks + 1 >= nkr);
+      __builtin_amdgcn_sched_barrier(0);
+      sync(ks + 1);
+      step(IC<1>{}, false);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    auto get = [&](int i, int j, int r) __attribute__((always_inline)) { return acc[i][j][r]; };
+    st = epilogue256_get<STATS, decltype(get), false, true>(get, a, rC, rS, m0, n0, wr, wc, fr, fg);
+  }
+  vm_wait(0);
+}
+
+// ---------------------------------------------------------------------------------
 // Persistent 256x256 NT kernel, two MFMA phases per 64-deep K-tile and the fill issued ~1.5
 // K-tiles ahead (gemm_nt256q_kernel, the default; XCP_NT_LOOP=4 keeps gemm_nt256p_kernel).
 //
@@ -2057,6 +2182,10 @@ bool nt_loop2() {
   const char* e = getenv("XCP_NT_LOOP");
   return e && e[0] == '2';
 }
+bool nt_8w() {   // XCP_NT_8W=1: gemm_nt8w_kernel for the persistent calls from K = 128 (read per call; A/B)
+  const char* e = getenv("XCP_NT_8W");
+  return e && e[0] == '1';
+}
 bool nt_4w() {   // XCP_NT_4W=1 / 2: gemm_nt4w_kernel (one wave per SIMD) for the persistent calls from K = 128 (read per call; A/B)
   const char* e = getenv("XCP_NT_4W");
   return e && (e[0] == '1' || e[0] == '2');
@@ -2161,6 +2290,11 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
           hipLaunchKernelGGL((gemm_nt256p_kernel<true, true, false>), dim3(grid), dim3(512), 0, stream, big);
         else
           hipLaunchKernelGGL((gemm_nt256p_kernel<false, true, false>), dim3(grid), dim3(512), 0, stream, big);
+      } else if (nt_8w() && K >= 128) {
+        if (stats)
+          hipLaunchKernelGGL(gemm_nt8w_kernel<true>, dim3(grid), dim3(512), 0, stream, big);
+        else
+          hipLaunchKernelGGL(gemm_nt8w_kernel<false>, dim3(grid), dim3(512), 0, stream, big);
       } else if (nt_4w() && K >= 128) {
         const bool ilv = nt_4w_ilv();
         if (stats && ilv)

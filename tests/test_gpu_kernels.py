@@ -1277,7 +1277,7 @@ def test_gemm_tn_loops_bitwise(ops, gpu, monkeypatch, M, N, K):
     torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
 
 
-@pytest.mark.parametrize("form", ["XCP_NT_HALF", "XCP_NT_PF2", "XCP_NT_4W"])
+@pytest.mark.parametrize("form", ["XCP_NT_HALF", "XCP_NT_PF2", "XCP_NT_4W", "XCP_NT_8W"])
 @pytest.mark.parametrize("M,N,K,stats", [(92416, 736, 736, True), (92416, 736, 736, False), (256 * 100 + 7, 768, 200, True),
                                          (256 * 100 + 7, 768, 392, False), (256 * 300 + 5, 512, 128, False)])
 def test_gemm_nt_half_tiles_bitwise(ops, gpu, monkeypatch, M, N, K, stats, form):
