@@ -980,6 +980,96 @@ void lstm_bwd_gather_kernel(const float* __restrict__ dout, const float* __restr
   }
 }
 
+// Backward, clip-grouped gather form (XCP_LSTM_BWD=cg): the gather kernel's workgroups split by clips as
+// well -- workgroup (unit group ug, clip group cg) keeps its 4 units' columns of W_hh and each of its 4
+// waves gathers one clip's dgates_{t+1} (8 16-B sc1 loads per lane instead of 32), so a step's gather
+// latency is a quarter of the gather kernel's, at H / 4 x ceil(B / 4) workgroups (two per CU at B = 16,
+// H = 512: 128-VGPR weights + one clip's 32 dgates per lane fit the 256 registers of two waves per SIMD).
+// Per-lane partial chains, reduce-scatter tree and cell update are the gather kernel's, so dgates are
+// bitwise its.
+template <int H>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void lstm_bwd_cg_kernel(const float* __restrict__ dout, const float* __restrict__ dhn,
+                        const float* __restrict__ dcn, const float* __restrict__ whh,
+                        const float* __restrict__ cst, const float* __restrict__ gates, float* dgates, int B,
+                        int T, LstmSync sy) {
+  constexpr int JL = 4 * H / 64, G4 = 4 * H, NG = H / LP_U;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ug = blockIdx.x % NG, cgp = blockIdx.x / NG;
+  const int u0 = ug * LP_U, j0 = lane * JL;
+  float w[JL][LP_U];
+#pragma unroll
+  for (int i = 0; i < JL; ++i) {
+    const float4 v4 = *reinterpret_cast<const float4*>(whh + (long)(j0 + i) * H + u0);
+    w[i][0] = v4.x; w[i][1] = v4.y; w[i][2] = v4.z; w[i][3] = v4.w;
+  }
+  const int b = cgp * 4 + wv;              // this wave's clip (waves past B idle, but keep every barrier)
+  const bool bok = b < B;
+  const int bb = bok ? b : B - 1;
+  const bool cell = (lane & 15) == 0;      // lane = u * 16 (unit u of this wave's clip)
+  const int k = u0 + (lane >> 4);
+  float carry = 0.f;
+  const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(dgates, (short)0, 0x7fffffff, LP_CSP);
+  for (int t = T - 1; t >= 0; --t) {
+    const bool last = t == T - 1;
+    const long ob = ((long)bb * T + t) * H + k, bk = (long)bb * H + k;
+    const float vc = cst[ob];
+    float vcp = cst[t > 0 ? ob - H : ob];
+    float vdo = *(dout ? dout + ob : cst + ob);
+    float vhn = *(dhn ? dhn + bk : cst + ob);
+    float vcn = *(dcn ? dcn + bk : cst + ob);
+    float vg[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vg[q] = gates[((long)bb * T + t) * G4 + q * H + k];
+    if (t == 0) vcp = 0.f;
+    if (!dout) vdo = 0.f;
+    if (!dhn) vhn = 0.f;
+    if (!dcn) vcn = 0.f;
+    if (!last && !lp_wait(sy, (unsigned)(T - 1 - t))) return;
+    float part[LP_U];
+    if (!last) {
+      float dg[JL];
+#pragma unroll
+      for (int i = 0; i < JL; i += 4) {
+        const float4 v4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+            rG, (int)((((long)bb * T + t + 1) * G4 + j0 + i) * 4), 0, LP_SC1));
+        dg[i] = v4.x; dg[i + 1] = v4.y; dg[i + 2] = v4.z; dg[i + 3] = v4.w;
+      }
+#pragma unroll
+      for (int u = 0; u < LP_U; ++u) {
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < JL; i += 2) {
+          a0 = fmaf(dg[i], w[i][u], a0);
+          a1 = fmaf(dg[i + 1], w[i + 1][u], a1);
+        }
+        part[u] = a0 + a1;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < LP_U; ++u) part[u] = 0.f;
+    }
+    const float rec = lp_rscatter(part, lane);   // unit lane >> 4
+    if (cell && bok) {
+      const float ig = vg[0], fg = vg[1], gg = vg[2], og = vg[3];
+      const float dhr = !last ? rec : vhn;
+      const float dcr = !last ? carry : vcn;
+      const float dh = dhr + vdo;
+      const float tc = tanhf(vc);
+      const float dO = dh * tc;
+      const float dc = dcr + dh * og * (1.f - tc * tc);
+      const float dI = dc * gg, dG = dc * ig, dF = dc * vcp;
+      carry = dc * fg;
+      float* dgo = dgates + ((long)b * T + t) * G4;
+      lp_st(dgo + k, dI * ig * (1.f - ig));
+      lp_st(dgo + H + k, dF * fg * (1.f - fg));
+      lp_st(dgo + 2 * H + k, dG * (1.f - gg * gg));
+      lp_st(dgo + 3 * H + k, dO * og * (1.f - og));
+    }
+    if (t > 0) lp_publish(sy);
+  }
+}
+
 __device__ unsigned g_lstm_sync[64][8 * LP_SHARD + 32];   // per (device, stream) slot: shards, error word
 
 // Kernel choice (`kernel` argument: 0 = auto, 1 = the generic kernels, used by tests to pin
@@ -998,7 +1088,8 @@ bool lstm_step(int B, int H, int kernel) {
 // occupancy query).  Default: the forward only -- at XceptionLSTMA's shape (B 16, T 120, H 512) it runs 4.6 us
 // per step against the per-step kernels' 6.3; the persistent backward (published dh partials) is faster at
 // small B (3.9 vs 4.6 us per step at B 2) but slower at B 16 (9.5 vs 7.3: the partials' sc1 traffic), so the
-// per-step backward stays (profiles/r06_lstm_ab.txt).  XCP_LSTM_PERSIST=0: neither, 1: both (read per call).
+// per-step backward stays there (profiles/r06_lstm_ab.txt); where the clip-grouped backward's workgroups fit
+// one per CU it is the default (xcp_lstm_bwd).  XCP_LSTM_PERSIST=0: neither, 1: both (read per call).
 int lstm_persist_mode() {
   const char* e = getenv("XCP_LSTM_PERSIST");
   return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 2 : 1;
@@ -1007,6 +1098,22 @@ bool lstm_persist_env(bool fwd) { return lstm_persist_mode() >= (fwd ? 1 : 2); }
 bool lstm_bwd_gather() {   // XCP_LSTM_BWD=gather: the persistent backward's gather form (A/B; read per call)
   const char* e = getenv("XCP_LSTM_BWD");
   return e && e[0] == 'g';
+}
+bool lstm_bwd_cg() {   // XCP_LSTM_BWD=cg: the clip-grouped gather form (A/B; read per call)
+  const char* e = getenv("XCP_LSTM_BWD");
+  return e && e[0] == 'c' && e[1] == 'g';
+}
+bool lstm_cg_default(int B, int H, int kernel) {
+  return kernel == 0 && B <= 32 && (H == 256 || H == 512) && lstm_persist_mode() == 1 && !getenv("XCP_LSTM_BWD");
+}
+int lp_cus() {
+  static const int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return n;
+  }();
+  return v;
 }
 template <typename K>
 bool lp_resident(K kern, int G) {
@@ -1134,7 +1241,28 @@ int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const fl
                  const float* gates, float* dgates, float* work, int B, int T, int H, int kernel, hipStream_t st) {
   if (B <= 0 || T <= 0) return XCP_OK;
   if (kernel < 0 || kernel > 1) return XCP_EINVAL;
+  const int gcg = (H / LP_U) * ((B + 3) / 4);   // clip-grouped form's workgroups
+  auto launch_cg = [&]() {
+    LstmSync sy;
+    const int rc = lp_sync(st, sy);
+    if (rc != XCP_OK) return rc;
+    if (H == 512)
+      hipLaunchKernelGGL(lstm_bwd_cg_kernel<512>, dim3(gcg), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates, dgates, B,
+                         T, sy);
+    else
+      hipLaunchKernelGGL(lstm_bwd_cg_kernel<256>, dim3(gcg), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates, dgates, B,
+                         T, sy);
+    return (int)hipGetLastError();
+  };
+  // default (XCP_LSTM_PERSIST and XCP_LSTM_BWD unset): the clip-grouped persistent backward where its workgroups fit
+  // one per CU (H = 512 up to 8 clips, H = 256 up to 16): 30-47 % faster than the per-step kernels there; at
+  // XceptionLSTMA's B 16 x H 512 (512 workgroups) the per-step kernels stay (profiles/r06_lstm_cg_ab.txt)
+  if (lstm_cg_default(B, H, kernel) && gcg <= lp_cus() &&
+      (H == 512 ? lp_resident(lstm_bwd_cg_kernel<512>, gcg) : lp_resident(lstm_bwd_cg_kernel<256>, gcg)))
+    return launch_cg();
   if (lstm_persist(B, H, kernel, false)) {
+    if (lstm_bwd_cg() && (H == 512 ? lp_resident(lstm_bwd_cg_kernel<512>, gcg) : lp_resident(lstm_bwd_cg_kernel<256>, gcg)))
+      return launch_cg();
     LstmSync sy;
     const int rc = lp_sync(st, sy);
     if (rc != XCP_OK) return rc;

@@ -45,20 +45,22 @@ def main():
         dg = torch.empty(B, T, G4, device=dev)
         fwd = lambda: ops.lstm_fwd(xp, whh, None, bih, bhh, out, hp, cs, gt, hn, cn, B, T, H)   # noqa: E731
         bwd = lambda: ops.lstm_bwd(dout, None, None, whh, cs, gt, dg, B, T, H)   # noqa: E731
-        forms = ("0", "1", "g")   # per-step kernels, persistent (backward: dh partials), persistent (backward: gather)
+        # per-step kernels, persistent (backward: dh partials), persistent (backward: gather), (backward: clip-grouped gather)
+        forms = ("0", "1", "g", "c")
         t = {(f, d): [] for f in forms for d in ("fwd", "bwd")}
         for _ in range(rounds):
             for form in forms:
                 os.environ["XCP_LSTM_PERSIST"] = "0" if form == "0" else "1"
-                os.environ["XCP_LSTM_BWD"] = "gather" if form == "g" else "partials"
+                os.environ["XCP_LSTM_BWD"] = {"g": "gather", "c": "cg"}.get(form, "partials")
                 t[(form, "fwd")].append(timeit(fwd))
                 t[(form, "bwd")].append(timeit(bwd))
         err = ops.lstm_sync_error()
         for d in ("fwd", "bwd"):
-            a, b, c = (statistics.median(t[(f, d)]) for f in forms)
+            a, b, c, cg = (statistics.median(t[(f, d)]) for f in forms)
             print(f"B={B:2d} T={T} H={H} {d}: per-step {a:8.1f} us ({a / T:5.2f} us/step)  persistent {b:8.1f} us "
                   f"({b / T:5.2f} us/step, {(b / a - 1) * 100:+6.1f} %)" +
-                  (f"  gather {c:8.1f} us ({c / T:5.2f} us/step, {(c / a - 1) * 100:+6.1f} %)" if d == "bwd" else "") +
+                  (f"  gather {c:8.1f} us ({c / T:5.2f} us/step, {(c / a - 1) * 100:+6.1f} %)"
+                   f"  clip-grouped {cg:8.1f} us ({cg / T:5.2f} us/step, {(cg / a - 1) * 100:+6.1f} %)" if d == "bwd" else "") +
                   f"  sync_error={err}", flush=True)
     os.environ.pop("XCP_LSTM_PERSIST", None)
     os.environ.pop("XCP_LSTM_BWD", None)
