@@ -980,20 +980,22 @@ void lstm_bwd_gather_kernel(const float* __restrict__ dout, const float* __restr
   }
 }
 
-// Backward, clip-grouped gather form (XCP_LSTM_BWD=cg): the gather kernel's workgroups split by clips as
+// Backward, clip-grouped gather form (XCP_LSTM_BWD=cg / cg2): the gather kernel's workgroups split by clips as
 // well -- workgroup (unit group ug, clip group cg) keeps its 4 units' columns of W_hh and each of its 4
-// waves gathers one clip's dgates_{t+1} (8 16-B sc1 loads per lane instead of 32), so a step's gather
-// latency is a quarter of the gather kernel's, at H / 4 x ceil(B / 4) workgroups (two per CU at B = 16,
-// H = 512: 128-VGPR weights + one clip's 32 dgates per lane fit the 256 registers of two waves per SIMD).
+// waves gathers CPW clips' dgates_{t+1} (8 CPW 16-B sc1 loads per lane instead of 32), at H / 4 x
+// ceil(B / (4 CPW)) workgroups (CPW 1: two per CU at B = 16, H = 512 -- 128-VGPR weights + one clip's 32
+// dgates per lane fit the 256 registers of two waves per SIMD; CPW 2: one per CU).  CPW = 4 with one clip
+// group is the gather kernel.
 // Per-lane partial chains, reduce-scatter tree and cell update are the gather kernel's, so dgates are
 // bitwise its.
-template <int H>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+template <int H, int CPW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CPW == 1 ? 2 : 1, CPW == 1 ? 2 : 1)))
 void lstm_bwd_cg_kernel(const float* __restrict__ dout, const float* __restrict__ dhn,
                         const float* __restrict__ dcn, const float* __restrict__ whh,
                         const float* __restrict__ cst, const float* __restrict__ gates, float* dgates, int B,
                         int T, LstmSync sy) {
-  constexpr int JL = 4 * H / 64, G4 = 4 * H, NG = H / LP_U;
+  constexpr int JL = 4 * H / 64, G4 = 4 * H, NG = H / LP_U, NP = CPW * LP_U;
+  constexpr int SH = CPW == 1 ? 4 : CPW == 2 ? 3 : 2;   // lane >> SH: index c * LP_U + u after the reduce-scatter
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ug = blockIdx.x % NG, cgp = blockIdx.x / NG;
   const int u0 = ug * LP_U, j0 = lane * JL;
@@ -1003,11 +1005,13 @@ void lstm_bwd_cg_kernel(const float* __restrict__ dout, const float* __restrict_
     const float4 v4 = *reinterpret_cast<const float4*>(whh + (long)(j0 + i) * H + u0);
     w[i][0] = v4.x; w[i][1] = v4.y; w[i][2] = v4.z; w[i][3] = v4.w;
   }
-  const int b = cgp * 4 + wv;              // this wave's clip (waves past B idle, but keep every barrier)
+  // this wave's clips (cgp * 4 + wv) * CPW + c; clips past B idle, but keep every barrier
+  const int cb = (cgp * 4 + wv) * CPW;
+  const int idx = lane >> SH;
+  const bool cell = (lane & ((1 << SH) - 1)) == 0;   // lane = (c * LP_U + u) << SH
+  const int b = cb + idx / LP_U, k = u0 + idx % LP_U;
   const bool bok = b < B;
   const int bb = bok ? b : B - 1;
-  const bool cell = (lane & 15) == 0;      // lane = u * 16 (unit u of this wave's clip)
-  const int k = u0 + (lane >> 4);
   float carry = 0.f;
   const __amdgpu_buffer_rsrc_t rG = __builtin_amdgcn_make_buffer_rsrc(dgates, (short)0, 0x7fffffff, LP_CSP);
   for (int t = T - 1; t >= 0; --t) {
@@ -1026,30 +1030,36 @@ void lstm_bwd_cg_kernel(const float* __restrict__ dout, const float* __restrict_
     if (!dhn) vhn = 0.f;
     if (!dcn) vcn = 0.f;
     if (!last && !lp_wait(sy, (unsigned)(T - 1 - t))) return;
-    float part[LP_U];
+    float part[NP];
     if (!last) {
-      float dg[JL];
+      float dg[CPW][JL];
 #pragma unroll
-      for (int i = 0; i < JL; i += 4) {
-        const float4 v4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
-            rG, (int)((((long)bb * T + t + 1) * G4 + j0 + i) * 4), 0, LP_SC1));
-        dg[i] = v4.x; dg[i + 1] = v4.y; dg[i + 2] = v4.z; dg[i + 3] = v4.w;
-      }
+      for (int c = 0; c < CPW; ++c) {
+        const int bc = min(cb + c, B - 1);
 #pragma unroll
-      for (int u = 0; u < LP_U; ++u) {
-        float a0 = 0.f, a1 = 0.f;
-#pragma unroll
-        for (int i = 0; i < JL; i += 2) {
-          a0 = fmaf(dg[i], w[i][u], a0);
-          a1 = fmaf(dg[i + 1], w[i + 1][u], a1);
+        for (int i = 0; i < JL; i += 4) {
+          const float4 v4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+              rG, (int)((((long)bc * T + t + 1) * G4 + j0 + i) * 4), 0, LP_SC1));
+          dg[c][i] = v4.x; dg[c][i + 1] = v4.y; dg[c][i + 2] = v4.z; dg[c][i + 3] = v4.w;
         }
-        part[u] = a0 + a1;
       }
+#pragma unroll
+      for (int c = 0; c < CPW; ++c)
+#pragma unroll
+        for (int u = 0; u < LP_U; ++u) {
+          float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+          for (int i = 0; i < JL; i += 2) {
+            a0 = fmaf(dg[c][i], w[i][u], a0);
+            a1 = fmaf(dg[c][i + 1], w[i + 1][u], a1);
+          }
+          part[c * LP_U + u] = a0 + a1;
+        }
     } else {
 #pragma unroll
-      for (int u = 0; u < LP_U; ++u) part[u] = 0.f;
+      for (int q = 0; q < NP; ++q) part[q] = 0.f;
     }
-    const float rec = lp_rscatter(part, lane);   // unit lane >> 4
+    const float rec = lp_rscatter(part, lane);   // index lane >> SH
     if (cell && bok) {
       const float ig = vg[0], fg = vg[1], gg = vg[2], og = vg[3];
       const float dhr = !last ? rec : vhn;
@@ -1088,8 +1098,8 @@ bool lstm_step(int B, int H, int kernel) {
 // occupancy query).  Default: the forward only -- at XceptionLSTMA's shape (B 16, T 120, H 512) it runs 4.6 us
 // per step against the per-step kernels' 6.3; the persistent backward (published dh partials) is faster at
 // small B (3.9 vs 4.6 us per step at B 2) but slower at B 16 (9.5 vs 7.3: the partials' sc1 traffic), so the
-// per-step backward stays there (profiles/r06_lstm_ab.txt); where the clip-grouped backward's workgroups fit
-// one per CU it is the default (xcp_lstm_bwd).  XCP_LSTM_PERSIST=0: neither, 1: both (read per call).
+// per-step backward stays there (profiles/r06_lstm_ab.txt); where the clip-grouped backward's workgroups take
+// at most half the CUs it is the default (xcp_lstm_bwd).  XCP_LSTM_PERSIST=0: neither, 1: both (read per call).
 int lstm_persist_mode() {
   const char* e = getenv("XCP_LSTM_PERSIST");
   return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 2 : 1;
@@ -1099,9 +1109,10 @@ bool lstm_bwd_gather() {   // XCP_LSTM_BWD=gather: the persistent backward's gat
   const char* e = getenv("XCP_LSTM_BWD");
   return e && e[0] == 'g';
 }
-bool lstm_bwd_cg() {   // XCP_LSTM_BWD=cg: the clip-grouped gather form (A/B; read per call)
+int lstm_bwd_cg() {   // XCP_LSTM_BWD=cg / cg2: the clip-grouped gather form, 1 / 2 clips per wave (A/B; read per call)
   const char* e = getenv("XCP_LSTM_BWD");
-  return e && e[0] == 'c' && e[1] == 'g';
+  if (!(e && e[0] == 'c' && e[1] == 'g')) return 0;
+  return e[2] == '2' ? 2 : 1;
 }
 bool lstm_cg_default(int B, int H, int kernel) {
   return kernel == 0 && B <= 32 && (H == 256 || H == 512) && lstm_persist_mode() == 1 && !getenv("XCP_LSTM_BWD");
@@ -1241,28 +1252,35 @@ int xcp_lstm_bwd(const float* dout, const float* dhn, const float* dcn, const fl
                  const float* gates, float* dgates, float* work, int B, int T, int H, int kernel, hipStream_t st) {
   if (B <= 0 || T <= 0) return XCP_OK;
   if (kernel < 0 || kernel > 1) return XCP_EINVAL;
-  const int gcg = (H / LP_U) * ((B + 3) / 4);   // clip-grouped form's workgroups
-  auto launch_cg = [&]() {
+  // clip-grouped form: cpw clips per wave, H / 4 x ceil(B / (4 cpw)) workgroups, if they can all be resident
+  auto cg_grid = [&](int cpw) { return (H / LP_U) * ((B + 4 * cpw - 1) / (4 * cpw)); };
+  auto cg_fits = [&](int cpw) {
+    const int g = cg_grid(cpw);
+    if (cpw == 1) return H == 512 ? lp_resident(lstm_bwd_cg_kernel<512, 1>, g) : lp_resident(lstm_bwd_cg_kernel<256, 1>, g);
+    return H == 512 ? lp_resident(lstm_bwd_cg_kernel<512, 2>, g) : lp_resident(lstm_bwd_cg_kernel<256, 2>, g);
+  };
+  auto launch_cg = [&](int cpw) {
     LstmSync sy;
     const int rc = lp_sync(st, sy);
     if (rc != XCP_OK) return rc;
-    if (H == 512)
-      hipLaunchKernelGGL(lstm_bwd_cg_kernel<512>, dim3(gcg), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates, dgates, B,
-                         T, sy);
-    else
-      hipLaunchKernelGGL(lstm_bwd_cg_kernel<256>, dim3(gcg), dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates, dgates, B,
-                         T, sy);
+    const dim3 g(cg_grid(cpw));
+#define XCP_LCG(HH, C) hipLaunchKernelGGL((lstm_bwd_cg_kernel<HH, C>), g, dim3(256), 0, st, dout, dhn, dcn, whh, cst, gates, dgates, B, T, sy)
+    if (H == 512 && cpw == 1) XCP_LCG(512, 1);
+    else if (H == 512) XCP_LCG(512, 2);
+    else if (cpw == 1) XCP_LCG(256, 1);
+    else XCP_LCG(256, 2);
+#undef XCP_LCG
     return (int)hipGetLastError();
   };
-  // default (XCP_LSTM_PERSIST and XCP_LSTM_BWD unset): the clip-grouped persistent backward where its workgroups fit
-  // one per CU (H = 512 up to 8 clips, H = 256 up to 16): 30-47 % faster than the per-step kernels there; at
-  // XceptionLSTMA's B 16 x H 512 (512 workgroups) the per-step kernels stay (profiles/r06_lstm_cg_ab.txt)
-  if (lstm_cg_default(B, H, kernel) && gcg <= lp_cus() &&
-      (H == 512 ? lp_resident(lstm_bwd_cg_kernel<512>, gcg) : lp_resident(lstm_bwd_cg_kernel<256>, gcg)))
-    return launch_cg();
+  // default (XCP_LSTM_PERSIST and XCP_LSTM_BWD unset): the clip-grouped persistent backward where its workgroups
+  // take at most half the CUs, as the persistent forward's do (H = 512 up to 4 clips, H = 256 up to 8): 30-47 %
+  // faster than the per-step kernels there.  Elsewhere the per-step kernels: at XceptionLSTMA's B 16 x H 512 the
+  // two-clips-per-wave form (XCP_LSTM_BWD=cg2) is 2 % faster but needs every CU resident at once
+  // (profiles/r06_lstm_cg_ab.txt)
+  if (lstm_cg_default(B, H, kernel) && 2 * cg_grid(1) <= lp_cus() && cg_fits(1)) return launch_cg(1);
   if (lstm_persist(B, H, kernel, false)) {
-    if (lstm_bwd_cg() && (H == 512 ? lp_resident(lstm_bwd_cg_kernel<512>, gcg) : lp_resident(lstm_bwd_cg_kernel<256>, gcg)))
-      return launch_cg();
+    const int cpw = lstm_bwd_cg();
+    if (cpw && cg_fits(cpw)) return launch_cg(cpw);
     LstmSync sy;
     const int rc = lp_sync(st, sy);
     if (rc != XCP_OK) return rc;

@@ -857,9 +857,10 @@ def test_lstm_persistent_vs_step_kernels(ops, gpu, monkeypatch, B, T, H):
         assert err < 1e-5, (k, err)
 
 
+@pytest.mark.parametrize("cg", ["cg", "cg2"])
 @pytest.mark.parametrize("B,T,H", [(16, 9, 512), (3, 5, 256), (13, 7, 512)])
-def test_lstm_bwd_clip_grouped_bitwise(ops, gpu, monkeypatch, B, T, H):
-    """XCP_LSTM_BWD=cg (the persistent backward split by clips as well as units, one clip per wave) against
+def test_lstm_bwd_clip_grouped_bitwise(ops, gpu, monkeypatch, B, T, H, cg):
+    """XCP_LSTM_BWD=cg / cg2 (the persistent backward split by clips as well as units, one / two clips per wave) against
     the gather form it restates: the same per-lane chains and reduction tree, so dgates bit for bit; every
     optional operand; B = 13 leaves idle waves in the last clip group; no poll timeout."""
     G4 = 4 * H
@@ -874,15 +875,15 @@ def test_lstm_bwd_clip_grouped_bitwise(ops, gpu, monkeypatch, B, T, H):
     hn, cn = torch.empty(B, H, device=gpu), torch.empty(B, H, device=gpu)
     ops.lstm_fwd(xp, whh, None, bih, bhh, f["out"], f["hprev"], f["cst"], f["gates"], hn, cn, B, T, H)
     res = {}
-    for form in ("gather", "cg"):
+    for form in ("gather", cg):
         monkeypatch.setenv("XCP_LSTM_BWD", form)
         dg = torch.full((B, T, G4), float("nan"), device=gpu)
         ops.lstm_bwd(dout, dhn, dcn, whh, f["cst"], f["gates"], dg, B, T, H)
         torch.cuda.synchronize()
         res[form] = dg
     assert ops.lstm_sync_error() == 0
-    assert not torch.isnan(res["cg"]).any()
-    assert torch.equal(res["cg"], res["gather"])
+    assert not torch.isnan(res[cg]).any()
+    assert torch.equal(res[cg], res["gather"])
 
 
 @pytest.mark.parametrize("kernel", ["register", "generic"])

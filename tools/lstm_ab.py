@@ -46,21 +46,22 @@ def main():
         fwd = lambda: ops.lstm_fwd(xp, whh, None, bih, bhh, out, hp, cs, gt, hn, cn, B, T, H)   # noqa: E731
         bwd = lambda: ops.lstm_bwd(dout, None, None, whh, cs, gt, dg, B, T, H)   # noqa: E731
         # per-step kernels, persistent (backward: dh partials), persistent (backward: gather), (backward: clip-grouped gather)
-        forms = ("0", "1", "g", "c")
+        forms = ("0", "1", "g", "c", "c2")
         t = {(f, d): [] for f in forms for d in ("fwd", "bwd")}
         for _ in range(rounds):
             for form in forms:
                 os.environ["XCP_LSTM_PERSIST"] = "0" if form == "0" else "1"
-                os.environ["XCP_LSTM_BWD"] = {"g": "gather", "c": "cg"}.get(form, "partials")
+                os.environ["XCP_LSTM_BWD"] = {"g": "gather", "c": "cg", "c2": "cg2"}.get(form, "partials")
                 t[(form, "fwd")].append(timeit(fwd))
                 t[(form, "bwd")].append(timeit(bwd))
         err = ops.lstm_sync_error()
         for d in ("fwd", "bwd"):
-            a, b, c, cg = (statistics.median(t[(f, d)]) for f in forms)
+            a, b, c, cg, cg2 = (statistics.median(t[(f, d)]) for f in forms)
             print(f"B={B:2d} T={T} H={H} {d}: per-step {a:8.1f} us ({a / T:5.2f} us/step)  persistent {b:8.1f} us "
                   f"({b / T:5.2f} us/step, {(b / a - 1) * 100:+6.1f} %)" +
                   (f"  gather {c:8.1f} us ({c / T:5.2f} us/step, {(c / a - 1) * 100:+6.1f} %)"
-                   f"  clip-grouped {cg:8.1f} us ({cg / T:5.2f} us/step, {(cg / a - 1) * 100:+6.1f} %)" if d == "bwd" else "") +
+                   f"  clip-grouped {cg:8.1f} us ({cg / T:5.2f} us/step, {(cg / a - 1) * 100:+6.1f} %)"
+                   f"  cg2 {cg2:8.1f} us ({cg2 / T:5.2f} us/step, {(cg2 / a - 1) * 100:+6.1f} %)" if d == "bwd" else "") +
                   f"  sync_error={err}", flush=True)
     os.environ.pop("XCP_LSTM_PERSIST", None)
     os.environ.pop("XCP_LSTM_BWD", None)
