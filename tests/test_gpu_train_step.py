@@ -286,6 +286,55 @@ def test_graph_captured_train_step_matches_eager(gpu):
         assert torch.equal(sa[k], sb[k]), k
 
 
+@pytest.mark.parametrize("B", [2, 16])
+def test_graph_captured_lstma_step_matches_eager(gpu, B):
+    """The C4 line's default execution (bench.py --model lstma: one HIP graph per step): an XceptionLSTMA(512)
+    train step with the frozen backbone (bf16 engine forward, the H = 512 LSTM on its persistent forward and --
+    B 2 -- the clip-grouped persistent backward or -- B 16 -- the per-step backward, BCE, clip + Adam with device
+    step counts) captured and replayed gives bit for bit the parameters of the same steps run eagerly, and no
+    persistent launch reports a poll timeout."""
+    import xcp
+    from torch.autograd.graph import increment_version
+    from xcp import ops
+    from xcp.optim import FusedAdamClip
+    from Models.XceptionLSTMA import XceptionLSTMA
+    x = seeded_uniform((B, 12, 3, 13), 41).to(gpu) * 2.0 - 1.0
+    y = (torch.arange(B, device=gpu) % 2).float().view(B, 1)
+    models = []
+    for capt in (False, True):
+        torch.manual_seed(0)
+        m = XceptionLSTMA(512, pretrained=False).to(gpu).train()
+        for p in m.feature_extractor.parameters():
+            p.requires_grad = False
+        params = [p for p in m.parameters() if p.requires_grad]
+        opt = FusedAdamClip(params, lr=1e-4, weight_decay=0.0, max_norm=1.0, capturable=capt)
+
+        def step():
+            opt.zero_grad(set_to_none=False)
+            nn.BCELoss()(m(m.extract_features(x, gpu)), y).backward()
+            opt.step()
+
+        with xcp.precision("bf16"):
+            if not capt:
+                for _ in range(4):
+                    step()
+            else:
+                step()
+                torch.cuda.synchronize()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    step()
+                for _ in range(3):
+                    graph.replay()
+                    increment_version(params)
+        torch.cuda.synchronize()
+        models.append(m)
+    assert ops.lstm_sync_error() == 0
+    sa, sb = models[0].state_dict(), models[1].state_dict()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+
+
 def test_fused_adam_capturable_late_parameter_vs_torch(gpu):
     """A parameter whose first gradient arrives at step 3 (the reference's unfreeze after epoch 3,
     train_visual.py:547-556) and one that skips a step keep their own step counts under
