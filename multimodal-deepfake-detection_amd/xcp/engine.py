@@ -157,6 +157,10 @@ CONV2_ACT_ON_LOAD = os.environ.get("XCP_CONV2_ACTIN", "1") != "0"
 # gradient, so the two overlap (A/B; +0.40 % on one box, -0.17 % on another: profiles/r05_wgrad_first_ab.txt;
 # off: the side stream waits for the input gradient)
 WGRAD_FIRST = os.environ.get("XCP_WGRAD_FIRST", "0") == "1"
+# XCP_WGRAD_DEFER=1: a unit's pointwise weight gradient is launched on the side stream after the NEXT unit's
+# input gradient instead of its own, so it runs beside the memory-bound depthwise backward / BN apply that
+# follow rather than beside the next input-gradient GEMM (A/B)
+WGRAD_DEFER = os.environ.get("XCP_WGRAD_DEFER", "0") == "1"
 # XCP_SKIP_WGRAD_LATE=1: a block's skip-conv weight gradient launched on the side stream after the block's
 # units instead of before them (A/B: off keeps it beside the block's own depthwise backward)
 SKIP_WGRAD_LATE = os.environ.get("XCP_SKIP_WGRAD_LATE", "0") == "1"
@@ -527,7 +531,9 @@ class XceptionEngine:
         # partials) go out together in one or two launches when the block is done (REDUCE_BATCH)
         rbatch = ops.ReduceBatch() if REDUCE_BATCH else None
 
-        def wgrad(G, X, M, Nn, K, name, shape, **kw):
+        deferred = []   # (WGRAD_DEFER) the last unit's weight gradient, launched after the next input gradient
+
+        def wgrad(G, X, M, Nn, K, name, shape, defer=False, **kw):
             """dW[Nn][K] = G^T X (logical channels; G / X at their channel pitches)"""
             kw.setdefault("ldg", pc(Nn))
             kw.setdefault("ldx", pc(K))
@@ -535,14 +541,28 @@ class XceptionEngine:
             if side is None:
                 ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, batch=rbatch, **kw)
                 return
+            if defer:
+                flush_deferred()
+                deferred.append((G, X, M, Nn, K, dst, acc, kw))
+                keep.extend((G, X))
+                return
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, batch=rbatch, **kw)
             keep.extend((G, X))   # dst: a gradient, referenced by the caller until the end
 
+        def flush_deferred():
+            if deferred:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    for G, X, M, Nn, K, dst, acc, kw in deferred:
+                        ops.weight_grad(G, X, M, Nn, K, dst, accumulate=acc, batch=rbatch, **kw)
+                deferred.clear()
+
         def done():
             """every gradient requested since the last call is enqueued: reduce the block's slabs,
             tell the sink"""
+            flush_deferred()
             if rbatch is not None and rbatch.jobs:
                 if side is not None:
                     side.wait_stream(main)   # the depthwise partials come from the main stream
@@ -591,7 +611,8 @@ class XceptionEngine:
                     wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
                 ops.gemm_nt(dY, pk[u.name + ".pwT"], dD, M, pc(u.cin), pc(u.cout), tile=NT_TILE)
                 if not WGRAD_FIRST:
-                    wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1))
+                    wgrad(dY, rec["d"], M, u.cout, u.cin, u.name + ".pointwise.weight", (u.cout, u.cin, 1, 1),
+                          defer=WGRAD_DEFER)
             dX = self._empty(M * pc(u.cin))
             dwg, acc = g(u.name + ".conv1.weight", (u.cin, 1, 3, 3))
             bnp = ops.dw_bwd(rec["act"], dD, rec["src"], pk[u.name + ".dw"], rec["sc"], rec["sh"], dX, dwg, N, H, W,

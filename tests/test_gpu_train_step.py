@@ -286,6 +286,28 @@ def test_graph_captured_train_step_matches_eager(gpu):
         assert torch.equal(sa[k], sb[k]), k
 
 
+@pytest.mark.parametrize("flag", ["WGRAD_DEFER", "WGRAD_FIRST", "SKIP_WGRAD_LATE"])
+def test_wgrad_schedule_switches_bitwise(gpu, monkeypatch, flag):
+    """The engine's side-stream schedule switches (a unit's weight gradient launched before its input gradient,
+    after the next unit's, the skip conv's after the block) only reorder independent launches: every gradient
+    of a bf16 xception backward is bit for bit the default schedule's."""
+    import xcp
+    from xcp import engine
+    from Models.Xception import xception
+    x = seeded_uniform((4, 3, 96, 96), 37).to(gpu)
+    grads = []
+    for on in (False, True):
+        monkeypatch.setattr(engine, flag, on)
+        torch.manual_seed(0)
+        m = xception(num_classes=1).to(gpu).train()
+        with xcp.precision("bf16"):
+            m(x).float().square().sum().backward()
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters()})
+    for n in grads[0]:
+        assert torch.equal(grads[0][n], grads[1][n]), n
+
+
 @pytest.mark.parametrize("B", [2, 16])
 def test_graph_captured_lstma_step_matches_eager(gpu, B):
     """The C4 line's default execution (bench.py --model lstma: one HIP graph per step): an XceptionLSTMA(512)
