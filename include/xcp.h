@@ -131,10 +131,14 @@ int xcp_bn_bwd_reduce(int dtype, const void* dZ, const void* Y, const float* mea
 int xcp_bn_finalize_part(const float* part, int R, int C, int CP, double count, const float* gamma, const float* beta,
                          float* rmean, float* rvar, float momentum, float eps, float* mean_o, float* invstd_o,
                          float* scale_o, float* shift_o, xcp_stream_t stream);
-/* (dgamma, dbeta may be null; accumulate = 1 adds to them: gradient accumulation into param.grad) */
+/* (dgamma, dbeta may be null.)  flags: XCP_FIN_ACCUMULATE adds to dgamma / dbeta (gradient accumulation into
+ * param.grad); XCP_FIN_NARROW reduces with 4-wave instead of 16-wave workgroups, which fit beside a kernel
+ * that holds every CU (other summation order: same values to fp64 rounding, not the same bits) */
+#define XCP_FIN_ACCUMULATE 1
+#define XCP_FIN_NARROW 2
 int xcp_bn_bwd_finalize_part(const float* part, int R, int C, int CP, double count, const float* gamma,
                              const float* mean, const float* invstd, float* alpha, float* bcoef, float* delta,
-                             float* dgamma, float* dbeta, int accumulate, xcp_stream_t stream);
+                             float* dgamma, float* dbeta, int flags, xcp_stream_t stream);
 int xcp_bn_finalize(const double* part2, int G, int C, int CP, double count, const float* gamma, const float* beta,
                     float* rmean, float* rvar, float momentum, float eps, int train, float* mean, float* invstd,
                     float* scale, float* shift, xcp_stream_t stream);

@@ -327,8 +327,12 @@ __global__ void bn_finalize_kernel(const double* __restrict__ part2, int G, int 
 // epilogue's / the fused depthwise backward's per-chunk sums): one 1024-thread workgroup
 // per 32 channels; lane l of wave w sums statistic l>>5 of channel l&31 over rows w, w+16, ... in fp64 (four independent accumulators, so
 // many loads stay in flight), the 16 waves fold in LDS, and 32 threads finalize.
-constexpr int FIN_CH = 32, FIN_WAVES = 16;
+// FIN_WAVES_NARROW (xcp_bn_bwd_finalize_part flag XCP_FIN_NARROW): 4 waves -- one per SIMD, 58 VGPRs each -- fit
+// beside a kernel that holds every CU (the stem conv2 weight gradient: 2 waves x 169 VGPRs per SIMD), where the
+// 16-wave workgroup (4 per SIMD) waited for it to finish (144 us per step)
+constexpr int FIN_CH = 32, FIN_WAVES = 16, FIN_WAVES_NARROW = 4;
 
+template <int NW>
 XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, int c0, double (*red)[64], double& s0,
                         double& s1) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -344,12 +348,12 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, in
   if (c < C) {
     const float* col = part + (long)stat * CP + c;
     const int ws = __builtin_amdgcn_readfirstlane(w);
-    for (int r0 = ws; r0 < R; r0 += FIN_U * FIN_WAVES) {
+    for (int r0 = ws; r0 < R; r0 += FIN_U * NW) {
       float v[FIN_U];
 #pragma unroll
-      for (int u = 0; u < FIN_U; ++u) v[u] = col[min(r0 + u * FIN_WAVES, R - 1) * 2 * CP];
+      for (int u = 0; u < FIN_U; ++u) v[u] = col[min(r0 + u * NW, R - 1) * 2 * CP];
 #pragma unroll
-      for (int u = 0; u < FIN_U; ++u) a += r0 + u * FIN_WAVES < R ? (double)v[u] : 0.0;
+      for (int u = 0; u < FIN_U; ++u) a += r0 + u * NW < R ? (double)v[u] : 0.0;
     }
   }
   red[w][lane] = a;
@@ -357,14 +361,14 @@ XCP_DEV void fin_reduce(const float* __restrict__ part, int R, int C, int CP, in
   s0 = s1 = 0.0;
   if (threadIdx.x < FIN_CH) {
 #pragma unroll
-    for (int q = 0; q < FIN_WAVES; ++q) {
+    for (int q = 0; q < NW; ++q) {
       s0 += red[q][threadIdx.x];
       s1 += red[q][threadIdx.x + 32];
     }
   }
 }
 
-__global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C, int CP,
+__global__ __launch_bounds__(64 * FIN_WAVES) void bn_finalize_part_kernel(const float* __restrict__ part, int R, int C, int CP,
                                                                 double count, const float* gamma, const float* beta,
                                                                 float* rmean, float* rvar, float momentum, float eps,
                                                                 float* mean_o, float* invstd_o, float* scale_o,
@@ -372,7 +376,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __r
   __shared__ double red[FIN_WAVES][64];
   const int c0 = blockIdx.x * FIN_CH;
   double s, q;
-  fin_reduce(part, R, C, CP, c0, red, s, q);
+  fin_reduce<FIN_WAVES>(part, R, C, CP, c0, red, s, q);
   const int c = c0 + threadIdx.x;
   if (threadIdx.x >= FIN_CH || c >= CP) return;
   if (c >= C) {   // padding channel
@@ -395,15 +399,16 @@ __global__ __launch_bounds__(1024) void bn_finalize_part_kernel(const float* __r
   shift_o[c] = beta[c] - (float)mean * sc;
 }
 
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_part_kernel(const float* __restrict__ part, int R, int C,
+template <int NWAVES>
+__global__ __launch_bounds__(64 * NWAVES) void bn_bwd_finalize_part_kernel(const float* __restrict__ part, int R, int C,
                                                                     int CP, double count, const float* gamma,
                                                                     const float* mean, const float* invstd,
                                                                     float* alpha, float* bcoef, float* delta,
                                                                     float* dgamma, float* dbeta, int accumulate) {
-  __shared__ double red[FIN_WAVES][64];
+  __shared__ double red[NWAVES][64];
   const int c0 = blockIdx.x * FIN_CH;
   double sdz, sdzy;
-  fin_reduce(part, R, C, CP, c0, red, sdz, sdzy);
+  fin_reduce<NWAVES>(part, R, C, CP, c0, red, sdz, sdzy);
   const int c = c0 + threadIdx.x;
   if (threadIdx.x >= FIN_CH || c >= CP) return;
   if (c >= C) {   // padding channel: its gradient stays zero
@@ -1051,11 +1056,17 @@ int xcp_bn_finalize_part(const float* part, int R, int C, int CP, double count, 
 
 int xcp_bn_bwd_finalize_part(const float* part, int R, int C, int CP, double count, const float* gamma,
                              const float* mean, const float* invstd, float* alpha, float* bcoef, float* delta,
-                             float* dgamma, float* dbeta, int accumulate, hipStream_t st) {
+                             float* dgamma, float* dbeta, int flags, hipStream_t st) {
   if (C <= 0) return XCP_OK;
   if (R <= 0 || CP < C) return XCP_EINVAL;
-  hipLaunchKernelGGL(bn_bwd_finalize_part_kernel, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES), 0, st, part,
-                     R, C, CP, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta, accumulate);
+  const int acc = flags & XCP_FIN_ACCUMULATE;
+  if (flags & XCP_FIN_NARROW)
+    hipLaunchKernelGGL(bn_bwd_finalize_part_kernel<FIN_WAVES_NARROW>, dim3((CP + FIN_CH - 1) / FIN_CH),
+                       dim3(64 * FIN_WAVES_NARROW), 0, st, part, R, C, CP, count, gamma, mean, invstd, alpha, bcoef,
+                       delta, dgamma, dbeta, acc);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_part_kernel<FIN_WAVES>, dim3((CP + FIN_CH - 1) / FIN_CH), dim3(64 * FIN_WAVES),
+                       0, st, part, R, C, CP, count, gamma, mean, invstd, alpha, bcoef, delta, dgamma, dbeta, acc);
   return (int)hipGetLastError();
 }
 

@@ -23,6 +23,7 @@ enum XcpDtype { XCP_F32 = 0, XCP_BF16 = 1 };
 
 // error codes returned across the C-ABI (0 = success, otherwise hipError_t or these)
 enum XcpStatus { XCP_OK = 0, XCP_EINVAL = 1001, XCP_EUNSUPPORTED = 1002 };
+enum XcpFinFlags { XCP_FIN_ACCUMULATE = 1, XCP_FIN_NARROW = 2 };   // xcp_bn_bwd_finalize_part (include/xcp.h)
 
 XCP_DEV float to_f(float x) { return x; }
 XCP_DEV float to_f(bf16 x) { return (float)x; }

@@ -505,6 +505,200 @@ __global__ __launch_bounds__(512, 1) void conv3x3_wgrad_kernel(const bf16* __res
     for (int r = 0; r < 4; ++r) Pb[(16 * cb + 4 * fg + r) * 288 + t * 32 + 16 * bb + fr] = acc[t][r];
 }
 
+// Shifted-gradient form (conv3x3_wgrad_s_kernel<.., 1>, the default; XCP_CONV3_WGRAD=0 runs the kernel above).
+// The kernel above reads, per 32-pixel chunk, one dY fragment and nine X fragments (one per tap) for
+// 9 MFMAs: 20 transposed LDS reads (10 KB per wave) per 9 MFMAs.
+// Indexing the reduction by the INPUT pixel q = ow + kw instead,
+//   dW[co][kh, kw][ci] = sum_oh sum_q dY[oh][q - kw][co] * X[oh + kh][q][ci],
+// the nine taps need three X fragments (one per input row kh, unshifted) and three dY fragments (one
+// per column shift kw, shared by the three rows): 12 reads per 9 MFMAs.  The dY ring slot holds pixel
+// p at position p + 2 (positions 0, 1 and past OW + 1 are zero lines), so q - kw never leaves the slot
+// and every q >= OW + kw meets a zero gradient (also the junk an ACTIN row holds past IW).  CP = 2:
+// a wave owns two co blocks for the nine taps (6 dY + 3 X fragments per 18 MFMAs) and every other
+// chunk; the two chunk halves are summed through LDS at the end (one slab per workgroup either way).
+constexpr int WS_GPX = 176, WS_APX = 160;                   // positions per dY / X ring slot
+constexpr int WS_GSLOT = WS_GPX * 128, WS_ASLOT = WS_APX * 64;
+constexpr int WS_GI = WS_GSLOT / 1024, WS_AI = WS_ASLOT / 1024;   // 22, 10
+static_assert((WS_GI + WS_AI) == 32, "4 DMA instructions per wave per row");
+constexpr int WS_LDS = 3 * WS_GSLOT + 5 * WS_ASLOT;
+static_assert(WS_LDS >= 4 * 18 * 4 * 64 * 4, "the CP = 2 chunk-half reduction fits in the ring");
+
+template <bool ACTIN, int CP>
+__global__ __launch_bounds__(512, 1) void conv3x3_wgrad_s_kernel(const bf16* __restrict__ dY, const bf16* __restrict__ X,
+                                                                 float* __restrict__ P, int N, int IH, int IW, int nb,
+                                                                 int RB, const float* __restrict__ isc,
+                                                                 const float* __restrict__ ish) {
+  __shared__ __attribute__((aligned(16))) char smem[WS_LDS + (ACTIN ? 256 : 0)];
+  float* const sprm0 = reinterpret_cast<float*>(smem + WS_LDS);
+  float* const sprm1 = sprm0 + 32;
+  char* gs = smem;
+  char* as = smem + 3 * WS_GSLOT;
+  const int OH = IH - 2, OW = IW - 2;
+  const int n = blockIdx.x / nb, band = blockIdx.x - n * nb;
+  const int r0 = band * RB, r1 = min(OH, r0 + RB);
+  const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, fg = lane >> 4;
+  const int wsc = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bf16* Gn = dY + (long)n * OH * OW * 64;
+  const bf16* Xn = X + (long)n * IH * IW * 32;
+  auto dma = [](const void* src, char* dst) {
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                     (void __attribute__((address_space(3)))*)dst, 16, 0, 0);
+  };
+  auto g_instr = [&](int row, int j) {   // dY row: position pos holds pixel pos - 2
+    const int q = j * 64 + lane, pos = q >> 3, c = (q & 7) ^ (pos & 7), px = pos - 2;
+    const void* src = px >= 0 && px < OW ? (const void*)(Gn + ((long)row * OW + px) * 64 + c * 8) : (const void*)g_czero;
+    dma(src, gs + (row % 3) * WS_GSLOT + j * 1024);
+  };
+  auto a_instr = [&](int row, int j) {
+    const int q = j * 64 + lane, px = q >> 2, c = (q & 3) ^ (((px >> 2) & 1) << 1);
+    const void* src = px < IW ? (const void*)(Xn + ((long)row * IW + px) * 32 + c * 8) : (const void*)g_czero;
+    dma(src, as + (row % 5) * WS_ASLOT + j * 1024);
+  };
+  auto issue_step = [&](int oh) {   // dY row oh, X row oh + 2: 4 instructions per wave
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wsc * 4 + i;
+      if (j < WS_GI) g_instr(oh, j);
+      else a_instr(oh + 2, j - WS_GI);
+    }
+  };
+  if (r0 >= r1) return;   // uniform
+  if constexpr (ACTIN)
+    if (wsc == 0) c3_load_prm(sprm0, sprm1, isc, ish, 32, lane);
+  auto act_row = [&](int row) {
+    c3_act_chunks<(WS_APX * 4 + 511) / 512>(as + (row % 5) * WS_ASLOT, tid, 512, WS_APX * 4, sprm0, sprm1,
+                                            [](int q) { return ((q & 3) ^ ((((q >> 2) >> 2) & 1) << 1)) * 8; });
+  };
+  // prologue: dY row r0 and X rows r0 .. r0 + 2 (52 instructions over 7 per wave), then step r0 + 1
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int j = wsc * 7 + i;
+    if (j < WS_GI) g_instr(r0, j);
+    else if (j < WS_GI + 3 * WS_AI) a_instr(r0 + (j - WS_GI) / WS_AI, (j - WS_GI) % WS_AI);
+  }
+  if (r0 + 1 < r1) issue_step(r0 + 1);
+
+  // CP = 1: wave = (co block, ci block), every chunk; CP = 2: wave = (co pair, ci block, chunk half)
+  const int bb = CP == 1 ? (wsc & 1) : ((wsc >> 1) & 1);
+  const int cb0 = CP == 1 ? (wsc >> 1) : 2 * (wsc >> 2);
+  const int h = CP == 1 ? 0 : (wsc & 1);
+  const int q4 = fr >> 2, p4 = fr & 3, sub = (p4 & 1) * 8;
+  const int ach = 2 * bb + (p4 >> 1);
+  f32x4 acc[CP][9];
+#pragma unroll
+  for (int c = 0; c < CP; ++c)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nch = (IW + 31) / 32;
+  for (int oh = r0; oh < r1; ++oh) {
+    if (oh + 1 < r1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (oh + 2 < r1) issue_step(oh + 2);
+    if constexpr (ACTIN) {
+      if (oh == r0) {
+        act_row(r0);
+        act_row(r0 + 1);
+      }
+      act_row(oh + 2);
+      lds_barrier();
+    }
+    const char* gslot = gs + (oh % 3) * WS_GSLOT;
+    const char* arow[3] = {as + (oh % 5) * WS_ASLOT, as + ((oh + 1) % 5) * WS_ASLOT, as + ((oh + 2) % 5) * WS_ASLOT};
+    // chunk ch: dY fragments g[c][kw] (co block cb0 + c, pixels q - kw) and X fragments x[kh] (row oh + kh)
+    auto rd = [&](int ch, u64 (&g)[CP][3][2], u64 (&x)[3][2]) {
+      const int pb = ch * 32 + 4 * fg + q4;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        x[kh][0] = ds_read_tr_u64(arow[kh] + pb * 64 + ((ach ^ (((pb >> 2) & 1) << 1)) << 4) + sub);
+        x[kh][1] = ds_read_tr_u64(arow[kh] + (pb + 16) * 64 + ((ach ^ ((((pb + 16) >> 2) & 1) << 1)) << 4) + sub);
+      }
+#pragma unroll
+      for (int c = 0; c < CP; ++c) {
+        const int gch = 2 * (cb0 + c) + (p4 >> 1);
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int lo = pb - kw + 2, hi = lo + 16;
+          g[c][kw][0] = ds_read_tr_u64(gslot + lo * 128 + ((gch ^ (lo & 7)) << 4) + sub);
+          g[c][kw][1] = ds_read_tr_u64(gslot + hi * 128 + ((gch ^ (hi & 7)) << 4) + sub);
+        }
+      }
+    };
+    // retire the chunk's reads: the wait, then every fragment pinned after it (volatile asm keeps the order)
+    auto fence = [&](u64 (&g)[CP][3][2], u64 (&x)[3][2]) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) asm volatile("" : "+v"(x[kh][0]), "+v"(x[kh][1]));
+#pragma unroll
+      for (int c = 0; c < CP; ++c)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) asm volatile("" : "+v"(g[c][kw][0]), "+v"(g[c][kw][1]));
+    };
+    auto mma = [&](const u64 (&g)[CP][3][2], const u64 (&x)[3][2]) {
+#pragma unroll
+      for (int c = 0; c < CP; ++c)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw)
+            acc[c][kh * 3 + kw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, u64x2{g[c][kw][0], g[c][kw][1]}),
+                __builtin_bit_cast(bf16x8, u64x2{x[kh][0], x[kh][1]}), acc[c][kh * 3 + kw], 0, 0, 0);
+    };
+    // two register sets: the next chunk's reads fly under this chunk's MFMAs
+    u64 gA[CP][3][2], xA[3][2], gB[CP][3][2], xB[3][2];
+    if (h < nch) rd(h, gA, xA);
+    for (int ch = h; ch < nch; ch += 2 * CP) {
+      fence(gA, xA);
+      if (ch + CP < nch) rd(ch + CP, gB, xB);
+      mma(gA, xA);
+      if (ch + CP >= nch) break;
+      fence(gB, xB);
+      if (ch + 2 * CP < nch) rd(ch + 2 * CP, gA, xA);
+      mma(gB, xB);
+    }
+  }
+  // acc[c][t][r] = dW[co = 16 (cb0 + c) + 4 fg + r][tap t][ci = 16 bb + fr]
+  float* Pb = P + (long)blockIdx.x * 64 * 288;
+  if constexpr (CP == 2) {   // the odd-chunk waves hand their sums to the even-chunk waves through the ring
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem) + (wsc >> 1) * (18 * 4 * 64);
+    if (h == 1) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[((c * 9 + t) * 4 + r) * 64 + lane] = acc[c][t][r];
+    }
+    __syncthreads();
+    if (h == 1) return;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[c][t][r] += red[((c * 9 + t) * 4 + r) * 64 + lane];
+  }
+#pragma unroll
+  for (int c = 0; c < CP; ++c)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Pb[(16 * (cb0 + c) + 4 * fg + r) * 288 + t * 32 + 16 * bb + fr] = acc[c][t][r];
+}
+
+// XCP_CONV3_WGRAD: 0 = conv3x3_wgrad_kernel, 1 (default) = the shifted form, one co block per wave, 2 = two
+// co blocks per wave (read per call: the tests compare the forms in one process).  Alone at 256 x 149^2:
+// 392 / 345 / 343 us with the slab reduction; in the step form 1 is +0.35 % over form 0 and form 2 +0.1 %:
+// at 225-238 VGPRs form 2 leaves no room on its SIMDs for the BN1 sums (chanred, 138 VGPRs) that run beside
+// it, form 1 at 169 does (profiles/r06_conv3_wgrad_ab.txt)
+int conv3_wgrad_form() {
+  const char* e = getenv("XCP_CONV3_WGRAD");
+  return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
+}
+
 // bands per frame for the weight-gradient grid: about one workgroup per CU, >= 8 rows a band
 
 // rows per tile and the widest input each direction supports (two LDS tile buffers of 57 /
@@ -594,7 +788,7 @@ int xcp_conv3x3(int mode, const void* X, const void* W, void* Y, float* stats, i
 
 // slabs (= workgroups) of xcp_conv3x3_wgrad; 0 when the width is unsupported
 int xcp_conv3x3_wgrad_parts(int N, int IH, int IW) {
-  if (N <= 0 || IH < 3 || IW < 3 || IW - 2 > WG_GPX) return 0;
+  if (N <= 0 || IH < 3 || IW < 3 || (conv3_wgrad_form() ? IW > WS_APX : IW - 2 > WG_GPX)) return 0;
   int nb, rb;
   wgrad_bands(N, IH - 2, nb, rb);
   return N * nb;
@@ -606,9 +800,21 @@ int xcp_conv3x3_wgrad(const void* dY, const void* X, float* P, int N, int IH, in
                       const float* in_shift, hipStream_t st) {
   if (N <= 0) return XCP_OK;
   if (IH < 3 || IW < 3 || (in_scale != nullptr) != (in_shift != nullptr)) return XCP_EINVAL;
-  if (IW - 2 > WG_GPX) return XCP_EUNSUPPORTED;
+  const int form = conv3_wgrad_form();
+  if (form ? IW > WS_APX : IW - 2 > WG_GPX) return XCP_EUNSUPPORTED;
   int nb, rb;
   wgrad_bands(N, IH - 2, nb, rb);
+  if (form) {
+#define XCP_C3W(ACT, CP)                                                                                             \
+  hipLaunchKernelGGL((conv3x3_wgrad_s_kernel<ACT, CP>), dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, \
+                     N, IH, IW, nb, rb, in_scale, in_shift)
+    if (in_scale && form == 1) XCP_C3W(true, 1);
+    else if (in_scale) XCP_C3W(true, 2);
+    else if (form == 1) XCP_C3W(false, 1);
+    else XCP_C3W(false, 2);
+#undef XCP_C3W
+    return (int)hipGetLastError();
+  }
   if (in_scale)
     hipLaunchKernelGGL(conv3x3_wgrad_kernel<true>, dim3(N * nb), dim3(512), 0, st, (const bf16*)dY, (const bf16*)X, P, N, IH,
                        IW, nb, rb, in_scale, in_shift);

@@ -129,6 +129,10 @@ CONV1_BN_FUSED = os.environ.get("XCP_CONV1_BN_FUSED", "1") != "0"
 # no longer ends waiting for it (+0.2-0.5 % in two interleaved rounds, profiles/r04_stem_order_ab.txt;
 # XCP_STEM_WGRAD_EARLY=0: after BN1's coefficients)
 STEM_WGRAD_EARLY = os.environ.get("XCP_STEM_WGRAD_EARLY", "1") != "0"
+# BN1's backward finalize in 4-wave workgroups (XCP_FIN_NARROW) while conv2's weight gradient holds every CU on the
+# side stream: the 16-wave workgroup found no SIMD with room for 4 of its waves and waited for the whole weight
+# gradient (144 us per step, profiles/r06_conv3_wgrad_ab.txt).  XCP_STEM_FIN_NARROW=0: the 16-wave form (A/B)
+STEM_FIN_NARROW = os.environ.get("XCP_STEM_FIN_NARROW", "1") != "0"
 # BN1's batch statistics from conv1's forward (xcp_conv1_fwd_stats; XCP_CONV1_STATS_FUSED=0: a per-channel
 # reduce over the stored output, A/B)
 CONV1_STATS_FUSED = os.environ.get("XCP_CONV1_STATS_FUSED", "1") != "0"
@@ -574,7 +578,7 @@ class XceptionEngine:
                 notify(list(pending), side)
             pending.clear()
 
-        def bn_coef(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
+        def bn_coef(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False, narrow=False):
             """BN backward up to its coefficients (alpha, bcoef, delta; at the channel pitch);
             writes the affine grads"""
             P = part[1] if part is not None else 0
@@ -583,7 +587,7 @@ class XceptionEngine:
                 raise NotImplementedError(f"xcp engine: {name}.weight and .bias must both (or neither) require grad")
             return ops.bn_backward_coef(dZ, Y, rows, C, _bn_ref(bnmod), st, gw, gb,
                                         part=part[0] if part is not None else None, R=P, relu=relu, accumulate=acc,
-                                        CP=pc(C))
+                                        CP=pc(C), narrow=narrow)
 
         def bn_bwd(bnmod, name, dZ, Y, rows, C, st, part=None, relu=False):
             coef = bn_coef(bnmod, name, dZ, Y, rows, C, st, part, relu)
@@ -681,8 +685,10 @@ class XceptionEngine:
         # apply, conv1's weight gradient).  Launched the other way round, the finalize's one
         # 1024-thread workgroup waited for the side stream's conv2 weight gradient to leave the CUs:
         # 356 us per step on the main stream (profiles/r03_v3_kernels.txt)
+        # (narrow finalize: conv2's weight gradient holds every CU beside it when launched early)
         if STEM_BN1_FIRST:
-            coef1 = bn_coef(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], None, True)   # relu (Xception.py:170)
+            coef1 = bn_coef(m.bn1, "bn1", dA1, S["c1"], rows1, 32, S["s1"], None, True,   # relu (Xception.py:170)
+                            narrow=STEM_FIN_NARROW and STEM_WGRAD_EARLY and st2 is not None)
         if not (STEM_WGRAD_EARLY and st2 is not None):
             conv2_wgrad(st2)
         if not STEM_BN1_FIRST:

@@ -312,14 +312,16 @@ def row_stats(X, rows, C):
     return part, R
 
 
-def bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False, CP=None):
+def bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=None, R=0, relu=False, accumulate=False, CP=None,
+                     narrow=False):
     """BatchNorm2d backward (train-mode batch stats) up to the per-channel coefficients:
     returns coef fp32 [3][C] (alpha, bcoef, delta: dY = alpha*dZ' + bcoef*Y + delta, dZ' the
     ReLU-masked dZ when relu) and writes (accumulate: adds to) dgamma/dbeta.
     ``part`` ([R][2][CP] partial (sum dz, sum dz*zhat)) may come fused from the
     producer of dZ; otherwise it is reduced here.  relu=True: dZ is the gradient of
     relu(bn(Y)) (the ReLU mask is recomputed from Y and st's scale/shift).  CP (default C):
-    channel pitch of dZ / Y; coef then has CP entries per coefficient, zero for the padding."""
+    channel pitch of dZ / Y; coef then has CP entries per coefficient, zero for the padding.  narrow: the
+    finalize in 4-wave workgroups (room beside a kernel holding every CU; XCP_FIN_NARROW)."""
     CP = CP or C
     ms, mt = (_p(st["scale"]), _p(st["shift"])) if relu else (0, 0)
     dev, dt = Y.device, Y.dtype
@@ -334,7 +336,7 @@ def bn_backward_coef(dZ, Y, rows, C, bn, st, dgamma, dbeta, part=None, R=0, relu
     part, R = _fold(part, R, CP)
     _lib.call("xcp_bn_bwd_finalize_part", _p(part), R, C, CP, float(rows), _p(bn["weight"]), _p(st["mean"]),
               _p(st["invstd"]), _p(coef), _p(coef[CP:]), _p(coef[2 * CP:]), _p(dgamma), _p(dbeta),
-              1 if accumulate else 0, stream())
+              (1 if accumulate else 0) | (2 if narrow else 0), stream())
     return coef
 
 

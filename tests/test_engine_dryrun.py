@@ -45,8 +45,8 @@ def install_fake_lib(monkeypatch):
                 _, out, _, L, _, G, acc = jobs[7 * i:7 * i + 7]
                 _fill(out, L * G, acc)
         elif name == "xcp_bn_bwd_finalize_part" and args[11]:   # dgamma, dbeta (C each)
-            _fill(args[11], args[2], args[13])
-            _fill(args[12], args[2], args[13])
+            _fill(args[11], args[2], args[13] & 1)   # (flags: 1 accumulate, 2 narrow)
+            _fill(args[12], args[2], args[13] & 1)
         elif name == "xcp_permute3" and args[0] == 0:          # fp32 permute (stem conv2 gradient)
             _fill(args[2], args[3] * args[4] * args[5], False)
         if name == "xcp_dw_bwd_chunks":

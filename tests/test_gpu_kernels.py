@@ -595,6 +595,35 @@ def test_bn_padded_channel_pitch(ops, gpu, dt):
     torch.testing.assert_close(b1, b0, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("rows,C,CP,relu", [(256 * 147 * 147 // 64, 32, 32, True), (3 * 361, 728, 736, False),
+                                             (5, 64, 64, True)])
+def test_bn_bwd_finalize_narrow(ops, gpu, rows, C, CP, relu):
+    """XCP_FIN_NARROW (the stem BN1 finalize beside conv2's weight gradient): 4-wave workgroups reduce the
+    partial rows in another order than the 16-wave form -- the coefficients and the accumulated affine
+    gradients agree to fp64 rounding (rtol 1e-6), the padding channels stay zero."""
+    from xcp.engine import Stats
+    g = torch.Generator(device=gpu).manual_seed(rows + C)
+    y = torch.zeros(rows, CP, device=gpu, dtype=torch.bfloat16)
+    dz = torch.zeros(rows, CP, device=gpu, dtype=torch.bfloat16)
+    y[:, :C] = (torch.randn(rows, C, device=gpu, generator=g) * 2 + 0.7).bfloat16()
+    dz[:, :C] = torch.randn(rows, C, device=gpu, generator=g).bfloat16()
+    gamma, beta = torch.rand(C, device=gpu, generator=g) + 0.5, torch.randn(C, device=gpu, generator=g) * 0.1
+    bn = {"weight": gamma, "bias": beta, "running_mean": torch.zeros(C, device=gpu),
+          "running_var": torch.ones(C, device=gpu), "eps": 1e-5, "momentum": 0.1, "track": True}
+    part, R = ops.row_stats(y, rows, CP)
+    st = Stats(CP, gpu)
+    ops.finalize_stats(part, R, C, rows, bn, True, st, CP)
+    res = []
+    for narrow in (False, True):
+        dg, db = torch.ones(C, device=gpu), torch.ones(C, device=gpu)
+        coef = ops.bn_backward_coef(dz, y, rows, C, bn, st, dg, db, relu=relu, accumulate=True, CP=CP, narrow=narrow)
+        res.append((coef, dg, db))
+    torch.cuda.synchronize()
+    for a, b in zip(res[0], res[1]):
+        torch.testing.assert_close(b, a, rtol=1e-6, atol=1e-7)
+    assert torch.all(res[1][0].view(3, CP)[:, C:] == 0)
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("H", [147, 37, 19, 20])
 def test_tail_maxpool_fwd_bwd(ops, gpu, dt, H):
@@ -971,6 +1000,37 @@ def test_conv3x3_stem_fwd_dgrad(ops, gpu, N, IH, IW):
     ref_dw = torch.nn.grad.conv2d_weight(x.float(), (64, 32, 3, 3), dy.float())
     got = dW.view(64, 3, 3, 32).permute(0, 3, 1, 2)
     assert rel_err(got, ref_dw) < 1e-4
+
+
+@pytest.mark.parametrize("form", ["0", "1", "2"])
+@pytest.mark.parametrize("N,IH,IW", [(2, 149, 149), (3, 21, 38), (1, 6, 147), (2, 12, 160), (3, 3, 3), (1, 40, 34)])
+def test_conv3x3_wgrad_forms(ops, gpu, monkeypatch, form, N, IH, IW):
+    """The stem conv2 weight gradient in its three forms (XCP_CONV3_WGRAD: 0 = one dY and nine shifted X
+    fragments per chunk, 1 = the reduction indexed by input pixel -- three X and three shifted dY fragments,
+    2 = the same with two co blocks per wave and the chunk halves summed through LDS) against conv2d_weight
+    on the same bf16 operands, plain and with BN1 + ReLU applied on load (bitwise against the activated
+    input within each form); widths up to 160 (the shifted forms' ring), single-row and single-column images."""
+    monkeypatch.setenv("XCP_CONV3_WGRAD", form)
+    g = torch.Generator(device=gpu).manual_seed(IH * 3 + IW)
+    rows = N * IH * IW
+    x = (torch.randn(rows, 32, device=gpu, generator=g) * 1.5 + 0.3).bfloat16()
+    sc = torch.rand(32, device=gpu, generator=g) + 0.4
+    sh = torch.randn(32, device=gpu, generator=g) * 0.5
+    a = torch.empty_like(x)
+    ops.bn_act(x, a, sc, sh, True, rows, 32)
+    OH, OW = IH - 2, IW - 2
+    dy = torch.randn(N * OH * OW, 64, device=gpu, generator=g).bfloat16()
+    assert ops.conv3x3_wgrad_parts(N, IH, IW) > 0
+    dws = []
+    for src, kw in ((a, {}), (x, {"in_scale": sc, "in_shift": sh})):
+        dW = torch.full((64 * 288,), float("nan"), device=gpu)
+        ops.conv3x3_wgrad(dy, src, dW, N, IH, IW, **kw)
+        dws.append(dW)
+    torch.cuda.synchronize()
+    assert torch.equal(dws[0], dws[1])
+    ref_dw = torch.nn.grad.conv2d_weight(nchw(a.view(N, IH, IW, 32)).float(), (64, 32, 3, 3),
+                                         nchw(dy.view(N, OH, OW, 64)).float())
+    assert rel_err(dws[0].view(64, 3, 3, 32).permute(0, 3, 1, 2), ref_dw) < 1e-4
 
 
 @pytest.mark.parametrize("N,IH,IW", [(2, 149, 149), (3, 21, 38), (1, 6, 147)])
