@@ -573,6 +573,10 @@ def main():
         else:
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    # XCP_BENCH_MAIN_PRIO=high (A/B): the whole run on a stream at the device's greatest priority, so the engine's
+    # weight-gradient stream (default priority) ranks below the main stream at the workgroup dispatcher
+    if os.environ.get("XCP_BENCH_MAIN_PRIO", "") == "high":
+        torch.cuda.set_stream(torch.cuda.Stream(dev, priority=torch.cuda.Stream.priority_range()[1]))
 
     import xcp
     from xcp import engine, ops
