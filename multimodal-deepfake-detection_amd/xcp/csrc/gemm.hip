@@ -108,6 +108,7 @@ struct NTArgs {
   Gather ga;
   int tqs;                // gemm_nt256p_kernel: tile-queue slot + 1 (0: static tile walk)
   int nsplit;             // gemm_nt256p_kernel: the last nsplit tiles are walked as 2 half tiles each, first
+  int khalf;              // gemm_nt256p_kernel: a last K-tile with K % 64 in (0, 32] multiplies its first half only
 };
 
 // ---------------------------------------------------------------------------------
@@ -802,26 +803,34 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
 
   f32x4 acc[8][4];
   const int nk = (a.K + 63) / 64;
+  // (XCP_NT_KHALF=0: every K-tile whole; the A/B switch, read per launch on the host)
+  const bool khalf = a.khalf && (a.K & 63) != 0 && (a.K & 63) <= 32;
   const int fr = lane & 15, fg = lane >> 4;
   bf16x8 af[4][2], bl[2][2], br[2][2];
-  auto mfma_q = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
+  // NKS: 32-deep halves of the K-tile to multiply (1: the last K-tile of a K with K % 64 in (0, 32], whose
+  // second half is all zero lines -- adding its +0 products leaves every accumulator's bits unchanged)
+  bool lastk = false;   // (wave-uniform) the K-tile being multiplied is the last one
+  auto mfma_q = [&](int ih, const bf16x8 (&b)[2][2], int jh, auto nks) {
+    constexpr int NKS = decltype(nks)::value;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (ks == 1 && khalf && lastk) break;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[ih * 4 + i][jh * 2 + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][ks], af[i][ks], acc[ih * 4 + i][jh * 2 + j], 0, 0, 0);
+    }
   };
   int side = 0;   // of the current item (wave-uniform)
-  auto sync_mfma = [&](int ih, const bf16x8 (&b)[2][2], int jh) {
+  auto sync_mfma = [&](int ih, const bf16x8 (&b)[2][2], int jh, auto nks) {
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     if (!HALF || side != 2 - jh) {   // (a half tile skips the other side's quadrants)
       __builtin_amdgcn_s_setprio(1);
-      mfma_q(ih, b, jh);
+      mfma_q(ih, b, jh, nks);
       __builtin_amdgcn_s_setprio(0);
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -867,12 +876,13 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
     // with PF2 it issues nothing (K-tile 1 is in flight) and its Q3 wait leaves the stores in flight.
     // MODE 2 (PF2, kt == 1): the previous epilogue's S_ST stores sit between K-tile 1's loads and K-tile
     // 2's, so its Q0 / Q1 waits allow S_ST more; its Q3 wait retires them.
-    auto ktile = [&](int kt, auto mode) {
+    auto ktile = [&](int kt, auto mode, auto nks) {
       constexpr int MODE = decltype(mode)::value;
       constexpr bool ISSUE = !(PF2 && MODE == 1);
       const char* sa = smem + (kt & 1) * K_SLOT;
       const char* sb = sa + K_OP;
       const bool nxt = kt + 1 < nk;
+      lastk = !nxt;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -891,7 +901,7 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
         } else if (extra) vm_wait(2 + S_ST);
         else vm_wait(2);
       }
-      sync_mfma(0, bl, 0);
+      sync_mfma(0, bl, 0, nks);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -904,14 +914,14 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
         else if (extra) vm_wait(4 + S_ST);
         else vm_wait(4);
       }
-      sync_mfma(0, br, 1);
+      sync_mfma(0, br, 1, nks);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           af[i][ks] = *reinterpret_cast<const bf16x8*>(sa + swz(wr * 128 + 64 + i * 16 + fr, ks * 4 + fg));
       if (ISSUE && nxt) issue(2, kt + 1);
-      sync_mfma(1, br, 1);
+      sync_mfma(1, br, 1, nks);
       if (nxt) {
         if constexpr (ISSUE) {
           issue(3, kt + 1);
@@ -922,14 +932,15 @@ __global__ __launch_bounds__(512) void gemm_nt256p_kernel(NTArgs a) {
           vm_wait(4);
         }
       }
-      sync_mfma(1, bl, 0);
+      sync_mfma(1, bl, 0, nks);
     };
-    ktile(0, IC<1>{});
     if constexpr (PF2) {
-      if (nk > 1) ktile(1, IC<2>{});
-      for (int kt = 2; kt < nk; ++kt) ktile(kt, IC<0>{});
+      ktile(0, IC<1>{}, IC<2>{});
+      if (nk > 1) ktile(1, IC<2>{}, IC<2>{});
+      for (int kt = 2; kt < nk; ++kt) ktile(kt, IC<0>{}, IC<2>{});
     } else {
-      for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{});
+      ktile(0, IC<1>{}, IC<2>{});
+      for (int kt = 1; kt < nk; ++kt) ktile(kt, IC<0>{}, IC<2>{});
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();   // every wave is done reading both ring slots
     const int cm0 = m0, cn0 = n0, cside = side;
@@ -2198,6 +2209,14 @@ bool nt_pf2() {   // XCP_NT_PF2=1: gemm_nt256p_kernel's two-K-tile prefetch at t
   const char* e = getenv("XCP_NT_PF2");
   return e && e[0] == '1';
 }
+// The 256p kernel's last K-tile multiplies only its first 32-deep half when the rest of it is past K (the
+// 728-channel flow at its 736 pitch: K = 728 / 736, 24 / 32 of the last 64): 32 of the tile's 768 MFMAs
+// per wave skipped, C and the statistics bitwise equal (the skipped products are +0).  XCP_NT_KHALF=0:
+// every K-tile whole (read per call; A/B)
+bool nt_khalf() {
+  const char* e = getenv("XCP_NT_KHALF");
+  return !(e && e[0] == '0');
+}
 bool nt_half() {   // XCP_NT_HALF=1 (read per call; A/B)
   const char* e = getenv("XCP_NT_HALF");
   return e && e[0] == '1';
@@ -2246,6 +2265,7 @@ int xcp_gemm_nt(int dtype, const void* A, long lda, const void* B, long ldb, voi
   if (gmode < 0 || gmode > 3 || (gmode >= 2 && (gC % 8 || gC * 9 != K))) return XCP_EINVAL;
   if (tile < 0 || tile > 4) return XCP_EINVAL;
   NTArgs a{A, lda, B, ldb, C, ldc, M, N, K, stats, Gather{gmode, gH, gW, gOH, gOW, gS > 0 ? gS : 1, gC}};
+  a.khalf = nt_khalf() ? 1 : 0;
   if (nt_big(dtype, gmode, M, N, K, tile)) {
     // automatic choice (tile 0): the persistent kernel; tile 4: the automatic choice with the
     // one-shot kernel (A/B)

@@ -1366,15 +1366,17 @@ def test_gemm_tn_loops_bitwise(ops, gpu, monkeypatch, M, N, K):
     torch.testing.assert_close(got, ref, rtol=2e-3, atol=2e-3 * ref.abs().max().item())
 
 
-@pytest.mark.parametrize("form", ["XCP_NT_HALF", "XCP_NT_PF2", "XCP_NT_4W", "XCP_NT_8W"])
+@pytest.mark.parametrize("form", ["XCP_NT_HALF", "XCP_NT_PF2", "XCP_NT_4W", "XCP_NT_8W", "XCP_NT_KHALF"])
 @pytest.mark.parametrize("M,N,K,stats", [(92416, 736, 736, True), (92416, 736, 736, False), (256 * 100 + 7, 768, 200, True),
-                                         (256 * 100 + 7, 768, 392, False), (256 * 300 + 5, 512, 128, False)])
+                                         (256 * 100 + 7, 768, 392, False), (256 * 300 + 5, 512, 128, False),
+                                         (256 * 100 + 7, 736, 728, True)])
 def test_gemm_nt_half_tiles_bitwise(ops, gpu, monkeypatch, M, N, K, stats, form):
     """XCP_NT_HALF=1: the persistent kernel walks the last round's tiles as two half tiles each (only one
     B half's quadrants and columns per half) before the whole tiles; XCP_NT_PF2=1: it issues the next tile's
     first two K-tiles ahead of each epilogue (K = 128: two K-tiles, every wait of the second one's form);
     XCP_NT_4W=1: the one-wave-per-SIMD kernel (gemm_nt4w_kernel; K = 200 / 392 / 736: an odd number of
-    32-deep steps, padded by a step of zero fragments) --
+    32-deep steps, padded by a step of zero fragments); XCP_NT_KHALF (0 in the reference run, 1 = the default):
+    a last K-tile with K % 64 in (0, 32] multiplies its first 32-deep half only (K = 200 / 392 / 728 / 736) --
     with the static walk (statistics) and with the tile queue (none): output and statistics bits identical
     to the reference run for every row: the one-shot kernel for the half tiles (every row on the persistent
     kernel), the default persistent kernel (same sparse last round on the 128x128 kernel) for the others."""
