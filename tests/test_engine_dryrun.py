@@ -220,6 +220,22 @@ def test_header_matches_binding():
         assert n == len(_lib.SIGNATURES[name]), name
 
 
+def test_header_constants_match_kernel_enums():
+    """Every XCP_* constant the C header defines that the kernels' common.h also defines (dtypes, statuses,
+    the finalize flags) has the same value on both sides of the ABI."""
+    import os
+    import re
+    root = os.path.join(os.path.dirname(__file__), "..")
+    hdr = open(os.path.join(root, "include", "xcp.h")).read()
+    common = open(os.path.join(root, "multimodal-deepfake-detection_amd", "xcp", "csrc", "common.h")).read()
+    h = {k: int(v) for k, v in re.findall(r"#define\s+(XCP_[A-Z0-9_]+)\s+(-?\d+)\b", hdr)}
+    c = {k: int(v) for k, v in re.findall(r"\b(XCP_[A-Z0-9_]+)\s*=\s*(-?\d+)", common)}
+    shared = set(h) & set(c)
+    assert {"XCP_F32", "XCP_BF16", "XCP_FIN_ACCUMULATE", "XCP_FIN_NARROW"} <= shared, sorted(shared)
+    for k in shared:
+        assert h[k] == c[k], k
+
+
 def test_library_exports_every_symbol():
     """libxcp.so (built in-tree) loads and exports every symbol of include/xcp.h.
     Loading needs no GPU; no compute call is made."""
