@@ -27,6 +27,9 @@ extern "C" {
 
 typedef void* xcp_stream_t; /* hipStream_t */
 
+#define XCP_OK 0
+#define XCP_EINVAL 1001
+#define XCP_EUNSUPPORTED 1002
 #define XCP_F32 0
 #define XCP_BF16 1
 #define XCP_ACT_NONE 0

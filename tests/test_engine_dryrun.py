@@ -231,7 +231,8 @@ def test_header_constants_match_kernel_enums():
     h = {k: int(v) for k, v in re.findall(r"#define\s+(XCP_[A-Z0-9_]+)\s+(-?\d+)\b", hdr)}
     c = {k: int(v) for k, v in re.findall(r"\b(XCP_[A-Z0-9_]+)\s*=\s*(-?\d+)", common)}
     shared = set(h) & set(c)
-    assert {"XCP_F32", "XCP_BF16", "XCP_FIN_ACCUMULATE", "XCP_FIN_NARROW"} <= shared, sorted(shared)
+    assert {"XCP_OK", "XCP_EINVAL", "XCP_EUNSUPPORTED", "XCP_F32", "XCP_BF16", "XCP_FIN_ACCUMULATE",
+            "XCP_FIN_NARROW"} <= shared, sorted(shared)
     for k in shared:
         assert h[k] == c[k], k
 
